@@ -1,0 +1,188 @@
+#!/usr/bin/env python3
+"""Headline benchmark: HTTP req/s + p50/p99 latency of GET /api/hola (BASELINE.json).
+
+One rank per "GPU slot" of the node = one hola replica. Every rank:
+  * starts a `hola` replica pinned to its own share of the host cores (the GPUs stay idle:
+    the reference has no tensor work — SURVEY.md §0),
+  * drives it with the native closed-loop load generator on disjoint cores; the generator's
+    64 keep-alive connections per replica are dealt round-robin over ALL replicas of the
+    node (client-side round-robin, BASELINE.json config 4: "512 connections against 8
+    replicas behind round-robin"; N=1 is config 3: 64 connections, 1 replica).
+A step = every connection completes `--reqs-per-conn` requests (weak scaling: the work per
+replica is fixed). W warmup steps, then exactly K timed steps between barriers; the elapsed
+time is the MAX over ranks, `value` is the node-wide total req/s, and p50/p99 come from the
+merged latency histograms of all ranks.
+
+  python bench.py --gpus N --steps K --warmup W
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent))
+
+from hola_amd.native import ensure_built  # noqa: E402
+from hola_amd.parallel.loadgen import ControlledLoadgen, decode_hist, merge_hists, percentile  # noqa: E402
+from hola_amd.server import HolaProcess  # noqa: E402
+from hola_amd.utils.cpu import cgroup_cpu_quota, cpu_budget, format_cpu_list, plan_cores  # noqa: E402
+
+METRIC = "HTTP req/sec + p50/p99 latency, GET /api/hola at 1/2/4/8 replicas"
+BASELINE_VALUE = None  # the reference publishes no numbers
+
+
+def parse_args():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1, help="replicas on this node (one per rank)")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--connections", type=int, default=64, help="keep-alive connections per replica")
+    ap.add_argument("--reqs-per-conn", type=int, default=1000, help="requests per connection per step")
+    ap.add_argument("--cores", type=int, default=0, help="host cores per replica (server + load generator)")
+    ap.add_argument("--server-threads", type=int, default=0, help="0 = half of the rank's cores")
+    ap.add_argument("--base-port", type=int, default=int(os.environ.get("HOLA_BENCH_PORT", "18400")))
+    ap.add_argument("--path", default="/api/hola")
+    ap.add_argument("--no-tracing", action="store_true", help="run replicas with tracing off")
+    return ap.parse_args()
+
+
+def main() -> int:
+    a = parse_args()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    if world != a.gpus:
+        print(f"bench: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # gloo: replicas exchange only a few numbers (no device data)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    ensure_built("release")  # file-locked: concurrent ranks build once
+
+    # ---- core plan: server + loadgen on disjoint physical cores of this rank's share ----
+    cores = plan_cores(local_rank, local_world, a.cores or None)
+    n = len(cores)
+    s_threads = a.server_threads or max(1, n // 2)
+    s_threads = min(s_threads, max(1, n - 1)) if n > 1 else 1
+    server_cpus, load_cpus = cores[:s_threads], (cores[s_threads:] or cores)
+    port = a.base_port + local_rank
+    targets = [("127.0.0.1", a.base_port + i) for i in range(local_world)]
+
+    env = {"HOSTNAME": f"replica-{rank}"}
+    args = ["--no-tracing"] if a.no_tracing else []
+    server = HolaProcess(args=args, env=env, port=port, threads=s_threads, cpu_list=format_cpu_list(server_cpus),
+                         log_level="warn")
+    server.start()
+    loadgen = None
+    try:
+        if dist:
+            dist.barrier()  # every replica is listening before any connection is made
+        loadgen = ControlledLoadgen(targets, a.connections, len(load_cpus), cpu_list=format_cpu_list(load_cpus),
+                                    path=a.path, target_offset=local_rank)
+        for _ in range(a.warmup):
+            loadgen.run(a.reqs_per_conn)
+        loadgen.reset()
+
+        cuda = _cuda_sync_fn(local_rank)
+        if dist:
+            dist.barrier()
+        cuda()
+        t0 = time.perf_counter()
+        reqs = errs = 0
+        for _ in range(a.steps):
+            r = loadgen.run(a.reqs_per_conn)
+            reqs += r["requests"]
+            errs += r["errors"]
+        if dist:
+            dist.barrier()
+        cuda()
+        elapsed = time.perf_counter() - t0
+        st = loadgen.stats()
+
+        local = {"elapsed": elapsed, "requests": reqs, "errors": errs, "hist": st.get("hist", ""),
+                 "non2xx": st.get("non2xx", 0), "server_cpus": format_cpu_list(server_cpus),
+                 "load_cpus": format_cpu_list(load_cpus)}
+        if dist:
+            gathered = [None] * world
+            dist.all_gather_object(gathered, local)
+        else:
+            gathered = [local]
+    finally:
+        if loadgen:
+            loadgen.close()
+        server.stop()
+
+    if rank == 0:
+        t = max(g["elapsed"] for g in gathered)
+        total = sum(g["requests"] for g in gathered)
+        hist = merge_hists([decode_hist(g["hist"]) for g in gathered])
+        value = total / t if t > 0 else 0.0
+        out = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "req/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(t * 1000.0 / a.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None if BASELINE_VALUE is None else round(value / BASELINE_VALUE, 4),
+            "dtype": "n/a (host-CPU HTTP service; no tensor compute)",
+            "data": "synthetic closed-loop HTTP load (native loadgen, keep-alive, 1 request in flight per connection)",
+            "p50_ms": round(percentile(hist, 50) / 1e6, 4),
+            "p99_ms": round(percentile(hist, 99) / 1e6, 4),
+            "p999_ms": round(percentile(hist, 99.9) / 1e6, 4),
+            "requests": total,
+            "errors": sum(g["errors"] for g in gathered),
+            "non2xx": sum(g["non2xx"] for g in gathered),
+            "config": {
+                "model": "hola GET /api/hola (native C++ replica, default greeting, tracing "
+                         + ("off" if a.no_tracing else "on") + ")",
+                "global_batch": a.connections * world,
+                "seq_len": 1,
+                "parallelism": f"replicas{world}",
+                "connections_per_replica": a.connections,
+                "reqs_per_conn_per_step": a.reqs_per_conn,
+                "lb": "client-side round-robin over replica ports",
+                "server_threads_per_replica": s_threads,
+                "loadgen_threads_per_replica": len(load_cpus),
+                "cpu_map": {f"rank{i}": {"server": g["server_cpus"], "loadgen": g["load_cpus"]}
+                            for i, g in enumerate(gathered)},
+                "cpu_budget": cpu_budget(),
+                "cgroup_quota": cgroup_cpu_quota(),
+            },
+        }
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+def _cuda_sync_fn(local_rank: int):
+    """torch.cuda.synchronize bracket required by the bench contract. The service launches
+    no device work, so this is a no-op fence; it only runs when a GPU is present (and after
+    every child process has been started)."""
+    if os.environ.get("HOLA_BENCH_CUDA_SYNC", "1") != "1":
+        return lambda: None
+    try:
+        import torch
+        if torch.cuda.is_available():
+            torch.cuda.set_device(local_rank % max(1, torch.cuda.device_count()))
+            return torch.cuda.synchronize
+    except Exception:
+        pass
+    return lambda: None
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,466 @@
+// hola_loadgen — wrk-style closed-loop HTTP/1.1 load generator.
+//
+// C keep-alive connections spread over T pinned threads; each connection keeps exactly
+// one request in flight (no pipelining, like wrk's default) and records send->last-byte
+// latency in a log-linear histogram. Connections are dealt round-robin over --targets
+// (client-side round-robin across replicas, BASELINE.json config 4).
+//
+// Modes:
+//   --duration S [--warmup S]   timed run, prints one JSON line (rps, p50/p90/p99/p99.9)
+//   --control                   stdin protocol used by bench.py:
+//        run <R>     every connection completes exactly R requests; replies
+//                    {"elapsed_ns":..,"requests":..,"errors":..}
+//        stats       {"count":..,"p50_ns":..,...,"hist":"bin:count,..."} (since last reset)
+//        reset       clears the histogram
+//        quit
+#include <errno.h>
+#include <netinet/in.h>
+#include <sys/epoll.h>
+#include <sys/eventfd.h>
+#include <sys/socket.h>
+#include <signal.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <iostream>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "bench/histogram.h"
+#include "core/affinity.h"
+#include "core/clock.h"
+#include "core/net.h"
+
+using namespace hola;
+using hola::bench::Histogram;
+
+namespace {
+
+struct Target {
+  std::string host;
+  int port;
+  sockaddr_storage addr;
+  socklen_t len;
+};
+
+struct Options {
+  std::vector<Target> targets;
+  int connections = 64;
+  int threads = 1;
+  std::vector<int> cpus;
+  std::string path = "/api/hola";
+  std::string method = "GET";
+  double duration_s = 0, warmup_s = 0;
+  bool control = false;
+  int target_offset = 0;
+  std::vector<std::string> extra_headers;
+};
+
+struct Conn {
+  int fd = -1;
+  int target = 0;
+  std::string req;
+  char buf[4096];
+  size_t have = 0;
+  int64_t t0 = 0;
+  int64_t quota = 0;  // remaining requests in control mode
+  bool busy = false;
+};
+
+struct ThreadState {
+  int index = 0;
+  int epfd = -1;
+  int wakefd = -1;
+  std::vector<std::unique_ptr<Conn>> conns;
+  Histogram hist;
+  std::mutex hist_mu;
+  uint64_t completed = 0, errors = 0, non2xx = 0, reconnects = 0;
+  std::atomic<int64_t> run_quota{0};  // control: requests per connection for the next run
+  std::atomic<uint64_t> run_gen{0};
+  std::atomic<uint64_t> done_gen{0};
+  std::atomic<uint64_t> done_requests{0}, done_errors{0};
+  bool recording = true;
+};
+
+std::atomic<bool> g_stop{false};
+int g_donefd = -1;  // EFD_SEMAPHORE: one count per thread finishing a control run
+
+void signal_done() {
+  uint64_t one = 1;
+  ssize_t w = ::write(g_donefd, &one, sizeof one);
+  (void)w;
+}
+
+bool connect_conn(Conn* c, const Options& o) {
+  const Target& t = o.targets[size_t(c->target)];
+  c->fd = connect_blocking(t.addr, t.len, 5000);
+  if (c->fd < 0) return false;
+  set_nonblocking(c->fd, true);
+  set_nodelay(c->fd);
+  c->have = 0;
+  c->busy = false;
+  return true;
+}
+
+bool send_req(Conn* c) {
+  c->t0 = mono_ns();
+  c->busy = true;
+  c->have = 0;
+  size_t off = 0;
+  while (off < c->req.size()) {
+    ssize_t w = ::send(c->fd, c->req.data() + off, c->req.size() - off, MSG_NOSIGNAL);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      if (errno == EAGAIN) continue;  // tiny request; socket buffer is never full here
+      return false;
+    }
+    off += size_t(w);
+  }
+  return true;
+}
+
+// Returns 1 when a full response is in buf, 0 if more is needed, -1 on malformed input.
+int response_complete(Conn* c, int* status, bool* close) {
+  std::string_view s(c->buf, c->have);
+  size_t he = s.find("\r\n\r\n");
+  if (he == std::string_view::npos) return c->have >= sizeof c->buf ? -1 : 0;
+  if (s.size() < 12 || s.substr(0, 5) != "HTTP/") return -1;
+  *status = (s[9] - '0') * 100 + (s[10] - '0') * 10 + (s[11] - '0');
+  std::string_view head = s.substr(0, he);
+  size_t cl = 0;
+  size_t p = head.find("Content-Length: ");
+  if (p == std::string_view::npos) p = head.find("content-length: ");
+  if (p != std::string_view::npos) cl = size_t(atol(std::string(head.substr(p + 16, 12)).c_str()));
+  *close = head.find("Connection: close") != std::string_view::npos;
+  if (he + 4 + cl > sizeof c->buf) return -1;
+  return c->have >= he + 4 + cl ? 1 : 0;
+}
+
+void thread_main(ThreadState* ts, const Options* o) {
+  if (!o->cpus.empty()) pin_current_thread(o->cpus[size_t(ts->index) % o->cpus.size()]);
+  epoll_event ev{};
+  for (auto& c : ts->conns) {
+    ev.events = EPOLLIN;
+    ev.data.ptr = c.get();
+    epoll_ctl(ts->epfd, EPOLL_CTL_ADD, c->fd, &ev);
+  }
+  ev.events = EPOLLIN;
+  ev.data.ptr = nullptr;
+  epoll_ctl(ts->epfd, EPOLL_CTL_ADD, ts->wakefd, &ev);
+
+  const bool control = o->control;
+  uint64_t seen_gen = 0;
+  int64_t outstanding = 0;  // control: connections with quota left
+  uint64_t run_requests = 0, run_errors = 0;
+  int64_t warm_end = o->duration_s > 0 ? mono_ns() + int64_t(o->warmup_s * 1e9) : 0;
+  int64_t end = o->duration_s > 0 ? warm_end + int64_t(o->duration_s * 1e9) : 0;
+  ts->recording = !(o->warmup_s > 0);
+
+  auto start_all = [&]() {
+    for (auto& c : ts->conns) {
+      if (c->busy || c->quota <= 0) continue;
+      if (!send_req(c.get())) ++ts->errors;
+    }
+  };
+  if (!control) {
+    for (auto& c : ts->conns) c->quota = INT64_MAX;
+    start_all();
+  }
+
+  epoll_event evs[256];
+  while (!g_stop.load(std::memory_order_relaxed)) {
+    int n = epoll_wait(ts->epfd, evs, 256, control ? -1 : 5);
+    int64_t now = mono_ns();
+    if (!control) {
+      if (!ts->recording && now >= warm_end) {
+        std::lock_guard<std::mutex> g(ts->hist_mu);
+        ts->hist.reset();
+        ts->completed = 0;
+        ts->recording = true;
+      }
+      if (now >= end) break;
+    }
+    for (int i = 0; i < n; ++i) {
+      Conn* c = static_cast<Conn*>(evs[i].data.ptr);
+      if (!c) {  // control wake-up
+        uint64_t v;
+        while (::read(ts->wakefd, &v, sizeof v) > 0) {
+        }
+        uint64_t g = ts->run_gen.load();
+        if (g != seen_gen) {
+          seen_gen = g;
+          int64_t q = ts->run_quota.load();
+          outstanding = 0;
+          run_requests = run_errors = 0;
+          for (auto& cc : ts->conns) {
+            cc->quota = q;
+            if (q > 0) ++outstanding;
+          }
+          if (outstanding == 0) {
+            ts->done_requests.store(0);
+            ts->done_errors.store(0);
+            ts->done_gen.store(seen_gen);
+            signal_done();
+          }
+          start_all();
+        }
+        continue;
+      }
+      ssize_t r = ::recv(c->fd, c->buf + c->have, sizeof c->buf - c->have, 0);
+      if (r <= 0) {
+        if (r < 0 && (errno == EAGAIN || errno == EINTR)) continue;
+        // peer closed: reconnect and retry
+        epoll_ctl(ts->epfd, EPOLL_CTL_DEL, c->fd, nullptr);
+        ::close(c->fd);
+        ++ts->errors;
+        ++run_errors;
+        ++ts->reconnects;
+        if (!connect_conn(c, *o)) {
+          g_stop.store(true);
+          signal_done();
+          break;
+        }
+        ev.events = EPOLLIN;
+        ev.data.ptr = c;
+        epoll_ctl(ts->epfd, EPOLL_CTL_ADD, c->fd, &ev);
+        if (c->quota > 0 && !send_req(c)) ++ts->errors;
+        continue;
+      }
+      c->have += size_t(r);
+      int status = 0;
+      bool close = false;
+      int rc = response_complete(c, &status, &close);
+      if (rc == 0) continue;
+      if (rc < 0) {
+        ++ts->errors;
+        ++run_errors;
+        close = true;
+      } else {
+        int64_t lat = mono_ns() - c->t0;
+        // (the histogram is only read between control runs / after the run: no lock)
+        if (ts->recording) {
+          ts->hist.add(uint64_t(lat));
+          ++ts->completed;
+        }
+        if (status < 200 || status > 299) ++ts->non2xx;
+        ++run_requests;
+      }
+      c->busy = false;
+      if (close) {
+        epoll_ctl(ts->epfd, EPOLL_CTL_DEL, c->fd, nullptr);
+        ::close(c->fd);
+        ++ts->reconnects;
+        if (!connect_conn(c, *o)) {
+          g_stop.store(true);
+          signal_done();
+          break;
+        }
+        ev.events = EPOLLIN;
+        ev.data.ptr = c;
+        epoll_ctl(ts->epfd, EPOLL_CTL_ADD, c->fd, &ev);
+      }
+      if (control) {
+        if (--c->quota <= 0) {
+          if (--outstanding == 0) {
+            ts->done_requests.store(run_requests);
+            ts->done_errors.store(run_errors);
+            ts->done_gen.store(seen_gen);
+            signal_done();
+          }
+          continue;
+        }
+      }
+      if (!send_req(c)) ++ts->errors;
+    }
+  }
+}
+
+bool parse_targets(const std::string& s, std::vector<Target>* out) {
+  size_t i = 0;
+  while (i < s.size()) {
+    size_t j = s.find(',', i);
+    if (j == std::string::npos) j = s.size();
+    std::string t = s.substr(i, j - i);
+    i = j + 1;
+    size_t colon = t.rfind(':');
+    if (colon == std::string::npos) return false;
+    Target tg;
+    tg.host = t.substr(0, colon);
+    tg.port = atoi(t.substr(colon + 1).c_str());
+    std::string err;
+    if (!resolve_host(tg.host, tg.port, &tg.addr, &tg.len, &err)) {
+      fprintf(stderr, "loadgen: %s\n", err.c_str());
+      return false;
+    }
+    out->push_back(tg);
+  }
+  return !out->empty();
+}
+
+std::string stats_json(std::vector<std::unique_ptr<ThreadState>>& ts, bool with_hist) {
+  Histogram h;
+  uint64_t errors = 0, non2xx = 0, reconnects = 0;
+  for (auto& t : ts) {
+    std::lock_guard<std::mutex> g(t->hist_mu);
+    h.merge(t->hist);
+    errors += t->errors;
+    non2xx += t->non2xx;
+    reconnects += t->reconnects;
+  }
+  char buf[512];
+  snprintf(buf, sizeof buf,
+           "{\"count\":%llu,\"mean_ns\":%.0f,\"p50_ns\":%llu,\"p90_ns\":%llu,\"p99_ns\":%llu,\"p999_ns\":%llu,"
+           "\"max_ns\":%llu,\"errors\":%llu,\"non2xx\":%llu,\"reconnects\":%llu",
+           (unsigned long long)h.count(), h.mean(), (unsigned long long)h.percentile(50),
+           (unsigned long long)h.percentile(90), (unsigned long long)h.percentile(99),
+           (unsigned long long)h.percentile(99.9), (unsigned long long)h.max(), (unsigned long long)errors,
+           (unsigned long long)non2xx, (unsigned long long)reconnects);
+  std::string s = buf;
+  if (with_hist) s += ",\"hist\":\"" + h.encode() + "\"";
+  return s + "}";
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  Options o;
+  std::string targets = "127.0.0.1:8080", cpu_list;
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    auto val = [&]() -> std::string {
+      if (i + 1 >= argc) {
+        fprintf(stderr, "loadgen: %s needs a value\n", a.c_str());
+        exit(2);
+      }
+      return argv[++i];
+    };
+    if (a == "--targets") targets = val();
+    else if (a == "--connections" || a == "-c") o.connections = atoi(val().c_str());
+    else if (a == "--threads" || a == "-t") o.threads = atoi(val().c_str());
+    else if (a == "--cpu-list") cpu_list = val();
+    else if (a == "--path") o.path = val();
+    else if (a == "--method") o.method = val();
+    else if (a == "--duration" || a == "-d") o.duration_s = atof(val().c_str());
+    else if (a == "--warmup") o.warmup_s = atof(val().c_str());
+    else if (a == "--control") o.control = true;
+    else if (a == "--target-offset") o.target_offset = atoi(val().c_str());
+    else if (a == "--header" || a == "-H") o.extra_headers.push_back(val());
+    else {
+      fprintf(stderr,
+              "usage: hola_loadgen --targets h:p[,h:p..] -c CONNS -t THREADS [--cpu-list L] [--path P]\n"
+              "                    (--duration S [--warmup S] | --control) [--target-offset K] [-H 'Name: v']\n");
+      return 2;
+    }
+  }
+  if (!parse_targets(targets, &o.targets)) return 2;
+  if (!cpu_list.empty() && !parse_cpu_list(cpu_list, &o.cpus)) {
+    fprintf(stderr, "loadgen: bad --cpu-list\n");
+    return 2;
+  }
+  if (o.threads < 1) o.threads = 1;
+  if (o.connections < o.threads) o.connections = o.threads;
+  if (!o.control && o.duration_s <= 0) o.duration_s = 10;
+  signal(SIGPIPE, SIG_IGN);
+  g_donefd = eventfd(0, EFD_SEMAPHORE | EFD_CLOEXEC);
+
+  std::vector<std::unique_ptr<ThreadState>> ts;
+  for (int t = 0; t < o.threads; ++t) {
+    auto s = std::make_unique<ThreadState>();
+    s->index = t;
+    s->epfd = epoll_create1(EPOLL_CLOEXEC);
+    s->wakefd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+    ts.push_back(std::move(s));
+  }
+  for (int i = 0; i < o.connections; ++i) {
+    auto c = std::make_unique<Conn>();
+    c->target = (i + o.target_offset) % int(o.targets.size());
+    const Target& t = o.targets[size_t(c->target)];
+    c->req = o.method + " " + o.path + " HTTP/1.1\r\nHost: " + t.host + ":" + std::to_string(t.port) + "\r\n";
+    for (auto& h : o.extra_headers) c->req += h + "\r\n";
+    c->req += "\r\n";
+    if (!connect_conn(c.get(), o)) {
+      fprintf(stderr, "loadgen: connect %s:%d failed: %s\n", t.host.c_str(), t.port, strerror(errno));
+      return 1;
+    }
+    ts[size_t(i % o.threads)]->conns.push_back(std::move(c));
+  }
+  std::vector<std::thread> th;
+  for (auto& s : ts) th.emplace_back(thread_main, s.get(), &o);
+
+  if (!o.control) {
+    for (auto& t : th) t.join();
+    std::string s = stats_json(ts, false);
+    uint64_t completed = 0;
+    for (auto& t : ts) completed += t->completed;
+    double rps = double(completed) / o.duration_s;
+    printf("{\"mode\":\"duration\",\"duration_s\":%.3f,\"connections\":%d,\"threads\":%d,\"targets\":%zu,\"rps\":%.1f,\"latency\":%s}\n",
+           o.duration_s, o.connections, o.threads, o.targets.size(), rps, s.c_str());
+    return 0;
+  }
+
+  // ---- control protocol ----
+  printf("{\"ready\":true,\"connections\":%d,\"threads\":%d}\n", o.connections, o.threads);
+  fflush(stdout);
+  std::string line;
+  uint64_t gen = 0;
+  while (std::getline(std::cin, line)) {
+    if (line.rfind("run ", 0) == 0) {
+      int64_t q = atoll(line.c_str() + 4);
+      ++gen;
+      int64_t t0 = mono_ns();
+      for (auto& t : ts) {
+        t->run_quota.store(q);
+        t->run_gen.store(gen);
+        uint64_t one = 1;
+        ssize_t w = ::write(t->wakefd, &one, sizeof one);
+        (void)w;
+      }
+      uint64_t reqs = 0, errs = 0;
+      for (size_t k = 0; k < ts.size(); ++k) {
+        uint64_t v;
+        while (::read(g_donefd, &v, sizeof v) < 0 && errno == EINTR) {
+        }
+        if (g_stop.load()) {
+          printf("{\"error\":\"connection failure\"}\n");
+          fflush(stdout);
+          return 1;
+        }
+      }
+      for (auto& t : ts) {
+        reqs += t->done_requests.load();
+        errs += t->done_errors.load();
+      }
+      int64_t el = mono_ns() - t0;
+      printf("{\"elapsed_ns\":%lld,\"requests\":%llu,\"errors\":%llu}\n", (long long)el, (unsigned long long)reqs,
+             (unsigned long long)errs);
+      fflush(stdout);
+    } else if (line == "stats") {
+      printf("%s\n", stats_json(ts, true).c_str());
+      fflush(stdout);
+    } else if (line == "reset") {
+      for (auto& t : ts) {
+        std::lock_guard<std::mutex> g(t->hist_mu);
+        t->hist.reset();
+        t->errors = t->non2xx = t->reconnects = 0;
+      }
+      printf("{\"reset\":true}\n");
+      fflush(stdout);
+    } else if (line == "quit") {
+      break;
+    }
+  }
+  g_stop.store(true);
+  for (auto& t : ts) {
+    uint64_t one = 1;
+    ssize_t w = ::write(t->wakefd, &one, sizeof one);
+    (void)w;
+  }
+  for (auto& t : th) t.join();
+  return 0;
+}

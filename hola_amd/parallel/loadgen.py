@@ -1,0 +1,116 @@
+"""Driver for the native closed-loop load generator (bench/loadgen.cc)."""
+from __future__ import annotations
+
+import json
+import subprocess
+
+from hola_amd.native import binary
+
+SUB = 64  # must match bench/histogram.h
+
+
+def bin_value(b: int) -> int:
+    if b < SUB:
+        return b
+    octave, sub = divmod(b - SUB, SUB)
+    msb = octave + 6
+    lo = (1 << msb) + (sub << (msb - 6))
+    return lo + ((1 << (msb - 6)) >> 1)
+
+
+def decode_hist(s: str) -> dict[int, int]:
+    out: dict[int, int] = {}
+    if not s:
+        return out
+    for part in s.split(","):
+        b, c = part.split(":")
+        out[int(b)] = out.get(int(b), 0) + int(c)
+    return out
+
+
+def merge_hists(hists: list[dict[int, int]]) -> dict[int, int]:
+    out: dict[int, int] = {}
+    for h in hists:
+        for b, c in h.items():
+            out[b] = out.get(b, 0) + c
+    return out
+
+
+def percentile(hist: dict[int, int], p: float) -> int:
+    total = sum(hist.values())
+    if not total:
+        return 0
+    need = max(1, min(total, int(p / 100.0 * total + 0.5)))
+    acc = 0
+    for b in sorted(hist):
+        acc += hist[b]
+        if acc >= need:
+            return bin_value(b)
+    return bin_value(max(hist))
+
+
+class ControlledLoadgen:
+    """`hola_loadgen --control`: each run(R) makes every connection complete R requests."""
+
+    def __init__(self, targets: list[tuple[str, int]], connections: int, threads: int,
+                 cpu_list: str | None = None, path: str = "/api/hola", target_offset: int = 0,
+                 headers: list[str] | None = None):
+        cmd = [str(binary("hola_loadgen")), "--targets", ",".join(f"{h}:{p}" for h, p in targets),
+               "-c", str(connections), "-t", str(threads), "--path", path, "--control",
+               "--target-offset", str(target_offset)]
+        if cpu_list:
+            cmd += ["--cpu-list", cpu_list]
+        for h in headers or []:
+            cmd += ["-H", h]
+        self.proc = subprocess.Popen(cmd, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, bufsize=1)
+        ready = self._read()
+        if not ready.get("ready"):
+            raise RuntimeError(f"loadgen failed to start: {ready}")
+
+    def _read(self) -> dict:
+        line = self.proc.stdout.readline()
+        if not line:
+            raise RuntimeError(f"loadgen exited (rc={self.proc.poll()})")
+        return json.loads(line)
+
+    def _cmd(self, c: str) -> dict:
+        self.proc.stdin.write(c + "\n")
+        self.proc.stdin.flush()
+        out = self._read()
+        if "error" in out:
+            raise RuntimeError(f"loadgen: {out['error']}")
+        return out
+
+    def run(self, reqs_per_conn: int) -> dict:
+        return self._cmd(f"run {reqs_per_conn}")
+
+    def stats(self) -> dict:
+        return self._cmd("stats")
+
+    def reset(self) -> dict:
+        return self._cmd("reset")
+
+    def close(self) -> None:
+        if self.proc.poll() is None:
+            try:
+                self.proc.stdin.write("quit\n")
+                self.proc.stdin.flush()
+                self.proc.wait(timeout=10)
+            except Exception:
+                self.proc.kill()
+                self.proc.wait()
+
+
+def run_duration(targets: list[tuple[str, int]], connections: int, threads: int, duration_s: float,
+                 warmup_s: float = 1.0, cpu_list: str | None = None, path: str = "/api/hola",
+                 timeout: float | None = None) -> dict:
+    """wrk-style timed run; returns the loadgen's JSON summary."""
+    cmd = [str(binary("hola_loadgen")), "--targets", ",".join(f"{h}:{p}" for h, p in targets),
+           "-c", str(connections), "-t", str(threads), "--path", path, "--duration", str(duration_s),
+           "--warmup", str(warmup_s)]
+    if cpu_list:
+        cmd += ["--cpu-list", cpu_list]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout or duration_s + warmup_s + 60)
+    if r.returncode != 0:
+        raise RuntimeError(f"loadgen failed: {r.stderr}")
+    return json.loads(r.stdout.strip().splitlines()[-1])

@@ -1,0 +1,116 @@
+"""Host CPU topology, cgroup quota and per-replica core planning.
+
+On the MI355X node the service runs on the EPYC host cores (2 sockets x 64 cores, SMT2 on
+the box probed for this build). A gpurun box is a CFS-quota slice of that host (cpu.max
+"1600000 100000" = 16 CPUs) with the full 256-CPU affinity mask, so plans are sized from
+the quota and laid out on distinct *physical* cores (one SMT sibling each), NUMA node by
+NUMA node, so replica i and replica j never share a core or an L2.
+"""
+from __future__ import annotations
+
+import os
+from pathlib import Path
+
+
+def parse_cpu_list(s: str) -> list[int]:
+    out: list[int] = []
+    for tok in s.split(","):
+        tok = tok.strip()
+        if not tok:
+            continue
+        if "-" in tok:
+            a, b = tok.split("-", 1)
+            out.extend(range(int(a), int(b) + 1))
+        else:
+            out.append(int(tok))
+    return out
+
+
+def format_cpu_list(cpus: list[int]) -> str:
+    cpus = sorted(cpus)
+    parts = []
+    i = 0
+    while i < len(cpus):
+        j = i
+        while j + 1 < len(cpus) and cpus[j + 1] == cpus[j] + 1:
+            j += 1
+        parts.append(str(cpus[i]) if i == j else f"{cpus[i]}-{cpus[j]}")
+        i = j + 1
+    return ",".join(parts)
+
+
+def allowed_cpus() -> list[int]:
+    return sorted(os.sched_getaffinity(0))
+
+
+def cgroup_cpu_quota() -> float:
+    """CPUs granted by cgroup v2 cpu.max; 0.0 when unlimited or unknown."""
+    try:
+        q, p = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q == "max":
+            return 0.0
+        return float(q) / float(p)
+    except (OSError, ValueError):
+        return 0.0
+
+
+def cpu_budget() -> int:
+    """Number of CPUs this process tree may keep busy."""
+    n = len(allowed_cpus())
+    q = cgroup_cpu_quota()
+    if q > 0:
+        n = min(n, int(q))
+    return max(1, n)
+
+
+def _read(path: str) -> str | None:
+    try:
+        return Path(path).read_text().strip()
+    except OSError:
+        return None
+
+
+def physical_cores(cpus: list[int] | None = None) -> list[int]:
+    """One CPU per physical core (the lowest SMT sibling), ordered by NUMA node then id."""
+    cpus = allowed_cpus() if cpus is None else cpus
+    allowed = set(cpus)
+    seen: set[tuple[str, str]] = set()
+    picked: list[tuple[int, int]] = []
+    for c in cpus:
+        base = f"/sys/devices/system/cpu/cpu{c}/topology"
+        sib = _read(f"{base}/thread_siblings_list") or _read(f"{base}/core_cpus_list")
+        pkg = _read(f"{base}/physical_package_id") or "0"
+        if sib is None:
+            picked.append((0, c))
+            continue
+        key = (pkg, sib)
+        if key in seen:
+            continue
+        seen.add(key)
+        first = min(x for x in parse_cpu_list(sib) if x in allowed) if any(
+            x in allowed for x in parse_cpu_list(sib)) else c
+        node = 0
+        for n in range(0, 16):
+            if Path(f"/sys/devices/system/cpu/cpu{first}/node{n}").exists():
+                node = n
+                break
+        picked.append((node, first))
+    picked.sort()
+    return [c for _, c in picked]
+
+
+def plan_cores(rank: int, local_world: int, per_rank: int | None = None) -> list[int]:
+    """Disjoint CPU set for `rank` out of `local_world` co-located ranks.
+
+    Defaults to an equal share of the CPU budget, on distinct physical cores when enough
+    exist (falls back to SMT siblings / any allowed CPU otherwise).
+    """
+    budget = cpu_budget()
+    if per_rank is None:
+        per_rank = max(1, budget // max(1, local_world))
+    phys = physical_cores()
+    pool = phys if len(phys) >= per_rank * local_world else allowed_cpus()
+    if len(pool) < per_rank * local_world:
+        per_rank = max(1, len(pool) // max(1, local_world))
+    start = rank * per_rank
+    return pool[start:start + per_rank] or pool[:per_rank]

@@ -1,0 +1,60 @@
+// The aloha call of /api/hola-chaining: the HystrixFeign proxy built in
+// HolaResource.getNextService() (HolaResource.java:94-113) re-designed for an event loop.
+//
+//   Feign target      http://aloha:8080/ + GET /api/aloha-chaining  (AlohaService.java:25)
+//   Hystrix command   "AlohaService#aloha()", group = target URL     [lib-default keying]
+//   fallback          ["Aloha response (fallback)"]                  (HolaResource.java:111-112)
+//   tracing           client span child of the server span + B3 headers (HolaResource.java:97-108)
+//   logging           Feign Logger.ErrorLogger at Level.BASIC        (HolaResource.java:109)
+#pragma once
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "app/chaining.h"
+#include "client/http_client.h"
+#include "resilience/hystrix.h"
+
+namespace hola::tracing {
+class Tracer;
+}
+
+namespace hola::app {
+
+struct AlohaOptions {
+  std::string url = "http://aloha:8080/";  // HolaResource.java:103
+  std::string path = "api/aloha-chaining";  // AlohaService.java:25
+  bool feign_log_basic = true;
+  std::string command_key = "AlohaService#aloha()";
+};
+
+class AlohaChainer final : public Chainer {
+ public:
+  AlohaChainer(AlohaOptions o, resilience::Settings s, int num_workers, tracing::Tracer* tracer,
+               const Clock& clock = SystemClock::instance());
+  ~AlohaChainer() override;
+  bool ok() const { return url_ok_; }
+  void start();  // DNS refresher
+  void stop();
+
+  void call(http::Worker& w, const tracing::SpanContext* parent,
+            std::function<void(const ChainResult&)> done) override;
+
+  resilience::Command& command() { return *cmd_; }
+  void update_settings(const resilience::Settings& s) { cmd_->update_settings(s); }
+  const std::string& full_url() const { return full_url_; }
+
+ private:
+  client::ClientPool& pool(http::Worker& w);
+  AlohaOptions o_;
+  client::Url target_;
+  bool url_ok_ = false;
+  std::string full_url_;
+  std::unique_ptr<client::AddressCache> addr_;
+  std::unique_ptr<resilience::Command> cmd_;
+  std::vector<std::unique_ptr<client::ClientPool>> pools_;
+  tracing::Tracer* tracer_;
+  const Clock& clock_;
+};
+
+}  // namespace hola::app

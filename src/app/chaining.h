@@ -1,0 +1,36 @@
+// Downstream call abstraction for GET /api/hola-chaining (HolaResource.java:69-78): the
+// handler asks a Chainer for aloha's greetings and gets either the decoded list or the
+// Hystrix fallback `["Aloha response (fallback)"]` (HolaResource.java:111-112).
+#pragma once
+#include <functional>
+#include <optional>
+#include <string>
+#include <string_view>
+#include <vector>
+
+namespace hola::http {
+class Worker;
+}
+namespace hola::tracing {
+struct SpanContext;
+}
+
+namespace hola::app {
+
+constexpr std::string_view kFallbackGreeting = "Aloha response (fallback)";
+
+struct ChainResult {
+  std::vector<std::optional<std::string>> items;
+  bool fallback = false;
+  std::string reason;  // why the fallback was used (timeout, short-circuited, ...)
+};
+
+class Chainer {
+ public:
+  virtual ~Chainer() = default;
+  // Runs on the worker thread; `done` is invoked exactly once, later, on the same thread.
+  virtual void call(http::Worker& w, const tracing::SpanContext* parent,
+                    std::function<void(const ChainResult&)> done) = 0;
+};
+
+}  // namespace hola::app

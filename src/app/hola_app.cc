@@ -1,0 +1,406 @@
+#include "app/hola_app.h"
+
+#include <cstring>
+
+#include "app/assets.h"
+#include "app/chaining.h"
+#include "config/jformat.h"
+#include "core/clock.h"
+#include "core/log.h"
+#include "http/negotiate.h"
+#include "json/json.h"
+#include "metrics/hystrix_stream.h"
+#include "metrics/prometheus.h"
+#include "tracing/tracer.h"
+
+namespace hola::app {
+
+using http::build_response;
+using http::Prepared;
+using http::ResponseSpec;
+
+namespace {
+constexpr std::string_view kTextPlain = "text/plain";
+constexpr std::string_view kJson = "application/json";
+constexpr std::string_view kHtml = "text/html";
+constexpr std::string_view kAllowApi = "Allow: HEAD, GET, OPTIONS\r\n";
+// Undertow's default error pages (the servlet container answers outside JAX-RS).
+constexpr std::string_view kUndertowNotFound = "<html><head><title>Error</title></head><body>Not Found</body></html>";
+constexpr std::string_view kUndertowError =
+    "<html><head><title>Error</title></head><body>Internal Server Error</body></html>";
+constexpr std::string_view kUndertowMethodNotAllowed =
+    "<html><head><title>Error</title></head><body>Method Not Allowed</body></html>";
+}  // namespace
+
+// Everything a worker needs to answer without touching shared state.
+struct HolaApp::WorkerCache {
+  uint64_t gen = ~0ull;
+  uint64_t date_version = ~0ull;
+  std::shared_ptr<const Content> content;
+  // [keep_alive][head]
+  Prepared hola[2][2], health[2][2], swagger[2][2], index[2][2], viewer[2][2];
+  Prepared chaining_fallback[2][2];
+  Prepared api_not_found[2], not_found[2][2], api_not_allowed[2], not_allowed[2], not_acceptable[2],
+      api_options[2], static_options[2], server_error[2][2];
+  std::vector<Prepared*> all;
+  std::string scratch;  // for dynamic bodies
+};
+
+const char* HolaApp::route_name(int r) {
+  static const char* kNames[] = {"/api/hola", "/api/hola-chaining", "/api/health", "/api/swagger.json",
+                                 "/", "/webjars/swagger-ui", "/hystrix.stream", "/metrics",
+                                 "/api/*(404)", "*(404)"};
+  return (r >= 0 && r < kNumRoutes) ? kNames[r] : "?";
+}
+
+std::shared_ptr<Content> compute_content(const config::Snapshot& snap, const AppOptions& o) {
+  auto c = std::make_shared<Content>();
+  c->generation = snap.generation;
+  config::Resolved r = snap.resolver->resolve(o.greeting_key, o.greeting_default);
+  c->translation = r.value;
+  c->source = r.source;
+  config::FormatResult f = config::java_format(r.value, {o.hostname});
+  c->ok = f.ok;
+  if (f.ok) c->greeting = std::move(f.value);
+  else c->error = f.error + ": " + f.detail;
+  return c;
+}
+
+HolaApp::HolaApp(AppOptions o) : o_(std::move(o)) {}
+HolaApp::~HolaApp() = default;
+
+void HolaApp::publish(std::shared_ptr<const Content> c) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    content_ = std::move(c);
+  }
+  gen_.fetch_add(1, std::memory_order_release);
+}
+
+std::shared_ptr<const Content> HolaApp::content() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return content_;
+}
+
+void HolaApp::on_config(const config::Snapshot& snap) {
+  auto c = compute_content(snap, o_);
+  if (o_.log_changes && (!logged_once_ || c->translation != last_translation_)) {
+    // DeltaSpike TypedResolver.logChanges(true): one INFO line per value change.
+    LOG_INFO("New value %s for key %s (source %s).", c->translation.c_str(), o_.greeting_key.c_str(),
+             c->source.c_str());
+    last_translation_ = c->translation;
+    logged_once_ = true;
+  }
+  if (!c->ok) LOG_WARN("greeting format failed: %s", c->error.c_str());
+  publish(std::move(c));
+}
+
+HolaApp::WorkerCache& HolaApp::cache(http::Worker& w) { return *static_cast<WorkerCache*>(w.app_data); }
+
+void HolaApp::on_worker_start(http::Worker& w) {
+  auto* wc = new WorkerCache();
+  w.app_data = wc;
+  refresh(w, *wc);
+}
+
+void HolaApp::on_worker_stop(http::Worker& w) {
+  delete static_cast<WorkerCache*>(w.app_data);
+  w.app_data = nullptr;
+}
+
+void HolaApp::refresh(http::Worker& w, WorkerCache& wc) {
+  uint64_t g = gen_.load(std::memory_order_acquire);
+  if (g != wc.gen) {
+    wc.gen = g;
+    wc.content = content();
+    const Content* c = wc.content.get();
+    const char* date = w.date();
+    wc.all.clear();
+    const assets::Asset* swagger = assets::find("swagger.json");
+    const assets::Asset* index = assets::find("index.html");
+    const assets::Asset* viewer = assets::find("swagger-ui.html");
+    std::string fallback_body;
+    if (c && c->ok) {
+      fallback_body = json::string_array({c->greeting, std::string(kFallbackGreeting)});
+    }
+    for (int ka = 0; ka < 2; ++ka) {
+      for (int head = 0; head < 2; ++head) {
+        ResponseSpec s;
+        s.keep_alive = ka;
+        s.head = head;
+        if (c && c->ok) {
+          s.status = 200;
+          s.cors = true;
+          s.content_type = kTextPlain;
+          s.body = c->greeting;
+        } else {
+          s.status = 500;
+          s.content_type = kHtml;
+          s.body = kUndertowError;
+        }
+        wc.hola[ka][head] = build_response(s, date);
+        ResponseSpec e = s;
+        e.status = 500;
+        e.cors = false;
+        e.content_type = kHtml;
+        e.body = kUndertowError;
+        wc.server_error[ka][head] = build_response(e, date);
+        if (c && c->ok) {
+          ResponseSpec f = s;
+          f.content_type = kJson;
+          f.body = fallback_body;
+          wc.chaining_fallback[ka][head] = build_response(f, date);
+        } else {
+          wc.chaining_fallback[ka][head] = wc.server_error[ka][head];
+        }
+        ResponseSpec h;
+        h.keep_alive = ka;
+        h.head = head;
+        h.cors = true;
+        h.content_type = kTextPlain;
+        h.body = "I'm ok";  // HolaResource.java:85
+        wc.health[ka][head] = build_response(h, date);
+        ResponseSpec sw = h;
+        sw.content_type = kJson;
+        sw.body = swagger ? swagger->view() : std::string_view("{}");
+        wc.swagger[ka][head] = build_response(sw, date);
+        ResponseSpec ix = h;
+        ix.cors = false;
+        ix.content_type = "text/html;charset=UTF-8";
+        ix.body = index ? index->view() : std::string_view();
+        wc.index[ka][head] = build_response(ix, date);
+        ix.body = viewer ? viewer->view() : std::string_view();
+        wc.viewer[ka][head] = build_response(ix, date);
+        ResponseSpec nf;
+        nf.keep_alive = ka;
+        nf.head = head;
+        nf.status = 404;
+        nf.content_type = kHtml;
+        nf.body = kUndertowNotFound;
+        wc.not_found[ka][head] = build_response(nf, date);
+        for (auto* p : {&wc.hola[ka][head], &wc.server_error[ka][head], &wc.chaining_fallback[ka][head],
+                        &wc.health[ka][head], &wc.swagger[ka][head], &wc.index[ka][head], &wc.viewer[ka][head],
+                        &wc.not_found[ka][head]})
+          wc.all.push_back(p);
+      }
+      ResponseSpec s;
+      s.keep_alive = ka;
+      s.cors = true;
+      s.status = 404;
+      wc.api_not_found[ka] = build_response(s, date);
+      s.status = 405;
+      s.extra_headers = std::string(kAllowApi);
+      wc.api_not_allowed[ka] = build_response(s, date);
+      s.status = 406;
+      s.extra_headers.clear();
+      wc.not_acceptable[ka] = build_response(s, date);
+      s.status = 200;
+      s.extra_headers = std::string(kAllowApi);
+      wc.api_options[ka] = build_response(s, date);
+      ResponseSpec so;
+      so.keep_alive = ka;
+      so.status = 200;
+      so.extra_headers = "Allow: GET, HEAD, OPTIONS\r\n";
+      wc.static_options[ka] = build_response(so, date);
+      so.status = 405;
+      so.content_type = kHtml;
+      so.body = kUndertowMethodNotAllowed;
+      so.extra_headers = "Allow: GET, HEAD, OPTIONS\r\n";
+      wc.not_allowed[ka] = build_response(so, date);
+      for (auto* p : {&wc.api_not_found[ka], &wc.api_not_allowed[ka], &wc.not_acceptable[ka], &wc.api_options[ka],
+                      &wc.static_options[ka], &wc.not_allowed[ka]})
+        wc.all.push_back(p);
+    }
+    wc.date_version = w.date_version();
+    return;
+  }
+  if (wc.date_version != w.date_version()) {
+    wc.date_version = w.date_version();
+    const char* d = w.date();
+    for (Prepared* p : wc.all) p->set_date(d);
+  }
+}
+
+std::string HolaApp::error_response(int status) {
+  ResponseSpec s;
+  s.status = status;
+  s.keep_alive = false;
+  char date[29];
+  format_http_date(wall_sec_coarse(), date);
+  return build_response(s, date).bytes;
+}
+
+namespace {
+
+enum class Method { kGet, kHead, kOptions, kOther };
+
+inline Method method_of(std::string_view m) {
+  if (m.size() == 3 && m == "GET") return Method::kGet;
+  if (m.size() == 4 && m == "HEAD") return Method::kHead;
+  if (m.size() == 7 && m == "OPTIONS") return Method::kOptions;
+  return Method::kOther;
+}
+
+inline bool path_is(std::string_view p, std::string_view route) {
+  // JAX-RS matching tolerates one trailing slash.
+  if (p.size() == route.size()) return p == route;
+  return p.size() == route.size() + 1 && p.back() == '/' && p.substr(0, route.size()) == route;
+}
+
+int route_of(std::string_view p) {
+  if (p.size() >= 4 && p.substr(0, 4) == "/api" && (p.size() == 4 || p[4] == '/')) {
+    std::string_view rest = p.substr(4);
+    if (path_is(rest, "/hola")) return HolaApp::kHola;
+    if (path_is(rest, "/hola-chaining")) return HolaApp::kChaining;
+    if (path_is(rest, "/health")) return HolaApp::kHealth;
+    if (rest == "/swagger.json") return HolaApp::kSwagger;
+    return HolaApp::kApiNotFound;
+  }
+  if (p == "/" || p == "/index.html") return HolaApp::kIndex;
+  if (p == "/hystrix.stream") return HolaApp::kHystrix;
+  if (p == "/metrics") return HolaApp::kMetrics;
+  if (p == "/webjars/swagger-ui/2.1.4/" || p == "/webjars/swagger-ui/2.1.4/index.html" ||
+      p == "/webjars/swagger-ui/2.1.4")
+    return HolaApp::kViewer;
+  return HolaApp::kNotFound;
+}
+
+}  // namespace
+
+void HolaApp::on_request(http::Connection& c, const http::Request& r) {
+  http::Worker& w = c.worker();
+  WorkerCache& wc = cache(w);
+  if (__builtin_expect(wc.gen != gen_.load(std::memory_order_relaxed) || wc.date_version != w.date_version(), 0))
+    refresh(w, wc);
+  const int ka = r.keep_alive ? 1 : 0;
+  if (!ka) c.close_after_response();
+
+  std::string_view path = r.path;
+  char decoded[512];
+  if (path.find('%') != std::string_view::npos) {
+    size_t n = 0;
+    if (path.size() <= sizeof decoded && http::percent_decode(path, decoded, &n)) path = std::string_view(decoded, n);
+  }
+  const int route = route_of(path);
+  const Method m = method_of(r.method);
+  const int head = m == Method::kHead ? 1 : 0;
+  if (prom_) prom_->count(w.index(), route);
+
+  switch (route) {
+    case kHola:
+    case kHealth:
+    case kChaining:
+    case kSwagger: {
+      if (m == Method::kOptions) {
+        c.send(wc.api_options[ka].view());
+        return;
+      }
+      if (m == Method::kOther) {
+        c.send(wc.api_not_allowed[ka].view());
+        return;
+      }
+      std::string_view subtype = (route == kChaining || route == kSwagger) ? "json" : "plain";
+      std::string_view type = (route == kChaining || route == kSwagger) ? "application" : "text";
+      if (r.has_accept && !http::accepts(r.accept, type, subtype)) {
+        c.send(wc.not_acceptable[ka].view());
+        return;
+      }
+      if (route == kHola) {
+        if (tracer_ && tracer_->enabled()) {
+          tracing::ServerSpan span = tracer_->begin_server(w.index(), r);
+          c.send(wc.hola[ka][head].view());
+          tracer_->end_server(w.index(), span, wc.content && wc.content->ok ? 200 : 500);
+        } else {
+          c.send(wc.hola[ka][head].view());
+        }
+      } else if (route == kHealth) {
+        c.send(wc.health[ka][head].view());
+      } else if (route == kSwagger) {
+        c.send(wc.swagger[ka][head].view());
+      } else {
+        handle_chaining(c, r, wc, 0);
+      }
+      return;
+    }
+    case kApiNotFound:
+      c.send(wc.api_not_found[ka].view());
+      return;
+    case kIndex:
+    case kViewer:
+      if (m == Method::kOptions) c.send(wc.static_options[ka].view());
+      else if (m == Method::kOther) c.send(wc.not_allowed[ka].view());
+      else c.send((route == kIndex ? wc.index : wc.viewer)[ka][head].view());
+      return;
+    case kHystrix:
+      if (hystrix_ && m == Method::kGet) {
+        hystrix_->subscribe(c, r);
+      } else if (m == Method::kOther || m == Method::kOptions || !hystrix_) {
+        c.send(hystrix_ ? wc.not_allowed[ka].view() : wc.not_found[ka][head].view());
+      } else {
+        c.send(wc.not_found[ka][head].view());  // HEAD on a stream: nothing to describe
+      }
+      return;
+    case kMetrics:
+      if (prom_ && o_.enable_metrics_endpoint && (m == Method::kGet || m == Method::kHead)) {
+        std::string body = prom_->render(server_);
+        ResponseSpec s;
+        s.keep_alive = ka;
+        s.head = head;
+        s.content_type = "text/plain; version=0.0.4";
+        s.body = body;
+        c.send(build_response(s, w.date()).view());
+      } else {
+        c.send(wc.not_found[ka][head].view());
+      }
+      return;
+    default:
+      c.send(wc.not_found[ka][head].view());
+      return;
+  }
+}
+
+void HolaApp::handle_chaining(http::Connection& c, const http::Request& r, WorkerCache& wc, int64_t) {
+  const int ka = r.keep_alive ? 1 : 0;
+  const int head = r.method == "HEAD" ? 1 : 0;
+  if (!wc.content || !wc.content->ok) {
+    // hola() throws before the downstream call is made (HolaResource.java:75)
+    c.send(wc.server_error[ka][head].view());
+    return;
+  }
+  tracing::ServerSpan span;
+  bool traced = tracer_ && tracer_->enabled();
+  if (traced) span = tracer_->begin_server(c.worker().index(), r);
+  if (!chainer_) {
+    c.send(wc.chaining_fallback[ka][head].view());
+    if (traced) tracer_->end_server(c.worker().index(), span, 200);
+    return;
+  }
+  // Async: the connection is parked until aloha answers, times out or is short-circuited.
+  c.park();
+  c.hold();
+  http::Connection* conn = &c;
+  std::shared_ptr<const Content> content = wc.content;
+  HolaApp* self = this;
+  chainer_->call(c.worker(), traced ? &span.ctx : nullptr,
+                 [self, conn, content, ka, head, traced, span](const ChainResult& res) {
+                   http::Worker& w = conn->worker();
+                   if (!conn->closed()) {
+                     std::vector<std::optional<std::string>> items;
+                     items.reserve(1 + res.items.size());
+                     items.push_back(content->greeting);
+                     for (auto& s : res.items) items.push_back(s);
+                     std::string body = json::string_array(items);
+                     ResponseSpec s;
+                     s.keep_alive = ka;
+                     s.head = head;
+                     s.cors = true;
+                     s.content_type = kJson;
+                     s.body = body;
+                     conn->complete(build_response(s, w.date()).view(), ka);
+                   }
+                   if (traced) self->tracer_->end_server(w.index(), span, 200);
+                   conn->release();
+                 });
+}
+
+}  // namespace hola::app

@@ -1,0 +1,397 @@
+#include "client/http_client.h"
+
+#include <errno.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+
+#include "core/net.h"
+#include "http/parser.h"
+
+namespace hola::client {
+
+// ---------------------------------------------------------------- AddressCache
+
+AddressCache::AddressCache(std::string host, int port, int refresh_ms)
+    : host_(std::move(host)), port_(port), refresh_ms_(refresh_ms) {}
+
+AddressCache::~AddressCache() { stop(); }
+
+void AddressCache::resolve_now() {
+  sockaddr_storage ss{};
+  socklen_t len = 0;
+  std::string err;
+  bool ok = resolve_host(host_, port_, &ss, &len, &err);
+  std::lock_guard<std::mutex> g(mu_);
+  ok_ = ok;
+  if (ok) {
+    addr_ = ss;
+    len_ = len;
+    err_.clear();
+  } else {
+    err_ = "UnknownHostException: " + err;
+  }
+}
+
+void AddressCache::start() {
+  th_ = std::thread([this] {
+    while (!stop_.load()) {
+      resolve_now();
+      for (int waited = 0; waited < refresh_ms_ && !stop_.load(); waited += 50)
+        std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    }
+  });
+}
+
+void AddressCache::stop() {
+  stop_.store(true);
+  if (th_.joinable()) th_.join();
+}
+
+bool AddressCache::get(sockaddr_storage* out, socklen_t* len, std::string* err) const {
+  std::lock_guard<std::mutex> g(mu_);
+  if (!ok_) {
+    if (err) *err = err_;
+    return false;
+  }
+  *out = addr_;
+  *len = len_;
+  return true;
+}
+
+// ---------------------------------------------------------------- connection
+
+struct ClientPool::Conn final : EventLoop::Handler {
+  enum State { kConnecting, kWriting, kReading, kIdle, kDead };
+  ClientPool* pool = nullptr;
+  int fd = -1;
+  State st = kDead;
+  std::string out;
+  size_t off = 0;
+  std::string in;
+  uint64_t id = 0;
+  Callback cb;
+  bool reused = false;
+  std::string req;
+  uint32_t interest = 0;
+
+  void set_interest(uint32_t ev) {
+    if (ev == interest) return;
+    interest = ev;
+    pool->loop_.mod(fd, ev, this);
+  }
+  void fail(const std::string& why);
+  void on_event(uint32_t ev) override;
+  void do_write();
+  void do_read();
+  // Returns 1 complete, 0 need more, -1 malformed; sets *keep on completion.
+  int try_parse(ClientResult* r, bool* keep, bool eof);
+};
+
+void ClientPool::Conn::fail(const std::string& why) {
+  // A kept-alive socket the server had already closed: retry once on a fresh connection.
+  if (reused && in.empty() && st != kConnecting) {
+    ClientPool* p = pool;
+    uint64_t rid = id;
+    Callback c = std::move(cb);
+    std::string r = req;
+    p->active_.erase(rid);
+    p->destroy(this);
+    auto* fresh = new Conn();
+    fresh->pool = p;
+    p->start_on(fresh, rid, r, std::move(c), false);
+    return;
+  }
+  ClientResult res;
+  res.ok = false;
+  res.error = why;
+  pool->finish(this, std::move(res), false);
+}
+
+void ClientPool::Conn::on_event(uint32_t ev) {
+  if (st == kDead) return;
+  if (st == kIdle) {
+    // Anything on an idle connection is a close or junk: drop it.
+    pool->idle_.erase(std::remove(pool->idle_.begin(), pool->idle_.end(), this), pool->idle_.end());
+    pool->destroy(this);
+    return;
+  }
+  if (st == kConnecting) {
+    int soerr = 0;
+    socklen_t sl = sizeof soerr;
+    getsockopt(fd, SOL_SOCKET, SO_ERROR, &soerr, &sl);
+    if (soerr != 0 || (ev & (EPOLLERR | EPOLLHUP))) {
+      fail(std::string("ConnectException: ") + strerror(soerr ? soerr : ECONNREFUSED));
+      return;
+    }
+    st = kWriting;
+  }
+  if (st == kWriting) {
+    do_write();
+    return;
+  }
+  if (st == kReading) do_read();
+}
+
+void ClientPool::Conn::do_write() {
+  while (off < out.size()) {
+    ssize_t w = ::send(fd, out.data() + off, out.size() - off, MSG_NOSIGNAL);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      if (errno == EAGAIN) {
+        set_interest(EPOLLOUT);
+        return;
+      }
+      fail(std::string("SocketException: ") + strerror(errno));
+      return;
+    }
+    off += size_t(w);
+  }
+  st = kReading;
+  set_interest(EPOLLIN | EPOLLRDHUP);
+}
+
+int ClientPool::Conn::try_parse(ClientResult* r, bool* keep, bool eof) {
+  size_t he = in.find("\r\n\r\n");
+  if (he == std::string::npos) return in.size() > 64 * 1024 ? -1 : 0;
+  std::string_view head(in.data(), he);
+  if (head.size() < 12 || head.substr(0, 5) != "HTTP/") return -1;
+  int status = atoi(std::string(head.substr(9, 3)).c_str());
+  if (status < 100) return -1;
+  bool http10 = head.substr(5, 3) == "1.0";
+  int64_t cl = -1;
+  bool chunked = false, close = http10;
+  size_t p = head.find("\r\n");
+  while (p != std::string_view::npos && p + 2 <= head.size()) {
+    size_t n = head.find("\r\n", p + 2);
+    std::string_view line = head.substr(p + 2, n == std::string_view::npos ? std::string_view::npos : n - p - 2);
+    size_t colon = line.find(':');
+    if (colon != std::string_view::npos) {
+      std::string_view k = line.substr(0, colon), v = line.substr(colon + 1);
+      while (!v.empty() && (v.front() == ' ' || v.front() == '\t')) v.remove_prefix(1);
+      if (http::iequals(k, "content-length")) cl = atoll(std::string(v).c_str());
+      else if (http::iequals(k, "transfer-encoding") && v.find("chunked") != std::string_view::npos) chunked = true;
+      else if (http::iequals(k, "connection")) {
+        if (http::iequals(v, "close")) close = true;
+        else if (http::iequals(v, "keep-alive")) close = false;
+      }
+    }
+    p = n;
+  }
+  size_t body = he + 4;
+  if (status == 204 || status == 304 || (status >= 100 && status < 200)) {
+    r->status = status;
+    *keep = !close;
+    return 1;
+  }
+  if (chunked) {
+    size_t consumed = 0;
+    http::Parse q = http::skip_chunked_body(in.data() + body, in.size() - body, &consumed);
+    if (q == http::Parse::kError) return -1;
+    if (q == http::Parse::kIncomplete) return in.size() > (1 << 20) ? -1 : 0;
+    std::string out;
+    size_t i = body;
+    for (;;) {
+      size_t nl = in.find("\r\n", i);
+      size_t sz = strtoul(in.substr(i, nl - i).c_str(), nullptr, 16);
+      i = nl + 2;
+      if (sz == 0) break;
+      out.append(in, i, sz);
+      i += sz + 2;
+    }
+    r->status = status;
+    r->body = std::move(out);
+    *keep = !close && body + consumed == in.size();
+    return 1;
+  }
+  if (cl >= 0) {
+    if (cl > (1 << 20)) return -1;
+    if (in.size() - body < size_t(cl)) return 0;
+    r->status = status;
+    r->body = in.substr(body, size_t(cl));
+    *keep = !close && body + size_t(cl) == in.size();
+    return 1;
+  }
+  // close-delimited body
+  if (!eof) return in.size() > (1 << 20) ? -1 : 0;
+  r->status = status;
+  r->body = in.substr(body);
+  *keep = false;
+  return 1;
+}
+
+void ClientPool::Conn::do_read() {
+  char buf[16384];
+  for (;;) {
+    ssize_t n = ::recv(fd, buf, sizeof buf, 0);
+    bool eof = false;
+    if (n > 0) {
+      in.append(buf, size_t(n));
+      reused = false;  // the server answered: no silent retry from here on
+    } else if (n == 0) {
+      eof = true;
+    } else {
+      if (errno == EINTR) continue;
+      if (errno == EAGAIN) return;
+      fail(std::string("SocketException: ") + strerror(errno));
+      return;
+    }
+    ClientResult r;
+    bool keep = false;
+    int rc = try_parse(&r, &keep, eof);
+    if (rc < 0) {
+      fail("ClientProtocolException: malformed response");
+      return;
+    }
+    if (rc == 1) {
+      r.ok = true;
+      pool->finish(this, std::move(r), keep && !eof);
+      return;
+    }
+    if (eof) {
+      fail(in.empty() ? "NoHttpResponseException: connection closed" : "TruncatedChunkException: premature EOF");
+      return;
+    }
+    if (size_t(n) < sizeof buf) return;  // drained for now (level-triggered)
+  }
+}
+
+// ---------------------------------------------------------------- pool
+
+ClientPool::ClientPool(EventLoop& loop, Url target, AddressCache* addr, size_t max_idle)
+    : loop_(loop), target_(std::move(target)), addr_(addr), max_idle_(max_idle) {
+  host_header_ = target_.host;
+  if (target_.port != 80) host_header_ += ":" + std::to_string(target_.port);
+}
+
+ClientPool::~ClientPool() {
+  for (Conn* c : idle_) {
+    if (c->fd >= 0) ::close(c->fd);
+    delete c;
+  }
+  for (auto& [id, c] : active_) {
+    if (c->fd >= 0) {
+      loop_.del(c->fd);
+      ::close(c->fd);
+    }
+    delete c;
+  }
+}
+
+std::string ClientPool::build_request(const std::string& path, const std::string& extra) const {
+  std::string r;
+  r.reserve(128 + extra.size());
+  r += "GET ";
+  r += path;
+  r += " HTTP/1.1\r\nHost: ";
+  r += host_header_;
+  r += "\r\nAccept: application/json\r\nConnection: keep-alive\r\n";
+  r += extra;
+  r += "\r\n";
+  return r;
+}
+
+uint64_t ClientPool::get(const std::string& path, const std::string& extra_headers, Callback cb) {
+  uint64_t id = next_id_++;
+  std::string req = build_request(path, extra_headers);
+  if (!idle_.empty()) {
+    Conn* c = idle_.back();
+    idle_.pop_back();
+    start_on(c, id, req, std::move(cb), true);
+  } else {
+    auto* c = new Conn();
+    c->pool = this;
+    start_on(c, id, req, std::move(cb), false);
+  }
+  return id;
+}
+
+void ClientPool::start_on(Conn* c, uint64_t id, const std::string& req, Callback cb, bool reused) {
+  c->id = id;
+  c->cb = std::move(cb);
+  c->req = req;
+  c->out = req;
+  c->off = 0;
+  c->in.clear();
+  c->reused = reused;
+  active_[id] = c;
+  if (reused) {
+    c->st = Conn::kWriting;
+    c->do_write();
+    return;
+  }
+  sockaddr_storage ss{};
+  socklen_t len = 0;
+  std::string err;
+  if (!addr_ || !addr_->get(&ss, &len, &err)) {
+    // Report asynchronously: callers expect the callback after get() returns.
+    c->st = Conn::kDead;
+    loop_.add_timer(0, [this, id, err] {
+      auto it = active_.find(id);
+      if (it == active_.end()) return;
+      ClientResult r;
+      r.error = err;
+      finish(it->second, std::move(r), false);
+    });
+    return;
+  }
+  bool inprog = false;
+  c->fd = connect_nonblocking(ss, len, &inprog);
+  if (c->fd < 0) {
+    std::string e = std::string("ConnectException: ") + strerror(errno);
+    c->st = Conn::kDead;
+    loop_.add_timer(0, [this, id, e] {
+      auto it = active_.find(id);
+      if (it == active_.end()) return;
+      ClientResult r;
+      r.error = e;
+      finish(it->second, std::move(r), false);
+    });
+    return;
+  }
+  ++opened_;
+  c->interest = EPOLLOUT;
+  loop_.add(c->fd, EPOLLOUT, c);
+  c->st = inprog ? Conn::kConnecting : Conn::kWriting;
+  if (!inprog) c->do_write();
+}
+
+void ClientPool::finish(Conn* c, ClientResult&& r, bool reusable) {
+  active_.erase(c->id);
+  Callback cb = std::move(c->cb);
+  c->cb = nullptr;
+  if (reusable && c->fd >= 0 && idle_.size() < max_idle_) {
+    c->st = Conn::kIdle;
+    c->in.clear();
+    c->set_interest(EPOLLIN | EPOLLRDHUP);
+    idle_.push_back(c);
+  } else {
+    destroy(c);
+  }
+  if (cb) cb(std::move(r));
+}
+
+void ClientPool::destroy(Conn* c) {
+  if (c->fd >= 0) {
+    loop_.del(c->fd);
+    ::close(c->fd);
+    c->fd = -1;
+  }
+  c->st = Conn::kDead;
+  c->cb = nullptr;
+  loop_.retire(c);
+}
+
+void ClientPool::cancel(uint64_t id) {
+  auto it = active_.find(id);
+  if (it == active_.end()) return;
+  Conn* c = it->second;
+  active_.erase(it);
+  destroy(c);
+}
+
+}  // namespace hola::client

@@ -1,0 +1,76 @@
+#include "core/affinity.h"
+
+#include <pthread.h>
+#include <sched.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+
+namespace hola {
+
+bool parse_cpu_list(const std::string& s, std::vector<int>* out) {
+  out->clear();
+  size_t i = 0;
+  while (i < s.size()) {
+    size_t j = s.find(',', i);
+    if (j == std::string::npos) j = s.size();
+    std::string tok = s.substr(i, j - i);
+    i = j + 1;
+    if (tok.empty()) continue;
+    size_t dash = tok.find('-');
+    char* end = nullptr;
+    long a = strtol(tok.c_str(), &end, 10);
+    if (end == tok.c_str() || a < 0) return false;
+    long b = a;
+    if (dash != std::string::npos) {
+      b = strtol(tok.c_str() + dash + 1, &end, 10);
+      if (*end || b < a) return false;
+    } else if (*end) {
+      return false;
+    }
+    for (long c = a; c <= b; ++c) out->push_back(int(c));
+  }
+  return true;
+}
+
+std::string format_cpu_list(const std::vector<int>& cpus) {
+  std::string r;
+  size_t i = 0;
+  while (i < cpus.size()) {
+    size_t j = i;
+    while (j + 1 < cpus.size() && cpus[j + 1] == cpus[j] + 1) ++j;
+    if (!r.empty()) r += ",";
+    r += std::to_string(cpus[i]);
+    if (j > i) r += "-" + std::to_string(cpus[j]);
+    i = j + 1;
+  }
+  return r;
+}
+
+std::vector<int> allowed_cpus() {
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  std::vector<int> r;
+  if (sched_getaffinity(0, sizeof set, &set) != 0) return r;
+  for (int c = 0; c < CPU_SETSIZE; ++c)
+    if (CPU_ISSET(c, &set)) r.push_back(c);
+  return r;
+}
+
+bool pin_current_thread(int cpu) {
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  CPU_SET(cpu, &set);
+  return pthread_setaffinity_np(pthread_self(), sizeof set, &set) == 0;
+}
+
+double cgroup_cpu_quota() {
+  std::ifstream f("/sys/fs/cgroup/cpu.max");
+  std::string q, p;
+  if (!(f >> q >> p) || q == "max") return 0;
+  double qv = atof(q.c_str()), pv = atof(p.c_str());
+  return pv > 0 ? qv / pv : 0;
+}
+
+}  // namespace hola

@@ -1,0 +1,18 @@
+// CPU pinning helpers: one event loop per pinned host core.
+#pragma once
+#include <string>
+#include <vector>
+
+namespace hola {
+
+// Parses a Linux cpu-list ("0-3,8,10-11"); false on syntax error.
+bool parse_cpu_list(const std::string& s, std::vector<int>* out);
+std::string format_cpu_list(const std::vector<int>& cpus);
+// CPUs in this process' affinity mask.
+std::vector<int> allowed_cpus();
+// Pins the calling thread to one CPU; false on failure (e.g. CPU not in the cgroup).
+bool pin_current_thread(int cpu);
+// CPU quota from cgroup v2 cpu.max (e.g. 16.0 for "1600000 100000"); 0 when unlimited.
+double cgroup_cpu_quota();
+
+}  // namespace hola

@@ -1,0 +1,61 @@
+// Clocks. The service never reads time through anything but these helpers so that the
+// resilience code (rolling windows, breaker sleep window) can be driven by a fake clock in
+// tests — the reference relies on Hystrix's wall-clock timers (config.properties:17,19).
+#pragma once
+#include <atomic>
+#include <cstdint>
+#include <ctime>
+
+namespace hola {
+
+inline int64_t mono_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return int64_t(ts.tv_sec) * 1000000000 + ts.tv_nsec;
+}
+inline int64_t mono_ms() { return mono_ns() / 1000000; }
+inline int64_t wall_us() {
+  timespec ts;
+  clock_gettime(CLOCK_REALTIME, &ts);
+  return int64_t(ts.tv_sec) * 1000000 + ts.tv_nsec / 1000;
+}
+inline int64_t wall_ms() { return wall_us() / 1000; }
+// Coarse (jiffy-resolution) wall clock seconds: used for the HTTP Date header.
+inline int64_t wall_sec_coarse() {
+  timespec ts;
+  clock_gettime(CLOCK_REALTIME_COARSE, &ts);
+  return ts.tv_sec;
+}
+
+// Millisecond clock abstraction for the resilience layer.
+class Clock {
+ public:
+  virtual ~Clock() = default;
+  virtual int64_t now_ms() const = 0;
+};
+
+class SystemClock final : public Clock {
+ public:
+  int64_t now_ms() const override { return mono_ms(); }
+  static SystemClock& instance() {
+    static SystemClock c;
+    return c;
+  }
+};
+
+class FakeClock final : public Clock {
+ public:
+  explicit FakeClock(int64_t start = 1000000) : t_(start) {}
+  int64_t now_ms() const override { return t_.load(std::memory_order_relaxed); }
+  void advance(int64_t ms) { t_.fetch_add(ms, std::memory_order_relaxed); }
+  void set(int64_t ms) { t_.store(ms, std::memory_order_relaxed); }
+
+ private:
+  std::atomic<int64_t> t_;
+};
+
+// Formats `sec` (Unix time) as an IMF-fixdate, e.g. "Thu, 15 Oct 2026 21:52:00 GMT".
+// Writes exactly 29 bytes to out.
+void format_http_date(int64_t sec, char out[29]);
+
+}  // namespace hola

@@ -1,0 +1,56 @@
+// Asynchronous console logger. Request threads only enqueue; one background
+// thread writes to stderr. The reference instead println()s the config path on every request
+// (Configuration.java:28), serialising all workers on the stdout lock; here log lines happen
+// only on events (config change, outbound call with Feign BASIC logging, errors).
+#pragma once
+#include <atomic>
+#include <condition_variable>
+#include <cstdarg>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <thread>
+
+namespace hola {
+
+enum class LogLevel : int { kDebug = 0, kInfo = 1, kWarn = 2, kError = 3, kOff = 4 };
+
+class Logger {
+ public:
+  static Logger& instance();
+  void set_level(LogLevel l) { level_.store(int(l), std::memory_order_relaxed); }
+  LogLevel level() const { return LogLevel(level_.load(std::memory_order_relaxed)); }
+  bool enabled(LogLevel l) const { return int(l) >= level_.load(std::memory_order_relaxed); }
+  void log(LogLevel l, const char* fmt, ...) __attribute__((format(printf, 3, 4)));
+  void vlog(LogLevel l, const char* fmt, va_list ap);
+  // Blocks until every queued line has been written.
+  void flush();
+  uint64_t dropped() const { return dropped_.load(std::memory_order_relaxed); }
+  ~Logger();
+
+ private:
+  Logger();
+  void run();
+  std::atomic<int> level_{int(LogLevel::kInfo)};
+  std::mutex mu_;
+  std::condition_variable cv_, flushed_;
+  std::deque<std::string> q_;
+  bool stop_ = false;
+  uint64_t written_ = 0, enqueued_ = 0;
+  std::atomic<uint64_t> dropped_{0};
+  std::thread th_;
+};
+
+bool parse_log_level(const std::string& s, LogLevel* out);
+
+}  // namespace hola
+
+#define HOLA_LOG(lvl, ...)                                                 \
+  do {                                                                     \
+    if (::hola::Logger::instance().enabled(lvl))                           \
+      ::hola::Logger::instance().log(lvl, __VA_ARGS__);                    \
+  } while (0)
+#define LOG_DEBUG(...) HOLA_LOG(::hola::LogLevel::kDebug, __VA_ARGS__)
+#define LOG_INFO(...) HOLA_LOG(::hola::LogLevel::kInfo, __VA_ARGS__)
+#define LOG_WARN(...) HOLA_LOG(::hola::LogLevel::kWarn, __VA_ARGS__)
+#define LOG_ERROR(...) HOLA_LOG(::hola::LogLevel::kError, __VA_ARGS__)

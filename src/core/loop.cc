@@ -1,0 +1,133 @@
+#include "core/loop.h"
+
+#include <errno.h>
+#include <sys/eventfd.h>
+#include <unistd.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+#include "core/clock.h"
+
+namespace hola {
+
+EventLoop::EventLoop() {
+  epfd_ = epoll_create1(EPOLL_CLOEXEC);
+  wakefd_ = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
+  if (epfd_ < 0 || wakefd_ < 0) {
+    perror("event loop init");
+    abort();
+  }
+  wake_.loop = this;
+  add(wakefd_, EPOLLIN, &wake_);
+  now_ms_ = mono_ms();
+}
+
+EventLoop::~EventLoop() {
+  for (Handler* h : retired_) delete h;
+  if (wakefd_ >= 0) ::close(wakefd_);
+  if (epfd_ >= 0) ::close(epfd_);
+}
+
+bool EventLoop::add(int fd, uint32_t events, Handler* h) {
+  epoll_event ev{};
+  ev.events = events;
+  ev.data.ptr = h;
+  return epoll_ctl(epfd_, EPOLL_CTL_ADD, fd, &ev) == 0;
+}
+
+bool EventLoop::mod(int fd, uint32_t events, Handler* h) {
+  epoll_event ev{};
+  ev.events = events;
+  ev.data.ptr = h;
+  return epoll_ctl(epfd_, EPOLL_CTL_MOD, fd, &ev) == 0;
+}
+
+void EventLoop::del(int fd) { epoll_ctl(epfd_, EPOLL_CTL_DEL, fd, nullptr); }
+
+EventLoop::TimerId EventLoop::add_timer(int64_t delay_ms, std::function<void()> cb) {
+  TimerId id = next_timer_++;
+  heap_.push({mono_ms() + (delay_ms < 0 ? 0 : delay_ms), id});
+  timers_.emplace(id, std::move(cb));
+  return id;
+}
+
+void EventLoop::cancel_timer(TimerId id) { timers_.erase(id); }
+
+void EventLoop::post(std::function<void()> fn) {
+  {
+    std::lock_guard<std::mutex> g(post_mu_);
+    posted_.push_back(std::move(fn));
+  }
+  uint64_t one = 1;
+  ssize_t r = ::write(wakefd_, &one, sizeof one);
+  (void)r;
+}
+
+void EventLoop::stop() {
+  stop_.store(true, std::memory_order_relaxed);
+  uint64_t one = 1;
+  ssize_t r = ::write(wakefd_, &one, sizeof one);
+  (void)r;
+}
+
+void EventLoop::WakeHandler::on_event(uint32_t) {
+  uint64_t v;
+  while (::read(loop->wakefd_, &v, sizeof v) > 0) {
+  }
+  loop->drain_posted();
+}
+
+void EventLoop::drain_posted() {
+  std::vector<std::function<void()>> fns;
+  {
+    std::lock_guard<std::mutex> g(post_mu_);
+    fns.swap(posted_);
+  }
+  for (auto& f : fns) f();
+}
+
+void EventLoop::run_timers() {
+  while (!heap_.empty() && heap_.top().deadline <= now_ms_) {
+    TimerId id = heap_.top().id;
+    heap_.pop();
+    auto it = timers_.find(id);
+    if (it == timers_.end()) continue;  // cancelled
+    auto cb = std::move(it->second);
+    timers_.erase(it);
+    cb();
+  }
+  // Drop cancelled entries at the top so they do not cause spurious wakeups.
+  while (!heap_.empty() && !timers_.count(heap_.top().id)) heap_.pop();
+}
+
+int EventLoop::next_timeout_ms() {
+  if (heap_.empty()) return -1;
+  int64_t d = heap_.top().deadline - mono_ms();
+  if (d <= 0) return 0;
+  return d > 1000000 ? 1000000 : int(d);
+}
+
+void EventLoop::run() {
+  constexpr int kMaxEvents = 256;
+  epoll_event evs[kMaxEvents];
+  while (!stop_.load(std::memory_order_relaxed)) {
+    if (tick_) tick_();
+    int n = epoll_wait(epfd_, evs, kMaxEvents, next_timeout_ms());
+    if (n < 0 && errno != EINTR) {
+      perror("epoll_wait");
+      break;
+    }
+    now_ms_ = mono_ms();
+    for (int i = 0; i < n; ++i) static_cast<Handler*>(evs[i].data.ptr)->on_event(evs[i].events);
+    if (!heap_.empty()) run_timers();
+    if (!retired_.empty()) {
+      for (Handler* h : retired_) delete h;
+      retired_.clear();
+    }
+  }
+  drain_posted();
+  if (on_exit_) on_exit_();
+}
+
+}  // namespace hola

@@ -1,0 +1,87 @@
+// Single-threaded epoll event loop with a timer heap and a cross-thread task queue.
+//
+// This replaces Undertow's IO-thread + worker-thread-pool pair (SURVEY.md T1, §2d "request
+// concurrency"): each loop is pinned to one host core and owns its connections outright, so
+// the hot path has no locks, no thread hand-off and no per-request allocation. Timers drive
+// the outbound 600 ms timeout (config.properties:17) instead of Hystrix's timer thread.
+#pragma once
+#include <sys/epoll.h>
+
+#include <atomic>
+#include <cstdint>
+#include <functional>
+#include <mutex>
+#include <queue>
+#include <unordered_map>
+#include <vector>
+
+namespace hola {
+
+class EventLoop {
+ public:
+  struct Handler {
+    virtual ~Handler() = default;
+    virtual void on_event(uint32_t events) = 0;
+  };
+  using TimerId = uint64_t;
+
+  EventLoop();
+  ~EventLoop();
+  EventLoop(const EventLoop&) = delete;
+  EventLoop& operator=(const EventLoop&) = delete;
+
+  bool add(int fd, uint32_t events, Handler* h);
+  bool mod(int fd, uint32_t events, Handler* h);
+  void del(int fd);
+
+  // One-shot timer; callback runs on the loop thread. Returns an id usable with cancel_timer.
+  TimerId add_timer(int64_t delay_ms, std::function<void()> cb);
+  void cancel_timer(TimerId id);
+
+  // Thread-safe: run fn on the loop thread soon.
+  void post(std::function<void()> fn);
+  // Handlers whose lifetime ends inside an event batch are deleted after the batch.
+  void retire(Handler* h) { retired_.push_back(h); }
+
+  void run();
+  void stop();  // thread-safe
+  bool stopping() const { return stop_.load(std::memory_order_relaxed); }
+
+  // Millisecond monotonic time cached at the top of each iteration.
+  int64_t now_ms() const { return now_ms_; }
+  // Called once per iteration before blocking (e.g. refresh cached Date header).
+  void set_tick(std::function<void()> fn) { tick_ = std::move(fn); }
+  // Optional callback when the loop exits run().
+  void set_on_exit(std::function<void()> fn) { on_exit_ = std::move(fn); }
+
+ private:
+  struct WakeHandler : Handler {
+    EventLoop* loop;
+    void on_event(uint32_t) override;
+  };
+  struct TimerEntry {
+    int64_t deadline;
+    TimerId id;
+    bool operator>(const TimerEntry& o) const {
+      return deadline != o.deadline ? deadline > o.deadline : id > o.id;
+    }
+  };
+  void run_timers();
+  void drain_posted();
+  int next_timeout_ms();
+
+  int epfd_ = -1;
+  int wakefd_ = -1;
+  WakeHandler wake_;
+  std::atomic<bool> stop_{false};
+  int64_t now_ms_ = 0;
+  std::priority_queue<TimerEntry, std::vector<TimerEntry>, std::greater<TimerEntry>> heap_;
+  std::unordered_map<TimerId, std::function<void()>> timers_;
+  TimerId next_timer_ = 1;
+  std::mutex post_mu_;
+  std::vector<std::function<void()>> posted_;
+  std::vector<Handler*> retired_;
+  std::function<void()> tick_, on_exit_;
+};
+
+}  // namespace hola

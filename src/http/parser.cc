@@ -1,0 +1,311 @@
+#include "http/parser.h"
+
+#include <cstring>
+
+namespace hola::http {
+
+namespace {
+
+inline char lower(char c) { return (c >= 'A' && c <= 'Z') ? char(c + 32) : c; }
+
+inline bool is_tchar(unsigned char c) {
+  // RFC 9110 token characters.
+  static const bool* table = [] {
+    static bool t[256] = {false};
+    for (int c = '0'; c <= '9'; ++c) t[c] = true;
+    for (int c = 'a'; c <= 'z'; ++c) t[c] = true;
+    for (int c = 'A'; c <= 'Z'; ++c) t[c] = true;
+    for (char c : std::string_view("!#$%&'*+-.^_`|~")) t[(unsigned char)c] = true;
+    return t;
+  }();
+  return table[c];
+}
+
+inline std::string_view trim_ows(std::string_view s) {
+  while (!s.empty() && (s.front() == ' ' || s.front() == '\t')) s.remove_prefix(1);
+  while (!s.empty() && (s.back() == ' ' || s.back() == '\t')) s.remove_suffix(1);
+  return s;
+}
+
+// Iterates comma-separated tokens of a Connection header.
+template <class F>
+void for_each_token(std::string_view v, F f) {
+  while (!v.empty()) {
+    size_t c = v.find(',');
+    std::string_view t = trim_ows(v.substr(0, c));
+    if (!t.empty()) f(t);
+    if (c == std::string_view::npos) break;
+    v.remove_prefix(c + 1);
+  }
+}
+
+bool parse_uint(std::string_view s, int64_t* out) {
+  if (s.empty() || s.size() > 18) return false;
+  int64_t v = 0;
+  for (char c : s) {
+    if (c < '0' || c > '9') return false;
+    v = v * 10 + (c - '0');
+  }
+  *out = v;
+  return true;
+}
+
+}  // namespace
+
+bool iequals(std::string_view a, std::string_view b) {
+  if (a.size() != b.size()) return false;
+  for (size_t i = 0; i < a.size(); ++i)
+    if (lower(a[i]) != lower(b[i])) return false;
+  return true;
+}
+
+bool percent_decode(std::string_view in, char* out, size_t* out_len) {
+  auto hex = [](char c) -> int {
+    if (c >= '0' && c <= '9') return c - '0';
+    c = lower(c);
+    if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+    return -1;
+  };
+  size_t o = 0;
+  for (size_t i = 0; i < in.size(); ++i) {
+    if (in[i] == '%') {
+      if (i + 2 >= in.size()) return false;
+      int h = hex(in[i + 1]), l = hex(in[i + 2]);
+      if (h < 0 || l < 0) return false;
+      out[o++] = char(h * 16 + l);
+      i += 2;
+    } else {
+      out[o++] = in[i];
+    }
+  }
+  *out_len = o;
+  return true;
+}
+
+Parse parse_request(const char* buf, size_t len, Request* req, int* status) {
+  *req = Request();
+  size_t pos = 0;
+  // RFC 9112 §2.2: ignore at least one empty line before the request-line.
+  while (pos < len && (buf[pos] == '\r' || buf[pos] == '\n')) ++pos;
+  if (pos == len) return Parse::kIncomplete;
+
+  // ---- request line ----
+  const char* line = buf + pos;
+  const char* nl = static_cast<const char*>(memchr(line, '\n', len - pos));
+  if (!nl) {
+    if (len - pos > kMaxRequestLine) {
+      *status = 414;
+      return Parse::kError;
+    }
+    return Parse::kIncomplete;
+  }
+  size_t line_len = size_t(nl - line);
+  if (line_len > kMaxRequestLine) {
+    *status = 414;
+    return Parse::kError;
+  }
+  if (line_len && line[line_len - 1] == '\r') --line_len;
+  std::string_view rl(line, line_len);
+  size_t sp1 = rl.find(' ');
+  if (sp1 == 0 || sp1 == std::string_view::npos) {
+    *status = 400;
+    return Parse::kError;
+  }
+  req->method = rl.substr(0, sp1);
+  for (char c : req->method)
+    if (!is_tchar((unsigned char)c)) {
+      *status = 400;
+      return Parse::kError;
+    }
+  size_t sp2 = rl.find(' ', sp1 + 1);
+  if (sp2 == std::string_view::npos || sp2 == sp1 + 1) {
+    *status = 400;
+    return Parse::kError;
+  }
+  req->target = rl.substr(sp1 + 1, sp2 - sp1 - 1);
+  std::string_view ver = rl.substr(sp2 + 1);
+  if (ver.size() != 8 || ver.substr(0, 5) != "HTTP/" || ver[6] != '.' || ver[5] < '0' ||
+      ver[5] > '9' || ver[7] < '0' || ver[7] > '9') {
+    *status = 400;
+    return Parse::kError;
+  }
+  if (ver[5] != '1') {
+    *status = 505;
+    return Parse::kError;
+  }
+  req->version_minor = ver[7] - '0';
+  for (char c : req->target)
+    if ((unsigned char)c <= 0x20 || c == 0x7f) {
+      *status = 400;
+      return Parse::kError;
+    }
+  size_t q = req->target.find('?');
+  req->path = req->target.substr(0, q);
+  if (q != std::string_view::npos) req->query = req->target.substr(q + 1);
+  // Absolute-form targets (proxies): strip scheme://authority.
+  if (req->path.size() > 7 && (req->path.substr(0, 7) == "http://" || req->path.substr(0, 8) == "https://")) {
+    size_t s = req->path.find('/', req->path.find("//") + 2);
+    req->path = s == std::string_view::npos ? std::string_view("/") : req->path.substr(s);
+  }
+
+  // ---- header fields ----
+  bool conn_close = false, conn_keep = false, have_cl = false, have_te = false;
+  size_t p = size_t(nl - buf) + 1;
+  for (;;) {
+    if (p >= len) {
+      if (len > kMaxHeadBytes) {
+        *status = 431;
+        return Parse::kError;
+      }
+      return Parse::kIncomplete;
+    }
+    const char* hl = buf + p;
+    const char* he = static_cast<const char*>(memchr(hl, '\n', len - p));
+    if (!he) {
+      if (len > kMaxHeadBytes) {
+        *status = 431;
+        return Parse::kError;
+      }
+      return Parse::kIncomplete;
+    }
+    size_t hlen = size_t(he - hl);
+    p = size_t(he - buf) + 1;
+    if (p > kMaxHeadBytes) {
+      *status = 431;
+      return Parse::kError;
+    }
+    if (hlen && hl[hlen - 1] == '\r') --hlen;
+    if (hlen == 0) break;  // end of head
+    if (hl[0] == ' ' || hl[0] == '\t') {  // obs-fold: reject (RFC 9112 §5.2)
+      *status = 400;
+      return Parse::kError;
+    }
+    std::string_view h(hl, hlen);
+    size_t colon = h.find(':');
+    if (colon == 0 || colon == std::string_view::npos) {
+      *status = 400;
+      return Parse::kError;
+    }
+    std::string_view name = h.substr(0, colon);
+    for (char c : name)
+      if (!is_tchar((unsigned char)c)) {  // includes whitespace before the colon
+        *status = 400;
+        return Parse::kError;
+      }
+    std::string_view value = trim_ows(h.substr(colon + 1));
+    switch (name.size()) {
+      case 2:
+        if (iequals(name, "b3")) req->b3_single = value;
+        break;
+      case 4:
+        if (iequals(name, "host")) req->host = value;
+        break;
+      case 6:
+        if (iequals(name, "accept")) {
+          // Multiple Accept fields are equivalent to one comma-joined field; keep the first
+          // and let the negotiation treat a second one conservatively (rare in practice).
+          if (!req->has_accept) req->accept = value;
+          req->has_accept = true;
+        }
+        break;
+      case 10:
+        if (iequals(name, "connection")) {
+          for_each_token(value, [&](std::string_view t) {
+            if (iequals(t, "close")) conn_close = true;
+            else if (iequals(t, "keep-alive")) conn_keep = true;
+          });
+        } else if (iequals(name, "x-b3-flags")) {
+          req->b3_flags = value;
+        }
+        break;
+      case 12:
+        if (iequals(name, "x-b3-traceid")) req->b3_trace_id = value;
+        else if (iequals(name, "x-b3-sampled")) req->b3_sampled = value;
+        break;
+      case 11:
+        if (iequals(name, "x-b3-spanid")) req->b3_span_id = value;
+        break;
+      case 14:
+        if (iequals(name, "content-length")) {
+          int64_t v;
+          if (!parse_uint(value, &v) || (have_cl && v != req->content_length)) {
+            *status = 400;
+            return Parse::kError;
+          }
+          have_cl = true;
+          req->content_length = v;
+        }
+        break;
+      case 17:
+        if (iequals(name, "transfer-encoding")) {
+          have_te = true;
+          std::string_view last;
+          for_each_token(value, [&](std::string_view t) { last = t; });
+          if (iequals(last, "chunked")) {
+            req->chunked = true;
+          } else {
+            *status = 501;
+            return Parse::kError;
+          }
+        } else if (iequals(name, "x-b3-parentspanid")) {
+          req->b3_parent_id = value;
+        }
+        break;
+      default:
+        break;
+    }
+  }
+  if (have_te && have_cl) {  // request smuggling guard (RFC 9112 §6.3)
+    *status = 400;
+    return Parse::kError;
+  }
+  if (req->version_minor == 0) req->keep_alive = conn_keep && !conn_close;
+  else req->keep_alive = !conn_close;
+  req->head_bytes = p;
+  return Parse::kOk;
+}
+
+Parse skip_chunked_body(const char* buf, size_t len, size_t* consumed) {
+  size_t p = 0;
+  for (;;) {
+    const char* nl = static_cast<const char*>(memchr(buf + p, '\n', len - p));
+    if (!nl) return len - p > 1024 ? Parse::kError : Parse::kIncomplete;
+    std::string_view line(buf + p, size_t(nl - (buf + p)));
+    if (!line.empty() && line.back() == '\r') line.remove_suffix(1);
+    size_t semi = line.find(';');
+    std::string_view hexs = line.substr(0, semi);
+    while (!hexs.empty() && (hexs.back() == ' ' || hexs.back() == '\t')) hexs.remove_suffix(1);
+    if (hexs.empty() || hexs.size() > 15) return Parse::kError;
+    uint64_t sz = 0;
+    for (char c : hexs) {
+      int d;
+      if (c >= '0' && c <= '9') d = c - '0';
+      else if ((c | 32) >= 'a' && (c | 32) <= 'f') d = (c | 32) - 'a' + 10;
+      else return Parse::kError;
+      sz = sz * 16 + uint64_t(d);
+    }
+    p = size_t(nl - buf) + 1;
+    if (sz == 0) {
+      // trailer section, terminated by an empty line
+      for (;;) {
+        const char* tl = static_cast<const char*>(memchr(buf + p, '\n', len - p));
+        if (!tl) return Parse::kIncomplete;
+        size_t l = size_t(tl - (buf + p));
+        bool empty = l == 0 || (l == 1 && buf[p] == '\r');
+        p = size_t(tl - buf) + 1;
+        if (empty) {
+          *consumed = p;
+          return Parse::kOk;
+        }
+      }
+    }
+    if (len - p < sz + 2) return Parse::kIncomplete;
+    p += sz;
+    if (buf[p] == '\r') ++p;
+    if (p >= len) return Parse::kIncomplete;
+    if (buf[p] != '\n') return Parse::kError;
+    ++p;
+  }
+}
+
+}  // namespace hola::http

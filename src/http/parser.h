@@ -1,0 +1,48 @@
+// Incremental, pipelining-safe HTTP/1.1 request parser (the Undertow role).
+//
+// Zero-copy: every field is a string_view into the connection's receive buffer and is valid
+// only until the buffer is compacted. Only the headers the service acts on are extracted;
+// the rest are validated and skipped.
+#pragma once
+#include <cstddef>
+#include <cstdint>
+#include <string_view>
+
+namespace hola::http {
+
+constexpr size_t kMaxHeadBytes = 16 * 1024;
+constexpr size_t kMaxRequestLine = 8 * 1024;
+
+struct Request {
+  std::string_view method;
+  std::string_view target;  // raw request-target (path + optional ?query)
+  std::string_view path;    // raw path part (no query), still percent-encoded
+  std::string_view query;   // without '?'
+  int version_minor = 1;    // HTTP/1.<minor>
+  bool keep_alive = true;   // after applying Connection header + version default
+  bool has_accept = false;
+  std::string_view accept;
+  std::string_view host;
+  // B3 propagation headers (X-B3-*, and the single "b3" header).
+  std::string_view b3_trace_id, b3_span_id, b3_parent_id, b3_sampled, b3_flags, b3_single;
+  int64_t content_length = 0;
+  bool chunked = false;
+  size_t head_bytes = 0;  // bytes of request-line + headers + terminating blank line
+};
+
+enum class Parse { kOk, kIncomplete, kError };
+
+// Parses one request head from [buf, buf+len). On kError, *status holds the HTTP status to
+// answer with (400, 414, 431, 501, 505).
+Parse parse_request(const char* buf, size_t len, Request* req, int* status);
+
+// For a chunked body starting at buf: on kOk sets *consumed to the full body length
+// (including the last-chunk and trailers).
+Parse skip_chunked_body(const char* buf, size_t len, size_t* consumed);
+
+// Case-insensitive ASCII equality.
+bool iequals(std::string_view a, std::string_view b);
+// Percent-decodes a path; false on malformed escapes. Output written to out (len <= in len).
+bool percent_decode(std::string_view in, char* out, size_t* out_len);
+
+}  // namespace hola::http

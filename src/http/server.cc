@@ -1,0 +1,450 @@
+#include "http/server.h"
+
+#include <errno.h>
+#include <netinet/in.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cstring>
+
+#include "core/affinity.h"
+#include "core/clock.h"
+#include "core/log.h"
+#include "core/net.h"
+
+namespace hola::http {
+
+namespace {
+constexpr size_t kMaxBufferedOutput = 1 << 20;  // stop reading while this much is unsent
+constexpr int64_t kMaxBody = 1 << 20;           // request bodies are read and discarded
+
+const char* reason_phrase(int status) {
+  switch (status) {
+    case 400: return "Bad Request";
+    case 413: return "Request Entity Too Large";
+    case 414: return "Request-URI Too Long";
+    case 431: return "Request Header Fields Too Large";
+    case 501: return "Not Implemented";
+    case 505: return "HTTP Version Not Supported";
+    default: return "Error";
+  }
+}
+}  // namespace
+
+std::string RequestHandler::error_response(int status) {
+  std::string s = "HTTP/1.1 " + std::to_string(status) + " " + reason_phrase(status) +
+                  "\r\nConnection: close\r\nContent-Length: 0\r\n\r\n";
+  return s;
+}
+
+// ---------------------------------------------------------------- Connection
+
+Connection::Connection(Worker* w, int fd, uint64_t id) : worker_(w), fd_(fd), id_(id) {}
+
+Connection::~Connection() {
+  if (fd_ >= 0) ::close(fd_);
+}
+
+void Connection::on_event(uint32_t ev) {
+  if (closed_) return;
+  if (ev & EPOLLERR) {
+    close();
+    return;
+  }
+  if (ev & EPOLLOUT) {
+    on_writable();
+    if (closed_) return;
+  }
+  if (ev & (EPOLLIN | EPOLLHUP | EPOLLRDHUP)) on_readable();
+}
+
+void Connection::on_readable() {
+  WorkerStats& st = worker_->stats();
+  if (streaming_) {
+    char buf[4096];
+    ssize_t n = ::recv(fd_, buf, sizeof buf, 0);
+    if (n == 0 || (n < 0 && errno != EAGAIN && errno != EINTR)) close();
+    return;
+  }
+  if (parked_ || !reading_) return;
+  if (in_.empty()) {
+    char* buf = worker_->scratch();
+    ssize_t n = ::recv(fd_, buf, worker_->scratch_size(), 0);
+    if (n <= 0) {
+      if (n == 0 || (errno != EAGAIN && errno != EINTR)) close();
+      return;
+    }
+    WorkerStats::bump(st.bytes_in, uint64_t(n));
+    size_t consumed = 0;
+    if (!process(buf, size_t(n), &consumed)) return;
+    if (consumed < size_t(n)) in_.assign(buf + consumed, size_t(n) - consumed);
+  } else {
+    size_t old = in_.size();
+    size_t chunk = worker_->server().options().read_chunk;
+    in_.resize(old + chunk);
+    ssize_t n = ::recv(fd_, &in_[old], chunk, 0);
+    if (n <= 0) {
+      in_.resize(old);
+      if (n == 0 || (errno != EAGAIN && errno != EINTR)) close();
+      return;
+    }
+    WorkerStats::bump(st.bytes_in, uint64_t(n));
+    in_.resize(old + size_t(n));
+    size_t consumed = 0;
+    std::string buf;
+    buf.swap(in_);  // handlers may park: leftovers are re-stored below
+    if (!process(buf.data(), buf.size(), &consumed)) return;
+    if (consumed < buf.size()) in_.assign(buf, consumed, std::string::npos);
+  }
+  flush();
+}
+
+bool Connection::process(const char* data, size_t len, size_t* consumed) {
+  WorkerStats& st = worker_->stats();
+  RequestHandler& h = worker_->handler();
+  in_process_ = true;
+  size_t off = 0;
+  while (off < len && !parked_ && !streaming_ && !closed_ && !close_after_flush_) {
+    Request r;
+    int status = 400;
+    Parse p = parse_request(data + off, len - off, &r, &status);
+    if (p == Parse::kIncomplete) break;
+    if (p == Parse::kError) {
+      WorkerStats::bump(st.parse_errors);
+      error_response(status);
+      off = len;
+      break;
+    }
+    size_t total = r.head_bytes;
+    if (r.chunked) {
+      size_t body = 0;
+      Parse q = skip_chunked_body(data + off + total, len - off - total, &body);
+      if (q == Parse::kIncomplete) {
+        if (len - off > size_t(kMaxBody)) {
+          error_response(413);
+          off = len;
+        }
+        break;
+      }
+      if (q == Parse::kError) {
+        WorkerStats::bump(st.parse_errors);
+        error_response(400);
+        off = len;
+        break;
+      }
+      total += body;
+    } else if (r.content_length > 0) {
+      if (r.content_length > kMaxBody) {
+        error_response(413);
+        off = len;
+        break;
+      }
+      if (len - off - total < size_t(r.content_length)) break;
+      total += size_t(r.content_length);
+    }
+    off += total;
+    WorkerStats::bump(st.requests);
+    h.on_request(*this, r);
+    if (worker_->server().draining()) close_after_flush_ = true;
+  }
+  in_process_ = false;
+  *consumed = off;
+  if (closed_) return false;
+  if (parked_ || streaming_) update_interest();
+  return true;
+}
+
+void Connection::error_response(int status) {
+  std::string s = worker_->handler().error_response(status);
+  send(s.data(), s.size());
+  close_after_flush_ = true;
+}
+
+void Connection::send(const char* p, size_t n) {
+  if (closed_) return;
+  out_.append(p, n);
+  if (!in_process_) flush();
+}
+
+void Connection::complete(std::string_view response, bool keep_alive) {
+  if (closed_) {
+    parked_ = false;
+    return;
+  }
+  parked_ = false;
+  if (!keep_alive || worker_->server().draining()) close_after_flush_ = true;
+  out_.append(response.data(), response.size());
+  if (in_process_) return;
+  // Continue with pipelined requests that arrived while parked.
+  if (!in_.empty() && !close_after_flush_) {
+    std::string buf;
+    buf.swap(in_);
+    size_t consumed = 0;
+    if (!process(buf.data(), buf.size(), &consumed)) return;
+    if (consumed < buf.size()) in_.assign(buf, consumed, std::string::npos);
+  }
+  flush();
+  if (!closed_) update_interest();
+}
+
+void Connection::start_streaming(std::function<void()> on_close) {
+  streaming_ = true;
+  on_close_ = std::move(on_close);
+}
+
+void Connection::flush() {
+  WorkerStats& st = worker_->stats();
+  while (out_off_ < out_.size()) {
+    ssize_t w = ::send(fd_, out_.data() + out_off_, out_.size() - out_off_, MSG_NOSIGNAL);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      if (errno == EAGAIN) {
+        if (!want_write_) {
+          want_write_ = true;
+          if (out_.size() - out_off_ > kMaxBufferedOutput) reading_ = false;
+          update_interest();
+        }
+        return;
+      }
+      close();
+      return;
+    }
+    WorkerStats::bump(st.bytes_out, uint64_t(w));
+    out_off_ += size_t(w);
+  }
+  out_.clear();
+  out_off_ = 0;
+  if (want_write_ || !reading_) {
+    want_write_ = false;
+    reading_ = true;
+    update_interest();
+  }
+  if (close_after_flush_ && !parked_) {
+    ::shutdown(fd_, SHUT_WR);
+    close();
+  }
+}
+
+void Connection::on_writable() { flush(); }
+
+void Connection::update_interest() {
+  if (closed_) return;
+  uint32_t ev = 0;
+  if (streaming_) ev |= EPOLLIN | EPOLLRDHUP;
+  else if (reading_ && !parked_) ev |= EPOLLIN | EPOLLRDHUP;
+  if (want_write_) ev |= EPOLLOUT;
+  worker_->loop().mod(fd_, ev, this);
+}
+
+void Connection::close() {
+  if (closed_) return;
+  closed_ = true;
+  worker_->loop().del(fd_);
+  ::close(fd_);
+  fd_ = -1;
+  WorkerStats::bump(worker_->stats().closed);
+  worker_->on_connection_closed(this);
+  if (on_close_) {
+    auto f = std::move(on_close_);
+    on_close_ = nullptr;
+    f();
+  }
+  if (holds_ == 0) worker_->loop().retire(this);
+}
+
+void Connection::release() {
+  if (--holds_ == 0 && closed_) worker_->loop().retire(this);
+}
+
+std::string Connection::peer() const {
+  sockaddr_storage ss{};
+  socklen_t len = sizeof ss;
+  if (fd_ < 0 || getpeername(fd_, reinterpret_cast<sockaddr*>(&ss), &len) != 0) return "?";
+  return sockaddr_to_string(ss);
+}
+
+// ---------------------------------------------------------------- Worker
+
+Worker::Worker(Server* s, int index) : server_(s), index_(index) {
+  scratch_.resize(s->options().read_chunk);
+  memset(date_, ' ', sizeof date_);
+  tick();
+  loop_.set_tick([this] { tick(); });
+}
+
+RequestHandler& Worker::handler() { return server_->handler(); }
+
+void Worker::tick() {
+  int64_t s = wall_sec_coarse();
+  if (s != date_sec_) {
+    date_sec_ = s;
+    format_http_date(s, date_);
+    ++date_version_;
+  }
+}
+
+void Worker::on_connection_closed(Connection* c) {
+  --nconns_;
+  if (c->prev_) c->prev_->next_ = c->next_;
+  else conns_ = c->next_;
+  if (c->next_) c->next_->prev_ = c->prev_;
+  c->prev_ = c->next_ = nullptr;
+}
+
+void Worker::close_idle_connections() {
+  for (Connection* c = conns_; c;) {
+    Connection* next = c->next_;
+    if (c->streaming() || c->idle()) c->close();
+    c = next;
+  }
+}
+
+void Worker::adopt(int fd) {
+  loop_.post([this, fd] { adopt_here(fd); });
+}
+
+void Worker::adopt_here(int fd) {
+  auto* c = new Connection(this, fd, (uint64_t(index_) << 48) | next_conn_id_++);
+  if (server_->draining() || !loop_.add(fd, EPOLLIN | EPOLLRDHUP, c)) {
+    delete c;
+    return;
+  }
+  ++nconns_;
+  WorkerStats::bump(stats_.accepted);
+  c->next_ = conns_;
+  if (conns_) conns_->prev_ = c;
+  conns_ = c;
+}
+
+// ---------------------------------------------------------------- Server
+
+Server::Server(ServerOptions opts, RequestHandler* handler) : opts_(std::move(opts)), handler_(handler) {
+  if (opts_.threads < 1) opts_.threads = 1;
+  for (int i = 0; i < opts_.threads; ++i) workers_.push_back(std::make_unique<Worker>(this, i));
+}
+
+Server::~Server() {
+  for (auto& a : acceptors_)
+    if (a->fd >= 0) ::close(a->fd);
+}
+
+bool Server::bind(std::string* err) {
+  ListenOptions lo;
+  lo.host = opts_.host;
+  lo.port = opts_.port;
+  lo.backlog = opts_.backlog;
+  lo.reuseport = opts_.reuseport_accept;
+  size_t n = opts_.reuseport_accept ? workers_.size() : 1;
+  for (size_t i = 0; i < n; ++i) {
+    int fd = listen_tcp(lo, err);
+    if (fd < 0) return false;
+    if (i == 0) {
+      port_ = bound_port(fd);
+      lo.port = port_;  // with port 0, every reuseport listener must share the chosen port
+    }
+    auto a = std::make_unique<Acceptor>();
+    a->server = this;
+    a->worker = workers_[i].get();
+    a->fd = fd;
+    acceptors_.push_back(std::move(a));
+  }
+  return true;
+}
+
+void Server::Acceptor::on_event(uint32_t) {
+  for (int i = 0; i < 256; ++i) {
+    int c = ::accept4(fd, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
+    if (c < 0) {
+      if (errno == EINTR || errno == ECONNABORTED) continue;
+      if (errno == EMFILE || errno == ENFILE) {
+        LOG_WARN("accept: %s (fd limit); pausing accepts", strerror(errno));
+        // back off for a moment; the listener stays level-triggered
+        worker->loop().del(fd);
+        int lfd = fd;
+        Acceptor* self = this;
+        worker->loop().add_timer(50, [self, lfd] {
+          if (!self->server->draining()) self->worker->loop().add(lfd, EPOLLIN, self);
+        });
+      }
+      return;
+    }
+    if (server->opts_.reuseport_accept) {
+      worker->adopt_here(c);
+    } else {
+      size_t k = server->rr_.fetch_add(1, std::memory_order_relaxed) % server->workers_.size();
+      Worker* w = server->workers_[k].get();
+      if (w == worker) w->adopt_here(c);
+      else w->adopt(c);
+    }
+  }
+}
+
+void Server::start() {
+  for (auto& a : acceptors_) a->worker->loop().add(a->fd, EPOLLIN, a.get());
+  for (auto& w : workers_) {
+    Worker* wp = w.get();
+    threads_.emplace_back([this, wp] {
+      if (!opts_.cpus.empty()) {
+        int cpu = opts_.cpus[size_t(wp->index()) % opts_.cpus.size()];
+        if (!pin_current_thread(cpu)) LOG_WARN("worker %d: could not pin to cpu %d", wp->index(), cpu);
+      }
+      handler_->on_worker_start(*wp);
+      wp->loop().run();
+      handler_->on_worker_stop(*wp);
+    });
+  }
+}
+
+uint64_t Server::total_requests() const {
+  uint64_t n = 0;
+  for (auto& w : workers_) n += w->stats_.requests.load(std::memory_order_relaxed);
+  return n;
+}
+
+void Server::shutdown(int drain_ms) {
+  draining_.store(true);
+  for (auto& a : acceptors_) {
+    Acceptor* ap = a.get();
+    std::atomic<bool> done{false};
+    ap->worker->loop().post([ap, &done] {
+      ap->worker->loop().del(ap->fd);
+      ::close(ap->fd);
+      ap->fd = -1;
+      done.store(true);
+    });
+    while (!done.load()) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+  }
+  // Idle keep-alive and streaming connections close now; busy ones close after their
+  // current response (process() sets close_after_flush_ while draining).
+  for (auto& w : workers_) {
+    Worker* wp = w.get();
+    wp->loop().post([wp] { wp->close_idle_connections(); });
+  }
+  auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(drain_ms);
+  for (;;) {
+    size_t open = 0;
+    for (auto& w : workers_) {
+      std::atomic<size_t> n{0};
+      std::atomic<bool> done{false};
+      Worker* wp = w.get();
+      wp->loop().post([wp, &n, &done] {
+        n.store(wp->open_connections());
+        done.store(true);
+      });
+      while (!done.load()) std::this_thread::sleep_for(std::chrono::microseconds(200));
+      open += n.load();
+    }
+    if (open == 0 || std::chrono::steady_clock::now() >= deadline) break;
+    std::this_thread::sleep_for(std::chrono::milliseconds(10));
+  }
+  for (auto& w : workers_) w->loop().stop();
+}
+
+void Server::join() {
+  for (auto& t : threads_)
+    if (t.joinable()) t.join();
+  threads_.clear();
+}
+
+}  // namespace hola::http

@@ -1,0 +1,206 @@
+// HTTP/1.1 server: N pinned workers, each an EventLoop that owns its connections.
+//
+// Replaces the Undertow IO/worker pools of the reference's WildFly Swarm runtime
+// (SURVEY.md T1, CS2). Accepted sockets are dealt round-robin to workers by the acceptor
+// (loop 0) so a closed-loop benchmark with a few dozen keep-alive connections is balanced
+// exactly; `reuseport` mode instead gives every worker its own SO_REUSEPORT listener.
+#pragma once
+#include <atomic>
+#include <cstdint>
+#include <functional>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "core/loop.h"
+#include "http/parser.h"
+
+namespace hola::http {
+
+class Worker;
+class Server;
+
+// Per-worker request counters, readable (relaxed) from other threads for /metrics.
+struct alignas(64) WorkerStats {
+  std::atomic<uint64_t> requests{0};
+  std::atomic<uint64_t> accepted{0};
+  std::atomic<uint64_t> closed{0};
+  std::atomic<uint64_t> parse_errors{0};
+  std::atomic<uint64_t> bytes_in{0};
+  std::atomic<uint64_t> bytes_out{0};
+  // single-writer increment without a locked RMW
+  static void bump(std::atomic<uint64_t>& c, uint64_t d = 1) {
+    c.store(c.load(std::memory_order_relaxed) + d, std::memory_order_relaxed);
+  }
+};
+
+class Connection final : public EventLoop::Handler {
+ public:
+  Connection(Worker* w, int fd, uint64_t id);
+  ~Connection() override;
+
+  void on_event(uint32_t events) override;
+
+  Worker& worker() { return *worker_; }
+  int fd() const { return fd_; }
+  uint64_t id() const { return id_; }
+  bool closed() const { return closed_; }
+
+  // Queue response bytes (copied unless the socket takes them immediately). Order preserved.
+  void send(const char* p, size_t n);
+  void send(std::string_view s) { send(s.data(), s.size()); }
+  // After the current response: close the connection once all queued bytes are written.
+  void close_after_response() { close_after_flush_ = true; }
+
+  // Async requests: park() from inside on_request; later call complete() (on the worker
+  // thread) with the full response. Input processing resumes after completion.
+  void park() { parked_ = true; }
+  void complete(std::string_view response, bool keep_alive);
+
+  // Long-lived streaming responses (SSE): no further request parsing; `on_close` fires when
+  // the peer goes away or close() is called.
+  void start_streaming(std::function<void()> on_close);
+  bool streaming() const { return streaming_; }
+
+  // Keeps the object alive across async callbacks even if the socket closes meanwhile.
+  void hold() { ++holds_; }
+  void release();
+
+  void close();
+
+  // Remote address (for tracing / logs).
+  std::string peer() const;
+  // Idle = no request in progress and nothing buffered either way.
+  bool idle() const { return !parked_ && in_.empty() && out_.size() == out_off_; }
+
+ private:
+  void on_readable();
+  void on_writable();
+  // Parses and dispatches buffered requests; returns false if the connection closed.
+  bool process(const char* data, size_t len, size_t* consumed);
+  void flush();
+  void update_interest();
+  void error_response(int status);
+
+  Worker* worker_;
+  int fd_;
+  uint64_t id_;
+  std::string in_;   // unconsumed input carried across reads
+  std::string out_;  // unsent output
+  size_t out_off_ = 0;
+  bool closed_ = false;
+  bool parked_ = false;
+  bool streaming_ = false;
+  bool close_after_flush_ = false;
+  bool want_write_ = false;
+  bool reading_ = true;
+  bool in_process_ = false;  // inside process(): batch writes instead of sending eagerly
+  int holds_ = 0;
+  std::function<void()> on_close_;
+  // intrusive per-worker list (for draining on shutdown)
+  Connection* prev_ = nullptr;
+  Connection* next_ = nullptr;
+  friend class Worker;
+};
+
+class RequestHandler {
+ public:
+  virtual ~RequestHandler() = default;
+  // Runs on the worker thread. Must either send exactly one complete response with
+  // c.send() (and c.close_after_response() when !r.keep_alive) or call c.park().
+  virtual void on_request(Connection& c, const Request& r) = 0;
+  // Per-worker setup/teardown on the worker thread.
+  virtual void on_worker_start(Worker& w) {}
+  virtual void on_worker_stop(Worker& w) {}
+  // Response for protocol errors (400/414/431/501/505); default is a minimal empty response.
+  virtual std::string error_response(int status);
+};
+
+struct ServerOptions {
+  std::string host = "0.0.0.0";
+  int port = 8080;
+  int threads = 1;
+  std::vector<int> cpus;          // pin worker i to cpus[i % size]; empty = no pinning
+  bool reuseport_accept = false;  // per-worker SO_REUSEPORT listeners instead of round-robin
+  int backlog = 4096;
+  size_t read_chunk = 64 * 1024;
+};
+
+class Worker {
+ public:
+  Worker(Server* s, int index);
+  EventLoop& loop() { return loop_; }
+  int index() const { return index_; }
+  Server& server() { return *server_; }
+  WorkerStats& stats() { return stats_; }
+  RequestHandler& handler();
+  // Shared scratch receive buffer (connections copy out only leftovers).
+  char* scratch() { return scratch_.data(); }
+  size_t scratch_size() const { return scratch_.size(); }
+  // Current Date header value (29 bytes) and a counter bumped whenever it changes.
+  const char* date() const { return date_; }
+  uint64_t date_version() const { return date_version_; }
+  // Accepted fd handed over from the acceptor (thread-safe).
+  void adopt(int fd);
+  void adopt_here(int fd);
+  size_t open_connections() const { return nconns_; }
+  void on_connection_closed(Connection* c);
+  // Closes idle and streaming connections (shutdown drain); runs on the worker thread.
+  void close_idle_connections();
+  // Per-worker slot for the application.
+  void* app_data = nullptr;
+
+ private:
+  friend class Server;
+  void tick();
+  Server* server_;
+  int index_;
+  EventLoop loop_;
+  WorkerStats stats_;
+  std::vector<char> scratch_;
+  char date_[29];
+  int64_t date_sec_ = 0;
+  uint64_t date_version_ = 0;
+  uint64_t next_conn_id_ = 1;
+  size_t nconns_ = 0;
+  Connection* conns_ = nullptr;
+};
+
+class Server {
+ public:
+  Server(ServerOptions opts, RequestHandler* handler);
+  ~Server();
+  // Binds listeners; false with *err on failure.
+  bool bind(std::string* err);
+  int port() const { return port_; }
+  // Starts worker threads (returns immediately).
+  void start();
+  // Stops accepting, lets workers finish in-flight responses for up to drain_ms, then stops.
+  void shutdown(int drain_ms);
+  void join();
+  size_t num_workers() const { return workers_.size(); }
+  Worker& worker(size_t i) { return *workers_[i]; }
+  RequestHandler& handler() { return *handler_; }
+  const ServerOptions& options() const { return opts_; }
+  bool draining() const { return draining_.load(std::memory_order_relaxed); }
+  uint64_t total_requests() const;
+
+ private:
+  struct Acceptor : EventLoop::Handler {
+    Server* server;
+    Worker* worker;
+    int fd;
+    void on_event(uint32_t) override;
+  };
+  ServerOptions opts_;
+  RequestHandler* handler_;
+  std::vector<std::unique_ptr<Worker>> workers_;
+  std::vector<std::unique_ptr<Acceptor>> acceptors_;
+  std::vector<std::thread> threads_;
+  std::atomic<bool> draining_{false};
+  std::atomic<uint64_t> rr_{0};
+  int port_ = 0;
+};
+
+}  // namespace hola::http

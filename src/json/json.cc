@@ -1,0 +1,265 @@
+#include "json/json.h"
+
+#include <cstdio>
+
+#include "config/properties.h"
+
+namespace hola::json {
+
+void append_string(std::string* out, std::string_view s) {
+  out->push_back('"');
+  for (char ch : s) {
+    unsigned char c = (unsigned char)ch;
+    switch (c) {
+      case '"': out->append("\\\""); break;
+      case '\\': out->append("\\\\"); break;
+      case '\b': out->append("\\b"); break;
+      case '\f': out->append("\\f"); break;
+      case '\n': out->append("\\n"); break;
+      case '\r': out->append("\\r"); break;
+      case '\t': out->append("\\t"); break;
+      default:
+        if (c < 0x20) {
+          char buf[8];
+          snprintf(buf, sizeof buf, "\\u%04X", c);
+          out->append(buf);
+        } else {
+          out->push_back(ch);
+        }
+    }
+  }
+  out->push_back('"');
+}
+
+std::string quote(std::string_view s) {
+  std::string r;
+  append_string(&r, s);
+  return r;
+}
+
+std::string string_array(const std::vector<std::optional<std::string>>& items) {
+  std::string r = "[";
+  for (size_t i = 0; i < items.size(); ++i) {
+    if (i) r.push_back(',');
+    if (items[i]) append_string(&r, *items[i]);
+    else r.append("null");
+  }
+  r.push_back(']');
+  return r;
+}
+
+const Value* Value::get(std::string_view key) const {
+  for (const auto& kv : obj)
+    if (kv.first == key) return &kv.second;
+  return nullptr;
+}
+
+namespace {
+
+struct Parser {
+  std::string_view s;
+  size_t i = 0;
+  std::string err;
+  int depth = 0;
+
+  void ws() {
+    while (i < s.size() && (s[i] == ' ' || s[i] == '\t' || s[i] == '\n' || s[i] == '\r')) ++i;
+  }
+  bool fail(const char* m) {
+    if (err.empty()) err = std::string(m) + " at offset " + std::to_string(i);
+    return false;
+  }
+  bool lit(std::string_view w) {
+    if (s.substr(i, w.size()) != w) return fail("bad literal");
+    i += w.size();
+    return true;
+  }
+  bool hex4(uint32_t* v) {
+    if (i + 4 > s.size()) return fail("short \\u escape");
+    *v = 0;
+    for (int k = 0; k < 4; ++k) {
+      char c = s[i++];
+      int h = (c >= '0' && c <= '9') ? c - '0' : (c >= 'a' && c <= 'f') ? c - 'a' + 10 : (c >= 'A' && c <= 'F') ? c - 'A' + 10 : -1;
+      if (h < 0) return fail("bad \\u escape");
+      *v = *v * 16 + uint32_t(h);
+    }
+    return true;
+  }
+  bool str(std::string* out) {
+    if (i >= s.size() || s[i] != '"') return fail("expected string");
+    ++i;
+    out->clear();
+    while (i < s.size()) {
+      char c = s[i++];
+      if (c == '"') return true;
+      if ((unsigned char)c < 0x20) return fail("control character in string");
+      if (c != '\\') {
+        out->push_back(c);
+        continue;
+      }
+      if (i >= s.size()) break;
+      c = s[i++];
+      switch (c) {
+        case '"': out->push_back('"'); break;
+        case '\\': out->push_back('\\'); break;
+        case '/': out->push_back('/'); break;
+        case 'b': out->push_back('\b'); break;
+        case 'f': out->push_back('\f'); break;
+        case 'n': out->push_back('\n'); break;
+        case 'r': out->push_back('\r'); break;
+        case 't': out->push_back('\t'); break;
+        case 'u': {
+          uint32_t v;
+          if (!hex4(&v)) return false;
+          if (v >= 0xD800 && v <= 0xDBFF && i + 6 <= s.size() && s[i] == '\\' && s[i + 1] == 'u') {
+            size_t save = i;
+            i += 2;
+            uint32_t lo;
+            if (hex4(&lo) && lo >= 0xDC00 && lo <= 0xDFFF) {
+              config::append_utf8(out, 0x10000 + ((v - 0xD800) << 10) + (lo - 0xDC00));
+              break;
+            }
+            i = save;
+            err.clear();
+          }
+          if (v >= 0xD800 && v <= 0xDFFF) out->push_back('?');
+          else config::append_utf8(out, v);
+          break;
+        }
+        default: return fail("bad escape");
+      }
+    }
+    return fail("unterminated string");
+  }
+  bool num(Value* v) {
+    size_t st = i;
+    if (i < s.size() && s[i] == '-') ++i;
+    if (i >= s.size()) return fail("bad number");
+    if (s[i] == '0') ++i;
+    else if (s[i] >= '1' && s[i] <= '9') while (i < s.size() && s[i] >= '0' && s[i] <= '9') ++i;
+    else return fail("bad number");
+    if (i < s.size() && s[i] == '.') {
+      ++i;
+      if (i >= s.size() || s[i] < '0' || s[i] > '9') return fail("bad fraction");
+      while (i < s.size() && s[i] >= '0' && s[i] <= '9') ++i;
+    }
+    if (i < s.size() && (s[i] == 'e' || s[i] == 'E')) {
+      ++i;
+      if (i < s.size() && (s[i] == '+' || s[i] == '-')) ++i;
+      if (i >= s.size() || s[i] < '0' || s[i] > '9') return fail("bad exponent");
+      while (i < s.size() && s[i] >= '0' && s[i] <= '9') ++i;
+    }
+    v->type = Value::Type::kNumber;
+    v->text = std::string(s.substr(st, i - st));
+    return true;
+  }
+  bool value(Value* v) {
+    if (++depth > 64) return fail("nesting too deep");
+    ws();
+    if (i >= s.size()) return fail("unexpected end");
+    char c = s[i];
+    bool ok;
+    if (c == '"') {
+      v->type = Value::Type::kString;
+      ok = str(&v->text);
+    } else if (c == '[') {
+      ++i;
+      v->type = Value::Type::kArray;
+      ws();
+      ok = true;
+      if (i < s.size() && s[i] == ']') {
+        ++i;
+      } else {
+        for (;;) {
+          v->arr.emplace_back();
+          if (!value(&v->arr.back())) { ok = false; break; }
+          ws();
+          if (i < s.size() && s[i] == ',') { ++i; continue; }
+          if (i < s.size() && s[i] == ']') { ++i; break; }
+          ok = fail("expected , or ]");
+          break;
+        }
+      }
+    } else if (c == '{') {
+      ++i;
+      v->type = Value::Type::kObject;
+      ws();
+      ok = true;
+      if (i < s.size() && s[i] == '}') {
+        ++i;
+      } else {
+        for (;;) {
+          ws();
+          std::string k;
+          if (!str(&k)) { ok = false; break; }
+          ws();
+          if (i >= s.size() || s[i] != ':') { ok = fail("expected :"); break; }
+          ++i;
+          v->obj.emplace_back(std::move(k), Value());
+          if (!value(&v->obj.back().second)) { ok = false; break; }
+          ws();
+          if (i < s.size() && s[i] == ',') { ++i; continue; }
+          if (i < s.size() && s[i] == '}') { ++i; break; }
+          ok = fail("expected , or }");
+          break;
+        }
+      }
+    } else if (c == 't') {
+      v->type = Value::Type::kBool;
+      v->b = true;
+      ok = lit("true");
+    } else if (c == 'f') {
+      v->type = Value::Type::kBool;
+      ok = lit("false");
+    } else if (c == 'n') {
+      v->type = Value::Type::kNull;
+      ok = lit("null");
+    } else {
+      ok = num(v);
+    }
+    --depth;
+    return ok;
+  }
+};
+
+}  // namespace
+
+bool parse(std::string_view in, Value* out, std::string* err) {
+  Parser p{in};
+  *out = Value();
+  if (!p.value(out)) {
+    if (err) *err = p.err;
+    return false;
+  }
+  p.ws();
+  if (p.i != in.size()) {
+    if (err) *err = "trailing characters at offset " + std::to_string(p.i);
+    return false;
+  }
+  return true;
+}
+
+bool decode_string_list(std::string_view in, std::vector<std::optional<std::string>>* out,
+                        std::string* err) {
+  Value v;
+  if (!parse(in, &v, err)) return false;
+  out->clear();
+  if (v.type != Value::Type::kArray) {
+    if (err) *err = "expected a JSON array";
+    return false;
+  }
+  for (const Value& e : v.arr) {
+    switch (e.type) {
+      case Value::Type::kNull: out->push_back(std::nullopt); break;
+      case Value::Type::kBool: out->push_back(std::string(e.b ? "true" : "false")); break;
+      case Value::Type::kNumber:
+      case Value::Type::kString: out->push_back(e.text); break;
+      default:
+        if (err) *err = "cannot deserialize java.lang.String out of a nested array/object";
+        return false;
+    }
+  }
+  return true;
+}
+
+}  // namespace hola::json

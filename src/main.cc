@@ -1,0 +1,232 @@
+// hola — native replacement for the WildFly Swarm uber-jar.
+//
+// Boot sequence (the reference's contextInitialized listeners, in explicit code):
+//   config sources + watcher   (Configuration.java, ConfigSource SPI, config.properties)
+//   tracer                      (ZipkinResource.java, ZipKinFilter.java)
+//   aloha chainer + Hystrix     (HolaResource.getNextService, config.properties:17,19)
+//   /hystrix.stream             (HystrixServlet.java)
+//   HTTP server on :8080        (Dockerfile:8, pom.xml:74)
+// SIGTERM/SIGINT: stop accepting, drain in-flight requests, flush spans, exit 0.
+#include <signal.h>
+#include <unistd.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <string>
+
+#include "app/aloha_chainer.h"
+#include "app/hola_app.h"
+#include "config/manager.h"
+#include "config/resolver.h"
+#include "core/affinity.h"
+#include "core/log.h"
+#include "core/net.h"
+#include "http/server.h"
+#include "metrics/hystrix_stream.h"
+#include "metrics/prometheus.h"
+#include "tracing/tracer.h"
+
+using namespace hola;
+
+namespace {
+
+void usage() {
+  fprintf(stderr,
+          "usage: hola [options] [-Dkey=value ...]\n"
+          "  --port N                 listen port (default 8080)\n"
+          "  --host ADDR              listen address (default 0.0.0.0)\n"
+          "  --threads N              event-loop workers (default: one per allowed CPU, capped by cgroup quota)\n"
+          "  --cpu-list LIST          pin workers to these CPUs, e.g. 0-3,8\n"
+          "  --accept rr|reuseport    connection distribution (default rr)\n"
+          "  --conf PATH              greeting properties file (same as -Dconf=PATH)\n"
+          "  --deltaspike-properties PATH   ordinal-100 properties file\n"
+          "  --hystrix-config PATH    Hystrix properties (Archaius config.properties role)\n"
+          "  --hostname NAME          override $HOSTNAME for the greeting\n"
+          "  --zipkin-url URL         span collector (default $ZIPKIN_SERVER_URL)\n"
+          "  --zipkin-v2              POST /api/v2/spans instead of /api/v1/spans\n"
+          "  --trace-sample-rate R    0..1 (default 1)\n"
+          "  --no-tracing             disable tracing entirely\n"
+          "  --aloha-url URL          downstream service (default http://aloha:8080/)\n"
+          "  --feign-log basic|none   outbound call logging (default basic)\n"
+          "  --hystrix-stream-max N   max /hystrix.stream subscribers (default 5)\n"
+          "  --config-poll-ms N       config re-check interval (default 1000)\n"
+          "  --drain-ms N             graceful shutdown drain budget (default 5000)\n"
+          "  --port-file PATH         write the bound port here once listening\n"
+          "  --log-level L            debug|info|warn|error|off (default info)\n"
+          "  --no-metrics             disable the /metrics endpoint\n");
+}
+
+bool need(int i, int argc, const char* flag) {
+  if (i + 1 >= argc) {
+    fprintf(stderr, "hola: %s needs a value\n", flag);
+    return false;
+  }
+  return true;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  http::ServerOptions so;
+  std::map<std::string, std::string> sysprops;
+  const char* jo = getenv("JAVA_OPTIONS");
+  if (jo) sysprops = config::parse_java_options(jo);  // `oc env dc/hola JAVA_OPTIONS=-Dconf=...`
+  config::ManagerOptions mo;
+  app::AppOptions ao;
+  app::AlohaOptions alo;
+  tracing::TracerOptions to;
+  const char* zu = getenv("ZIPKIN_SERVER_URL");
+  if (zu) to.collector_url = zu;
+  const char* hn = getenv("HOSTNAME");
+  if (hn) ao.hostname = hn;  // HolaResource.java:57 getOrDefault("HOSTNAME", "unknown")
+  int threads = 0, drain_ms = 5000, stream_max = 5;
+  std::string cpu_list, port_file;
+  bool no_tracing = false;
+
+  for (int i = 1; i < argc; ++i) {
+    std::string a = argv[i];
+    auto val = [&](const char* f) -> std::string {
+      if (!need(i, argc, f)) exit(2);
+      return argv[++i];
+    };
+    if (a.rfind("-D", 0) == 0 && a.size() > 2) {
+      size_t eq = a.find('=');
+      if (eq == std::string::npos) sysprops[a.substr(2)] = "";
+      else sysprops[a.substr(2, eq - 2)] = a.substr(eq + 1);
+    } else if (a == "--port") so.port = atoi(val("--port").c_str());
+    else if (a == "--host") so.host = val("--host");
+    else if (a == "--threads") threads = atoi(val("--threads").c_str());
+    else if (a == "--cpu-list") cpu_list = val("--cpu-list");
+    else if (a == "--accept") {
+      std::string m = val("--accept");
+      if (m == "reuseport") so.reuseport_accept = true;
+      else if (m != "rr") { fprintf(stderr, "hola: --accept rr|reuseport\n"); return 2; }
+    } else if (a == "--conf") sysprops["conf"] = val("--conf");
+    else if (a == "--deltaspike-properties") mo.deltaspike_properties = val("--deltaspike-properties");
+    else if (a == "--hystrix-config") mo.hystrix_config = val("--hystrix-config");
+    else if (a == "--hostname") ao.hostname = val("--hostname");
+    else if (a == "--zipkin-url") to.collector_url = val("--zipkin-url");
+    else if (a == "--zipkin-v2") to.v2 = true;
+    else if (a == "--trace-sample-rate") to.sample_rate = atof(val("--trace-sample-rate").c_str());
+    else if (a == "--no-tracing") no_tracing = true;
+    else if (a == "--aloha-url") alo.url = val("--aloha-url");
+    else if (a == "--feign-log") alo.feign_log_basic = val("--feign-log") == "basic";
+    else if (a == "--hystrix-stream-max") stream_max = atoi(val("--hystrix-stream-max").c_str());
+    else if (a == "--config-poll-ms") mo.poll_ms = atoi(val("--config-poll-ms").c_str());
+    else if (a == "--drain-ms") drain_ms = atoi(val("--drain-ms").c_str());
+    else if (a == "--port-file") port_file = val("--port-file");
+    else if (a == "--no-metrics") ao.enable_metrics_endpoint = false;
+    else if (a == "--log-level") {
+      LogLevel l;
+      if (!parse_log_level(val("--log-level"), &l)) { fprintf(stderr, "hola: bad --log-level\n"); return 2; }
+      Logger::instance().set_level(l);
+    } else if (a == "-h" || a == "--help") {
+      usage();
+      return 0;
+    } else {
+      fprintf(stderr, "hola: unknown argument '%s'\n", a.c_str());
+      usage();
+      return 2;
+    }
+  }
+
+  // ---- CPUs / workers ----
+  std::vector<int> cpus;
+  if (!cpu_list.empty() && !parse_cpu_list(cpu_list, &cpus)) {
+    fprintf(stderr, "hola: bad --cpu-list '%s'\n", cpu_list.c_str());
+    return 2;
+  }
+  if (threads <= 0) {
+    size_t n = cpus.empty() ? allowed_cpus().size() : cpus.size();
+    double quota = cgroup_cpu_quota();
+    if (quota > 0 && double(n) > quota) n = size_t(quota);
+    threads = n ? int(n) : 1;
+  }
+  so.threads = threads;
+  so.cpus = cpus;
+
+  // Block termination signals in every thread; main waits for them with sigwait.
+  sigset_t sigs;
+  sigemptyset(&sigs);
+  sigaddset(&sigs, SIGTERM);
+  sigaddset(&sigs, SIGINT);
+  pthread_sigmask(SIG_BLOCK, &sigs, nullptr);
+  signal(SIGPIPE, SIG_IGN);
+
+  // ---- config ----
+  mo.sysprops = sysprops;
+  mo.env = config::environment_map();
+  config::Manager cfg(mo);
+
+  // ---- app, tracer, chainer, stream ----
+  app::HolaApp app(ao);
+  http::Server server(so, &app);
+  std::string err;
+  if (!server.bind(&err)) {
+    fprintf(stderr, "hola: %s\n", err.c_str());
+    return 1;
+  }
+  app.set_server(&server);
+
+  to.enabled = !no_tracing;
+  to.ipv4 = local_ipv4();
+  to.port = server.port();
+  tracing::Tracer tracer(to, threads);
+  if (to.enabled) app.set_tracer(&tracer);
+
+  // Built-in Hystrix defaults = the reference's tuned config.properties:17,19.
+  std::map<std::string, std::string> hystrix_defaults = {
+      {"hystrix.command.default.execution.isolation.thread.timeoutInMilliseconds", "600"},
+      {"hystrix.command.default.circuitBreaker.requestVolumeThreshold", "5"}};
+  auto hystrix_settings = [&](const std::map<std::string, std::string>& props) {
+    std::map<std::string, std::string> merged = hystrix_defaults;
+    for (auto& [k, v] : props) merged[k] = v;
+    return resilience::settings_from(merged, alo.command_key, alo.url);
+  };
+  app::AlohaChainer chainer(alo, hystrix_settings({}), threads, to.enabled ? &tracer : nullptr);
+  app.set_chainer(&chainer);
+  metrics::HystrixStream stream(stream_max);
+  stream.add_command(&chainer.command());
+  app.set_hystrix_stream(&stream);
+  metrics::Prometheus prom(threads, app::HolaApp::kNumRoutes);
+  prom.set_tracer(to.enabled ? &tracer : nullptr);
+  prom.set_command(&chainer.command());
+  app.set_prometheus(&prom);
+
+  cfg.start([&](const config::Snapshot& s) {
+    app.on_config(s);
+    chainer.update_settings(hystrix_settings(s.hystrix));
+  });
+
+  chainer.start();
+  tracer.start();
+  server.start();
+
+  LOG_INFO("hola listening on %s:%d (workers=%d, cpus=%s, accept=%s, tracing=%s, aloha=%s)", so.host.c_str(),
+           server.port(), threads, cpus.empty() ? "unpinned" : format_cpu_list(cpus).c_str(),
+           so.reuseport_accept ? "reuseport" : "rr",
+           !to.enabled ? "off" : (to.collector_url.empty() ? "on (no collector: spans dropped)" : to.collector_url.c_str()),
+           chainer.full_url().c_str());
+  if (!port_file.empty()) {
+    std::string tmp = port_file + ".tmp";
+    {
+      std::ofstream f(tmp);
+      f << server.port() << "\n";
+    }
+    rename(tmp.c_str(), port_file.c_str());
+  }
+
+  int sig = 0;
+  sigwait(&sigs, &sig);
+  LOG_INFO("received %s: draining (up to %d ms)", sig == SIGTERM ? "SIGTERM" : "SIGINT", drain_ms);
+  server.shutdown(drain_ms);
+  server.join();
+  cfg.stop();
+  chainer.stop();
+  tracer.stop();
+  LOG_INFO("shutdown complete (%llu requests served)", (unsigned long long)server.total_requests());
+  Logger::instance().flush();
+  return 0;
+}

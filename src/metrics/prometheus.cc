@@ -1,0 +1,67 @@
+#include "metrics/prometheus.h"
+
+#include "app/hola_app.h"
+#include "http/server.h"
+#include "resilience/hystrix.h"
+#include "tracing/tracer.h"
+
+namespace hola::metrics {
+
+Prometheus::Prometheus(int num_workers, int num_routes)
+    : nworkers_(num_workers), nroutes_(num_routes), counts_(new Counter[size_t(num_workers) * size_t(num_routes)]) {}
+
+std::string Prometheus::render(http::Server* server) const {
+  std::string o;
+  o += "# HELP hola_requests_total Requests by route.\n# TYPE hola_requests_total counter\n";
+  for (int r = 0; r < nroutes_; ++r) {
+    uint64_t n = 0;
+    for (int w = 0; w < nworkers_; ++w)
+      n += counts_[size_t(w) * size_t(nroutes_) + size_t(r)].v.load(std::memory_order_relaxed);
+    o += "hola_requests_total{route=\"";
+    o += app::HolaApp::route_name(r);
+    o += "\"} " + std::to_string(n) + "\n";
+  }
+  if (server) {
+    uint64_t acc = 0, closed = 0, perr = 0, bin = 0, bout = 0, req = 0;
+    for (size_t i = 0; i < server->num_workers(); ++i) {
+      auto& s = server->worker(i).stats();
+      acc += s.accepted.load(std::memory_order_relaxed);
+      closed += s.closed.load(std::memory_order_relaxed);
+      perr += s.parse_errors.load(std::memory_order_relaxed);
+      bin += s.bytes_in.load(std::memory_order_relaxed);
+      bout += s.bytes_out.load(std::memory_order_relaxed);
+      req += s.requests.load(std::memory_order_relaxed);
+    }
+    o += "# TYPE hola_http_requests_total counter\nhola_http_requests_total " + std::to_string(req) + "\n";
+    o += "# TYPE hola_connections_accepted_total counter\nhola_connections_accepted_total " + std::to_string(acc) + "\n";
+    o += "# TYPE hola_connections_open gauge\nhola_connections_open " + std::to_string(acc - closed) + "\n";
+    o += "# TYPE hola_parse_errors_total counter\nhola_parse_errors_total " + std::to_string(perr) + "\n";
+    o += "# TYPE hola_bytes_in_total counter\nhola_bytes_in_total " + std::to_string(bin) + "\n";
+    o += "# TYPE hola_bytes_out_total counter\nhola_bytes_out_total " + std::to_string(bout) + "\n";
+    o += "# TYPE hola_workers gauge\nhola_workers " + std::to_string(server->num_workers()) + "\n";
+  }
+  if (tracer_) {
+    tracing::TracerStats t = tracer_->stats();
+    o += "# TYPE hola_spans_recorded_total counter\nhola_spans_recorded_total " + std::to_string(t.recorded) + "\n";
+    o += "# TYPE hola_spans_reported_total counter\nhola_spans_reported_total " + std::to_string(t.reported) + "\n";
+    o += "# TYPE hola_spans_dropped_total counter\nhola_spans_dropped_total{reason=\"ring_full\"} " +
+         std::to_string(t.dropped_ring) + "\nhola_spans_dropped_total{reason=\"collector\"} " +
+         std::to_string(t.dropped_no_collector) + "\n";
+    o += "# TYPE hola_span_post_failures_total counter\nhola_span_post_failures_total " + std::to_string(t.post_failures) + "\n";
+  }
+  if (cmd_) {
+    resilience::CommandSnapshot s = cmd_->snapshot();
+    o += "# TYPE hola_hystrix_events_total counter\n";
+    for (int e = 0; e < resilience::kNumEvents; ++e) {
+      if (!s.cumulative[size_t(e)]) continue;
+      o += "hola_hystrix_events_total{command=\"" + s.name + "\",event=\"" + resilience::event_name(resilience::Event(e)) +
+           "\"} " + std::to_string(s.cumulative[size_t(e)]) + "\n";
+    }
+    o += "# TYPE hola_hystrix_circuit_open gauge\nhola_hystrix_circuit_open{command=\"" + s.name + "\"} " +
+         (s.circuit_open ? "1" : "0") + "\n";
+  }
+  if (reloads_) o += "# TYPE hola_config_reloads_total counter\nhola_config_reloads_total " + std::to_string(reloads_->load()) + "\n";
+  return o;
+}
+
+}  // namespace hola::metrics

@@ -1,0 +1,241 @@
+// hola_amd._native — Python bindings to the C++ core, used by the unit tests so they exercise
+// the exact code the server runs (properties parser, String.format subset, B3 codec, Accept
+// negotiation, HTTP parser, JSON codec, Hystrix state machine on a fake clock, span encoding).
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "config/jformat.h"
+#include "config/properties.h"
+#include "config/resolver.h"
+#include "http/negotiate.h"
+#include "http/parser.h"
+#include "json/json.h"
+#include "resilience/hystrix.h"
+#include "tracing/b3.h"
+#include "tracing/tracer.h"
+#include "metrics/hystrix_stream.h"
+
+namespace py = pybind11;
+using namespace hola;
+
+namespace {
+
+py::dict parse_properties_py(py::bytes data) {
+  std::string s = data;
+  config::PropertiesResult r = config::parse_properties(s);
+  py::dict out;
+  out["ok"] = r.ok;
+  out["error"] = r.error;
+  py::dict m;
+  for (auto& [k, v] : r.map) m[py::bytes(k)] = py::bytes(v);
+  out["map"] = m;
+  return out;
+}
+
+py::object java_format_py(const std::string& fmt, const std::vector<std::string>& args) {
+  config::FormatResult r = config::java_format(fmt, args);
+  if (r.ok) return py::bytes(r.value);
+  return py::make_tuple(r.error, r.detail);
+}
+
+py::object parse_request_py(py::bytes data) {
+  std::string s = data;
+  http::Request r;
+  int status = 0;
+  http::Parse p = http::parse_request(s.data(), s.size(), &r, &status);
+  if (p == http::Parse::kIncomplete) return py::str("incomplete");
+  if (p == http::Parse::kError) return py::int_(status);
+  py::dict d;
+  d["method"] = std::string(r.method);
+  d["target"] = std::string(r.target);
+  d["path"] = std::string(r.path);
+  d["query"] = std::string(r.query);
+  d["version_minor"] = r.version_minor;
+  d["keep_alive"] = r.keep_alive;
+  d["has_accept"] = r.has_accept;
+  d["accept"] = std::string(r.accept);
+  d["host"] = std::string(r.host);
+  d["content_length"] = r.content_length;
+  d["chunked"] = r.chunked;
+  d["head_bytes"] = r.head_bytes;
+  d["b3_trace_id"] = std::string(r.b3_trace_id);
+  d["b3_span_id"] = std::string(r.b3_span_id);
+  d["b3_parent_id"] = std::string(r.b3_parent_id);
+  d["b3_sampled"] = std::string(r.b3_sampled);
+  d["b3_flags"] = std::string(r.b3_flags);
+  d["b3_single"] = std::string(r.b3_single);
+  return d;
+}
+
+py::object skip_chunked_py(py::bytes data) {
+  std::string s = data;
+  size_t n = 0;
+  http::Parse p = http::skip_chunked_body(s.data(), s.size(), &n);
+  if (p == http::Parse::kIncomplete) return py::str("incomplete");
+  if (p == http::Parse::kError) return py::str("error");
+  return py::int_(n);
+}
+
+py::object b3_extract_py(const std::string& t, const std::string& s, const std::string& p, const std::string& smp,
+                         const std::string& flags, const std::string& single) {
+  tracing::SpanContext c;
+  tracing::Extract e = tracing::extract(t, s, p, smp, flags, single, &c);
+  if (e == tracing::Extract::kNone) return py::str("none");
+  if (e == tracing::Extract::kNotSampled) return py::str("not_sampled");
+  py::dict d;
+  d["trace_id"] = tracing::trace_id_hex(c.trace_hi, c.trace_id);
+  d["span_id"] = tracing::hex64(c.span_id);
+  d["parent_id"] = c.has_parent ? py::object(py::str(tracing::hex64(c.parent_id))) : py::object(py::none());
+  d["sampled"] = c.sampled;
+  d["debug"] = c.debug;
+  return d;
+}
+
+std::string b3_inject_py(const std::string& trace_id, const std::string& span_id, py::object parent, bool sampled,
+                         bool debug) {
+  tracing::SpanContext c;
+  tracing::parse_trace_id(trace_id, &c.trace_hi, &c.trace_id);
+  tracing::parse_hex64(span_id, &c.span_id);
+  if (!parent.is_none()) {
+    c.has_parent = true;
+    tracing::parse_hex64(parent.cast<std::string>(), &c.parent_id);
+  }
+  c.sampled = sampled;
+  c.debug = debug;
+  std::string h;
+  tracing::inject(c, &h);
+  return h;
+}
+
+py::object decode_string_list_py(py::bytes data) {
+  std::string s = data;
+  std::vector<std::optional<std::string>> out;
+  std::string err;
+  if (!json::decode_string_list(s, &out, &err)) return py::make_tuple("error", err);
+  py::list l;
+  for (auto& o : out) l.append(o ? py::object(py::bytes(*o)) : py::object(py::none()));
+  return l;
+}
+
+py::bytes string_array_py(const std::vector<std::optional<std::string>>& items) {
+  return py::bytes(json::string_array(items));
+}
+
+// Fake-clock Hystrix command for state-machine tests.
+struct PyCommand {
+  FakeClock clock;
+  std::unique_ptr<resilience::Command> cmd;
+  PyCommand(const std::map<std::string, std::string>& props) : clock(1000000) {
+    resilience::Settings s = resilience::settings_from(props, "AlohaService#aloha()", "aloha");
+    cmd = std::make_unique<resilience::Command>("AlohaService#aloha()", "aloha", "aloha", s, clock);
+  }
+  std::string try_start() {
+    switch (cmd->try_start()) {
+      case resilience::Command::Admit::kRun: return "run";
+      case resilience::Command::Admit::kShortCircuited: return "short_circuited";
+      default: return "rejected";
+    }
+  }
+  void finish(const std::string& outcome, int64_t ms) {
+    resilience::Event e = outcome == "success" ? resilience::Event::kSuccess
+                          : outcome == "timeout" ? resilience::Event::kTimeout
+                          : outcome == "bad_request" ? resilience::Event::kBadRequest
+                                                     : resilience::Event::kFailure;
+    cmd->finish(e, ms);
+    if (e != resilience::Event::kSuccess) cmd->fallback(resilience::Event::kFallbackSuccess);
+  }
+  void advance(int64_t ms) { clock.advance(ms); }
+  bool is_open() { return cmd->circuit_open(); }
+  py::dict health() {
+    auto h = cmd->health();
+    py::dict d;
+    d["total"] = h.total;
+    d["errors"] = h.errors;
+    d["error_pct"] = h.error_pct;
+    return d;
+  }
+  std::string stream_json() { return metrics::HystrixStream::command_json(cmd->snapshot()); }
+  std::string pool_json() { return metrics::HystrixStream::threadpool_json(cmd->snapshot()); }
+  py::dict settings() {
+    auto s = cmd->settings();
+    py::dict d;
+    d["timeout_ms"] = s.timeout_ms;
+    d["request_volume_threshold"] = s.request_volume_threshold;
+    d["error_threshold_pct"] = s.error_threshold_pct;
+    d["sleep_window_ms"] = s.sleep_window_ms;
+    d["pool_core_size"] = s.pool_core_size;
+    d["rolling_window_ms"] = s.rolling_window_ms;
+    d["health_snapshot_ms"] = s.health_snapshot_ms;
+    return d;
+  }
+};
+
+std::string encode_spans_py(bool v2, const std::string& trace_id, const std::string& span_id, py::object parent,
+                            const std::string& kind, int64_t start_us, int64_t end_us, const std::string& url,
+                            int status, bool shared) {
+  tracing::TracerOptions o;
+  o.collector_url = "";
+  o.ipv4 = 0x0100007f;  // 127.0.0.1
+  o.port = 8080;
+  tracing::Tracer t(o, 1);
+  tracing::SpanRecord r{};
+  tracing::parse_trace_id(trace_id, &r.trace_hi, &r.trace_id);
+  tracing::parse_hex64(span_id, &r.span_id);
+  r.has_parent = !parent.is_none();
+  if (r.has_parent) tracing::parse_hex64(parent.cast<std::string>(), &r.parent_id);
+  r.kind = kind == "client" ? tracing::Kind::kClient : tracing::Kind::kServer;
+  r.start_us = start_us;
+  r.end_us = end_us;
+  r.status = uint16_t(status);
+  r.shared = shared;
+  r.method_len = 3;
+  memcpy(r.method, "GET", 3);
+  r.url_len = uint16_t(std::min(url.size(), tracing::kMaxUrl));
+  memcpy(r.url, url.data(), r.url_len);
+  r.error_len = 0;
+  return v2 ? t.encode_v2({r}) : t.encode_v1({r});
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_native, m) {
+  m.doc() = "hola native core (C++20) bindings";
+  m.def("parse_properties", &parse_properties_py, "java.util.Properties.load semantics on UTF-8 bytes");
+  m.def("java_format", &java_format_py, "java.lang.String.format subset; bytes or (exception, detail)");
+  m.def("java_string_hash", [](const std::string& s) { return config::java_string_hash(s); });
+  m.def("parse_java_options", &config::parse_java_options);
+  m.def("resolve", [](const std::vector<std::tuple<std::string, int, std::map<std::string, std::string>>>& srcs,
+                      const std::string& key, const std::string& def) {
+    std::vector<config::Source> v;
+    for (auto& [n, o, vals] : srcs) v.push_back({n, o, vals});
+    config::Resolver r(v);
+    config::Resolved x = r.resolve(key, def);
+    return py::make_tuple(x.value, x.source, x.key, x.found);
+  });
+  m.def("accepts", [](const std::string& accept, const std::string& t, const std::string& st) {
+    return http::accepts(accept, t, st);
+  });
+  m.def("parse_request", &parse_request_py);
+  m.def("skip_chunked_body", &skip_chunked_py);
+  m.def("b3_extract", &b3_extract_py, py::arg("trace_id") = "", py::arg("span_id") = "", py::arg("parent_id") = "",
+        py::arg("sampled") = "", py::arg("flags") = "", py::arg("single") = "");
+  m.def("b3_inject", &b3_inject_py, py::arg("trace_id"), py::arg("span_id"), py::arg("parent") = py::none(),
+        py::arg("sampled") = true, py::arg("debug") = false);
+  m.def("decode_string_list", &decode_string_list_py);
+  m.def("string_array", &string_array_py);
+  m.def("json_quote", [](const std::string& s) { return py::bytes(json::quote(s)); });
+  m.def("encode_span", &encode_spans_py, py::arg("v2"), py::arg("trace_id"), py::arg("span_id"),
+        py::arg("parent") = py::none(), py::arg("kind") = "server", py::arg("start_us") = 1000,
+        py::arg("end_us") = 2000, py::arg("url") = "http://localhost/api/hola", py::arg("status") = 200,
+        py::arg("shared") = false);
+  py::class_<PyCommand>(m, "HystrixCommand")
+      .def(py::init<const std::map<std::string, std::string>&>(), py::arg("props") = std::map<std::string, std::string>{})
+      .def("try_start", &PyCommand::try_start)
+      .def("finish", &PyCommand::finish)
+      .def("advance", &PyCommand::advance)
+      .def("is_open", &PyCommand::is_open)
+      .def("health", &PyCommand::health)
+      .def("stream_json", &PyCommand::stream_json)
+      .def("pool_json", &PyCommand::pool_json)
+      .def("settings", &PyCommand::settings);
+}

@@ -1,0 +1,181 @@
+// Hystrix-compatible resilience for the aloha call:
+// circuit breaker + bulkhead + timeout + fallback, with Hystrix's rolling-window metrics
+// so /hystrix.stream can report dashboard-compatible JSON.
+//
+// Semantics follow Hystrix 1.5.1 (pom.xml:60) [lib-default]:
+//  * health counts over a rolling window (10 s in 10 buckets), recomputed at most every
+//    healthSnapshot interval (500 ms);
+//  * the breaker trips when requests >= requestVolumeThreshold (tuned to 5 in
+//    config.properties:19) and error% >= errorThresholdPercentage (50);
+//    errors = FAILURE + TIMEOUT + THREAD_POOL_REJECTED + SEMAPHORE_REJECTED;
+//  * while open, one trial request is let through every sleepWindow (5 s); a success closes
+//    the circuit and resets the counts;
+//  * bulkhead = thread pool of coreSize 10 with no queue (maxQueueSize -1): the 11th
+//    concurrent call is rejected straight to the fallback;
+//  * execution timeout 1000 ms by default, 600 ms per config.properties:17.
+// All time comes from an injectable Clock so tests can drive the state machine.
+#pragma once
+#include <array>
+#include <cstdint>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "core/clock.h"
+
+namespace hola::resilience {
+
+enum class Event : int {
+  kSuccess = 0, kFailure, kTimeout, kShortCircuited, kThreadPoolRejected, kSemaphoreRejected,
+  kBadRequest, kFallbackSuccess, kFallbackFailure, kFallbackRejection, kFallbackMissing,
+  kExceptionThrown, kResponseFromCache, kEmit, kFallbackEmit, kCollapsed, kNumEvents
+};
+constexpr int kNumEvents = int(Event::kNumEvents);
+const char* event_name(Event e);
+
+struct Settings {
+  // command
+  int timeout_ms = 1000;
+  bool timeout_enabled = true;
+  bool circuit_enabled = true;
+  int request_volume_threshold = 20;
+  int error_threshold_pct = 50;
+  int sleep_window_ms = 5000;
+  bool force_open = false;
+  bool force_closed = false;
+  int rolling_window_ms = 10000;
+  int rolling_buckets = 10;
+  int health_snapshot_ms = 500;
+  int percentile_window_ms = 60000;
+  int percentile_buckets = 6;
+  bool percentile_enabled = true;
+  bool fallback_enabled = true;
+  int fallback_max_concurrent = 10;
+  int semaphore_max_concurrent = 10;
+  std::string isolation = "THREAD";
+  bool request_cache_enabled = true;
+  bool request_log_enabled = true;
+  // thread pool (bulkhead)
+  int pool_core_size = 10;
+  int pool_max_queue = -1;
+  int pool_queue_reject_threshold = 5;
+  int pool_keep_alive_minutes = 1;
+};
+
+// Resolves `hystrix.command.<cmd>.*` > `hystrix.command.default.*` > built-in defaults, and
+// `hystrix.threadpool.<pool>.*` > `hystrix.threadpool.default.*`.
+Settings settings_from(const std::map<std::string, std::string>& props, const std::string& command_key,
+                       const std::string& pool_key);
+
+// Bucketed rolling event counter.
+class RollingCounter {
+ public:
+  RollingCounter(int window_ms, int buckets);
+  void add(int64_t now_ms, Event e, int64_t n = 1);
+  void update_max_concurrency(int64_t now_ms, int64_t v);
+  std::array<int64_t, kNumEvents> sums(int64_t now_ms);
+  int64_t max_concurrency(int64_t now_ms);
+  std::array<int64_t, kNumEvents> cumulative() const { return cumulative_; }
+  void reset(int64_t now_ms);
+
+ private:
+  struct Bucket {
+    int64_t start = -1;
+    std::array<int64_t, kNumEvents> c{};
+    int64_t max_conc = 0;
+  };
+  Bucket& current(int64_t now_ms);
+  int window_ms_, nb_, bucket_ms_;
+  std::vector<Bucket> b_;
+  std::array<int64_t, kNumEvents> cumulative_{};
+};
+
+// Rolling latency percentiles (log-linear histogram per bucket, 0.1 ms .. ~1 h).
+class RollingPercentile {
+ public:
+  RollingPercentile(int window_ms, int buckets);
+  void add(int64_t now_ms, int64_t value_ms);
+  // Percentile in ms for p in [0,100]; mean. Returns 0 when empty.
+  int64_t percentile(int64_t now_ms, double p);
+  int64_t mean(int64_t now_ms);
+
+ private:
+  static constexpr int kBins = 512;
+  static int bin_of(int64_t v);
+  static int64_t bin_value(int b);
+  struct Bucket {
+    int64_t start = -1;
+    std::array<uint32_t, kBins> h{};
+    int64_t sum = 0, count = 0;
+  };
+  Bucket& current(int64_t now_ms);
+  void merged(int64_t now_ms, std::array<uint64_t, kBins>* h, int64_t* sum, int64_t* count);
+  int window_ms_, nb_, bucket_ms_;
+  std::vector<Bucket> b_;
+};
+
+struct HealthCounts {
+  int64_t total = 0, errors = 0;
+  int error_pct = 0;
+};
+
+struct CommandSnapshot {
+  std::string name, group, pool;
+  int64_t now_wall_ms = 0;
+  bool circuit_open = false;
+  HealthCounts health;
+  std::array<int64_t, kNumEvents> rolling{}, cumulative{};
+  int64_t concurrent = 0, rolling_max_concurrent = 0;
+  // percentiles 0,25,50,75,90,95,99,99.5,100 + mean
+  std::array<int64_t, 9> latency_execute{}, latency_total{};
+  int64_t latency_execute_mean = 0, latency_total_mean = 0;
+  Settings settings;
+  // thread pool view
+  int64_t pool_active = 0, pool_largest = 0, pool_completed = 0, pool_rolling_executed = 0,
+          pool_rolling_max_active = 0, pool_rolling_rejected = 0;
+  bool has_executed = false;
+};
+
+class Command {
+ public:
+  Command(std::string name, std::string group, std::string pool, Settings s, const Clock& clock);
+
+  enum class Admit { kRun, kShortCircuited, kRejected };
+  // Breaker + bulkhead admission. kRun takes a bulkhead slot that finish() releases.
+  Admit try_start();
+  // Outcome of an admitted execution: kSuccess, kFailure, kTimeout or kBadRequest.
+  void finish(Event outcome, int64_t execute_ms);
+  // After a short-circuit/rejection/failure/timeout the fallback runs; record its result
+  // and the total latency of the whole command.
+  void fallback(Event fallback_event);
+  void total_latency(int64_t total_ms);
+
+  bool circuit_open();            // evaluates health like HystrixCircuitBreaker.isOpen()
+  HealthCounts health();
+  CommandSnapshot snapshot();
+  void update_settings(const Settings& s);
+  Settings settings();
+  const std::string& name() const { return name_; }
+
+ private:
+  bool is_open_locked(int64_t now);
+  bool allow_request_locked(int64_t now);
+  HealthCounts health_locked(int64_t now);
+
+  std::string name_, group_, pool_;
+  Settings s_;
+  const Clock& clock_;
+  std::mutex mu_;
+  RollingCounter counter_;
+  RollingCounter pool_counter_;
+  RollingPercentile exec_lat_, total_lat_;
+  bool open_ = false;
+  int64_t opened_or_tested_ = 0;
+  HealthCounts health_cache_;
+  int64_t health_at_ = -1;
+  int64_t active_ = 0, largest_ = 0, completed_ = 0;
+  bool executed_ = false;
+};
+
+}  // namespace hola::resilience

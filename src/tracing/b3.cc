@@ -1,0 +1,107 @@
+#include "tracing/b3.h"
+
+namespace hola::tracing {
+
+namespace {
+int hexdigit(char c) {
+  if (c >= '0' && c <= '9') return c - '0';
+  if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+  if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+  return -1;
+}
+bool is_true(std::string_view s) { return s == "1" || s == "true" || s == "TRUE" || s == "True"; }
+bool is_false(std::string_view s) { return s == "0" || s == "false" || s == "FALSE" || s == "False"; }
+}  // namespace
+
+bool parse_hex64(std::string_view s, uint64_t* out) {
+  if (s.empty() || s.size() > 16) return false;
+  uint64_t v = 0;
+  for (char c : s) {
+    int d = hexdigit(c);
+    if (d < 0) return false;
+    v = (v << 4) | uint64_t(d);
+  }
+  *out = v;
+  return true;
+}
+
+bool parse_trace_id(std::string_view s, uint64_t* hi, uint64_t* lo) {
+  if (s.size() > 16) {
+    if (s.size() != 32) return false;
+    return parse_hex64(s.substr(0, 16), hi) && parse_hex64(s.substr(16), lo);
+  }
+  *hi = 0;
+  return parse_hex64(s, lo);
+}
+
+void hex64(uint64_t v, char out[16]) {
+  static const char* d = "0123456789abcdef";
+  for (int i = 15; i >= 0; --i) {
+    out[i] = d[v & 15];
+    v >>= 4;
+  }
+}
+
+std::string hex64(uint64_t v) {
+  char b[16];
+  hex64(v, b);
+  return std::string(b, 16);
+}
+
+std::string trace_id_hex(uint64_t hi, uint64_t lo) { return hi ? hex64(hi) + hex64(lo) : hex64(lo); }
+
+Extract extract(std::string_view trace_id, std::string_view span_id, std::string_view parent_id,
+                std::string_view sampled, std::string_view flags, std::string_view single,
+                SpanContext* out) {
+  *out = SpanContext();
+  if (!single.empty()) {
+    // b3: {TraceId}-{SpanId}[-{SamplingState}[-{ParentSpanId}]]  or just {SamplingState}
+    if (single == "0") return Extract::kNotSampled;
+    if (single.find('-') == std::string_view::npos) return Extract::kNone;  // "1"/"d": no ids
+    size_t a = single.find('-');
+    std::string_view t = single.substr(0, a);
+    std::string_view rest = single.substr(a + 1);
+    size_t b = rest.find('-');
+    std::string_view sp = rest.substr(0, b);
+    std::string_view state, parent;
+    if (b != std::string_view::npos) {
+      rest = rest.substr(b + 1);
+      size_t c = rest.find('-');
+      state = rest.substr(0, c);
+      if (c != std::string_view::npos) parent = rest.substr(c + 1);
+    }
+    if (state == "0") return Extract::kNotSampled;
+    if (!parse_trace_id(t, &out->trace_hi, &out->trace_id) || !parse_hex64(sp, &out->span_id))
+      return Extract::kNone;
+    if (!parent.empty() && parse_hex64(parent, &out->parent_id)) out->has_parent = true;
+    out->sampled = true;
+    out->debug = state == "d";
+    return Extract::kContext;
+  }
+  bool debug = flags == "1";
+  if (sampled.empty() && !debug) return Extract::kNone;
+  if (!debug && is_false(sampled)) return Extract::kNotSampled;
+  if (!debug && !is_true(sampled)) return Extract::kNone;
+  if (trace_id.empty() || span_id.empty()) return Extract::kNone;
+  if (!parse_trace_id(trace_id, &out->trace_hi, &out->trace_id) || !parse_hex64(span_id, &out->span_id))
+    return Extract::kNone;
+  if (!parent_id.empty() && parse_hex64(parent_id, &out->parent_id)) out->has_parent = true;
+  out->sampled = true;
+  out->debug = debug;
+  return Extract::kContext;
+}
+
+void inject(const SpanContext& ctx, std::string* h) {
+  *h += "X-B3-TraceId: ";
+  *h += trace_id_hex(ctx.trace_hi, ctx.trace_id);
+  *h += "\r\nX-B3-SpanId: ";
+  *h += hex64(ctx.span_id);
+  if (ctx.has_parent) {
+    *h += "\r\nX-B3-ParentSpanId: ";
+    *h += hex64(ctx.parent_id);
+  }
+  *h += ctx.sampled ? "\r\nX-B3-Sampled: 1\r\n" : "\r\nX-B3-Sampled: 0\r\n";
+  if (ctx.debug) *h += "X-B3-Flags: 1\r\n";
+}
+
+}  // namespace hola::tracing

@@ -1,0 +1,135 @@
+// Zipkin tracing — the Brave role (ZipkinResource.java:31-41, ZipKinFilter.java:39-44,
+// HolaResource.java:97-108).
+//
+// Request path cost: one B3 parse, one random id, two clock reads and a fixed-size record
+// copied into the worker's single-producer ring. One reporter thread drains all rings about
+// every second and POSTs Zipkin v1 JSON to $ZIPKIN_SERVER_URL/api/v1/spans (v2 optional).
+// When the collector is unset or down, spans are dropped and counted — never blocking.
+#pragma once
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "tracing/b3.h"
+
+namespace hola::http {
+struct Request;
+}
+
+namespace hola::tracing {
+
+constexpr size_t kMaxUrl = 200;
+
+struct ServerSpan {
+  SpanContext ctx;
+  int64_t start_us = 0;
+  bool record = false;  // sampled: emit on end
+  bool shared = false;  // joined the caller's span id (caller owns timestamp/duration)
+  uint8_t method_len = 0;
+  char method[8] = {0};
+  uint16_t url_len = 0;
+  char url[kMaxUrl] = {0};
+};
+
+enum class Kind : uint8_t { kServer = 0, kClient = 1 };
+
+struct SpanRecord {
+  uint64_t trace_hi, trace_id, span_id, parent_id;
+  int64_t start_us, end_us;
+  Kind kind;
+  bool has_parent, shared, debug;
+  uint16_t status;
+  uint8_t method_len;
+  char method[8];
+  uint16_t url_len;
+  char url[kMaxUrl];
+  uint16_t error_len;
+  char error[48];
+};
+
+// Bounded single-producer/single-consumer ring.
+class SpanRing {
+ public:
+  explicit SpanRing(size_t capacity_pow2);
+  bool push(const SpanRecord& r);
+  size_t drain(std::vector<SpanRecord>* out);
+
+ private:
+  std::vector<SpanRecord> buf_;
+  size_t mask_;
+  alignas(64) std::atomic<uint64_t> head_{0};  // consumer
+  alignas(64) std::atomic<uint64_t> tail_{0};  // producer
+};
+
+struct TracerOptions {
+  std::string service_name = "hola";  // Brave.Builder("hola"), ZipkinResource.java:36
+  std::string collector_url;          // $ZIPKIN_SERVER_URL; empty => spans dropped (counted)
+  bool enabled = true;
+  double sample_rate = 1.0;           // Brave default: sample everything
+  int flush_interval_ms = 1000;       // HttpSpanCollector default flush interval
+  bool v2 = false;                    // POST /api/v2/spans instead of /api/v1/spans
+  uint32_t ipv4 = 0;                  // endpoint address (network order)
+  int port = 8080;
+  size_t ring_capacity = 8192;
+};
+
+struct TracerStats {
+  uint64_t recorded = 0, dropped_ring = 0, dropped_no_collector = 0, reported = 0, post_failures = 0;
+};
+
+class Tracer {
+ public:
+  Tracer(TracerOptions o, int num_workers);
+  ~Tracer();
+  bool enabled() const { return o_.enabled; }
+  void start();
+  void stop();  // flushes what is buffered
+
+  // Server side (ServerRequestInterceptor / ServerResponseInterceptor).
+  ServerSpan begin_server(int worker, const http::Request& r);
+  void end_server(int worker, const ServerSpan& s, int status);
+  // Client side (BraveHttpRequestInterceptor / ResponseInterceptor): child of `parent`.
+  SpanContext new_child(int worker, const SpanContext& parent);
+  void record_client(int worker, const SpanContext& ctx, int64_t start_us, int64_t end_us,
+                     std::string_view url, int status, std::string_view error);
+
+  TracerStats stats() const;
+  // Zipkin JSON for a batch (exposed for tests).
+  std::string encode_v1(const std::vector<SpanRecord>& spans) const;
+  std::string encode_v2(const std::vector<SpanRecord>& spans) const;
+  const TracerOptions& options() const { return o_; }
+  // Drains all rings and reports synchronously (used by shutdown and tests).
+  void flush();
+
+ private:
+  uint64_t next_id(int worker);
+  void push(int worker, const SpanRecord& r);
+  void run();
+  bool post(const std::string& body);
+  void endpoint_json(std::string* out) const;
+
+  TracerOptions o_;
+  struct alignas(64) WorkerState {
+    uint64_t s0, s1;  // xorshift128+
+    std::unique_ptr<SpanRing> ring;
+    std::atomic<uint64_t> recorded{0}, dropped{0};
+  };
+  std::vector<std::unique_ptr<WorkerState>> ws_;
+  std::thread th_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  bool stop_ = false, running_ = false;
+  std::mutex flush_mu_;
+  std::atomic<uint64_t> reported_{0}, dropped_no_collector_{0}, post_failures_{0};
+  // collector connection (reporter thread only)
+  int cfd_ = -1;
+  std::string chost_, cpath_;
+  int cport_ = 0;
+};
+
+}  // namespace hola::tracing

@@ -1,0 +1,189 @@
+"""The behavioural contract of the reference service, end to end against the
+native server binary."""
+import json
+import socket
+
+import pytest
+
+
+def test_hola_default_greeting(hola):
+    s = hola(env={"HOSTNAME": "h"})
+    st, h, body = s.get("/api/hola")
+    assert st == 200
+    assert body == b"Hola de h"
+    assert h["content-type"].split(";")[0] == "text/plain"
+    assert h["access-control-allow-origin"] == "*"  # CorsFilter.java:31
+
+
+def test_hola_hostname_unset(hola_bin):
+    from hola_amd.server import HolaProcess
+
+    with HolaProcess(env={}) as s:  # HOSTNAME absent -> "unknown" (HolaResource.java:57)
+        st, _, body = s.get("/api/hola")
+    assert (st, body) == (200, b"Hola de unknown")
+
+
+def test_hola_with_translation_file(hola):
+    from pathlib import Path
+
+    conf = Path(__file__).resolve().parent.parent / "translation.properties"
+    s = hola(args=[f"-Dconf={conf}"], env={"HOSTNAME": "h"})
+    st, _, body = s.get("/api/hola")
+    # translation.properties ends in a literal backslash-n escape -> a real newline
+    assert (st, body) == (200, b"Hola de h mediante el archivo de configuraciones\n")
+
+
+def test_chaining_fallback_when_aloha_down(hola):
+    s = hola(args=["--aloha-url", "http://127.0.0.1:1/", "--feign-log", "none"], env={"HOSTNAME": "h"})
+    st, h, body = s.get("/api/hola-chaining")
+    assert st == 200
+    assert h["content-type"].split(";")[0] == "application/json"
+    assert h["access-control-allow-origin"] == "*"
+    assert json.loads(body) == ["Hola de h", "Aloha response (fallback)"]
+
+
+def test_health(hola):
+    s = hola()
+    st, h, body = s.get("/api/health")
+    assert (st, body) == (200, b"I'm ok")
+    assert h["content-type"].split(";")[0] == "text/plain"
+    assert h["access-control-allow-origin"] == "*"
+
+
+def test_head(hola):
+    s = hola(env={"HOSTNAME": "h"})
+    st, h, body = s.get("/api/hola", method="HEAD")
+    assert st == 200 and body == b""
+    assert h["content-length"] == str(len("Hola de h"))
+    assert h["access-control-allow-origin"] == "*"
+
+
+def test_options(hola):
+    s = hola()
+    st, h, body = s.get("/api/hola", method="OPTIONS")
+    assert st == 200
+    assert set(x.strip() for x in h["allow"].split(",")) == {"GET", "HEAD", "OPTIONS"}
+
+
+@pytest.mark.parametrize("method", ["POST", "PUT", "DELETE", "PATCH"])
+def test_method_not_allowed(hola, method):
+    s = hola()
+    st, h, _ = s.get("/api/hola", method=method, body=b"x" if method != "DELETE" else None)
+    assert st == 405
+    assert "GET" in h["allow"]
+
+
+@pytest.mark.parametrize("accept,status", [
+    ("application/json", 406),
+    ("text/plain", 200),
+    ("text/*", 200),
+    ("*/*", 200),
+    ("text/html, */*;q=0.1", 200),
+    ("*/*, text/plain;q=0", 406),
+    ("text/html, image/gif, image/jpeg, *; q=.2, */*; q=.2", 200),  # Java HttpURLConnection default
+])
+def test_negotiation(hola, accept, status):
+    s = hola()
+    st, _, _ = s.get("/api/hola", headers={"Accept": accept})
+    assert st == status
+
+
+def test_chaining_negotiation(hola):
+    s = hola(args=["--aloha-url", "http://127.0.0.1:1/", "--feign-log", "none"])
+    assert s.get("/api/hola-chaining", headers={"Accept": "text/plain"})[0] == 406
+    assert s.get("/api/hola-chaining", headers={"Accept": "application/json"})[0] == 200
+
+
+def test_not_found(hola):
+    s = hola()
+    assert s.get("/api/nope")[0] == 404
+    assert s.get("/api")[0] == 404
+    st, h, body = s.get("/nope")
+    assert st == 404 and b"Not Found" in body
+
+
+def test_index_and_swagger(hola):
+    s = hola()
+    st, h, body = s.get("/")
+    assert st == 200 and h["content-type"].startswith("text/html")
+    assert b"webjars/swagger-ui/2.1.4/?url=" in body and b"api/swagger.json" in body
+    st, h, body = s.get("/api/swagger.json")
+    assert st == 200 and h["content-type"].split(";")[0] == "application/json"
+    doc = json.loads(body)
+    assert doc["swagger"] == "2.0"
+    info = doc["info"]  # SwaggerListener.java:31-40
+    assert info["title"] == "Hola microservices REST API"
+    assert info["version"] == "1.0.0"
+    assert info["description"] == "Operations that can be invoked in the hola microservices"
+    assert info["license"] == {"name": "Apache 2.0", "url": "http://www.apache.org/licenses/LICENSE-2.0.html"}
+    assert info["contact"]["name"] == "developer@redhat.com"
+    assert doc["basePath"] == "/api" and doc["schemes"] == ["http"]
+    assert set(doc["paths"]) == {"/hola", "/hola-chaining", "/health"}
+    st, h, body = s.get("/webjars/swagger-ui/2.1.4/?url=http://x/api/swagger.json")
+    assert st == 200 and b"swagger" in body.lower()
+
+
+def test_trailing_slash_and_percent_encoding(hola):
+    s = hola(env={"HOSTNAME": "h"})
+    assert s.get("/api/hola/")[2] == b"Hola de h"
+    assert s.get("/api/hol%61")[2] == b"Hola de h"
+    assert s.get("/api/hola?x=1&y=2")[2] == b"Hola de h"
+
+
+def _raw(port, data: bytes, timeout=3.0) -> bytes:
+    with socket.create_connection(("127.0.0.1", port), timeout=timeout) as c:
+        c.sendall(data)
+        c.shutdown(socket.SHUT_WR)
+        out = b""
+        while True:
+            b = c.recv(65536)
+            if not b:
+                break
+            out += b
+    return out
+
+
+def test_pipelining_keeps_order(hola):
+    s = hola(env={"HOSTNAME": "h"})
+    req = b"GET /api/hola HTTP/1.1\r\nHost: x\r\n\r\nGET /api/health HTTP/1.1\r\nHost: x\r\n\r\n" \
+          b"GET /api/hola HTTP/1.1\r\nHost: x\r\nConnection: close\r\n\r\n"
+    out = _raw(s.port, req)
+    assert out.count(b"HTTP/1.1 200 OK") == 3
+    i1, i2, i3 = out.find(b"Hola de h"), out.find(b"I'm ok"), out.rfind(b"Hola de h")
+    assert 0 < i1 < i2 < i3
+    assert b"Connection: close" in out
+
+
+def test_http10_closes(hola):
+    s = hola(env={"HOSTNAME": "h"})
+    out = _raw(s.port, b"GET /api/hola HTTP/1.0\r\n\r\n")
+    assert out.startswith(b"HTTP/1.1 200 OK") and b"Connection: close" in out and out.endswith(b"Hola de h")
+
+
+@pytest.mark.parametrize("raw,status", [
+    (b"GARBAGE\r\n\r\n", b"400"),
+    (b"GET /api/hola HTTP/2.0\r\n\r\n", b"505"),
+    (b"GET /api/hola HTTP/1.1\r\nBad Header\r\n\r\n", b"400"),
+    (b"GET /api/hola HTTP/1.1\r\nContent-Length: 5\r\nTransfer-Encoding: chunked\r\n\r\n", b"400"),
+])
+def test_malformed_requests(hola, raw, status):
+    s = hola()
+    out = _raw(s.port, raw)
+    assert out.split(b" ")[1] == status
+    # the server survives
+    assert s.get("/api/health")[0] == 200
+
+
+def test_request_bodies_are_skipped(hola):
+    s = hola(env={"HOSTNAME": "h"})
+    req = (b"GET /api/hola HTTP/1.1\r\nContent-Length: 4\r\n\r\nabcd"
+           b"GET /api/hola HTTP/1.1\r\nTransfer-Encoding: chunked\r\n\r\n3\r\nabc\r\n0\r\n\r\n"
+           b"GET /api/health HTTP/1.1\r\nConnection: close\r\n\r\n")
+    out = _raw(s.port, req)
+    assert out.count(b"200 OK") == 3 and out.endswith(b"I'm ok")
+
+
+def test_date_header(hola):
+    s = hola()
+    _, h, _ = s.get("/api/hola")
+    assert h["date"].endswith("GMT") and len(h["date"]) == 29

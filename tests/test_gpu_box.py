@@ -1,0 +1,35 @@
+"""Checks that run on the MI355X box (marked `gpu`): the headline benchmark end to end on the
+real host, and that the native artefacts are the code under test."""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+@pytest.mark.gpu
+def test_native_module_loaded_from_tree(native):
+    # The tests exercise the in-tree C++ core, not a Python stand-in.
+    assert Path(native.__file__).resolve().parent == ROOT / "hola_amd"
+    assert native.java_format("Hola de %s", ["x"]) == b"Hola de x"
+
+
+@pytest.mark.gpu
+def test_bench_json_contract_on_host():
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--steps", "3", "--warmup", "1",
+                        "--reqs-per-conn", "200"], capture_output=True, text=True, timeout=600,
+                       env={**os.environ, "HOLA_BENCH_PORT": "18700"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    out = json.loads(line)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in out
+    assert out["n_gpus"] == 1 and out["steps"] == 3 and out["warmup"] == 1
+    assert out["errors"] == 0 and out["non2xx"] == 0
+    assert out["value"] > 10000  # a pinned native replica on EPYC cores does far more than this
+    assert out["p50_ms"] > 0 and out["p99_ms"] >= out["p50_ms"]
