@@ -1,0 +1,151 @@
+"""In-process fake downstream services for integration tests.
+
+* :class:`FakeAloha`  — the `aloha` service hola chains to (AlohaService.java:25). Its mode can
+  be switched at runtime: ``ok`` / ``slow`` / ``error`` (HTTP 500) / ``garbage`` (invalid
+  JSON) / ``chunked`` / ``close`` (drop the connection). Records every request's headers so
+  tests can check B3 propagation.
+* :class:`FakeZipkin` — a span collector recording POST /api/v1/spans and /api/v2/spans.
+"""
+from __future__ import annotations
+
+import json
+import socket
+import threading
+import time
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+
+
+class _Server(ThreadingHTTPServer):
+    daemon_threads = True
+    allow_reuse_address = True
+
+
+class _Base:
+    def __init__(self, handler_cls):
+        self.server = _Server(("127.0.0.1", 0), handler_cls)
+        self.server.owner = self  # type: ignore[attr-defined]
+        self.port = self.server.server_address[1]
+        self.thread = threading.Thread(target=self.server.serve_forever, daemon=True)
+
+    @property
+    def url(self) -> str:
+        return f"http://127.0.0.1:{self.port}/"
+
+    def start(self):
+        self.thread.start()
+        return self
+
+    def stop(self):
+        self.server.shutdown()
+        self.server.server_close()
+
+    def __enter__(self):
+        return self.start()
+
+    def __exit__(self, *exc):
+        self.stop()
+
+
+class _AlohaHandler(BaseHTTPRequestHandler):
+    protocol_version = "HTTP/1.1"
+
+    def log_message(self, *a):  # silence
+        pass
+
+    def do_GET(self):
+        owner: FakeAloha = self.server.owner  # type: ignore[attr-defined]
+        with owner.lock:
+            owner.requests.append({"path": self.path, "headers": {k.lower(): v for k, v in self.headers.items()}})
+            mode, delay, payload = owner.mode, owner.delay_s, owner.payload
+        if mode == "slow":
+            time.sleep(delay)
+        if mode == "close":
+            self.close_connection = True
+            self.connection.shutdown(socket.SHUT_RDWR)
+            return
+        if self.path != "/api/aloha-chaining":
+            body, status = b"not found", 404
+        elif mode == "error":
+            body, status = b"boom", 500
+        elif mode == "garbage":
+            body, status = b"{not json", 200
+        else:
+            body, status = json.dumps(payload).encode(), 200
+        self.send_response(status)
+        self.send_header("Content-Type", "application/json")
+        if mode == "chunked":
+            self.send_header("Transfer-Encoding", "chunked")
+            self.end_headers()
+            half = len(body) // 2
+            for part in (body[:half], body[half:]):
+                self.wfile.write(b"%x\r\n%s\r\n" % (len(part), part))
+            self.wfile.write(b"0\r\n\r\n")
+        else:
+            self.send_header("Content-Length", str(len(body)))
+            self.end_headers()
+            self.wfile.write(body)
+
+
+class FakeAloha(_Base):
+    def __init__(self, payload=None, mode: str = "ok", delay_s: float = 1.0):
+        self.lock = threading.Lock()
+        self.requests: list[dict] = []
+        self.mode = mode
+        self.delay_s = delay_s
+        self.payload = payload if payload is not None else ["Aloha mai aloha-1", "Bonjour de bonjour-1"]
+        super().__init__(_AlohaHandler)
+
+    def set_mode(self, mode: str, delay_s: float | None = None):
+        with self.lock:
+            self.mode = mode
+            if delay_s is not None:
+                self.delay_s = delay_s
+
+
+class _ZipkinHandler(BaseHTTPRequestHandler):
+    protocol_version = "HTTP/1.1"
+
+    def log_message(self, *a):
+        pass
+
+    def do_POST(self):
+        owner: FakeZipkin = self.server.owner  # type: ignore[attr-defined]
+        n = int(self.headers.get("Content-Length", "0"))
+        body = self.rfile.read(n)
+        with owner.lock:
+            owner.posts.append({"path": self.path, "content_type": self.headers.get("Content-Type"),
+                                "spans": json.loads(body)})
+            status = owner.status
+        self.send_response(status)
+        self.send_header("Content-Length", "0")
+        self.end_headers()
+
+
+class FakeZipkin(_Base):
+    def __init__(self, status: int = 202):
+        self.lock = threading.Lock()
+        self.posts: list[dict] = []
+        self.status = status
+        super().__init__(_ZipkinHandler)
+
+    def spans(self) -> list[dict]:
+        with self.lock:
+            return [s for p in self.posts for s in p["spans"]]
+
+    def wait_for(self, pred, timeout: float = 10.0) -> list[dict]:
+        deadline = time.monotonic() + timeout
+        while time.monotonic() < deadline:
+            sp = self.spans()
+            if pred(sp):
+                return sp
+            time.sleep(0.05)
+        return self.spans()
+
+
+def closed_port() -> int:
+    """A localhost port with nothing listening (connection refused)."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port

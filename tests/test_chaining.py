@@ -1,0 +1,151 @@
+"""GET /api/hola-chaining against a fake aloha: success path, every failure mode falling
+back to ["Aloha response (fallback)"] (HolaResource.java:111-112), the 600 ms timeout
+(config.properties:17), the circuit breaker (config.properties:19) and the bulkhead."""
+import json
+import threading
+import time
+
+import pytest
+
+from hola_amd.testing.fakes import FakeAloha, closed_port
+
+FALLBACK = "Aloha response (fallback)"
+
+
+@pytest.fixture
+def aloha():
+    a = FakeAloha().start()
+    yield a
+    a.stop()
+
+
+def chain(s):
+    st, h, body = s.get("/api/hola-chaining", timeout=10)
+    assert st == 200, body
+    return json.loads(body)
+
+
+def test_success_appends_aloha_list(hola, aloha):
+    s = hola(args=["--aloha-url", aloha.url, "--no-tracing"], env={"HOSTNAME": "h"})
+    assert chain(s) == ["Hola de h", "Aloha mai aloha-1", "Bonjour de bonjour-1"]
+    assert aloha.requests[-1]["path"] == "/api/aloha-chaining"
+
+
+def test_keepalive_reuse(hola, aloha):
+    s = hola(args=["--aloha-url", aloha.url, "--no-tracing", "--feign-log", "none"], threads=1)
+    for _ in range(5):
+        assert chain(s)[1] == "Aloha mai aloha-1"
+    st, _, body = s.get("/metrics")
+    assert st == 200
+
+
+def test_chunked_response(hola, aloha):
+    aloha.set_mode("chunked")
+    s = hola(args=["--aloha-url", aloha.url])
+    assert chain(s)[1:] == ["Aloha mai aloha-1", "Bonjour de bonjour-1"]
+
+
+@pytest.mark.parametrize("mode", ["error", "garbage", "close"])
+def test_failures_fall_back(hola, aloha, mode):
+    aloha.set_mode(mode)
+    s = hola(args=["--aloha-url", aloha.url])
+    assert chain(s) == ["Hola de testhost", FALLBACK]
+
+
+def test_connection_refused_falls_back(hola):
+    s = hola(args=["--aloha-url", f"http://127.0.0.1:{closed_port()}/"])
+    t0 = time.monotonic()
+    assert chain(s)[1:] == [FALLBACK]
+    assert time.monotonic() - t0 < 0.5
+
+
+def test_unknown_host_falls_back(hola):
+    s = hola(args=["--aloha-url", "http://aloha.invalid:8080/"])
+    assert chain(s)[1:] == [FALLBACK]
+
+
+def test_timeout_600ms(hola, aloha):
+    aloha.set_mode("slow", delay_s=2.0)
+    s = hola(args=["--aloha-url", aloha.url])
+    t0 = time.monotonic()
+    assert chain(s)[1:] == [FALLBACK]
+    dt = time.monotonic() - t0
+    assert 0.55 <= dt < 1.5, dt
+
+
+def test_timeout_is_configurable(hola, aloha):
+    aloha.set_mode("slow", delay_s=1.0)
+    s = hola(args=["--aloha-url", aloha.url,
+                   "-Dhystrix.command.default.execution.isolation.thread.timeoutInMilliseconds=150"])
+    t0 = time.monotonic()
+    assert chain(s)[1:] == [FALLBACK]
+    assert time.monotonic() - t0 < 0.6
+
+
+def test_circuit_opens_after_volume_threshold(hola, aloha):
+    aloha.set_mode("error")
+    s = hola(args=["--aloha-url", aloha.url, "--feign-log", "none",
+                   "-Dhystrix.command.default.metrics.healthSnapshot.intervalInMilliseconds=0"])
+    for _ in range(5):  # requestVolumeThreshold=5, 100 % errors
+        assert chain(s)[1:] == [FALLBACK]
+    n_before = len(aloha.requests)
+    aloha.set_mode("ok")
+    for _ in range(5):  # open: short-circuited, aloha is not called
+        assert chain(s)[1:] == [FALLBACK]
+    assert len(aloha.requests) == n_before
+    st, _, body = s.get("/metrics")
+    assert b'hola_hystrix_circuit_open{command="AlohaService#aloha()"} 1' in body
+    assert b'event="SHORT_CIRCUITED"' in body
+
+
+def test_circuit_half_open_recovers_after_sleep_window(hola, aloha):
+    aloha.set_mode("error")
+    s = hola(args=["--aloha-url", aloha.url, "--feign-log", "none",
+                   "-Dhystrix.command.default.metrics.healthSnapshot.intervalInMilliseconds=0",
+                   "-Dhystrix.command.default.circuitBreaker.sleepWindowInMilliseconds=300"])
+    for _ in range(6):
+        chain(s)
+    aloha.set_mode("ok")
+    assert chain(s)[1:] == [FALLBACK]  # still open
+    time.sleep(0.4)
+    assert chain(s)[1] == "Aloha mai aloha-1"  # single trial succeeds -> closed
+    assert chain(s)[1] == "Aloha mai aloha-1"
+
+
+def test_bulkhead_rejects_beyond_pool(hola, aloha):
+    aloha.set_mode("slow", delay_s=0.4)
+    s = hola(args=["--aloha-url", aloha.url, "--feign-log", "none",
+                   "-Dhystrix.threadpool.default.coreSize=2",
+                   "-Dhystrix.command.default.circuitBreaker.enabled=false"], threads=1)
+    results = []
+
+    def one():
+        results.append(chain(s))
+
+    ts = [threading.Thread(target=one) for _ in range(5)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    ok = [r for r in results if r[1] != FALLBACK]
+    assert len(ok) == 2 and len(results) == 5
+    st, _, body = s.get("/metrics")
+    assert b'event="THREAD_POOL_REJECTED"' in body
+
+
+def test_format_error_skips_downstream_call(hola, aloha, tmp_path):
+    conf = tmp_path / "t.properties"
+    conf.write_text("hello=%d\n")
+    s = hola(args=["--aloha-url", aloha.url, f"-Dconf={conf}"])
+    st, _, _ = s.get("/api/hola-chaining")
+    assert st == 500
+    assert aloha.requests == []
+
+
+def test_feign_basic_logging(hola, aloha):
+    s = hola(args=["--aloha-url", aloha.url])
+    chain(s)
+    time.sleep(0.2)
+    log = s.log()
+    assert "[AlohaService#aloha()] ---> GET " in log and "/api/aloha-chaining HTTP/1.1" in log
+    assert "<--- HTTP/1.1 200" in log
