@@ -1,0 +1,130 @@
+"""HTTP/1.1 request parser, Accept negotiation and JSON codec (native), incl. fuzzing."""
+import json
+
+import pytest
+from hypothesis import given, settings, strategies as st
+
+
+def test_simple_request(native):
+    r = native.parse_request(b"GET /api/hola?x=1 HTTP/1.1\r\nHost: a:1\r\nAccept: text/plain\r\n\r\n")
+    assert r["method"] == "GET" and r["path"] == "/api/hola" and r["query"] == "x=1"
+    assert r["host"] == "a:1" and r["accept"] == "text/plain" and r["keep_alive"]
+    assert r["head_bytes"] == len(b"GET /api/hola?x=1 HTTP/1.1\r\nHost: a:1\r\nAccept: text/plain\r\n\r\n")
+
+
+@pytest.mark.parametrize("raw", [b"", b"GET /api/hola HTTP/1.1\r\n", b"GET /api/hola HTTP/1.1\r\nHost: x\r\n",
+                                 b"GET /api/ho"])
+def test_incomplete(native, raw):
+    assert native.parse_request(raw) == "incomplete"
+
+
+@pytest.mark.parametrize("raw,status", [
+    (b"GET\r\n\r\n", 400),
+    (b"GET /x HTTP/1.1 extra\r\n\r\n", 400),
+    (b"G@T /x HTTP/1.1\r\n\r\n", 400),
+    (b"GET /x HTTP/3.0\r\n\r\n", 505),
+    (b"GET /x HTTX/1.1\r\n\r\n", 400),
+    (b"GET /x HTTP/1.1\r\n folded\r\n\r\n", 400),
+    (b"GET /x HTTP/1.1\r\nName : v\r\n\r\n", 400),
+    (b"GET /x HTTP/1.1\r\nContent-Length: abc\r\n\r\n", 400),
+    (b"GET /x HTTP/1.1\r\nContent-Length: 1\r\nContent-Length: 2\r\n\r\n", 400),
+    (b"GET /x HTTP/1.1\r\nTransfer-Encoding: gzip\r\n\r\n", 501),
+    (b"GET /" + b"a" * 9000 + b" HTTP/1.1\r\n\r\n", 414),
+    (b"GET /x HTTP/1.1\r\n" + b"X-Pad: " + b"a" * 17000 + b"\r\n\r\n", 431),
+])
+def test_errors(native, raw, status):
+    assert native.parse_request(raw) == status
+
+
+def test_connection_semantics(native):
+    assert not native.parse_request(b"GET / HTTP/1.1\r\nConnection: close\r\n\r\n")["keep_alive"]
+    assert not native.parse_request(b"GET / HTTP/1.0\r\n\r\n")["keep_alive"]
+    assert native.parse_request(b"GET / HTTP/1.0\r\nConnection: Keep-Alive\r\n\r\n")["keep_alive"]
+    assert not native.parse_request(b"GET / HTTP/1.1\r\nConnection: upgrade, close\r\n\r\n")["keep_alive"]
+
+
+def test_lf_only_and_leading_crlf(native):
+    r = native.parse_request(b"\r\nGET /a HTTP/1.1\nHost: x\n\n")
+    assert r["path"] == "/a" and r["host"] == "x"
+
+
+def test_b3_header_extraction(native):
+    r = native.parse_request(b"GET / HTTP/1.1\r\nX-B3-TraceId: ab\r\nx-b3-spanid: cd\r\nX-B3-ParentSpanId: ef\r\n"
+                             b"X-B3-Sampled: 1\r\nX-B3-Flags: 1\r\nb3: 1-2-1\r\n\r\n")
+    assert (r["b3_trace_id"], r["b3_span_id"], r["b3_parent_id"], r["b3_sampled"], r["b3_flags"], r["b3_single"]) == \
+        ("ab", "cd", "ef", "1", "1", "1-2-1")
+
+
+def test_absolute_form_target(native):
+    r = native.parse_request(b"GET http://host:8080/api/hola?q HTTP/1.1\r\n\r\n")
+    assert r["path"] == "/api/hola"
+
+
+def test_chunked_body(native):
+    assert native.skip_chunked_body(b"3\r\nabc\r\n0\r\n\r\n") == 13
+    assert native.skip_chunked_body(b"3;ext=1\r\nabc\r\n0\r\nTrailer: x\r\n\r\nNEXT") == 31
+    assert native.skip_chunked_body(b"3\r\nab") == "incomplete"
+    assert native.skip_chunked_body(b"zz\r\n") == "error"
+
+
+_token = st.text(alphabet="abcdefghijklmnopqrstuvwxyz-", min_size=1, max_size=10)
+
+
+@settings(max_examples=200, deadline=None)
+@given(st.lists(st.tuples(_token, st.text(alphabet=st.characters(min_codepoint=0x21, max_codepoint=0x7e),
+                                          max_size=20)), max_size=6),
+       st.integers(min_value=1, max_value=40))
+def test_incremental_equals_whole(native, headers, cut):
+    raw = b"GET /p HTTP/1.1\r\n" + b"".join(f"{k}: {v}\r\n".encode() for k, v in headers) + b"\r\n"
+    whole = native.parse_request(raw)
+    if isinstance(whole, int):
+        return
+    for i in range(0, len(raw), cut):
+        part = native.parse_request(raw[:i])
+        assert part == "incomplete" or (isinstance(part, int) and part == whole)
+    assert whole["head_bytes"] == len(raw)
+
+
+@settings(max_examples=500, deadline=None)
+@given(st.binary(max_size=400))
+def test_fuzz_parser_total(native, data):
+    r = native.parse_request(data)
+    assert r == "incomplete" or isinstance(r, (int, dict))
+
+
+# ---- negotiation ----
+
+@pytest.mark.parametrize("accept,ok", [
+    ("text/plain", True), ("TEXT/PLAIN", True), ("text/*", True), ("*/*", True), ("*", True),
+    ("application/json", False), ("text/html", False), ("text/plain;q=0", False),
+    ("*/*;q=0.5, text/plain;q=0", False), ("text/*;q=0, text/plain;q=0.1", True),
+    ("text/plain; charset=utf-8", True), ("", True), ("garbage", True), ("text/plain;q=2", True),
+    ("application/json, text/plain;q=0.001", True),
+])
+def test_accepts_text_plain(native, accept, ok):
+    assert native.accepts(accept, "text", "plain") is ok
+
+
+# ---- JSON ----
+
+def test_json_string_array(native):
+    assert native.string_array(["a", None, 'q"\\\n\x01é']) == '["a",null,"q\\"\\\\\\n\\u0001é"]'.encode()
+    assert native.string_array([]) == b"[]"
+
+
+def test_decode_string_list(native):
+    assert native.decode_string_list(b'["a","b"]') == [b"a", b"b"]
+    assert native.decode_string_list(b' [ "\\u00e9\\ud83d\\ude00", 1.5, true, null ] ') == \
+        ["é😀".encode(), b"1.5", b"true", None]
+    for bad in (b'{"a":1}', b'["a",', b'[["x"]]', b'["a"] x', b'', b'[01]'):
+        r = native.decode_string_list(bad)
+        assert isinstance(r, tuple) and r[0] == "error"
+
+
+@settings(max_examples=300, deadline=None)
+@given(st.lists(st.one_of(st.none(), st.text(max_size=20)), max_size=8))
+def test_json_roundtrip(native, items):
+    enc = native.string_array(items)
+    assert json.loads(enc) == items
+    dec = native.decode_string_list(enc)
+    assert [None if x is None else x.decode() for x in dec] == items

@@ -1,0 +1,184 @@
+"""Hystrix 1.5.1 circuit-breaker state machine on a fake clock (native Command), the
+properties that tune it (config.properties:16-19) and /hystrix.stream (HystrixServlet.java)."""
+import json
+import socket
+import time
+
+import pytest
+
+from hola_amd.testing.fakes import FakeAloha
+
+TUNED = {
+    "hystrix.command.default.execution.isolation.thread.timeoutInMilliseconds": "600",
+    "hystrix.command.default.circuitBreaker.requestVolumeThreshold": "5",
+}
+
+
+def fail_n(cmd, n, outcome="failure"):
+    for _ in range(n):
+        assert cmd.try_start() == "run"
+        cmd.finish(outcome, 3)
+
+
+def test_settings_resolution(native):
+    c = native.HystrixCommand(TUNED)
+    s = c.settings()
+    assert s["timeout_ms"] == 600 and s["request_volume_threshold"] == 5
+    assert s["error_threshold_pct"] == 50 and s["sleep_window_ms"] == 5000  # [lib-default]
+    assert s["pool_core_size"] == 10 and s["rolling_window_ms"] == 10000
+    # command-specific keys beat the defaults
+    c = native.HystrixCommand({**TUNED, "hystrix.command.AlohaService#aloha().circuitBreaker.requestVolumeThreshold": "7",
+                               "hystrix.threadpool.aloha.coreSize": "3"})
+    assert c.settings()["request_volume_threshold"] == 7 and c.settings()["pool_core_size"] == 3
+
+
+def test_below_volume_threshold_stays_closed(native):
+    c = native.HystrixCommand(TUNED)
+    fail_n(c, 4)
+    c.advance(600)
+    assert not c.is_open()
+    assert c.try_start() == "run"
+
+
+def test_trips_at_threshold_and_error_percentage(native):
+    c = native.HystrixCommand(TUNED)
+    fail_n(c, 5)
+    c.advance(600)  # health snapshot interval (500 ms)
+    assert c.is_open()
+    assert c.try_start() == "short_circuited"
+    h = c.health()
+    assert h["total"] == 5 and h["errors"] == 5 and h["error_pct"] == 100
+
+
+def test_error_percentage_below_50_stays_closed(native):
+    c = native.HystrixCommand(TUNED)
+    fail_n(c, 4)
+    fail_n(c, 6, "success")
+    c.advance(600)
+    assert not c.is_open()
+    assert c.health()["error_pct"] == 40
+
+
+def test_timeouts_count_as_errors(native):
+    c = native.HystrixCommand(TUNED)
+    fail_n(c, 5, "timeout")
+    c.advance(600)
+    assert c.is_open()
+
+
+def test_single_trial_after_sleep_window(native):
+    c = native.HystrixCommand(TUNED)
+    fail_n(c, 5)
+    c.advance(600)
+    assert c.try_start() == "short_circuited"
+    c.advance(5000)
+    assert c.try_start() == "short_circuited"   # sleepWindow must be strictly exceeded
+    c.advance(1)
+    assert c.try_start() == "run"               # the single test request
+    assert c.try_start() == "short_circuited"   # only one per window
+    c.finish("failure", 1)                      # trial fails: stays open
+    c.advance(100)
+    assert c.try_start() == "short_circuited"
+    c.advance(5001)
+    assert c.try_start() == "run"
+    c.finish("success", 1)                      # trial succeeds: closes and resets
+    assert not c.is_open()
+    assert c.health()["total"] == 0  # markSuccess() resets the health stream
+    assert c.try_start() == "run"
+
+
+def test_rolling_window_expires_old_failures(native):
+    c = native.HystrixCommand(TUNED)
+    fail_n(c, 4)
+    c.advance(10_500)  # older than the 10 s window
+    fail_n(c, 1)
+    c.advance(600)
+    assert not c.is_open()
+
+
+def test_bulkhead(native):
+    c = native.HystrixCommand({**TUNED, "hystrix.threadpool.default.coreSize": "2"})
+    assert c.try_start() == "run" and c.try_start() == "run"
+    assert c.try_start() == "rejected"
+    c.finish("success", 1)
+    assert c.try_start() == "run"
+
+
+def test_force_open_and_closed(native):
+    c = native.HystrixCommand({"hystrix.command.default.circuitBreaker.forceOpen": "true"})
+    assert c.try_start() == "short_circuited"
+    c = native.HystrixCommand({**TUNED, "hystrix.command.default.circuitBreaker.forceClosed": "true"})
+    fail_n(c, 10)
+    c.advance(600)
+    assert c.try_start() == "run"
+
+
+def test_stream_json_schema(native):
+    c = native.HystrixCommand(TUNED)
+    fail_n(c, 2)
+    fail_n(c, 3, "success")
+    d = json.loads(c.stream_json())
+    assert d["type"] == "HystrixCommand" and d["name"] == "AlohaService#aloha()"
+    for k in ("errorPercentage", "errorCount", "requestCount", "rollingCountSuccess", "rollingCountFailure",
+              "rollingCountTimeout", "rollingCountShortCircuited", "rollingCountThreadPoolRejected",
+              "rollingCountFallbackSuccess", "isCircuitBreakerOpen", "latencyExecute", "latencyTotal",
+              "latencyExecute_mean", "propertyValue_circuitBreakerRequestVolumeThreshold",
+              "propertyValue_executionIsolationThreadTimeoutInMilliseconds", "reportingHosts", "currentTime"):
+        assert k in d, k
+    assert d["rollingCountSuccess"] == 3 and d["rollingCountFailure"] == 2
+    assert d["rollingCountFallbackSuccess"] == 2
+    assert set(d["latencyExecute"]) == {"0", "25", "50", "75", "90", "95", "99", "99.5", "100"}
+    assert d["propertyValue_circuitBreakerRequestVolumeThreshold"] == 5
+    assert d["propertyValue_executionIsolationThreadTimeoutInMilliseconds"] == 600
+    p = json.loads(c.pool_json())
+    assert p["type"] == "HystrixThreadPool" and p["currentCorePoolSize"] == 10
+
+
+def _read_sse(port, path="/hystrix.stream?delay=100", seconds=0.6) -> bytes:
+    with socket.create_connection(("127.0.0.1", port), timeout=3) as s:
+        s.sendall(f"GET {path} HTTP/1.1\r\nHost: x\r\n\r\n".encode())
+        s.settimeout(0.2)
+        out = b""
+        end = time.monotonic() + seconds
+        while time.monotonic() < end:
+            try:
+                b = s.recv(65536)
+                if not b:
+                    break
+                out += b
+            except socket.timeout:
+                pass
+    return out
+
+
+def test_stream_pings_before_first_command(hola):
+    s = hola()
+    out = _read_sse(s.port)
+    head, _, body = out.partition(b"\r\n\r\n")
+    assert b"200 OK" in head and b"text/event-stream" in head
+    assert b"access-control-allow-origin" not in head.lower()  # servlet, not JAX-RS
+    assert b"ping: " in body
+
+
+def test_stream_reports_command_after_chaining(hola):
+    with FakeAloha() as aloha:
+        s = hola(args=["--aloha-url", aloha.url, "--feign-log", "none"])
+        s.get("/api/hola-chaining")
+        out = _read_sse(s.port)
+    events = [json.loads(l[6:]) for l in out.decode(errors="replace").splitlines() if l.startswith("data: {")]
+    types = {e["type"] for e in events}
+    assert types == {"HystrixCommand", "HystrixThreadPool"}
+    cmd = next(e for e in events if e["type"] == "HystrixCommand")
+    assert cmd["name"] == "AlohaService#aloha()" and cmd["rollingCountSuccess"] >= 1
+
+
+def test_stream_connection_limit(hola):
+    s = hola(args=["--hystrix-stream-max", "1"])
+    with socket.create_connection(("127.0.0.1", s.port), timeout=3) as first:
+        first.sendall(b"GET /hystrix.stream HTTP/1.1\r\nHost: x\r\n\r\n")
+        first.recv(100)
+        st, _, body = s.get("/hystrix.stream")
+        assert st == 503
+    time.sleep(0.2)
+    out = _read_sse(s.port, seconds=0.3)
+    assert b"200 OK" in out

@@ -1,0 +1,165 @@
+"""Zipkin tracing parity (ZipkinResource.java, ZipKinFilter.java, HolaResource.java:97-108)
+against a fake collector, plus the B3 codec."""
+import json
+import time
+
+import pytest
+
+from hola_amd.testing.fakes import FakeAloha, FakeZipkin
+
+
+@pytest.fixture
+def zipkin():
+    z = FakeZipkin().start()
+    yield z
+    z.stop()
+
+
+def _annotations(span):
+    return {a["value"] for a in span.get("annotations", [])}
+
+
+def test_server_span_for_hola(hola, zipkin):
+    s = hola(args=["--zipkin-url", zipkin.url.rstrip("/")])
+    assert s.get("/api/hola")[0] == 200
+    spans = zipkin.wait_for(lambda sp: len(sp) >= 1)
+    assert len(spans) == 1
+    sp = spans[0]
+    assert zipkin.posts[0]["path"] == "/api/v1/spans"
+    assert zipkin.posts[0]["content_type"] == "application/json"
+    assert sp["name"] == "get"
+    assert _annotations(sp) == {"sr", "ss"}
+    assert all(a["endpoint"]["serviceName"] == "hola" for a in sp["annotations"])
+    assert sp["traceId"] == sp["id"] and "parentId" not in sp  # new root trace
+    assert "timestamp" in sp and sp["duration"] >= 1
+    urls = [b["value"] for b in sp["binaryAnnotations"] if b["key"] == "http.url"]
+    assert urls and urls[0].endswith("/api/hola")
+
+
+def test_health_is_not_traced(hola, zipkin):
+    s = hola(args=["--zipkin-url", zipkin.url])
+    for _ in range(3):
+        s.get("/api/health")
+    s.get("/api/hola")
+    spans = zipkin.wait_for(lambda sp: len(sp) >= 1)
+    time.sleep(1.2)
+    spans = zipkin.spans()
+    assert len(spans) == 1 and spans[0]["binaryAnnotations"][0]["value"].endswith("/api/hola")
+
+
+def test_joins_incoming_b3_trace(hola, zipkin):
+    s = hola(args=["--zipkin-url", zipkin.url])
+    s.get("/api/hola", headers={"X-B3-TraceId": "463ac35c9f6413ad", "X-B3-SpanId": "a2fb4a1d1a96d312",
+                                "X-B3-ParentSpanId": "0020000000000001", "X-B3-Sampled": "1"})
+    sp = zipkin.wait_for(lambda sp: len(sp) >= 1)[0]
+    assert sp["traceId"] == "463ac35c9f6413ad"
+    assert sp["id"] == "a2fb4a1d1a96d312"
+    assert sp["parentId"] == "0020000000000001"
+    assert "timestamp" not in sp  # shared span: the caller owns timestamp/duration
+
+
+def test_ids_without_sampled_header_start_new_trace(hola, zipkin):
+    # Brave 3.9's HttpServerRequestAdapter only honours incoming ids with X-B3-Sampled.
+    s = hola(args=["--zipkin-url", zipkin.url])
+    s.get("/api/hola", headers={"X-B3-TraceId": "463ac35c9f6413ad", "X-B3-SpanId": "a2fb4a1d1a96d312"})
+    sp = zipkin.wait_for(lambda sp: len(sp) >= 1)[0]
+    assert sp["traceId"] != "463ac35c9f6413ad"
+
+
+def test_not_sampled_is_not_reported(hola, zipkin):
+    s = hola(args=["--zipkin-url", zipkin.url])
+    s.get("/api/hola", headers={"X-B3-Sampled": "0"})
+    s.get("/api/hola", headers={"b3": "0"})
+    time.sleep(1.5)
+    assert zipkin.spans() == []
+
+
+def test_chaining_client_span_and_b3_propagation(hola, zipkin):
+    with FakeAloha() as aloha:
+        s = hola(args=["--zipkin-url", zipkin.url, "--aloha-url", aloha.url])
+        st, _, body = s.get("/api/hola-chaining")
+        assert st == 200 and json.loads(body)[1] == "Aloha mai aloha-1"
+        spans = zipkin.wait_for(lambda sp: len(sp) >= 2)
+        server = next(x for x in spans if "sr" in _annotations(x))
+        client = next(x for x in spans if "cs" in _annotations(x))
+        assert _annotations(client) == {"cs", "cr"}
+        assert client["traceId"] == server["traceId"]
+        assert client["parentId"] == server["id"]
+        hdr = aloha.requests[-1]["headers"]
+        assert hdr["x-b3-traceid"] == server["traceId"]
+        assert hdr["x-b3-spanid"] == client["id"]
+        assert hdr["x-b3-parentspanid"] == server["id"]
+        assert hdr["x-b3-sampled"] == "1"
+        url = [b["value"] for b in client["binaryAnnotations"] if b["key"] == "http.url"][0]
+        assert url.endswith("/api/aloha-chaining")
+
+
+def test_v2_format(hola, zipkin):
+    s = hola(args=["--zipkin-url", zipkin.url, "--zipkin-v2"])
+    s.get("/api/hola")
+    sp = zipkin.wait_for(lambda sp: len(sp) >= 1)[0]
+    assert zipkin.posts[0]["path"] == "/api/v2/spans"
+    assert sp["kind"] == "SERVER" and sp["localEndpoint"]["serviceName"] == "hola"
+    assert sp["tags"]["http.url"].endswith("/api/hola")
+
+
+def test_collector_down_never_blocks(hola):
+    s = hola(args=["--zipkin-url", "http://127.0.0.1:1"])
+    t0 = time.monotonic()
+    for _ in range(200):
+        assert s.get("/api/hola")[0] == 200
+    assert time.monotonic() - t0 < 5
+    time.sleep(1.3)
+    st, _, body = s.get("/metrics")
+    assert b"hola_span_post_failures_total" in body
+
+
+def test_spans_flushed_on_shutdown(hola_bin, zipkin):
+    from hola_amd.server import HolaProcess
+
+    s = HolaProcess(args=["--zipkin-url", zipkin.url], env={"HOSTNAME": "h"}).start()
+    s.get("/api/hola")
+    s.stop()  # SIGTERM well before the 1 s flush interval
+    assert len(zipkin.spans()) == 1
+
+
+# ---- codec ----
+
+def test_b3_extract_multi(native):
+    d = native.b3_extract(trace_id="463ac35c9f6413ad48485a3953bb6124", span_id="a2fb4a1d1a96d312",
+                          sampled="true")
+    assert d["trace_id"] == "463ac35c9f6413ad48485a3953bb6124" and d["span_id"] == "a2fb4a1d1a96d312"
+    assert d["parent_id"] is None and d["sampled"]
+    assert native.b3_extract(sampled="0") == "not_sampled"
+    assert native.b3_extract(sampled="false", trace_id="1", span_id="2") == "not_sampled"
+    assert native.b3_extract(trace_id="1", span_id="2") == "none"
+    assert native.b3_extract(trace_id="zz", span_id="2", sampled="1") == "none"
+    d = native.b3_extract(trace_id="1", span_id="2", flags="1")
+    assert d["debug"] and d["trace_id"] == "0000000000000001"
+
+
+def test_b3_extract_single(native):
+    d = native.b3_extract(single="80f198ee56343ba864fe8b2a57d3eff7-e457b5a2e4d86bd1-1-05e3ac9a4f6e3b90")
+    assert d["trace_id"] == "80f198ee56343ba864fe8b2a57d3eff7"
+    assert d["span_id"] == "e457b5a2e4d86bd1" and d["parent_id"] == "05e3ac9a4f6e3b90"
+    assert native.b3_extract(single="0") == "not_sampled"
+    assert native.b3_extract(single="a-b-0") == "not_sampled"
+    assert native.b3_extract(single="d") == "none"  # a sampling flag alone carries no ids
+    assert native.b3_extract(single="1-2-d")["debug"]
+
+
+def test_b3_inject(native):
+    h = native.b3_inject("463ac35c9f6413ad", "a2fb4a1d1a96d312", parent="0020000000000001")
+    assert h == ("X-B3-TraceId: 463ac35c9f6413ad\r\nX-B3-SpanId: a2fb4a1d1a96d312\r\n"
+                 "X-B3-ParentSpanId: 0020000000000001\r\nX-B3-Sampled: 1\r\n")
+
+
+def test_span_json_v1(native):
+    sp = json.loads(native.encode_span(False, "1", "2", parent="3", kind="client", start_us=10, end_us=25,
+                                       url="http://aloha:8080/api/aloha-chaining", status=500))[0]
+    assert sp["traceId"] == "0000000000000001" and sp["parentId"] == "0000000000000003"
+    assert sp["timestamp"] == 10 and sp["duration"] == 15
+    assert [a["value"] for a in sp["annotations"]] == ["cs", "cr"]
+    keys = {b["key"]: b["value"] for b in sp["binaryAnnotations"]}
+    assert keys["http.status_code"] == "500"
+    assert sp["annotations"][0]["endpoint"] == {"serviceName": "hola", "ipv4": "127.0.0.1", "port": 8080}
