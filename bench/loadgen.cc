@@ -97,15 +97,27 @@ void signal_done() {
   (void)w;
 }
 
-bool connect_conn(Conn* c, const Options& o) {
+bool connect_once(Conn* c, const Options& o) {
   const Target& t = o.targets[size_t(c->target)];
-  c->fd = connect_blocking(t.addr, t.len, 5000);
+  c->fd = connect_blocking(t.addr, t.len, 1000);
   if (c->fd < 0) return false;
   set_nonblocking(c->fd, true);
   set_nodelay(c->fd);
   c->have = 0;
   c->busy = false;
   return true;
+}
+
+// Reconnect after a failure: like a client-side load balancer, fail over to the next
+// target when the current one refuses, retrying for up to ~5 s (a replica restart).
+bool connect_conn(Conn* c, const Options& o) {
+  const int n = int(o.targets.size());
+  for (int attempt = 0; attempt < 100; ++attempt) {
+    if (connect_once(c, o)) return true;
+    c->target = (c->target + 1) % n;
+    if ((attempt + 1) % n == 0) usleep(50000);
+  }
+  return false;
 }
 
 bool send_req(Conn* c) {
@@ -384,7 +396,7 @@ int main(int argc, char** argv) {
     c->req = o.method + " " + o.path + " HTTP/1.1\r\nHost: " + t.host + ":" + std::to_string(t.port) + "\r\n";
     for (auto& h : o.extra_headers) c->req += h + "\r\n";
     c->req += "\r\n";
-    if (!connect_conn(c.get(), o)) {
+    if (!connect_once(c.get(), o)) {
       fprintf(stderr, "loadgen: connect %s:%d failed: %s\n", t.host.c_str(), t.port, strerror(errno));
       return 1;
     }
@@ -429,7 +441,7 @@ int main(int argc, char** argv) {
         if (g_stop.load()) {
           printf("{\"error\":\"connection failure\"}\n");
           fflush(stdout);
-          return 1;
+          _exit(1);
         }
       }
       for (auto& t : ts) {

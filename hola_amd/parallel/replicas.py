@@ -1,0 +1,159 @@
+"""Pinned replica sets with a supervisor, and the round-robin proxy in front of them.
+
+This is the node-local version of the reference's deployment model: N
+stateless `hola` pods behind a `LoadBalancer` Service (pom.xml:77-80), readiness-gated on
+/api/health (pom.xml:90-94), restarted by the platform when they die.
+"""
+from __future__ import annotations
+
+import os
+import signal
+import subprocess
+import tempfile
+import threading
+import time
+from pathlib import Path
+
+from hola_amd.native import binary
+from hola_amd.server import HolaProcess
+from hola_amd.utils.cpu import format_cpu_list
+from hola_amd.utils.net import free_port, wait_http
+
+
+class ReplicaSet:
+    """N `hola` replicas on distinct ports, each pinned to its own CPU list.
+
+    HOSTNAME is set to ``replica-<i>`` so responses identify the replica (the k8s pod name
+    plays that role in the reference). With ``supervise=True`` a background thread restarts
+    any replica that exits (the platform's restart policy).
+    """
+
+    def __init__(self, n: int, cpu_plan: list[list[int]] | None = None, threads_per_replica: int = 1,
+                 args: list[str] | None = None, env: dict | None = None, supervise: bool = True,
+                 base_port: int = 0, log_level: str = "warn"):
+        self.n = n
+        self.cpu_plan = cpu_plan
+        self.threads = threads_per_replica
+        self.args = list(args or [])
+        self.env = dict(env or {})
+        self.supervise = supervise
+        self.log_level = log_level
+        self.ports = [base_port + i if base_port else free_port() for i in range(n)]
+        self.procs: list[HolaProcess | None] = [None] * n
+        self.restarts = [0] * n
+        self._stop = threading.Event()
+        self._lock = threading.Lock()
+        self._sup: threading.Thread | None = None
+
+    def _spawn(self, i: int) -> HolaProcess:
+        cpus = self.cpu_plan[i] if self.cpu_plan else None
+        p = HolaProcess(args=self.args, env={**self.env, "HOSTNAME": f"replica-{i}"}, port=self.ports[i],
+                        threads=len(cpus) if cpus else self.threads,
+                        cpu_list=format_cpu_list(cpus) if cpus else None, log_level=self.log_level)
+        return p.start()
+
+    def start(self, timeout: float = 30.0) -> "ReplicaSet":
+        for i in range(self.n):
+            self.procs[i] = self._spawn(i)
+        for i in range(self.n):
+            if not wait_http("127.0.0.1", self.ports[i], timeout=timeout):
+                raise RuntimeError(f"replica {i} not ready")
+        if self.supervise:
+            self._sup = threading.Thread(target=self._supervise, daemon=True)
+            self._sup.start()
+        return self
+
+    def _supervise(self) -> None:
+        while not self._stop.wait(0.1):
+            for i, p in enumerate(self.procs):
+                if p is None or p.proc is None or p.proc.poll() is None:
+                    continue
+                with self._lock:
+                    if self._stop.is_set():
+                        return
+                    try:
+                        self.procs[i] = self._spawn(i)
+                        self.restarts[i] += 1
+                    except Exception:
+                        time.sleep(0.2)
+
+    def kill(self, i: int, sig: int = signal.SIGKILL) -> None:
+        p = self.procs[i]
+        if p and p.proc and p.proc.poll() is None:
+            p.proc.send_signal(sig)
+            p.proc.wait()
+
+    @property
+    def targets(self) -> list[tuple[str, int]]:
+        return [("127.0.0.1", p) for p in self.ports]
+
+    def stop(self) -> None:
+        self._stop.set()
+        if self._sup:
+            self._sup.join(timeout=5)
+        with self._lock:
+            for p in self.procs:
+                if p:
+                    p.stop()
+
+    def __enter__(self) -> "ReplicaSet":
+        return self.start()
+
+    def __exit__(self, *exc) -> None:
+        self.stop()
+
+
+class RRProxy:
+    """`hola_rrproxy`: L4 round-robin over healthy backends (health = GET /api/health)."""
+
+    def __init__(self, backends: list[tuple[str, int]], port: int = 0, threads: int = 1,
+                 cpu_list: str | None = None, health_ms: int = 200):
+        self._tmp = tempfile.TemporaryDirectory(prefix="rrproxy-")
+        self.port_file = os.path.join(self._tmp.name, "port")
+        cmd = [str(binary("hola_rrproxy")), "--host", "127.0.0.1", "--port", str(port), "--threads", str(threads),
+               "--backends", ",".join(f"{h}:{p}" for h, p in backends), "--health-ms", str(health_ms),
+               "--port-file", self.port_file]
+        if cpu_list:
+            cmd += ["--cpu-list", cpu_list]
+        self.cmd = cmd
+        self.proc: subprocess.Popen | None = None
+        self.port = port
+        self.log_path = os.path.join(self._tmp.name, "stderr.log")
+
+    def start(self, timeout: float = 10.0) -> "RRProxy":
+        self._log = open(self.log_path, "wb")
+        self.proc = subprocess.Popen(self.cmd, stdout=subprocess.DEVNULL, stderr=self._log)
+        deadline = time.monotonic() + timeout
+        while time.monotonic() < deadline:
+            if self.proc.poll() is not None:
+                raise RuntimeError(f"rrproxy exited: {self.log()}")
+            if os.path.exists(self.port_file):
+                self.port = int(Path(self.port_file).read_text())
+                return self
+            time.sleep(0.01)
+        raise RuntimeError("rrproxy did not start")
+
+    def log(self) -> str:
+        try:
+            return Path(self.log_path).read_text(errors="replace")
+        except OSError:
+            return ""
+
+    def stop(self) -> None:
+        if self.proc and self.proc.poll() is None:
+            self.proc.send_signal(signal.SIGTERM)
+            try:
+                self.proc.wait(timeout=10)
+            except subprocess.TimeoutExpired:
+                self.proc.kill()
+        try:
+            self._log.close()
+        except Exception:
+            pass
+
+    def __enter__(self) -> "RRProxy":
+        return self.start()
+
+    def __exit__(self, *exc) -> None:
+        self.stop()
+        self._tmp.cleanup()

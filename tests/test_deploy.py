@@ -1,0 +1,65 @@
+"""Deploy-descriptor parity with the reference's fabric8/docker configuration
+(pom.xml:65-94, 242-280; Dockerfile:1-10). Structural checks only: there is no cluster or
+docker daemon here to apply/build them."""
+from pathlib import Path
+
+import yaml
+
+ROOT = Path(__file__).resolve().parent.parent
+OS = ROOT / "deploy" / "openshift"
+
+
+def items():
+    doc = yaml.safe_load((OS / "hola.yaml").read_text())
+    return {i["kind"]: i for i in doc["items"]}
+
+
+def test_service_matches_fabric8_properties():
+    svc = items()["Service"]
+    assert svc["metadata"]["name"] == "hola"                       # fabric8.service.name
+    assert svc["spec"]["type"] == "LoadBalancer"                   # fabric8.service.type
+    (port,) = svc["spec"]["ports"]
+    assert port["port"] == 8080 and port["targetPort"] == 8080     # service.port / containerPort
+    labels = svc["metadata"]["labels"]
+    assert labels["group"] == "msa" and labels["hystrix.enabled"] == "true"  # Turbine discovery
+
+
+def test_deployment_env_ports_probe():
+    dep = items()["Deployment"]
+    tpl = dep["spec"]["template"]
+    assert set(dep["spec"]["selector"]["matchLabels"].items()) <= set(tpl["metadata"]["labels"].items())
+    svc_sel = items()["Service"]["spec"]["selector"]
+    assert set(svc_sel.items()) <= set(tpl["metadata"]["labels"].items())
+    (c,) = tpl["spec"]["containers"]
+    env = {e["name"]: e.get("value") for e in c["env"]}
+    assert env["AB_OFF"] == "true" and env["JAVA_OPTIONS"] == "-Xmx512m"
+    assert env["ZIPKIN_SERVER_URL"] == "http://zipkin-query:9411"
+    ports = {p["name"]: p["containerPort"] for p in c["ports"]}
+    assert ports == {"http": 8080, "jolokia": 8778}
+    rp = c["readinessProbe"]
+    assert rp["httpGet"] == {"path": "/api/health", "port": 8080}
+    assert rp["initialDelaySeconds"] == 5 and rp["timeoutSeconds"] == 30
+    assert "livenessProbe" not in c  # the reference declares none
+
+
+def test_configmap_payload_matches_translation_properties(native):
+    cm = yaml.safe_load((OS / "translation-configmap.yaml").read_text())
+    payload = cm["data"]["translation.properties"].encode()
+    parsed = native.parse_properties(payload)["map"]
+    from_file = native.parse_properties((ROOT / "translation.properties").read_bytes())["map"]
+    assert parsed == from_file
+    patch = yaml.safe_load((OS / "translation-patch.yaml").read_text())
+    c = patch["spec"]["template"]["spec"]["containers"][0]
+    opts = next(e["value"] for e in c["env"] if e["name"] == "JAVA_OPTIONS")
+    conf = native.parse_java_options(opts)["conf"]
+    mount = c["volumeMounts"][0]["mountPath"]
+    assert conf == f"{mount}/translation.properties"
+
+
+def test_dockerfile_contract():
+    df = (ROOT / "deploy" / "Dockerfile").read_text()
+    assert "EXPOSE 8080" in df
+    for k in ("AB_OFF=true", "JAVA_OPTIONS=-Xmx512m", "ZIPKIN_SERVER_URL=http://zipkin-query:9411"):
+        assert k in df
+    for path in ("CMakeLists.txt", "src", "assets", "conf/config.properties", "translation.properties"):
+        assert (ROOT / path).exists()

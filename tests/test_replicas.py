@@ -1,0 +1,107 @@
+"""Replica scale-out without a cluster: N pinned replicas behind the
+native round-robin proxy, greeting rotation, failure of a replica under load, supervisor
+restarts, graceful shutdown."""
+import json
+import signal
+import subprocess
+import threading
+import time
+
+import pytest
+
+from hola_amd.parallel.replicas import ReplicaSet, RRProxy
+from hola_amd.utils.net import http_get
+
+
+def greeting_via(port):
+    st, _, body = http_get("127.0.0.1", port, "/api/hola")
+    assert st == 200
+    return body.decode()
+
+
+def test_proxy_round_robin_rotation():
+    with ReplicaSet(3, threads_per_replica=1, supervise=False) as rs, RRProxy(rs.targets) as px:
+        seen = [greeting_via(px.port) for _ in range(6)]  # one connection per request
+    assert sorted(set(seen)) == ["Hola de replica-0", "Hola de replica-1", "Hola de replica-2"]
+    assert seen[:3] != seen[3:6] or len(set(seen[:3])) == 3
+
+
+def test_proxy_skips_dead_replica_and_recovers():
+    rs = ReplicaSet(2, threads_per_replica=1, supervise=False).start()
+    try:
+        with RRProxy(rs.targets, health_ms=50) as px:
+            rs.kill(1)
+            time.sleep(0.3)  # health checker marks it DOWN
+            seen = {greeting_via(px.port) for _ in range(8)}
+            assert seen == {"Hola de replica-0"}
+            assert "is DOWN" in px.log()
+            rs.procs[1] = rs._spawn(1)  # platform restarts the pod
+            time.sleep(0.3)
+            seen = {greeting_via(px.port) for _ in range(8)}
+            assert seen == {"Hola de replica-0", "Hola de replica-1"}
+    finally:
+        rs.stop()
+
+
+def test_supervisor_restarts_crashed_replica():
+    with ReplicaSet(2, threads_per_replica=1, supervise=True) as rs:
+        old = rs.procs[0].proc.pid
+        rs.kill(0)
+        deadline = time.time() + 10
+        while time.time() < deadline and (rs.restarts[0] == 0):
+            time.sleep(0.05)
+        assert rs.restarts[0] == 1 and rs.procs[0].proc.pid != old
+        assert greeting_via(rs.ports[0]) == "Hola de replica-0"
+
+
+def test_kill_replica_under_load_client_rr():
+    """Chaos: SIGKILL one replica mid-run; the other keeps answering, the loadgen reconnects."""
+    from hola_amd.parallel.loadgen import ControlledLoadgen
+
+    with ReplicaSet(2, threads_per_replica=1, supervise=True) as rs:
+        lg = ControlledLoadgen(rs.targets, connections=8, threads=1)
+        try:
+            lg.run(50)
+            rs.kill(1)
+            r = lg.run(50)  # reconnects to the restarted replica
+            assert r["requests"] >= 8 * 50 - 8
+        finally:
+            lg.close()
+
+
+def test_graceful_shutdown_drains_inflight(hola):
+    """SIGTERM while a chaining request waits on a slow aloha: the response still completes."""
+    from hola_amd.testing.fakes import FakeAloha
+
+    with FakeAloha(mode="slow", delay_s=0.3) as aloha:
+        s = hola(args=["--aloha-url", aloha.url, "--feign-log", "none"])
+        out = {}
+
+        def req():
+            out["r"] = s.get("/api/hola-chaining", timeout=5)
+
+        t = threading.Thread(target=req)
+        t.start()
+        time.sleep(0.1)
+        s.proc.send_signal(signal.SIGTERM)
+        t.join()
+        assert out["r"][0] == 200 and json.loads(out["r"][2])[1] == "Aloha mai aloha-1"
+        assert s.proc.wait(timeout=10) == 0
+        assert "shutdown complete" in s.log()
+
+
+def test_scaling_harness_smoke():
+    from hola_amd.parallel import scaling
+
+    rows = []
+    import io
+    import contextlib
+
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        scaling.main(["--replicas", "1,2", "--duration", "0.5", "--warmup", "0.2", "--budget", "6",
+                      "--connections-per-replica", "8"])
+    lines = [json.loads(l) for l in buf.getvalue().splitlines() if l.startswith("{")]
+    assert [r["replicas"] for r in lines] == [1, 2]
+    assert all(r["rps"] > 0 and r["errors"] == 0 for r in lines)
+    assert lines[1]["connections"] == 16
