@@ -29,7 +29,8 @@ sys.path.insert(0, str(Path(__file__).resolve().parent))
 from hola_amd.native import ensure_built  # noqa: E402
 from hola_amd.parallel.loadgen import ControlledLoadgen, decode_hist, merge_hists, percentile  # noqa: E402
 from hola_amd.server import HolaProcess  # noqa: E402
-from hola_amd.utils.cpu import cgroup_cpu_quota, cpu_budget, format_cpu_list, plan_cores  # noqa: E402
+from hola_amd.utils.cpu import (  # noqa: E402
+    cgroup_cpu_quota, cpu_budget, format_cpu_list, plan_node, split_server_loadgen)
 
 METRIC = "HTTP req/sec + p50/p99 latency, GET /api/hola at 1/2/4/8 replicas"
 BASELINE_VALUE = None  # the reference publishes no numbers
@@ -47,6 +48,10 @@ def parse_args():
     ap.add_argument("--base-port", type=int, default=int(os.environ.get("HOLA_BENCH_PORT", "18400")))
     ap.add_argument("--path", default="/api/hola")
     ap.add_argument("--no-tracing", action="store_true", help="run replicas with tracing off")
+    ap.add_argument("--no-avoid-busy", action="store_true",
+                    help="take cores in id order instead of the quietest L3 domains first")
+    ap.add_argument("--busy-poll-us", type=int, default=0,
+                    help="spin this long in epoll before sleeping (server and load generator)")
     return ap.parse_args()
 
 
@@ -67,17 +72,27 @@ def main() -> int:
 
     ensure_built("release")  # file-locked: concurrent ranks build once
 
-    # ---- core plan: server + loadgen on disjoint physical cores of this rank's share ----
-    cores = plan_cores(local_rank, local_world, a.cores or None)
+    # ---- core plan: disjoint physical cores per rank, quietest L3 domains first (computed
+    # once on rank 0 and broadcast, since load measurements differ between processes);
+    # within a rank, server worker t and loadgen thread t share an L3 domain. ----
+    plan = [plan_node(local_world, a.cores or None, avoid_busy=not a.no_avoid_busy)] if rank == 0 else [None]
+    if dist:
+        dist.broadcast_object_list(plan, src=0)
+    cores = plan[0][local_rank]
     n = len(cores)
     s_threads = a.server_threads or max(1, n // 2)
     s_threads = min(s_threads, max(1, n - 1)) if n > 1 else 1
-    server_cpus, load_cpus = cores[:s_threads], (cores[s_threads:] or cores)
+    if n > 1:
+        server_cpus, load_cpus = split_server_loadgen(cores, s_threads)
+    else:
+        server_cpus, load_cpus = cores, cores
     port = a.base_port + local_rank
     targets = [("127.0.0.1", a.base_port + i) for i in range(local_world)]
 
     env = {"HOSTNAME": f"replica-{rank}"}
     args = ["--no-tracing"] if a.no_tracing else []
+    if a.busy_poll_us:
+        args += ["--busy-poll-us", str(a.busy_poll_us)]
     server = HolaProcess(args=args, env=env, port=port, threads=s_threads, cpu_list=format_cpu_list(server_cpus),
                          log_level="warn")
     server.start()
@@ -86,7 +101,7 @@ def main() -> int:
         if dist:
             dist.barrier()  # every replica is listening before any connection is made
         loadgen = ControlledLoadgen(targets, a.connections, len(load_cpus), cpu_list=format_cpu_list(load_cpus),
-                                    path=a.path, target_offset=local_rank)
+                                    path=a.path, target_offset=local_rank, busy_poll_us=a.busy_poll_us)
         for _ in range(a.warmup):
             loadgen.run(a.reqs_per_conn)
         loadgen.reset()
@@ -95,6 +110,7 @@ def main() -> int:
         if dist:
             dist.barrier()
         cuda()
+        cpu0 = (_proc_cpu_s(server.proc.pid), _proc_cpu_s(loadgen.proc.pid))
         t0 = time.perf_counter()
         reqs = errs = 0
         for _ in range(a.steps):
@@ -105,11 +121,13 @@ def main() -> int:
             dist.barrier()
         cuda()
         elapsed = time.perf_counter() - t0
+        cpu1 = (_proc_cpu_s(server.proc.pid), _proc_cpu_s(loadgen.proc.pid))
         st = loadgen.stats()
 
         local = {"elapsed": elapsed, "requests": reqs, "errors": errs, "hist": st.get("hist", ""),
                  "non2xx": st.get("non2xx", 0), "server_cpus": format_cpu_list(server_cpus),
-                 "load_cpus": format_cpu_list(load_cpus)}
+                 "load_cpus": format_cpu_list(load_cpus),
+                 "server_cpu_s": cpu1[0] - cpu0[0], "loadgen_cpu_s": cpu1[1] - cpu0[1]}
         if dist:
             gathered = [None] * world
             dist.all_gather_object(gathered, local)
@@ -142,6 +160,9 @@ def main() -> int:
             "p99_ms": round(percentile(hist, 99) / 1e6, 4),
             "p999_ms": round(percentile(hist, 99.9) / 1e6, 4),
             "requests": total,
+            # host CPU time per request (user+sys, all threads) over the timed region
+            "server_cpu_us_per_req": round(1e6 * sum(g["server_cpu_s"] for g in gathered) / max(1, total), 3),
+            "loadgen_cpu_us_per_req": round(1e6 * sum(g["loadgen_cpu_s"] for g in gathered) / max(1, total), 3),
             "errors": sum(g["errors"] for g in gathered),
             "non2xx": sum(g["non2xx"] for g in gathered),
             "config": {
@@ -155,6 +176,7 @@ def main() -> int:
                 "lb": "client-side round-robin over replica ports",
                 "server_threads_per_replica": s_threads,
                 "loadgen_threads_per_replica": len(load_cpus),
+                "busy_poll_us": a.busy_poll_us,
                 "cpu_map": {f"rank{i}": {"server": g["server_cpus"], "loadgen": g["load_cpus"]}
                             for i, g in enumerate(gathered)},
                 "cpu_budget": cpu_budget(),
@@ -166,6 +188,16 @@ def main() -> int:
         dist.barrier()
         dist.destroy_process_group()
     return 0
+
+
+def _proc_cpu_s(pid: int) -> float:
+    """user+system CPU seconds of a process (all threads) from /proc/<pid>/stat."""
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            fields = f.read().rsplit(")", 1)[1].split()
+        return (int(fields[11]) + int(fields[12])) / os.sysconf("SC_CLK_TCK")
+    except (OSError, IndexError, ValueError):
+        return 0.0
 
 
 def _cuda_sync_fn(local_rank: int):

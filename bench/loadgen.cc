@@ -60,6 +60,7 @@ struct Options {
   bool control = false;
   int target_offset = 0;
   std::vector<std::string> extra_headers;
+  int busy_poll_us = 0;
 };
 
 struct Conn {
@@ -187,7 +188,14 @@ void thread_main(ThreadState* ts, const Options* o) {
 
   epoll_event evs[256];
   while (!g_stop.load(std::memory_order_relaxed)) {
-    int n = epoll_wait(ts->epfd, evs, 256, control ? -1 : 5);
+    int n = 0;
+    if (o->busy_poll_us > 0) {
+      int64_t until = mono_ns() + int64_t(o->busy_poll_us) * 1000;
+      do {
+        n = epoll_wait(ts->epfd, evs, 256, 0);
+      } while (n == 0 && mono_ns() < until);
+    }
+    if (n == 0) n = epoll_wait(ts->epfd, evs, 256, control ? -1 : 5);
     int64_t now = mono_ns();
     if (!control) {
       if (!ts->recording && now >= warm_end) {
@@ -363,6 +371,7 @@ int main(int argc, char** argv) {
     else if (a == "--control") o.control = true;
     else if (a == "--target-offset") o.target_offset = atoi(val().c_str());
     else if (a == "--header" || a == "-H") o.extra_headers.push_back(val());
+    else if (a == "--busy-poll-us") o.busy_poll_us = atoi(val().c_str());
     else {
       fprintf(stderr,
               "usage: hola_loadgen --targets h:p[,h:p..] -c CONNS -t THREADS [--cpu-list L] [--path P]\n"

@@ -54,7 +54,7 @@ class ControlledLoadgen:
 
     def __init__(self, targets: list[tuple[str, int]], connections: int, threads: int,
                  cpu_list: str | None = None, path: str = "/api/hola", target_offset: int = 0,
-                 headers: list[str] | None = None):
+                 headers: list[str] | None = None, busy_poll_us: int = 0):
         cmd = [str(binary("hola_loadgen")), "--targets", ",".join(f"{h}:{p}" for h, p in targets),
                "-c", str(connections), "-t", str(threads), "--path", path, "--control",
                "--target-offset", str(target_offset)]
@@ -62,6 +62,8 @@ class ControlledLoadgen:
             cmd += ["--cpu-list", cpu_list]
         for h in headers or []:
             cmd += ["-H", h]
+        if busy_poll_us:
+            cmd += ["--busy-poll-us", str(busy_poll_us)]
         self.proc = subprocess.Popen(cmd, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, bufsize=1)
         ready = self._read()
         if not ready.get("ready"):

@@ -99,6 +99,90 @@ def physical_cores(cpus: list[int] | None = None) -> list[int]:
     return [c for _, c in picked]
 
 
+def l3_domain(cpu: int) -> int:
+    """Id of the L3 (CCD on EPYC) a CPU belongs to; 0 when unknown."""
+    v = _read(f"/sys/devices/system/cpu/cpu{cpu}/cache/index3/id")
+    try:
+        return int(v) if v is not None else 0
+    except ValueError:
+        return 0
+
+
+def siblings(cpu: int) -> list[int]:
+    v = _read(f"/sys/devices/system/cpu/cpu{cpu}/topology/thread_siblings_list")
+    return parse_cpu_list(v) if v else [cpu]
+
+
+def cpu_busy(interval: float = 0.3) -> dict[int, float]:
+    """Host-wide per-CPU busy fraction over `interval` seconds (from /proc/stat)."""
+    import time
+
+    def snap():
+        d = {}
+        with open("/proc/stat") as f:
+            for line in f:
+                if line.startswith("cpu") and line[3].isdigit():
+                    parts = line.split()
+                    v = list(map(int, parts[1:]))
+                    d[int(parts[0][3:])] = (sum(v), v[3] + v[4])
+        return d
+
+    a = snap()
+    time.sleep(interval)
+    b = snap()
+    return {c: 1.0 - (b[c][1] - a[c][1]) / max(1, b[c][0] - a[c][0]) for c in a if c in b}
+
+
+def plan_node(local_world: int, per_rank: int | None = None, avoid_busy: bool = True) -> list[list[int]]:
+    """Disjoint core lists for every co-located rank, L3-domain (CCD) aware.
+
+    Physical cores are grouped by L3 domain; with ``avoid_busy`` the quietest domains (by
+    host-wide /proc/stat load, which on a shared box includes other tenants) are used first.
+    Each rank gets whole domains where possible so its server and load generator share an L3.
+    Compute once (rank 0) and broadcast: measurements differ between processes.
+    """
+    budget = cpu_budget()
+    if per_rank is None:
+        per_rank = max(1, budget // max(1, local_world))
+    phys = physical_cores()
+    if len(phys) < per_rank * local_world:
+        phys = allowed_cpus()
+        per_rank = max(1, min(per_rank, len(phys) // max(1, local_world)))
+    busy = cpu_busy() if avoid_busy else {}
+    load = {c: sum(busy.get(x, 0.0) for x in siblings(c)) for c in phys}
+    domains: dict[int, list[int]] = {}
+    for c in phys:
+        domains.setdefault(l3_domain(c), []).append(c)
+    # quietest domains first; inside a domain, quietest cores first (stable by id)
+    order = sorted(domains, key=lambda d: (round(sum(load[c] for c in domains[d]) / len(domains[d]), 1), d))
+    pool = []
+    for d in order:
+        pool.extend(sorted(domains[d], key=lambda c: (round(load[c], 1), c)))
+    return [pool[r * per_rank:(r + 1) * per_rank] for r in range(local_world)]
+
+
+def split_server_loadgen(cores: list[int], server_threads: int) -> tuple[list[int], list[int]]:
+    """Splits a rank's cores so that server worker t and load-generator thread t sit in the
+    same L3 domain (connections are dealt round-robin on both sides, so connection i joins
+    loadgen thread i%L to server worker i%S: with S == L each pair talks through one L3)."""
+    by_dom: dict[int, list[int]] = {}
+    for c in cores:
+        by_dom.setdefault(l3_domain(c), []).append(c)
+    server, load = [], []
+    for dom_cores in by_dom.values():
+        for i, c in enumerate(dom_cores):
+            (server if i % 2 == 0 else load).append(c)
+    # honour the requested server share
+    while len(server) > server_threads and len(server) > 1:
+        load.append(server.pop())
+    while len(server) < server_threads and len(load) > 1:
+        server.append(load.pop())
+    # interleave so index t of each list is in the same domain whenever possible
+    server.sort(key=lambda c: (l3_domain(c), c))
+    load.sort(key=lambda c: (l3_domain(c), c))
+    return server, load
+
+
 def plan_cores(rank: int, local_world: int, per_rank: int | None = None) -> list[int]:
     """Disjoint CPU set for `rank` out of `local_world` co-located ranks.
 

@@ -113,7 +113,14 @@ void EventLoop::run() {
   epoll_event evs[kMaxEvents];
   while (!stop_.load(std::memory_order_relaxed)) {
     if (tick_) tick_();
-    int n = epoll_wait(epfd_, evs, kMaxEvents, next_timeout_ms());
+    int n = 0;
+    if (busy_poll_ns_ > 0) {
+      int64_t until = mono_ns() + busy_poll_ns_;
+      do {
+        n = epoll_wait(epfd_, evs, kMaxEvents, 0);
+      } while (n == 0 && mono_ns() < until && !stop_.load(std::memory_order_relaxed));
+    }
+    if (n == 0) n = epoll_wait(epfd_, evs, kMaxEvents, next_timeout_ms());
     if (n < 0 && errno != EINTR) {
       perror("epoll_wait");
       break;

@@ -53,6 +53,9 @@ class EventLoop {
   void set_tick(std::function<void()> fn) { tick_ = std::move(fn); }
   // Optional callback when the loop exits run().
   void set_on_exit(std::function<void()> fn) { on_exit_ = std::move(fn); }
+  // Before blocking in epoll_wait, poll without sleeping for up to `us` microseconds
+  // (trades idle CPU for fewer sleep/wake-up cycles under closed-loop load). 0 = off.
+  void set_busy_poll_us(int us) { busy_poll_ns_ = int64_t(us) * 1000; }
 
  private:
   struct WakeHandler : Handler {
@@ -82,6 +85,7 @@ class EventLoop {
   std::vector<std::function<void()>> posted_;
   std::vector<Handler*> retired_;
   std::function<void()> tick_, on_exit_;
+  int64_t busy_poll_ns_ = 0;
 };
 
 }  // namespace hola

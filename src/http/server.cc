@@ -271,6 +271,7 @@ Worker::Worker(Server* s, int index) : server_(s), index_(index) {
   memset(date_, ' ', sizeof date_);
   tick();
   loop_.set_tick([this] { tick(); });
+  loop_.set_busy_poll_us(s->options().busy_poll_us);
 }
 
 RequestHandler& Worker::handler() { return server_->handler(); }

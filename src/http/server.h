@@ -125,6 +125,7 @@ struct ServerOptions {
   bool reuseport_accept = false;  // per-worker SO_REUSEPORT listeners instead of round-robin
   int backlog = 4096;
   size_t read_chunk = 64 * 1024;
+  int busy_poll_us = 0;  // see EventLoop::set_busy_poll_us
 };
 
 class Worker {

@@ -54,6 +54,7 @@ void usage() {
           "  --config-poll-ms N       config re-check interval (default 1000)\n"
           "  --drain-ms N             graceful shutdown drain budget (default 5000)\n"
           "  --port-file PATH         write the bound port here once listening\n"
+          "  --busy-poll-us N         spin up to N us in epoll before sleeping (default 0)\n"
           "  --log-level L            debug|info|warn|error|off (default info)\n"
           "  --no-metrics             disable the /metrics endpoint\n");
 }
@@ -117,6 +118,7 @@ int main(int argc, char** argv) {
     else if (a == "--config-poll-ms") mo.poll_ms = atoi(val("--config-poll-ms").c_str());
     else if (a == "--drain-ms") drain_ms = atoi(val("--drain-ms").c_str());
     else if (a == "--port-file") port_file = val("--port-file");
+    else if (a == "--busy-poll-us") so.busy_poll_us = atoi(val("--busy-poll-us").c_str());
     else if (a == "--no-metrics") ao.enable_metrics_endpoint = false;
     else if (a == "--log-level") {
       LogLevel l;

@@ -4,6 +4,7 @@
 #include <sys/random.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstring>
 
@@ -61,6 +62,7 @@ Tracer::Tracer(TracerOptions o, int num_workers) : o_(std::move(o)) {
       chost_ = u.host;
       cport_ = u.port;
       cpath_ = u.base_path + (o_.v2 ? "api/v2/spans" : "api/v1/spans");
+      collecting_ = true;
     } else {
       LOG_WARN("ZIPKIN_SERVER_URL '%s' is not an http:// URL; spans will be dropped", o_.collector_url.c_str());
     }
@@ -102,6 +104,14 @@ ServerSpan Tracer::begin_server(int worker, const http::Request& r) {
     s.ctx.trace_id = id;
     s.ctx.span_id = id;
     s.ctx.sampled = true;
+  }
+  if (!collecting_) {
+    // No collector (ZIPKIN_SERVER_URL unset): ids still flow downstream via B3, but the span
+    // is counted and dropped here rather than after a copy through the ring — the observable
+    // result of Brave posting to an unreachable collector (ZipkinResource.java:37-38).
+    auto& u = ws_[size_t(worker)]->unreported;
+    u.store(u.load(std::memory_order_relaxed) + 1, std::memory_order_relaxed);
+    return s;
   }
   s.record = true;
   s.start_us = wall_us();
@@ -160,6 +170,11 @@ SpanContext Tracer::new_child(int worker, const SpanContext& parent) {
 void Tracer::record_client(int worker, const SpanContext& ctx, int64_t start_us, int64_t end_us,
                            std::string_view url, int status, std::string_view error) {
   if (!ctx.sampled) return;
+  if (!collecting_) {
+    auto& u = ws_[size_t(worker)]->unreported;
+    u.store(u.load(std::memory_order_relaxed) + 1, std::memory_order_relaxed);
+    return;
+  }
   SpanRecord r;
   r.trace_hi = ctx.trace_hi;
   r.trace_id = ctx.trace_id;
@@ -283,18 +298,21 @@ bool Tracer::post(const std::string& body) {
   return ok && resp.status >= 200 && resp.status < 300;
 }
 
-void Tracer::flush() {
-  std::lock_guard<std::mutex> g(flush_mu_);
-  std::vector<SpanRecord> batch;
-  for (auto& w : ws_) w->ring->drain(&batch);
-  if (batch.empty()) return;
+void Tracer::drain_rings() {
+  for (auto& w : ws_) w->ring->drain(&pending_);
+}
+
+void Tracer::post_pending() {
+  if (pending_.empty()) return;
   if (chost_.empty()) {
-    dropped_no_collector_.fetch_add(batch.size());
+    dropped_no_collector_.fetch_add(pending_.size());
+    pending_.clear();
     return;
   }
   constexpr size_t kChunk = 500;
-  for (size_t i = 0; i < batch.size(); i += kChunk) {
-    std::vector<SpanRecord> part(batch.begin() + long(i), batch.begin() + long(std::min(batch.size(), i + kChunk)));
+  for (size_t i = 0; i < pending_.size(); i += kChunk) {
+    std::vector<SpanRecord> part(pending_.begin() + long(i),
+                                 pending_.begin() + long(std::min(pending_.size(), i + kChunk)));
     std::string body = o_.v2 ? encode_v2(part) : encode_v1(part);
     if (post(body)) {
       reported_.fetch_add(part.size());
@@ -303,14 +321,32 @@ void Tracer::flush() {
       dropped_no_collector_.fetch_add(part.size());
     }
   }
+  pending_.clear();
+}
+
+void Tracer::flush() {
+  std::lock_guard<std::mutex> g(flush_mu_);
+  drain_rings();
+  post_pending();
 }
 
 void Tracer::run() {
+  // Rings are drained every drain_interval_ms (so they stay small and cache-resident);
+  // batches are POSTed every flush_interval_ms, or earlier when large.
+  int64_t last_post = mono_ms();
   std::unique_lock<std::mutex> g(mu_);
   while (!stop_) {
-    cv_.wait_for(g, std::chrono::milliseconds(o_.flush_interval_ms), [this] { return stop_; });
+    cv_.wait_for(g, std::chrono::milliseconds(o_.drain_interval_ms), [this] { return stop_; });
     g.unlock();
-    flush();
+    {
+      std::lock_guard<std::mutex> f(flush_mu_);
+      drain_rings();
+      int64_t now = mono_ms();
+      if (now - last_post >= o_.flush_interval_ms || pending_.size() >= 5000) {
+        post_pending();
+        last_post = now;
+      }
+    }
     g.lock();
   }
 }
@@ -346,6 +382,7 @@ TracerStats Tracer::stats() const {
   }
   s.reported = reported_.load();
   s.dropped_no_collector = dropped_no_collector_.load();
+  for (auto& w : ws_) s.dropped_no_collector += w->unreported.load(std::memory_order_relaxed);
   s.post_failures = post_failures_.load();
   return s;
 }
