@@ -151,6 +151,22 @@ std::string chunk(const std::string& data, bool chunked) {
 }
 }  // namespace
 
+struct HystrixStream::Ticker : std::enable_shared_from_this<HystrixStream::Ticker> {
+  std::shared_ptr<Sub> sub;
+  HystrixStream* stream = nullptr;
+  http::Connection* conn = nullptr;
+  EventLoop* loop = nullptr;
+  void fire() {
+    if (!sub->alive || conn->closed()) {
+      conn->release();  // balances the hold() taken at subscribe time
+      return;
+    }
+    conn->send(chunk(stream->render_events(), sub->chunked));
+    auto self = shared_from_this();
+    loop->add_timer(sub->delay_ms, [self] { self->fire(); });
+  }
+};
+
 void HystrixStream::subscribe(http::Connection& c, const http::Request& r) {
   if (subscribers_.fetch_add(1) >= max_connections_) {
     subscribers_.fetch_sub(1);
@@ -181,24 +197,14 @@ void HystrixStream::subscribe(http::Connection& c, const http::Request& r) {
     sub->alive = false;
     self->subscribers_.fetch_sub(1);
   });
-  http::Connection* conn = &c;
-  EventLoop& loop = c.worker().loop();
-  // Emit immediately, then every delay_ms until the subscriber goes away.
-  auto tick = std::make_shared<std::function<void()>>();
-  *tick = [sub, self, conn, &loop, tick] {
-    if (!sub->alive || conn->closed()) {
-      *tick = nullptr;  // break the self-reference
-      conn->release();
-      return;
-    }
-    conn->send(chunk(self->render_events(), sub->chunked));
-    loop.add_timer(sub->delay_ms, [tick] {
-      if (*tick) (*tick)();
-    });
-  };
-  loop.add_timer(0, [tick] {
-    if (*tick) (*tick)();
-  });
+  auto t = std::make_shared<Ticker>();
+  t->sub = sub;
+  t->stream = this;
+  t->conn = &c;
+  t->loop = &c.worker().loop();
+  // Emit immediately, then every delay_ms until the subscriber goes away. The pending timer
+  // owns the ticker; when it is not re-armed the ticker is freed.
+  t->loop->add_timer(0, [t] { t->fire(); });
 }
 
 }  // namespace hola::metrics

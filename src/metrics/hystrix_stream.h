@@ -29,6 +29,7 @@ class HystrixStream {
   static std::string threadpool_json(const resilience::CommandSnapshot& s);
 
  private:
+  struct Ticker;
   int max_connections_;
   int default_delay_ms_;
   std::vector<resilience::Command*> commands_;

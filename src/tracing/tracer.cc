@@ -1,6 +1,8 @@
 #include "tracing/tracer.h"
 
 #include <arpa/inet.h>
+#include <poll.h>
+#include <sys/eventfd.h>
 #include <sys/random.h>
 #include <unistd.h>
 
@@ -44,6 +46,7 @@ size_t SpanRing::drain(std::vector<SpanRecord>* out) {
 // ---------------------------------------------------------------- Tracer
 
 Tracer::Tracer(TracerOptions o, int num_workers) : o_(std::move(o)) {
+  stopfd_ = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
   for (int i = 0; i < num_workers + 1; ++i) {  // +1: slot for non-worker producers (tests)
     auto w = std::make_unique<WorkerState>();
     uint64_t seed[2] = {0, 0};
@@ -69,7 +72,10 @@ Tracer::Tracer(TracerOptions o, int num_workers) : o_(std::move(o)) {
   }
 }
 
-Tracer::~Tracer() { stop(); }
+Tracer::~Tracer() {
+  stop();
+  if (stopfd_ >= 0) ::close(stopfd_);
+}
 
 uint64_t Tracer::next_id(int worker) {
   WorkerState& w = *ws_[size_t(worker)];
@@ -192,7 +198,7 @@ void Tracer::record_client(int worker, const SpanContext& ctx, int64_t start_us,
   r.url_len = uint16_t(url.size() < kMaxUrl ? url.size() : kMaxUrl);
   memcpy(r.url, url.data(), r.url_len);
   r.error_len = uint16_t(error.size() < sizeof r.error ? error.size() : sizeof r.error);
-  memcpy(r.error, error.data(), r.error_len);
+  if (r.error_len) memcpy(r.error, error.data(), r.error_len);
   push(worker, r);
 }
 
@@ -332,45 +338,40 @@ void Tracer::flush() {
 
 void Tracer::run() {
   // Rings are drained every drain_interval_ms (so they stay small and cache-resident);
-  // batches are POSTed every flush_interval_ms, or earlier when large.
+  // batches are POSTed every flush_interval_ms, or earlier when large. The wait is a poll()
+  // on an eventfd rather than a timed condition variable (gcc 11's TSan does not intercept
+  // pthread_cond_clockwait, which turns timed cv waits into false race reports).
   int64_t last_post = mono_ms();
-  std::unique_lock<std::mutex> g(mu_);
-  while (!stop_) {
-    cv_.wait_for(g, std::chrono::milliseconds(o_.drain_interval_ms), [this] { return stop_; });
-    g.unlock();
-    {
-      std::lock_guard<std::mutex> f(flush_mu_);
-      drain_rings();
-      int64_t now = mono_ms();
-      if (now - last_post >= o_.flush_interval_ms || pending_.size() >= 5000) {
-        post_pending();
-        last_post = now;
-      }
+  for (;;) {
+    pollfd p{stopfd_, POLLIN, 0};
+    ::poll(&p, 1, o_.drain_interval_ms);
+    if (stopping_.load(std::memory_order_acquire)) break;
+    std::lock_guard<std::mutex> f(flush_mu_);
+    drain_rings();
+    int64_t now = mono_ms();
+    if (now - last_post >= o_.flush_interval_ms || pending_.size() >= 5000) {
+      post_pending();
+      last_post = now;
     }
-    g.lock();
   }
 }
 
 void Tracer::start() {
-  if (!o_.enabled) return;
-  std::lock_guard<std::mutex> g(mu_);
-  if (running_) return;
+  if (!o_.enabled || running_) return;
   running_ = true;
   th_ = std::thread([this] { run(); });
 }
 
 void Tracer::stop() {
-  {
-    std::lock_guard<std::mutex> g(mu_);
-    if (!running_) return;
-    stop_ = true;
-  }
-  cv_.notify_all();
+  if (!running_) return;
+  stopping_.store(true, std::memory_order_release);
+  uint64_t one = 1;
+  ssize_t w = ::write(stopfd_, &one, sizeof one);
+  (void)w;
   if (th_.joinable()) th_.join();
   flush();
   if (cfd_ >= 0) ::close(cfd_);
   cfd_ = -1;
-  std::lock_guard<std::mutex> g(mu_);
   running_ = false;
 }
 

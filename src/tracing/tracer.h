@@ -8,7 +8,6 @@
 // unset or down, spans are dropped and counted — never blocking a worker.
 #pragma once
 #include <atomic>
-#include <condition_variable>
 #include <cstdint>
 #include <memory>
 #include <mutex>
@@ -124,9 +123,9 @@ class Tracer {
   };
   std::vector<std::unique_ptr<WorkerState>> ws_;
   std::thread th_;
-  std::mutex mu_;
-  std::condition_variable cv_;
-  bool stop_ = false, running_ = false;
+  int stopfd_ = -1;
+  std::atomic<bool> stopping_{false};
+  bool running_ = false;  // start()/stop() are called from the owning (main) thread
   std::mutex flush_mu_;
   std::atomic<uint64_t> reported_{0}, dropped_no_collector_{0}, post_failures_{0};
   bool collecting_ = false;            // a collector URL is configured
