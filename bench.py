@@ -48,6 +48,8 @@ def parse_args():
     ap.add_argument("--base-port", type=int, default=int(os.environ.get("HOLA_BENCH_PORT", "18400")))
     ap.add_argument("--path", default="/api/hola")
     ap.add_argument("--no-tracing", action="store_true", help="run replicas with tracing off")
+    ap.add_argument("--profile-dir", default="",
+                    help="run replicas with --profile and write their stage histograms here")
     ap.add_argument("--no-avoid-busy", action="store_true",
                     help="take cores in id order instead of the quietest L3 domains first")
     ap.add_argument("--busy-poll-us", type=int, default=0,
@@ -93,6 +95,10 @@ def main() -> int:
     args = ["--no-tracing"] if a.no_tracing else []
     if a.busy_poll_us:
         args += ["--busy-poll-us", str(a.busy_poll_us)]
+    if a.profile_dir:
+        os.makedirs(a.profile_dir, exist_ok=True)
+        args += ["--profile", "--profile-out", os.path.join(os.path.abspath(a.profile_dir),
+                                                            f"server_profile_rank{rank}.json")]
     server = HolaProcess(args=args, env=env, port=port, threads=s_threads, cpu_list=format_cpu_list(server_cpus),
                          log_level="warn")
     server.start()

@@ -32,13 +32,13 @@
 #include <thread>
 #include <vector>
 
-#include "bench/histogram.h"
+#include "core/histogram.h"
 #include "core/affinity.h"
 #include "core/clock.h"
 #include "core/net.h"
 
 using namespace hola;
-using hola::bench::Histogram;
+using hola::Histogram;
 
 namespace {
 

@@ -1,0 +1,110 @@
+"""Command line entry point: ``python -m hola_amd <command>``.
+
+  build [--preset release|debug|tsan|asan]   compile the native artefacts in-tree
+  serve [hola args...]                       run the service (same flags as the binary)
+  cluster --replicas N [--port P]            N pinned replicas + the round-robin proxy on P
+  scaling [...]                              replica scaling curve (hola_amd.parallel.scaling)
+  bench [...]                                the headline benchmark (bench.py)
+  info                                       host CPU topology / quota / plan for this node
+
+The local equivalents of the reference's `mvn wildfly-swarm:run` (Readme.md:13) and
+`mvn clean package docker:build fabric8:json fabric8:apply` (Readme.md:24) are
+`python -m hola_amd serve` and deploy/Dockerfile + deploy/openshift/*.yaml.
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import signal
+import subprocess
+import sys
+import time
+from pathlib import Path
+
+from hola_amd import native
+
+
+def _serve(argv: list[str]) -> int:
+    exe = native.binary("hola")
+    # Runs as a child (never exec from a process that might have touched a GPU).
+    p = subprocess.Popen([str(exe), *argv])
+    try:
+        return p.wait()
+    except KeyboardInterrupt:
+        p.send_signal(signal.SIGINT)
+        return p.wait()
+
+
+def _cluster(argv: list[str]) -> int:
+    from hola_amd.parallel.replicas import ReplicaSet, RRProxy
+    from hola_amd.utils.cpu import format_cpu_list, plan_node
+
+    ap = argparse.ArgumentParser(prog="python -m hola_amd cluster")
+    ap.add_argument("--replicas", type=int, default=2)
+    ap.add_argument("--port", type=int, default=8080)
+    ap.add_argument("--cores-per-replica", type=int, default=0)
+    ap.add_argument("--proxy-threads", type=int, default=2)
+    ap.add_argument("hola_args", nargs=argparse.REMAINDER)
+    a = ap.parse_args(argv)
+    plan = plan_node(a.replicas + 1, a.cores_per_replica or None)
+    with ReplicaSet(a.replicas, cpu_plan=plan[:a.replicas], args=a.hola_args, supervise=True) as rs:
+        with RRProxy(rs.targets, port=a.port, threads=a.proxy_threads,
+                     cpu_list=format_cpu_list(plan[-1][:a.proxy_threads])) as px:
+            print(f"hola cluster: {a.replicas} replicas on ports {rs.ports} behind :{px.port} (Ctrl-C to stop)",
+                  flush=True)
+            try:
+                while True:
+                    time.sleep(1)
+            except KeyboardInterrupt:
+                pass
+    return 0
+
+
+def _info() -> int:
+    from hola_amd.utils.cpu import (allowed_cpus, cgroup_cpu_quota, cpu_budget, format_cpu_list, l3_domain,
+                                    physical_cores, plan_node)
+
+    phys = physical_cores()
+    doms: dict[int, list[int]] = {}
+    for c in phys:
+        doms.setdefault(l3_domain(c), []).append(c)
+    print(f"allowed cpus   : {format_cpu_list(allowed_cpus())}")
+    print(f"physical cores : {len(phys)} in {len(doms)} L3 domains")
+    print(f"cgroup quota   : {cgroup_cpu_quota() or 'unlimited'}  -> budget {cpu_budget()} CPUs")
+    for n in (1, 2, 4, 8):
+        print(f"plan x{n}: {[format_cpu_list(p) for p in plan_node(n, avoid_busy=False)]}")
+    return 0
+
+
+def main(argv: list[str] | None = None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    if not argv or argv[0] in ("-h", "--help"):
+        print(__doc__)
+        return 0
+    cmd, rest = argv[0], argv[1:]
+    if cmd == "build":
+        ap = argparse.ArgumentParser(prog="python -m hola_amd build")
+        ap.add_argument("--preset", default="release", choices=sorted(native.PRESETS))
+        a = ap.parse_args(rest)
+        d = native.build(a.preset, quiet=False)
+        print(f"built {a.preset} -> {d}")
+        return 0
+    if cmd == "serve":
+        return _serve(rest)
+    if cmd == "cluster":
+        return _cluster(rest)
+    if cmd == "scaling":
+        from hola_amd.parallel import scaling
+
+        return scaling.main(rest)
+    if cmd == "bench":
+        root = Path(__file__).resolve().parent.parent
+        return subprocess.call([sys.executable, str(root / "bench.py"), *rest])
+    if cmd == "info":
+        return _info()
+    print(f"unknown command {cmd!r}\n{__doc__}", file=sys.stderr)
+    return 2
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -6,7 +6,7 @@ import subprocess
 
 from hola_amd.native import binary
 
-SUB = 64  # must match bench/histogram.h
+SUB = 64  # must match src/core/histogram.h
 
 
 def bin_value(b: int) -> int:

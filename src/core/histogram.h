@@ -1,12 +1,12 @@
 // Log-linear latency histogram (HDR-style: 64 sub-buckets per power of two, ~1.6 %
-// relative precision) for the load generator. Mergeable across threads and processes.
+// relative precision) for the load generator and the server --profile mode. Mergeable across threads/processes.
 #pragma once
 #include <algorithm>
 #include <cstdint>
 #include <string>
 #include <vector>
 
-namespace hola::bench {
+namespace hola {
 
 class Histogram {
  public:
@@ -80,4 +80,4 @@ class Histogram {
   uint64_t count_ = 0, sum_ = 0, max_ = 0, min_ = UINT64_MAX;
 };
 
-}  // namespace hola::bench
+}  // namespace hola

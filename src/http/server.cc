@@ -6,6 +6,7 @@
 #include <unistd.h>
 
 #include <chrono>
+#include <cstdio>
 #include <cstring>
 
 #include "core/affinity.h"
@@ -68,9 +69,12 @@ void Connection::on_readable() {
     return;
   }
   if (parked_ || !reading_) return;
+  StageProfile* prof = worker_->profile();
+  int64_t t0 = prof ? mono_ns() : 0;
   if (in_.empty()) {
     char* buf = worker_->scratch();
     ssize_t n = ::recv(fd_, buf, worker_->scratch_size(), 0);
+    if (prof && n > 0) prof->recv.add(uint64_t(mono_ns() - t0));
     if (n <= 0) {
       if (n == 0 || (errno != EAGAIN && errno != EINTR)) close();
       return;
@@ -105,10 +109,14 @@ bool Connection::process(const char* data, size_t len, size_t* consumed) {
   RequestHandler& h = worker_->handler();
   in_process_ = true;
   size_t off = 0;
+  uint64_t handled = 0;
   while (off < len && !parked_ && !streaming_ && !closed_ && !close_after_flush_) {
     Request r;
     int status = 400;
+    StageProfile* prof = worker_->profile();
+    int64_t tp = prof ? mono_ns() : 0;
     Parse p = parse_request(data + off, len - off, &r, &status);
+    if (prof && p == Parse::kOk) prof->parse.add(uint64_t(mono_ns() - tp));
     if (p == Parse::kIncomplete) break;
     if (p == Parse::kError) {
       WorkerStats::bump(st.parse_errors);
@@ -145,10 +153,18 @@ bool Connection::process(const char* data, size_t len, size_t* consumed) {
     }
     off += total;
     WorkerStats::bump(st.requests);
-    h.on_request(*this, r);
+    ++handled;
+    if (prof) {
+      int64_t th = mono_ns();
+      h.on_request(*this, r);
+      prof->handle.add(uint64_t(mono_ns() - th));
+    } else {
+      h.on_request(*this, r);
+    }
     if (worker_->server().draining()) close_after_flush_ = true;
   }
   in_process_ = false;
+  if (StageProfile* prof = worker_->profile(); prof && handled) prof->batch.add(handled);
   *consumed = off;
   if (closed_) return false;
   if (parked_ || streaming_) update_interest();
@@ -195,8 +211,11 @@ void Connection::start_streaming(std::function<void()> on_close) {
 
 void Connection::flush() {
   WorkerStats& st = worker_->stats();
+  StageProfile* prof = worker_->profile();
   while (out_off_ < out_.size()) {
+    int64_t ts = prof ? mono_ns() : 0;
     ssize_t w = ::send(fd_, out_.data() + out_off_, out_.size() - out_off_, MSG_NOSIGNAL);
+    if (prof && w > 0) prof->send.add(uint64_t(mono_ns() - ts));
     if (w < 0) {
       if (errno == EINTR) continue;
       if (errno == EAGAIN) {
@@ -268,6 +287,7 @@ std::string Connection::peer() const {
 
 Worker::Worker(Server* s, int index) : server_(s), index_(index) {
   scratch_.resize(s->options().read_chunk);
+  if (s->options().profile) profile_ = std::make_unique<StageProfile>();
   memset(date_, ' ', sizeof date_);
   tick();
   loop_.set_tick([this] { tick(); });
@@ -440,6 +460,29 @@ void Server::shutdown(int drain_ms) {
     std::this_thread::sleep_for(std::chrono::milliseconds(10));
   }
   for (auto& w : workers_) w->loop().stop();
+}
+
+std::string Server::profile_json() const {
+  if (!opts_.profile) return "{}";
+  StageProfile all;
+  for (auto& w : workers_) {
+    const StageProfile* p = w->profile_.get();
+    all.recv.merge(p->recv);
+    all.parse.merge(p->parse);
+    all.handle.merge(p->handle);
+    all.send.merge(p->send);
+    all.batch.merge(p->batch);
+  }
+  auto one = [](const char* name, const Histogram& h) {
+    char buf[256];
+    snprintf(buf, sizeof buf, "\"%s\":{\"count\":%llu,\"mean\":%.1f,\"p50\":%llu,\"p99\":%llu,\"p999\":%llu,\"max\":%llu}",
+             name, (unsigned long long)h.count(), h.mean(), (unsigned long long)h.percentile(50),
+             (unsigned long long)h.percentile(99), (unsigned long long)h.percentile(99.9),
+             (unsigned long long)h.max());
+    return std::string(buf);
+  };
+  return "{\"unit\":\"ns (batch: requests per recv)\"," + one("recv", all.recv) + "," + one("parse", all.parse) + "," +
+         one("handle", all.handle) + "," + one("send", all.send) + "," + one("batch", all.batch) + "}";
 }
 
 void Server::join() {

@@ -13,6 +13,7 @@
 #include <thread>
 #include <vector>
 
+#include "core/histogram.h"
 #include "core/loop.h"
 #include "http/parser.h"
 
@@ -126,6 +127,12 @@ struct ServerOptions {
   int backlog = 4096;
   size_t read_chunk = 64 * 1024;
   int busy_poll_us = 0;  // see EventLoop::set_busy_poll_us
+  bool profile = false;  // per-stage latency histograms (SURVEY.md §5.1 --profile)
+};
+
+// Per-worker stage timings (ns) collected with --profile; read after the workers stop.
+struct StageProfile {
+  Histogram recv, parse, handle, send, batch;  // batch = requests handled per recv()
 };
 
 class Worker {
@@ -151,6 +158,7 @@ class Worker {
   void close_idle_connections();
   // Per-worker slot for the application.
   void* app_data = nullptr;
+  StageProfile* profile() { return profile_.get(); }
 
  private:
   friend class Server;
@@ -166,6 +174,7 @@ class Worker {
   uint64_t next_conn_id_ = 1;
   size_t nconns_ = 0;
   Connection* conns_ = nullptr;
+  std::unique_ptr<StageProfile> profile_;
 };
 
 class Server {
@@ -186,6 +195,8 @@ class Server {
   const ServerOptions& options() const { return opts_; }
   bool draining() const { return draining_.load(std::memory_order_relaxed); }
   uint64_t total_requests() const;
+  // JSON summary of the --profile histograms (call after join()).
+  std::string profile_json() const;
 
  private:
   struct Acceptor : EventLoop::Handler {

@@ -55,6 +55,8 @@ void usage() {
           "  --drain-ms N             graceful shutdown drain budget (default 5000)\n"
           "  --port-file PATH         write the bound port here once listening\n"
           "  --busy-poll-us N         spin up to N us in epoll before sleeping (default 0)\n"
+          "  --profile                per-stage latency histograms (recv/parse/handle/send), dumped at exit\n"
+          "  --profile-out PATH       write the --profile JSON here (default: stderr)\n"
           "  --log-level L            debug|info|warn|error|off (default info)\n"
           "  --no-metrics             disable the /metrics endpoint\n");
 }
@@ -83,7 +85,7 @@ int main(int argc, char** argv) {
   const char* hn = getenv("HOSTNAME");
   if (hn) ao.hostname = hn;  // HolaResource.java:57 getOrDefault("HOSTNAME", "unknown")
   int threads = 0, drain_ms = 5000, stream_max = 5;
-  std::string cpu_list, port_file;
+  std::string cpu_list, port_file, profile_out;
   bool no_tracing = false;
 
   for (int i = 1; i < argc; ++i) {
@@ -119,6 +121,8 @@ int main(int argc, char** argv) {
     else if (a == "--drain-ms") drain_ms = atoi(val("--drain-ms").c_str());
     else if (a == "--port-file") port_file = val("--port-file");
     else if (a == "--busy-poll-us") so.busy_poll_us = atoi(val("--busy-poll-us").c_str());
+    else if (a == "--profile") so.profile = true;
+    else if (a == "--profile-out") profile_out = val("--profile-out");
     else if (a == "--no-metrics") ao.enable_metrics_endpoint = false;
     else if (a == "--log-level") {
       LogLevel l;
@@ -225,6 +229,15 @@ int main(int argc, char** argv) {
   LOG_INFO("received %s: draining (up to %d ms)", sig == SIGTERM ? "SIGTERM" : "SIGINT", drain_ms);
   server.shutdown(drain_ms);
   server.join();
+  if (so.profile) {
+    std::string pj = server.profile_json();
+    if (profile_out.empty()) {
+      LOG_INFO("profile: %s", pj.c_str());
+    } else {
+      std::ofstream f(profile_out);
+      f << pj << "\n";
+    }
+  }
   cfg.stop();
   chainer.stop();
   tracer.stop();
