@@ -5,6 +5,7 @@
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstring>
@@ -41,7 +42,8 @@ std::string RequestHandler::error_response(int status) {
 
 // ---------------------------------------------------------------- Connection
 
-Connection::Connection(Worker* w, int fd, uint64_t id) : worker_(w), fd_(fd), id_(id) {}
+Connection::Connection(Worker* w, int fd, uint64_t id)
+    : worker_(w), fd_(fd), id_(id), last_active_ms_(w->loop().now_ms()) {}
 
 Connection::~Connection() {
   if (fd_ >= 0) ::close(fd_);
@@ -62,6 +64,7 @@ void Connection::on_event(uint32_t ev) {
 
 void Connection::on_readable() {
   WorkerStats& st = worker_->stats();
+  last_active_ms_ = worker_->loop().now_ms();
   if (streaming_) {
     char buf[4096];
     ssize_t n = ::recv(fd_, buf, sizeof buf, 0);
@@ -307,6 +310,7 @@ void Worker::tick() {
 
 void Worker::on_connection_closed(Connection* c) {
   --nconns_;
+  server_->open_.fetch_sub(1, std::memory_order_relaxed);
   if (c->prev_) c->prev_->next_ = c->next_;
   else conns_ = c->next_;
   if (c->next_) c->next_->prev_ = c->prev_;
@@ -321,17 +325,34 @@ void Worker::close_idle_connections() {
   }
 }
 
+void Worker::sweep_idle() {
+  const int64_t limit = server_->options().idle_timeout_ms;
+  const int64_t now = loop_.now_ms();
+  for (Connection* c = conns_; c;) {
+    Connection* next = c->next_;
+    if (!c->streaming() && c->idle() && now - c->last_active_ms() > limit) c->close();
+    c = next;
+  }
+}
+
 void Worker::adopt(int fd) {
   loop_.post([this, fd] { adopt_here(fd); });
 }
 
 void Worker::adopt_here(int fd) {
   auto* c = new Connection(this, fd, (uint64_t(index_) << 48) | next_conn_id_++);
+  const size_t maxc = server_->options().max_connections;
+  if (maxc && server_->open_connections() >= maxc) {
+    WorkerStats::bump(stats_.rejected);
+    delete c;  // over the limit: refuse by closing (the client sees a reset/EOF)
+    return;
+  }
   if (server_->draining() || !loop_.add(fd, EPOLLIN | EPOLLRDHUP, c)) {
     delete c;
     return;
   }
   ++nconns_;
+  server_->open_.fetch_add(1, std::memory_order_relaxed);
   WorkerStats::bump(stats_.accepted);
   c->next_ = conns_;
   if (conns_) conns_->prev_ = c;
@@ -411,6 +432,18 @@ void Server::start() {
         if (!pin_current_thread(cpu)) LOG_WARN("worker %d: could not pin to cpu %d", wp->index(), cpu);
       }
       handler_->on_worker_start(*wp);
+      if (opts_.idle_timeout_ms > 0) {
+        int period = std::max(50, std::min(1000, opts_.idle_timeout_ms / 4));
+        auto sweep = std::make_shared<std::function<void()>>();
+        Worker* w = wp;
+        std::weak_ptr<std::function<void()>> weak = sweep;
+        *sweep = [w, period, weak] {
+          w->sweep_idle();
+          if (auto f = weak.lock()) w->loop().add_timer(period, [f] { (*f)(); });
+        };
+        wp->sweep_ = sweep;
+        wp->loop().add_timer(period, [sweep] { (*sweep)(); });
+      }
       wp->loop().run();
       handler_->on_worker_stop(*wp);
     });

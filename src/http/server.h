@@ -28,6 +28,7 @@ struct alignas(64) WorkerStats {
   std::atomic<uint64_t> accepted{0};
   std::atomic<uint64_t> closed{0};
   std::atomic<uint64_t> parse_errors{0};
+  std::atomic<uint64_t> rejected{0};  // refused over max_connections
   std::atomic<uint64_t> bytes_in{0};
   std::atomic<uint64_t> bytes_out{0};
   // single-writer increment without a locked RMW
@@ -74,6 +75,7 @@ class Connection final : public EventLoop::Handler {
   std::string peer() const;
   // Idle = no request in progress and nothing buffered either way.
   bool idle() const { return !parked_ && in_.empty() && out_.size() == out_off_; }
+  int64_t last_active_ms() const { return last_active_ms_; }
 
  private:
   void on_readable();
@@ -98,6 +100,7 @@ class Connection final : public EventLoop::Handler {
   bool reading_ = true;
   bool in_process_ = false;  // inside process(): batch writes instead of sending eagerly
   int holds_ = 0;
+  int64_t last_active_ms_ = 0;
   std::function<void()> on_close_;
   // intrusive per-worker list (for draining on shutdown)
   Connection* prev_ = nullptr;
@@ -128,6 +131,10 @@ struct ServerOptions {
   size_t read_chunk = 64 * 1024;
   int busy_poll_us = 0;  // see EventLoop::set_busy_poll_us
   bool profile = false;  // per-stage latency histograms (SURVEY.md §5.1 --profile)
+  // Close keep-alive connections idle this long (Undertow/WildFly no-request-timeout is
+  // 60 s by default); 0 disables.
+  int idle_timeout_ms = 60000;
+  size_t max_connections = 0;  // per replica; 0 = unlimited (bounded by RLIMIT_NOFILE)
 };
 
 // Per-worker stage timings (ns) collected with --profile; read after the workers stop.
@@ -156,6 +163,8 @@ class Worker {
   void on_connection_closed(Connection* c);
   // Closes idle and streaming connections (shutdown drain); runs on the worker thread.
   void close_idle_connections();
+  // Closes keep-alive connections idle for longer than the idle timeout.
+  void sweep_idle();
   // Per-worker slot for the application.
   void* app_data = nullptr;
   StageProfile* profile() { return profile_.get(); }
@@ -175,6 +184,7 @@ class Worker {
   size_t nconns_ = 0;
   Connection* conns_ = nullptr;
   std::unique_ptr<StageProfile> profile_;
+  std::shared_ptr<std::function<void()>> sweep_;  // idle-timeout sweeper (owned here)
 };
 
 class Server {
@@ -195,6 +205,7 @@ class Server {
   const ServerOptions& options() const { return opts_; }
   bool draining() const { return draining_.load(std::memory_order_relaxed); }
   uint64_t total_requests() const;
+  size_t open_connections() const { return open_.load(std::memory_order_relaxed); }
   // JSON summary of the --profile histograms (call after join()).
   std::string profile_json() const;
 
@@ -212,7 +223,9 @@ class Server {
   std::vector<std::thread> threads_;
   std::atomic<bool> draining_{false};
   std::atomic<uint64_t> rr_{0};
+  std::atomic<size_t> open_{0};
   int port_ = 0;
+  friend class Worker;
 };
 
 }  // namespace hola::http

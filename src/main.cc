@@ -55,6 +55,8 @@ void usage() {
           "  --drain-ms N             graceful shutdown drain budget (default 5000)\n"
           "  --port-file PATH         write the bound port here once listening\n"
           "  --busy-poll-us N         spin up to N us in epoll before sleeping (default 0)\n"
+          "  --idle-timeout-ms N      close keep-alive connections idle this long (default 60000, 0 = never)\n"
+          "  --max-connections N      refuse connections beyond N per replica (default unlimited)\n"
           "  --profile                per-stage latency histograms (recv/parse/handle/send), dumped at exit\n"
           "  --profile-out PATH       write the --profile JSON here (default: stderr)\n"
           "  --log-level L            debug|info|warn|error|off (default info)\n"
@@ -122,6 +124,8 @@ int main(int argc, char** argv) {
     else if (a == "--port-file") port_file = val("--port-file");
     else if (a == "--busy-poll-us") so.busy_poll_us = atoi(val("--busy-poll-us").c_str());
     else if (a == "--profile") so.profile = true;
+    else if (a == "--idle-timeout-ms") so.idle_timeout_ms = atoi(val("--idle-timeout-ms").c_str());
+    else if (a == "--max-connections") so.max_connections = size_t(atol(val("--max-connections").c_str()));
     else if (a == "--profile-out") profile_out = val("--profile-out");
     else if (a == "--no-metrics") ao.enable_metrics_endpoint = false;
     else if (a == "--log-level") {

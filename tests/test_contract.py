@@ -2,6 +2,7 @@
 native server binary."""
 import json
 import socket
+import time
 
 import pytest
 
@@ -187,3 +188,33 @@ def test_date_header(hola):
     s = hola()
     _, h, _ = s.get("/api/hola")
     assert h["date"].endswith("GMT") and len(h["date"]) == 29
+
+
+def test_idle_keepalive_connections_are_closed(hola):
+    s = hola(args=["--idle-timeout-ms", "200"])
+    with socket.create_connection(("127.0.0.1", s.port), timeout=3) as c:
+        c.sendall(b"GET /api/health HTTP/1.1\r\nHost: x\r\n\r\n")
+        assert b"I'm ok" in c.recv(4096)
+        time.sleep(0.8)
+        assert c.recv(4096) == b""  # server closed the idle connection
+
+
+def test_max_connections(hola):
+    s = hola(args=["--max-connections", "2"], threads=1)
+    socks = [socket.create_connection(("127.0.0.1", s.port), timeout=3) for _ in range(2)]
+    try:
+        for c in socks:
+            c.sendall(b"GET /api/health HTTP/1.1\r\nHost: x\r\n\r\n")
+            assert b"I'm ok" in c.recv(4096)
+        with socket.create_connection(("127.0.0.1", s.port), timeout=3) as extra:
+            extra.sendall(b"GET /api/health HTTP/1.1\r\nHost: x\r\n\r\n")
+            try:
+                data = extra.recv(4096)
+            except ConnectionResetError:
+                data = b""
+            assert data == b""
+    finally:
+        for c in socks:
+            c.close()
+    time.sleep(0.1)
+    assert s.get("/api/health")[0] == 200  # capacity returns once connections close
