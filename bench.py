@@ -30,7 +30,7 @@ from hola_amd.native import ensure_built  # noqa: E402
 from hola_amd.parallel.loadgen import ControlledLoadgen, decode_hist, merge_hists, percentile  # noqa: E402
 from hola_amd.server import HolaProcess  # noqa: E402
 from hola_amd.utils.cpu import (  # noqa: E402
-    cgroup_cpu_quota, cpu_budget, format_cpu_list, plan_node, split_server_loadgen)
+    cgroup_cpu_quota, cpu_budget, format_cpu_list, plan_replicas_with_loadgen)
 
 METRIC = "HTTP req/sec + p50/p99 latency, GET /api/hola at 1/2/4/8 replicas"
 BASELINE_VALUE = None  # the reference publishes no numbers
@@ -77,17 +77,12 @@ def main() -> int:
     # ---- core plan: disjoint physical cores per rank, quietest L3 domains first (computed
     # once on rank 0 and broadcast, since load measurements differ between processes);
     # within a rank, server worker t and loadgen thread t share an L3 domain. ----
-    plan = [plan_node(local_world, a.cores or None, avoid_busy=not a.no_avoid_busy)] if rank == 0 else [None]
+    plan = [plan_replicas_with_loadgen(local_world, a.cores or None, a.server_threads,
+                                       avoid_busy=not a.no_avoid_busy)] if rank == 0 else [None]
     if dist:
         dist.broadcast_object_list(plan, src=0)
-    cores = plan[0][local_rank]
-    n = len(cores)
-    s_threads = a.server_threads or max(1, n // 2)
-    s_threads = min(s_threads, max(1, n - 1)) if n > 1 else 1
-    if n > 1:
-        server_cpus, load_cpus = split_server_loadgen(cores, s_threads)
-    else:
-        server_cpus, load_cpus = cores, cores
+    server_cpus, load_cpus = plan[0][local_rank]["server"], plan[0][local_rank]["loadgen"]
+    s_threads = len(server_cpus)
     port = a.base_port + local_rank
     targets = [("127.0.0.1", a.base_port + i) for i in range(local_world)]
 
@@ -106,7 +101,7 @@ def main() -> int:
     try:
         if dist:
             dist.barrier()  # every replica is listening before any connection is made
-        loadgen = ControlledLoadgen(targets, a.connections, len(load_cpus), cpu_list=format_cpu_list(load_cpus),
+        loadgen = ControlledLoadgen(targets, a.connections, len(load_cpus), cpu_list=",".join(map(str, load_cpus)),
                                     path=a.path, target_offset=local_rank, busy_poll_us=a.busy_poll_us)
         for _ in range(a.warmup):
             loadgen.run(a.reqs_per_conn)

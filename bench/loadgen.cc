@@ -91,6 +91,8 @@ struct ThreadState {
 
 std::atomic<bool> g_stop{false};
 int g_donefd = -1;  // EFD_SEMAPHORE: one count per thread finishing a control run
+std::atomic<bool> g_connect_failed{false};
+char g_connect_error[256];
 
 void signal_done() {
   uint64_t one = 1;
@@ -157,6 +159,17 @@ int response_complete(Conn* c, int* status, bool* close) {
 
 void thread_main(ThreadState* ts, const Options* o) {
   if (!o->cpus.empty()) pin_current_thread(o->cpus[size_t(ts->index) % o->cpus.size()]);
+  for (auto& c : ts->conns) {
+    if (!connect_once(c.get(), *o)) {
+      const Target& t = o->targets[size_t(c->target)];
+      if (!g_connect_failed.exchange(true))
+        snprintf(g_connect_error, sizeof g_connect_error, "connect %s:%d failed: %s", t.host.c_str(), t.port,
+                 strerror(errno));
+      signal_done();
+      return;
+    }
+  }
+  signal_done();
   epoll_event ev{};
   for (auto& c : ts->conns) {
     ev.events = EPOLLIN;
@@ -405,14 +418,21 @@ int main(int argc, char** argv) {
     c->req = o.method + " " + o.path + " HTTP/1.1\r\nHost: " + t.host + ":" + std::to_string(t.port) + "\r\n";
     for (auto& h : o.extra_headers) c->req += h + "\r\n";
     c->req += "\r\n";
-    if (!connect_once(c.get(), o)) {
-      fprintf(stderr, "loadgen: connect %s:%d failed: %s\n", t.host.c_str(), t.port, strerror(errno));
-      return 1;
-    }
     ts[size_t(i % o.threads)]->conns.push_back(std::move(c));
   }
   std::vector<std::thread> th;
   for (auto& s : ts) th.emplace_back(thread_main, s.get(), &o);
+  // Each thread connects its own connections from its pinned CPU (as wrk does), so the
+  // server sees every connection's packets arrive on the CPU that will drive it.
+  for (size_t k = 0; k < ts.size(); ++k) {
+    uint64_t v;
+    while (::read(g_donefd, &v, sizeof v) < 0 && errno == EINTR) {
+    }
+  }
+  if (g_connect_failed.load()) {
+    fprintf(stderr, "loadgen: %s\n", g_connect_error);
+    _exit(1);
+  }
 
   if (!o.control) {
     for (auto& t : th) t.join();

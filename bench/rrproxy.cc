@@ -4,9 +4,8 @@
 // Each accepted client connection is bound to the next *healthy* backend (round-robin).
 // Health = GET /api/health answered 200 (the readiness probe of pom.xml:90-94), checked
 // every --health-ms by a background thread; unhealthy replicas are skipped until they pass
-// again. Bytes are relayed with splice(2) through per-direction pipes (zero-copy).
+// again. Bytes are relayed with recv/send through a small per-direction buffer.
 #include <errno.h>
-#include <fcntl.h>
 #include <signal.h>
 #include <sys/epoll.h>
 #include <sys/socket.h>
@@ -52,9 +51,10 @@ Backend* pick() {
   return nullptr;
 }
 
-struct Pipe {
-  int r = -1, w = -1;
-  size_t buffered = 0;
+// One direction of a session: bytes read from `from` waiting to be written to `to`.
+struct Dir {
+  char buf[16384];
+  size_t len = 0, off = 0;
 };
 
 struct Session;
@@ -65,25 +65,73 @@ struct Ev {
 
 struct Session {
   int cfd = -1, bfd = -1;
-  Pipe c2b, b2c;
+  Dir c2b, b2c;
   bool closing = false;
   Ev ec{this, true}, eb{this, false};
+  uint32_t cint = EPOLLIN | EPOLLRDHUP, bint = EPOLLIN | EPOLLRDHUP;
 };
 
-bool relay(int from, Pipe& p, int to) {
+// Plain recv/send relay: for the small request/response messages of this service it costs
+// two syscalls per hop, less than splice(2) through a pipe (four).
+// Returns false when the session must close.
+bool pump(int epfd, Session* s, bool from_client) {
+  int from = from_client ? s->cfd : s->bfd, to = from_client ? s->bfd : s->cfd;
+  Dir& d = from_client ? s->c2b : s->b2c;
   for (;;) {
-    if (p.buffered == 0) {
-      ssize_t n = splice(from, nullptr, p.w, nullptr, 1 << 16, SPLICE_F_MOVE | SPLICE_F_NONBLOCK);
-      if (n == 0) return false;  // EOF
-      if (n < 0) return errno == EAGAIN;
-      p.buffered = size_t(n);
+    if (d.off < d.len) {
+      ssize_t m = ::send(to, d.buf + d.off, d.len - d.off, MSG_NOSIGNAL);
+      if (m < 0) {
+        if (errno == EAGAIN) {
+          // destination full: stop reading `from`, wait for `to` to drain
+          uint32_t& fi = from_client ? s->cint : s->bint;
+          uint32_t& ti = from_client ? s->bint : s->cint;
+          epoll_event ev{};
+          fi = EPOLLRDHUP;
+          ev.events = fi;
+          ev.data.ptr = from_client ? &s->ec : &s->eb;
+          epoll_ctl(epfd, EPOLL_CTL_MOD, from, &ev);
+          ti |= EPOLLOUT;
+          ev.events = ti;
+          ev.data.ptr = from_client ? &s->eb : &s->ec;
+          epoll_ctl(epfd, EPOLL_CTL_MOD, to, &ev);
+          return true;
+        }
+        return false;
+      }
+      d.off += size_t(m);
+      continue;
     }
-    while (p.buffered) {
-      ssize_t m = splice(p.r, nullptr, to, nullptr, p.buffered, SPLICE_F_MOVE | SPLICE_F_NONBLOCK);
-      if (m < 0) return errno == EAGAIN;  // destination full: retry on next readiness
-      p.buffered -= size_t(m);
-    }
+    d.off = d.len = 0;
+    ssize_t n = ::recv(from, d.buf, sizeof d.buf, 0);
+    if (n == 0) return false;
+    if (n < 0) return errno == EAGAIN || errno == EINTR;
+    d.len = size_t(n);
   }
+}
+
+// `fd` became writable: flush what was waiting for it and resume reading the other side.
+bool drained(int epfd, Session* s, bool client_writable) {
+  bool from_client = !client_writable;  // data flowing *to* the writable socket
+  Dir& d = from_client ? s->c2b : s->b2c;
+  int to = client_writable ? s->cfd : s->bfd, from = client_writable ? s->bfd : s->cfd;
+  while (d.off < d.len) {
+    ssize_t m = ::send(to, d.buf + d.off, d.len - d.off, MSG_NOSIGNAL);
+    if (m < 0) return errno == EAGAIN;
+    d.off += size_t(m);
+  }
+  d.off = d.len = 0;
+  uint32_t& ti = client_writable ? s->cint : s->bint;
+  uint32_t& fi = client_writable ? s->bint : s->cint;
+  epoll_event ev{};
+  ti &= ~uint32_t(EPOLLOUT);
+  ev.events = ti;
+  ev.data.ptr = client_writable ? &s->ec : &s->eb;
+  epoll_ctl(epfd, EPOLL_CTL_MOD, to, &ev);
+  fi = EPOLLIN | EPOLLRDHUP | (fi & EPOLLOUT);
+  ev.events = fi;
+  ev.data.ptr = client_writable ? &s->eb : &s->ec;
+  epoll_ctl(epfd, EPOLL_CTL_MOD, from, &ev);
+  return pump(epfd, s, from_client);
 }
 
 void close_session(int epfd, Session* s) {
@@ -91,7 +139,6 @@ void close_session(int epfd, Session* s) {
   epoll_ctl(epfd, EPOLL_CTL_DEL, s->bfd, nullptr);
   ::close(s->cfd);
   ::close(s->bfd);
-  for (int fd : {s->c2b.r, s->c2b.w, s->b2c.r, s->b2c.w}) ::close(fd);
 }
 
 void worker(int lfd, int cpu) {
@@ -127,18 +174,10 @@ void worker(int lfd, int cpu) {
           auto* s = new Session();
           s->cfd = c;
           s->bfd = bfd;
-          int p1[2], p2[2];
-          if (pipe2(p1, O_NONBLOCK | O_CLOEXEC) || pipe2(p2, O_NONBLOCK | O_CLOEXEC)) {
-            ::close(c);
-            ::close(bfd);
-            delete s;
-            continue;
-          }
-          s->c2b = {p1[0], p1[1], 0};
-          s->b2c = {p2[0], p2[1], 0};
-          ev.events = EPOLLIN | EPOLLRDHUP;
+          ev.events = s->cint;
           ev.data.ptr = &s->ec;
           epoll_ctl(epfd, EPOLL_CTL_ADD, c, &ev);
+          ev.events = s->bint;
           ev.data.ptr = &s->eb;
           epoll_ctl(epfd, EPOLL_CTL_ADD, bfd, &ev);
         }
@@ -147,8 +186,11 @@ void worker(int lfd, int cpu) {
       Ev* e = static_cast<Ev*>(evs[i].data.ptr);
       Session* s = e->s;
       if (s->closing) continue;
-      bool ok = e->client ? relay(s->cfd, s->c2b, s->bfd) : relay(s->bfd, s->b2c, s->cfd);
-      if (!ok || (evs[i].events & (EPOLLERR | EPOLLHUP))) {
+      bool ok = true;
+      uint32_t evm = evs[i].events;
+      if (evm & EPOLLOUT) ok = drained(epfd, s, e->client);
+      if (ok && (evm & (EPOLLIN | EPOLLRDHUP | EPOLLHUP))) ok = pump(epfd, s, e->client);
+      if (!ok || (evm & EPOLLERR)) {
         s->closing = true;
         close_session(epfd, s);
         dead.push_back(s);  // the peer's event may still be in this batch: free afterwards

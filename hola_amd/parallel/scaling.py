@@ -17,22 +17,39 @@ import time
 
 from hola_amd.parallel.loadgen import run_duration
 from hola_amd.parallel.replicas import ReplicaSet, RRProxy
-from hola_amd.utils.cpu import cgroup_cpu_quota, cpu_budget, format_cpu_list, physical_cores, allowed_cpus
+from hola_amd.utils.cpu import cgroup_cpu_quota, cpu_budget, format_cpu_list, plan_node, split_server_loadgen
 
 
 def plan(n_replicas: int, budget: int, server_share: float, proxy_threads: int) -> dict:
-    cores = physical_cores()
-    if len(cores) < budget:
-        cores = allowed_cpus()
-    cores = cores[:budget]
-    n_server = max(n_replicas, int(round(budget * server_share)))
-    n_server = min(n_server, budget - 1 - proxy_threads)
-    per = max(1, n_server // n_replicas)
-    replica_cpus = [cores[i * per:(i + 1) * per] for i in range(n_replicas)]
-    used = per * n_replicas
-    proxy_cpus = cores[used:used + proxy_threads] if proxy_threads else []
-    load_cpus = cores[used + proxy_threads:] or cores[-1:]
-    return {"replicas": replica_cpus, "proxy": proxy_cpus, "loadgen": load_cpus}
+    """Cores for N replicas + one load generator (+ proxy) inside `budget` CPUs.
+
+    Each replica gets an equal slice of the quietest L3 domains, split between its server
+    loops and the load-generator threads that drive it: the generator deals connection i to
+    thread i % T and replica i % N, so thread t is placed in replica (t % N)'s L3 domain.
+    """
+    usable = budget - proxy_threads
+    per = max(2, usable // n_replicas) if usable >= 2 * n_replicas else max(1, usable // n_replicas)
+    slices = plan_node(n_replicas + (1 if proxy_threads else 0), per_rank=per)
+    replica_cpus, load_by_replica = [], []
+    for k in range(n_replicas):
+        cores = slices[k]
+        if len(cores) > 1:
+            srv, lg = split_server_loadgen(cores, max(1, int(round(len(cores) * server_share))))
+        else:
+            srv, lg = cores, cores
+        replica_cpus.append(srv)
+        load_by_replica.append(lg)
+    load = []
+    t = 0
+    while any(load_by_replica):
+        k = t % n_replicas
+        if load_by_replica[k]:
+            load.append(load_by_replica[k].pop(0))
+        t += 1
+        if t > 10000:
+            break
+    proxy_cpus = slices[-1][:proxy_threads] if proxy_threads else []
+    return {"replicas": replica_cpus, "proxy": proxy_cpus, "loadgen": load}
 
 
 def run_point(n: int, args) -> dict:
@@ -46,10 +63,10 @@ def run_point(n: int, args) -> dict:
             with RRProxy(rs.targets, threads=proxy_threads, cpu_list=format_cpu_list(p["proxy"])) as px:
                 targets = [("127.0.0.1", px.port)]
                 res = run_duration(targets, conns, len(p["loadgen"]), args.duration, args.warmup,
-                                   cpu_list=format_cpu_list(p["loadgen"]))
+                                   cpu_list=",".join(map(str, p["loadgen"])))
         else:
             res = run_duration(rs.targets, conns, len(p["loadgen"]), args.duration, args.warmup,
-                               cpu_list=format_cpu_list(p["loadgen"]))
+                               cpu_list=",".join(map(str, p["loadgen"])))
     lat = res["latency"]
     return {
         "replicas": n, "connections": conns, "lb": args.lb, "rps": res["rps"],
@@ -82,11 +99,11 @@ def main(argv=None) -> int:
         rows.append(row)
         print(json.dumps(row), flush=True)
         time.sleep(0.5)
-    base = rows[0]["rps"] / rows[0]["replicas"] if rows else 0
-    table = ["| replicas | connections | LB | req/s | p50 ms | p99 ms | per-replica vs N=1 |",
+    base = rows[0]["rps"] if rows else 0
+    table = ["| replicas | connections | LB | req/s | p50 ms | p99 ms | total vs N=1 (same CPU budget) |",
              "|---|---|---|---|---|---|---|"]
     for r in rows:
-        eff = (r["rps"] / r["replicas"]) / base if base else 0
+        eff = r["rps"] / base if base else 0
         table.append(f"| {r['replicas']} | {r['connections']} | {r['lb']} | {r['rps']:.0f} | {r['p50_ms']:.3f} | "
                      f"{r['p99_ms']:.3f} | {eff:.2f} |")
     print("\n".join(table))

@@ -183,6 +183,40 @@ def split_server_loadgen(cores: list[int], server_threads: int) -> tuple[list[in
     return server, load
 
 
+def plan_replicas_with_loadgen(local_world: int, per_rank: int | None = None, server_threads: int = 0,
+                               avoid_busy: bool = True) -> list[dict]:
+    """Core plan for `local_world` co-located (replica + load generator) ranks with
+    client-side round-robin over all replicas.
+
+    Rank r's load-generator thread t drives replica (t + r) % N (connection i -> thread i % T,
+    target (i + r) % N, so with T % N == 0 each thread talks to exactly one replica). Its CPU
+    is therefore taken from the *target* replica's L3 domains, so every connection's client
+    and server ends share an L3 even though traffic crosses ranks. Returns, per rank,
+    {"server": [...], "loadgen": [... one CPU per thread, in thread order]}.
+    """
+    nodes = plan_node(local_world, per_rank, avoid_busy=avoid_busy)
+    splits = []
+    for cores in nodes:
+        if len(cores) > 1:
+            st = server_threads or max(1, len(cores) // 2)
+            st = min(st, len(cores) - 1)
+            splits.append(split_server_loadgen(cores, st))
+        else:
+            splits.append((cores, cores))
+    n = local_world
+    t_threads = len(splits[0][1])
+    uniform = all(len(sp[1]) == t_threads for sp in splits)
+    plans = []
+    for r in range(n):
+        if n > 1 and uniform and t_threads % n == 0:
+            per = t_threads // n
+            load = [splits[(t + r) % n][1][r * per + t // n] for t in range(t_threads)]
+        else:
+            load = splits[r][1]
+        plans.append({"server": splits[r][0], "loadgen": load})
+    return plans
+
+
 def plan_cores(rank: int, local_world: int, per_rank: int | None = None) -> list[int]:
     """Disjoint CPU set for `rank` out of `local_world` co-located ranks.
 

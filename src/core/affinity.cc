@@ -65,6 +65,29 @@ bool pin_current_thread(int cpu) {
   return pthread_setaffinity_np(pthread_self(), sizeof set, &set) == 0;
 }
 
+int l3_domain_of(int cpu) {
+  // Read once for every possible CPU (thread-safe static init); lookups are then lock-free.
+  static const std::vector<int> table = [] {
+    std::vector<int> v;
+    for (int c = 0; c < CPU_SETSIZE; ++c) {
+      std::ifstream f("/sys/devices/system/cpu/cpu" + std::to_string(c) + "/cache/index3/id");
+      if (!f) {
+        if (c > 0 && v.size() == size_t(c)) {
+          std::ifstream online("/sys/devices/system/cpu/cpu" + std::to_string(c));
+          if (!online) break;  // past the last CPU
+        }
+        v.push_back(-1);
+        continue;
+      }
+      int id = -1;
+      if (!(f >> id)) id = -1;
+      v.push_back(id);
+    }
+    return v;
+  }();
+  return (cpu >= 0 && size_t(cpu) < table.size()) ? table[size_t(cpu)] : -1;
+}
+
 double cgroup_cpu_quota() {
   std::ifstream f("/sys/fs/cgroup/cpu.max");
   std::string q, p;

@@ -12,6 +12,8 @@ std::string format_cpu_list(const std::vector<int>& cpus);
 std::vector<int> allowed_cpus();
 // Pins the calling thread to one CPU; false on failure (e.g. CPU not in the cgroup).
 bool pin_current_thread(int cpu);
+// L3 cache domain (a CCD on EPYC) of a CPU from sysfs; -1 when unknown. Cached.
+int l3_domain_of(int cpu);
 // CPU quota from cgroup v2 cpu.max (e.g. 16.0 for "1600000 100000"); 0 when unlimited.
 double cgroup_cpu_quota();
 

@@ -310,6 +310,7 @@ void Worker::tick() {
 
 void Worker::on_connection_closed(Connection* c) {
   --nconns_;
+  server_->assigned_[size_t(index_)].fetch_sub(1, std::memory_order_relaxed);
   server_->open_.fetch_sub(1, std::memory_order_relaxed);
   if (c->prev_) c->prev_->next_ = c->next_;
   else conns_ = c->next_;
@@ -344,10 +345,12 @@ void Worker::adopt_here(int fd) {
   const size_t maxc = server_->options().max_connections;
   if (maxc && server_->open_connections() >= maxc) {
     WorkerStats::bump(stats_.rejected);
+    server_->assigned_[size_t(index_)].fetch_sub(1, std::memory_order_relaxed);
     delete c;  // over the limit: refuse by closing (the client sees a reset/EOF)
     return;
   }
   if (server_->draining() || !loop_.add(fd, EPOLLIN | EPOLLRDHUP, c)) {
+    server_->assigned_[size_t(index_)].fetch_sub(1, std::memory_order_relaxed);
     delete c;
     return;
   }
@@ -364,6 +367,56 @@ void Worker::adopt_here(int fd) {
 Server::Server(ServerOptions opts, RequestHandler* handler) : opts_(std::move(opts)), handler_(handler) {
   if (opts_.threads < 1) opts_.threads = 1;
   for (int i = 0; i < opts_.threads; ++i) workers_.push_back(std::make_unique<Worker>(this, i));
+  assigned_.reset(new std::atomic<int32_t>[workers_.size()]);
+  for (size_t i = 0; i < workers_.size(); ++i) assigned_[i].store(0);
+  if (opts_.steer_l3 && !opts_.cpus.empty() && !opts_.reuseport_accept) {
+    for (size_t i = 0; i < workers_.size(); ++i) {
+      int dom = l3_domain_of(opts_.cpus[i % opts_.cpus.size()]);
+      if (dom < 0) {
+        domain_workers_.clear();
+        break;
+      }
+      auto it = std::find_if(domain_workers_.begin(), domain_workers_.end(),
+                             [dom](const auto& p) { return p.first == dom; });
+      if (it == domain_workers_.end()) domain_workers_.push_back({dom, {i}});
+      else it->second.push_back(i);
+    }
+    if (domain_workers_.size() <= 1) domain_workers_.clear();  // one domain: nothing to steer
+    domain_rr_.reset(new std::atomic<uint32_t>[domain_workers_.size() + 1]);
+    for (size_t i = 0; i <= domain_workers_.size(); ++i) domain_rr_[i].store(0);
+  }
+}
+
+Worker* Server::pick_worker(int fd) {
+  const size_t n = workers_.size();
+  size_t k = rr_.fetch_add(1, std::memory_order_relaxed) % n;
+  if (!domain_workers_.empty()) {
+    // The CPU that processed this connection's latest packet: for loopback clients, the
+    // client thread's own CPU. Serving it from the same L3 keeps both socket buffers in
+    // one cache domain (cross-CCD hand-offs more than double the cost of send()).
+    int cpu = -1;
+    socklen_t len = sizeof cpu;
+    if (getsockopt(fd, SOL_SOCKET, SO_INCOMING_CPU, &cpu, &len) == 0 && cpu >= 0) {
+      int dom = l3_domain_of(cpu);
+      for (size_t d = 0; d < domain_workers_.size(); ++d) {
+        if (domain_workers_[d].first != dom) continue;
+        const auto& ws = domain_workers_[d].second;
+        size_t cand = ws[domain_rr_[d].fetch_add(1, std::memory_order_relaxed) % ws.size()];
+        // Keep balance: do not pile onto a domain that is far ahead of the least loaded worker.
+        int32_t least = assigned_[0].load(std::memory_order_relaxed);
+        for (size_t i = 1; i < n; ++i) least = std::min(least, assigned_[i].load(std::memory_order_relaxed));
+        if (assigned_[cand].load(std::memory_order_relaxed) <= least + 8) {
+          k = cand;
+          ++steered_;
+        } else {
+          ++unsteered_;
+        }
+        break;
+      }
+    }
+  }
+  assigned_[k].fetch_add(1, std::memory_order_relaxed);
+  return workers_[k].get();
 }
 
 Server::~Server() {
@@ -412,10 +465,10 @@ void Server::Acceptor::on_event(uint32_t) {
       return;
     }
     if (server->opts_.reuseport_accept) {
+      server->assigned_[size_t(worker->index())].fetch_add(1, std::memory_order_relaxed);
       worker->adopt_here(c);
     } else {
-      size_t k = server->rr_.fetch_add(1, std::memory_order_relaxed) % server->workers_.size();
-      Worker* w = server->workers_[k].get();
+      Worker* w = server->pick_worker(c);
       if (w == worker) w->adopt_here(c);
       else w->adopt(c);
     }

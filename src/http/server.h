@@ -135,6 +135,9 @@ struct ServerOptions {
   // 60 s by default); 0 disables.
   int idle_timeout_ms = 60000;
   size_t max_connections = 0;  // per replica; 0 = unlimited (bounded by RLIMIT_NOFILE)
+  // Steer each accepted connection to a worker in the L3 domain where its packets arrive
+  // (SO_INCOMING_CPU), when workers are pinned; otherwise plain round-robin.
+  bool steer_l3 = true;
 };
 
 // Per-worker stage timings (ns) collected with --profile; read after the workers stop.
@@ -205,6 +208,7 @@ class Server {
   const ServerOptions& options() const { return opts_; }
   bool draining() const { return draining_.load(std::memory_order_relaxed); }
   uint64_t total_requests() const;
+  bool steering() const { return !domain_workers_.empty(); }
   size_t open_connections() const { return open_.load(std::memory_order_relaxed); }
   // JSON summary of the --profile histograms (call after join()).
   std::string profile_json() const;
@@ -225,6 +229,12 @@ class Server {
   std::atomic<uint64_t> rr_{0};
   std::atomic<size_t> open_{0};
   int port_ = 0;
+  // L3-domain steering state (built in the constructor from opts_.cpus).
+  Worker* pick_worker(int fd);
+  std::vector<std::pair<int, std::vector<size_t>>> domain_workers_;  // (l3 id, worker indices)
+  std::unique_ptr<std::atomic<uint32_t>[]> domain_rr_;
+  std::unique_ptr<std::atomic<int32_t>[]> assigned_;  // live connections per worker
+  uint64_t steered_ = 0, unsteered_ = 0;
   friend class Worker;
 };
 

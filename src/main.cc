@@ -57,6 +57,7 @@ void usage() {
           "  --busy-poll-us N         spin up to N us in epoll before sleeping (default 0)\n"
           "  --idle-timeout-ms N      close keep-alive connections idle this long (default 60000, 0 = never)\n"
           "  --max-connections N      refuse connections beyond N per replica (default unlimited)\n"
+          "  --no-steer               plain round-robin accept (default: L3-domain steering when pinned)\n"
           "  --profile                per-stage latency histograms (recv/parse/handle/send), dumped at exit\n"
           "  --profile-out PATH       write the --profile JSON here (default: stderr)\n"
           "  --log-level L            debug|info|warn|error|off (default info)\n"
@@ -124,6 +125,7 @@ int main(int argc, char** argv) {
     else if (a == "--port-file") port_file = val("--port-file");
     else if (a == "--busy-poll-us") so.busy_poll_us = atoi(val("--busy-poll-us").c_str());
     else if (a == "--profile") so.profile = true;
+    else if (a == "--no-steer") so.steer_l3 = false;
     else if (a == "--idle-timeout-ms") so.idle_timeout_ms = atoi(val("--idle-timeout-ms").c_str());
     else if (a == "--max-connections") so.max_connections = size_t(atol(val("--max-connections").c_str()));
     else if (a == "--profile-out") profile_out = val("--profile-out");
@@ -216,7 +218,7 @@ int main(int argc, char** argv) {
 
   LOG_INFO("hola listening on %s:%d (workers=%d, cpus=%s, accept=%s, tracing=%s, aloha=%s)", so.host.c_str(),
            server.port(), threads, cpus.empty() ? "unpinned" : format_cpu_list(cpus).c_str(),
-           so.reuseport_accept ? "reuseport" : "rr",
+           so.reuseport_accept ? "reuseport" : (server.steering() ? "rr+l3-steering" : "rr"),
            !to.enabled ? "off" : (to.collector_url.empty() ? "on (no collector: spans dropped)" : to.collector_url.c_str()),
            chainer.full_url().c_str());
   if (!port_file.empty()) {
