@@ -1,0 +1,69 @@
+"""Core planning for replicas and load generators (hola_amd/utils/cpu.py) on a mocked
+2-socket EPYC topology: 8-core L3 domains, SMT siblings at +128, 16-CPU cgroup quota."""
+import pytest
+
+from hola_amd.utils import cpu
+
+
+@pytest.fixture
+def epyc(monkeypatch):
+    cpus = list(range(256))
+    monkeypatch.setattr(cpu, "allowed_cpus", lambda: cpus)
+    monkeypatch.setattr(cpu, "cgroup_cpu_quota", lambda: 16.0)
+    monkeypatch.setattr(cpu, "physical_cores", lambda cpus=None: list(range(128)))
+    monkeypatch.setattr(cpu, "l3_domain", lambda c: (c % 128) // 8)
+    monkeypatch.setattr(cpu, "siblings", lambda c: [c % 128, c % 128 + 128])
+    busy = {c: 0.0 for c in cpus}
+    monkeypatch.setattr(cpu, "cpu_busy", lambda interval=0.3: busy)
+    return busy
+
+
+def test_parse_format_roundtrip():
+    assert cpu.parse_cpu_list("0-3,8,10-11") == [0, 1, 2, 3, 8, 10, 11]
+    assert cpu.format_cpu_list([11, 0, 1, 2, 3, 8, 10]) == "0-3,8,10-11"
+
+
+def test_budget_from_quota(epyc):
+    assert cpu.cpu_budget() == 16
+
+
+def test_plan_node_disjoint_whole_domains(epyc):
+    plans = cpu.plan_node(2)
+    assert [len(p) for p in plans] == [8, 8]
+    assert not set(plans[0]) & set(plans[1])
+    for p in plans:
+        assert len({cpu.l3_domain(c) for c in p}) == 1  # a rank fits one L3 domain
+
+
+def test_plan_node_avoids_busy_domains(epyc):
+    for c in range(0, 8):
+        epyc[c] = 1.0  # another tenant saturates domain 0
+    plans = cpu.plan_node(1)
+    assert all(cpu.l3_domain(c) != 0 for c in plans[0])
+
+
+def test_split_pairs_server_and_loadgen_per_domain(epyc):
+    cores = list(range(0, 16))  # domains 0 and 1
+    srv, lg = cpu.split_server_loadgen(cores, 8)
+    assert len(srv) == len(lg) == 8 and not set(srv) & set(lg)
+    assert [cpu.l3_domain(c) for c in srv] == [cpu.l3_domain(c) for c in lg]
+
+
+def test_cross_rank_loadgen_sits_with_target_replica(epyc):
+    plans = cpu.plan_replicas_with_loadgen(2, per_rank=16)  # pretend 32 CPUs
+    n = 2
+    for r, p in enumerate(plans):
+        for t, c in enumerate(p["loadgen"]):
+            target = (t + r) % n
+            assert cpu.l3_domain(c) in {cpu.l3_domain(x) for x in plans[target]["server"]}
+    used = [c for p in plans for c in p["server"] + p["loadgen"]]
+    assert len(used) == len(set(used)) == 32
+
+
+def test_scaling_plan_places_threads_with_replicas(epyc, monkeypatch):
+    from hola_amd.parallel import scaling
+
+    p = scaling.plan(4, 16, 0.5, 0)
+    assert len(p["replicas"]) == 4
+    for t, c in enumerate(p["loadgen"]):
+        assert cpu.l3_domain(c) in {cpu.l3_domain(x) for x in p["replicas"][t % 4]}
