@@ -7,6 +7,8 @@
 //
 // Modes:
 //   --duration S [--warmup S]   timed run, prints one JSON line (rps, p50/p90/p99/p99.9)
+//   --duration S --rate R       open loop at R req/s total (wrk2-style): latency counted from
+//                               each request's intended send time (no coordinated omission)
 //   --control                   stdin protocol used by bench.py:
 //        run <R>     every connection completes exactly R requests; replies
 //                    {"elapsed_ns":..,"requests":..,"errors":..}
@@ -21,6 +23,7 @@
 #include <signal.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -61,6 +64,7 @@ struct Options {
   int target_offset = 0;
   std::vector<std::string> extra_headers;
   int busy_poll_us = 0;
+  double rate = 0;  // --rate: open-loop total req/s (wrk2-style, latency from intended time)
 };
 
 struct Conn {
@@ -72,6 +76,8 @@ struct Conn {
   int64_t t0 = 0;
   int64_t quota = 0;  // remaining requests in control mode
   bool busy = false;
+  int64_t next_due = 0;   // --rate: intended send time of the next request
+  int64_t intended = 0;   // --rate: intended send time of the in-flight request
 };
 
 struct ThreadState {
@@ -194,10 +200,36 @@ void thread_main(ThreadState* ts, const Options* o) {
       if (!send_req(c.get())) ++ts->errors;
     }
   };
-  if (!control) {
+  // --rate (open loop): connection k of this thread sends every `interval` ns on a fixed
+  // schedule; latency is measured from the *intended* send time, so a stalled server is
+  // charged for the requests it delayed (no coordinated omission).
+  const bool rate_mode = !control && o->rate > 0;
+  const int64_t interval = rate_mode ? int64_t(double(o->connections) * 1e9 / o->rate) : 0;
+  if (rate_mode) {
+    int64_t t0 = mono_ns();
+    size_t k = 0;
+    for (auto& c : ts->conns) {
+      c->quota = INT64_MAX;
+      c->next_due = t0 + interval * int64_t(k++) / int64_t(ts->conns.size());
+    }
+  } else if (!control) {
     for (auto& c : ts->conns) c->quota = INT64_MAX;
     start_all();
   }
+  auto send_due = [&](int64_t now) -> int64_t {  // returns ns until the next due send
+    int64_t wait = INT64_MAX;
+    for (auto& c : ts->conns) {
+      if (c->busy) continue;
+      if (c->next_due <= now) {
+        c->intended = c->next_due;
+        c->next_due += interval;
+        if (!send_req(c.get())) ++ts->errors;
+      } else {
+        wait = std::min(wait, c->next_due - now);
+      }
+    }
+    return wait;
+  };
 
   epoll_event evs[256];
   while (!g_stop.load(std::memory_order_relaxed)) {
@@ -208,7 +240,16 @@ void thread_main(ThreadState* ts, const Options* o) {
         n = epoll_wait(ts->epfd, evs, 256, 0);
       } while (n == 0 && mono_ns() < until);
     }
-    if (n == 0) n = epoll_wait(ts->epfd, evs, 256, control ? -1 : 5);
+    if (n == 0) {
+      if (rate_mode) {
+        int64_t wait = send_due(mono_ns());
+        if (wait > 5000000) wait = 5000000;
+        timespec tmo{0, wait == INT64_MAX ? 5000000 : long(wait)};
+        n = epoll_pwait2(ts->epfd, evs, 256, &tmo, nullptr);
+      } else {
+        n = epoll_wait(ts->epfd, evs, 256, control ? -1 : 5);
+      }
+    }
     int64_t now = mono_ns();
     if (!control) {
       if (!ts->recording && now >= warm_end) {
@@ -275,7 +316,7 @@ void thread_main(ThreadState* ts, const Options* o) {
         ++run_errors;
         close = true;
       } else {
-        int64_t lat = mono_ns() - c->t0;
+        int64_t lat = mono_ns() - (rate_mode ? c->intended : c->t0);
         // (the histogram is only read between control runs / after the run: no lock)
         if (ts->recording) {
           ts->hist.add(uint64_t(lat));
@@ -309,8 +350,10 @@ void thread_main(ThreadState* ts, const Options* o) {
           continue;
         }
       }
+      if (rate_mode) continue;  // the schedule decides when this connection sends next
       if (!send_req(c)) ++ts->errors;
     }
+    if (rate_mode) send_due(mono_ns());
   }
 }
 
@@ -385,6 +428,7 @@ int main(int argc, char** argv) {
     else if (a == "--target-offset") o.target_offset = atoi(val().c_str());
     else if (a == "--header" || a == "-H") o.extra_headers.push_back(val());
     else if (a == "--busy-poll-us") o.busy_poll_us = atoi(val().c_str());
+    else if (a == "--rate" || a == "-R") o.rate = atof(val().c_str());
     else {
       fprintf(stderr,
               "usage: hola_loadgen --targets h:p[,h:p..] -c CONNS -t THREADS [--cpu-list L] [--path P]\n"
@@ -440,8 +484,9 @@ int main(int argc, char** argv) {
     uint64_t completed = 0;
     for (auto& t : ts) completed += t->completed;
     double rps = double(completed) / o.duration_s;
-    printf("{\"mode\":\"duration\",\"duration_s\":%.3f,\"connections\":%d,\"threads\":%d,\"targets\":%zu,\"rps\":%.1f,\"latency\":%s}\n",
-           o.duration_s, o.connections, o.threads, o.targets.size(), rps, s.c_str());
+    printf("{\"mode\":\"%s\",\"duration_s\":%.3f,\"connections\":%d,\"threads\":%d,\"targets\":%zu,\"target_rate\":%.1f,\"rps\":%.1f,\"latency\":%s}\n",
+           o.rate > 0 ? "open-loop" : "duration", o.duration_s, o.connections, o.threads, o.targets.size(), o.rate, rps,
+           s.c_str());
     return 0;
   }
 

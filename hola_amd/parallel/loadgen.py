@@ -105,13 +105,16 @@ class ControlledLoadgen:
 
 def run_duration(targets: list[tuple[str, int]], connections: int, threads: int, duration_s: float,
                  warmup_s: float = 1.0, cpu_list: str | None = None, path: str = "/api/hola",
-                 timeout: float | None = None) -> dict:
-    """wrk-style timed run; returns the loadgen's JSON summary."""
+                 timeout: float | None = None, rate: float = 0.0) -> dict:
+    """wrk-style timed run (closed loop), or wrk2-style open loop at `rate` req/s with latency
+    measured from intended send times; returns the loadgen's JSON summary."""
     cmd = [str(binary("hola_loadgen")), "--targets", ",".join(f"{h}:{p}" for h, p in targets),
            "-c", str(connections), "-t", str(threads), "--path", path, "--duration", str(duration_s),
            "--warmup", str(warmup_s)]
     if cpu_list:
         cmd += ["--cpu-list", cpu_list]
+    if rate > 0:
+        cmd += ["--rate", str(rate)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout or duration_s + warmup_s + 60)
     if r.returncode != 0:
         raise RuntimeError(f"loadgen failed: {r.stderr}")

@@ -105,3 +105,13 @@ def test_scaling_harness_smoke():
     assert [r["replicas"] for r in lines] == [1, 2]
     assert all(r["rps"] > 0 and r["errors"] == 0 for r in lines)
     assert lines[1]["connections"] == 16
+
+
+def test_open_loop_rate_mode(hola):
+    from hola_amd.parallel.loadgen import run_duration
+
+    s = hola(threads=1)
+    res = run_duration([("127.0.0.1", s.port)], 8, 1, 1.0, 0.3, rate=5000)
+    assert res["mode"] == "open-loop"
+    assert 4500 <= res["rps"] <= 5500
+    assert res["latency"]["errors"] == 0 and res["latency"]["p50_ns"] > 0
