@@ -205,6 +205,7 @@ int main(int argc, char** argv) {
   metrics::Prometheus prom(threads, app::HolaApp::kNumRoutes);
   prom.set_tracer(to.enabled ? &tracer : nullptr);
   prom.set_command(&chainer.command());
+  prom.set_config_reloads([&cfg] { return cfg.reloads(); });
   app.set_prometheus(&prom);
 
   cfg.start([&](const config::Snapshot& s) {

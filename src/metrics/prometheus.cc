@@ -22,12 +22,13 @@ std::string Prometheus::render(http::Server* server) const {
     o += "\"} " + std::to_string(n) + "\n";
   }
   if (server) {
-    uint64_t acc = 0, closed = 0, perr = 0, bin = 0, bout = 0, req = 0;
+    uint64_t acc = 0, closed = 0, perr = 0, bin = 0, bout = 0, req = 0, rej = 0;
     for (size_t i = 0; i < server->num_workers(); ++i) {
       auto& s = server->worker(i).stats();
       acc += s.accepted.load(std::memory_order_relaxed);
       closed += s.closed.load(std::memory_order_relaxed);
       perr += s.parse_errors.load(std::memory_order_relaxed);
+      rej += s.rejected.load(std::memory_order_relaxed);
       bin += s.bytes_in.load(std::memory_order_relaxed);
       bout += s.bytes_out.load(std::memory_order_relaxed);
       req += s.requests.load(std::memory_order_relaxed);
@@ -36,6 +37,7 @@ std::string Prometheus::render(http::Server* server) const {
     o += "# TYPE hola_connections_accepted_total counter\nhola_connections_accepted_total " + std::to_string(acc) + "\n";
     o += "# TYPE hola_connections_open gauge\nhola_connections_open " + std::to_string(acc - closed) + "\n";
     o += "# TYPE hola_parse_errors_total counter\nhola_parse_errors_total " + std::to_string(perr) + "\n";
+    o += "# TYPE hola_connections_rejected_total counter\nhola_connections_rejected_total " + std::to_string(rej) + "\n";
     o += "# TYPE hola_bytes_in_total counter\nhola_bytes_in_total " + std::to_string(bin) + "\n";
     o += "# TYPE hola_bytes_out_total counter\nhola_bytes_out_total " + std::to_string(bout) + "\n";
     o += "# TYPE hola_workers gauge\nhola_workers " + std::to_string(server->num_workers()) + "\n";
@@ -60,7 +62,7 @@ std::string Prometheus::render(http::Server* server) const {
     o += "# TYPE hola_hystrix_circuit_open gauge\nhola_hystrix_circuit_open{command=\"" + s.name + "\"} " +
          (s.circuit_open ? "1" : "0") + "\n";
   }
-  if (reloads_) o += "# TYPE hola_config_reloads_total counter\nhola_config_reloads_total " + std::to_string(reloads_->load()) + "\n";
+  if (reloads_) o += "# TYPE hola_config_reloads_total counter\nhola_config_reloads_total " + std::to_string(reloads_()) + "\n";
   return o;
 }
 

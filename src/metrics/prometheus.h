@@ -4,6 +4,7 @@
 #pragma once
 #include <atomic>
 #include <cstdint>
+#include <functional>
 #include <memory>
 #include <string>
 #include <vector>
@@ -29,7 +30,7 @@ class Prometheus {
   }
   void set_tracer(tracing::Tracer* t) { tracer_ = t; }
   void set_command(resilience::Command* c) { cmd_ = c; }
-  void set_config_reloads(std::atomic<uint64_t>* r) { reloads_ = r; }
+  void set_config_reloads(std::function<uint64_t()> f) { reloads_ = std::move(f); }
   std::string render(http::Server* server) const;
 
  private:
@@ -40,7 +41,7 @@ class Prometheus {
   std::unique_ptr<Counter[]> counts_;
   tracing::Tracer* tracer_ = nullptr;
   resilience::Command* cmd_ = nullptr;
-  std::atomic<uint64_t>* reloads_ = nullptr;
+  std::function<uint64_t()> reloads_;
 };
 
 }  // namespace hola::metrics

@@ -142,3 +142,26 @@ def test_no_file_descriptor_leak(hola, tmp_path):
     time.sleep(0.1)
     n1 = len(os.listdir(f"/proc/{pid}/fd"))
     assert n1 <= n0 + 2, (n0, n1)
+
+
+def test_hystrix_config_file_hot_reload(hola, tmp_path):
+    """Archaius re-reads config.properties; here the watcher re-applies Hystrix settings."""
+    from hola_amd.testing.fakes import FakeAloha
+
+    hc = tmp_path / "config.properties"
+    hc.write_text("hystrix.command.default.execution.isolation.thread.timeoutInMilliseconds=2000\n")
+    with FakeAloha(mode="slow", delay_s=0.5) as aloha:
+        s = hola(args=["--aloha-url", aloha.url, "--hystrix-config", str(hc), "--feign-log", "none"])
+        t0 = time.monotonic()
+        st, _, body = s.get("/api/hola-chaining")
+        assert b"Aloha mai" in body and time.monotonic() - t0 >= 0.45  # 2000 ms budget: no timeout
+        hc.write_text("hystrix.command.default.execution.isolation.thread.timeoutInMilliseconds=100\n")
+        deadline = time.monotonic() + 3
+        while time.monotonic() < deadline:
+            _, _, body = s.get("/api/hola-chaining")
+            if b"fallback" in body:
+                break
+        assert b"Aloha response (fallback)" in body
+        metrics = s.get("/metrics")[2].decode()
+        reloads = int(metrics.split("hola_config_reloads_total ")[1].split()[0])
+        assert reloads >= 1

@@ -218,3 +218,27 @@ def test_max_connections(hola):
             c.close()
     time.sleep(0.1)
     assert s.get("/api/health")[0] == 200  # capacity returns once connections close
+
+
+def test_many_concurrent_connections(hola):
+    """1000 simultaneous keep-alive connections on 2 workers, each served in turn."""
+    s = hola(threads=2, env={"HOSTNAME": "h"})
+    socks = [socket.create_connection(("127.0.0.1", s.port), timeout=5) for _ in range(1000)]
+    try:
+        for c in socks:
+            c.sendall(b"GET /api/hola HTTP/1.1\r\nHost: x\r\n\r\n")
+        ok = 0
+        for c in socks:
+            data = b""
+            while not data.endswith(b"Hola de h"):
+                chunk = c.recv(4096)
+                if not chunk:
+                    break
+                data += chunk
+            ok += data.startswith(b"HTTP/1.1 200 OK")
+        assert ok == 1000
+        _, _, m = s.get("/metrics")
+        assert b"hola_connections_open 10" in m  # 1000 + the metrics connection itself
+    finally:
+        for c in socks:
+            c.close()

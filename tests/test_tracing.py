@@ -163,3 +163,19 @@ def test_span_json_v1(native):
     keys = {b["key"]: b["value"] for b in sp["binaryAnnotations"]}
     assert keys["http.status_code"] == "500"
     assert sp["annotations"][0]["endpoint"] == {"serviceName": "hola", "ipv4": "127.0.0.1", "port": 8080}
+
+
+def test_sample_rate_zero_reports_nothing(hola, zipkin):
+    s = hola(args=["--zipkin-url", zipkin.url, "--trace-sample-rate", "0"])
+    for _ in range(20):
+        s.get("/api/hola")
+    time.sleep(1.3)
+    assert zipkin.spans() == []
+
+
+def test_sample_rate_half(hola, zipkin):
+    s = hola(args=["--zipkin-url", zipkin.url, "--trace-sample-rate", "0.5"], threads=1)
+    for _ in range(400):
+        s.get("/api/hola")
+    spans = zipkin.wait_for(lambda sp: len(sp) >= 120, timeout=5)
+    assert 120 <= len(spans) <= 280
