@@ -163,5 +163,5 @@ def test_hystrix_config_file_hot_reload(hola, tmp_path):
                 break
         assert b"Aloha response (fallback)" in body
         metrics = s.get("/metrics")[2].decode()
-        reloads = int(metrics.split("hola_config_reloads_total ")[1].split()[0])
+        reloads = int(next(l for l in metrics.splitlines() if l.startswith("hola_config_reloads_total ")).split()[1])
         assert reloads >= 1
