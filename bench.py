@@ -39,10 +39,11 @@ BASELINE_VALUE = None  # the reference publishes no numbers
 def parse_args():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1, help="replicas on this node (one per rank)")
-    ap.add_argument("--steps", type=int, default=20)
+    # Defaults give a ~30 s timed region at ~4M req/s (BASELINE configs 3/4 are 30 s wrk runs).
+    ap.add_argument("--steps", type=int, default=40)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--connections", type=int, default=64, help="keep-alive connections per replica")
-    ap.add_argument("--reqs-per-conn", type=int, default=1000, help="requests per connection per step")
+    ap.add_argument("--reqs-per-conn", type=int, default=50000, help="requests per connection per step")
     ap.add_argument("--cores", type=int, default=0, help="host cores per replica (server + load generator)")
     ap.add_argument("--server-threads", type=int, default=0, help="0 = half of the rank's cores")
     ap.add_argument("--base-port", type=int, default=int(os.environ.get("HOLA_BENCH_PORT", "18400")))
