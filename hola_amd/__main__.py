@@ -6,6 +6,7 @@
   scaling [...]                              replica scaling curve (hola_amd.parallel.scaling)
   bench [...]                                the headline benchmark (bench.py)
   info                                       host CPU topology / quota / plan for this node
+  units --replicas N --out DIR               systemd units: N pinned replicas + proxy on :8080
 
 The local equivalents of the reference's `mvn wildfly-swarm:run` (Readme.md:13) and
 `mvn clean package docker:build fabric8:json fabric8:apply` (Readme.md:24) are
@@ -102,6 +103,20 @@ def main(argv: list[str] | None = None) -> int:
         return subprocess.call([sys.executable, str(root / "bench.py"), *rest])
     if cmd == "info":
         return _info()
+    if cmd == "units":
+        from hola_amd.deploy import write_units
+
+        ap = argparse.ArgumentParser(prog="python -m hola_amd units")
+        ap.add_argument("--replicas", type=int, default=8)
+        ap.add_argument("--out", required=True)
+        ap.add_argument("--prefix", default="/opt/hola")
+        ap.add_argument("--port", type=int, default=8080)
+        ap.add_argument("--cores-per-replica", type=int, default=0)
+        a = ap.parse_args(rest)
+        for p in write_units(a.out, replicas=a.replicas, prefix=a.prefix, public_port=a.port,
+                             cores_per_replica=a.cores_per_replica or None):
+            print(p)
+        return 0
     print(f"unknown command {cmd!r}\n{__doc__}", file=sys.stderr)
     return 2
 

@@ -49,6 +49,23 @@ def _sources_newer_than(target: Path) -> bool:
     return (REPO / "CMakeLists.txt").stat().st_mtime > t
 
 
+def _drop_stale_cache(bdir: Path) -> None:
+    """A build tree copied to another path (e.g. a repo snapshot on a GPU box, where
+    /root/repo is a symlink) keeps the old absolute paths in CMakeCache.txt and CMake
+    refuses to reuse it. Reconfigure from scratch in that case (objects are rebuilt)."""
+    cache = bdir / "CMakeCache.txt"
+    if not cache.exists():
+        return
+    recorded = None
+    for line in cache.read_text(errors="replace").splitlines():
+        if line.startswith("CMAKE_CACHEFILE_DIR:"):
+            recorded = line.split("=", 1)[1].strip()
+            break
+    if recorded is None or recorded != str(bdir):
+        shutil.rmtree(bdir / "CMakeFiles", ignore_errors=True)
+        cache.unlink(missing_ok=True)
+
+
 def build(preset: str = "release", jobs: int | None = None, quiet: bool = True) -> Path:
     """Configures and builds `preset` in-tree; returns the build directory.
 
@@ -67,6 +84,7 @@ def build(preset: str = "release", jobs: int | None = None, quiet: bool = True) 
         fcntl.flock(lock, fcntl.LOCK_EX)
         try:
             out = subprocess.DEVNULL if quiet else None
+            _drop_stale_cache(bdir)
             if not (bdir / "CMakeCache.txt").exists():
                 cmd = ["cmake", "-S", str(REPO), "-B", str(bdir), *gen, *PRESETS[preset],
                        f"-DPython3_EXECUTABLE={sys.executable}"]

@@ -63,3 +63,22 @@ def test_dockerfile_contract():
         assert k in df
     for path in ("CMakeLists.txt", "src", "assets", "conf/config.properties", "translation.properties"):
         assert (ROOT / path).exists()
+
+
+def test_systemd_units_render(tmp_path):
+    from hola_amd.deploy import write_units
+    from hola_amd.utils.cpu import parse_cpu_list
+
+    paths = write_units(tmp_path, replicas=2)
+    names = sorted(p.name for p in paths)
+    assert names == ["hola-replica0.service", "hola-replica1.service", "hola-rrproxy.service", "hola.target"]
+    r0 = (tmp_path / "hola-replica0.service").read_text()
+    r1 = (tmp_path / "hola-replica1.service").read_text()
+    cpus0 = r0.split("--cpu-list ")[1].split()[0]
+    cpus1 = r1.split("--cpu-list ")[1].split()[0]
+    assert not set(parse_cpu_list(cpus0)) & set(parse_cpu_list(cpus1))  # disjoint pinning
+    assert f"CPUAffinity={cpus0.replace(',', ' ')}" in r0
+    assert "Restart=always" in r0 and "--port 18080" in r0 and "--port 18081" in r1
+    px = (tmp_path / "hola-rrproxy.service").read_text()
+    assert "--port 8080" in px and "--backends 127.0.0.1:18080,127.0.0.1:18081" in px
+    assert "hola-replica1.service" in (tmp_path / "hola.target").read_text()
