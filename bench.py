@@ -78,14 +78,18 @@ def main() -> int:
     # ---- core plan: disjoint physical cores per rank, quietest L3 domains first (computed
     # once on rank 0 and broadcast, since load measurements differ between processes);
     # within a rank, server worker t and loadgen thread t share an L3 domain. ----
-    plan = [plan_replicas_with_loadgen(local_world, a.cores or None, a.server_threads,
-                                       avoid_busy=not a.no_avoid_busy)] if rank == 0 else [None]
+    plan = [None]
+    if rank == 0:
+        plan = [{"cores": plan_replicas_with_loadgen(local_world, a.cores or None, a.server_threads,
+                                                     avoid_busy=not a.no_avoid_busy),
+                 "base_port": _free_port_block(a.base_port, local_world)}]
     if dist:
         dist.broadcast_object_list(plan, src=0)
-    server_cpus, load_cpus = plan[0][local_rank]["server"], plan[0][local_rank]["loadgen"]
+    server_cpus, load_cpus = plan[0]["cores"][local_rank]["server"], plan[0]["cores"][local_rank]["loadgen"]
     s_threads = len(server_cpus)
-    port = a.base_port + local_rank
-    targets = [("127.0.0.1", a.base_port + i) for i in range(local_world)]
+    base_port = plan[0]["base_port"]
+    port = base_port + local_rank
+    targets = [("127.0.0.1", base_port + i) for i in range(local_world)]
 
     env = {"HOSTNAME": f"replica-{rank}"}
     args = ["--no-tracing"] if a.no_tracing else []
@@ -190,6 +194,28 @@ def main() -> int:
         dist.barrier()
         dist.destroy_process_group()
     return 0
+
+
+def _free_port_block(start: int, n: int) -> int:
+    """First base >= start such that base..base+n-1 can all be bound on 127.0.0.1."""
+    import socket
+
+    base = start
+    for _ in range(200):
+        socks = []
+        try:
+            for i in range(n):
+                sk = socket.socket()
+                sk.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+                sk.bind(("127.0.0.1", base + i))
+                socks.append(sk)
+            return base
+        except OSError:
+            base += n + 7
+        finally:
+            for sk in socks:
+                sk.close()
+    return start
 
 
 def _proc_cpu_s(pid: int) -> float:
