@@ -172,8 +172,10 @@ def main() -> int:
             "errors": sum(g["errors"] for g in gathered),
             "non2xx": sum(g["non2xx"] for g in gathered),
             "config": {
-                "model": "hola GET /api/hola (native C++ replica, default greeting, tracing "
-                         + ("off" if a.no_tracing else "on") + ")",
+                "model": "hola GET /api/hola (native C++ replica, default greeting, "
+                         + ("tracing off" if a.no_tracing else
+                            "B3 tracing on without a collector: spans counted and dropped, as Brave "
+                            "does with ZIPKIN_SERVER_URL unset") + ")",
                 "global_batch": a.connections * world,
                 "seq_len": 1,
                 "parallelism": f"replicas{world}",
