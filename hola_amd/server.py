@@ -29,8 +29,9 @@ class HolaProcess:
         self.threads = threads
         self.cpu_list = cpu_list
         self.exe = exe or binary("hola", preset)
-        base = dict(os.environ) if inherit_env else {
-            k: v for k, v in os.environ.items() if k in ("PATH", "LANG", "LC_ALL", "TMPDIR", "LD_LIBRARY_PATH")}
+        keep = ("PATH", "LANG", "LC_ALL", "TMPDIR", "LD_LIBRARY_PATH", "TSAN_OPTIONS", "ASAN_OPTIONS",
+                "UBSAN_OPTIONS", "LSAN_OPTIONS")
+        base = dict(os.environ) if inherit_env else {k: v for k, v in os.environ.items() if k in keep}
         if not inherit_env:
             base.pop("HOSTNAME", None)
         base.update(env or {})

@@ -51,6 +51,9 @@ void usage() {
           "  --aloha-url URL          downstream service (default http://aloha:8080/)\n"
           "  --feign-log basic|none   outbound call logging (default basic)\n"
           "  --hystrix-stream-max N   max /hystrix.stream subscribers (default 5)\n"
+          "  --hystrix-timeout-ms N | --hystrix-request-volume N | --hystrix-error-pct N |\n"
+          "  --hystrix-sleep-window-ms N | --hystrix-pool-size N\n"
+          "                           shorthands for -Dhystrix.command.default.* / threadpool.default.*\n"
           "  --config-poll-ms N       config re-check interval (default 1000)\n"
           "  --drain-ms N             graceful shutdown drain budget (default 5000)\n"
           "  --port-file PATH         write the bound port here once listening\n"
@@ -117,6 +120,15 @@ int main(int argc, char** argv) {
     else if (a == "--zipkin-v2") to.v2 = true;
     else if (a == "--trace-sample-rate") to.sample_rate = atof(val("--trace-sample-rate").c_str());
     else if (a == "--no-tracing") no_tracing = true;
+    else if (a == "--hystrix-timeout-ms")
+      sysprops["hystrix.command.default.execution.isolation.thread.timeoutInMilliseconds"] = val(a.c_str());
+    else if (a == "--hystrix-request-volume")
+      sysprops["hystrix.command.default.circuitBreaker.requestVolumeThreshold"] = val(a.c_str());
+    else if (a == "--hystrix-error-pct")
+      sysprops["hystrix.command.default.circuitBreaker.errorThresholdPercentage"] = val(a.c_str());
+    else if (a == "--hystrix-sleep-window-ms")
+      sysprops["hystrix.command.default.circuitBreaker.sleepWindowInMilliseconds"] = val(a.c_str());
+    else if (a == "--hystrix-pool-size") sysprops["hystrix.threadpool.default.coreSize"] = val(a.c_str());
     else if (a == "--aloha-url") alo.url = val("--aloha-url");
     else if (a == "--feign-log") alo.feign_log_basic = val("--feign-log") == "basic";
     else if (a == "--hystrix-stream-max") stream_max = atoi(val("--hystrix-stream-max").c_str());

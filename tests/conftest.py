@@ -8,6 +8,22 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
 
 
+def pytest_sessionstart(session):
+    # HOLA_SANITIZER=tsan|asan: build that preset and run every integration test against it
+    # (SURVEY.md §5.2), e.g. `HOLA_SANITIZER=asan pytest tests/test_contract.py tests/test_chaining.py`.
+    san = os.environ.get("HOLA_SANITIZER")
+    if san:
+        from hola_amd.native import build, build_dir
+
+        build(san)
+        os.environ["HOLA_BIN_DIR"] = str(build_dir(san))
+        if san == "tsan":
+            os.environ.setdefault("TSAN_OPTIONS", "halt_on_error=1 exitcode=66")
+        else:
+            os.environ.setdefault("ASAN_OPTIONS", "detect_leaks=1 halt_on_error=1 exitcode=66")
+            os.environ.setdefault("UBSAN_OPTIONS", "halt_on_error=1 print_stacktrace=1")
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: runs on the MI355X box (host-side perf/bench checks)")
     config.addinivalue_line("markers", "slow: longer integration tests")

@@ -149,3 +149,11 @@ def test_feign_basic_logging(hola, aloha):
     log = s.log()
     assert "[AlohaService#aloha()] ---> GET " in log and "/api/aloha-chaining HTTP/1.1" in log
     assert "<--- HTTP/1.1 200" in log
+
+
+def test_hystrix_flag_shorthands(hola, aloha):
+    aloha.set_mode("slow", delay_s=1.0)
+    s = hola(args=["--aloha-url", aloha.url, "--hystrix-timeout-ms", "120", "--feign-log", "none"])
+    t0 = time.monotonic()
+    assert chain(s)[1:] == [FALLBACK]
+    assert time.monotonic() - t0 < 0.6
