@@ -201,7 +201,9 @@ Parse parse_request(const char* buf, size_t len, Request* req, int* status) {
         if (iequals(name, "host")) req->host = value;
         break;
       case 6:
-        if (iequals(name, "accept")) {
+        if (iequals(name, "expect")) {
+          req->expect_continue = iequals(value, "100-continue");
+        } else if (iequals(name, "accept")) {
           // Multiple Accept fields are equivalent to one comma-joined field; keep the first
           // and let the negotiation treat a second one conservatively (rare in practice).
           if (!req->has_accept) req->accept = value;

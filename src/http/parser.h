@@ -27,6 +27,7 @@ struct Request {
   std::string_view b3_trace_id, b3_span_id, b3_parent_id, b3_sampled, b3_flags, b3_single;
   int64_t content_length = 0;
   bool chunked = false;
+  bool expect_continue = false;  // "Expect: 100-continue"
   size_t head_bytes = 0;  // bytes of request-line + headers + terminating blank line
 };
 

@@ -151,7 +151,17 @@ bool Connection::process(const char* data, size_t len, size_t* consumed) {
         off = len;
         break;
       }
-      if (len - off - total < size_t(r.content_length)) break;
+      if (len - off - total < size_t(r.content_length)) {
+        // RFC 9110 §10.1.1: a client waiting on "Expect: 100-continue" gets the interim
+        // response once, then sends the body.
+        if (r.expect_continue && !continue_sent_) {
+          static constexpr std::string_view k100 = "HTTP/1.1 100 Continue\r\n\r\n";
+          out_.append(k100.data(), k100.size());
+          continue_sent_ = true;
+        }
+        break;
+      }
+      continue_sent_ = false;
       total += size_t(r.content_length);
     }
     off += total;

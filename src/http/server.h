@@ -99,6 +99,7 @@ class Connection final : public EventLoop::Handler {
   bool want_write_ = false;
   bool reading_ = true;
   bool in_process_ = false;  // inside process(): batch writes instead of sending eagerly
+  bool continue_sent_ = false;  // "100 Continue" already sent for the pending request
   int holds_ = 0;
   int64_t last_active_ms_ = 0;
   std::function<void()> on_close_;

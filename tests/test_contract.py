@@ -242,3 +242,13 @@ def test_many_concurrent_connections(hola):
     finally:
         for c in socks:
             c.close()
+
+
+def test_expect_100_continue(hola):
+    s = hola()
+    with socket.create_connection(("127.0.0.1", s.port), timeout=3) as c:
+        c.sendall(b"POST /api/hola HTTP/1.1\r\nHost: x\r\nContent-Length: 4\r\nExpect: 100-continue\r\n\r\n")
+        assert c.recv(4096).startswith(b"HTTP/1.1 100 Continue\r\n\r\n")
+        c.sendall(b"abcd")
+        data = c.recv(4096)
+        assert data.startswith(b"HTTP/1.1 405")
