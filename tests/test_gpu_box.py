@@ -33,3 +33,20 @@ def test_bench_json_contract_on_host():
     assert out["errors"] == 0 and out["non2xx"] == 0
     assert out["value"] > 10000  # a pinned native replica on EPYC cores does far more than this
     assert out["p50_ms"] > 0 and out["p99_ms"] >= out["p50_ms"]
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_on_host():
+    """The multi-replica path (torchrun, gloo barriers, client-side round-robin across
+    replicas, cross-rank L3-aware load-generator placement) on the real host."""
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", "29517", str(ROOT / "bench.py"),
+                        "--gpus", "2", "--steps", "3", "--warmup", "1", "--reqs-per-conn", "500"],
+                       capture_output=True, text=True, timeout=600,
+                       env={**os.environ, "HOLA_BENCH_PORT": "18760"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "replicas2"
+    assert out["requests"] == 2 * 64 * 500 * 3
+    assert out["errors"] == 0 and out["non2xx"] == 0
+    assert set(out["config"]["cpu_map"]) == {"rank0", "rank1"}
