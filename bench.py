@@ -129,11 +129,13 @@ def main() -> int:
         elapsed = time.perf_counter() - t0
         cpu1 = (_proc_cpu_s(server.proc.pid), _proc_cpu_s(loadgen.proc.pid))
         st = loadgen.stats()
+        mem = server.memory_kb()
 
         local = {"elapsed": elapsed, "requests": reqs, "errors": errs, "hist": st.get("hist", ""),
                  "non2xx": st.get("non2xx", 0), "server_cpus": format_cpu_list(server_cpus),
                  "load_cpus": format_cpu_list(load_cpus),
-                 "server_cpu_s": cpu1[0] - cpu0[0], "loadgen_cpu_s": cpu1[1] - cpu0[1]}
+                 "server_cpu_s": cpu1[0] - cpu0[0], "loadgen_cpu_s": cpu1[1] - cpu0[1],
+                 "startup_ms": server.startup_ms, "rss_peak_kb": mem.get("VmHWM", 0)}
         if dist:
             gathered = [None] * world
             dist.all_gather_object(gathered, local)
@@ -169,6 +171,9 @@ def main() -> int:
             # host CPU time per request (user+sys, all threads) over the timed region
             "server_cpu_us_per_req": round(1e6 * sum(g["server_cpu_s"] for g in gathered) / max(1, total), 3),
             "loadgen_cpu_us_per_req": round(1e6 * sum(g["loadgen_cpu_s"] for g in gathered) / max(1, total), 3),
+            # replica footprint: exec -> listening, and peak resident memory (max over ranks)
+            "server_startup_ms": round(max(g["startup_ms"] or 0 for g in gathered), 1),
+            "server_rss_peak_mb": round(max(g["rss_peak_kb"] for g in gathered) / 1024.0, 1),
             "errors": sum(g["errors"] for g in gathered),
             "non2xx": sum(g["non2xx"] for g in gathered),
             "config": {

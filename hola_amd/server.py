@@ -38,6 +38,7 @@ class HolaProcess:
         self.env = base
         self.log_level = log_level
         self.proc: subprocess.Popen | None = None
+        self.startup_ms: float | None = None
         self._tmp = tempfile.TemporaryDirectory(prefix="hola-")
         self.stderr_path = stderr_path or os.path.join(self._tmp.name, "stderr.log")
 
@@ -56,6 +57,7 @@ class HolaProcess:
         if self.cpu_list:
             cmd += ["--cpu-list", self.cpu_list]
         self._stderr = open(self.stderr_path, "wb")
+        t0 = time.monotonic()
         self.proc = subprocess.Popen(cmd, env=self.env, stdout=subprocess.DEVNULL, stderr=self._stderr)
         deadline = time.monotonic() + timeout
         while time.monotonic() < deadline:
@@ -64,6 +66,7 @@ class HolaProcess:
             if os.path.exists(port_file):
                 try:
                     self.port = int(Path(port_file).read_text().strip())
+                    self.startup_ms = (time.monotonic() - t0) * 1000.0  # exec -> listening
                     break
                 except ValueError:
                     pass
@@ -76,6 +79,18 @@ class HolaProcess:
     def get(self, path: str, headers: dict | None = None, method: str = "GET", timeout: float = 5.0,
             body: bytes | None = None):
         return http_get("127.0.0.1", self.port, path, headers=headers, method=method, timeout=timeout, body=body)
+
+    def memory_kb(self) -> dict:
+        """VmRSS / VmHWM (peak) of the running server, in kB."""
+        out = {}
+        try:
+            for line in Path(f"/proc/{self.proc.pid}/status").read_text().splitlines():
+                if line.startswith(("VmRSS:", "VmHWM:")):
+                    k, v = line.split(":", 1)
+                    out[k] = int(v.split()[0])
+        except (OSError, ValueError, AttributeError):
+            pass
+        return out
 
     def log(self) -> str:
         try:

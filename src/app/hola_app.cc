@@ -38,7 +38,7 @@ struct HolaApp::WorkerCache {
   uint64_t date_version = ~0ull;
   std::shared_ptr<const Content> content;
   // [keep_alive][head]
-  Prepared hola[2][2], health[2][2], swagger[2][2], index[2][2], viewer[2][2];
+  Prepared hola[2][2], health[2][2], swagger[2][2], swagger_yaml[2][2], index[2][2], viewer[2][2];
   Prepared chaining_fallback[2][2];
   Prepared api_not_found[2], not_found[2][2], api_not_allowed[2], not_allowed[2], not_acceptable[2],
       api_options[2], static_options[2], server_error[2][2];
@@ -49,7 +49,7 @@ struct HolaApp::WorkerCache {
 const char* HolaApp::route_name(int r) {
   static const char* kNames[] = {"/api/hola", "/api/hola-chaining", "/api/health", "/api/swagger.json",
                                  "/", "/webjars/swagger-ui", "/hystrix.stream", "/metrics",
-                                 "/api/*(404)", "*(404)"};
+                                 "/api/*(404)", "*(404)", "/api/swagger.yaml"};
   return (r >= 0 && r < kNumRoutes) ? kNames[r] : "?";
 }
 
@@ -117,6 +117,7 @@ void HolaApp::refresh(http::Worker& w, WorkerCache& wc) {
     const char* date = w.date();
     wc.all.clear();
     const assets::Asset* swagger = assets::find("swagger.json");
+    const assets::Asset* swagger_yaml = assets::find("swagger.yaml");
     const assets::Asset* index = assets::find("index.html");
     const assets::Asset* viewer = assets::find("swagger-ui.html");
     std::string fallback_body;
@@ -164,6 +165,9 @@ void HolaApp::refresh(http::Worker& w, WorkerCache& wc) {
         sw.content_type = kJson;
         sw.body = swagger ? swagger->view() : std::string_view("{}");
         wc.swagger[ka][head] = build_response(sw, date);
+        sw.content_type = "application/yaml";
+        sw.body = swagger_yaml ? swagger_yaml->view() : std::string_view();
+        wc.swagger_yaml[ka][head] = build_response(sw, date);
         ResponseSpec ix = h;
         ix.cors = false;
         ix.content_type = "text/html;charset=UTF-8";
@@ -179,7 +183,8 @@ void HolaApp::refresh(http::Worker& w, WorkerCache& wc) {
         nf.body = kUndertowNotFound;
         wc.not_found[ka][head] = build_response(nf, date);
         for (auto* p : {&wc.hola[ka][head], &wc.server_error[ka][head], &wc.chaining_fallback[ka][head],
-                        &wc.health[ka][head], &wc.swagger[ka][head], &wc.index[ka][head], &wc.viewer[ka][head],
+                        &wc.health[ka][head], &wc.swagger[ka][head], &wc.swagger_yaml[ka][head], &wc.index[ka][head],
+                        &wc.viewer[ka][head],
                         &wc.not_found[ka][head]})
           wc.all.push_back(p);
       }
@@ -254,6 +259,7 @@ int route_of(std::string_view p) {
     if (path_is(rest, "/hola-chaining")) return HolaApp::kChaining;
     if (path_is(rest, "/health")) return HolaApp::kHealth;
     if (rest == "/swagger.json") return HolaApp::kSwagger;
+    if (rest == "/swagger.yaml") return HolaApp::kSwaggerYaml;
     return HolaApp::kApiNotFound;
   }
   if (p == "/" || p == "/index.html") return HolaApp::kIndex;
@@ -290,7 +296,8 @@ void HolaApp::on_request(http::Connection& c, const http::Request& r) {
     case kHola:
     case kHealth:
     case kChaining:
-    case kSwagger: {
+    case kSwagger:
+    case kSwaggerYaml: {
       if (m == Method::kOptions) {
         c.send(wc.api_options[ka].view());
         return;
@@ -299,8 +306,9 @@ void HolaApp::on_request(http::Connection& c, const http::Request& r) {
         c.send(wc.api_not_allowed[ka].view());
         return;
       }
-      std::string_view subtype = (route == kChaining || route == kSwagger) ? "json" : "plain";
-      std::string_view type = (route == kChaining || route == kSwagger) ? "application" : "text";
+      std::string_view subtype = route == kSwaggerYaml ? "yaml"
+                                 : (route == kChaining || route == kSwagger) ? "json" : "plain";
+      std::string_view type = (route == kChaining || route == kSwagger || route == kSwaggerYaml) ? "application" : "text";
       if (r.has_accept && !http::accepts(r.accept, type, subtype)) {
         c.send(wc.not_acceptable[ka].view());
         return;
@@ -317,6 +325,8 @@ void HolaApp::on_request(http::Connection& c, const http::Request& r) {
         c.send(wc.health[ka][head].view());
       } else if (route == kSwagger) {
         c.send(wc.swagger[ka][head].view());
+      } else if (route == kSwaggerYaml) {
+        c.send(wc.swagger_yaml[ka][head].view());
       } else {
         handle_chaining(c, r, wc, 0);
       }

@@ -78,7 +78,7 @@ class HolaApp final : public http::RequestHandler {
   // Route ids (also used for per-route metrics).
   enum Route : int {
     kHola = 0, kChaining, kHealth, kSwagger, kIndex, kViewer, kHystrix, kMetrics,
-    kApiNotFound, kNotFound, kNumRoutes
+    kApiNotFound, kNotFound, kSwaggerYaml, kNumRoutes
   };
   static const char* route_name(int r);
 

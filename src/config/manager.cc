@@ -1,5 +1,7 @@
 #include "config/manager.h"
 
+#include <cstdlib>
+
 #include "config/properties.h"
 #include "core/log.h"
 
@@ -26,6 +28,13 @@ std::shared_ptr<Snapshot> Manager::build(const FileWatcher::Contents& files) {
     if (f != files.end() && f->second) {
       PropertiesResult pr = parse_properties(*f->second);
       if (pr.ok) ds.values = pr.map;
+      // DeltaSpike property-file sources may override their own ordinal [lib-default].
+      auto o = ds.values.find("deltaspike_ordinal");
+      if (o != ds.values.end()) {
+        char* end = nullptr;
+        long v = strtol(o->second.c_str(), &end, 10);
+        if (end && *end == '\0' && !o->second.empty()) ds.ordinal = int(v);
+      }
     }
     sources.push_back(std::move(ds));
   }

@@ -165,3 +165,10 @@ def test_hystrix_config_file_hot_reload(hola, tmp_path):
         metrics = s.get("/metrics")[2].decode()
         reloads = int(next(l for l in metrics.splitlines() if l.startswith("hola_config_reloads_total ")).split()[1])
         assert reloads >= 1
+
+
+def test_deltaspike_ordinal_override(hola, tmp_path):
+    ds = tmp_path / "apache-deltaspike.properties"
+    ds.write_text("deltaspike_ordinal=500\nhello=ds %s\n")  # now above system properties (400)
+    s = hola(args=["--deltaspike-properties", str(ds), "-Dhello=sys %s"], env={"HOSTNAME": "h"})
+    assert s.get("/api/hola")[2] == b"ds h"

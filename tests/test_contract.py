@@ -252,3 +252,13 @@ def test_expect_100_continue(hola):
         c.sendall(b"abcd")
         data = c.recv(4096)
         assert data.startswith(b"HTTP/1.1 405")
+
+
+def test_swagger_yaml_matches_json(hola):
+    import yaml
+
+    s = hola()
+    st, h, body = s.get("/api/swagger.yaml")
+    assert st == 200 and h["content-type"] == "application/yaml"
+    assert h["access-control-allow-origin"] == "*"
+    assert yaml.safe_load(body) == json.loads(s.get("/api/swagger.json")[2])
