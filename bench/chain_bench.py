@@ -1,0 +1,53 @@
+#!/usr/bin/env python3
+"""Throughput of the chaining path with a native downstream: load generator ->
+hola A `/api/hola-chaining` -> hola B `/api/hola-chaining`. B plays aloha: its JSON list
+(`["Hola de B", "Aloha response (fallback)"]`, its own aloha being unreachable) is what A
+decodes as `List<String>`.
+
+Every request crosses two HTTP hops, A's per-worker keep-alive client pool, the Hystrix
+command (breaker + bulkhead + 600 ms timer) and B3 propagation. The bulkhead is widened
+with --pool so it measures the path rather than the (intentionally tiny) default of 10.
+
+    python bench/chain_bench.py --duration 10 [--pool 128]
+"""
+import argparse
+import json
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+
+from hola_amd.parallel.loadgen import run_duration  # noqa: E402
+from hola_amd.server import HolaProcess  # noqa: E402
+from hola_amd.utils.cpu import format_cpu_list, plan_node  # noqa: E402
+
+ap = argparse.ArgumentParser(description=__doc__)
+ap.add_argument("--duration", type=float, default=10)
+ap.add_argument("--connections", type=int, default=64)
+ap.add_argument("--pool", type=int, default=128, help="hystrix thread-pool (bulkhead) size on A")
+ap.add_argument("--out", default="")
+a = ap.parse_args()
+
+cores = plan_node(3)  # A, B, load generator
+# B answers /api/hola-chaining itself with its own fallback (its aloha is unreachable and its
+# breaker opens), so A decodes ["Hola de B", "Aloha response (fallback)"].
+with HolaProcess(args=["--aloha-url", "http://127.0.0.1:1/", "--feign-log", "none", "--no-tracing",
+                       "--log-level", "warn"], env={"HOSTNAME": "B"}, threads=len(cores[1]),
+                 cpu_list=format_cpu_list(cores[1])) as b:
+    with HolaProcess(args=["--aloha-url", f"http://127.0.0.1:{b.port}/", "--aloha-path", "api/hola-chaining",
+                           "--feign-log", "none", "--hystrix-pool-size", str(a.pool)],
+                     env={"HOSTNAME": "A"}, threads=len(cores[0]), cpu_list=format_cpu_list(cores[0])) as s:
+        st, _, body = s.get("/api/hola-chaining")
+        assert st == 200, body
+        sample = json.loads(body)
+        res = run_duration([("127.0.0.1", s.port)], a.connections, len(cores[2]), a.duration, 2.0,
+                           cpu_list=format_cpu_list(cores[2]), path="/api/hola-chaining")
+        _, _, metrics = s.get("/metrics")
+events = {l.split('event="')[1].split('"')[0]: int(l.split()[-1]) for l in metrics.decode().splitlines()
+          if l.startswith("hola_hystrix_events_total")}
+out = {"sample": sample, "rps": res["rps"], "p50_ms": res["latency"]["p50_ns"] / 1e6,
+       "p99_ms": res["latency"]["p99_ns"] / 1e6, "errors": res["latency"]["errors"], "hystrix_events": events,
+       "cpu_map": {"A": format_cpu_list(cores[0]), "B": format_cpu_list(cores[1]), "loadgen": format_cpu_list(cores[2])}}
+print(json.dumps(out))
+if a.out:
+    Path(a.out).write_text(json.dumps(out, indent=1))

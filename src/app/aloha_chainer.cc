@@ -18,6 +18,7 @@ AlohaChainer::AlohaChainer(AlohaOptions o, resilience::Settings s, int num_worke
   full_url_ = "http://" + target_.host + ":" + std::to_string(target_.port) + target_.base_path + o_.path;
   // HystrixFeign keys: command = Feign configKey, group (and pool) = target name (the URL).
   cmd_ = std::make_unique<Command>(o_.command_key, o_.url, o_.url, s, clock_);
+  timeout_ms_.store(s.timeout_enabled ? s.timeout_ms : 0);
   if (url_ok_) addr_ = std::make_unique<client::AddressCache>(target_.host, target_.port);
   pools_.resize(size_t(num_workers));
 }
@@ -73,8 +74,7 @@ void AlohaChainer::call(http::Worker& w, const tracing::SpanContext* parent,
   Command::Admit a = url_ok_ ? cmd->try_start() : Command::Admit::kRun;
   if (a != Command::Admit::kRun) {
     const char* why = a == Command::Admit::kShortCircuited ? "short-circuited" : "thread-pool-rejected";
-    cmd->fallback(Event::kFallbackSuccess);
-    cmd->total_latency(clock_.now_ms() - call->start_ms);
+    cmd->rejected(clock_.now_ms() - call->start_ms);
     loop.add_timer(0, [call, why] { call->cb(fallback_result(why)); });
     return;
   }
@@ -93,7 +93,7 @@ void AlohaChainer::call(http::Worker& w, const tracing::SpanContext* parent,
 
   const int worker_index = w.index();
   client::ClientPool& p = pool(w);
-  const resilience::Settings st = cmd->settings();
+  const int timeout_ms = timeout_ms_.load(std::memory_order_relaxed);
   bool log = o_.feign_log_basic;
   const std::string key = o_.command_key;
   const std::string url = full_url_;
@@ -130,20 +130,18 @@ void AlohaChainer::call(http::Worker& w, const tracing::SpanContext* parent,
       tracer->record_client(worker_index, call->ctx, call->start_us, wall_us(), url, r.ok ? r.status : 0,
                             success ? std::string_view() : std::string_view(err));
     if (success) {
-      cmd->finish(Event::kSuccess, elapsed);
+      cmd->complete(Event::kSuccess, elapsed, false, clock->now_ms() - call->start_ms);
     } else {
-      cmd->finish(Event::kFailure, elapsed);
-      cmd->fallback(Event::kFallbackSuccess);
+      cmd->complete(Event::kFailure, elapsed, true, clock->now_ms() - call->start_ms);
       res = fallback_result("failure");
       res.reason = err;
     }
-    cmd->total_latency(clock->now_ms() - call->start_ms);
     call->cb(res);
   });
 
-  if (st.timeout_enabled && !call->done) {
+  if (timeout_ms > 0 && !call->done) {
     client::ClientPool* pp = &p;
-    call->timer = loop.add_timer(st.timeout_ms, [call, cmd, pp, log, key, tracer, worker_index, url, clock] {
+    call->timer = loop.add_timer(timeout_ms, [call, cmd, pp, log, key, tracer, worker_index, url, clock] {
       if (call->done) return;
       call->done = true;
       call->timer = 0;
@@ -152,9 +150,7 @@ void AlohaChainer::call(http::Worker& w, const tracing::SpanContext* parent,
       if (log) LOG_INFO("[%s] <--- ERROR HystrixTimeoutException (%lldms)", key.c_str(), (long long)elapsed);
       if (call->traced && tracer)
         tracer->record_client(worker_index, call->ctx, call->start_us, wall_us(), url, 0, "timeout");
-      cmd->finish(Event::kTimeout, elapsed);
-      cmd->fallback(Event::kFallbackSuccess);
-      cmd->total_latency(elapsed);
+      cmd->complete(Event::kTimeout, elapsed, true, elapsed);
       call->cb(fallback_result("timeout"));
     });
   }

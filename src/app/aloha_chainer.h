@@ -7,6 +7,7 @@
 //   tracing           client span child of the server span + B3 headers (HolaResource.java:97-108)
 //   logging           Feign Logger.ErrorLogger at Level.BASIC        (HolaResource.java:109)
 #pragma once
+#include <atomic>
 #include <memory>
 #include <string>
 #include <vector>
@@ -41,7 +42,10 @@ class AlohaChainer final : public Chainer {
             std::function<void(const ChainResult&)> done) override;
 
   resilience::Command& command() { return *cmd_; }
-  void update_settings(const resilience::Settings& s) { cmd_->update_settings(s); }
+  void update_settings(const resilience::Settings& s) {
+    cmd_->update_settings(s);
+    timeout_ms_.store(s.timeout_enabled ? s.timeout_ms : 0, std::memory_order_relaxed);
+  }
   const std::string& full_url() const { return full_url_; }
 
  private:
@@ -55,6 +59,7 @@ class AlohaChainer final : public Chainer {
   std::vector<std::unique_ptr<client::ClientPool>> pools_;
   tracing::Tracer* tracer_;
   const Clock& clock_;
+  std::atomic<int> timeout_ms_{0};  // 0 = execution timeout disabled (read per call, lock-free)
 };
 
 }  // namespace hola::app

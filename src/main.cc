@@ -49,6 +49,7 @@ void usage() {
           "  --trace-sample-rate R    0..1 (default 1)\n"
           "  --no-tracing             disable tracing entirely\n"
           "  --aloha-url URL          downstream service (default http://aloha:8080/)\n"
+          "  --aloha-path PATH        downstream path (default api/aloha-chaining)\n"
           "  --feign-log basic|none   outbound call logging (default basic)\n"
           "  --hystrix-stream-max N   max /hystrix.stream subscribers (default 5)\n"
           "  --hystrix-timeout-ms N | --hystrix-request-volume N | --hystrix-error-pct N |\n"
@@ -130,6 +131,10 @@ int main(int argc, char** argv) {
       sysprops["hystrix.command.default.circuitBreaker.sleepWindowInMilliseconds"] = val(a.c_str());
     else if (a == "--hystrix-pool-size") sysprops["hystrix.threadpool.default.coreSize"] = val(a.c_str());
     else if (a == "--aloha-url") alo.url = val("--aloha-url");
+    else if (a == "--aloha-path") {
+      alo.path = val("--aloha-path");
+      while (!alo.path.empty() && alo.path.front() == '/') alo.path.erase(0, 1);
+    }
     else if (a == "--feign-log") alo.feign_log_basic = val("--feign-log") == "basic";
     else if (a == "--hystrix-stream-max") stream_max = atoi(val("--hystrix-stream-max").c_str());
     else if (a == "--config-poll-ms") mo.poll_ms = atoi(val("--config-poll-ms").c_str());

@@ -293,9 +293,7 @@ Command::Admit Command::try_start() {
   return Admit::kRun;
 }
 
-void Command::finish(Event outcome, int64_t execute_ms) {
-  std::lock_guard<std::mutex> g(mu_);
-  int64_t now = clock_.now_ms();
+void Command::finish_locked(int64_t now, Event outcome, int64_t execute_ms) {
   if (active_ > 0) --active_;
   ++completed_;
   counter_.add(now, outcome);
@@ -309,6 +307,26 @@ void Command::finish(Event outcome, int64_t execute_ms) {
   } else if (outcome == Event::kFailure) {
     exec_lat_.add(now, execute_ms);
   }
+}
+
+void Command::finish(Event outcome, int64_t execute_ms) {
+  std::lock_guard<std::mutex> g(mu_);
+  finish_locked(clock_.now_ms(), outcome, execute_ms);
+}
+
+void Command::complete(Event outcome, int64_t execute_ms, bool with_fallback, int64_t total_ms) {
+  std::lock_guard<std::mutex> g(mu_);
+  int64_t now = clock_.now_ms();
+  finish_locked(now, outcome, execute_ms);
+  if (with_fallback) counter_.add(now, Event::kFallbackSuccess);
+  total_lat_.add(now, total_ms);
+}
+
+void Command::rejected(int64_t total_ms) {
+  std::lock_guard<std::mutex> g(mu_);
+  int64_t now = clock_.now_ms();
+  counter_.add(now, Event::kFallbackSuccess);
+  total_lat_.add(now, total_ms);
 }
 
 void Command::fallback(Event e) {

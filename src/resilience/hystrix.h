@@ -150,6 +150,10 @@ class Command {
   // and the total latency of the whole command.
   void fallback(Event fallback_event);
   void total_latency(int64_t total_ms);
+  // finish() + optional fallback() + total_latency() under one lock acquisition.
+  void complete(Event outcome, int64_t execute_ms, bool with_fallback, int64_t total_ms);
+  // Short-circuit / rejection path: fallback + total latency under one lock.
+  void rejected(int64_t total_ms);
 
   bool circuit_open();            // evaluates health like HystrixCircuitBreaker.isOpen()
   HealthCounts health();
@@ -159,6 +163,7 @@ class Command {
   const std::string& name() const { return name_; }
 
  private:
+  void finish_locked(int64_t now, Event outcome, int64_t execute_ms);
   bool is_open_locked(int64_t now);
   bool allow_request_locked(int64_t now);
   HealthCounts health_locked(int64_t now);
