@@ -1,0 +1,42 @@
+#!/usr/bin/env python3
+"""Open-loop latency curve for GET /api/hola (wrk2-style): one pinned replica driven at fixed
+request rates, latency measured from each request's *intended* send time, so queueing delay
+is not hidden by coordinated omission. Complements the closed-loop headline in bench.py.
+
+    python bench/latency_curve.py --rates 250000,1000000,2000000,3000000 --duration 8
+"""
+import argparse
+import json
+import sys
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+
+from hola_amd.parallel.loadgen import run_duration  # noqa: E402
+from hola_amd.server import HolaProcess  # noqa: E402
+from hola_amd.utils.cpu import format_cpu_list, plan_node, split_server_loadgen  # noqa: E402
+
+ap = argparse.ArgumentParser(description=__doc__)
+ap.add_argument("--rates", default="250000,1000000,2000000,3000000,3500000")
+ap.add_argument("--duration", type=float, default=8)
+ap.add_argument("--connections", type=int, default=64)
+ap.add_argument("--out", default="")
+a = ap.parse_args()
+
+cores = plan_node(1)[0]
+srv, lg = split_server_loadgen(cores, max(1, len(cores) // 2))
+rows = []
+with HolaProcess(env={"HOSTNAME": "h"}, threads=len(srv), cpu_list=format_cpu_list(srv), log_level="warn") as s:
+    for rate in [float(x) for x in a.rates.split(",")]:
+        r = run_duration([("127.0.0.1", s.port)], a.connections, len(lg), a.duration, 2.0,
+                         cpu_list=",".join(map(str, lg)), rate=rate)
+        lat = r["latency"]
+        row = {"target_rps": rate, "achieved_rps": r["rps"], "p50_us": lat["p50_ns"] / 1e3,
+               "p90_us": lat["p90_ns"] / 1e3, "p99_us": lat["p99_ns"] / 1e3, "p999_us": lat["p999_ns"] / 1e3,
+               "max_us": lat["max_ns"] / 1e3, "errors": lat["errors"]}
+        rows.append(row)
+        print(json.dumps(row), flush=True)
+out = {"cpu_map": {"server": format_cpu_list(srv), "loadgen": format_cpu_list(lg)}, "connections": a.connections,
+       "rows": rows}
+if a.out:
+    Path(a.out).write_text(json.dumps(out, indent=1))
