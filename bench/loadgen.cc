@@ -18,6 +18,7 @@
 #include <errno.h>
 #include <netinet/in.h>
 #include <sys/epoll.h>
+#include <sys/prctl.h>
 #include <sys/eventfd.h>
 #include <sys/socket.h>
 #include <signal.h>
@@ -206,6 +207,7 @@ void thread_main(ThreadState* ts, const Options* o) {
   const bool rate_mode = !control && o->rate > 0;
   const int64_t interval = rate_mode ? int64_t(double(o->connections) * 1e9 / o->rate) : 0;
   if (rate_mode) {
+    prctl(PR_SET_TIMERSLACK, 1UL, 0, 0, 0);  // precise wake-ups for the send schedule
     int64_t t0 = mono_ns();
     size_t k = 0;
     for (auto& c : ts->conns) {
