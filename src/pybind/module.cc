@@ -14,6 +14,9 @@
 #include "tracing/b3.h"
 #include "tracing/tracer.h"
 #include "metrics/hystrix_stream.h"
+#include "core/histogram.h"
+#include "core/loop.h"
+#include "core/clock.h"
 
 namespace py = pybind11;
 using namespace hola;
@@ -196,6 +199,45 @@ std::string encode_spans_py(bool v2, const std::string& trace_id, const std::str
   return v2 ? t.encode_v2({r}) : t.encode_v1({r});
 }
 
+std::vector<uint64_t> histogram_percentiles(const std::vector<uint64_t>& values, const std::vector<double>& ps) {
+  hola::Histogram h;
+  for (uint64_t v : values) h.add(v);
+  std::vector<uint64_t> out;
+  for (double p : ps) out.push_back(h.percentile(p));
+  return out;
+}
+
+// Runs an EventLoop with one timer per delay (ms) plus cancellations; returns firing order.
+std::vector<int> loop_timer_order(const std::vector<int>& delays, const std::vector<int>& cancel) {
+  EventLoop loop;
+  std::vector<int> fired;
+  std::vector<EventLoop::TimerId> ids;
+  for (size_t i = 0; i < delays.size(); ++i)
+    ids.push_back(loop.add_timer(delays[i], [&fired, i] { fired.push_back(int(i)); }));
+  for (int c : cancel) loop.cancel_timer(ids[size_t(c)]);
+  int max_delay = 0;
+  for (int d : delays) max_delay = std::max(max_delay, d);
+  loop.add_timer(max_delay + 20, [&loop] { loop.stop(); });
+  loop.post([&fired] { fired.push_back(-1); });  // cross-thread task runs first
+  loop.run();
+  return fired;
+}
+
+std::pair<size_t, size_t> span_ring(size_t capacity, size_t pushes) {
+  tracing::SpanRing ring(capacity);
+  tracing::SpanRecord r{};
+  size_t ok = 0;
+  for (size_t i = 0; i < pushes; ++i) {
+    r.span_id = i;
+    ok += ring.push(r) ? 1 : 0;
+  }
+  std::vector<tracing::SpanRecord> out;
+  ring.drain(&out);
+  for (size_t i = 0; i < out.size(); ++i)
+    if (out[i].span_id != i) return {size_t(-1), 0};
+  return {ok, out.size()};
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_native, m) {
@@ -228,6 +270,9 @@ PYBIND11_MODULE(_native, m) {
         py::arg("parent") = py::none(), py::arg("kind") = "server", py::arg("start_us") = 1000,
         py::arg("end_us") = 2000, py::arg("url") = "http://localhost/api/hola", py::arg("status") = 200,
         py::arg("shared") = false);
+  m.def("histogram_percentiles", &histogram_percentiles);
+  m.def("loop_timer_order", &loop_timer_order, py::arg("delays"), py::arg("cancel") = std::vector<int>{});
+  m.def("span_ring", &span_ring);
   py::class_<PyCommand>(m, "HystrixCommand")
       .def(py::init<const std::map<std::string, std::string>&>(), py::arg("props") = std::map<std::string, std::string>{})
       .def("try_start", &PyCommand::try_start)
