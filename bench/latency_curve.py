@@ -7,6 +7,8 @@ is not hidden by coordinated omission. Complements the closed-loop headline in b
 """
 import argparse
 import json
+import os
+import resource
 import sys
 from pathlib import Path
 
@@ -27,13 +29,25 @@ cores = plan_node(1)[0]
 srv, lg = split_server_loadgen(cores, max(1, len(cores) // 2))
 rows = []
 with HolaProcess(env={"HOSTNAME": "h"}, threads=len(srv), cpu_list=format_cpu_list(srv), log_level="warn") as s:
+    def server_cpu():
+        with open(f"/proc/{s.proc.pid}/stat") as f:
+            v = f.read().rsplit(")", 1)[1].split()
+        return (int(v[11]) + int(v[12])) / os.sysconf("SC_CLK_TCK")
+
     for rate in [float(x) for x in a.rates.split(",")]:
+        c0 = resource.getrusage(resource.RUSAGE_CHILDREN)
+        s0 = server_cpu()
         r = run_duration([("127.0.0.1", s.port)], a.connections, len(lg), a.duration, 2.0,
                          cpu_list=",".join(map(str, lg)), rate=rate)
+        c1 = resource.getrusage(resource.RUSAGE_CHILDREN)
+        s1 = server_cpu()
+        wall = a.duration + 2.0  # warmup included in both CPU figures
         lat = r["latency"]
         row = {"target_rps": rate, "achieved_rps": r["rps"], "p50_us": lat["p50_ns"] / 1e3,
                "p90_us": lat["p90_ns"] / 1e3, "p99_us": lat["p99_ns"] / 1e3, "p999_us": lat["p999_ns"] / 1e3,
-               "max_us": lat["max_ns"] / 1e3, "errors": lat["errors"]}
+               "max_us": lat["max_ns"] / 1e3, "errors": lat["errors"],
+               "server_cpus_busy": round((s1 - s0) / wall, 2),
+               "loadgen_cpus_busy": round((c1.ru_utime + c1.ru_stime - c0.ru_utime - c0.ru_stime) / wall, 2)}
         rows.append(row)
         print(json.dumps(row), flush=True)
 out = {"cpu_map": {"server": format_cpu_list(srv), "loadgen": format_cpu_list(lg)}, "connections": a.connections,
