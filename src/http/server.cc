@@ -341,7 +341,9 @@ void Worker::sweep_idle() {
   const int64_t now = loop_.now_ms();
   for (Connection* c = conns_; c;) {
     Connection* next = c->next_;
-    if (!c->streaming() && c->idle() && now - c->last_active_ms() > limit) c->close();
+    // Includes connections holding a partial request (slow-loris): nothing arrived for the
+    // whole timeout, so the request will not complete.
+    if (!c->streaming() && c->quiet() && now - c->last_active_ms() > limit) c->close();
     c = next;
   }
 }

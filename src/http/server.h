@@ -75,6 +75,8 @@ class Connection final : public EventLoop::Handler {
   std::string peer() const;
   // Idle = no request in progress and nothing buffered either way.
   bool idle() const { return !parked_ && in_.empty() && out_.size() == out_off_; }
+  // No response owed and nothing queued to send (a partial request may be buffered).
+  bool quiet() const { return !parked_ && out_.size() == out_off_; }
   int64_t last_active_ms() const { return last_active_ms_; }
 
  private:

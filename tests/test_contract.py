@@ -262,3 +262,11 @@ def test_swagger_yaml_matches_json(hola):
     assert st == 200 and h["content-type"] == "application/yaml"
     assert h["access-control-allow-origin"] == "*"
     assert yaml.safe_load(body) == json.loads(s.get("/api/swagger.json")[2])
+
+
+def test_slowloris_partial_request_times_out(hola):
+    s = hola(args=["--idle-timeout-ms", "200"])
+    with socket.create_connection(("127.0.0.1", s.port), timeout=3) as c:
+        c.sendall(b"GET /api/hola HTTP/1.1\r\nHost: x\r\nX-Slow: ")  # never finished
+        time.sleep(0.8)
+        assert c.recv(4096) == b""
