@@ -44,7 +44,10 @@ def parse_args():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--connections", type=int, default=64, help="keep-alive connections per replica")
     ap.add_argument("--reqs-per-conn", type=int, default=50000, help="requests per connection per step")
-    ap.add_argument("--cores", type=int, default=0, help="host cores per replica (server + load generator)")
+    ap.add_argument("--cores", type=int, default=16,
+                    help="host cores per replica (server + load generator), capped by the node's CPU "
+                         "budget / replicas; 16 = the CPU share of one GPU slot, so every N runs each "
+                         "replica on the same resources (weak scaling)")
     ap.add_argument("--server-threads", type=int, default=0, help="0 = half of the rank's cores")
     ap.add_argument("--base-port", type=int, default=int(os.environ.get("HOLA_BENCH_PORT", "18400")))
     ap.add_argument("--path", default="/api/hola")
@@ -80,7 +83,8 @@ def main() -> int:
     # within a rank, server worker t and loadgen thread t share an L3 domain. ----
     plan = [None]
     if rank == 0:
-        plan = [{"cores": plan_replicas_with_loadgen(local_world, a.cores or None, a.server_threads,
+        per_rank = min(a.cores, max(1, cpu_budget() // local_world)) if a.cores else None
+        plan = [{"cores": plan_replicas_with_loadgen(local_world, per_rank, a.server_threads,
                                                      avoid_busy=not a.no_avoid_busy),
                  "base_port": _free_port_block(a.base_port, local_world)}]
     if dist:
@@ -187,6 +191,7 @@ def main() -> int:
                 "connections_per_replica": a.connections,
                 "reqs_per_conn_per_step": a.reqs_per_conn,
                 "lb": "client-side round-robin over replica ports",
+                "cores_per_replica": s_threads + len(load_cpus),
                 "server_threads_per_replica": s_threads,
                 "loadgen_threads_per_replica": len(load_cpus),
                 "busy_poll_us": a.busy_poll_us,
