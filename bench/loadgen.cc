@@ -66,6 +66,7 @@ struct Options {
   std::vector<std::string> extra_headers;
   int busy_poll_us = 0;
   double rate = 0;  // --rate: open-loop total req/s (wrk2-style, latency from intended time)
+  int spin_us = 0;  // --rate: spin instead of sleeping when the next send is this close (burns CPU)
 };
 
 struct Conn {
@@ -245,9 +246,16 @@ void thread_main(ThreadState* ts, const Options* o) {
     if (n == 0) {
       if (rate_mode) {
         int64_t wait = send_due(mono_ns());
-        if (wait > 5000000) wait = 5000000;
-        timespec tmo{0, wait == INT64_MAX ? 5000000 : long(wait)};
-        n = epoll_pwait2(ts->epfd, evs, 256, &tmo, nullptr);
+        if (wait <= int64_t(o->spin_us) * 1000) {
+          // The next send is close: poll instead of sleeping, so the schedule is kept to
+          // within a few microseconds (a timer sleep + wake-up costs more than the gap).
+          n = epoll_wait(ts->epfd, evs, 256, 0);
+        } else {
+          wait -= int64_t(o->spin_us) * 1000;  // wake early, then spin the rest
+          if (wait > 5000000) wait = 5000000;
+          timespec tmo{0, long(wait)};
+          n = epoll_pwait2(ts->epfd, evs, 256, &tmo, nullptr);
+        }
       } else {
         n = epoll_wait(ts->epfd, evs, 256, control ? -1 : 5);
       }
@@ -431,6 +439,7 @@ int main(int argc, char** argv) {
     else if (a == "--header" || a == "-H") o.extra_headers.push_back(val());
     else if (a == "--busy-poll-us") o.busy_poll_us = atoi(val().c_str());
     else if (a == "--rate" || a == "-R") o.rate = atof(val().c_str());
+    else if (a == "--spin-us") o.spin_us = atoi(val().c_str());
     else {
       fprintf(stderr,
               "usage: hola_loadgen --targets h:p[,h:p..] -c CONNS -t THREADS [--cpu-list L] [--path P]\n"
