@@ -27,6 +27,10 @@ std::optional<std::string> read_file(const std::string& path) {
     }
     if (n == 0) break;
     s.append(buf, size_t(n));
+    if (s.size() > (4u << 20)) {  // config files are tiny; refuse /dev/zero-style inputs
+      ::close(fd);
+      return std::nullopt;
+    }
   }
   ::close(fd);  // (the reference leaks this descriptor on every request: Configuration.java:29)
   return s;

@@ -172,3 +172,8 @@ def test_deltaspike_ordinal_override(hola, tmp_path):
     ds.write_text("deltaspike_ordinal=500\nhello=ds %s\n")  # now above system properties (400)
     s = hola(args=["--deltaspike-properties", str(ds), "-Dhello=sys %s"], env={"HOSTNAME": "h"})
     assert s.get("/api/hola")[2] == b"ds h"
+
+
+def test_unbounded_conf_source_is_refused(hola):
+    s = hola(args=["-Dconf=/dev/zero"], env={"HOSTNAME": "h"})
+    assert s.get("/api/hola")[2] == b"Hola de h"
