@@ -174,6 +174,10 @@ def test_deltaspike_ordinal_override(hola, tmp_path):
     assert s.get("/api/hola")[2] == b"ds h"
 
 
-def test_unbounded_conf_source_is_refused(hola):
+def test_non_regular_conf_sources_are_refused(hola, tmp_path):
     s = hola(args=["-Dconf=/dev/zero"], env={"HOSTNAME": "h"})
+    assert s.get("/api/hola")[2] == b"Hola de h"
+    fifo = tmp_path / "fifo"
+    os.mkfifo(fifo)  # opening a FIFO with no writer must not hang startup or the watcher
+    s = hola(args=[f"-Dconf={fifo}"], env={"HOSTNAME": "h"})
     assert s.get("/api/hola")[2] == b"Hola de h"
