@@ -23,8 +23,10 @@ class HolaProcess:
     def __init__(self, args: list[str] | None = None, env: dict | None = None, port: int = 0,
                  threads: int = 2, cpu_list: str | None = None, preset: str = "release",
                  inherit_env: bool = False, log_level: str = "info", exe: Path | None = None,
-                 stderr_path: str | None = None):
+                 stderr_path: str | None = None, wrapper: list[str] | None = None):
         self.args = list(args or [])
+        # e.g. ["setarch", "x86_64", "-R"] for TSan builds; $HOLA_WRAPPER supplies a default
+        self.wrapper = list(wrapper) if wrapper is not None else os.environ.get("HOLA_WRAPPER", "").split()
         self.port = port
         self.threads = threads
         self.cpu_list = cpu_list
@@ -52,7 +54,7 @@ class HolaProcess:
 
     def start(self, timeout: float = 30.0) -> "HolaProcess":
         port_file = os.path.join(self._tmp.name, "port")
-        cmd = [str(self.exe), "--host", "127.0.0.1", "--port", str(self.port), "--threads", str(self.threads),
+        cmd = [*self.wrapper, str(self.exe), "--host", "127.0.0.1", "--port", str(self.port), "--threads", str(self.threads),
                "--port-file", port_file, "--log-level", self.log_level, *self.args]
         if self.cpu_list:
             cmd += ["--cpu-list", self.cpu_list]

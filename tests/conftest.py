@@ -18,7 +18,12 @@ def pytest_sessionstart(session):
         build(san)
         os.environ["HOLA_BIN_DIR"] = str(build_dir(san))
         if san == "tsan":
+            import platform
+            import shutil
+
             os.environ.setdefault("TSAN_OPTIONS", "halt_on_error=1 exitcode=66")
+            if shutil.which("setarch"):  # gcc 11 TSan vs high-entropy mmap ASLR (see test_sanitizers)
+                os.environ.setdefault("HOLA_WRAPPER", f"setarch {platform.machine()} -R")
         else:
             os.environ.setdefault("ASAN_OPTIONS", "detect_leaks=1 halt_on_error=1 exitcode=66")
             os.environ.setdefault("UBSAN_OPTIONS", "halt_on_error=1 print_stacktrace=1")

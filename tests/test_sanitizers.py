@@ -86,6 +86,15 @@ def _workload(s: HolaProcess, aloha: FakeAloha, conf):
     return errors
 
 
+def tsan_wrapper():
+    """gcc 11's TSan aborts with "unexpected memory mapping" on kernels with high mmap ASLR
+    entropy (seen on the MI355X host's 6.18 kernel); run it with address randomisation off."""
+    import platform
+    import shutil
+
+    return ["setarch", platform.machine(), "-R"] if shutil.which("setarch") else []
+
+
 @pytest.mark.parametrize("preset", ["tsan", "asan"])
 def test_sanitized_server(preset, tmp_path):
     build(preset)
@@ -95,7 +104,8 @@ def test_sanitized_server(preset, tmp_path):
     with FakeAloha() as aloha, FakeZipkin() as zipkin:
         s = HolaProcess(args=["--aloha-url", aloha.url, "--zipkin-url", zipkin.url, "--feign-log", "none",
                               f"-Dconf={conf}", "-Dhystrix.command.default.metrics.healthSnapshot.intervalInMilliseconds=0"],
-                        env={"HOSTNAME": "san", **SAN_ENV[preset]}, threads=4, exe=exe, log_level="warn")
+                        env={"HOSTNAME": "san", **SAN_ENV[preset]}, threads=4, exe=exe, log_level="warn",
+                        wrapper=tsan_wrapper() if preset == "tsan" else None)
         s.start(timeout=60)
         try:
             errors = _workload(s, aloha, conf)
