@@ -5,11 +5,16 @@ The service itself is the ``hola`` executable (epoll event loops pinned to the E
 cores). This Python package is the tooling around it:
 
 * :mod:`hola_amd.native`   — build / locate / load the native artefacts
+* :mod:`hola_amd.ops`      — Python API over the native core operations (Properties parser,
+  String.format, Accept negotiation, B3, JSON) — the code the server itself runs
+* :mod:`hola_amd.models`   — the service's HTTP contract as data (routes, media types, CORS,
+  tracing), checked against the running server by the tests
 * :mod:`hola_amd.server`   — run a ``hola`` process (tests, smoke, bench)
 * :mod:`hola_amd.parallel` — replica scale-out: pinned replica sets, round-robin proxy,
   the 1/2/4/8 scaling harness (the service's analogue of data parallelism)
 * :mod:`hola_amd.utils`    — host CPU topology / cgroup quota / port helpers
 * :mod:`hola_amd.testing`  — fake aloha and fake Zipkin collector for integration tests
+* :mod:`hola_amd.deploy`   — systemd units for a bare-metal node (replicas + proxy)
 
 The GPUs stay idle by design: the reference has no tensor compute.
 """
