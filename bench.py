@@ -74,7 +74,8 @@ def main() -> int:
     if world > 1:
         import torch.distributed as dist  # gloo: replicas exchange only a few numbers (no device data)
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        with _stdout_to_stderr():  # gloo prints "[Gloo] Rank N is connected..." on fd 1
+            dist.init_process_group("gloo", rank=rank, world_size=world)
 
     ensure_built("release")  # file-locked: concurrent ranks build once
 
@@ -203,9 +204,25 @@ def main() -> int:
         }
         print(json.dumps(out), flush=True)
     if dist:
-        dist.barrier()
-        dist.destroy_process_group()
+        with _stdout_to_stderr():
+            dist.barrier()
+            dist.destroy_process_group()
     return 0
+
+
+class _stdout_to_stderr:
+    """Points file descriptor 1 at stderr for a block, so native libraries that print to
+    stdout cannot break the one-JSON-line contract of this script."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
 
 
 def _free_port_block(start: int, n: int) -> int:

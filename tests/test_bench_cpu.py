@@ -1,0 +1,39 @@
+"""bench.py's output contract, exercised on CPU with a tiny run (1 rank, and 2 ranks over
+gloo) — the same code path the driver runs on the MI355X node."""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config")
+
+
+def run(cmd, port):
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env={**os.environ, "HOLA_BENCH_PORT": str(port)})
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, r.stdout  # exactly one JSON line on stdout
+    return json.loads(lines[0])
+
+
+def test_bench_one_rank():
+    out = run([sys.executable, str(ROOT / "bench.py"), "--steps", "2", "--warmup", "1", "--reqs-per-conn", "100"], 18800)
+    for k in KEYS:
+        assert k in out
+    assert out["metric"] == json.loads((ROOT / "BASELINE.json").read_text())["metric"]
+    assert out["n_gpus"] == 1 and out["steps"] == 2 and out["warmup"] == 1
+    assert out["requests"] == 64 * 100 * 2 and out["errors"] == 0
+    assert out["scaling"] == "weak" and out["higher_is_better"] is True and out["vs_baseline"] is None
+    assert out["config"]["global_batch"] == 64 and out["config"]["parallelism"] == "replicas1"
+    assert abs(out["value"] - out["requests"] / (out["ms_per_step"] * out["steps"] / 1000)) / out["value"] < 0.01
+
+
+def test_bench_two_ranks_gloo():
+    out = run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+               "--master-addr", "127.0.0.1", "--master-port", "29561", str(ROOT / "bench.py"), "--gpus", "2",
+               "--steps", "2", "--warmup", "1", "--reqs-per-conn", "100"], 18820)
+    assert out["n_gpus"] == 2 and out["requests"] == 2 * 64 * 100 * 2
+    assert out["config"]["global_batch"] == 128
