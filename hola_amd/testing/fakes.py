@@ -2,7 +2,7 @@
 
 * :class:`FakeAloha`  — the `aloha` service hola chains to (AlohaService.java:25). Its mode can
   be switched at runtime: ``ok`` / ``slow`` / ``error`` (HTTP 500) / ``garbage`` (invalid
-  JSON) / ``chunked`` / ``close`` (drop the connection). Records every request's headers so
+  JSON) / ``chunked`` / ``chunked_lf`` (chunk lines ended by a bare LF) / ``close`` (drop the connection). Records every request's headers so
   tests can check B3 propagation.
 * :class:`FakeZipkin` — a span collector recording POST /api/v1/spans and /api/v2/spans.
 """
@@ -78,13 +78,14 @@ class _AlohaHandler(BaseHTTPRequestHandler):
             body, status = json.dumps(payload).encode(), 200
         self.send_response(status)
         self.send_header("Content-Type", "application/json")
-        if mode == "chunked":
+        if mode in ("chunked", "chunked_lf"):
+            eol = b"\r\n" if mode == "chunked" else b"\n"  # bare LF: tolerated framing (RFC 9112 §2.2)
             self.send_header("Transfer-Encoding", "chunked")
             self.end_headers()
             half = len(body) // 2
             for part in (body[:half], body[half:]):
-                self.wfile.write(b"%x\r\n%s\r\n" % (len(part), part))
-            self.wfile.write(b"0\r\n\r\n")
+                self.wfile.write(b"%x%s%s%s" % (len(part), eol, part, eol))
+            self.wfile.write(b"0" + eol + eol)
         else:
             self.send_header("Content-Length", str(len(body)))
             self.end_headers()

@@ -190,19 +190,10 @@ int ClientPool::Conn::try_parse(ClientResult* r, bool* keep, bool eof) {
   }
   if (chunked) {
     size_t consumed = 0;
-    http::Parse q = http::skip_chunked_body(in.data() + body, in.size() - body, &consumed);
+    std::string out;
+    http::Parse q = http::decode_chunked_body(in.data() + body, in.size() - body, &consumed, &out);
     if (q == http::Parse::kError) return -1;
     if (q == http::Parse::kIncomplete) return in.size() > (1 << 20) ? -1 : 0;
-    std::string out;
-    size_t i = body;
-    for (;;) {
-      size_t nl = in.find("\r\n", i);
-      size_t sz = strtoul(in.substr(i, nl - i).c_str(), nullptr, 16);
-      i = nl + 2;
-      if (sz == 0) break;
-      out.append(in, i, sz);
-      i += sz + 2;
-    }
     r->status = status;
     r->body = std::move(out);
     *keep = !close && body + consumed == in.size();

@@ -95,28 +95,20 @@ bool read_response(int fd, BlockingResponse* out, bool* close_delimited) {
   size_t body_start = head_end + 4;
   *close_delimited = conn_close;
   if (chunked) {
+    std::string body;
     for (;;) {
       size_t consumed = 0;
-      http::Parse p = http::skip_chunked_body(buf.data() + body_start, buf.size() - body_start, &consumed);
+      body.clear();
+      http::Parse p = http::decode_chunked_body(buf.data() + body_start, buf.size() - body_start, &consumed, &body);
       if (p == http::Parse::kError) return false;
       if (p == http::Parse::kOk) break;
-      if (!recv_some(fd, &buf)) return false;
-    }
-    // de-chunk
-    std::string body;
-    size_t p = body_start;
-    for (;;) {
-      size_t nl = buf.find("\r\n", p);
-      size_t sz = strtoul(buf.substr(p, nl - p).c_str(), nullptr, 16);
-      p = nl + 2;
-      if (sz == 0) break;
-      body.append(buf, p, sz);
-      p += sz + 2;
+      if (buf.size() > (1 << 20) || !recv_some(fd, &buf)) return false;
     }
     out->body = std::move(body);
     return true;
   }
   if (cl >= 0) {
+    if (cl > (1 << 20)) return false;
     while (buf.size() - body_start < size_t(cl))
       if (!recv_some(fd, &buf)) return false;
     out->body = buf.substr(body_start, size_t(cl));

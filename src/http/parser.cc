@@ -87,6 +87,10 @@ Parse parse_request(const char* buf, size_t len, Request* req, int* status) {
   size_t pos = 0;
   // RFC 9112 §2.2: ignore at least one empty line before the request-line.
   while (pos < len && (buf[pos] == '\r' || buf[pos] == '\n')) ++pos;
+  if (pos > kMaxHeadBytes) {  // a stream of bare line breaks must not grow the buffer forever
+    *status = 400;
+    return Parse::kError;
+  }
   if (pos == len) return Parse::kIncomplete;
 
   // ---- request line ----
@@ -268,6 +272,10 @@ Parse parse_request(const char* buf, size_t len, Request* req, int* status) {
 }
 
 Parse skip_chunked_body(const char* buf, size_t len, size_t* consumed) {
+  return decode_chunked_body(buf, len, consumed, nullptr);
+}
+
+Parse decode_chunked_body(const char* buf, size_t len, size_t* consumed, std::string* body) {
   size_t p = 0;
   for (;;) {
     const char* nl = static_cast<const char*>(memchr(buf + p, '\n', len - p));
@@ -302,6 +310,7 @@ Parse skip_chunked_body(const char* buf, size_t len, size_t* consumed) {
       }
     }
     if (len - p < sz + 2) return Parse::kIncomplete;
+    if (body) body->append(buf + p, size_t(sz));
     p += sz;
     if (buf[p] == '\r') ++p;
     if (p >= len) return Parse::kIncomplete;

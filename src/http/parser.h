@@ -6,6 +6,7 @@
 #pragma once
 #include <cstddef>
 #include <cstdint>
+#include <string>
 #include <string_view>
 
 namespace hola::http {
@@ -40,6 +41,9 @@ Parse parse_request(const char* buf, size_t len, Request* req, int* status);
 // For a chunked body starting at buf: on kOk sets *consumed to the full body length
 // (including the last-chunk and trailers).
 Parse skip_chunked_body(const char* buf, size_t len, size_t* consumed);
+// Same framing rules, also appending the de-chunked payload to *body (clients). *body is
+// meaningful only on kOk: pass a fresh string per attempt.
+Parse decode_chunked_body(const char* buf, size_t len, size_t* consumed, std::string* body);
 
 // Case-insensitive ASCII equality.
 bool iequals(std::string_view a, std::string_view b);

@@ -79,6 +79,15 @@ py::object skip_chunked_py(py::bytes data) {
   return py::int_(n);
 }
 
+py::object decode_chunked_py(py::bytes data) {
+  std::string s = data, body;
+  size_t n = 0;
+  http::Parse p = http::decode_chunked_body(s.data(), s.size(), &n, &body);
+  if (p == http::Parse::kIncomplete) return py::str("incomplete");
+  if (p == http::Parse::kError) return py::str("error");
+  return py::make_tuple(n, py::bytes(body));
+}
+
 py::object b3_extract_py(const std::string& t, const std::string& s, const std::string& p, const std::string& smp,
                          const std::string& flags, const std::string& single) {
   tracing::SpanContext c;
@@ -259,6 +268,7 @@ PYBIND11_MODULE(_native, m) {
   });
   m.def("parse_request", &parse_request_py);
   m.def("skip_chunked_body", &skip_chunked_py);
+  m.def("decode_chunked_body", &decode_chunked_py);
   m.def("b3_extract", &b3_extract_py, py::arg("trace_id") = "", py::arg("span_id") = "", py::arg("parent_id") = "",
         py::arg("sampled") = "", py::arg("flags") = "", py::arg("single") = "");
   m.def("b3_inject", &b3_inject_py, py::arg("trace_id"), py::arg("span_id"), py::arg("parent") = py::none(),

@@ -39,10 +39,12 @@ def test_keepalive_reuse(hola, aloha):
     assert st == 200
 
 
-def test_chunked_response(hola, aloha):
-    aloha.set_mode("chunked")
+@pytest.mark.parametrize("mode", ["chunked", "chunked_lf"])
+def test_chunked_response(hola, aloha, mode):
+    aloha.set_mode(mode)
     s = hola(args=["--aloha-url", aloha.url])
-    assert chain(s)[1:] == ["Aloha mai aloha-1", "Bonjour de bonjour-1"]
+    for _ in range(3):  # also over the kept-alive connection
+        assert chain(s)[1:] == ["Aloha mai aloha-1", "Bonjour de bonjour-1"]
 
 
 @pytest.mark.parametrize("mode", ["error", "garbage", "close"])

@@ -31,6 +31,7 @@ def test_incomplete(native, raw):
     (b"GET /x HTTP/1.1\r\nTransfer-Encoding: gzip\r\n\r\n", 501),
     (b"GET /" + b"a" * 9000 + b" HTTP/1.1\r\n\r\n", 414),
     (b"GET /x HTTP/1.1\r\n" + b"X-Pad: " + b"a" * 17000 + b"\r\n\r\n", 431),
+    (b"\r\n" * 9000, 400),  # endless blank lines before a request line are bounded too
 ])
 def test_errors(native, raw, status):
     assert native.parse_request(raw) == status
@@ -65,6 +66,31 @@ def test_chunked_body(native):
     assert native.skip_chunked_body(b"3;ext=1\r\nabc\r\n0\r\nTrailer: x\r\n\r\nNEXT") == 31
     assert native.skip_chunked_body(b"3\r\nab") == "incomplete"
     assert native.skip_chunked_body(b"zz\r\n") == "error"
+
+
+def test_decode_chunked_body(native):
+    assert native.decode_chunked_body(b"3\r\nabc\r\n2;x=y\r\nde\r\n0\r\n\r\n") == (24, b"abcde")
+    # bare-LF chunk lines (accepted by the framing) must decode, not overrun the buffer
+    assert native.decode_chunked_body(b"3\nabc\n2\nde\n0\n\n") == (14, b"abcde")
+    assert native.decode_chunked_body(b"3\r\nabc\r\n") == "incomplete"
+
+
+@settings(max_examples=200, deadline=None)
+@given(st.lists(st.binary(min_size=1, max_size=40), max_size=6), st.booleans())
+def test_chunked_roundtrip(native, parts, crlf):
+    eol = b"\r\n" if crlf else b"\n"
+    raw = b"".join(b"%x" % len(p) + eol + p + eol for p in parts) + b"0" + eol + eol
+    assert native.decode_chunked_body(raw) == (len(raw), b"".join(parts))
+    assert native.skip_chunked_body(raw) == len(raw)
+    for cut in range(len(raw)):
+        assert native.decode_chunked_body(raw[:cut]) in ("incomplete", "error")
+
+
+@settings(max_examples=300, deadline=None)
+@given(st.binary(max_size=200))
+def test_fuzz_chunked_total(native, data):
+    r = native.decode_chunked_body(data)
+    assert r in ("incomplete", "error") or (isinstance(r, tuple) and r[0] <= len(data))
 
 
 _token = st.text(alphabet="abcdefghijklmnopqrstuvwxyz-", min_size=1, max_size=10)
