@@ -380,9 +380,11 @@ void HolaApp::handle_chaining(http::Connection& c, const http::Request& r, Worke
   tracing::ServerSpan span;
   bool traced = tracer_ && tracer_->enabled();
   if (traced) span = tracer_->begin_server(c.worker().index(), r);
+  const int64_t t0 = mono_ns();
   if (!chainer_) {
     c.send(wc.chaining_fallback[ka][head].view());
     if (traced) tracer_->end_server(c.worker().index(), span, 200);
+    if (prom_) prom_->observe_chaining_us(c.worker().index(), uint64_t(mono_ns() - t0) / 1000);
     return;
   }
   // Async: the connection is parked until aloha answers, times out or is short-circuited.
@@ -392,7 +394,7 @@ void HolaApp::handle_chaining(http::Connection& c, const http::Request& r, Worke
   std::shared_ptr<const Content> content = wc.content;
   HolaApp* self = this;
   chainer_->call(c.worker(), traced ? &span.ctx : nullptr,
-                 [self, conn, content, ka, head, traced, span](const ChainResult& res) {
+                 [self, conn, content, ka, head, traced, span, t0](const ChainResult& res) {
                    http::Worker& w = conn->worker();
                    if (!conn->closed()) {
                      std::vector<std::optional<std::string>> items;
@@ -409,6 +411,7 @@ void HolaApp::handle_chaining(http::Connection& c, const http::Request& r, Worke
                      conn->complete(build_response(s, w.date()).view(), ka);
                    }
                    if (traced) self->tracer_->end_server(w.index(), span, 200);
+                   if (self->prom_) self->prom_->observe_chaining_us(w.index(), uint64_t(mono_ns() - t0) / 1000);
                    conn->release();
                  });
 }

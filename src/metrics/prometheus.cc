@@ -1,5 +1,7 @@
 #include "metrics/prometheus.h"
 
+#include <cstdio>
+
 #include "app/hola_app.h"
 #include "http/server.h"
 #include "resilience/hystrix.h"
@@ -8,7 +10,8 @@
 namespace hola::metrics {
 
 Prometheus::Prometheus(int num_workers, int num_routes)
-    : nworkers_(num_workers), nroutes_(num_routes), counts_(new Counter[size_t(num_workers) * size_t(num_routes)]) {}
+    : nworkers_(num_workers), nroutes_(num_routes), counts_(new Counter[size_t(num_workers) * size_t(num_routes)]),
+      chain_lat_(new LatencyHist[size_t(num_workers)]) {}
 
 std::string Prometheus::render(http::Server* server) const {
   std::string o;
@@ -20,6 +23,32 @@ std::string Prometheus::render(http::Server* server) const {
     o += "hola_requests_total{route=\"";
     o += app::HolaApp::route_name(r);
     o += "\"} " + std::to_string(n) + "\n";
+  }
+  {
+    uint64_t b[kLatencyBuckets + 1] = {}, sum_us = 0, count = 0;
+    for (int w = 0; w < nworkers_; ++w) {
+      const LatencyHist& h = chain_lat_[size_t(w)];
+      for (int i = 0; i <= kLatencyBuckets; ++i) b[i] += h.bucket[i].load(std::memory_order_relaxed);
+      sum_us += h.sum_us.load(std::memory_order_relaxed);
+      count += h.count.load(std::memory_order_relaxed);
+    }
+    o += "# HELP hola_chaining_duration_seconds /api/hola-chaining latency (aloha call, timeout or fallback).\n"
+         "# TYPE hola_chaining_duration_seconds histogram\n";
+    uint64_t cum = 0;
+    char num[64];
+    for (int i = 0; i <= kLatencyBuckets; ++i) {
+      cum += b[i];
+      if (i < kLatencyBuckets) snprintf(num, sizeof num, "%g", double(kLatencyBoundsUs[i]) / 1e6);
+      o += "hola_chaining_duration_seconds_bucket{le=\"";
+      o += i < kLatencyBuckets ? num : "+Inf";
+      o += "\"} " + std::to_string(cum) + "\n";
+    }
+    // Buckets are read before sum/count without a lock: under load the three may differ by
+    // a few in-flight observations, which Prometheus tolerates.
+    snprintf(num, sizeof num, "%.6f", double(sum_us) / 1e6);
+    o += "hola_chaining_duration_seconds_sum ";
+    o += num;
+    o += "\nhola_chaining_duration_seconds_count " + std::to_string(count) + "\n";
   }
   if (server) {
     uint64_t acc = 0, closed = 0, perr = 0, bin = 0, bout = 0, req = 0, rej = 0;

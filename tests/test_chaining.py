@@ -135,6 +135,36 @@ def test_bulkhead_rejects_beyond_pool(hola, aloha):
     assert b'event="THREAD_POOL_REJECTED"' in body
 
 
+def _histogram(body: bytes, name: str) -> tuple[dict, float, int]:
+    buckets, total, count = {}, None, None
+    for line in body.decode().splitlines():
+        if line.startswith(name + "_bucket{le=\""):
+            le = line.split('"')[1]
+            buckets[le] = int(line.rsplit(" ", 1)[1])
+        elif line.startswith(name + "_sum "):
+            total = float(line.split()[1])
+        elif line.startswith(name + "_count "):
+            count = int(line.split()[1])
+    return buckets, total, count
+
+
+def test_chaining_latency_histogram(hola, aloha):
+    s = hola(args=["--aloha-url", aloha.url, "--feign-log", "none", "--no-tracing",
+                   "-Dhystrix.command.default.circuitBreaker.enabled=false"], threads=2)
+    for _ in range(4):
+        chain(s)
+    aloha.set_mode("slow", delay_s=1.0)
+    for _ in range(2):  # both end at the 600 ms Hystrix timeout
+        assert chain(s)[1:] == [FALLBACK]
+    _, _, body = s.get("/metrics")
+    b, total, count = _histogram(body, "hola_chaining_duration_seconds")
+    les = list(b)
+    assert les[-1] == "+Inf" and count == 6 and b["+Inf"] == 6
+    assert all(b[x] <= b[y] for x, y in zip(les, les[1:]))  # cumulative
+    assert b["0.5"] == 4 and b["1"] == 6  # the timed-out calls sit between 0.5 s and 1 s
+    assert 1.2 <= total < 2.5
+
+
 def test_format_error_skips_downstream_call(hola, aloha, tmp_path):
     conf = tmp_path / "t.properties"
     conf.write_text("hello=%d\n")
