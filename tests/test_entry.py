@@ -24,3 +24,39 @@ def test_cli_info_and_help(capsys):
     out = capsys.readouterr().out
     assert "physical cores" in out and "plan x8" in out
     assert main([]) == 0
+
+
+def test_cli_cluster_round_robin(hola_bin):
+    """`python -m hola_amd cluster`: 2 supervised replicas behind the round-robin proxy,
+    stopped with SIGINT (what Ctrl-C does)."""
+    import http.client
+    import signal
+    import subprocess
+    import sys
+    import time
+
+    from hola_amd.utils.net import free_port
+
+    port = free_port()
+    p = subprocess.Popen([sys.executable, "-m", "hola_amd", "cluster", "--replicas", "2", "--port", str(port),
+                          "--proxy-threads", "1"], cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                         text=True)
+    try:
+        line = ""
+        deadline = time.monotonic() + 60
+        while "hola cluster:" not in line and time.monotonic() < deadline and p.poll() is None:
+            line = p.stdout.readline()
+        assert "hola cluster:" in line, line
+        seen = set()
+        for _ in range(8):
+            c = http.client.HTTPConnection("127.0.0.1", port, timeout=5)
+            c.request("GET", "/api/hola")
+            r = c.getresponse()
+            assert r.status == 200
+            seen.add(r.read())
+            c.close()
+        assert seen == {b"Hola de replica-0", b"Hola de replica-1"}
+    finally:
+        p.send_signal(signal.SIGINT)
+        rc = p.wait(timeout=30)
+    assert rc == 0
