@@ -159,7 +159,8 @@ int response_complete(Conn* c, int* status, bool* close) {
   size_t cl = 0;
   size_t p = head.find("Content-Length: ");
   if (p == std::string_view::npos) p = head.find("content-length: ");
-  if (p != std::string_view::npos) cl = size_t(atol(std::string(head.substr(p + 16, 12)).c_str()));
+  if (p != std::string_view::npos)
+    for (size_t i = p + 16; i < head.size() && head[i] >= '0' && head[i] <= '9'; ++i) cl = cl * 10 + size_t(head[i] - '0');
   *close = head.find("Connection: close") != std::string_view::npos;
   if (he + 4 + cl > sizeof c->buf) return -1;
   return c->have >= he + 4 + cl ? 1 : 0;
