@@ -348,11 +348,12 @@ void Worker::sweep_idle() {
   }
 }
 
-void Worker::adopt(int fd) {
-  loop_.post([this, fd] { adopt_here(fd); });
+void Worker::adopt(int fd, int64_t accepted_ns) {
+  loop_.post([this, fd, accepted_ns] { adopt_here(fd, accepted_ns); });
 }
 
-void Worker::adopt_here(int fd) {
+void Worker::adopt_here(int fd, int64_t accepted_ns) {
+  if (profile_ && accepted_ns) profile_->accept.add(uint64_t(mono_ns() - accepted_ns));
   auto* c = new Connection(this, fd, (uint64_t(index_) << 48) | next_conn_id_++);
   const size_t maxc = server_->options().max_connections;
   if (maxc && server_->open_connections() >= maxc) {
@@ -460,7 +461,9 @@ bool Server::bind(std::string* err) {
 }
 
 void Server::Acceptor::on_event(uint32_t) {
+  const bool prof = server->opts_.profile;
   for (int i = 0; i < 256; ++i) {
+    const int64_t t0 = prof ? mono_ns() : 0;
     int c = ::accept4(fd, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
     if (c < 0) {
       if (errno == EINTR || errno == ECONNABORTED) continue;
@@ -478,11 +481,11 @@ void Server::Acceptor::on_event(uint32_t) {
     }
     if (server->opts_.reuseport_accept) {
       server->assigned_[size_t(worker->index())].fetch_add(1, std::memory_order_relaxed);
-      worker->adopt_here(c);
+      worker->adopt_here(c, t0);
     } else {
       Worker* w = server->pick_worker(c);
-      if (w == worker) w->adopt_here(c);
-      else w->adopt(c);
+      if (w == worker) w->adopt_here(c, t0);
+      else w->adopt(c, t0);
     }
   }
 }
@@ -565,6 +568,7 @@ std::string Server::profile_json() const {
   StageProfile all;
   for (auto& w : workers_) {
     const StageProfile* p = w->profile_.get();
+    all.accept.merge(p->accept);
     all.recv.merge(p->recv);
     all.parse.merge(p->parse);
     all.handle.merge(p->handle);
@@ -579,7 +583,7 @@ std::string Server::profile_json() const {
              (unsigned long long)h.max());
     return std::string(buf);
   };
-  return "{\"unit\":\"ns (batch: requests per recv)\"," + one("recv", all.recv) + "," + one("parse", all.parse) + "," +
+  return "{\"unit\":\"ns (batch: requests per recv)\"," + one("accept", all.accept) + "," + one("recv", all.recv) + "," + one("parse", all.parse) + "," +
          one("handle", all.handle) + "," + one("send", all.send) + "," + one("batch", all.batch) + "}";
 }
 

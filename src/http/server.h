@@ -145,7 +145,9 @@ struct ServerOptions {
 
 // Per-worker stage timings (ns) collected with --profile; read after the workers stop.
 struct StageProfile {
-  Histogram recv, parse, handle, send, batch;  // batch = requests handled per recv()
+  // accept = accept4() until the owning worker adopts the socket (includes the cross-worker
+  // hand-off); batch = requests handled per recv().
+  Histogram accept, recv, parse, handle, send, batch;
 };
 
 class Worker {
@@ -163,8 +165,9 @@ class Worker {
   const char* date() const { return date_; }
   uint64_t date_version() const { return date_version_; }
   // Accepted fd handed over from the acceptor (thread-safe).
-  void adopt(int fd);
-  void adopt_here(int fd);
+  // accepted_ns: mono_ns() taken before accept4 (0 when not profiling).
+  void adopt(int fd, int64_t accepted_ns = 0);
+  void adopt_here(int fd, int64_t accepted_ns = 0);
   size_t open_connections() const { return nconns_; }
   void on_connection_closed(Connection* c);
   // Closes idle and streaming connections (shutdown drain); runs on the worker thread.

@@ -62,7 +62,7 @@ void usage() {
           "  --idle-timeout-ms N      close keep-alive connections idle this long (default 60000, 0 = never)\n"
           "  --max-connections N      refuse connections beyond N per replica (default unlimited)\n"
           "  --no-steer               plain round-robin accept (default: L3-domain steering when pinned)\n"
-          "  --profile                per-stage latency histograms (recv/parse/handle/send), dumped at exit\n"
+          "  --profile                per-stage latency histograms (accept/recv/parse/handle/send), dumped at exit\n"
           "  --profile-out PATH       write the --profile JSON here (default: stderr)\n"
           "  --log-level L            debug|info|warn|error|off (default info)\n"
           "  --no-metrics             disable the /metrics endpoint\n");

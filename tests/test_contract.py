@@ -270,3 +270,23 @@ def test_slowloris_partial_request_times_out(hola):
         c.sendall(b"GET /api/hola HTTP/1.1\r\nHost: x\r\nX-Slow: ")  # never finished
         time.sleep(0.8)
         assert c.recv(4096) == b""
+
+
+def test_profile_stage_histograms(hola, tmp_path):
+    """`--profile`: per-stage latency histograms dumped at exit."""
+    import signal
+
+    out = tmp_path / "prof.json"
+    s = hola(args=["--profile", "--profile-out", str(out)], threads=2)
+    for _ in range(3):
+        with socket.create_connection(("127.0.0.1", s.port), timeout=5) as c:
+            c.sendall(b"GET /api/hola HTTP/1.1\r\nHost: x\r\n\r\n" * 4 + b"GET /api/health HTTP/1.1\r\nConnection: close\r\n\r\n")
+            while c.recv(65536):
+                pass
+    assert s.stop(signal.SIGTERM, timeout=10) == 0
+    prof = json.loads(out.read_text())
+    for stage in ("accept", "recv", "parse", "handle", "send", "batch"):
+        assert stage in prof, prof
+    assert prof["accept"]["count"] == 3
+    assert prof["parse"]["count"] == 15 and prof["handle"]["count"] == 15
+    assert prof["batch"]["max"] >= 2  # pipelined requests handled from one recv()
