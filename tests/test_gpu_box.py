@@ -24,8 +24,9 @@ def test_bench_json_contract_on_host():
                         "--reqs-per-conn", "200"], capture_output=True, text=True, timeout=600,
                        env={**os.environ, "HOLA_BENCH_PORT": "18700"})
     assert r.returncode == 0, r.stderr[-3000:]
-    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
-    out = json.loads(line)
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, r.stdout[-2000:]  # the driver's contract: ONE JSON line
+    out = json.loads(lines[0])
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
               "scaling", "vs_baseline", "dtype", "data", "config"):
         assert k in out
@@ -45,7 +46,9 @@ def test_bench_two_ranks_on_host():
                        capture_output=True, text=True, timeout=600,
                        env={**os.environ, "HOLA_BENCH_PORT": "18760"})
     assert r.returncode == 0, r.stderr[-3000:]
-    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, r.stdout[-2000:]  # gloo's "[Gloo] Rank N is connected" goes to stderr
+    out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "replicas2"
     assert out["requests"] == 2 * 64 * 500 * 3
     assert out["errors"] == 0 and out["non2xx"] == 0
