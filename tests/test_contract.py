@@ -290,3 +290,20 @@ def test_profile_stage_histograms(hola, tmp_path):
     assert prof["accept"]["count"] == 3
     assert prof["parse"]["count"] == 15 and prof["handle"]["count"] == 15
     assert prof["batch"]["max"] >= 2  # pipelined requests handled from one recv()
+
+
+def test_ipv6_listener(hola):
+    """`--host ::1`: the listener is address-family agnostic (getaddrinfo)."""
+    try:
+        probe = socket.socket(socket.AF_INET6, socket.SOCK_STREAM)
+        probe.bind(("::1", 0))
+        probe.close()
+    except OSError:
+        pytest.skip("no IPv6 loopback here")
+    s = hola(args=["--host", "::1"], env={"HOSTNAME": "v6"})
+    with socket.create_connection(("::1", s.port), timeout=5) as c:
+        c.sendall(b"GET /api/hola HTTP/1.1\r\nHost: [::1]\r\nConnection: close\r\n\r\n")
+        data = b""
+        while chunk := c.recv(65536):
+            data += chunk
+    assert data.startswith(b"HTTP/1.1 200 OK") and data.endswith(b"\r\n\r\nHola de v6")
