@@ -2,11 +2,14 @@
 
   build [--preset release|debug|tsan|asan]   compile the native artefacts in-tree
   serve [hola args...]                       run the service (same flags as the binary)
-  cluster --replicas N [--port P]            N pinned replicas + the round-robin proxy on P
+  cluster --replicas N [--port P] [--lb L]   N pinned replicas on P: behind the round-robin
+                                             proxy (--lb proxy) or one SO_REUSEPORT group
+                                             spread by the kernel (--lb reuseport)
   scaling [...]                              replica scaling curve (hola_amd.parallel.scaling)
   bench [...]                                the headline benchmark (bench.py)
   info                                       host CPU topology / quota / plan for this node
-  units --replicas N --out DIR               systemd units: N pinned replicas + proxy on :8080
+  units --replicas N --out DIR [--lb L]      systemd units: N pinned replicas + proxy on :8080
+                                             (or --lb reuseport: replicas share :8080)
 
 The local equivalents of the reference's `mvn wildfly-swarm:run` (Readme.md:13) and
 `mvn clean package docker:build fabric8:json fabric8:apply` (Readme.md:24) are
@@ -45,19 +48,33 @@ def _cluster(argv: list[str]) -> int:
     ap.add_argument("--port", type=int, default=8080)
     ap.add_argument("--cores-per-replica", type=int, default=0)
     ap.add_argument("--proxy-threads", type=int, default=2)
+    ap.add_argument("--lb", choices=["proxy", "reuseport"], default="proxy",
+                    help="proxy: hola_rrproxy health-checks /api/health and round-robins connections; "
+                         "reuseport: replicas share the port and the kernel spreads connections (no hop)")
     ap.add_argument("hola_args", nargs=argparse.REMAINDER)
     a = ap.parse_args(argv)
+
+    def wait():
+        try:
+            while True:
+                time.sleep(1)
+        except KeyboardInterrupt:
+            pass
+
+    if a.lb == "reuseport":
+        plan = plan_node(a.replicas, a.cores_per_replica or None)
+        with ReplicaSet(a.replicas, cpu_plan=plan, args=a.hola_args, supervise=True, shared_port=a.port) as rs:
+            print(f"hola cluster: {a.replicas} replicas sharing :{rs.shared_port} (SO_REUSEPORT; Ctrl-C to stop)",
+                  flush=True)
+            wait()
+        return 0
     plan = plan_node(a.replicas + 1, a.cores_per_replica or None)
     with ReplicaSet(a.replicas, cpu_plan=plan[:a.replicas], args=a.hola_args, supervise=True) as rs:
         with RRProxy(rs.targets, port=a.port, threads=a.proxy_threads,
                      cpu_list=format_cpu_list(plan[-1][:a.proxy_threads])) as px:
             print(f"hola cluster: {a.replicas} replicas on ports {rs.ports} behind :{px.port} (Ctrl-C to stop)",
                   flush=True)
-            try:
-                while True:
-                    time.sleep(1)
-            except KeyboardInterrupt:
-                pass
+            wait()
     return 0
 
 
@@ -112,9 +129,10 @@ def main(argv: list[str] | None = None) -> int:
         ap.add_argument("--prefix", default="/opt/hola")
         ap.add_argument("--port", type=int, default=8080)
         ap.add_argument("--cores-per-replica", type=int, default=0)
+        ap.add_argument("--lb", choices=["proxy", "reuseport"], default="proxy")
         a = ap.parse_args(rest)
         for p in write_units(a.out, replicas=a.replicas, prefix=a.prefix, public_port=a.port,
-                             cores_per_replica=a.cores_per_replica or None):
+                             cores_per_replica=a.cores_per_replica or None, lb=a.lb):
             print(p)
         return 0
     print(f"unknown command {cmd!r}\n{__doc__}", file=sys.stderr)

@@ -21,7 +21,14 @@ from hola_amd.utils.net import free_port, wait_http
 
 
 class ReplicaSet:
-    """N `hola` replicas on distinct ports, each pinned to its own CPU list.
+    """N `hola` replicas, each pinned to its own CPU list.
+
+    By default every replica has its own port (a front — client-side round-robin or
+    :class:`RRProxy` — spreads the load). With ``shared_port`` all replicas listen on that
+    one port with ``--accept reuseport``: they join a single SO_REUSEPORT group and the
+    kernel spreads incoming connections over every replica's listeners, with no proxy hop.
+    A replica that dies leaves the group when its sockets close, so new connections go to
+    the survivors (the role of kube-proxy's endpoint removal).
 
     HOSTNAME is set to ``replica-<i>`` so responses identify the replica (the k8s pod name
     plays that role in the reference). With ``supervise=True`` a background thread restarts
@@ -30,7 +37,7 @@ class ReplicaSet:
 
     def __init__(self, n: int, cpu_plan: list[list[int]] | None = None, threads_per_replica: int = 1,
                  args: list[str] | None = None, env: dict | None = None, supervise: bool = True,
-                 base_port: int = 0, log_level: str = "warn"):
+                 base_port: int = 0, log_level: str = "warn", shared_port: int | None = None):
         self.n = n
         self.cpu_plan = cpu_plan
         self.threads = threads_per_replica
@@ -38,7 +45,13 @@ class ReplicaSet:
         self.env = dict(env or {})
         self.supervise = supervise
         self.log_level = log_level
-        self.ports = [base_port + i if base_port else free_port() for i in range(n)]
+        self.shared_port = shared_port
+        if shared_port is not None:
+            self.shared_port = shared_port or free_port()
+            self.ports = [self.shared_port] * n
+            self.args = ["--accept", "reuseport", *self.args]
+        else:
+            self.ports = [base_port + i if base_port else free_port() for i in range(n)]
         self.procs: list[HolaProcess | None] = [None] * n
         self.restarts = [0] * n
         self._stop = threading.Event()
@@ -85,7 +98,7 @@ class ReplicaSet:
 
     @property
     def targets(self) -> list[tuple[str, int]]:
-        return [("127.0.0.1", p) for p in self.ports]
+        return [("127.0.0.1", p) for p in sorted(set(self.ports))]
 
     def stop(self) -> None:
         self._stop.set()

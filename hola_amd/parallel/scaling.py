@@ -1,6 +1,6 @@
 """Replica scaling curve for GET /api/hola on one node (BASELINE.json configs 2-4).
 
-    python -m hola_amd.parallel.scaling --replicas 1,2,4,8 --duration 10 [--lb client|proxy]
+    python -m hola_amd.parallel.scaling --replicas 1,2,4,8 --duration 10 [--lb client|proxy|reuseport]
 
 For each replica count N the host CPU budget is split into disjoint core sets: one per
 replica (server event loops) plus one for the load generator (and the proxy, with
@@ -58,7 +58,8 @@ def run_point(n: int, args) -> dict:
     p = plan(n, budget, args.server_share, proxy_threads)
     conns = args.connections_per_replica * n if args.mode == "weak" else args.connections
     extra = ["--no-tracing"] if args.no_tracing else []
-    with ReplicaSet(n, cpu_plan=p["replicas"], args=extra, supervise=False) as rs:
+    shared = 0 if args.lb == "reuseport" else None
+    with ReplicaSet(n, cpu_plan=p["replicas"], args=extra, supervise=False, shared_port=shared) as rs:
         if args.lb == "proxy":
             with RRProxy(rs.targets, threads=proxy_threads, cpu_list=format_cpu_list(p["proxy"])) as px:
                 targets = [("127.0.0.1", px.port)]
@@ -86,7 +87,9 @@ def main(argv=None) -> int:
     ap.add_argument("--mode", choices=["weak", "strong"], default="weak")
     ap.add_argument("--connections-per-replica", type=int, default=64)
     ap.add_argument("--connections", type=int, default=512)
-    ap.add_argument("--lb", choices=["client", "proxy"], default="client")
+    ap.add_argument("--lb", choices=["client", "proxy", "reuseport"], default="client",
+                    help="client: load generator round-robins over replica ports; proxy: hola_rrproxy; "
+                         "reuseport: one shared port, the kernel spreads connections")
     ap.add_argument("--proxy-threads", type=int, default=2)
     ap.add_argument("--budget", type=int, default=0, help="CPUs to use (default: cgroup quota / affinity)")
     ap.add_argument("--server-share", type=float, default=0.5)

@@ -3,6 +3,7 @@
 docker daemon here to apply/build them."""
 from pathlib import Path
 
+import pytest
 import yaml
 
 ROOT = Path(__file__).resolve().parent.parent
@@ -82,3 +83,17 @@ def test_systemd_units_render(tmp_path):
     px = (tmp_path / "hola-rrproxy.service").read_text()
     assert "--port 8080" in px and "--backends 127.0.0.1:18080,127.0.0.1:18081" in px
     assert "hola-replica1.service" in (tmp_path / "hola.target").read_text()
+
+
+def test_systemd_units_reuseport(tmp_path):
+    from hola_amd.deploy import render_units
+
+    units = render_units(replicas=3, lb="reuseport", public_port=80)
+    assert sorted(units) == ["hola-replica0.service", "hola-replica1.service", "hola-replica2.service", "hola.target"]
+    for i in range(3):
+        u = units[f"hola-replica{i}.service"]
+        assert "--port 80 --accept reuseport" in u and "--host 127.0.0.1" not in u
+        assert "AmbientCapabilities=CAP_NET_BIND_SERVICE" in u  # binds :80 itself
+    assert "SO_REUSEPORT" in units["hola.target"]
+    with pytest.raises(ValueError):
+        render_units(replicas=1, lb="dns")

@@ -2,6 +2,8 @@
 import importlib.util
 from pathlib import Path
 
+import pytest
+
 ROOT = Path(__file__).resolve().parent.parent
 
 
@@ -26,9 +28,10 @@ def test_cli_info_and_help(capsys):
     assert main([]) == 0
 
 
-def test_cli_cluster_round_robin(hola_bin):
-    """`python -m hola_amd cluster`: 2 supervised replicas behind the round-robin proxy,
-    stopped with SIGINT (what Ctrl-C does)."""
+@pytest.mark.parametrize("lb", ["proxy", "reuseport"])
+def test_cli_cluster_round_robin(hola_bin, lb):
+    """`python -m hola_amd cluster`: 2 supervised replicas behind the round-robin proxy or in
+    one SO_REUSEPORT group, stopped with SIGINT (what Ctrl-C does)."""
     import http.client
     import signal
     import subprocess
@@ -39,7 +42,7 @@ def test_cli_cluster_round_robin(hola_bin):
 
     port = free_port()
     p = subprocess.Popen([sys.executable, "-m", "hola_amd", "cluster", "--replicas", "2", "--port", str(port),
-                          "--proxy-threads", "1"], cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                          "--proxy-threads", "1", "--lb", lb], cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
                          text=True)
     try:
         line = ""
@@ -48,7 +51,7 @@ def test_cli_cluster_round_robin(hola_bin):
             line = p.stdout.readline()
         assert "hola cluster:" in line, line
         seen = set()
-        for _ in range(8):
+        for _ in range(8 if lb == "proxy" else 60):  # reuseport: kernel hash, not strict rotation
             c = http.client.HTTPConnection("127.0.0.1", port, timeout=5)
             c.request("GET", "/api/hola")
             r = c.getresponse()

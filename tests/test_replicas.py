@@ -69,6 +69,20 @@ def test_kill_replica_under_load_client_rr():
             lg.close()
 
 
+def test_reuseport_group_spreads_and_survives_a_kill():
+    """--lb reuseport: replicas share one port; the kernel spreads connections over the
+    SO_REUSEPORT group, and a killed replica's listeners leave it, so every new connection
+    lands on a live replica (no proxy, no health check needed)."""
+    with ReplicaSet(3, threads_per_replica=1, supervise=False, shared_port=0) as rs:
+        assert len(set(rs.ports)) == 1 and rs.targets == [("127.0.0.1", rs.shared_port)]
+        seen = {greeting_via(rs.shared_port) for _ in range(60)}
+        assert seen == {"Hola de replica-0", "Hola de replica-1", "Hola de replica-2"}
+        rs.kill(1)
+        after = [greeting_via(rs.shared_port) for _ in range(40)]
+        assert "Hola de replica-1" not in after
+        assert set(after) == {"Hola de replica-0", "Hola de replica-2"}
+
+
 def test_graceful_shutdown_drains_inflight(hola):
     """SIGTERM while a chaining request waits on a slow aloha: the response still completes."""
     from hola_amd.testing.fakes import FakeAloha
