@@ -12,7 +12,9 @@ with --pool so it measures the path rather than the (intentionally tiny) default
 """
 import argparse
 import json
+import os
 import sys
+import time
 from pathlib import Path
 
 sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
@@ -28,6 +30,14 @@ ap.add_argument("--pool", type=int, default=128, help="hystrix thread-pool (bulk
 ap.add_argument("--out", default="")
 a = ap.parse_args()
 
+
+
+def cpu_s(pid: int) -> float:
+    """utime + stime of a process, in seconds."""
+    f = Path(f"/proc/{pid}/stat").read_text().rsplit(")", 1)[1].split()
+    return (int(f[11]) + int(f[12])) / os.sysconf("SC_CLK_TCK")
+
+
 cores = plan_node(3)  # A, B, load generator
 # B answers /api/hola-chaining itself with its own fallback (its aloha is unreachable and its
 # breaker opens), so A decodes ["Hola de B", "Aloha response (fallback)"].
@@ -40,13 +50,19 @@ with HolaProcess(args=["--aloha-url", "http://127.0.0.1:1/", "--feign-log", "non
         st, _, body = s.get("/api/hola-chaining")
         assert st == 200, body
         sample = json.loads(body)
+        c0, w0 = (cpu_s(s.proc.pid), cpu_s(b.proc.pid)), time.perf_counter()
         res = run_duration([("127.0.0.1", s.port)], a.connections, len(cores[2]), a.duration, 2.0,
                            cpu_list=format_cpu_list(cores[2]), path="/api/hola-chaining")
+        wall = time.perf_counter() - w0
+        busy = {"A": (cpu_s(s.proc.pid) - c0[0]) / wall, "B": (cpu_s(b.proc.pid) - c0[1]) / wall}
         _, _, metrics = s.get("/metrics")
 events = {l.split('event="')[1].split('"')[0]: int(l.split()[-1]) for l in metrics.decode().splitlines()
           if l.startswith("hola_hystrix_events_total")}
 out = {"sample": sample, "rps": res["rps"], "p50_ms": res["latency"]["p50_ns"] / 1e6,
        "p99_ms": res["latency"]["p99_ns"] / 1e6, "errors": res["latency"]["errors"], "hystrix_events": events,
+       # cores kept busy (warmup included) and CPU µs per request at the measured rate
+       "cpus_busy": {k: round(v, 2) for k, v in busy.items()},
+       "cpu_us_per_req": {k: round(v / res["rps"] * 1e6, 2) for k, v in busy.items()},
        "cpu_map": {"A": format_cpu_list(cores[0]), "B": format_cpu_list(cores[1]), "loadgen": format_cpu_list(cores[2])}}
 print(json.dumps(out))
 if a.out:

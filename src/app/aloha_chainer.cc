@@ -61,6 +61,13 @@ ChainResult fallback_result(const char* why) {
   r.items.push_back(std::string(kFallbackGreeting));
   return r;
 }
+
+// Short-circuited / rejected calls are the hot fallbacks when aloha is down: built once.
+const ChainResult& static_fallback(Command::Admit a) {
+  static const ChainResult short_circuited = fallback_result("short-circuited");
+  static const ChainResult rejected = fallback_result("thread-pool-rejected");
+  return a == Command::Admit::kShortCircuited ? short_circuited : rejected;
+}
 }  // namespace
 
 void AlohaChainer::call(http::Worker& w, const tracing::SpanContext* parent,
@@ -73,13 +80,12 @@ void AlohaChainer::call(http::Worker& w, const tracing::SpanContext* parent,
 
   Command::Admit a = url_ok_ ? cmd->try_start() : Command::Admit::kRun;
   if (a != Command::Admit::kRun) {
-    const char* why = a == Command::Admit::kShortCircuited ? "short-circuited" : "thread-pool-rejected";
     cmd->rejected(clock_.now_ms() - call->start_ms);
-    loop.add_timer(0, [call, why] { call->cb(fallback_result(why)); });
+    call->cb(static_fallback(a));
     return;
   }
   if (!url_ok_) {
-    loop.add_timer(0, [call] { call->cb(fallback_result("bad-url")); });
+    call->cb(fallback_result("bad-url"));
     return;
   }
   std::string headers;

@@ -28,7 +28,9 @@ struct ChainResult {
 class Chainer {
  public:
   virtual ~Chainer() = default;
-  // Runs on the worker thread; `done` is invoked exactly once, later, on the same thread.
+  // Runs on the worker thread; `done` is invoked exactly once, on the same thread. It may run
+  // before call() returns: Hystrix runs the fallback of a short-circuited or rejected command
+  // on the caller's thread, and so does this (no timer round trip).
   virtual void call(http::Worker& w, const tracing::SpanContext* parent,
                     std::function<void(const ChainResult&)> done) = 0;
 };

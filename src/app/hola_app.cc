@@ -396,7 +396,19 @@ void HolaApp::handle_chaining(http::Connection& c, const http::Request& r, Worke
   chainer_->call(c.worker(), traced ? &span.ctx : nullptr,
                  [self, conn, content, ka, head, traced, span, t0](const ChainResult& res) {
                    http::Worker& w = conn->worker();
-                   if (!conn->closed()) {
+                   WorkerCache& wc = self->cache(w);
+                   bool answered = false;
+                   if (!conn->closed() && res.fallback) {
+                     // The prepared ["<greeting>","Aloha response (fallback)"] response, if the
+                     // configuration has not changed since the request arrived.
+                     if (wc.gen != self->gen_.load(std::memory_order_relaxed) || wc.date_version != w.date_version())
+                       self->refresh(w, wc);
+                     if (wc.content == content) {
+                       conn->complete(wc.chaining_fallback[ka][head].view(), ka);
+                       answered = true;
+                     }
+                   }
+                   if (!answered && !conn->closed()) {
                      std::vector<std::optional<std::string>> items;
                      items.reserve(1 + res.items.size());
                      items.push_back(content->greeting);

@@ -4,6 +4,10 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <atomic>
+#include <thread>
+
+
 #include "config/jformat.h"
 #include "config/properties.h"
 #include "config/resolver.h"
@@ -182,6 +186,59 @@ struct PyCommand {
   }
 };
 
+// Hammers one Command from `threads` C++ threads (the server's workers share one): every
+// admitted call completes (failing every `fail_every`-th, 0 = never), every other call takes
+// the fallback. Returns the callers' own tallies next to the Command's merged snapshot so
+// tests can check the sharded counters and the atomic bulkhead add up.
+py::dict hystrix_stress(int threads, int iters, int pool, int fail_every, int volume) {
+  resilience::Settings st;
+  st.pool_core_size = pool;
+  st.request_volume_threshold = volume;
+  st.health_snapshot_ms = 0;
+  st.sleep_window_ms = 1;
+  SystemClock clk;
+  resilience::Command cmd("stress", "g", "g", st, clk);
+  std::atomic<int64_t> runs{0}, fails{0}, shorts{0}, rejects{0};
+  std::vector<std::thread> ts;
+  {
+    py::gil_scoped_release nogil;
+    for (int t = 0; t < threads; ++t)
+      ts.emplace_back([&, t] {
+        int64_t r = 0, f = 0, sc = 0, rj = 0;
+        for (int i = 0; i < iters; ++i) {
+          auto a = cmd.try_start();
+          if (a == resilience::Command::Admit::kRun) {
+            bool fail = fail_every > 0 && (i + t) % fail_every == 0;
+            cmd.complete(fail ? resilience::Event::kFailure : resilience::Event::kSuccess, 1, fail, 1);
+            ++r;
+            f += fail;
+          } else {
+            cmd.rejected(0);
+            (a == resilience::Command::Admit::kShortCircuited ? sc : rj) += 1;
+          }
+        }
+        runs += r;
+        fails += f;
+        shorts += sc;
+        rejects += rj;
+      });
+    for (auto& th : ts) th.join();
+  }
+  auto snap = cmd.snapshot();
+  py::dict d, ev;
+  for (int e = 0; e < resilience::kNumEvents; ++e)
+    if (snap.cumulative[size_t(e)]) ev[resilience::event_name(resilience::Event(e))] = snap.cumulative[size_t(e)];
+  d["runs"] = runs.load();
+  d["failures"] = fails.load();
+  d["short_circuited"] = shorts.load();
+  d["rejected"] = rejects.load();
+  d["events"] = ev;
+  d["concurrent"] = snap.concurrent;
+  d["largest"] = snap.pool_largest;
+  d["completed"] = snap.pool_completed;
+  return d;
+}
+
 std::string encode_spans_py(bool v2, const std::string& trace_id, const std::string& span_id, py::object parent,
                             const std::string& kind, int64_t start_us, int64_t end_us, const std::string& url,
                             int status, bool shared) {
@@ -283,6 +340,8 @@ PYBIND11_MODULE(_native, m) {
   m.def("histogram_percentiles", &histogram_percentiles);
   m.def("loop_timer_order", &loop_timer_order, py::arg("delays"), py::arg("cancel") = std::vector<int>{});
   m.def("span_ring", &span_ring);
+  m.def("hystrix_stress", &hystrix_stress, py::arg("threads"), py::arg("iters"), py::arg("pool") = 10,
+        py::arg("fail_every") = 0, py::arg("volume") = 20);
   py::class_<PyCommand>(m, "HystrixCommand")
       .def(py::init<const std::map<std::string, std::string>&>(), py::arg("props") = std::map<std::string, std::string>{})
       .def("try_start", &PyCommand::try_start)

@@ -181,9 +181,7 @@ void RollingPercentile::add(int64_t now, int64_t v) {
   ++b.count;
 }
 
-void RollingPercentile::merged(int64_t now, std::array<uint64_t, kBins>* h, int64_t* sum, int64_t* count) {
-  h->fill(0);
-  *sum = *count = 0;
+void RollingPercentile::accumulate(int64_t now, Bins* h, int64_t* sum, int64_t* count) const {
   int64_t lo = now - (now % bucket_ms_) - int64_t(window_ms_) + bucket_ms_;
   for (const Bucket& b : b_) {
     if (b.start < lo || b.start > now) continue;
@@ -193,10 +191,7 @@ void RollingPercentile::merged(int64_t now, std::array<uint64_t, kBins>* h, int6
   }
 }
 
-int64_t RollingPercentile::percentile(int64_t now, double p) {
-  std::array<uint64_t, kBins> h;
-  int64_t sum, count;
-  merged(now, &h, &sum, &count);
+int64_t RollingPercentile::percentile_of(const Bins& h, int64_t count, double p) {
   if (count == 0) return 0;
   if (p <= 0) {
     for (int i = 0; i < kBins; ++i)
@@ -213,144 +208,221 @@ int64_t RollingPercentile::percentile(int64_t now, double p) {
   return bin_value(kBins - 1);
 }
 
+int64_t RollingPercentile::percentile(int64_t now, double p) {
+  Bins h{};
+  int64_t sum = 0, count = 0;
+  accumulate(now, &h, &sum, &count);
+  return percentile_of(h, count, p);
+}
+
 int64_t RollingPercentile::mean(int64_t now) {
-  std::array<uint64_t, kBins> h;
-  int64_t sum, count;
-  merged(now, &h, &sum, &count);
+  Bins h{};
+  int64_t sum = 0, count = 0;
+  accumulate(now, &h, &sum, &count);
   return count ? sum / count : 0;
 }
 
 // ---------------------------------------------------------------- Command
 
-Command::Command(std::string name, std::string group, std::string pool, Settings s, const Clock& clock)
-    : name_(std::move(name)),
-      group_(std::move(group)),
-      pool_(std::move(pool)),
-      s_(s),
-      clock_(clock),
-      counter_(s.rolling_window_ms, s.rolling_buckets),
-      pool_counter_(s.rolling_window_ms, s.rolling_buckets),
-      exec_lat_(s.percentile_window_ms, s.percentile_buckets),
-      total_lat_(s.percentile_window_ms, s.percentile_buckets) {}
+struct alignas(64) Command::Shard {
+  std::mutex mu;
+  RollingCounter counter, pool_counter;
+  RollingPercentile exec_lat, total_lat;
+  int64_t completed = 0;
+  explicit Shard(const Settings& s)
+      : counter(s.rolling_window_ms, s.rolling_buckets),
+        pool_counter(s.rolling_window_ms, s.rolling_buckets),
+        exec_lat(s.percentile_window_ms, s.percentile_buckets),
+        total_lat(s.percentile_window_ms, s.percentile_buckets) {}
+};
 
-HealthCounts Command::health_locked(int64_t now) {
-  if (health_at_ >= 0 && now - health_at_ < s_.health_snapshot_ms) return health_cache_;
-  auto c = counter_.sums(now);
+Command::Command(std::string name, std::string group, std::string pool, Settings s, const Clock& clock)
+    : name_(std::move(name)), group_(std::move(group)), pool_(std::move(pool)), clock_(clock), s_(s) {
+  apply_hot(s);
+  for (int i = 0; i < kShards; ++i) shards_.push_back(std::make_unique<Shard>(s));
+}
+
+Command::~Command() = default;
+
+void Command::apply_hot(const Settings& s) {
+  circuit_enabled_.store(s.circuit_enabled, std::memory_order_relaxed);
+  force_open_.store(s.force_open, std::memory_order_relaxed);
+  force_closed_.store(s.force_closed, std::memory_order_relaxed);
+  volume_.store(s.request_volume_threshold, std::memory_order_relaxed);
+  error_pct_.store(s.error_threshold_pct, std::memory_order_relaxed);
+  sleep_window_ms_.store(s.sleep_window_ms, std::memory_order_relaxed);
+  pool_core_.store(s.pool_core_size, std::memory_order_relaxed);
+  health_ms_.store(s.health_snapshot_ms, std::memory_order_relaxed);
+}
+
+Command::Shard& Command::shard() {
+  // Threads are dealt shards round-robin on first use: one event-loop worker per shard up
+  // to kShards workers, so shard mutexes are in practice uncontended.
+  static std::atomic<unsigned> next{0};
+  thread_local unsigned idx = next.fetch_add(1, std::memory_order_relaxed);
+  return *shards_[idx % kShards];
+}
+
+HealthCounts Command::health_at(int64_t now) {
+  int64_t at = health_at_.load(std::memory_order_acquire);
+  if (at < 0 || now - at >= health_ms_.load(std::memory_order_relaxed)) {
+    // One thread refreshes; the others keep deciding on the previous snapshot meanwhile
+    // (Hystrix's HealthCountsStream publishes snapshots the same way).
+    std::unique_lock<std::mutex> g(health_mu_, std::try_to_lock);
+    if (g.owns_lock()) {
+      at = health_at_.load(std::memory_order_relaxed);
+      if (at < 0 || now - at >= health_ms_.load(std::memory_order_relaxed)) {
+        std::array<int64_t, kNumEvents> c{};
+        for (auto& sh : shards_) {
+          std::lock_guard<std::mutex> l(sh->mu);
+          auto part = sh->counter.sums(now);
+          for (int i = 0; i < kNumEvents; ++i) c[size_t(i)] += part[size_t(i)];
+        }
+        uint64_t errors = uint64_t(c[size_t(Event::kFailure)] + c[size_t(Event::kTimeout)] +
+                                   c[size_t(Event::kThreadPoolRejected)] + c[size_t(Event::kSemaphoreRejected)]);
+        uint64_t total = errors + uint64_t(c[size_t(Event::kSuccess)]);
+        health_packed_.store((std::min<uint64_t>(total, 0xffffffffu) << 32) | std::min<uint64_t>(errors, 0xffffffffu),
+                             std::memory_order_relaxed);
+        health_at_.store(now, std::memory_order_release);
+      }
+    }
+  }
+  uint64_t packed = health_packed_.load(std::memory_order_relaxed);
   HealthCounts h;
-  h.errors = c[size_t(Event::kFailure)] + c[size_t(Event::kTimeout)] + c[size_t(Event::kThreadPoolRejected)] +
-             c[size_t(Event::kSemaphoreRejected)];
-  h.total = h.errors + c[size_t(Event::kSuccess)];
+  h.total = int64_t(packed >> 32);
+  h.errors = int64_t(packed & 0xffffffffu);
   h.error_pct = h.total > 0 ? int(double(h.errors) / double(h.total) * 100.0) : 0;
-  health_cache_ = h;
-  health_at_ = now;
   return h;
 }
 
-bool Command::is_open_locked(int64_t now) {
-  if (open_) return true;
-  HealthCounts h = health_locked(now);
-  if (h.total < s_.request_volume_threshold) return false;
-  if (h.error_pct < s_.error_threshold_pct) return false;
-  open_ = true;
-  opened_or_tested_ = now;
+bool Command::is_open(int64_t now) {
+  if (open_.load(std::memory_order_acquire)) return true;
+  HealthCounts h = health_at(now);
+  if (h.total < volume_.load(std::memory_order_relaxed)) return false;
+  if (h.error_pct < error_pct_.load(std::memory_order_relaxed)) return false;
+  bool expected = false;
+  if (open_.compare_exchange_strong(expected, true)) opened_or_tested_.store(now, std::memory_order_release);
   return true;
 }
 
-bool Command::allow_request_locked(int64_t now) {
-  if (!s_.circuit_enabled) return true;
-  if (s_.force_open) return false;
-  if (s_.force_closed) {
-    is_open_locked(now);  // still tracks the would-be state
+bool Command::allow_request(int64_t now) {
+  if (!circuit_enabled_.load(std::memory_order_relaxed)) return true;
+  if (force_open_.load(std::memory_order_relaxed)) return false;
+  if (force_closed_.load(std::memory_order_relaxed)) {
+    is_open(now);  // still tracks the would-be state
     return true;
   }
-  if (!is_open_locked(now)) return true;
-  // allowSingleTest(): one trial per sleep window
-  if (open_ && now > opened_or_tested_ + s_.sleep_window_ms) {
-    opened_or_tested_ = now;
-    return true;
-  }
+  if (!is_open(now)) return true;
+  // allowSingleTest(): one trial per sleep window, won by a single CAS.
+  int64_t t = opened_or_tested_.load(std::memory_order_acquire);
+  if (open_.load(std::memory_order_acquire) && now > t + sleep_window_ms_.load(std::memory_order_relaxed))
+    return opened_or_tested_.compare_exchange_strong(t, now);
   return false;
 }
 
 Command::Admit Command::try_start() {
-  std::lock_guard<std::mutex> g(mu_);
   int64_t now = clock_.now_ms();
-  executed_ = true;
-  if (!allow_request_locked(now)) {
-    counter_.add(now, Event::kShortCircuited);
+  if (!executed_.load(std::memory_order_relaxed)) executed_.store(true, std::memory_order_relaxed);
+  if (!allow_request(now)) {
+    Shard& sh = shard();
+    std::lock_guard<std::mutex> g(sh.mu);
+    sh.counter.add(now, Event::kShortCircuited);
     return Admit::kShortCircuited;
   }
-  if (active_ >= s_.pool_core_size) {  // SynchronousQueue: no waiting room
-    counter_.add(now, Event::kThreadPoolRejected);
-    pool_counter_.add(now, Event::kThreadPoolRejected);
+  int64_t active = active_.fetch_add(1, std::memory_order_acq_rel) + 1;
+  if (active > pool_core_.load(std::memory_order_relaxed)) {  // SynchronousQueue: no waiting room
+    active_.fetch_sub(1, std::memory_order_acq_rel);
+    Shard& sh = shard();
+    std::lock_guard<std::mutex> g(sh.mu);
+    sh.counter.add(now, Event::kThreadPoolRejected);
+    sh.pool_counter.add(now, Event::kThreadPoolRejected);
     return Admit::kRejected;
   }
-  ++active_;
-  largest_ = std::max(largest_, active_);
-  counter_.update_max_concurrency(now, active_);
-  pool_counter_.update_max_concurrency(now, active_);
-  pool_counter_.add(now, Event::kSuccess);  // "threads executed"
+  int64_t largest = largest_.load(std::memory_order_relaxed);
+  while (active > largest && !largest_.compare_exchange_weak(largest, active, std::memory_order_relaxed)) {
+  }
+  Shard& sh = shard();
+  std::lock_guard<std::mutex> g(sh.mu);
+  sh.counter.update_max_concurrency(now, active);
+  sh.pool_counter.update_max_concurrency(now, active);
+  sh.pool_counter.add(now, Event::kSuccess);  // "threads executed"
   return Admit::kRun;
 }
 
-void Command::finish_locked(int64_t now, Event outcome, int64_t execute_ms) {
-  if (active_ > 0) --active_;
-  ++completed_;
-  counter_.add(now, outcome);
-  if (outcome == Event::kSuccess) {
-    exec_lat_.add(now, execute_ms);
-    if (open_) {  // markSuccess(): close and reset the health stream
-      open_ = false;
-      counter_.reset(now);
-      health_at_ = -1;
-    }
-  } else if (outcome == Event::kFailure) {
-    exec_lat_.add(now, execute_ms);
+void Command::finish_in(Shard& sh, int64_t now, Event outcome, int64_t execute_ms) {
+  int64_t a = active_.load(std::memory_order_relaxed);
+  while (a > 0 && !active_.compare_exchange_weak(a, a - 1, std::memory_order_acq_rel)) {
   }
+  ++sh.completed;
+  sh.counter.add(now, outcome);
+  if (outcome == Event::kSuccess || outcome == Event::kFailure) sh.exec_lat.add(now, execute_ms);
+}
+
+void Command::mark_success(int64_t now) {
+  // markSuccess(): close the circuit and reset the health stream (only the thread whose CAS
+  // closes it does the reset).
+  if (!open_.load(std::memory_order_acquire)) return;
+  bool expected = true;
+  if (!open_.compare_exchange_strong(expected, false)) return;
+  std::lock_guard<std::mutex> h(health_mu_);  // no snapshot refresh may straddle the reset
+  for (auto& sh : shards_) {
+    std::lock_guard<std::mutex> g(sh->mu);
+    sh->counter.reset(now);
+  }
+  health_packed_.store(0, std::memory_order_relaxed);
+  health_at_.store(-1, std::memory_order_release);
 }
 
 void Command::finish(Event outcome, int64_t execute_ms) {
-  std::lock_guard<std::mutex> g(mu_);
-  finish_locked(clock_.now_ms(), outcome, execute_ms);
+  int64_t now = clock_.now_ms();
+  {
+    Shard& sh = shard();
+    std::lock_guard<std::mutex> g(sh.mu);
+    finish_in(sh, now, outcome, execute_ms);
+  }
+  if (outcome == Event::kSuccess) mark_success(now);
 }
 
 void Command::complete(Event outcome, int64_t execute_ms, bool with_fallback, int64_t total_ms) {
-  std::lock_guard<std::mutex> g(mu_);
   int64_t now = clock_.now_ms();
-  finish_locked(now, outcome, execute_ms);
-  if (with_fallback) counter_.add(now, Event::kFallbackSuccess);
-  total_lat_.add(now, total_ms);
+  {
+    Shard& sh = shard();
+    std::lock_guard<std::mutex> g(sh.mu);
+    finish_in(sh, now, outcome, execute_ms);
+    if (with_fallback) sh.counter.add(now, Event::kFallbackSuccess);
+    sh.total_lat.add(now, total_ms);
+  }
+  if (outcome == Event::kSuccess) mark_success(now);
 }
 
 void Command::rejected(int64_t total_ms) {
-  std::lock_guard<std::mutex> g(mu_);
   int64_t now = clock_.now_ms();
-  counter_.add(now, Event::kFallbackSuccess);
-  total_lat_.add(now, total_ms);
+  Shard& sh = shard();
+  std::lock_guard<std::mutex> g(sh.mu);
+  sh.counter.add(now, Event::kFallbackSuccess);
+  sh.total_lat.add(now, total_ms);
 }
 
 void Command::fallback(Event e) {
-  std::lock_guard<std::mutex> g(mu_);
-  counter_.add(clock_.now_ms(), e);
+  int64_t now = clock_.now_ms();
+  Shard& sh = shard();
+  std::lock_guard<std::mutex> g(sh.mu);
+  sh.counter.add(now, e);
 }
 
 void Command::total_latency(int64_t total_ms) {
-  std::lock_guard<std::mutex> g(mu_);
-  total_lat_.add(clock_.now_ms(), total_ms);
+  int64_t now = clock_.now_ms();
+  Shard& sh = shard();
+  std::lock_guard<std::mutex> g(sh.mu);
+  sh.total_lat.add(now, total_ms);
 }
 
-bool Command::circuit_open() {
-  std::lock_guard<std::mutex> g(mu_);
-  return is_open_locked(clock_.now_ms());
-}
+bool Command::circuit_open() { return is_open(clock_.now_ms()); }
 
-HealthCounts Command::health() {
-  std::lock_guard<std::mutex> g(mu_);
-  return health_locked(clock_.now_ms());
-}
+HealthCounts Command::health() { return health_at(clock_.now_ms()); }
 
 void Command::update_settings(const Settings& s) {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<std::mutex> g(settings_mu_);
   // Window geometry is fixed at construction (as in Hystrix); the rest is dynamic.
   int rw = s_.rolling_window_ms, rb = s_.rolling_buckets, pw = s_.percentile_window_ms, pb = s_.percentile_buckets;
   s_ = s;
@@ -358,43 +430,56 @@ void Command::update_settings(const Settings& s) {
   s_.rolling_buckets = rb;
   s_.percentile_window_ms = pw;
   s_.percentile_buckets = pb;
+  apply_hot(s_);
 }
 
 Settings Command::settings() {
-  std::lock_guard<std::mutex> g(mu_);
+  std::lock_guard<std::mutex> g(settings_mu_);
   return s_;
 }
 
 CommandSnapshot Command::snapshot() {
-  std::lock_guard<std::mutex> g(mu_);
   int64_t now = clock_.now_ms();
   CommandSnapshot s;
   s.name = name_;
   s.group = group_;
   s.pool = pool_;
   s.now_wall_ms = wall_ms();
-  s.circuit_open = is_open_locked(now);
-  s.health = health_locked(now);
-  s.rolling = counter_.sums(now);
-  s.cumulative = counter_.cumulative();
-  s.concurrent = active_;
-  s.rolling_max_concurrent = counter_.max_concurrency(now);
+  s.circuit_open = is_open(now);
+  s.health = health_at(now);
+  RollingPercentile::Bins exec_h{}, total_h{};
+  int64_t exec_sum = 0, exec_n = 0, total_sum = 0, total_n = 0;
+  std::array<int64_t, kNumEvents> pc{};
+  for (auto& sh : shards_) {
+    std::lock_guard<std::mutex> g(sh->mu);
+    auto r = sh->counter.sums(now);
+    auto c = sh->counter.cumulative();
+    auto p = sh->pool_counter.sums(now);
+    for (int i = 0; i < kNumEvents; ++i) {
+      s.rolling[size_t(i)] += r[size_t(i)];
+      s.cumulative[size_t(i)] += c[size_t(i)];
+      pc[size_t(i)] += p[size_t(i)];
+    }
+    s.rolling_max_concurrent = std::max(s.rolling_max_concurrent, sh->counter.max_concurrency(now));
+    s.pool_rolling_max_active = std::max(s.pool_rolling_max_active, sh->pool_counter.max_concurrency(now));
+    s.pool_completed += sh->completed;
+    sh->exec_lat.accumulate(now, &exec_h, &exec_sum, &exec_n);
+    sh->total_lat.accumulate(now, &total_h, &total_sum, &total_n);
+  }
+  s.concurrent = active_.load(std::memory_order_relaxed);
   static const double kPcts[9] = {0, 25, 50, 75, 90, 95, 99, 99.5, 100};
   for (int i = 0; i < 9; ++i) {
-    s.latency_execute[size_t(i)] = exec_lat_.percentile(now, kPcts[i]);
-    s.latency_total[size_t(i)] = total_lat_.percentile(now, kPcts[i]);
+    s.latency_execute[size_t(i)] = RollingPercentile::percentile_of(exec_h, exec_n, kPcts[i]);
+    s.latency_total[size_t(i)] = RollingPercentile::percentile_of(total_h, total_n, kPcts[i]);
   }
-  s.latency_execute_mean = exec_lat_.mean(now);
-  s.latency_total_mean = total_lat_.mean(now);
-  s.settings = s_;
-  auto pc = pool_counter_.sums(now);
-  s.pool_active = active_;
-  s.pool_largest = largest_;
-  s.pool_completed = completed_;
+  s.latency_execute_mean = exec_n ? exec_sum / exec_n : 0;
+  s.latency_total_mean = total_n ? total_sum / total_n : 0;
+  s.settings = settings();
+  s.pool_active = s.concurrent;
+  s.pool_largest = largest_.load(std::memory_order_relaxed);
   s.pool_rolling_executed = pc[size_t(Event::kSuccess)];
   s.pool_rolling_rejected = pc[size_t(Event::kThreadPoolRejected)];
-  s.pool_rolling_max_active = pool_counter_.max_concurrency(now);
-  s.has_executed = executed_;
+  s.has_executed = executed_.load(std::memory_order_relaxed);
   return s;
 }
 

@@ -16,8 +16,10 @@
 // All time comes from an injectable Clock so tests can drive the state machine.
 #pragma once
 #include <array>
+#include <atomic>
 #include <cstdint>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -94,23 +96,26 @@ class RollingCounter {
 // Rolling latency percentiles (log-linear histogram per bucket, 0.1 ms .. ~1 h).
 class RollingPercentile {
  public:
+  static constexpr int kBins = 512;
+  using Bins = std::array<uint64_t, kBins>;
   RollingPercentile(int window_ms, int buckets);
   void add(int64_t now_ms, int64_t value_ms);
   // Percentile in ms for p in [0,100]; mean. Returns 0 when empty.
   int64_t percentile(int64_t now_ms, double p);
   int64_t mean(int64_t now_ms);
+  // Adds this window's live buckets into (*h, *sum, *count): merging across shards.
+  void accumulate(int64_t now_ms, Bins* h, int64_t* sum, int64_t* count) const;
+  static int64_t percentile_of(const Bins& h, int64_t count, double p);
 
  private:
-  static constexpr int kBins = 512;
   static int bin_of(int64_t v);
   static int64_t bin_value(int b);
   struct Bucket {
     int64_t start = -1;
-    std::array<uint32_t, kBins> h{};
+    Bins h{};
     int64_t sum = 0, count = 0;
   };
   Bucket& current(int64_t now_ms);
-  void merged(int64_t now_ms, std::array<uint64_t, kBins>* h, int64_t* sum, int64_t* count);
   int window_ms_, nb_, bucket_ms_;
   std::vector<Bucket> b_;
 };
@@ -137,9 +142,15 @@ struct CommandSnapshot {
   bool has_executed = false;
 };
 
+// Concurrency: the request path never takes a shared lock. Breaker state, the health
+// snapshot and the bulkhead are atomics (as in Hystrix: AtomicBoolean circuitOpen, AtomicLong
+// circuitOpenedOrLastTestedTime, a volatile HealthCounts). Rolling counters and latency
+// histograms are sharded per thread, each shard behind its own (uncontended) mutex, and
+// merged when the health snapshot is refreshed or the stream/metrics read them.
 class Command {
  public:
   Command(std::string name, std::string group, std::string pool, Settings s, const Clock& clock);
+  ~Command();
 
   enum class Admit { kRun, kShortCircuited, kRejected };
   // Breaker + bulkhead admission. kRun takes a bulkhead slot that finish() releases.
@@ -150,9 +161,9 @@ class Command {
   // and the total latency of the whole command.
   void fallback(Event fallback_event);
   void total_latency(int64_t total_ms);
-  // finish() + optional fallback() + total_latency() under one lock acquisition.
+  // finish() + optional fallback() + total_latency() in one shard visit.
   void complete(Event outcome, int64_t execute_ms, bool with_fallback, int64_t total_ms);
-  // Short-circuit / rejection path: fallback + total latency under one lock.
+  // Short-circuit / rejection path: fallback + total latency in one shard visit.
   void rejected(int64_t total_ms);
 
   bool circuit_open();            // evaluates health like HystrixCircuitBreaker.isOpen()
@@ -163,24 +174,34 @@ class Command {
   const std::string& name() const { return name_; }
 
  private:
-  void finish_locked(int64_t now, Event outcome, int64_t execute_ms);
-  bool is_open_locked(int64_t now);
-  bool allow_request_locked(int64_t now);
-  HealthCounts health_locked(int64_t now);
+  struct Shard;
+  static constexpr int kShards = 16;
+  Shard& shard();
+  void finish_in(Shard& sh, int64_t now, Event outcome, int64_t execute_ms);
+  void mark_success(int64_t now);
+  bool is_open(int64_t now);
+  bool allow_request(int64_t now);
+  HealthCounts health_at(int64_t now);
+  void apply_hot(const Settings& s);
 
   std::string name_, group_, pool_;
-  Settings s_;
   const Clock& clock_;
-  std::mutex mu_;
-  RollingCounter counter_;
-  RollingCounter pool_counter_;
-  RollingPercentile exec_lat_, total_lat_;
-  bool open_ = false;
-  int64_t opened_or_tested_ = 0;
-  HealthCounts health_cache_;
-  int64_t health_at_ = -1;
-  int64_t active_ = 0, largest_ = 0, completed_ = 0;
-  bool executed_ = false;
+  std::mutex settings_mu_;  // full Settings (snapshot/settings(); rare)
+  Settings s_;
+  // Settings read on every call, updated by config reloads.
+  std::atomic<bool> circuit_enabled_{true}, force_open_{false}, force_closed_{false};
+  std::atomic<int> volume_{20}, error_pct_{50}, sleep_window_ms_{5000}, pool_core_{10}, health_ms_{500};
+  std::vector<std::unique_ptr<Shard>> shards_;
+  // breaker (HystrixCircuitBreakerImpl)
+  std::atomic<bool> open_{false};
+  std::atomic<int64_t> opened_or_tested_{0};
+  // health snapshot: (total << 32 | errors), refreshed at most every health_ms_
+  std::mutex health_mu_;
+  std::atomic<int64_t> health_at_{-1};
+  std::atomic<uint64_t> health_packed_{0};
+  // bulkhead (thread pool of pool_core_ threads, no queue)
+  std::atomic<int64_t> active_{0}, largest_{0};
+  std::atomic<bool> executed_{false};
 };
 
 }  // namespace hola::resilience

@@ -182,3 +182,23 @@ def test_stream_connection_limit(hola):
     time.sleep(0.2)
     out = _read_sse(s.port, seconds=0.3)
     assert b"200 OK" in out
+
+
+@pytest.mark.parametrize("fail_every", [0, 1, 3])
+def test_concurrent_accounting_adds_up(native, fail_every):
+    """8 C++ threads share one command (as the server's workers do). The per-thread metric
+    shards, the atomic bulkhead and the CAS-driven breaker must account for every call."""
+    r = native.hystrix_stress(threads=8, iters=20000, pool=4, fail_every=fail_every, volume=5)
+    ev = r["events"]
+    total = 8 * 20000
+    assert r["runs"] + r["short_circuited"] + r["rejected"] == total
+    assert ev.get("SUCCESS", 0) + ev.get("FAILURE", 0) == r["runs"] == r["completed"]
+    assert ev.get("FAILURE", 0) == r["failures"]
+    assert ev.get("SHORT_CIRCUITED", 0) == r["short_circuited"]
+    assert ev.get("THREAD_POOL_REJECTED", 0) == r["rejected"]
+    assert ev.get("FALLBACK_SUCCESS", 0) == r["failures"] + r["short_circuited"] + r["rejected"]
+    assert r["concurrent"] == 0 and 1 <= r["largest"] <= 4
+    if fail_every == 1:  # every call fails: the breaker must open and short-circuit most calls
+        assert r["short_circuited"] > total // 2
+    if fail_every == 0:
+        assert r["short_circuited"] == 0
