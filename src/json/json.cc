@@ -6,10 +6,20 @@
 
 namespace hola::json {
 
+namespace {
+// 1 = must be escaped: control characters, '"' and '\\'.
+constexpr bool needs_escape(unsigned char c) { return c < 0x20 || c == '"' || c == '\\'; }
+}  // namespace
+
 void append_string(std::string* out, std::string_view s) {
+  out->reserve(out->size() + s.size() + 2);
   out->push_back('"');
-  for (char ch : s) {
-    unsigned char c = (unsigned char)ch;
+  size_t run = 0;  // start of the pending run of characters copied verbatim
+  for (size_t i = 0; i < s.size(); ++i) {
+    unsigned char c = (unsigned char)s[i];
+    if (!needs_escape(c)) continue;
+    out->append(s.data() + run, i - run);
+    run = i + 1;
     switch (c) {
       case '"': out->append("\\\""); break;
       case '\\': out->append("\\\\"); break;
@@ -18,16 +28,14 @@ void append_string(std::string* out, std::string_view s) {
       case '\n': out->append("\\n"); break;
       case '\r': out->append("\\r"); break;
       case '\t': out->append("\\t"); break;
-      default:
-        if (c < 0x20) {
-          char buf[8];
-          snprintf(buf, sizeof buf, "\\u%04X", c);
-          out->append(buf);
-        } else {
-          out->push_back(ch);
-        }
+      default: {
+        char buf[8];
+        snprintf(buf, sizeof buf, "\\u%04X", c);
+        out->append(buf);
+      }
     }
   }
+  out->append(s.data() + run, s.size() - run);
   out->push_back('"');
 }
 
@@ -109,12 +117,12 @@ struct Parser {
         case 'r': out->push_back('\r'); break;
         case 't': out->push_back('\t'); break;
         case 'u': {
-          uint32_t v;
+          uint32_t v = 0;
           if (!hex4(&v)) return false;
           if (v >= 0xD800 && v <= 0xDBFF && i + 6 <= s.size() && s[i] == '\\' && s[i + 1] == 'u') {
             size_t save = i;
             i += 2;
-            uint32_t lo;
+            uint32_t lo = 0;
             if (hex4(&lo) && lo >= 0xDC00 && lo <= 0xDFFF) {
               config::append_utf8(out, 0x10000 + ((v - 0xD800) << 10) + (lo - 0xDC00));
               break;
@@ -225,7 +233,8 @@ struct Parser {
 }  // namespace
 
 bool parse(std::string_view in, Value* out, std::string* err) {
-  Parser p{in};
+  Parser p;
+  p.s = in;
   *out = Value();
   if (!p.value(out)) {
     if (err) *err = p.err;
@@ -241,24 +250,61 @@ bool parse(std::string_view in, Value* out, std::string* err) {
 
 bool decode_string_list(std::string_view in, std::vector<std::optional<std::string>>* out,
                         std::string* err) {
-  Value v;
-  if (!parse(in, &v, err)) return false;
+  // Streams straight into *out (no DOM): this runs once per aloha response.
+  Parser p;
+  p.s = in;
   out->clear();
-  if (v.type != Value::Type::kArray) {
-    if (err) *err = "expected a JSON array";
+  auto fail = [&](const std::string& m) {
+    if (err) *err = p.err.empty() ? m : p.err;
     return false;
+  };
+  p.ws();
+  if (p.i >= in.size() || in[p.i] != '[') {
+    if (p.i < in.size() && in[p.i] == '{') return fail("expected a JSON array");
+    Value v;  // not an array: report what a full parse would (syntax error or wrong type)
+    std::string e;
+    if (!parse(in, &v, &e)) return fail(e);
+    return fail("expected a JSON array");
   }
-  for (const Value& e : v.arr) {
-    switch (e.type) {
-      case Value::Type::kNull: out->push_back(std::nullopt); break;
-      case Value::Type::kBool: out->push_back(std::string(e.b ? "true" : "false")); break;
-      case Value::Type::kNumber:
-      case Value::Type::kString: out->push_back(e.text); break;
-      default:
-        if (err) *err = "cannot deserialize java.lang.String out of a nested array/object";
-        return false;
+  ++p.i;
+  p.ws();
+  if (p.i < in.size() && in[p.i] == ']') {
+    ++p.i;
+  } else {
+    for (;;) {
+      p.ws();
+      if (p.i >= in.size()) return fail("unexpected end at offset " + std::to_string(p.i));
+      char c = in[p.i];
+      if (c == '"') {
+        out->emplace_back(std::string());
+        if (!p.str(&**(out->end() - 1))) return fail("bad string");
+      } else if (c == 'n') {
+        if (!p.lit("null")) return fail("bad literal");
+        out->emplace_back(std::nullopt);
+      } else if (c == 't' || c == 'f') {
+        if (!p.lit(c == 't' ? "true" : "false")) return fail("bad literal");
+        out->emplace_back(std::string(c == 't' ? "true" : "false"));
+      } else if (c == '[' || c == '{') {
+        return fail("cannot deserialize java.lang.String out of a nested array/object");
+      } else {
+        Value v;
+        if (!p.num(&v)) return fail("bad number");
+        out->emplace_back(std::move(v.text));
+      }
+      p.ws();
+      if (p.i < in.size() && in[p.i] == ',') {
+        ++p.i;
+        continue;
+      }
+      if (p.i < in.size() && in[p.i] == ']') {
+        ++p.i;
+        break;
+      }
+      return fail("expected , or ] at offset " + std::to_string(p.i));
     }
   }
+  p.ws();
+  if (p.i != in.size()) return fail("trailing characters at offset " + std::to_string(p.i));
   return true;
 }
 

@@ -57,19 +57,20 @@ Extract extract(std::string_view trace_id, std::string_view span_id, std::string
   if (!single.empty()) {
     // b3: {TraceId}-{SpanId}[-{SamplingState}[-{ParentSpanId}]]  or just {SamplingState}
     if (single == "0") return Extract::kNotSampled;
-    if (single.find('-') == std::string_view::npos) return Extract::kNone;  // "1"/"d": no ids
-    size_t a = single.find('-');
-    std::string_view t = single.substr(0, a);
-    std::string_view rest = single.substr(a + 1);
-    size_t b = rest.find('-');
-    std::string_view sp = rest.substr(0, b);
-    std::string_view state, parent;
-    if (b != std::string_view::npos) {
-      rest = rest.substr(b + 1);
-      size_t c = rest.find('-');
-      state = rest.substr(0, c);
-      if (c != std::string_view::npos) parent = rest.substr(c + 1);
+    // Split on '-' by hand (gcc 11 mis-warns on chained string_view::find here).
+    std::string_view part[4];
+    int n = 0;
+    size_t from = 0;
+    for (size_t i = 0; i <= single.size() && n < 3; ++i) {
+      if (i == single.size() || single[i] == '-') {
+        part[n++] = single.substr(from, i - from);
+        from = i + 1;
+      }
     }
+    if (n == 3 && from <= single.size()) part[n++] = single.substr(from);  // parent: the rest
+    if (n < 2) return Extract::kNone;  // "1"/"d": no ids
+    std::string_view t = part[0], sp = part[1], state = n > 2 ? part[2] : std::string_view(),
+                     parent = n > 3 ? part[3] : std::string_view();
     if (state == "0") return Extract::kNotSampled;
     if (!parse_trace_id(t, &out->trace_hi, &out->trace_id) || !parse_hex64(sp, &out->span_id))
       return Extract::kNone;
@@ -92,16 +93,24 @@ Extract extract(std::string_view trace_id, std::string_view span_id, std::string
 }
 
 void inject(const SpanContext& ctx, std::string* h) {
-  *h += "X-B3-TraceId: ";
-  *h += trace_id_hex(ctx.trace_hi, ctx.trace_id);
-  *h += "\r\nX-B3-SpanId: ";
-  *h += hex64(ctx.span_id);
+  // Formatted in place: this runs on every traced downstream call.
+  char id[16];
+  auto put = [&](uint64_t v) {
+    hex64(v, id);
+    h->append(id, 16);
+  };
+  h->reserve(h->size() + 128);
+  h->append("X-B3-TraceId: ");
+  if (ctx.trace_hi) put(ctx.trace_hi);
+  put(ctx.trace_id);
+  h->append("\r\nX-B3-SpanId: ");
+  put(ctx.span_id);
   if (ctx.has_parent) {
-    *h += "\r\nX-B3-ParentSpanId: ";
-    *h += hex64(ctx.parent_id);
+    h->append("\r\nX-B3-ParentSpanId: ");
+    put(ctx.parent_id);
   }
-  *h += ctx.sampled ? "\r\nX-B3-Sampled: 1\r\n" : "\r\nX-B3-Sampled: 0\r\n";
-  if (ctx.debug) *h += "X-B3-Flags: 1\r\n";
+  h->append(ctx.sampled ? "\r\nX-B3-Sampled: 1\r\n" : "\r\nX-B3-Sampled: 0\r\n");
+  if (ctx.debug) h->append("X-B3-Flags: 1\r\n");
 }
 
 }  // namespace hola::tracing
