@@ -43,7 +43,10 @@ struct HolaApp::WorkerCache {
   Prepared api_not_found[2], not_found[2][2], api_not_allowed[2], not_allowed[2], not_acceptable[2],
       api_options[2], static_options[2], server_error[2][2];
   std::vector<Prepared*> all;
-  std::string scratch;  // for dynamic bodies
+  // Dynamic /api/hola-chaining success responses: the head up to and including
+  // "Content-Length: " per keep-alive mode, and the body's `["<greeting>"` prefix.
+  std::string chain_head[2];
+  std::string chain_json_prefix;
 };
 
 const char* HolaApp::route_name(int r) {
@@ -121,8 +124,20 @@ void HolaApp::refresh(http::Worker& w, WorkerCache& wc) {
     const assets::Asset* index = assets::find("index.html");
     const assets::Asset* viewer = assets::find("swagger-ui.html");
     std::string fallback_body;
+    wc.chain_json_prefix.clear();
     if (c && c->ok) {
       fallback_body = json::string_array({c->greeting, std::string(kFallbackGreeting)});
+      wc.chain_json_prefix = "[";
+      json::append_string(&wc.chain_json_prefix, c->greeting);
+      for (int ka = 0; ka < 2; ++ka) {
+        ResponseSpec js;  // same spec as the generic path below, cut before the length
+        js.keep_alive = ka;
+        js.cors = true;
+        js.content_type = kJson;
+        std::string full = build_response(js, date).bytes;
+        constexpr std::string_view kLen = "Content-Length: ";
+        wc.chain_head[ka] = full.substr(0, full.find(kLen) + kLen.size());
+      }
     }
     for (int ka = 0; ka < 2; ++ka) {
       for (int head = 0; head < 2; ++head) {
@@ -405,6 +420,36 @@ void HolaApp::handle_chaining(http::Connection& c, const http::Request& r, Worke
                        self->refresh(w, wc);
                      if (wc.content == content) {
                        conn->complete(wc.chaining_fallback[ka][head].view(), ka);
+                       answered = true;
+                     }
+                   }
+                   if (!answered && !conn->closed() && wc.content == content && !wc.chain_json_prefix.empty()) {
+                     // One allocation: [greeting, ...aloha] written straight into the response.
+                     if (wc.gen != self->gen_.load(std::memory_order_relaxed) || wc.date_version != w.date_version())
+                       self->refresh(w, wc);
+                     if (wc.content == content) {
+                       size_t body_len = wc.chain_json_prefix.size() + 1;
+                       for (auto& it : res.items) body_len += 1 + (it ? it->size() + 2 : 4);
+                       std::string resp;
+                       resp.reserve(wc.chain_head[ka].size() + 48 + body_len + 16);
+                       resp += wc.chain_head[ka];
+                       const size_t len_at = resp.size();
+                       resp += "\r\nDate: ";
+                       resp.append(w.date(), 29);
+                       resp += "\r\n\r\n";
+                       const size_t body_at = resp.size();
+                       resp += wc.chain_json_prefix;
+                       for (auto& it : res.items) {
+                         resp += ',';
+                         if (it) json::append_string(&resp, *it);
+                         else resp += "null";
+                       }
+                       resp += ']';
+                       // Content-Length goes in front of the Date line now that the body is known.
+                       std::string len = std::to_string(resp.size() - body_at);
+                       resp.insert(len_at, len);
+                       if (head) resp.resize(body_at + len.size());
+                       conn->complete(resp, ka);
                        answered = true;
                      }
                    }

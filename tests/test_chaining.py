@@ -2,6 +2,7 @@
 back to ["Aloha response (fallback)"] (HolaResource.java:111-112), the 600 ms timeout
 (config.properties:17), the circuit breaker (config.properties:19) and the bulkhead."""
 import json
+import socket
 import threading
 import time
 
@@ -189,3 +190,29 @@ def test_hystrix_flag_shorthands(hola, aloha):
     t0 = time.monotonic()
     assert chain(s)[1:] == [FALLBACK]
     assert time.monotonic() - t0 < 0.6
+
+
+def test_success_response_framing_get_and_head(hola, aloha):
+    """The success response is assembled in one buffer: headers in the same order as every
+    prepared response, Content-Length matching the body, and HEAD keeping the length."""
+    aloha.payload = ["Aloha \"quoted\"", None, "tab\there"]
+    s = hola(args=["--aloha-url", aloha.url, "--feign-log", "none"], env={"HOSTNAME": "h"})
+
+    def raw(method):
+        with socket.create_connection(("127.0.0.1", s.port), timeout=5) as c:
+            c.sendall(f"{method} /api/hola-chaining HTTP/1.1\r\nHost: x\r\nConnection: close\r\n\r\n".encode())
+            data = b""
+            while chunk := c.recv(65536):
+                data += chunk
+        head, _, body = data.partition(b"\r\n\r\n")
+        return head.decode().split("\r\n"), body
+
+    lines, body = raw("GET")
+    assert lines[0] == "HTTP/1.1 200 OK"
+    names = [l.split(":")[0] for l in lines[1:]]
+    assert names == ["Connection", "Access-Control-Allow-Origin", "Content-Type", "Content-Length", "Date"]
+    assert json.loads(body) == ["Hola de h", "Aloha \"quoted\"", None, "tab\there"]
+    length = int(dict(l.split(": ", 1) for l in lines[1:])["Content-Length"])
+    assert length == len(body)
+    hlines, hbody = raw("HEAD")
+    assert hbody == b"" and dict(l.split(": ", 1) for l in hlines[1:])["Content-Length"] == str(length)
