@@ -75,8 +75,7 @@ struct ClientPool::Conn final : EventLoop::Handler {
   std::string in;
   uint64_t id = 0;
   Callback cb;
-  bool reused = false;
-  std::string req;
+  bool reused = false;  // the request goes out unchanged in `out` (kept for the silent retry)
   uint32_t interest = 0;
 
   void set_interest(uint32_t ev) {
@@ -98,12 +97,12 @@ void ClientPool::Conn::fail(const std::string& why) {
     ClientPool* p = pool;
     uint64_t rid = id;
     Callback c = std::move(cb);
-    std::string r = req;
+    std::string r = std::move(out);
     p->active_.erase(rid);
     p->destroy(this);
     auto* fresh = new Conn();
     fresh->pool = p;
-    p->start_on(fresh, rid, r, std::move(c), false);
+    p->start_on(fresh, rid, std::move(r), std::move(c), false);
     return;
   }
   ClientResult res;
@@ -160,7 +159,11 @@ int ClientPool::Conn::try_parse(ClientResult* r, bool* keep, bool eof) {
   if (he == std::string::npos) return in.size() > 64 * 1024 ? -1 : 0;
   std::string_view head(in.data(), he);
   if (head.size() < 12 || head.substr(0, 5) != "HTTP/") return -1;
-  int status = atoi(std::string(head.substr(9, 3)).c_str());
+  int status = 0;
+  for (size_t k = 9; k < 12; ++k) {
+    if (head[k] < '0' || head[k] > '9') return -1;
+    status = status * 10 + (head[k] - '0');
+  }
   if (status < 100) return -1;
   bool http10 = head.substr(5, 3) == "1.0";
   int64_t cl = -1;
@@ -173,7 +176,14 @@ int ClientPool::Conn::try_parse(ClientResult* r, bool* keep, bool eof) {
     if (colon != std::string_view::npos) {
       std::string_view k = line.substr(0, colon), v = line.substr(colon + 1);
       while (!v.empty() && (v.front() == ' ' || v.front() == '\t')) v.remove_prefix(1);
-      if (http::iequals(k, "content-length")) cl = atoll(std::string(v).c_str());
+      if (http::iequals(k, "content-length")) {
+        cl = 0;
+        for (char d : v) {
+          if (d < '0' || d > '9') break;
+          cl = cl * 10 + (d - '0');
+          if (cl > (1 << 20)) break;  // over the body cap: rejected below
+        }
+      }
       else if (http::iequals(k, "transfer-encoding") && v.find("chunked") != std::string_view::npos) chunked = true;
       else if (http::iequals(k, "connection")) {
         if (http::iequals(v, "close")) close = true;
@@ -292,20 +302,19 @@ uint64_t ClientPool::get(const std::string& path, const std::string& extra_heade
   if (!idle_.empty()) {
     Conn* c = idle_.back();
     idle_.pop_back();
-    start_on(c, id, req, std::move(cb), true);
+    start_on(c, id, std::move(req), std::move(cb), true);
   } else {
     auto* c = new Conn();
     c->pool = this;
-    start_on(c, id, req, std::move(cb), false);
+    start_on(c, id, std::move(req), std::move(cb), false);
   }
   return id;
 }
 
-void ClientPool::start_on(Conn* c, uint64_t id, const std::string& req, Callback cb, bool reused) {
+void ClientPool::start_on(Conn* c, uint64_t id, std::string req, Callback cb, bool reused) {
   c->id = id;
   c->cb = std::move(cb);
-  c->req = req;
-  c->out = req;
+  c->out = std::move(req);
   c->off = 0;
   c->in.clear();
   c->reused = reused;

@@ -68,7 +68,7 @@ class ClientPool {
  private:
   struct Conn;
   friend struct Conn;
-  void start_on(Conn* c, uint64_t id, const std::string& req, Callback cb, bool reused);
+  void start_on(Conn* c, uint64_t id, std::string req, Callback cb, bool reused);
   void finish(Conn* c, ClientResult&& r, bool reusable);
   void destroy(Conn* c);
   std::string build_request(const std::string& path, const std::string& extra) const;
