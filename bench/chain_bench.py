@@ -21,7 +21,7 @@ sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
 
 from hola_amd.parallel.loadgen import run_duration  # noqa: E402
 from hola_amd.server import HolaProcess  # noqa: E402
-from hola_amd.utils.cpu import format_cpu_list, plan_node  # noqa: E402
+from hola_amd.utils.cpu import format_cpu_list, plan_mirrored  # noqa: E402
 
 ap = argparse.ArgumentParser(description=__doc__)
 ap.add_argument("--duration", type=float, default=10)
@@ -38,7 +38,10 @@ def cpu_s(pid: int) -> float:
     return (int(f[11]) + int(f[12])) / os.sysconf("SC_CLK_TCK")
 
 
-cores = plan_node(3)  # A, B, load generator
+# Every L3 domain holds a share of A, B and the load generator (A does two hops' work), so
+# accept steering keeps loadgen->A and A->B connections inside one L3 each.
+plan = plan_mirrored({"A": 2, "B": 1, "loadgen": 1})
+cores = [plan["A"], plan["B"], plan["loadgen"]]
 # B answers /api/hola-chaining itself with its own fallback (its aloha is unreachable and its
 # breaker opens), so A decodes ["Hola de B", "Aloha response (fallback)"].
 with HolaProcess(args=["--aloha-url", "http://127.0.0.1:1/", "--feign-log", "none", "--no-tracing",

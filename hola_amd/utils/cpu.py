@@ -217,6 +217,42 @@ def plan_replicas_with_loadgen(local_world: int, per_rank: int | None = None, se
     return plans
 
 
+def plan_mirrored(weights: dict[str, int], total: int | None = None, avoid_busy: bool = True) -> dict[str, list[int]]:
+    """Splits `total` cores (quietest L3 domains first) between several processes so that
+    EVERY L3 domain holds a share of each, in proportion to `weights`.
+
+    For a chain of processes (load generator -> hola A -> hola B), accept steering
+    (SO_INCOMING_CPU) then keeps each hop inside one L3: a connection lands on a worker in
+    the domain of the thread that opened it. Returns {name: [cores...]}, each non-empty.
+    """
+    names = list(weights)
+    cores = plan_node(1, total, avoid_busy=avoid_busy)[0]
+    by_dom: dict[int, list[int]] = {}
+    for c in cores:
+        by_dom.setdefault(l3_domain(c), []).append(c)
+    out: dict[str, list[int]] = {n: [] for n in names}
+    wsum = sum(weights.values())
+    for dom_cores in by_dom.values():
+        m = len(dom_cores)
+        if m < len(names):  # too small to mirror: give it to the heaviest process
+            out[max(names, key=lambda n: weights[n])].extend(dom_cores)
+            continue
+        shares = {n: max(1, round(m * weights[n] / wsum)) for n in names}
+        while sum(shares.values()) > m:  # rounding overflow: trim the largest share
+            shares[max(names, key=lambda n: shares[n])] -= 1
+        while sum(shares.values()) < m:
+            shares[max(names, key=lambda n: weights[n])] += 1
+        i = 0
+        for n in names:
+            out[n].extend(dom_cores[i:i + shares[n]])
+            i += shares[n]
+    for n in names:  # a domain-starved process still needs one core
+        if not out[n]:
+            donor = max(names, key=lambda k: len(out[k]))
+            out[n].append(out[donor].pop())
+    return out
+
+
 def plan_cores(rank: int, local_world: int, per_rank: int | None = None) -> list[int]:
     """Disjoint CPU set for `rank` out of `local_world` co-located ranks.
 

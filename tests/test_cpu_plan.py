@@ -67,3 +67,19 @@ def test_scaling_plan_places_threads_with_replicas(epyc, monkeypatch):
     assert len(p["replicas"]) == 4
     for t, c in enumerate(p["loadgen"]):
         assert cpu.l3_domain(c) in {cpu.l3_domain(x) for x in p["replicas"][t % 4]}
+
+
+def test_plan_mirrored_every_domain_holds_every_process(epyc):
+    plan = cpu.plan_mirrored({"A": 2, "B": 1, "loadgen": 1})  # 16 cores = 2 domains
+    assert sorted(len(v) for v in plan.values()) == [4, 4, 8]
+    assert len(plan["A"]) == 8
+    every = [c for v in plan.values() for c in v]
+    assert len(every) == len(set(every)) == 16
+    for name, cores in plan.items():
+        assert {cpu.l3_domain(c) for c in cores} == {0, 1}, name  # a share in both L3s
+
+
+def test_plan_mirrored_small_budget_still_gives_each_a_core(epyc):
+    plan = cpu.plan_mirrored({"A": 2, "B": 1, "loadgen": 1}, total=3)
+    assert all(len(v) >= 1 for v in plan.values())
+    assert len({c for v in plan.values() for c in v}) == 3
