@@ -22,13 +22,17 @@ ap = argparse.ArgumentParser(description=__doc__)
 ap.add_argument("--rates", default="250000,1000000,2000000,3000000,3500000")
 ap.add_argument("--duration", type=float, default=8)
 ap.add_argument("--connections", type=int, default=64)
+ap.add_argument("--busy-poll-us", type=int, default=0, help="server and load generator spin in epoll this long")
+ap.add_argument("--spin-us", type=int, default=0, help="load generator spins when its next send is this close")
 ap.add_argument("--out", default="")
 a = ap.parse_args()
 
 cores = plan_node(1)[0]
 srv, lg = split_server_loadgen(cores, max(1, len(cores) // 2))
 rows = []
-with HolaProcess(env={"HOSTNAME": "h"}, threads=len(srv), cpu_list=format_cpu_list(srv), log_level="warn") as s:
+server_args = ["--busy-poll-us", str(a.busy_poll_us)] if a.busy_poll_us else []
+with HolaProcess(args=server_args, env={"HOSTNAME": "h"}, threads=len(srv), cpu_list=format_cpu_list(srv),
+                 log_level="warn") as s:
     def server_cpu():
         with open(f"/proc/{s.proc.pid}/stat") as f:
             v = f.read().rsplit(")", 1)[1].split()
@@ -38,7 +42,8 @@ with HolaProcess(env={"HOSTNAME": "h"}, threads=len(srv), cpu_list=format_cpu_li
         c0 = resource.getrusage(resource.RUSAGE_CHILDREN)
         s0 = server_cpu()
         r = run_duration([("127.0.0.1", s.port)], a.connections, len(lg), a.duration, 2.0,
-                         cpu_list=",".join(map(str, lg)), rate=rate)
+                         cpu_list=",".join(map(str, lg)), rate=rate, busy_poll_us=a.busy_poll_us,
+                         spin_us=a.spin_us)
         c1 = resource.getrusage(resource.RUSAGE_CHILDREN)
         s1 = server_cpu()
         wall = a.duration + 2.0  # warmup included in both CPU figures
@@ -51,6 +56,6 @@ with HolaProcess(env={"HOSTNAME": "h"}, threads=len(srv), cpu_list=format_cpu_li
         rows.append(row)
         print(json.dumps(row), flush=True)
 out = {"cpu_map": {"server": format_cpu_list(srv), "loadgen": format_cpu_list(lg)}, "connections": a.connections,
-       "rows": rows}
+       "busy_poll_us": a.busy_poll_us, "spin_us": a.spin_us, "rows": rows}
 if a.out:
     Path(a.out).write_text(json.dumps(out, indent=1))

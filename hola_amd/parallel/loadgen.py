@@ -105,9 +105,12 @@ class ControlledLoadgen:
 
 def run_duration(targets: list[tuple[str, int]], connections: int, threads: int, duration_s: float,
                  warmup_s: float = 1.0, cpu_list: str | None = None, path: str = "/api/hola",
-                 timeout: float | None = None, rate: float = 0.0) -> dict:
+                 timeout: float | None = None, rate: float = 0.0, busy_poll_us: int = 0,
+                 spin_us: int = 0) -> dict:
     """wrk-style timed run (closed loop), or wrk2-style open loop at `rate` req/s with latency
-    measured from intended send times; returns the loadgen's JSON summary."""
+    measured from intended send times; returns the loadgen's JSON summary. `busy_poll_us`
+    spins in epoll after activity; `spin_us` (open loop) spins instead of sleeping when the
+    next scheduled send is that close."""
     cmd = [str(binary("hola_loadgen")), "--targets", ",".join(f"{h}:{p}" for h, p in targets),
            "-c", str(connections), "-t", str(threads), "--path", path, "--duration", str(duration_s),
            "--warmup", str(warmup_s)]
@@ -115,6 +118,10 @@ def run_duration(targets: list[tuple[str, int]], connections: int, threads: int,
         cmd += ["--cpu-list", cpu_list]
     if rate > 0:
         cmd += ["--rate", str(rate)]
+    if busy_poll_us:
+        cmd += ["--busy-poll-us", str(busy_poll_us)]
+    if spin_us:
+        cmd += ["--spin-us", str(spin_us)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout or duration_s + warmup_s + 60)
     if r.returncode != 0:
         raise RuntimeError(f"loadgen failed: {r.stderr}")
