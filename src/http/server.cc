@@ -382,7 +382,7 @@ Server::Server(ServerOptions opts, RequestHandler* handler) : opts_(std::move(op
   for (int i = 0; i < opts_.threads; ++i) workers_.push_back(std::make_unique<Worker>(this, i));
   assigned_.reset(new std::atomic<int32_t>[workers_.size()]);
   for (size_t i = 0; i < workers_.size(); ++i) assigned_[i].store(0);
-  if (opts_.steer_l3 && !opts_.cpus.empty() && !opts_.reuseport_accept) {
+  if (opts_.steer_l3 && !opts_.cpus.empty()) {
     for (size_t i = 0; i < workers_.size(); ++i) {
       int dom = l3_domain_of(opts_.cpus[i % opts_.cpus.size()]);
       if (dom < 0) {
@@ -479,10 +479,13 @@ void Server::Acceptor::on_event(uint32_t) {
       }
       return;
     }
-    if (server->opts_.reuseport_accept) {
+    if (server->opts_.reuseport_accept && server->domain_workers_.empty()) {
+      // The kernel already spread connections over the workers' listeners.
       server->assigned_[size_t(worker->index())].fetch_add(1, std::memory_order_relaxed);
       worker->adopt_here(c, t0);
     } else {
+      // Round-robin accept, or reuseport with L3 steering: the kernel's hash ignores where
+      // the client runs, so the connection may still move to a worker in the client's L3.
       Worker* w = server->pick_worker(c);
       if (w == worker) w->adopt_here(c, t0);
       else w->adopt(c, t0);
