@@ -83,3 +83,21 @@ def test_plan_mirrored_small_budget_still_gives_each_a_core(epyc):
     plan = cpu.plan_mirrored({"A": 2, "B": 1, "loadgen": 1}, total=3)
     assert all(len(v) >= 1 for v in plan.values())
     assert len({c for v in plan.values() for c in v}) == 3
+
+
+def test_full_node_eight_ranks(epyc, monkeypatch):
+    """The driver's N=8 run on a whole node (no quota: 256 CPUs, 128 physical cores in 16 L3
+    domains): 16 cores per rank, disjoint, no SMT siblings, every load-generator thread in
+    the L3 of the replica it drives. Planning only; nothing is launched."""
+    monkeypatch.setattr(cpu, "cgroup_cpu_quota", lambda: 0.0)
+    n = 8
+    per_rank = min(16, cpu.cpu_budget() // n)
+    assert per_rank == 16
+    plans = cpu.plan_replicas_with_loadgen(n, per_rank)
+    used = [c for p in plans for c in p["server"] + p["loadgen"]]
+    assert len(used) == len(set(used)) == 128 and max(used) < 128  # physical cores only
+    for r, p in enumerate(plans):
+        assert len(p["server"]) == 8 and len(p["loadgen"]) == 8
+        for t, c in enumerate(p["loadgen"]):
+            target = (t + r) % n
+            assert cpu.l3_domain(c) in {cpu.l3_domain(x) for x in plans[target]["server"]}
