@@ -236,7 +236,8 @@ int main(int argc, char** argv) {
 
   LOG_INFO("hola listening on %s:%d (workers=%d, cpus=%s, accept=%s, tracing=%s, aloha=%s)", so.host.c_str(),
            server.port(), threads, cpus.empty() ? "unpinned" : format_cpu_list(cpus).c_str(),
-           so.reuseport_accept ? "reuseport" : (server.steering() ? "rr+l3-steering" : "rr"),
+           so.reuseport_accept ? (server.steering() ? "reuseport+l3-steering" : "reuseport")
+                               : (server.steering() ? "rr+l3-steering" : "rr"),
            !to.enabled ? "off" : (to.collector_url.empty() ? "on (no collector: spans dropped)" : to.collector_url.c_str()),
            chainer.full_url().c_str());
   if (!port_file.empty()) {
