@@ -8,8 +8,8 @@ One rank per "GPU slot" of the node = one hola replica. Every rank:
     64 keep-alive connections per replica are dealt round-robin over ALL replicas of the
     node (client-side round-robin, BASELINE.json config 4: "512 connections against 8
     replicas behind round-robin"; N=1 is config 3: 64 connections, 1 replica).
-A step = every connection completes `--reqs-per-conn` requests (weak scaling: the work per
-replica is fixed). W warmup steps, then exactly K timed steps between barriers; the elapsed
+A step = connections x `--reqs-per-conn` requests per replica, drawn by the connections from
+a shared budget (weak scaling: the work per replica is fixed). W warmup steps, then exactly K timed steps between barriers; the elapsed
 time is the MAX over ranks, `value` is the node-wide total req/s, and p50/p99 come from the
 merged latency histograms of all ranks.
 
@@ -56,6 +56,9 @@ def parse_args():
                     help="run replicas with --profile and write their stage histograms here")
     ap.add_argument("--no-avoid-busy", action="store_true",
                     help="take cores in id order instead of the quietest L3 domains first")
+    ap.add_argument("--per-conn-quota", action="store_true",
+                    help="every connection does exactly --reqs-per-conn per step (default: the step's "
+                         "connections x reqs-per-conn requests are shared, so no connection idles at the end)")
     ap.add_argument("--busy-poll-us", type=int, default=20,
                     help="spin this long in epoll before sleeping (server and load generator); "
                          "20 us measured best on the box (profiles/r11_box_session), 0 = off")
@@ -113,7 +116,8 @@ def main() -> int:
         if dist:
             dist.barrier()  # every replica is listening before any connection is made
         loadgen = ControlledLoadgen(targets, a.connections, len(load_cpus), cpu_list=",".join(map(str, load_cpus)),
-                                    path=a.path, target_offset=local_rank, busy_poll_us=a.busy_poll_us)
+                                    path=a.path, target_offset=local_rank, busy_poll_us=a.busy_poll_us,
+                                    per_conn_quota=a.per_conn_quota)
         for _ in range(a.warmup):
             loadgen.run(a.reqs_per_conn)
         loadgen.reset()
@@ -197,6 +201,7 @@ def main() -> int:
                 "server_threads_per_replica": s_threads,
                 "loadgen_threads_per_replica": len(load_cpus),
                 "busy_poll_us": a.busy_poll_us,
+                "step_budget": "per-connection" if a.per_conn_quota else "shared",
                 "cpu_map": {f"rank{i}": {"server": g["server_cpus"], "loadgen": g["load_cpus"]}
                             for i, g in enumerate(gathered)},
                 "cpu_budget": cpu_budget(),

@@ -67,6 +67,10 @@ struct Options {
   int busy_poll_us = 0;
   double rate = 0;  // --rate: open-loop total req/s (wrk2-style, latency from intended time)
   int spin_us = 0;  // --rate: spin instead of sleeping when the next send is this close (burns CPU)
+  // control: a run of R requests per connection is R x connections requests drawn from one
+  // shared budget (connections that answer faster do more, so no thread idles at the end of
+  // a run waiting for a slower one); --per-conn-quota gives each connection exactly R.
+  bool per_conn_quota = false;
 };
 
 struct Conn {
@@ -98,6 +102,7 @@ struct ThreadState {
 };
 
 std::atomic<bool> g_stop{false};
+std::atomic<int64_t> g_budget{0};  // control, shared mode: requests left in this run
 int g_donefd = -1;  // EFD_SEMAPHORE: one count per thread finishing a control run
 std::atomic<bool> g_connect_failed{false};
 char g_connect_error[256];
@@ -193,6 +198,20 @@ void thread_main(ThreadState* ts, const Options* o) {
   uint64_t seen_gen = 0;
   int64_t outstanding = 0;  // control: connections with quota left
   uint64_t run_requests = 0, run_errors = 0;
+  // Shared-budget claims are taken in batches so threads rarely touch the global counter.
+  constexpr int64_t kClaimBatch = 32;
+  int64_t local_claims = 0;
+  const bool shared = control && !o->per_conn_quota;
+  auto claim = [&]() -> bool {
+    if (local_claims > 0) {
+      --local_claims;
+      return true;
+    }
+    int64_t before = g_budget.fetch_sub(kClaimBatch, std::memory_order_relaxed);
+    if (before <= 0) return false;
+    local_claims = std::min(kClaimBatch, before) - 1;
+    return true;
+  };
   int64_t warm_end = o->duration_s > 0 ? mono_ns() + int64_t(o->warmup_s * 1e9) : 0;
   int64_t end = o->duration_s > 0 ? warm_end + int64_t(o->duration_s * 1e9) : 0;
   ts->recording = !(o->warmup_s > 0);
@@ -283,9 +302,10 @@ void thread_main(ThreadState* ts, const Options* o) {
           int64_t q = ts->run_quota.load();
           outstanding = 0;
           run_requests = run_errors = 0;
+          local_claims = 0;
           for (auto& cc : ts->conns) {
-            cc->quota = q;
-            if (q > 0) ++outstanding;
+            cc->quota = shared ? (claim() ? 1 : 0) : q;  // shared: 1 = holds a claimed request
+            if (cc->quota > 0) ++outstanding;
           }
           if (outstanding == 0) {
             ts->done_requests.store(0);
@@ -351,7 +371,9 @@ void thread_main(ThreadState* ts, const Options* o) {
         epoll_ctl(ts->epfd, EPOLL_CTL_ADD, c->fd, &ev);
       }
       if (control) {
-        if (--c->quota <= 0) {
+        if (shared) c->quota = claim() ? 1 : 0;
+        else --c->quota;
+        if (c->quota <= 0) {
           if (--outstanding == 0) {
             ts->done_requests.store(run_requests);
             ts->done_errors.store(run_errors);
@@ -441,10 +463,12 @@ int main(int argc, char** argv) {
     else if (a == "--busy-poll-us") o.busy_poll_us = atoi(val().c_str());
     else if (a == "--rate" || a == "-R") o.rate = atof(val().c_str());
     else if (a == "--spin-us") o.spin_us = atoi(val().c_str());
+    else if (a == "--per-conn-quota") o.per_conn_quota = true;
     else {
       fprintf(stderr,
               "usage: hola_loadgen --targets h:p[,h:p..] -c CONNS -t THREADS [--cpu-list L] [--path P]\n"
-              "                    (--duration S [--warmup S] | --control) [--target-offset K] [-H 'Name: v']\n");
+              "                    (--duration S [--warmup S] [--rate R [--spin-us N]] | --control [--per-conn-quota])\n"
+              "                    [--target-offset K] [--busy-poll-us N] [-H 'Name: v']\n");
       return 2;
     }
   }
@@ -512,6 +536,7 @@ int main(int argc, char** argv) {
       int64_t q = atoll(line.c_str() + 4);
       ++gen;
       int64_t t0 = mono_ns();
+      g_budget.store(q * int64_t(o.connections));
       for (auto& t : ts) {
         t->run_quota.store(q);
         t->run_gen.store(gen);

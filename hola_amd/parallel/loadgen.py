@@ -50,11 +50,12 @@ def percentile(hist: dict[int, int], p: float) -> int:
 
 
 class ControlledLoadgen:
-    """`hola_loadgen --control`: each run(R) makes every connection complete R requests."""
+    """`hola_loadgen --control`: each run(R) completes R x connections requests, drawn by the
+    connections from one shared budget (or exactly R per connection with `per_conn_quota`)."""
 
     def __init__(self, targets: list[tuple[str, int]], connections: int, threads: int,
                  cpu_list: str | None = None, path: str = "/api/hola", target_offset: int = 0,
-                 headers: list[str] | None = None, busy_poll_us: int = 0):
+                 headers: list[str] | None = None, busy_poll_us: int = 0, per_conn_quota: bool = False):
         cmd = [str(binary("hola_loadgen")), "--targets", ",".join(f"{h}:{p}" for h, p in targets),
                "-c", str(connections), "-t", str(threads), "--path", path, "--control",
                "--target-offset", str(target_offset)]
@@ -64,6 +65,8 @@ class ControlledLoadgen:
             cmd += ["-H", h]
         if busy_poll_us:
             cmd += ["--busy-poll-us", str(busy_poll_us)]
+        if per_conn_quota:
+            cmd += ["--per-conn-quota"]
         self.proc = subprocess.Popen(cmd, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, bufsize=1)
         ready = self._read()
         if not ready.get("ready"):
