@@ -127,6 +127,7 @@ def main() -> int:
             dist.barrier()
         cuda()
         cpu0 = (_proc_cpu_s(server.proc.pid), _proc_cpu_s(loadgen.proc.pid))
+        tcp0 = _tcp_counters()
         t0 = time.perf_counter()
         reqs = errs = 0
         for _ in range(a.steps):
@@ -138,6 +139,7 @@ def main() -> int:
         cuda()
         elapsed = time.perf_counter() - t0
         cpu1 = (_proc_cpu_s(server.proc.pid), _proc_cpu_s(loadgen.proc.pid))
+        tcp1 = _tcp_counters()
         st = loadgen.stats()
         mem = server.memory_kb()
 
@@ -145,7 +147,8 @@ def main() -> int:
                  "non2xx": st.get("non2xx", 0), "server_cpus": format_cpu_list(server_cpus),
                  "load_cpus": format_cpu_list(load_cpus),
                  "server_cpu_s": cpu1[0] - cpu0[0], "loadgen_cpu_s": cpu1[1] - cpu0[1],
-                 "startup_ms": server.startup_ms, "rss_peak_kb": mem.get("VmHWM", 0)}
+                 "startup_ms": server.startup_ms, "rss_peak_kb": mem.get("VmHWM", 0),
+                 "tcp": {k: tcp1[k] - tcp0[k] for k in tcp1 if k in tcp0}}
         if dist:
             gathered = [None] * world
             dist.all_gather_object(gathered, local)
@@ -184,6 +187,10 @@ def main() -> int:
             # replica footprint: exec -> listening, and peak resident memory (max over ranks)
             "server_startup_ms": round(max(g["startup_ms"] or 0 for g in gathered), 1),
             "server_rss_peak_mb": round(max(g["rss_peak_kb"] for g in gathered) / 1024.0, 1),
+            # loopback TCP segments per request over the timed region (the network namespace
+            # is shared by all ranks, so rank 0's delta covers the node): ~2 = one request and
+            # one response segment with the ACKs piggybacked
+            "tcp_per_req": {k: round(v / max(1, total), 3) for k, v in gathered[0]["tcp"].items()},
             "errors": sum(g["errors"] for g in gathered),
             "non2xx": sum(g["non2xx"] for g in gathered),
             "config": {
@@ -261,6 +268,30 @@ def _proc_cpu_s(pid: int) -> float:
         return (int(fields[11]) + int(fields[12])) / os.sysconf("SC_CLK_TCK")
     except (OSError, IndexError, ValueError):
         return 0.0
+
+
+def _tcp_counters() -> dict[str, int]:
+    """Network-namespace-wide TCP counters (/proc/net/snmp `Tcp:`, /proc/net/netstat
+    `TcpExt:`): segments, and the ACK counts that show whether ACKs ride on the request and
+    response segments or travel as extra pure-ACK packets through the loopback path."""
+    want = {"Tcp": ("OutSegs", "InSegs", "RetransSegs"),
+            "TcpExt": ("DelayedACKs", "TCPPureAcks", "TCPHPAcks", "TCPAutoCorking")}
+    out: dict[str, int] = {}
+    for path in ("/proc/net/snmp", "/proc/net/netstat"):
+        try:
+            with open(path) as f:
+                lines = f.read().splitlines()
+        except OSError:
+            continue
+        for names, vals in zip(lines[::2], lines[1::2]):
+            group = names.split(":", 1)[0]
+            if group not in want:
+                continue
+            row = dict(zip(names.split()[1:], vals.split()[1:]))
+            for field in want[group]:
+                if row.get(field, "").lstrip("-").isdigit():
+                    out[field] = int(row[field])
+    return out
 
 
 def _cuda_sync_fn(local_rank: int):

@@ -29,6 +29,9 @@ def test_bench_one_rank():
     assert out["scaling"] == "weak" and out["higher_is_better"] is True and out["vs_baseline"] is None
     assert out["config"]["global_batch"] == 64 and out["config"]["parallelism"] == "replicas1"
     assert abs(out["value"] - out["requests"] / (out["ms_per_step"] * out["steps"] / 1000)) / out["value"] < 0.01
+    # loopback TCP: at least one request and one response segment per request
+    if out["tcp_per_req"]:
+        assert out["tcp_per_req"]["OutSegs"] >= 1.9
 
 
 def test_bench_two_ranks_gloo():
