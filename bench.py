@@ -59,6 +59,9 @@ def parse_args():
     ap.add_argument("--per-conn-quota", action="store_true",
                     help="every connection does exactly --reqs-per-conn per step (default: the step's "
                          "connections x reqs-per-conn requests are shared, so no connection idles at the end)")
+    ap.add_argument("--smt", choices=("off", "split", "pair"), default="off",
+                    help="use the SMT sibling of each planned physical core: off = idle, split = "
+                         "same side, pair = server worker + its load-generator thread on one core")
     ap.add_argument("--busy-poll-us", type=int, default=20,
                     help="spin this long in epoll before sleeping (server and load generator); "
                          "20 us measured best on the box (profiles/r11_box_session), 0 = off")
@@ -90,7 +93,7 @@ def main() -> int:
     if rank == 0:
         per_rank = min(a.cores, max(1, cpu_budget() // local_world)) if a.cores else None
         plan = [{"cores": plan_replicas_with_loadgen(local_world, per_rank, a.server_threads,
-                                                     avoid_busy=not a.no_avoid_busy),
+                                                     avoid_busy=not a.no_avoid_busy, smt=a.smt),
                  "base_port": _free_port_block(a.base_port, local_world)}]
     if dist:
         dist.broadcast_object_list(plan, src=0)
@@ -208,6 +211,7 @@ def main() -> int:
                 "server_threads_per_replica": s_threads,
                 "loadgen_threads_per_replica": len(load_cpus),
                 "busy_poll_us": a.busy_poll_us,
+                "smt": a.smt,
                 "step_budget": "per-connection" if a.per_conn_quota else "shared",
                 "cpu_map": {f"rank{i}": {"server": g["server_cpus"], "loadgen": g["load_cpus"]}
                             for i, g in enumerate(gathered)},

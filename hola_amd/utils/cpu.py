@@ -183,8 +183,24 @@ def split_server_loadgen(cores: list[int], server_threads: int) -> tuple[list[in
     return server, load
 
 
+def sibling_of(cpu: int) -> int | None:
+    """The other SMT thread of `cpu`'s physical core, if it exists and is allowed."""
+    allowed = set(allowed_cpus())
+    for s in siblings(cpu):
+        if s != cpu and s in allowed:
+            return s
+    return None
+
+
+def smt_fits(local_world: int, per_rank: int) -> bool:
+    """True when both SMT threads of every planned physical core can run without the CPU
+    budget (cgroup quota) throttling them: the budget covers 2 x per_rank x local_world."""
+    return cpu_budget() >= 2 * per_rank * local_world and all(
+        sibling_of(c) is not None for c in physical_cores()[:per_rank * local_world])
+
+
 def plan_replicas_with_loadgen(local_world: int, per_rank: int | None = None, server_threads: int = 0,
-                               avoid_busy: bool = True) -> list[dict]:
+                               avoid_busy: bool = True, smt: str = "off") -> list[dict]:
     """Core plan for `local_world` co-located (replica + load generator) ranks with
     client-side round-robin over all replicas.
 
@@ -193,16 +209,33 @@ def plan_replicas_with_loadgen(local_world: int, per_rank: int | None = None, se
     is therefore taken from the *target* replica's L3 domains, so every connection's client
     and server ends share an L3 even though traffic crosses ranks. Returns, per rank,
     {"server": [...], "loadgen": [... one CPU per thread, in thread order]}.
+
+    `smt` decides what happens to the SMT sibling of each planned physical core:
+      * "off"   - left idle (one thread per physical core);
+      * "split" - the sibling joins the same side, so server and load generator each get
+                  twice the threads on the same physical cores;
+      * "pair"  - every physical core runs one server worker and, on its sibling, the
+                  load-generator thread that drives it (the server steers a connection to
+                  the worker on the client's own core: both socket buffers share L1/L2).
     """
     nodes = plan_node(local_world, per_rank, avoid_busy=avoid_busy)
     splits = []
     for cores in nodes:
+        if smt == "pair":
+            sib = [sibling_of(c) for c in cores]
+            if all(x is not None for x in sib):
+                splits.append((list(cores), sib))
+                continue
         if len(cores) > 1:
             st = server_threads or max(1, len(cores) // 2)
             st = min(st, len(cores) - 1)
-            splits.append(split_server_loadgen(cores, st))
+            sv, ld = split_server_loadgen(cores, st)
         else:
-            splits.append((cores, cores))
+            sv, ld = cores, cores
+        if smt == "split":
+            sv = sv + [x for x in map(sibling_of, sv) if x is not None]
+            ld = ld + [x for x in map(sibling_of, ld) if x is not None]
+        splits.append((sv, ld))
     n = local_world
     t_threads = len(splits[0][1])
     uniform = all(len(sp[1]) == t_threads for sp in splits)

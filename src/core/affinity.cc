@@ -88,6 +88,32 @@ int l3_domain_of(int cpu) {
   return (cpu >= 0 && size_t(cpu) < table.size()) ? table[size_t(cpu)] : -1;
 }
 
+int core_of(int cpu) {
+  static const std::vector<int> table = [] {
+    std::vector<int> v;
+    for (int c = 0; c < CPU_SETSIZE; ++c) {
+      std::ifstream f("/sys/devices/system/cpu/cpu" + std::to_string(c) + "/topology/thread_siblings_list");
+      if (!f) {
+        std::ifstream online("/sys/devices/system/cpu/cpu" + std::to_string(c));
+        if (!online) break;  // past the last CPU
+        v.push_back(-1);
+        continue;
+      }
+      std::string line;
+      std::vector<int> sib;
+      if (std::getline(f, line) && parse_cpu_list(line, &sib) && !sib.empty()) {
+        int lo = sib[0];
+        for (int x : sib) lo = x < lo ? x : lo;
+        v.push_back(lo);
+      } else {
+        v.push_back(-1);
+      }
+    }
+    return v;
+  }();
+  return (cpu >= 0 && size_t(cpu) < table.size()) ? table[size_t(cpu)] : -1;
+}
+
 double cgroup_cpu_quota() {
   std::ifstream f("/sys/fs/cgroup/cpu.max");
   std::string q, p;

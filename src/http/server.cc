@@ -394,6 +394,20 @@ Server::Server(ServerOptions opts, RequestHandler* handler) : opts_(std::move(op
       if (it == domain_workers_.end()) domain_workers_.push_back({dom, {i}});
       else it->second.push_back(i);
     }
+    // Workers pinned to a core whose SMT sibling may run a client thread: a connection from
+    // that sibling is served on the same physical core (shared L1/L2 for both socket
+    // buffers). Only cores holding exactly one worker qualify.
+    for (size_t i = 0; i < workers_.size() && i < opts_.cpus.size(); ++i) {
+      int core = core_of(opts_.cpus[i]);
+      if (core < 0) continue;
+      auto it = std::find_if(core_workers_.begin(), core_workers_.end(),
+                             [core](const auto& p) { return p.first == core; });
+      if (it == core_workers_.end()) core_workers_.push_back({core, i});
+      else it->first = -1;  // two workers on one core: no single partner
+    }
+    core_workers_.erase(std::remove_if(core_workers_.begin(), core_workers_.end(),
+                                       [](const auto& p) { return p.first < 0; }),
+                        core_workers_.end());
     if (domain_workers_.size() <= 1) domain_workers_.clear();  // one domain: nothing to steer
     domain_rr_.reset(new std::atomic<uint32_t>[domain_workers_.size() + 1]);
     for (size_t i = 0; i <= domain_workers_.size(); ++i) domain_rr_[i].store(0);
@@ -403,26 +417,40 @@ Server::Server(ServerOptions opts, RequestHandler* handler) : opts_(std::move(op
 Worker* Server::pick_worker(int fd) {
   const size_t n = workers_.size();
   size_t k = rr_.fetch_add(1, std::memory_order_relaxed) % n;
-  if (!domain_workers_.empty()) {
+  if (!domain_workers_.empty() || !core_workers_.empty()) {
     // The CPU that processed this connection's latest packet: for loopback clients, the
     // client thread's own CPU. Serving it from the same L3 keeps both socket buffers in
     // one cache domain (cross-CCD hand-offs more than double the cost of send()).
     int cpu = -1;
     socklen_t len = sizeof cpu;
     if (getsockopt(fd, SOL_SOCKET, SO_INCOMING_CPU, &cpu, &len) == 0 && cpu >= 0) {
-      int dom = l3_domain_of(cpu);
+      auto least_assigned = [&] {
+        int32_t least = assigned_[0].load(std::memory_order_relaxed);
+        for (size_t i = 1; i < n; ++i) least = std::min(least, assigned_[i].load(std::memory_order_relaxed));
+        return least;
+      };
+      // Same physical core first (the client runs on this worker's SMT sibling).
+      const int core = core_workers_.empty() ? -1 : core_of(cpu);
+      for (const auto& [c, wi] : core_workers_) {
+        if (c != core || opts_.cpus[wi] == cpu) continue;
+        if (assigned_[wi].load(std::memory_order_relaxed) <= least_assigned() + 8) {
+          assigned_[wi].fetch_add(1, std::memory_order_relaxed);
+          steered_core_.fetch_add(1, std::memory_order_relaxed);
+          return workers_[wi].get();
+        }
+        break;
+      }
+      int dom = domain_workers_.empty() ? -2 : l3_domain_of(cpu);
       for (size_t d = 0; d < domain_workers_.size(); ++d) {
         if (domain_workers_[d].first != dom) continue;
         const auto& ws = domain_workers_[d].second;
         size_t cand = ws[domain_rr_[d].fetch_add(1, std::memory_order_relaxed) % ws.size()];
         // Keep balance: do not pile onto a domain that is far ahead of the least loaded worker.
-        int32_t least = assigned_[0].load(std::memory_order_relaxed);
-        for (size_t i = 1; i < n; ++i) least = std::min(least, assigned_[i].load(std::memory_order_relaxed));
-        if (assigned_[cand].load(std::memory_order_relaxed) <= least + 8) {
+        if (assigned_[cand].load(std::memory_order_relaxed) <= least_assigned() + 8) {
           k = cand;
-          ++steered_;
+          steered_.fetch_add(1, std::memory_order_relaxed);
         } else {
-          ++unsteered_;
+          unsteered_.fetch_add(1, std::memory_order_relaxed);
         }
         break;
       }
@@ -479,7 +507,7 @@ void Server::Acceptor::on_event(uint32_t) {
       }
       return;
     }
-    if (server->opts_.reuseport_accept && server->domain_workers_.empty()) {
+    if (server->opts_.reuseport_accept && !server->steering()) {
       // The kernel already spread connections over the workers' listeners.
       server->assigned_[size_t(worker->index())].fetch_add(1, std::memory_order_relaxed);
       worker->adopt_here(c, t0);
@@ -586,7 +614,11 @@ std::string Server::profile_json() const {
              (unsigned long long)h.max());
     return std::string(buf);
   };
-  return "{\"unit\":\"ns (batch: requests per recv)\"," + one("accept", all.accept) + "," + one("recv", all.recv) + "," + one("parse", all.parse) + "," +
+  char steer[160];
+  snprintf(steer, sizeof steer, "\"steering\":{\"same_core\":%llu,\"same_l3\":%llu,\"unsteered\":%llu},",
+           (unsigned long long)steered_core_.load(), (unsigned long long)steered_.load(),
+           (unsigned long long)unsteered_.load());
+  return "{\"unit\":\"ns (batch: requests per recv)\"," + std::string(steer) + one("accept", all.accept) + "," + one("recv", all.recv) + "," + one("parse", all.parse) + "," +
          one("handle", all.handle) + "," + one("send", all.send) + "," + one("batch", all.batch) + "}";
 }
 

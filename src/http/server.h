@@ -214,7 +214,7 @@ class Server {
   const ServerOptions& options() const { return opts_; }
   bool draining() const { return draining_.load(std::memory_order_relaxed); }
   uint64_t total_requests() const;
-  bool steering() const { return !domain_workers_.empty(); }
+  bool steering() const { return !domain_workers_.empty() || !core_workers_.empty(); }
   size_t open_connections() const { return open_.load(std::memory_order_relaxed); }
   // JSON summary of the --profile histograms (call after join()).
   std::string profile_json() const;
@@ -238,9 +238,10 @@ class Server {
   // L3-domain steering state (built in the constructor from opts_.cpus).
   Worker* pick_worker(int fd);
   std::vector<std::pair<int, std::vector<size_t>>> domain_workers_;  // (l3 id, worker indices)
+  std::vector<std::pair<int, size_t>> core_workers_;  // (physical core, worker index), one per core
   std::unique_ptr<std::atomic<uint32_t>[]> domain_rr_;
   std::unique_ptr<std::atomic<int32_t>[]> assigned_;  // live connections per worker
-  uint64_t steered_ = 0, unsteered_ = 0;
+  std::atomic<uint64_t> steered_core_{0}, steered_{0}, unsteered_{0};  // accept steering outcomes
   friend class Worker;
 };
 

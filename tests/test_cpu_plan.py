@@ -101,3 +101,34 @@ def test_full_node_eight_ranks(epyc, monkeypatch):
         for t, c in enumerate(p["loadgen"]):
             target = (t + r) % n
             assert cpu.l3_domain(c) in {cpu.l3_domain(x) for x in plans[target]["server"]}
+
+
+def test_smt_pair_puts_each_loadgen_thread_on_its_workers_sibling(epyc, monkeypatch):
+    """--smt pair: rank r's load-generator thread t runs on the SMT sibling of one server
+    core of the replica it drives, and every sibling is used once across the node."""
+    monkeypatch.setattr(cpu, "cgroup_cpu_quota", lambda: 0.0)
+    n = 8
+    assert cpu.smt_fits(n, 16)
+    plans = cpu.plan_replicas_with_loadgen(n, 16, smt="pair")
+    used = [c for p in plans for c in p["server"] + p["loadgen"]]
+    assert len(used) == len(set(used)) == 256
+    for r, p in enumerate(plans):
+        assert len(p["server"]) == 16 and len(p["loadgen"]) == 16
+        assert max(p["server"]) < 128
+        for t, c in enumerate(p["loadgen"]):
+            target = (t + r) % n
+            assert c % 128 in plans[target]["server"]  # sibling of one of the target's cores
+
+
+def test_smt_split_doubles_threads_on_the_same_cores(epyc):
+    plans = cpu.plan_replicas_with_loadgen(1, 8, smt="split")
+    p = plans[0]
+    assert len(p["server"]) == 8 and len(p["loadgen"]) == 8
+    assert {c % 128 for c in p["server"]}.isdisjoint({c % 128 for c in p["loadgen"]})
+    assert not cpu.smt_fits(1, 16)  # the 16-CPU quota cannot run 32 threads
+
+
+def test_smt_pair_single_rank_under_quota(epyc):
+    p = cpu.plan_replicas_with_loadgen(1, 8, smt="pair")[0]
+    assert [c + 128 for c in p["server"]] == p["loadgen"]
+    assert cpu.smt_fits(1, 8)
