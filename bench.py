@@ -30,7 +30,7 @@ from hola_amd.native import ensure_built  # noqa: E402
 from hola_amd.parallel.loadgen import ControlledLoadgen, decode_hist, merge_hists, percentile  # noqa: E402
 from hola_amd.server import HolaProcess  # noqa: E402
 from hola_amd.utils.cpu import (  # noqa: E402
-    cgroup_cpu_quota, cpu_budget, format_cpu_list, plan_replicas_with_loadgen)
+    cgroup_cpu_quota, cpu_budget, format_cpu_list, plan_replicas_with_loadgen, siblings, smt_fits)
 
 METRIC = "HTTP req/sec + p50/p99 latency, GET /api/hola at 1/2/4/8 replicas"
 BASELINE_VALUE = None  # the reference publishes no numbers
@@ -59,9 +59,12 @@ def parse_args():
     ap.add_argument("--per-conn-quota", action="store_true",
                     help="every connection does exactly --reqs-per-conn per step (default: the step's "
                          "connections x reqs-per-conn requests are shared, so no connection idles at the end)")
-    ap.add_argument("--smt", choices=("off", "split", "pair"), default="off",
+    ap.add_argument("--smt", choices=("auto", "off", "split", "pair"), default="auto",
                     help="use the SMT sibling of each planned physical core: off = idle, split = "
-                         "same side, pair = server worker + its load-generator thread on one core")
+                         "same side, pair = server worker + its load-generator thread on one core "
+                         "(1.55x req/s per physical core, profiles/r16_smt); auto = pair when one GPU "
+                         "slot's CPU share (budget / GPUs on the node) holds both threads of --cores "
+                         "cores, else off. Decided per node, so every N runs replicas alike")
     ap.add_argument("--busy-poll-us", type=int, default=20,
                     help="spin this long in epoll before sleeping (server and load generator); "
                          "20 us measured best on the box (profiles/r11_box_session), 0 = off")
@@ -92,13 +95,19 @@ def main() -> int:
     plan = [None]
     if rank == 0:
         per_rank = min(a.cores, max(1, cpu_budget() // local_world)) if a.cores else None
+        smt = a.smt
+        if smt == "auto":
+            slots = max(local_world, _gpu_slots())
+            smt = "pair" if per_rank and smt_fits(slots, per_rank) else "off"
         plan = [{"cores": plan_replicas_with_loadgen(local_world, per_rank, a.server_threads,
-                                                     avoid_busy=not a.no_avoid_busy, smt=a.smt),
+                                                     avoid_busy=not a.no_avoid_busy, smt=smt),
+                 "smt": smt,
                  "base_port": _free_port_block(a.base_port, local_world)}]
     if dist:
         dist.broadcast_object_list(plan, src=0)
     server_cpus, load_cpus = plan[0]["cores"][local_rank]["server"], plan[0]["cores"][local_rank]["loadgen"]
     s_threads = len(server_cpus)
+    smt = plan[0]["smt"]
     base_port = plan[0]["base_port"]
     port = base_port + local_rank
     targets = [("127.0.0.1", base_port + i) for i in range(local_world)]
@@ -207,11 +216,12 @@ def main() -> int:
                 "connections_per_replica": a.connections,
                 "reqs_per_conn_per_step": a.reqs_per_conn,
                 "lb": "client-side round-robin over replica ports",
-                "cores_per_replica": s_threads + len(load_cpus),
+                "cores_per_replica": len({min(siblings(c)) for c in list(server_cpus) + list(load_cpus)}),
                 "server_threads_per_replica": s_threads,
                 "loadgen_threads_per_replica": len(load_cpus),
                 "busy_poll_us": a.busy_poll_us,
-                "smt": a.smt,
+                "smt": smt,
+                "cpus_per_replica": len(set(server_cpus) | set(load_cpus)),
                 "step_budget": "per-connection" if a.per_conn_quota else "shared",
                 "cpu_map": {f"rank{i}": {"server": g["server_cpus"], "loadgen": g["load_cpus"]}
                             for i, g in enumerate(gathered)},
@@ -272,6 +282,15 @@ def _proc_cpu_s(pid: int) -> float:
         return (int(fields[11]) + int(fields[12])) / os.sysconf("SC_CLK_TCK")
     except (OSError, IndexError, ValueError):
         return 0.0
+
+
+def _gpu_slots() -> int:
+    """GPUs on this node (one replica slot each). device_count() does not initialise HIP."""
+    try:
+        import torch
+        return int(torch.cuda.device_count())
+    except Exception:
+        return 0
 
 
 def _tcp_counters() -> dict[str, int]:

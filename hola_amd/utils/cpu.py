@@ -195,8 +195,10 @@ def sibling_of(cpu: int) -> int | None:
 def smt_fits(local_world: int, per_rank: int) -> bool:
     """True when both SMT threads of every planned physical core can run without the CPU
     budget (cgroup quota) throttling them: the budget covers 2 x per_rank x local_world."""
-    return cpu_budget() >= 2 * per_rank * local_world and all(
-        sibling_of(c) is not None for c in physical_cores()[:per_rank * local_world])
+    need = per_rank * local_world
+    phys = physical_cores()
+    return (cpu_budget() >= 2 * need and len(phys) >= need
+            and all(sibling_of(c) is not None for c in phys[:need]))
 
 
 def plan_replicas_with_loadgen(local_world: int, per_rank: int | None = None, server_threads: int = 0,

@@ -132,3 +132,16 @@ def test_smt_pair_single_rank_under_quota(epyc):
     p = cpu.plan_replicas_with_loadgen(1, 8, smt="pair")[0]
     assert [c + 128 for c in p["server"]] == p["loadgen"]
     assert cpu.smt_fits(1, 8)
+
+
+def test_smt_auto_is_decided_per_node(epyc, monkeypatch):
+    """bench.py --smt auto asks whether one GPU slot's CPU share holds both SMT threads of
+    its 16 cores: yes on an unconstrained 256-CPU 8-GPU node, no under a 128-CPU quota or
+    the 1-GPU box's 16-CPU quota, whatever the number of ranks N in this run."""
+    assert not cpu.smt_fits(1, 16)  # 1-GPU box: quota 16
+    monkeypatch.setattr(cpu, "cgroup_cpu_quota", lambda: 128.0)
+    assert not cpu.smt_fits(8, 16)
+    monkeypatch.setattr(cpu, "cgroup_cpu_quota", lambda: 0.0)
+    assert cpu.smt_fits(8, 16)
+    monkeypatch.setattr(cpu, "physical_cores", lambda cpus=None: list(range(64)))
+    assert not cpu.smt_fits(8, 16)  # not enough physical cores for 8 x 16
