@@ -285,7 +285,17 @@ def _proc_cpu_s(pid: int) -> float:
 
 
 def _gpu_slots() -> int:
-    """GPUs on this node (one replica slot each). device_count() does not initialise HIP."""
+    """GPUs on this node (one replica slot each), visible to this process or not: the KFD
+    topology lists every GPU agent (gpu_id != 0), whatever HIP_VISIBLE_DEVICES says; falls
+    back to torch.cuda.device_count() (which does not initialise HIP)."""
+    n = 0
+    for gid in Path("/sys/class/kfd/kfd/topology/nodes").glob("*/gpu_id"):
+        try:
+            n += int(gid.read_text().strip() or "0") != 0
+        except (OSError, ValueError):
+            pass
+    if n:
+        return n
     try:
         import torch
         return int(torch.cuda.device_count())
