@@ -65,6 +65,10 @@ def parse_args():
                          "(1.55x req/s per physical core, profiles/r16_smt); auto = pair when one GPU "
                          "slot's CPU share (budget / GPUs on the node) holds both threads of --cores "
                          "cores, else off. Decided per node, so every N runs replicas alike")
+    ap.add_argument("--busy-poll-pause", type=int, default=-1,
+                    help="PAUSE instructions between empty polls while busy-polling (both sides); "
+                         "-1 = 16 with --smt pair (+6%% req/s: the spinning sibling leaves issue slots "
+                         "to the working one, profiles/r19_pause), else 0")
     ap.add_argument("--busy-poll-us", type=int, default=20,
                     help="spin this long in epoll before sleeping (server and load generator); "
                          "20 us measured best on the box (profiles/r11_box_session), 0 = off")
@@ -108,6 +112,8 @@ def main() -> int:
     server_cpus, load_cpus = plan[0]["cores"][local_rank]["server"], plan[0]["cores"][local_rank]["loadgen"]
     s_threads = len(server_cpus)
     smt = plan[0]["smt"]
+    if a.busy_poll_pause < 0:
+        a.busy_poll_pause = 16 if smt == "pair" else 0
     base_port = plan[0]["base_port"]
     port = base_port + local_rank
     targets = [("127.0.0.1", base_port + i) for i in range(local_world)]
@@ -116,6 +122,8 @@ def main() -> int:
     args = ["--no-tracing"] if a.no_tracing else []
     if a.busy_poll_us:
         args += ["--busy-poll-us", str(a.busy_poll_us)]
+        if a.busy_poll_pause:
+            args += ["--busy-poll-pause", str(a.busy_poll_pause)]
     if a.profile_dir:
         os.makedirs(a.profile_dir, exist_ok=True)
         args += ["--profile", "--profile-out", os.path.join(os.path.abspath(a.profile_dir),
@@ -129,6 +137,7 @@ def main() -> int:
             dist.barrier()  # every replica is listening before any connection is made
         loadgen = ControlledLoadgen(targets, a.connections, len(load_cpus), cpu_list=",".join(map(str, load_cpus)),
                                     path=a.path, target_offset=local_rank, busy_poll_us=a.busy_poll_us,
+                                    busy_poll_pause=a.busy_poll_pause,
                                     per_conn_quota=a.per_conn_quota)
         for _ in range(a.warmup):
             loadgen.run(a.reqs_per_conn)
@@ -220,6 +229,7 @@ def main() -> int:
                 "server_threads_per_replica": s_threads,
                 "loadgen_threads_per_replica": len(load_cpus),
                 "busy_poll_us": a.busy_poll_us,
+                "busy_poll_pause": a.busy_poll_pause,
                 "smt": smt,
                 "cpus_per_replica": len(set(server_cpus) | set(load_cpus)),
                 "step_budget": "per-connection" if a.per_conn_quota else "shared",

@@ -65,6 +65,7 @@ struct Options {
   int target_offset = 0;
   std::vector<std::string> extra_headers;
   int busy_poll_us = 0;
+  int busy_poll_pause = 0;  // PAUSE instructions between empty polls
   double rate = 0;  // --rate: open-loop total req/s (wrk2-style, latency from intended time)
   int spin_us = 0;  // --rate: spin instead of sleeping when the next send is this close (burns CPU)
   // control: a run of R requests per connection is R x connections requests drawn from one
@@ -259,9 +260,11 @@ void thread_main(ThreadState* ts, const Options* o) {
     int n = 0;
     if (o->busy_poll_us > 0) {
       int64_t until = mono_ns() + int64_t(o->busy_poll_us) * 1000;
-      do {
+      for (;;) {
         n = epoll_wait(ts->epfd, evs, 256, 0);
-      } while (n == 0 && mono_ns() < until);
+        if (n != 0 || mono_ns() >= until) break;
+        for (int k = 0; k < o->busy_poll_pause; ++k) __builtin_ia32_pause();
+      }
     }
     if (n == 0) {
       if (rate_mode) {
@@ -461,6 +464,7 @@ int main(int argc, char** argv) {
     else if (a == "--target-offset") o.target_offset = atoi(val().c_str());
     else if (a == "--header" || a == "-H") o.extra_headers.push_back(val());
     else if (a == "--busy-poll-us") o.busy_poll_us = atoi(val().c_str());
+    else if (a == "--busy-poll-pause") o.busy_poll_pause = atoi(val().c_str());
     else if (a == "--rate" || a == "-R") o.rate = atof(val().c_str());
     else if (a == "--spin-us") o.spin_us = atoi(val().c_str());
     else if (a == "--per-conn-quota") o.per_conn_quota = true;
@@ -468,7 +472,7 @@ int main(int argc, char** argv) {
       fprintf(stderr,
               "usage: hola_loadgen --targets h:p[,h:p..] -c CONNS -t THREADS [--cpu-list L] [--path P]\n"
               "                    (--duration S [--warmup S] [--rate R [--spin-us N]] | --control [--per-conn-quota])\n"
-              "                    [--target-offset K] [--busy-poll-us N] [-H 'Name: v']\n");
+              "                    [--target-offset K] [--busy-poll-us N [--busy-poll-pause P]] [-H 'Name: v']\n");
       return 2;
     }
   }

@@ -116,9 +116,11 @@ void EventLoop::run() {
     int n = 0;
     if (busy_poll_ns_ > 0) {
       int64_t until = mono_ns() + busy_poll_ns_;
-      do {
+      for (;;) {
         n = epoll_wait(epfd_, evs, kMaxEvents, 0);
-      } while (n == 0 && mono_ns() < until && !stop_.load(std::memory_order_relaxed));
+        if (n != 0 || mono_ns() >= until || stop_.load(std::memory_order_relaxed)) break;
+        for (int i = 0; i < busy_poll_pause_; ++i) __builtin_ia32_pause();
+      }
     }
     if (n == 0) n = epoll_wait(epfd_, evs, kMaxEvents, next_timeout_ms());
     if (n < 0 && errno != EINTR) {

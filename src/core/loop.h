@@ -56,6 +56,9 @@ class EventLoop {
   // Before blocking in epoll_wait, poll without sleeping for up to `us` microseconds
   // (trades idle CPU for fewer sleep/wake-up cycles under closed-loop load). 0 = off.
   void set_busy_poll_us(int us) { busy_poll_ns_ = int64_t(us) * 1000; }
+  // While busy-polling, execute this many PAUSE instructions after each empty poll, so a
+  // spinning thread leaves issue slots to its SMT sibling. 0 = poll back to back.
+  void set_busy_poll_pause(int n) { busy_poll_pause_ = n; }
 
  private:
   struct WakeHandler : Handler {
@@ -86,6 +89,7 @@ class EventLoop {
   std::vector<Handler*> retired_;
   std::function<void()> tick_, on_exit_;
   int64_t busy_poll_ns_ = 0;
+  int busy_poll_pause_ = 0;
 };
 
 }  // namespace hola

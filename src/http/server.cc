@@ -305,6 +305,7 @@ Worker::Worker(Server* s, int index) : server_(s), index_(index) {
   tick();
   loop_.set_tick([this] { tick(); });
   loop_.set_busy_poll_us(s->options().busy_poll_us);
+  loop_.set_busy_poll_pause(s->options().busy_poll_pause);
 }
 
 RequestHandler& Worker::handler() { return server_->handler(); }

@@ -133,6 +133,7 @@ struct ServerOptions {
   int backlog = 4096;
   size_t read_chunk = 64 * 1024;
   int busy_poll_us = 0;  // see EventLoop::set_busy_poll_us
+  int busy_poll_pause = 0;  // see EventLoop::set_busy_poll_pause
   bool profile = false;  // per-stage latency histograms (SURVEY.md §5.1 --profile)
   // Close keep-alive connections idle this long (Undertow/WildFly no-request-timeout is
   // 60 s by default); 0 disables.

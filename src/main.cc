@@ -59,6 +59,7 @@ void usage() {
           "  --drain-ms N             graceful shutdown drain budget (default 5000)\n"
           "  --port-file PATH         write the bound port here once listening\n"
           "  --busy-poll-us N         spin up to N us in epoll before sleeping (default 0)\n"
+          "  --busy-poll-pause N      PAUSE instructions between empty polls (SMT-friendly spin)\n"
           "  --idle-timeout-ms N      close keep-alive connections idle this long (default 60000, 0 = never)\n"
           "  --max-connections N      refuse connections beyond N per replica (default unlimited)\n"
           "  --no-steer               plain round-robin accept (default: L3-domain steering when pinned)\n"
@@ -141,6 +142,7 @@ int main(int argc, char** argv) {
     else if (a == "--drain-ms") drain_ms = atoi(val("--drain-ms").c_str());
     else if (a == "--port-file") port_file = val("--port-file");
     else if (a == "--busy-poll-us") so.busy_poll_us = atoi(val("--busy-poll-us").c_str());
+    else if (a == "--busy-poll-pause") so.busy_poll_pause = atoi(val("--busy-poll-pause").c_str());
     else if (a == "--profile") so.profile = true;
     else if (a == "--no-steer") so.steer_l3 = false;
     else if (a == "--idle-timeout-ms") so.idle_timeout_ms = atoi(val("--idle-timeout-ms").c_str());
