@@ -63,6 +63,8 @@ void usage() {
           "  --idle-timeout-ms N      close keep-alive connections idle this long (default 60000, 0 = never)\n"
           "  --max-connections N      refuse connections beyond N per replica (default unlimited)\n"
           "  --no-steer               plain round-robin accept (default: L3-domain steering when pinned)\n"
+          "  --no-pin                 leave workers unpinned even when the affinity mask has exactly\n"
+          "                           one CPU per worker (e.g. a kubelet static-CPU-manager cpuset)\n"
           "  --profile                per-stage latency histograms (accept/recv/parse/handle/send), dumped at exit\n"
           "  --profile-out PATH       write the --profile JSON here (default: stderr)\n"
           "  --log-level L            debug|info|warn|error|off (default info)\n"
@@ -94,6 +96,7 @@ int main(int argc, char** argv) {
   if (hn) ao.hostname = hn;  // HolaResource.java:57 getOrDefault("HOSTNAME", "unknown")
   int threads = 0, drain_ms = 5000, stream_max = 5;
   std::string cpu_list, port_file, profile_out;
+  bool auto_pin = true;
   bool no_tracing = false;
 
   for (int i = 1; i < argc; ++i) {
@@ -145,6 +148,7 @@ int main(int argc, char** argv) {
     else if (a == "--busy-poll-pause") so.busy_poll_pause = atoi(val("--busy-poll-pause").c_str());
     else if (a == "--profile") so.profile = true;
     else if (a == "--no-steer") so.steer_l3 = false;
+    else if (a == "--no-pin") auto_pin = false;
     else if (a == "--idle-timeout-ms") so.idle_timeout_ms = atoi(val("--idle-timeout-ms").c_str());
     else if (a == "--max-connections") so.max_connections = size_t(atol(val("--max-connections").c_str()));
     else if (a == "--profile-out") profile_out = val("--profile-out");
@@ -174,6 +178,12 @@ int main(int argc, char** argv) {
     double quota = cgroup_cpu_quota();
     if (quota > 0 && double(n) > quota) n = size_t(quota);
     threads = n ? int(n) : 1;
+  }
+  if (cpus.empty() && auto_pin && threads > 1) {
+    // Exclusive cpuset (Guaranteed pod with integer CPUs under the static CPU manager, or
+    // taskset): one worker per allowed CPU, each pinned, which also enables accept steering.
+    std::vector<int> allowed = allowed_cpus();
+    if (allowed.size() == size_t(threads)) cpus = allowed;
   }
   so.threads = threads;
   so.cpus = cpus;

@@ -1,6 +1,8 @@
 """The behavioural contract of the reference service, end to end against the
 native server binary."""
 import json
+import os
+import shutil
 import socket
 import time
 
@@ -307,3 +309,16 @@ def test_ipv6_listener(hola):
         while chunk := c.recv(65536):
             data += chunk
     assert data.startswith(b"HTTP/1.1 200 OK") and data.endswith(b"\r\n\r\nHola de v6")
+
+
+@pytest.mark.skipif(shutil.which("taskset") is None or len(os.sched_getaffinity(0)) < 2, reason="needs taskset, 2 CPUs")
+def test_workers_pin_to_an_exclusive_cpuset(hola):
+    """A cpuset with exactly one CPU per worker (kubelet static CPU manager) pins the workers
+    without --cpu-list; --no-pin opts out."""
+    cpus = sorted(os.sched_getaffinity(0))[:2]
+    wrap = ["taskset", "-c", ",".join(map(str, cpus))]
+    s = hola(wrapper=wrap, threads=2)
+    assert s.get("/api/hola")[0] == 200
+    assert f"cpus={cpus[0]},{cpus[1]}" in s.log() or f"cpus={cpus[0]}-{cpus[1]}" in s.log(), s.log()
+    s2 = hola(wrapper=wrap, threads=2, args=["--no-pin"])
+    assert "cpus=unpinned" in s2.log(), s2.log()
