@@ -68,6 +68,8 @@ def parse_args():
                          "(1.55x req/s per physical core, profiles/r16_smt); auto = pair when one GPU "
                          "slot's CPU share (budget / GPUs on the node) holds both threads of --cores "
                          "cores, else off. Decided per node, so every N runs replicas alike")
+    ap.add_argument("--epoll-lt", action="store_true",
+                    help="level-triggered epoll for connection sockets on both sides (default: edge)")
     ap.add_argument("--busy-poll-pause", type=int, default=-1,
                     help="PAUSE instructions between empty polls while busy-polling (both sides); "
                          "-1 = 16 with --smt pair (+6%% req/s: the spinning sibling leaves issue slots "
@@ -128,6 +130,8 @@ def main() -> int:
     args = ["--no-tracing"] if a.no_tracing else []
     if host != "127.0.0.1":
         args += ["--host", host]
+    if a.epoll_lt:
+        args += ["--epoll-lt"]
     if a.busy_poll_us:
         args += ["--busy-poll-us", str(a.busy_poll_us)]
         if a.busy_poll_pause:
@@ -145,7 +149,7 @@ def main() -> int:
             dist.barrier()  # every replica is listening before any connection is made
         loadgen = ControlledLoadgen(targets, a.connections, len(load_cpus), cpu_list=",".join(map(str, load_cpus)),
                                     path=a.path, target_offset=local_rank, busy_poll_us=a.busy_poll_us,
-                                    busy_poll_pause=a.busy_poll_pause,
+                                    busy_poll_pause=a.busy_poll_pause, epoll_lt=a.epoll_lt,
                                     per_conn_quota=a.per_conn_quota)
         for _ in range(a.warmup):
             loadgen.run(a.reqs_per_conn)
@@ -239,6 +243,7 @@ def main() -> int:
                 "loadgen_threads_per_replica": len(load_cpus),
                 "busy_poll_us": a.busy_poll_us,
                 "busy_poll_pause": a.busy_poll_pause,
+                "epoll": "level" if a.epoll_lt else "edge",
                 "smt": smt,
                 "cpus_per_replica": len(set(server_cpus) | set(load_cpus)),
                 "step_budget": "per-connection" if a.per_conn_quota else "shared",

@@ -66,6 +66,9 @@ struct Options {
   std::vector<std::string> extra_headers;
   int busy_poll_us = 0;
   int busy_poll_pause = 0;  // PAUSE instructions between empty polls
+  // Edge-triggered connection sockets: a response (<4 KiB) arrives in one read, so a short
+  // read drains the socket and no re-poll of level-triggered items is needed.
+  bool edge_triggered = true;
   double rate = 0;  // --rate: open-loop total req/s (wrk2-style, latency from intended time)
   int spin_us = 0;  // --rate: spin instead of sleeping when the next send is this close (burns CPU)
   // control: a run of R requests per connection is R x connections requests drawn from one
@@ -186,8 +189,9 @@ void thread_main(ThreadState* ts, const Options* o) {
   }
   signal_done();
   epoll_event ev{};
+  const uint32_t conn_events = EPOLLIN | (o->edge_triggered ? uint32_t(EPOLLET) : 0u);
   for (auto& c : ts->conns) {
-    ev.events = EPOLLIN;
+    ev.events = conn_events;
     ev.data.ptr = c.get();
     epoll_ctl(ts->epfd, EPOLL_CTL_ADD, c->fd, &ev);
   }
@@ -334,7 +338,7 @@ void thread_main(ThreadState* ts, const Options* o) {
           signal_done();
           break;
         }
-        ev.events = EPOLLIN;
+        ev.events = conn_events;
         ev.data.ptr = c;
         epoll_ctl(ts->epfd, EPOLL_CTL_ADD, c->fd, &ev);
         if (c->quota > 0 && !send_req(c)) ++ts->errors;
@@ -369,7 +373,7 @@ void thread_main(ThreadState* ts, const Options* o) {
           signal_done();
           break;
         }
-        ev.events = EPOLLIN;
+        ev.events = conn_events;
         ev.data.ptr = c;
         epoll_ctl(ts->epfd, EPOLL_CTL_ADD, c->fd, &ev);
       }
@@ -465,6 +469,7 @@ int main(int argc, char** argv) {
     else if (a == "--header" || a == "-H") o.extra_headers.push_back(val());
     else if (a == "--busy-poll-us") o.busy_poll_us = atoi(val().c_str());
     else if (a == "--busy-poll-pause") o.busy_poll_pause = atoi(val().c_str());
+    else if (a == "--epoll-lt") o.edge_triggered = false;
     else if (a == "--rate" || a == "-R") o.rate = atof(val().c_str());
     else if (a == "--spin-us") o.spin_us = atoi(val().c_str());
     else if (a == "--per-conn-quota") o.per_conn_quota = true;
@@ -472,7 +477,7 @@ int main(int argc, char** argv) {
       fprintf(stderr,
               "usage: hola_loadgen --targets h:p[,h:p..] -c CONNS -t THREADS [--cpu-list L] [--path P]\n"
               "                    (--duration S [--warmup S] [--rate R [--spin-us N]] | --control [--per-conn-quota])\n"
-              "                    [--target-offset K] [--busy-poll-us N [--busy-poll-pause P]] [-H 'Name: v']\n");
+              "                    [--target-offset K] [--busy-poll-us N [--busy-poll-pause P]] [--epoll-lt] [-H 'Name: v']\n");
       return 2;
     }
   }

@@ -56,7 +56,7 @@ class ControlledLoadgen:
     def __init__(self, targets: list[tuple[str, int]], connections: int, threads: int,
                  cpu_list: str | None = None, path: str = "/api/hola", target_offset: int = 0,
                  headers: list[str] | None = None, busy_poll_us: int = 0, per_conn_quota: bool = False,
-                 busy_poll_pause: int = 0):
+                 busy_poll_pause: int = 0, epoll_lt: bool = False):
         cmd = [str(binary("hola_loadgen")), "--targets", ",".join(f"{h}:{p}" for h, p in targets),
                "-c", str(connections), "-t", str(threads), "--path", path, "--control",
                "--target-offset", str(target_offset)]
@@ -70,6 +70,8 @@ class ControlledLoadgen:
                 cmd += ["--busy-poll-pause", str(busy_poll_pause)]
         if per_conn_quota:
             cmd += ["--per-conn-quota"]
+        if epoll_lt:
+            cmd += ["--epoll-lt"]
         self.proc = subprocess.Popen(cmd, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, bufsize=1)
         ready = self._read()
         if not ready.get("ready"):

@@ -59,52 +59,74 @@ void Connection::on_event(uint32_t ev) {
     on_writable();
     if (closed_) return;
   }
-  if (ev & (EPOLLIN | EPOLLHUP | EPOLLRDHUP)) on_readable();
+  if (ev & (EPOLLIN | EPOLLHUP | EPOLLRDHUP)) on_readable((ev & (EPOLLHUP | EPOLLRDHUP)) != 0);
 }
 
-void Connection::on_readable() {
+void Connection::on_readable(bool peer_closed) {
   WorkerStats& st = worker_->stats();
   last_active_ms_ = worker_->loop().now_ms();
+  // Sockets are edge-triggered by default (ServerOptions::edge_triggered): a read that fills
+  // the buffer may have left data behind, so read again; a short read drained the socket.
+  // This saves the re-poll of every level-triggered ready item on the next epoll_wait. When
+  // the peer has shut down its side, its FIN may sit behind the data of this same edge: read
+  // on to the EOF, answer what was read, then close.
   if (streaming_) {
     char buf[4096];
-    ssize_t n = ::recv(fd_, buf, sizeof buf, 0);
-    if (n == 0 || (n < 0 && errno != EAGAIN && errno != EINTR)) close();
-    return;
+    for (;;) {
+      ssize_t n = ::recv(fd_, buf, sizeof buf, 0);
+      if (n < 0 && errno == EINTR) continue;
+      if (n == 0 || (n < 0 && errno != EAGAIN)) close();
+      if (n < ssize_t(sizeof buf)) return;
+    }
   }
-  if (parked_ || !reading_) return;
   StageProfile* prof = worker_->profile();
-  int64_t t0 = prof ? mono_ns() : 0;
-  if (in_.empty()) {
-    char* buf = worker_->scratch();
-    ssize_t n = ::recv(fd_, buf, worker_->scratch_size(), 0);
-    if (prof && n > 0) prof->recv.add(uint64_t(mono_ns() - t0));
-    if (n <= 0) {
-      if (n == 0 || (errno != EAGAIN && errno != EINTR)) close();
-      return;
+  while (!parked_ && reading_ && !streaming_ && !closed_) {
+    int64_t t0 = prof ? mono_ns() : 0;
+    bool more;
+    if (in_.empty()) {
+      char* buf = worker_->scratch();
+      const size_t cap = worker_->scratch_size();
+      ssize_t n = ::recv(fd_, buf, cap, 0);
+      if (prof && n > 0) prof->recv.add(uint64_t(mono_ns() - t0));
+      if (n <= 0) {
+        if (n < 0 && errno == EINTR) continue;
+        if (n == 0 || errno != EAGAIN) {
+          flush();
+          close();
+        }
+        break;
+      }
+      WorkerStats::bump(st.bytes_in, uint64_t(n));
+      more = size_t(n) == cap || peer_closed;
+      size_t consumed = 0;
+      if (!process(buf, size_t(n), &consumed)) return;
+      if (consumed < size_t(n)) in_.assign(buf + consumed, size_t(n) - consumed);
+    } else {
+      size_t old = in_.size();
+      size_t chunk = worker_->server().options().read_chunk;
+      in_.resize(old + chunk);
+      ssize_t n = ::recv(fd_, &in_[old], chunk, 0);
+      if (n <= 0) {
+        in_.resize(old);
+        if (n < 0 && errno == EINTR) continue;
+        if (n == 0 || errno != EAGAIN) {
+          flush();
+          close();
+        }
+        break;
+      }
+      WorkerStats::bump(st.bytes_in, uint64_t(n));
+      in_.resize(old + size_t(n));
+      more = size_t(n) == chunk || peer_closed;
+      size_t consumed = 0;
+      std::string buf;
+      buf.swap(in_);  // handlers may park: leftovers are re-stored below
+      if (!process(buf.data(), buf.size(), &consumed)) return;
+      if (consumed < buf.size()) in_.assign(buf, consumed, std::string::npos);
     }
-    WorkerStats::bump(st.bytes_in, uint64_t(n));
-    size_t consumed = 0;
-    if (!process(buf, size_t(n), &consumed)) return;
-    if (consumed < size_t(n)) in_.assign(buf + consumed, size_t(n) - consumed);
-  } else {
-    size_t old = in_.size();
-    size_t chunk = worker_->server().options().read_chunk;
-    in_.resize(old + chunk);
-    ssize_t n = ::recv(fd_, &in_[old], chunk, 0);
-    if (n <= 0) {
-      in_.resize(old);
-      if (n == 0 || (errno != EAGAIN && errno != EINTR)) close();
-      return;
-    }
-    WorkerStats::bump(st.bytes_in, uint64_t(n));
-    in_.resize(old + size_t(n));
-    size_t consumed = 0;
-    std::string buf;
-    buf.swap(in_);  // handlers may park: leftovers are re-stored below
-    if (!process(buf.data(), buf.size(), &consumed)) return;
-    if (consumed < buf.size()) in_.assign(buf, consumed, std::string::npos);
+    if (!more) break;
   }
-  flush();
+  if (!closed_) flush();
 }
 
 bool Connection::process(const char* data, size_t len, size_t* consumed) {
@@ -262,7 +284,7 @@ void Connection::on_writable() { flush(); }
 
 void Connection::update_interest() {
   if (closed_) return;
-  uint32_t ev = 0;
+  uint32_t ev = worker_->server().options().edge_triggered ? uint32_t(EPOLLET) : 0u;
   if (streaming_) ev |= EPOLLIN | EPOLLRDHUP;
   else if (reading_ && !parked_) ev |= EPOLLIN | EPOLLRDHUP;
   if (want_write_) ev |= EPOLLOUT;
@@ -363,7 +385,8 @@ void Worker::adopt_here(int fd, int64_t accepted_ns) {
     delete c;  // over the limit: refuse by closing (the client sees a reset/EOF)
     return;
   }
-  if (server_->draining() || !loop_.add(fd, EPOLLIN | EPOLLRDHUP, c)) {
+  const uint32_t et = server_->options().edge_triggered ? uint32_t(EPOLLET) : 0u;
+  if (server_->draining() || !loop_.add(fd, EPOLLIN | EPOLLRDHUP | et, c)) {
     server_->assigned_[size_t(index_)].fetch_sub(1, std::memory_order_relaxed);
     delete c;
     return;

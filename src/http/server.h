@@ -80,7 +80,7 @@ class Connection final : public EventLoop::Handler {
   int64_t last_active_ms() const { return last_active_ms_; }
 
  private:
-  void on_readable();
+  void on_readable(bool peer_closed);
   void on_writable();
   // Parses and dispatches buffered requests; returns false if the connection closed.
   bool process(const char* data, size_t len, size_t* consumed);
@@ -134,6 +134,7 @@ struct ServerOptions {
   size_t read_chunk = 64 * 1024;
   int busy_poll_us = 0;  // see EventLoop::set_busy_poll_us
   int busy_poll_pause = 0;  // see EventLoop::set_busy_poll_pause
+  bool edge_triggered = true;  // EPOLLET on connection sockets (--epoll-lt turns it off)
   bool profile = false;  // per-stage latency histograms (SURVEY.md §5.1 --profile)
   // Close keep-alive connections idle this long (Undertow/WildFly no-request-timeout is
   // 60 s by default); 0 disables.

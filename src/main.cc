@@ -63,6 +63,7 @@ void usage() {
           "  --idle-timeout-ms N      close keep-alive connections idle this long (default 60000, 0 = never)\n"
           "  --max-connections N      refuse connections beyond N per replica (default unlimited)\n"
           "  --no-steer               plain round-robin accept (default: L3-domain steering when pinned)\n"
+          "  --epoll-lt               level-triggered connection sockets (default: edge-triggered)\n"
           "  --no-pin                 leave workers unpinned even when the affinity mask has exactly\n"
           "                           one CPU per worker (e.g. a kubelet static-CPU-manager cpuset)\n"
           "  --profile                per-stage latency histograms (accept/recv/parse/handle/send), dumped at exit\n"
@@ -149,6 +150,7 @@ int main(int argc, char** argv) {
     else if (a == "--profile") so.profile = true;
     else if (a == "--no-steer") so.steer_l3 = false;
     else if (a == "--no-pin") auto_pin = false;
+    else if (a == "--epoll-lt") so.edge_triggered = false;
     else if (a == "--idle-timeout-ms") so.idle_timeout_ms = atoi(val("--idle-timeout-ms").c_str());
     else if (a == "--max-connections") so.max_connections = size_t(atol(val("--max-connections").c_str()));
     else if (a == "--profile-out") profile_out = val("--profile-out");

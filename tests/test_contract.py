@@ -322,3 +322,25 @@ def test_workers_pin_to_an_exclusive_cpuset(hola):
     assert f"cpus={cpus[0]},{cpus[1]}" in s.log() or f"cpus={cpus[0]}-{cpus[1]}" in s.log(), s.log()
     s2 = hola(wrapper=wrap, threads=2, args=["--no-pin"])
     assert "cpus=unpinned" in s2.log(), s2.log()
+
+
+@pytest.mark.parametrize("mode", [[], ["--epoll-lt"]], ids=["edge", "level"])
+def test_request_then_fin_is_answered_and_closed_promptly(hola, mode):
+    """A FIN that arrives with the request (same epoll edge) must still be seen: the server
+    answers, then closes at once instead of waiting for the idle sweep."""
+    s = hola(args=["--idle-timeout-ms", "5000", *mode])
+    for payload, want in ((b"GET /api/hola HTTP/1.1\r\nHost: x\r\n\r\n", b"Hola de testhost"),
+                          (b"GET /api/hola HTTP/1.1\r\nHost: x\r\nX-Partial: ", b"")):
+        c = socket.create_connection(("127.0.0.1", s.port), timeout=3)
+        c.sendall(payload)
+        c.shutdown(socket.SHUT_WR)
+        t0 = time.monotonic()
+        data = b""
+        while True:
+            chunk = c.recv(65536)
+            if not chunk:
+                break
+            data += chunk
+        c.close()
+        assert time.monotonic() - t0 < 1.0
+        assert want in data
