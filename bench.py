@@ -30,7 +30,7 @@ from hola_amd.native import ensure_built  # noqa: E402
 from hola_amd.parallel.loadgen import ControlledLoadgen, decode_hist, merge_hists, percentile  # noqa: E402
 from hola_amd.server import HolaProcess  # noqa: E402
 from hola_amd.utils.cpu import (  # noqa: E402
-    cgroup_cpu_quota, cpu_budget, format_cpu_list, plan_replicas_with_loadgen, siblings, smt_fits)
+    cgroup_cpu_quota, cpu_budget, format_cpu_list, plan_replicas_with_loadgen, siblings, slot_cores, smt_fits)
 
 METRIC = "HTTP req/sec + p50/p99 latency, GET /api/hola at 1/2/4/8 replicas"
 BASELINE_VALUE = None  # the reference publishes no numbers
@@ -44,10 +44,11 @@ def parse_args():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--connections", type=int, default=64, help="keep-alive connections per replica")
     ap.add_argument("--reqs-per-conn", type=int, default=50000, help="requests per connection per step")
-    ap.add_argument("--cores", type=int, default=16,
-                    help="host cores per replica (server + load generator), capped by the node's CPU "
-                         "budget / replicas; 16 = the CPU share of one GPU slot, so every N runs each "
-                         "replica on the same resources (weak scaling)")
+    ap.add_argument("--cores", type=int, default=0,
+                    help="physical host cores per replica (server + load generator); 0 = one GPU "
+                         "slot's share of the node: min(CPU budget, physical cores) / GPUs on the node "
+                         "(16 on the 16-CPU box and on a 2x64-core 8-GPU node), decided per node, so "
+                         "every N runs each replica on the same resources (weak scaling)")
     ap.add_argument("--server-threads", type=int, default=0, help="0 = half of the rank's cores")
     ap.add_argument("--base-port", type=int, default=int(os.environ.get("HOLA_BENCH_PORT", "18400")))
     ap.add_argument("--path", default="/api/hola")
@@ -103,15 +104,16 @@ def main() -> int:
     # within a rank, server worker t and loadgen thread t share an L3 domain. ----
     plan = [None]
     if rank == 0:
-        per_rank = min(a.cores, max(1, cpu_budget() // local_world)) if a.cores else None
+        slots = max(local_world, _gpu_slots())
+        cores = a.cores or slot_cores(slots)
+        per_rank = min(cores, max(1, cpu_budget() // local_world))
         host = a.host if a.host != "auto" else ("::1" if _can_bind("::1") else "127.0.0.1")
         smt = a.smt
         if smt == "auto":
-            slots = max(local_world, _gpu_slots())
-            smt = "pair" if per_rank and smt_fits(slots, per_rank) else "off"
+            smt = "pair" if smt_fits(slots, per_rank) else "off"
         plan = [{"cores": plan_replicas_with_loadgen(local_world, per_rank, a.server_threads,
                                                      avoid_busy=not a.no_avoid_busy, smt=smt),
-                 "smt": smt,
+                 "smt": smt, "gpu_slots": slots,
                  "host": host,
                  "base_port": _free_port_block(a.base_port, local_world, host)}]
     if dist:
@@ -245,6 +247,7 @@ def main() -> int:
                 "busy_poll_pause": a.busy_poll_pause,
                 "epoll": "level" if a.epoll_lt else "edge",
                 "smt": smt,
+                "gpu_slots_on_node": plan[0]["gpu_slots"],
                 "cpus_per_replica": len(set(server_cpus) | set(load_cpus)),
                 "step_budget": "per-connection" if a.per_conn_quota else "shared",
                 "cpu_map": {f"rank{i}": {"server": g["server_cpus"], "loadgen": g["load_cpus"]}

@@ -183,6 +183,13 @@ def split_server_loadgen(cores: list[int], server_threads: int) -> tuple[list[in
     return server, load
 
 
+def slot_cores(gpu_slots: int) -> int:
+    """Physical cores per GPU slot: the node's usable physical cores (CPU budget or physical
+    core count, whichever is smaller) divided by its GPUs. 16 on the 16-CPU gpurun box and on
+    a 2 x 64-core 8-GPU node; it grows with bigger hosts."""
+    return max(1, min(cpu_budget(), len(physical_cores())) // max(1, gpu_slots))
+
+
 def sibling_of(cpu: int) -> int | None:
     """The other SMT thread of `cpu`'s physical core, if it exists and is allowed."""
     allowed = set(allowed_cpus())

@@ -145,3 +145,14 @@ def test_smt_auto_is_decided_per_node(epyc, monkeypatch):
     assert cpu.smt_fits(8, 16)
     monkeypatch.setattr(cpu, "physical_cores", lambda cpus=None: list(range(64)))
     assert not cpu.smt_fits(8, 16)  # not enough physical cores for 8 x 16
+
+
+def test_slot_cores_per_node(epyc, monkeypatch):
+    """bench.py's default cores per replica: one GPU slot's share of the node."""
+    assert cpu.slot_cores(1) == 16  # 1-GPU box: 16-CPU quota
+    monkeypatch.setattr(cpu, "cgroup_cpu_quota", lambda: 0.0)
+    assert cpu.slot_cores(8) == 16  # 2 x 64 cores, 8 GPUs
+    assert cpu.smt_fits(8, cpu.slot_cores(8))
+    monkeypatch.setattr(cpu, "allowed_cpus", lambda: list(range(384)))
+    monkeypatch.setattr(cpu, "physical_cores", lambda cpus=None: list(range(192)))
+    assert cpu.slot_cores(8) == 24  # 2 x 96 cores
