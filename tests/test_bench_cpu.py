@@ -40,3 +40,17 @@ def test_bench_two_ranks_gloo():
                "--steps", "2", "--warmup", "1", "--reqs-per-conn", "100"], 18820)
     assert out["n_gpus"] == 2 and out["requests"] == 2 * 64 * 100 * 2
     assert out["config"]["global_batch"] == 128
+
+
+def test_bench_four_ranks_gloo():
+    """N=4 (BASELINE config 4 shape, scaled down): every rank's load generator deals its 64
+    connections over all 4 replicas; the JSON line reports the node-wide total."""
+    out = run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+               "--master-addr", "127.0.0.1", "--master-port", "29563", str(ROOT / "bench.py"), "--gpus", "4",
+               "--steps", "2", "--warmup", "1", "--reqs-per-conn", "50"], 18840)
+    assert out["n_gpus"] == 4 and out["requests"] == 4 * 64 * 50 * 2
+    assert out["errors"] == 0 and out["non2xx"] == 0
+    assert out["config"]["global_batch"] == 256 and out["config"]["parallelism"] == "replicas4"
+    from hola_amd.utils.cpu import parse_cpu_list
+    cpus = [c for r in out["config"]["cpu_map"].values() for side in r.values() for c in parse_cpu_list(side)]
+    assert len(cpus) == len(set(cpus))  # disjoint core sets across ranks
