@@ -75,6 +75,10 @@ def parse_args():
                     help="PAUSE instructions between empty polls while busy-polling (both sides); "
                          "-1 = 16 with --smt pair (+6%% req/s: the spinning sibling leaves issue slots "
                          "to the working one, profiles/r19_pause), else 0")
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="requests per connection sent back to back before waiting for their "
+                         "responses (wrk's pipeline.lua, as in the TechEmpower plaintext test); "
+                         "1 = wrk's default and the headline (BASELINE configs 2-4)")
     ap.add_argument("--busy-poll-us", type=int, default=20,
                     help="spin this long in epoll before sleeping (server and load generator); "
                          "20 us measured best on the box (profiles/r11_box_session), 0 = off")
@@ -152,7 +156,7 @@ def main() -> int:
         loadgen = ControlledLoadgen(targets, a.connections, len(load_cpus), cpu_list=",".join(map(str, load_cpus)),
                                     path=a.path, target_offset=local_rank, busy_poll_us=a.busy_poll_us,
                                     busy_poll_pause=a.busy_poll_pause, epoll_lt=a.epoll_lt,
-                                    per_conn_quota=a.per_conn_quota)
+                                    per_conn_quota=a.per_conn_quota, pipeline=a.pipeline)
         for _ in range(a.warmup):
             loadgen.run(a.reqs_per_conn)
         loadgen.reset()
@@ -211,7 +215,9 @@ def main() -> int:
             "scaling": "weak",
             "vs_baseline": None if BASELINE_VALUE is None else round(value / BASELINE_VALUE, 4),
             "dtype": "n/a (host-CPU HTTP service; no tensor compute)",
-            "data": "synthetic closed-loop HTTP load (native loadgen, keep-alive, 1 request in flight per connection)",
+            "data": "synthetic closed-loop HTTP load (native loadgen, keep-alive, "
+                    + ("1 request in flight per connection)" if a.pipeline == 1 else
+                       f"{a.pipeline} pipelined requests in flight per connection)"),
             "p50_ms": round(percentile(hist, 50) / 1e6, 4),
             "p99_ms": round(percentile(hist, 99) / 1e6, 4),
             "p999_ms": round(percentile(hist, 99.9) / 1e6, 4),
@@ -238,6 +244,7 @@ def main() -> int:
                 "parallelism": f"replicas{world}",
                 "connections_per_replica": a.connections,
                 "reqs_per_conn_per_step": a.reqs_per_conn,
+                "pipeline": a.pipeline,
                 "lb": "client-side round-robin over replica ports",
                 "loopback": host,
                 "cores_per_replica": len({min(siblings(c)) for c in list(server_cpus) + list(load_cpus)}),

@@ -2,7 +2,9 @@
 //
 // C keep-alive connections spread over T pinned threads; each connection keeps exactly
 // one request in flight (no pipelining, like wrk's default) and records send->last-byte
-// latency in a log-linear histogram. Connections are dealt round-robin over --targets
+// latency in a log-linear histogram. `--pipeline P` sends P requests back to back in one
+// write and waits for all P responses (wrk's pipeline.lua, the TechEmpower "plaintext"
+// setup); each response's latency is counted from the batch's send. Connections are dealt round-robin over --targets
 // (client-side round-robin across replicas, BASELINE.json config 4).
 //
 // Modes:
@@ -75,14 +77,16 @@ struct Options {
   // shared budget (connections that answer faster do more, so no thread idles at the end of
   // a run waiting for a slower one); --per-conn-quota gives each connection exactly R.
   bool per_conn_quota = false;
+  int pipeline = 1;  // requests per batch (closed loop only)
 };
 
 struct Conn {
   int fd = -1;
   int target = 0;
-  std::string req;
-  char buf[4096];
+  std::string req;   // one batch: `pipeline` copies of the request
+  char buf[16384];  // holds a whole batch of responses
   size_t have = 0;
+  int inflight = 0;  // responses still due for the batch in flight
   int64_t t0 = 0;
   int64_t quota = 0;  // remaining requests in control mode
   bool busy = false;
@@ -98,7 +102,7 @@ struct ThreadState {
   Histogram hist;
   std::mutex hist_mu;
   uint64_t completed = 0, errors = 0, non2xx = 0, reconnects = 0;
-  std::atomic<int64_t> run_quota{0};  // control: requests per connection for the next run
+  std::atomic<int64_t> run_quota{0};  // control: batches per connection for the next run
   std::atomic<uint64_t> run_gen{0};
   std::atomic<uint64_t> done_gen{0};
   std::atomic<uint64_t> done_requests{0}, done_errors{0};
@@ -140,10 +144,11 @@ bool connect_conn(Conn* c, const Options& o) {
   return false;
 }
 
-bool send_req(Conn* c) {
+bool send_req(Conn* c, int depth) {
   c->t0 = mono_ns();
   c->busy = true;
   c->have = 0;
+  c->inflight = depth;
   size_t off = 0;
   while (off < c->req.size()) {
     ssize_t w = ::send(c->fd, c->req.data() + off, c->req.size() - off, MSG_NOSIGNAL);
@@ -157,8 +162,9 @@ bool send_req(Conn* c) {
   return true;
 }
 
-// Returns 1 when a full response is in buf, 0 if more is needed, -1 on malformed input.
-int response_complete(Conn* c, int* status, bool* close) {
+// Returns 1 when a full response is at the start of buf (its size in *used), 0 if more is
+// needed, -1 on malformed input.
+int response_complete(Conn* c, int* status, bool* close, size_t* used) {
   std::string_view s(c->buf, c->have);
   size_t he = s.find("\r\n\r\n");
   if (he == std::string_view::npos) return c->have >= sizeof c->buf ? -1 : 0;
@@ -172,7 +178,8 @@ int response_complete(Conn* c, int* status, bool* close) {
     for (size_t i = p + 16; i < head.size() && head[i] >= '0' && head[i] <= '9'; ++i) cl = cl * 10 + size_t(head[i] - '0');
   *close = head.find("Connection: close") != std::string_view::npos;
   if (he + 4 + cl > sizeof c->buf) return -1;
-  return c->have >= he + 4 + cl ? 1 : 0;
+  *used = he + 4 + cl;
+  return c->have >= *used ? 1 : 0;
 }
 
 void thread_main(ThreadState* ts, const Options* o) {
@@ -224,7 +231,7 @@ void thread_main(ThreadState* ts, const Options* o) {
   auto start_all = [&]() {
     for (auto& c : ts->conns) {
       if (c->busy || c->quota <= 0) continue;
-      if (!send_req(c.get())) ++ts->errors;
+      if (!send_req(c.get(), o->pipeline)) ++ts->errors;
     }
   };
   // --rate (open loop): connection k of this thread sends every `interval` ns on a fixed
@@ -251,7 +258,7 @@ void thread_main(ThreadState* ts, const Options* o) {
       if (c->next_due <= now) {
         c->intended = c->next_due;
         c->next_due += interval;
-        if (!send_req(c.get())) ++ts->errors;
+        if (!send_req(c.get(), o->pipeline)) ++ts->errors;
       } else {
         wait = std::min(wait, c->next_due - now);
       }
@@ -341,20 +348,24 @@ void thread_main(ThreadState* ts, const Options* o) {
         ev.events = conn_events;
         ev.data.ptr = c;
         epoll_ctl(ts->epfd, EPOLL_CTL_ADD, c->fd, &ev);
-        if (c->quota > 0 && !send_req(c)) ++ts->errors;
+        if (c->quota > 0 && !send_req(c, o->pipeline)) ++ts->errors;
         continue;
       }
       c->have += size_t(r);
-      int status = 0;
       bool close = false;
-      int rc = response_complete(c, &status, &close);
-      if (rc == 0) continue;
-      if (rc < 0) {
-        ++ts->errors;
-        ++run_errors;
-        close = true;
-      } else {
-        int64_t lat = mono_ns() - (rate_mode ? c->intended : c->t0);
+      const int64_t now_rx = mono_ns();
+      for (;;) {  // every complete response in the buffer (several when pipelining)
+        int status = 0;
+        size_t used = 0;
+        int rc = response_complete(c, &status, &close, &used);
+        if (rc == 0) break;
+        if (rc < 0) {
+          ++ts->errors;
+          ++run_errors;
+          close = true;
+          break;
+        }
+        int64_t lat = now_rx - (rate_mode ? c->intended : c->t0);
         // (the histogram is only read between control runs / after the run: no lock)
         if (ts->recording) {
           ts->hist.add(uint64_t(lat));
@@ -362,7 +373,12 @@ void thread_main(ThreadState* ts, const Options* o) {
         }
         if (status < 200 || status > 299) ++ts->non2xx;
         ++run_requests;
+        --c->inflight;
+        c->have -= used;
+        if (c->have) memmove(c->buf, c->buf + used, c->have);
+        if (close || c->inflight <= 0) break;
       }
+      if (!close && c->inflight > 0) continue;  // the rest of the batch is still due
       c->busy = false;
       if (close) {
         epoll_ctl(ts->epfd, EPOLL_CTL_DEL, c->fd, nullptr);
@@ -391,7 +407,7 @@ void thread_main(ThreadState* ts, const Options* o) {
         }
       }
       if (rate_mode) continue;  // the schedule decides when this connection sends next
-      if (!send_req(c)) ++ts->errors;
+      if (!send_req(c, o->pipeline)) ++ts->errors;
     }
     if (rate_mode) send_due(mono_ns());
   }
@@ -473,11 +489,13 @@ int main(int argc, char** argv) {
     else if (a == "--rate" || a == "-R") o.rate = atof(val().c_str());
     else if (a == "--spin-us") o.spin_us = atoi(val().c_str());
     else if (a == "--per-conn-quota") o.per_conn_quota = true;
+    else if (a == "--pipeline") o.pipeline = atoi(val().c_str());
     else {
       fprintf(stderr,
               "usage: hola_loadgen --targets h:p[,h:p..] -c CONNS -t THREADS [--cpu-list L] [--path P]\n"
               "                    (--duration S [--warmup S] [--rate R [--spin-us N]] | --control [--per-conn-quota])\n"
-              "                    [--target-offset K] [--busy-poll-us N [--busy-poll-pause P]] [--epoll-lt] [-H 'Name: v']\n");
+              "                    [--target-offset K] [--busy-poll-us N [--busy-poll-pause P]] [--epoll-lt] [-H 'Name: v']\n"
+              "                    [--pipeline P]\n");
       return 2;
     }
   }
@@ -488,6 +506,10 @@ int main(int argc, char** argv) {
   }
   if (o.threads < 1) o.threads = 1;
   if (o.connections < o.threads) o.connections = o.threads;
+  if (o.pipeline < 1 || o.pipeline > 64 || (o.pipeline > 1 && o.rate > 0)) {
+    fprintf(stderr, "loadgen: --pipeline takes 1..64 and is closed-loop only\n");
+    return 2;
+  }
   if (!o.control && o.duration_s <= 0) o.duration_s = 10;
   signal(SIGPIPE, SIG_IGN);
   g_donefd = eventfd(0, EFD_SEMAPHORE | EFD_CLOEXEC);
@@ -507,6 +529,8 @@ int main(int argc, char** argv) {
     c->req = o.method + " " + o.path + " HTTP/1.1\r\nHost: " + t.host + ":" + std::to_string(t.port) + "\r\n";
     for (auto& h : o.extra_headers) c->req += h + "\r\n";
     c->req += "\r\n";
+    const std::string one = c->req;
+    for (int k = 1; k < o.pipeline; ++k) c->req += one;
     ts[size_t(i % o.threads)]->conns.push_back(std::move(c));
   }
   std::vector<std::thread> th;
@@ -545,9 +569,11 @@ int main(int argc, char** argv) {
       int64_t q = atoll(line.c_str() + 4);
       ++gen;
       int64_t t0 = mono_ns();
-      g_budget.store(q * int64_t(o.connections));
+      // Budgets count batches: with --pipeline P, a claim is P requests.
+      const int64_t P = o.pipeline;
+      g_budget.store((q * int64_t(o.connections) + P - 1) / P);
       for (auto& t : ts) {
-        t->run_quota.store(q);
+        t->run_quota.store(std::max<int64_t>(1, (q + P - 1) / P));
         t->run_gen.store(gen);
         uint64_t one = 1;
         ssize_t w = ::write(t->wakefd, &one, sizeof one);

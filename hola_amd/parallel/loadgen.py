@@ -56,7 +56,7 @@ class ControlledLoadgen:
     def __init__(self, targets: list[tuple[str, int]], connections: int, threads: int,
                  cpu_list: str | None = None, path: str = "/api/hola", target_offset: int = 0,
                  headers: list[str] | None = None, busy_poll_us: int = 0, per_conn_quota: bool = False,
-                 busy_poll_pause: int = 0, epoll_lt: bool = False):
+                 busy_poll_pause: int = 0, epoll_lt: bool = False, pipeline: int = 1):
         cmd = [str(binary("hola_loadgen")), "--targets", ",".join(f"{h}:{p}" for h, p in targets),
                "-c", str(connections), "-t", str(threads), "--path", path, "--control",
                "--target-offset", str(target_offset)]
@@ -72,6 +72,8 @@ class ControlledLoadgen:
             cmd += ["--per-conn-quota"]
         if epoll_lt:
             cmd += ["--epoll-lt"]
+        if pipeline > 1:
+            cmd += ["--pipeline", str(pipeline)]
         self.proc = subprocess.Popen(cmd, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, bufsize=1)
         ready = self._read()
         if not ready.get("ready"):
@@ -114,11 +116,12 @@ class ControlledLoadgen:
 def run_duration(targets: list[tuple[str, int]], connections: int, threads: int, duration_s: float,
                  warmup_s: float = 1.0, cpu_list: str | None = None, path: str = "/api/hola",
                  timeout: float | None = None, rate: float = 0.0, busy_poll_us: int = 0,
-                 spin_us: int = 0) -> dict:
+                 spin_us: int = 0, pipeline: int = 1) -> dict:
     """wrk-style timed run (closed loop), or wrk2-style open loop at `rate` req/s with latency
     measured from intended send times; returns the loadgen's JSON summary. `busy_poll_us`
     spins in epoll after activity; `spin_us` (open loop) spins instead of sleeping when the
-    next scheduled send is that close."""
+    next scheduled send is that close; `pipeline` > 1 sends that many requests per write
+    (closed loop only)."""
     cmd = [str(binary("hola_loadgen")), "--targets", ",".join(f"{h}:{p}" for h, p in targets),
            "-c", str(connections), "-t", str(threads), "--path", path, "--duration", str(duration_s),
            "--warmup", str(warmup_s)]
@@ -130,6 +133,8 @@ def run_duration(targets: list[tuple[str, int]], connections: int, threads: int,
         cmd += ["--busy-poll-us", str(busy_poll_us)]
     if spin_us:
         cmd += ["--spin-us", str(spin_us)]
+    if pipeline > 1:
+        cmd += ["--pipeline", str(pipeline)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout or duration_s + warmup_s + 60)
     if r.returncode != 0:
         raise RuntimeError(f"loadgen failed: {r.stderr}")

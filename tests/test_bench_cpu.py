@@ -54,3 +54,15 @@ def test_bench_four_ranks_gloo():
     from hola_amd.utils.cpu import parse_cpu_list
     cpus = [c for r in out["config"]["cpu_map"].values() for side in r.values() for c in parse_cpu_list(side)]
     assert len(cpus) == len(set(cpus))  # disjoint core sets across ranks
+
+
+def test_bench_pipelined():
+    """--pipeline 16 (wrk's pipeline.lua): a step still completes connections x reqs-per-conn
+    requests, every response is counted and checked, and the setting is recorded."""
+    out = run([sys.executable, str(ROOT / "bench.py"), "--steps", "2", "--warmup", "1", "--reqs-per-conn", "160",
+               "--pipeline", "16"], 18860)
+    assert out["requests"] == 64 * 160 * 2 and out["errors"] == 0 and out["non2xx"] == 0
+    assert out["config"]["pipeline"] == 16 and "16 pipelined" in out["data"]
+    # 16 requests per segment each way: far fewer than 2 segments per request
+    if out["tcp_per_req"]:
+        assert out["tcp_per_req"]["OutSegs"] < 1.0

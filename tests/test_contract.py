@@ -344,3 +344,14 @@ def test_request_then_fin_is_answered_and_closed_promptly(hola, mode):
         c.close()
         assert time.monotonic() - t0 < 1.0
         assert want in data
+
+
+def test_loadgen_pipelined_batches_counted(hola):
+    """hola_loadgen --pipeline: every response of a back-to-back batch is parsed and counted
+    (the server answers a batch from one recv with one send)."""
+    from hola_amd.parallel.loadgen import run_duration
+
+    s = hola()
+    out = run_duration([("127.0.0.1", s.port)], 4, 1, 0.5, 0.2, pipeline=8)
+    lat = out["latency"]
+    assert lat["errors"] == 0 and lat["non2xx"] == 0 and lat["count"] > 8 and lat["reconnects"] == 0
