@@ -8,18 +8,19 @@ namespace {
 
 inline char lower(char c) { return (c >= 'A' && c <= 'Z') ? char(c + 32) : c; }
 
-inline bool is_tchar(unsigned char c) {
-  // RFC 9110 token characters.
-  static const bool* table = [] {
-    static bool t[256] = {false};
+// RFC 9110 token characters, as a constant table (no initialisation guard on the hot path).
+struct TcharTable {
+  bool t[256] = {};
+  constexpr TcharTable() {
     for (int c = '0'; c <= '9'; ++c) t[c] = true;
     for (int c = 'a'; c <= 'z'; ++c) t[c] = true;
     for (int c = 'A'; c <= 'Z'; ++c) t[c] = true;
     for (char c : std::string_view("!#$%&'*+-.^_`|~")) t[(unsigned char)c] = true;
-    return t;
-  }();
-  return table[c];
-}
+  }
+};
+constexpr TcharTable kTchar;
+
+inline bool is_tchar(unsigned char c) { return kTchar.t[c]; }
 
 inline std::string_view trim_ows(std::string_view s) {
   while (!s.empty() && (s.front() == ' ' || s.front() == '\t')) s.remove_prefix(1);
@@ -109,25 +110,29 @@ Parse parse_request(const char* buf, size_t len, Request* req, int* status) {
     return Parse::kError;
   }
   if (line_len && line[line_len - 1] == '\r') --line_len;
-  std::string_view rl(line, line_len);
-  size_t sp1 = rl.find(' ');
-  if (sp1 == 0 || sp1 == std::string_view::npos) {
+  // One pass over the request line: method (token chars up to the first SP), target (up to
+  // the next SP, noting control characters and the '?'), then the 8-byte version.
+  size_t i = 0;
+  while (i < line_len && is_tchar((unsigned char)line[i])) ++i;
+  if (i == 0 || i == line_len || line[i] != ' ') {
     *status = 400;
     return Parse::kError;
   }
-  req->method = rl.substr(0, sp1);
-  for (char c : req->method)
-    if (!is_tchar((unsigned char)c)) {
-      *status = 400;
-      return Parse::kError;
-    }
-  size_t sp2 = rl.find(' ', sp1 + 1);
-  if (sp2 == std::string_view::npos || sp2 == sp1 + 1) {
+  req->method = std::string_view(line, i);
+  const size_t t0 = ++i;
+  size_t q = std::string_view::npos;
+  bool bad_target = false;
+  for (; i < line_len && line[i] != ' '; ++i) {
+    const unsigned char c = (unsigned char)line[i];
+    if (c <= 0x20 || c == 0x7f) bad_target = true;
+    else if (c == '?' && q == std::string_view::npos) q = i - t0;
+  }
+  if (i == line_len || i == t0) {
     *status = 400;
     return Parse::kError;
   }
-  req->target = rl.substr(sp1 + 1, sp2 - sp1 - 1);
-  std::string_view ver = rl.substr(sp2 + 1);
+  req->target = std::string_view(line + t0, i - t0);
+  std::string_view ver(line + i + 1, line_len - i - 1);
   if (ver.size() != 8 || ver.substr(0, 5) != "HTTP/" || ver[6] != '.' || ver[5] < '0' ||
       ver[5] > '9' || ver[7] < '0' || ver[7] > '9') {
     *status = 400;
@@ -138,12 +143,10 @@ Parse parse_request(const char* buf, size_t len, Request* req, int* status) {
     return Parse::kError;
   }
   req->version_minor = ver[7] - '0';
-  for (char c : req->target)
-    if ((unsigned char)c <= 0x20 || c == 0x7f) {
-      *status = 400;
-      return Parse::kError;
-    }
-  size_t q = req->target.find('?');
+  if (bad_target) {
+    *status = 400;
+    return Parse::kError;
+  }
   req->path = req->target.substr(0, q);
   if (q != std::string_view::npos) req->query = req->target.substr(q + 1);
   // Absolute-form targets (proxies): strip scheme://authority.
@@ -180,22 +183,16 @@ Parse parse_request(const char* buf, size_t len, Request* req, int* status) {
     }
     if (hlen && hl[hlen - 1] == '\r') --hlen;
     if (hlen == 0) break;  // end of head
-    if (hl[0] == ' ' || hl[0] == '\t') {  // obs-fold: reject (RFC 9112 §5.2)
+    // Field name: token characters up to the colon. Anything else before it (obs-fold
+    // leading whitespace, spaces before the colon, a missing colon) is a 400 (RFC 9112 §5).
+    size_t colon = 0;
+    while (colon < hlen && is_tchar((unsigned char)hl[colon])) ++colon;
+    if (colon == 0 || colon == hlen || hl[colon] != ':') {
       *status = 400;
       return Parse::kError;
     }
     std::string_view h(hl, hlen);
-    size_t colon = h.find(':');
-    if (colon == 0 || colon == std::string_view::npos) {
-      *status = 400;
-      return Parse::kError;
-    }
     std::string_view name = h.substr(0, colon);
-    for (char c : name)
-      if (!is_tchar((unsigned char)c)) {  // includes whitespace before the colon
-        *status = 400;
-        return Parse::kError;
-      }
     std::string_view value = trim_ows(h.substr(colon + 1));
     switch (name.size()) {
       case 2:
