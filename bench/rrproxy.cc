@@ -4,10 +4,16 @@
 // Each accepted client connection is bound to the next *healthy* backend (round-robin).
 // Health = GET /api/health answered 200 (the readiness probe of pom.xml:90-94), checked
 // every --health-ms by a background thread; unhealthy replicas are skipped until they pass
-// again. Bytes are relayed with recv/send through a small per-direction buffer.
+// again, and a backend that refuses a connect is marked down at once and the next one tried.
+//
+// Data path: one pinned EventLoop (src/core/loop.h, the server's own loop) per proxy thread.
+// Both sockets of a session live on one loop, registered once, edge-triggered, for
+// IN|OUT|RDHUP: no epoll_ctl per message. A read that comes back short has drained the
+// socket (no extra EAGAIN read); a send that would block parks the bytes until the OUT edge
+// and stops reading the other side until they are gone (backpressure). Accepted sockets are
+// handed to a loop in the client's L3 domain (SO_INCOMING_CPU), as the server does.
 #include <errno.h>
 #include <signal.h>
-#include <sys/epoll.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -23,6 +29,7 @@
 
 #include "client/url.h"
 #include "core/affinity.h"
+#include "core/loop.h"
 #include "core/net.h"
 
 using namespace hola;
@@ -43,7 +50,7 @@ std::atomic<uint64_t> g_rr{0};
 std::atomic<bool> g_stop{false};
 
 Backend* pick() {
-  size_t n = g_backends.size();
+  const size_t n = g_backends.size();
   for (size_t k = 0; k < n; ++k) {
     Backend* b = g_backends[g_rr.fetch_add(1, std::memory_order_relaxed) % n].get();
     if (b->healthy.load(std::memory_order_relaxed)) return b;
@@ -51,155 +58,271 @@ Backend* pick() {
   return nullptr;
 }
 
-// One direction of a session: bytes read from `from` waiting to be written to `to`.
-struct Dir {
+void mark_down(Backend* b, int err) {
+  if (b->healthy.exchange(false))
+    fprintf(stderr, "rrproxy: backend %s:%d is DOWN (%s)\n", b->host.c_str(), b->port, strerror(err));
+}
+
+// Starts a non-blocking connect to a healthy backend, failing over (and marking refusers
+// down) while connect() fails at once. The handshake may still be in progress: bytes sent
+// before it completes wait for the socket's OUT edge, and a refusal reported then fails over
+// from Session::on_event.
+int connect_backend(Backend** chosen, bool* in_progress) {
+  for (size_t tries = 0; tries < g_backends.size(); ++tries) {
+    Backend* b = pick();
+    if (!b) return -1;
+    int fd = connect_nonblocking(b->addr, b->len, in_progress);
+    if (fd >= 0) {
+      b->picked.fetch_add(1, std::memory_order_relaxed);
+      *chosen = b;
+      return fd;
+    }
+    mark_down(b, errno);
+  }
+  return -1;
+}
+
+class ProxyLoop;
+
+// One direction of a session: bytes read from one socket that the other has not taken yet.
+struct Pipe {
   char buf[16384];
   size_t len = 0, off = 0;
+  bool eof = false;   // the source sent its FIN
+  bool shut = false;  // ... and it was passed on (shutdown(SHUT_WR) of the destination)
+  bool hup = false;   // an edge carried RDHUP/HUP: read the source on to its EOF
+  bool pending() const { return off < len; }
 };
 
-struct Session;
-struct Ev {
-  Session* s;
-  bool client;  // event on the client socket
+struct Session : EventLoop::Handler {
+  struct Side : EventLoop::Handler {
+    Session* s = nullptr;
+    bool client = false;
+    void on_event(uint32_t ev) override { s->on_event(client, ev); }
+  };
+  ProxyLoop* owner;
+  int cfd, bfd;
+  Side cside, bside;
+  Pipe c2b, b2c;
+  Backend* backend = nullptr;
+  bool connecting = false;  // backend handshake not confirmed yet
+  int failovers = 0;
+  bool closed = false;
+
+  Session(ProxyLoop* o, int c, int b) : owner(o), cfd(c), bfd(b) {
+    cside.s = bside.s = this;
+    cside.client = true;
+  }
+  void on_event(uint32_t) override {}  // lifetime anchor for EventLoop::retire
+  void on_event(bool client_side, uint32_t ev);
+  bool flush(Pipe& p, int to);
+  bool pump(bool from_client);
+  void close();
+  bool backend_connected(uint32_t ev);
 };
 
-struct Session {
-  int cfd = -1, bfd = -1;
-  Dir c2b, b2c;
-  bool closing = false;
-  Ev ec{this, true}, eb{this, false};
-  uint32_t cint = EPOLLIN | EPOLLRDHUP, bint = EPOLLIN | EPOLLRDHUP;
+class ProxyLoop {
+ public:
+  ProxyLoop(int index, int cpu, int busy_poll_us, int busy_poll_pause) : index_(index), cpu_(cpu) {
+    loop_.set_busy_poll_us(busy_poll_us);
+    loop_.set_busy_poll_pause(busy_poll_pause);
+  }
+  EventLoop& loop() { return loop_; }
+  int cpu() const { return cpu_; }
+  int index() const { return index_; }
+  std::atomic<int64_t>& sessions() { return sessions_; }
+
+  void adopt(int cfd) {
+    loop_.post([this, cfd] { adopt_here(cfd); });
+  }
+  static constexpr uint32_t kEvents = EPOLLIN | EPOLLOUT | EPOLLRDHUP | EPOLLET;
+  void adopt_here(int cfd) {
+    Backend* b = nullptr;
+    bool inprog = false;
+    int bfd = connect_backend(&b, &inprog);
+    if (bfd < 0) {
+      ::close(cfd);
+      sessions_.fetch_sub(1, std::memory_order_relaxed);
+      return;
+    }
+    auto* s = new Session(this, cfd, bfd);
+    s->backend = b;
+    s->connecting = inprog;
+    loop_.add(bfd, kEvents, &s->bside);
+    loop_.add(cfd, kEvents, &s->cside);
+  }
+  void run() {
+    if (cpu_ >= 0) pin_current_thread(cpu_);
+    loop_.run();
+  }
+
+ private:
+  EventLoop loop_;
+  int index_, cpu_;
+  std::atomic<int64_t> sessions_{0};
 };
 
-// Plain recv/send relay: for the small request/response messages of this service it costs
-// two syscalls per hop, less than splice(2) through a pipe (four).
-// Returns false when the session must close.
-bool pump(int epfd, Session* s, bool from_client) {
-  int from = from_client ? s->cfd : s->bfd, to = from_client ? s->bfd : s->cfd;
-  Dir& d = from_client ? s->c2b : s->b2c;
+// Writes what `p` holds to `to`. False on a hard error; true otherwise (p may stay pending
+// when `to` is full: the OUT edge resumes it).
+bool Session::flush(Pipe& p, int to) {
+  while (p.pending()) {
+    ssize_t m = ::send(to, p.buf + p.off, p.len - p.off, MSG_NOSIGNAL);
+    if (m < 0) {
+      if (errno == EINTR) continue;
+      return errno == EAGAIN;
+    }
+    p.off += size_t(m);
+  }
+  p.off = p.len = 0;
+  return true;
+}
+
+// Moves bytes from one side to the other until the source is drained or the destination full.
+// A FIN is passed on as a half-close once the bytes before it are delivered (a client may
+// send its request and shut down its side, then read the response); the session ends when
+// both directions are shut. Returns false when the session must close.
+bool Session::pump(bool from_client) {
+  Pipe& p = from_client ? c2b : b2c;
+  const int from = from_client ? cfd : bfd, to = from_client ? bfd : cfd;
   for (;;) {
-    if (d.off < d.len) {
-      ssize_t m = ::send(to, d.buf + d.off, d.len - d.off, MSG_NOSIGNAL);
-      if (m < 0) {
-        if (errno == EAGAIN) {
-          // destination full: stop reading `from`, wait for `to` to drain
-          uint32_t& fi = from_client ? s->cint : s->bint;
-          uint32_t& ti = from_client ? s->bint : s->cint;
-          epoll_event ev{};
-          fi = EPOLLRDHUP;
-          ev.events = fi;
-          ev.data.ptr = from_client ? &s->ec : &s->eb;
-          epoll_ctl(epfd, EPOLL_CTL_MOD, from, &ev);
-          ti |= EPOLLOUT;
-          ev.events = ti;
-          ev.data.ptr = from_client ? &s->eb : &s->ec;
-          epoll_ctl(epfd, EPOLL_CTL_MOD, to, &ev);
-          return true;
-        }
-        return false;
+    if (!flush(p, to)) return false;
+    if (p.pending()) return true;  // destination full: wait for its OUT edge
+    if (p.eof) {
+      if (!p.shut) {
+        ::shutdown(to, SHUT_WR);
+        p.shut = true;
       }
-      d.off += size_t(m);
+      return !(c2b.shut && b2c.shut);
+    }
+    ssize_t n = ::recv(from, p.buf, sizeof p.buf, 0);
+    if (n == 0) {
+      p.eof = true;
       continue;
     }
-    d.off = d.len = 0;
-    ssize_t n = ::recv(from, d.buf, sizeof d.buf, 0);
-    if (n == 0) return false;
-    if (n < 0) return errno == EAGAIN || errno == EINTR;
-    d.len = size_t(n);
+    if (n < 0) {
+      if (errno == EINTR) continue;
+      return errno == EAGAIN;
+    }
+    p.len = size_t(n);
+    // A short read drained the source, unless this edge also carried its FIN: then read on
+    // to the EOF (the edge will not come again).
+    if (size_t(n) < sizeof p.buf && !p.hup) return flush(p, to);
   }
 }
 
-// `fd` became writable: flush what was waiting for it and resume reading the other side.
-bool drained(int epfd, Session* s, bool client_writable) {
-  bool from_client = !client_writable;  // data flowing *to* the writable socket
-  Dir& d = from_client ? s->c2b : s->b2c;
-  int to = client_writable ? s->cfd : s->bfd, from = client_writable ? s->bfd : s->cfd;
-  while (d.off < d.len) {
-    ssize_t m = ::send(to, d.buf + d.off, d.len - d.off, MSG_NOSIGNAL);
-    if (m < 0) return errno == EAGAIN;
-    d.off += size_t(m);
+// First event on a backend socket whose connect was in progress: true once the handshake
+// succeeded; on a refusal, marks the backend down and moves the session to the next one.
+bool Session::backend_connected(uint32_t ev) {
+  int soerr = 0;
+  socklen_t sl = sizeof soerr;
+  if (getsockopt(bfd, SOL_SOCKET, SO_ERROR, &soerr, &sl) != 0) soerr = errno;
+  if (soerr == 0 && !(ev & (EPOLLERR | EPOLLHUP))) {
+    connecting = false;
+    return true;
   }
-  d.off = d.len = 0;
-  uint32_t& ti = client_writable ? s->cint : s->bint;
-  uint32_t& fi = client_writable ? s->bint : s->cint;
-  epoll_event ev{};
-  ti &= ~uint32_t(EPOLLOUT);
-  ev.events = ti;
-  ev.data.ptr = client_writable ? &s->ec : &s->eb;
-  epoll_ctl(epfd, EPOLL_CTL_MOD, to, &ev);
-  fi = EPOLLIN | EPOLLRDHUP | (fi & EPOLLOUT);
-  ev.events = fi;
-  ev.data.ptr = client_writable ? &s->eb : &s->ec;
-  epoll_ctl(epfd, EPOLL_CTL_MOD, from, &ev);
-  return pump(epfd, s, from_client);
+  mark_down(backend, soerr ? soerr : ECONNRESET);
+  EventLoop& l = owner->loop();
+  l.del(bfd);
+  ::close(bfd);
+  bfd = -1;
+  if (++failovers > int(g_backends.size())) return false;
+  bool inprog = false;
+  bfd = connect_backend(&backend, &inprog);
+  if (bfd < 0) return false;
+  connecting = inprog;
+  l.add(bfd, ProxyLoop::kEvents, &bside);
+  return !connecting;  // connected at once: carry on; else wait for the new socket's edge
 }
 
-void close_session(int epfd, Session* s) {
-  epoll_ctl(epfd, EPOLL_CTL_DEL, s->cfd, nullptr);
-  epoll_ctl(epfd, EPOLL_CTL_DEL, s->bfd, nullptr);
-  ::close(s->cfd);
-  ::close(s->bfd);
+void Session::on_event(bool client_side, uint32_t ev) {
+  if (closed) return;
+  if (connecting) {
+    // The client is not read until the backend accepted, so a refusal can still fail over.
+    if (client_side) {
+      if (ev & (EPOLLRDHUP | EPOLLHUP)) c2b.hup = true;
+      if (ev & EPOLLERR) close();
+      return;
+    }
+    if (!(ev & (EPOLLOUT | EPOLLERR | EPOLLHUP))) return;
+    if (!backend_connected(ev)) {
+      if (bfd < 0) close();
+      return;  // closed, or waiting for the next backend's handshake
+    }
+    // What the client sent meanwhile, then anything the backend already sent.
+    if (!pump(true) || ((ev & (EPOLLIN | EPOLLRDHUP)) && !pump(false))) close();
+    return;
+  }
+  bool ok = !(ev & EPOLLERR);
+  // Writable: deliver what was parked for this side, then read the other side again (it
+  // was not read while the bytes waited).
+  if (ok && (ev & EPOLLOUT)) {
+    Pipe& into = client_side ? b2c : c2b;
+    if (into.pending()) {
+      ok = flush(into, client_side ? cfd : bfd);
+      if (ok && !into.pending()) ok = pump(!client_side);
+    }
+  }
+  if (ev & (EPOLLRDHUP | EPOLLHUP)) (client_side ? c2b : b2c).hup = true;
+  if (ok && (ev & (EPOLLIN | EPOLLRDHUP | EPOLLHUP))) ok = pump(client_side);
+  if (!ok) close();
 }
 
-void worker(int lfd, int cpu) {
-  if (cpu >= 0) pin_current_thread(cpu);
-  int epfd = epoll_create1(EPOLL_CLOEXEC);
-  epoll_event ev{};
-  ev.events = EPOLLIN;
-  ev.data.ptr = nullptr;
-  epoll_ctl(epfd, EPOLL_CTL_ADD, lfd, &ev);
-  epoll_event evs[256];
-  std::vector<Session*> dead;
-  while (!g_stop.load()) {
-    int n = epoll_wait(epfd, evs, 256, 200);
-    for (int i = 0; i < n; ++i) {
-      if (!evs[i].data.ptr) {
-        for (;;) {
-          int c = accept4(lfd, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
-          if (c < 0) break;
-          set_nodelay(c);
-          Backend* b = pick();
-          if (!b) {
-            ::close(c);
-            continue;
-          }
-          b->picked.fetch_add(1, std::memory_order_relaxed);
-          int bfd = connect_blocking(b->addr, b->len, 1000);
-          if (bfd < 0) {
-            b->healthy.store(false);
-            ::close(c);
-            continue;
-          }
-          set_nonblocking(bfd, true);
-          auto* s = new Session();
-          s->cfd = c;
-          s->bfd = bfd;
-          ev.events = s->cint;
-          ev.data.ptr = &s->ec;
-          epoll_ctl(epfd, EPOLL_CTL_ADD, c, &ev);
-          ev.events = s->bint;
-          ev.data.ptr = &s->eb;
-          epoll_ctl(epfd, EPOLL_CTL_ADD, bfd, &ev);
+void Session::close() {
+  if (closed) return;
+  closed = true;
+  EventLoop& l = owner->loop();
+  l.del(cfd);
+  ::close(cfd);
+  if (bfd >= 0) {
+    l.del(bfd);
+    ::close(bfd);
+  }
+  owner->sessions().fetch_sub(1, std::memory_order_relaxed);
+  l.retire(this);  // the other side's event may still be in this batch
+}
+
+// Accepts on one listener (on loop 0) and deals each connection to a loop in the client's L3
+// domain, least-loaded first, falling back to plain round-robin.
+struct Acceptor : EventLoop::Handler {
+  int fd = -1;
+  std::vector<std::unique_ptr<ProxyLoop>>* loops = nullptr;
+  bool steer = true;
+  uint64_t rr = 0;
+
+  ProxyLoop* choose(int cfd) {
+    auto& ls = *loops;
+    ProxyLoop* best = nullptr;
+    if (steer) {
+      int cpu = -1;
+      socklen_t len = sizeof cpu;
+      if (getsockopt(cfd, SOL_SOCKET, SO_INCOMING_CPU, &cpu, &len) == 0 && cpu >= 0) {
+        const int dom = l3_domain_of(cpu);
+        for (auto& l : ls) {
+          if (l->cpu() < 0 || l3_domain_of(l->cpu()) != dom) continue;
+          if (!best || l->sessions().load(std::memory_order_relaxed) < best->sessions().load(std::memory_order_relaxed))
+            best = l.get();
         }
-        continue;
-      }
-      Ev* e = static_cast<Ev*>(evs[i].data.ptr);
-      Session* s = e->s;
-      if (s->closing) continue;
-      bool ok = true;
-      uint32_t evm = evs[i].events;
-      if (evm & EPOLLOUT) ok = drained(epfd, s, e->client);
-      if (ok && (evm & (EPOLLIN | EPOLLRDHUP | EPOLLHUP))) ok = pump(epfd, s, e->client);
-      if (!ok || (evm & EPOLLERR)) {
-        s->closing = true;
-        close_session(epfd, s);
-        dead.push_back(s);  // the peer's event may still be in this batch: free afterwards
       }
     }
-    for (Session* s : dead) delete s;
-    dead.clear();
+    if (!best) best = ls[rr++ % ls.size()].get();
+    return best;
   }
-}
+
+  void on_event(uint32_t) override {
+    for (int i = 0; i < 256; ++i) {
+      int c = ::accept4(fd, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
+      if (c < 0) {
+        if (errno == EINTR || errno == ECONNABORTED) continue;
+        return;
+      }
+      set_nodelay(c);
+      ProxyLoop* l = choose(c);
+      l->sessions().fetch_add(1, std::memory_order_relaxed);
+      if (l == (*loops)[0].get()) l->adopt_here(c);
+      else l->adopt(c);
+    }
+  }
+};
 
 void health_loop(int interval_ms) {
   while (!g_stop.load()) {
@@ -221,7 +344,8 @@ void health_loop(int interval_ms) {
 }  // namespace
 
 int main(int argc, char** argv) {
-  int port = 8080, threads = 1, health_ms = 500;
+  int port = 8080, threads = 1, health_ms = 500, busy_poll_us = 0, busy_poll_pause = 0;
+  bool steer = true;
   std::string backends, cpu_list, host = "0.0.0.0", port_file;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
@@ -236,8 +360,13 @@ int main(int argc, char** argv) {
     else if (a == "--cpu-list") cpu_list = val();
     else if (a == "--health-ms") health_ms = atoi(val().c_str());
     else if (a == "--port-file") port_file = val();
+    else if (a == "--busy-poll-us") busy_poll_us = atoi(val().c_str());
+    else if (a == "--busy-poll-pause") busy_poll_pause = atoi(val().c_str());
+    else if (a == "--no-steer") steer = false;
     else {
-      fprintf(stderr, "usage: hola_rrproxy --backends h:p,h:p.. [--port N] [--threads N] [--cpu-list L] [--health-ms N]\n");
+      fprintf(stderr,
+              "usage: hola_rrproxy --backends h:p,h:p.. [--port N] [--host H] [--threads N] [--cpu-list L]\n"
+              "                    [--health-ms N] [--busy-poll-us N [--busy-poll-pause P]] [--no-steer] [--port-file F]\n");
       return 2;
     }
   }
@@ -264,30 +393,41 @@ int main(int argc, char** argv) {
     fprintf(stderr, "rrproxy: --backends required\n");
     return 2;
   }
+  if (threads < 1) threads = 1;
   std::vector<int> cpus;
-  if (!cpu_list.empty()) parse_cpu_list(cpu_list, &cpus);
+  if (!cpu_list.empty() && !parse_cpu_list(cpu_list, &cpus)) {
+    fprintf(stderr, "rrproxy: bad --cpu-list\n");
+    return 2;
+  }
   ListenOptions lo;
   lo.host = host;
   lo.port = port;
-  lo.reuseport = true;
-  std::vector<int> lfds;
   std::string err;
-  for (int t = 0; t < threads; ++t) {
-    int fd = listen_tcp(lo, &err);
-    if (fd < 0) {
-      fprintf(stderr, "rrproxy: %s\n", err.c_str());
-      return 1;
-    }
-    if (t == 0) lo.port = bound_port(fd);
-    lfds.push_back(fd);
+  Acceptor acc;
+  acc.fd = listen_tcp(lo, &err);
+  if (acc.fd < 0) {
+    fprintf(stderr, "rrproxy: %s\n", err.c_str());
+    return 1;
   }
+  lo.port = bound_port(acc.fd);
   if (!port_file.empty()) {
     FILE* f = fopen((port_file + ".tmp").c_str(), "w");
+    if (!f) return 1;
     fprintf(f, "%d\n", lo.port);
     fclose(f);
     rename((port_file + ".tmp").c_str(), port_file.c_str());
   }
-  fprintf(stderr, "rrproxy: listening on %s:%d -> %zu backends\n", host.c_str(), lo.port, g_backends.size());
+  fprintf(stderr, "rrproxy: listening on %s:%d -> %zu backends, %d threads\n", host.c_str(), lo.port,
+          g_backends.size(), threads);
+
+  std::vector<std::unique_ptr<ProxyLoop>> loops;
+  for (int t = 0; t < threads; ++t)
+    loops.push_back(std::make_unique<ProxyLoop>(t, cpus.empty() ? -1 : cpus[size_t(t) % cpus.size()], busy_poll_us,
+                                                busy_poll_pause));
+  acc.loops = &loops;
+  acc.steer = steer && !cpus.empty();
+  loops[0]->loop().add(acc.fd, EPOLLIN, &acc);
+
   sigset_t sigs;
   sigemptyset(&sigs);
   sigaddset(&sigs, SIGTERM);
@@ -295,12 +435,14 @@ int main(int argc, char** argv) {
   pthread_sigmask(SIG_BLOCK, &sigs, nullptr);
   std::thread hc(health_loop, health_ms);
   std::vector<std::thread> ws;
-  for (int t = 0; t < threads; ++t) ws.emplace_back(worker, lfds[size_t(t)], cpus.empty() ? -1 : cpus[size_t(t) % cpus.size()]);
+  for (auto& l : loops) ws.emplace_back([p = l.get()] { p->run(); });
   int sig;
   sigwait(&sigs, &sig);
   g_stop.store(true);
+  for (auto& l : loops) l->loop().stop();
   for (auto& w : ws) w.join();
   hc.join();
-  for (auto& b : g_backends) fprintf(stderr, "rrproxy: %s:%d picked %llu\n", b->host.c_str(), b->port, (unsigned long long)b->picked.load());
+  for (auto& b : g_backends)
+    fprintf(stderr, "rrproxy: %s:%d picked %llu\n", b->host.c_str(), b->port, (unsigned long long)b->picked.load());
   return 0;
 }

@@ -120,14 +120,17 @@ class RRProxy:
     """`hola_rrproxy`: L4 round-robin over healthy backends (health = GET /api/health)."""
 
     def __init__(self, backends: list[tuple[str, int]], port: int = 0, threads: int = 1,
-                 cpu_list: str | None = None, health_ms: int = 200):
+                 cpu_list: str | None = None, health_ms: int = 200, busy_poll_us: int = 0,
+                 exe: str | None = None):
         self._tmp = tempfile.TemporaryDirectory(prefix="rrproxy-")
         self.port_file = os.path.join(self._tmp.name, "port")
-        cmd = [str(binary("hola_rrproxy")), "--host", "127.0.0.1", "--port", str(port), "--threads", str(threads),
-               "--backends", ",".join(f"{h}:{p}" for h, p in backends), "--health-ms", str(health_ms),
-               "--port-file", self.port_file]
+        cmd = [exe or str(binary("hola_rrproxy")), "--host", "127.0.0.1", "--port", str(port),
+               "--threads", str(threads), "--backends", ",".join(f"{h}:{p}" for h, p in backends),
+               "--health-ms", str(health_ms), "--port-file", self.port_file]
         if cpu_list:
             cmd += ["--cpu-list", cpu_list]
+        if busy_poll_us:
+            cmd += ["--busy-poll-us", str(busy_poll_us)]
         self.cmd = cmd
         self.proc: subprocess.Popen | None = None
         self.port = port

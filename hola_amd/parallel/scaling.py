@@ -17,7 +17,8 @@ import time
 
 from hola_amd.parallel.loadgen import run_duration
 from hola_amd.parallel.replicas import ReplicaSet, RRProxy
-from hola_amd.utils.cpu import cgroup_cpu_quota, cpu_budget, format_cpu_list, plan_node, split_server_loadgen
+from hola_amd.utils.cpu import (cgroup_cpu_quota, cpu_budget, format_cpu_list, plan_mirrored, plan_node,
+                                split_server_loadgen)
 
 
 def plan(n_replicas: int, budget: int, server_share: float, proxy_threads: int) -> dict:
@@ -52,22 +53,43 @@ def plan(n_replicas: int, budget: int, server_share: float, proxy_threads: int) 
     return {"replicas": replica_cpus, "proxy": proxy_cpus, "loadgen": load}
 
 
+def plan_proxied(n_replicas: int, budget: int) -> dict:
+    """Cores for load generator -> proxy -> N replicas: every L3 domain holds servers, proxy
+    threads and load-generator threads in 1:2:1 (a proxied request costs the proxy two socket
+    hops, about twice the server's work). The proxy hands each client connection to a thread in
+    the client's L3, and that thread's backend connection lands on a server worker in its own
+    L3 (accept steering), so no hop crosses an L3 domain. Server cores are dealt to replicas
+    round-robin."""
+    m = plan_mirrored({"server": 1, "proxy": 2, "loadgen": 1}, total=budget)
+    srv = m["server"]
+    replicas = [srv[k::n_replicas] or [srv[k % len(srv)]] for k in range(n_replicas)]
+    return {"replicas": replicas, "proxy": m["proxy"], "loadgen": m["loadgen"]}
+
+
 def run_point(n: int, args) -> dict:
     budget = args.budget or cpu_budget()
-    proxy_threads = args.proxy_threads if args.lb == "proxy" else 0
-    p = plan(n, budget, args.server_share, proxy_threads)
+    if args.lb == "proxy" and not args.proxy_threads:
+        p = plan_proxied(n, budget)
+        proxy_threads = len(p["proxy"])
+    else:
+        proxy_threads = args.proxy_threads if args.lb == "proxy" else 0
+        p = plan(n, budget, args.server_share, proxy_threads)
     conns = args.connections_per_replica * n if args.mode == "weak" else args.connections
     extra = ["--no-tracing"] if args.no_tracing else []
+    if args.busy_poll_us:
+        extra += ["--busy-poll-us", str(args.busy_poll_us)]
     shared = 0 if args.lb == "reuseport" else None
     with ReplicaSet(n, cpu_plan=p["replicas"], args=extra, supervise=False, shared_port=shared) as rs:
         if args.lb == "proxy":
-            with RRProxy(rs.targets, threads=proxy_threads, cpu_list=format_cpu_list(p["proxy"])) as px:
+            with RRProxy(rs.targets, threads=proxy_threads, cpu_list=format_cpu_list(p["proxy"]),
+                         busy_poll_us=args.busy_poll_us if args.proxy_busy_poll_us < 0 else args.proxy_busy_poll_us,
+                         exe=args.proxy_exe or None) as px:
                 targets = [("127.0.0.1", px.port)]
                 res = run_duration(targets, conns, len(p["loadgen"]), args.duration, args.warmup,
-                                   cpu_list=",".join(map(str, p["loadgen"])))
+                                   cpu_list=",".join(map(str, p["loadgen"])), busy_poll_us=args.busy_poll_us)
         else:
             res = run_duration(rs.targets, conns, len(p["loadgen"]), args.duration, args.warmup,
-                               cpu_list=",".join(map(str, p["loadgen"])))
+                               cpu_list=",".join(map(str, p["loadgen"])), busy_poll_us=args.busy_poll_us)
     lat = res["latency"]
     return {
         "replicas": n, "connections": conns, "lb": args.lb, "rps": res["rps"],
@@ -90,7 +112,13 @@ def main(argv=None) -> int:
     ap.add_argument("--lb", choices=["client", "proxy", "reuseport"], default="client",
                     help="client: load generator round-robins over replica ports; proxy: hola_rrproxy; "
                          "reuseport: one shared port, the kernel spreads connections")
-    ap.add_argument("--proxy-threads", type=int, default=2)
+    ap.add_argument("--proxy-threads", type=int, default=0,
+                    help="0 = half the CPU budget, mirrored with the servers and the load generator "
+                         "in every L3 domain")
+    ap.add_argument("--proxy-exe", default="", help="alternative hola_rrproxy binary (A/B runs)")
+    ap.add_argument("--busy-poll-us", type=int, default=0,
+                    help="busy-poll window of the replicas, the load generator and the proxy")
+    ap.add_argument("--proxy-busy-poll-us", type=int, default=-1, help="-1 = --busy-poll-us")
     ap.add_argument("--budget", type=int, default=0, help="CPUs to use (default: cgroup quota / affinity)")
     ap.add_argument("--server-share", type=float, default=0.5)
     ap.add_argument("--no-tracing", action="store_true")

@@ -43,6 +43,47 @@ def test_proxy_skips_dead_replica_and_recovers():
         rs.stop()
 
 
+def test_proxy_half_close_and_backpressure():
+    """The proxy passes a client's FIN on after its request (the response still arrives), and
+    relays a pipelined burst far larger than its 16 KiB buffers in order."""
+    import socket
+
+    with ReplicaSet(1, threads_per_replica=1, supervise=False) as rs, RRProxy(rs.targets) as px:
+        with socket.create_connection(("127.0.0.1", px.port), timeout=5) as sk:
+            sk.sendall(b"GET /api/health HTTP/1.1\r\nHost: x\r\n\r\n")
+            sk.shutdown(socket.SHUT_WR)
+            data = b""
+            while chunk := sk.recv(65536):
+                data += chunk
+        assert data.startswith(b"HTTP/1.1 200") and data.endswith(b"I'm ok")
+        n = 300  # ~300 x the swagger document through one session
+        req = b"GET /api/swagger.json HTTP/1.1\r\nHost: x\r\n\r\n"
+        with socket.create_connection(("127.0.0.1", px.port), timeout=10) as sk:
+            sk.sendall(req * n + b"GET /api/hola HTTP/1.1\r\nHost: x\r\nConnection: close\r\n\r\n")
+            data = b""
+            while chunk := sk.recv(1 << 20):
+                data += chunk
+        assert data.count(b"HTTP/1.1 200 OK") == n + 1
+        assert data.endswith(b"Hola de replica-0")
+
+
+def test_proxy_fails_over_on_refused_connect():
+    """A backend that refuses is marked DOWN at once and the connection goes to the next one,
+    before any health check has run."""
+    rs = ReplicaSet(2, threads_per_replica=1, supervise=False).start()
+    try:
+        with RRProxy(rs.targets, health_ms=60000) as px:
+            time.sleep(0.3)  # the one health round (at start) saw both UP
+            assert "is DOWN" not in px.log()
+            rs.kill(0)
+            time.sleep(0.1)
+            seen = {greeting_via(px.port) for _ in range(6)}
+            assert seen == {"Hola de replica-1"}
+            assert "is DOWN" in px.log()
+    finally:
+        rs.stop()
+
+
 def test_supervisor_restarts_crashed_replica():
     with ReplicaSet(2, threads_per_replica=1, supervise=True) as rs:
         old = rs.procs[0].proc.pid
@@ -119,6 +160,22 @@ def test_scaling_harness_smoke():
     assert [r["replicas"] for r in lines] == [1, 2]
     assert all(r["rps"] > 0 and r["errors"] == 0 for r in lines)
     assert lines[1]["connections"] == 16
+
+
+def test_scaling_harness_proxy_mode():
+    """--lb proxy: load generator -> hola_rrproxy -> replicas, with the mirrored core plan."""
+    from hola_amd.parallel import scaling
+    import io
+    import contextlib
+
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        scaling.main(["--replicas", "1,2", "--duration", "0.5", "--warmup", "0.2", "--budget", "8",
+                      "--connections-per-replica", "8", "--lb", "proxy"])
+    lines = [json.loads(l) for l in buf.getvalue().splitlines() if l.startswith("{")]
+    assert [r["replicas"] for r in lines] == [1, 2]
+    assert all(r["rps"] > 0 and r["errors"] == 0 and r["lb"] == "proxy" for r in lines)
+    assert all(r["cpu_map"]["proxy"] for r in lines)
 
 
 def test_open_loop_rate_mode(hola):
