@@ -162,12 +162,13 @@ bool send_req(Conn* c, int depth) {
   return true;
 }
 
-// Returns 1 when a full response is at the start of buf (its size in *used), 0 if more is
+// Returns 1 when a full response starts at buf[from] (its size in *used), 0 if more is
 // needed, -1 on malformed input.
-int response_complete(Conn* c, int* status, bool* close, size_t* used) {
-  std::string_view s(c->buf, c->have);
-  size_t he = s.find("\r\n\r\n");
-  if (he == std::string_view::npos) return c->have >= sizeof c->buf ? -1 : 0;
+int response_complete(Conn* c, size_t from, int* status, bool* close, size_t* used) {
+  std::string_view s(c->buf + from, c->have - from);
+  const void* end = memmem(s.data(), s.size(), "\r\n\r\n", 4);
+  if (!end) return (from == 0 && c->have >= sizeof c->buf) ? -1 : 0;  // a head larger than buf
+  const size_t he = size_t(static_cast<const char*>(end) - s.data());
   if (s.size() < 12 || s.substr(0, 5) != "HTTP/") return -1;
   *status = (s[9] - '0') * 100 + (s[10] - '0') * 10 + (s[11] - '0');
   std::string_view head = s.substr(0, he);
@@ -179,7 +180,7 @@ int response_complete(Conn* c, int* status, bool* close, size_t* used) {
   *close = head.find("Connection: close") != std::string_view::npos;
   if (he + 4 + cl > sizeof c->buf) return -1;
   *used = he + 4 + cl;
-  return c->have >= *used ? 1 : 0;
+  return s.size() >= *used ? 1 : 0;
 }
 
 void thread_main(ThreadState* ts, const Options* o) {
@@ -354,10 +355,11 @@ void thread_main(ThreadState* ts, const Options* o) {
       c->have += size_t(r);
       bool close = false;
       const int64_t now_rx = mono_ns();
+      size_t at = 0;  // responses are consumed in place; what is left moves down once
       for (;;) {  // every complete response in the buffer (several when pipelining)
         int status = 0;
         size_t used = 0;
-        int rc = response_complete(c, &status, &close, &used);
+        int rc = response_complete(c, at, &status, &close, &used);
         if (rc == 0) break;
         if (rc < 0) {
           ++ts->errors;
@@ -374,9 +376,12 @@ void thread_main(ThreadState* ts, const Options* o) {
         if (status < 200 || status > 299) ++ts->non2xx;
         ++run_requests;
         --c->inflight;
-        c->have -= used;
-        if (c->have) memmove(c->buf, c->buf + used, c->have);
+        at += used;
         if (close || c->inflight <= 0) break;
+      }
+      if (at) {
+        c->have -= at;
+        if (c->have) memmove(c->buf, c->buf + at, c->have);
       }
       if (!close && c->inflight > 0) continue;  // the rest of the batch is still due
       c->busy = false;
