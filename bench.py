@@ -167,6 +167,7 @@ def main() -> int:
         cuda()
         cpu0 = (_proc_cpu_s(server.proc.pid), _proc_cpu_s(loadgen.proc.pid))
         tcp0 = _tcp_counters()
+        thr0 = _cgroup_cpu_stat()
         t0 = time.perf_counter()
         reqs = errs = 0
         for _ in range(a.steps):
@@ -179,6 +180,7 @@ def main() -> int:
         elapsed = time.perf_counter() - t0
         cpu1 = (_proc_cpu_s(server.proc.pid), _proc_cpu_s(loadgen.proc.pid))
         tcp1 = _tcp_counters()
+        thr1 = _cgroup_cpu_stat()
         st = loadgen.stats()
         mem = server.memory_kb()
 
@@ -187,7 +189,8 @@ def main() -> int:
                  "load_cpus": format_cpu_list(load_cpus),
                  "server_cpu_s": cpu1[0] - cpu0[0], "loadgen_cpu_s": cpu1[1] - cpu0[1],
                  "startup_ms": server.startup_ms, "rss_peak_kb": mem.get("VmHWM", 0),
-                 "tcp": {k: tcp1[k] - tcp0[k] for k in tcp1 if k in tcp0}}
+                 "tcp": {k: tcp1[k] - tcp0[k] for k in tcp1 if k in tcp0},
+                 "cgroup": {k: thr1[k] - thr0[k] for k in thr1 if k in thr0}}
         if dist:
             gathered = [None] * world
             dist.all_gather_object(gathered, local)
@@ -232,6 +235,12 @@ def main() -> int:
             # is shared by all ranks, so rank 0's delta covers the node): ~2 = one request and
             # one response segment with the ACKs piggybacked
             "tcp_per_req": {k: round(v / max(1, total), 3) for k, v in gathered[0]["tcp"].items()},
+            # CFS bandwidth throttling of this cgroup over the timed region (cgroup v2
+            # cpu.stat; shared by all ranks of one container): with a CPU quota, threads that
+            # exceed it in a 100 ms period all stop until the next one
+            "cgroup_throttle": {"periods": gathered[0]["cgroup"].get("nr_periods", 0),
+                                "throttled_periods": gathered[0]["cgroup"].get("nr_throttled", 0),
+                                "throttled_ms": round(gathered[0]["cgroup"].get("throttled_usec", 0) / 1000.0, 1)},
             "errors": sum(g["errors"] for g in gathered),
             "non2xx": sum(g["non2xx"] for g in gathered),
             "config": {
@@ -346,6 +355,18 @@ def _gpu_slots() -> int:
         return int(torch.cuda.device_count())
     except Exception:
         return 0
+
+
+def _cgroup_cpu_stat() -> dict[str, int]:
+    """cgroup v2 cpu.stat counters of this process's cgroup (empty when unavailable)."""
+    try:
+        rel = next((l[3:] for l in Path("/proc/self/cgroup").read_text().splitlines() if l.startswith("0::")), "/")
+        for path in (Path("/sys/fs/cgroup") / rel.lstrip("/") / "cpu.stat", Path("/sys/fs/cgroup/cpu.stat")):
+            if path.exists():
+                return {k: int(v) for k, v in (l.split() for l in path.read_text().splitlines() if l.strip())}
+    except (OSError, IndexError, ValueError):
+        pass
+    return {}
 
 
 def _tcp_counters() -> dict[str, int]:
