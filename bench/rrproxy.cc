@@ -108,6 +108,7 @@ struct Session : EventLoop::Handler {
   bool connecting = false;  // backend handshake not confirmed yet
   int failovers = 0;
   bool closed = false;
+  Session *prev = nullptr, *next = nullptr;  // the owning loop's list of open sessions
 
   Session(ProxyLoop* o, int c, int b) : owner(o), cfd(c), bfd(b) {
     cside.s = bside.s = this;
@@ -132,6 +133,20 @@ class ProxyLoop {
   int index() const { return index_; }
   std::atomic<int64_t>& sessions() { return sessions_; }
 
+  void link(Session* s) {
+    s->next = head_;
+    if (head_) head_->prev = s;
+    head_ = s;
+  }
+  void unlink(Session* s) {
+    if (s->prev) s->prev->next = s->next;
+    else head_ = s->next;
+    if (s->next) s->next->prev = s->prev;
+    s->prev = s->next = nullptr;
+  }
+  // After run() returned: closes what is still open (freed with the loop's retired handlers).
+  void close_all();
+
   void adopt(int cfd) {
     loop_.post([this, cfd] { adopt_here(cfd); });
   }
@@ -148,6 +163,7 @@ class ProxyLoop {
     auto* s = new Session(this, cfd, bfd);
     s->backend = b;
     s->connecting = inprog;
+    link(s);
     loop_.add(bfd, kEvents, &s->bside);
     loop_.add(cfd, kEvents, &s->cside);
   }
@@ -160,6 +176,7 @@ class ProxyLoop {
   EventLoop loop_;
   int index_, cpu_;
   std::atomic<int64_t> sessions_{0};
+  Session* head_ = nullptr;
 };
 
 // Writes what `p` holds to `to`. False on a hard error; true otherwise (p may stay pending
@@ -278,7 +295,12 @@ void Session::close() {
     ::close(bfd);
   }
   owner->sessions().fetch_sub(1, std::memory_order_relaxed);
+  owner->unlink(this);
   l.retire(this);  // the other side's event may still be in this batch
+}
+
+void ProxyLoop::close_all() {
+  while (head_) head_->close();
 }
 
 // Accepts on one listener (on loop 0) and deals each connection to a loop in the client's L3
@@ -442,6 +464,8 @@ int main(int argc, char** argv) {
   for (auto& l : loops) l->loop().stop();
   for (auto& w : ws) w.join();
   hc.join();
+  for (auto& l : loops) l->close_all();
+  ::close(acc.fd);
   for (auto& b : g_backends)
     fprintf(stderr, "rrproxy: %s:%d picked %llu\n", b->host.c_str(), b->port, (unsigned long long)b->picked.load());
   return 0;
