@@ -46,6 +46,10 @@ def _cluster(argv: list[str]) -> int:
     ap = argparse.ArgumentParser(prog="python -m hola_amd cluster")
     ap.add_argument("--replicas", type=int, default=2)
     ap.add_argument("--port", type=int, default=8080)
+    ap.add_argument("--host", default="127.0.0.1",
+                    help="address of the front (the proxy, or the replicas' shared port); pass the "
+                         "address clients reach it on to serve beyond this host. Replicas behind the "
+                         "proxy always listen on 127.0.0.1")
     ap.add_argument("--cores-per-replica", type=int, default=0)
     ap.add_argument("--proxy-threads", type=int, default=2)
     ap.add_argument("--lb", choices=["proxy", "reuseport"], default="proxy",
@@ -63,14 +67,15 @@ def _cluster(argv: list[str]) -> int:
 
     if a.lb == "reuseport":
         plan = plan_node(a.replicas, a.cores_per_replica or None)
-        with ReplicaSet(a.replicas, cpu_plan=plan, args=a.hola_args, supervise=True, shared_port=a.port) as rs:
+        with ReplicaSet(a.replicas, cpu_plan=plan, args=[*a.hola_args, "--host", a.host], supervise=True,
+                        shared_port=a.port) as rs:
             print(f"hola cluster: {a.replicas} replicas sharing :{rs.shared_port} (SO_REUSEPORT; Ctrl-C to stop)",
                   flush=True)
             wait()
         return 0
     plan = plan_node(a.replicas + 1, a.cores_per_replica or None)
     with ReplicaSet(a.replicas, cpu_plan=plan[:a.replicas], args=a.hola_args, supervise=True) as rs:
-        with RRProxy(rs.targets, port=a.port, threads=a.proxy_threads,
+        with RRProxy(rs.targets, port=a.port, threads=a.proxy_threads, host=a.host,
                      cpu_list=format_cpu_list(plan[-1][:a.proxy_threads])) as px:
             print(f"hola cluster: {a.replicas} replicas on ports {rs.ports} behind :{px.port} (Ctrl-C to stop)",
                   flush=True)

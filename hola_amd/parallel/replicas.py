@@ -121,10 +121,10 @@ class RRProxy:
 
     def __init__(self, backends: list[tuple[str, int]], port: int = 0, threads: int = 1,
                  cpu_list: str | None = None, health_ms: int = 200, busy_poll_us: int = 0,
-                 exe: str | None = None):
+                 exe: str | None = None, host: str = "127.0.0.1"):
         self._tmp = tempfile.TemporaryDirectory(prefix="rrproxy-")
         self.port_file = os.path.join(self._tmp.name, "port")
-        cmd = [exe or str(binary("hola_rrproxy")), "--host", "127.0.0.1", "--port", str(port),
+        cmd = [exe or str(binary("hola_rrproxy")), "--host", host, "--port", str(port),
                "--threads", str(threads), "--backends", ",".join(f"{h}:{p}" for h, p in backends),
                "--health-ms", str(health_ms), "--port-file", self.port_file]
         if cpu_list:
