@@ -98,6 +98,7 @@ struct ThreadState {
   int index = 0;
   int epfd = -1;
   int wakefd = -1;
+  std::vector<int> conn_ids;  // connection i goes to target (i + offset) % targets
   std::vector<std::unique_ptr<Conn>> conns;
   Histogram hist;
   std::mutex hist_mu;
@@ -185,6 +186,20 @@ int response_complete(Conn* c, size_t from, int* status, bool* close, size_t* us
 
 void thread_main(ThreadState* ts, const Options* o) {
   if (!o->cpus.empty()) pin_current_thread(o->cpus[size_t(ts->index) % o->cpus.size()]);
+  // Connections (and their receive buffers) are built here, after pinning, so their pages
+  // are first touched on this thread's NUMA node: on a 2-socket node a thread may drive a
+  // replica on the other socket from main()'s.
+  for (int i : ts->conn_ids) {
+    auto c = std::make_unique<Conn>();
+    c->target = (i + o->target_offset) % int(o->targets.size());
+    const Target& t = o->targets[size_t(c->target)];
+    c->req = o->method + " " + o->path + " HTTP/1.1\r\nHost: " + t.host + ":" + std::to_string(t.port) + "\r\n";
+    for (auto& h : o->extra_headers) c->req += h + "\r\n";
+    c->req += "\r\n";
+    const std::string one = c->req;
+    for (int k = 1; k < o->pipeline; ++k) c->req += one;
+    ts->conns.push_back(std::move(c));
+  }
   for (auto& c : ts->conns) {
     if (!connect_once(c.get(), *o)) {
       const Target& t = o->targets[size_t(c->target)];
@@ -527,17 +542,7 @@ int main(int argc, char** argv) {
     s->wakefd = eventfd(0, EFD_NONBLOCK | EFD_CLOEXEC);
     ts.push_back(std::move(s));
   }
-  for (int i = 0; i < o.connections; ++i) {
-    auto c = std::make_unique<Conn>();
-    c->target = (i + o.target_offset) % int(o.targets.size());
-    const Target& t = o.targets[size_t(c->target)];
-    c->req = o.method + " " + o.path + " HTTP/1.1\r\nHost: " + t.host + ":" + std::to_string(t.port) + "\r\n";
-    for (auto& h : o.extra_headers) c->req += h + "\r\n";
-    c->req += "\r\n";
-    const std::string one = c->req;
-    for (int k = 1; k < o.pipeline; ++k) c->req += one;
-    ts[size_t(i % o.threads)]->conns.push_back(std::move(c));
-  }
+  for (int i = 0; i < o.connections; ++i) ts[size_t(i % o.threads)]->conn_ids.push_back(i);
   std::vector<std::thread> th;
   for (auto& s : ts) th.emplace_back(thread_main, s.get(), &o);
   // Each thread connects its own connections from its pinned CPU (as wrk does), so the

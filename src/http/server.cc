@@ -321,7 +321,8 @@ std::string Connection::peer() const {
 // ---------------------------------------------------------------- Worker
 
 Worker::Worker(Server* s, int index) : server_(s), index_(index) {
-  scratch_.resize(s->options().read_chunk);
+  // scratch_ is allocated by the worker thread itself once pinned (Server::start), so its
+  // pages are first touched on the worker's own NUMA node.
   if (s->options().profile) profile_ = std::make_unique<StageProfile>();
   memset(date_, ' ', sizeof date_);
   tick();
@@ -554,6 +555,7 @@ void Server::start() {
         int cpu = opts_.cpus[size_t(wp->index()) % opts_.cpus.size()];
         if (!pin_current_thread(cpu)) LOG_WARN("worker %d: could not pin to cpu %d", wp->index(), cpu);
       }
+      wp->scratch_.assign(opts_.read_chunk, 0);
       handler_->on_worker_start(*wp);
       if (opts_.idle_timeout_ms > 0) {
         int period = std::max(50, std::min(1000, opts_.idle_timeout_ms / 4));
