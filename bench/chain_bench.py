@@ -28,6 +28,7 @@ ap.add_argument("--duration", type=float, default=10)
 ap.add_argument("--connections", type=int, default=64)
 ap.add_argument("--pool", type=int, default=128, help="hystrix thread-pool (bulkhead) size on A")
 ap.add_argument("--out", default="")
+ap.add_argument("--exe-a", default="", help="alternative hola binary for A (A/B runs)")
 a = ap.parse_args()
 
 
@@ -49,7 +50,8 @@ with HolaProcess(args=["--aloha-url", "http://127.0.0.1:1/", "--feign-log", "non
                  cpu_list=format_cpu_list(cores[1])) as b:
     with HolaProcess(args=["--aloha-url", f"http://127.0.0.1:{b.port}/", "--aloha-path", "api/hola-chaining",
                            "--feign-log", "none", "--hystrix-pool-size", str(a.pool)],
-                     env={"HOSTNAME": "A"}, threads=len(cores[0]), cpu_list=format_cpu_list(cores[0])) as s:
+                     env={"HOSTNAME": "A"}, threads=len(cores[0]), cpu_list=format_cpu_list(cores[0]),
+                     exe=Path(a.exe_a) if a.exe_a else None) as s:
         st, _, body = s.get("/api/hola-chaining")
         assert st == 200, body
         sample = json.loads(body)

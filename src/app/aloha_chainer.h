@@ -8,6 +8,7 @@
 //   logging           Feign Logger.ErrorLogger at Level.BASIC        (HolaResource.java:109)
 #pragma once
 #include <atomic>
+#include <deque>
 #include <memory>
 #include <string>
 #include <vector>
@@ -49,7 +50,16 @@ class AlohaChainer final : public Chainer {
   const std::string& full_url() const { return full_url_; }
 
  private:
+  struct Call;
+  struct WorkerCalls;
   client::ClientPool& pool(http::Worker& w);
+  WorkerCalls& calls(http::Worker& w);
+  uint32_t acquire(WorkerCalls& wc);
+  static void release(WorkerCalls& wc, uint32_t slot);
+  static bool dead(const WorkerCalls& wc, uint32_t slot, uint32_t gen);
+  void on_response(WorkerCalls& wc, uint32_t slot, uint32_t gen, int worker_index, client::ClientResult&& r);
+  void expire(EventLoop& loop, WorkerCalls& wc, client::ClientPool& p, int worker_index);
+  void arm(EventLoop& loop, WorkerCalls& wc, client::ClientPool& p, int worker_index);
   AlohaOptions o_;
   client::Url target_;
   bool url_ok_ = false;
@@ -57,6 +67,8 @@ class AlohaChainer final : public Chainer {
   std::unique_ptr<client::AddressCache> addr_;
   std::unique_ptr<resilience::Command> cmd_;
   std::vector<std::unique_ptr<client::ClientPool>> pools_;
+  std::vector<std::unique_ptr<WorkerCalls>> calls_;
+  std::string req_path_;  // target base path + aloha path
   tracing::Tracer* tracer_;
   const Clock& clock_;
   std::atomic<int> timeout_ms_{0};  // 0 = execution timeout disabled (read per call, lock-free)

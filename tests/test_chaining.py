@@ -216,3 +216,33 @@ def test_success_response_framing_get_and_head(hola, aloha):
     assert length == len(body)
     hlines, hbody = raw("HEAD")
     assert hbody == b"" and dict(l.split(": ", 1) for l in hlines[1:])["Content-Length"] == str(length)
+
+
+def test_shortened_timeout_does_not_wait_behind_older_calls(hola, aloha, tmp_path):
+    """Timeouts are kept per worker in deadline order. A call started after the timeout was
+    shortened (config reload) must time out on its own deadline, even while an older call with
+    the longer deadline is still in flight on the same worker."""
+    hc = tmp_path / "config.properties"
+    key = "hystrix.command.default.execution.isolation.thread.timeoutInMilliseconds"
+    hc.write_text(f"{key}=3000\n")
+    aloha.set_mode("slow", delay_s=1.5)
+    s = hola(args=["--aloha-url", aloha.url, "--hystrix-config", str(hc), "--feign-log", "none"], threads=1)
+
+    def reloads():
+        m = s.get("/metrics")[2].decode()
+        return int(next(l for l in m.splitlines() if l.startswith("hola_config_reloads_total ")).split()[1])
+
+    first = []
+    t = threading.Thread(target=lambda: first.append(chain(s)))
+    t.start()
+    time.sleep(0.2)  # the first call is in flight with a 3000 ms deadline
+    before = reloads()
+    hc.write_text(f"{key}=150\n")
+    deadline = time.monotonic() + 3
+    while reloads() == before and time.monotonic() < deadline:
+        time.sleep(0.02)
+    t0 = time.monotonic()
+    assert chain(s)[1:] == [FALLBACK]
+    assert time.monotonic() - t0 < 0.8  # its own 150 ms deadline, not the older 3000 ms one
+    t.join()
+    assert first and first[0][1:] != [FALLBACK]  # the older call still completed normally
