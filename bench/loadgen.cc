@@ -17,6 +17,10 @@
 //        stats       {"count":..,"p50_ns":..,...,"hist":"bin:count,..."} (since last reset)
 //        reset       clears the histogram
 //        quit
+//
+// wrk-style invocation: `hola_loadgen -t8 -c64 -d30s [--latency] http://host:port/path`
+// takes the target from the URL, accepts wrk's duration suffixes (s/m/h) and prints a
+// wrk-like text summary (`--json` keeps the JSON line).
 #include <errno.h>
 #include <netinet/in.h>
 #include <sys/epoll.h>
@@ -27,6 +31,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cctype>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -102,7 +107,7 @@ struct ThreadState {
   std::vector<std::unique_ptr<Conn>> conns;
   Histogram hist;
   std::mutex hist_mu;
-  uint64_t completed = 0, errors = 0, non2xx = 0, reconnects = 0;
+  uint64_t completed = 0, errors = 0, non2xx = 0, reconnects = 0, bytes = 0;
   std::atomic<int64_t> run_quota{0};  // control: batches per connection for the next run
   std::atomic<uint64_t> run_gen{0};
   std::atomic<uint64_t> done_gen{0};
@@ -368,6 +373,7 @@ void thread_main(ThreadState* ts, const Options* o) {
         continue;
       }
       c->have += size_t(r);
+      if (ts->recording) ts->bytes += uint64_t(r);
       bool close = false;
       const int64_t now_rx = mono_ns();
       size_t at = 0;  // responses are consumed in place; what is left moves down once
@@ -478,11 +484,63 @@ std::string stats_json(std::vector<std::unique_ptr<ThreadState>>& ts, bool with_
   return s + "}";
 }
 
+// wrk's duration syntax: "30", "30s", "2m", "1h".
+double parse_duration(const std::string& v) {
+  char* end = nullptr;
+  double x = strtod(v.c_str(), &end);
+  if (end && *end == 'm') x *= 60;
+  else if (end && *end == 'h') x *= 3600;
+  return x;
+}
+
+// "http://host:port/path" (host may be a bracketed IPv6 literal) -> "host:port", "/path".
+bool parse_url_arg(const std::string& url, std::string* target, std::string* path) {
+  if (url.rfind("http://", 0) != 0) return false;
+  std::string rest = url.substr(7);
+  size_t slash = rest.find('/');
+  std::string hostport = rest.substr(0, slash);
+  *path = slash == std::string::npos ? "/" : rest.substr(slash);
+  std::string host = hostport, port = "80";
+  if (!hostport.empty() && hostport[0] == '[') {
+    size_t rb = hostport.find(']');
+    if (rb == std::string::npos) return false;
+    host = hostport.substr(1, rb - 1);
+    if (rb + 1 < hostport.size() && hostport[rb + 1] == ':') port = hostport.substr(rb + 2);
+  } else if (size_t colon = hostport.rfind(':'); colon != std::string::npos) {
+    host = hostport.substr(0, colon);
+    port = hostport.substr(colon + 1);
+  }
+  *target = host + ":" + port;
+  return !host.empty();
+}
+
+std::string human_ns(double ns) {
+  char b[32];
+  if (ns < 1e3) snprintf(b, sizeof b, "%.0fns", ns);
+  else if (ns < 1e6) snprintf(b, sizeof b, "%.2fus", ns / 1e3);
+  else if (ns < 1e9) snprintf(b, sizeof b, "%.2fms", ns / 1e6);
+  else snprintf(b, sizeof b, "%.2fs", ns / 1e9);
+  return b;
+}
+
+std::string human_bytes(double b) {
+  const char* u[] = {"B", "KB", "MB", "GB", "TB"};
+  int k = 0;
+  while (b >= 1024 && k < 4) {
+    b /= 1024;
+    ++k;
+  }
+  char s[32];
+  snprintf(s, sizeof s, "%.2f%s", b, u[k]);
+  return s;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
   Options o;
-  std::string targets = "127.0.0.1:8080", cpu_list;
+  std::string targets = "127.0.0.1:8080", cpu_list, url;
+  bool json = false, latency = false;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto val = [&]() -> std::string {
@@ -498,7 +556,16 @@ int main(int argc, char** argv) {
     else if (a == "--cpu-list") cpu_list = val();
     else if (a == "--path") o.path = val();
     else if (a == "--method") o.method = val();
-    else if (a == "--duration" || a == "-d") o.duration_s = atof(val().c_str());
+    else if (a == "--duration" || a == "-d") o.duration_s = parse_duration(val());
+    else if (a.size() > 2 && (a.rfind("-d", 0) == 0 || a.rfind("-c", 0) == 0 || a.rfind("-t", 0) == 0) &&
+             (isdigit((unsigned char)a[2]))) {  // wrk's glued short options: -d30s -c64 -t8
+      if (a[1] == 'd') o.duration_s = parse_duration(a.substr(2));
+      else if (a[1] == 'c') o.connections = atoi(a.c_str() + 2);
+      else o.threads = atoi(a.c_str() + 2);
+    }
+    else if (a == "--latency") latency = true;
+    else if (a == "--json") json = true;
+    else if (a.rfind("http://", 0) == 0) url = a;
     else if (a == "--warmup") o.warmup_s = atof(val().c_str());
     else if (a == "--control") o.control = true;
     else if (a == "--target-offset") o.target_offset = atoi(val().c_str());
@@ -515,10 +582,18 @@ int main(int argc, char** argv) {
               "usage: hola_loadgen --targets h:p[,h:p..] -c CONNS -t THREADS [--cpu-list L] [--path P]\n"
               "                    (--duration S [--warmup S] [--rate R [--spin-us N]] | --control [--per-conn-quota])\n"
               "                    [--target-offset K] [--busy-poll-us N [--busy-poll-pause P]] [--epoll-lt] [-H 'Name: v']\n"
-              "                    [--pipeline P]\n");
+              "                    [--pipeline P]\n"
+              "       hola_loadgen -t T -c C -d 30s [--latency] [--json] [-H 'Name: v'] http://host:port/path   (wrk style)\n");
       return 2;
     }
   }
+  if (!url.empty()) {
+    if (!parse_url_arg(url, &targets, &o.path)) {
+      fprintf(stderr, "loadgen: bad URL %s\n", url.c_str());
+      return 2;
+    }
+  }
+  const bool wrk_text = !url.empty() && !json && !o.control;
   if (!parse_targets(targets, &o.targets)) return 2;
   if (!cpu_list.empty() && !parse_cpu_list(cpu_list, &o.cpus)) {
     fprintf(stderr, "loadgen: bad --cpu-list\n");
@@ -563,6 +638,30 @@ int main(int argc, char** argv) {
     uint64_t completed = 0;
     for (auto& t : ts) completed += t->completed;
     double rps = double(completed) / o.duration_s;
+    if (wrk_text) {
+      Histogram h;
+      uint64_t errors = 0, non2xx = 0, bytes = 0;
+      for (auto& t : ts) {
+        h.merge(t->hist);
+        errors += t->errors;
+        non2xx += t->non2xx;
+        bytes += t->bytes;
+      }
+      printf("Running %.0fs test @ %s\n  %d threads and %d connections\n", o.duration_s, url.c_str(), o.threads,
+             o.connections);
+      printf("  Latency   avg %s, max %s\n", human_ns(h.mean()).c_str(), human_ns(double(h.max())).c_str());
+      if (latency) {
+        printf("  Latency Distribution\n");
+        for (double p : {50.0, 75.0, 90.0, 99.0, 99.9})
+          printf("  %6.2f%%  %s\n", p, human_ns(double(h.percentile(p))).c_str());
+      }
+      printf("  %llu requests in %.2fs, %s read\n", (unsigned long long)completed, o.duration_s,
+             human_bytes(double(bytes)).c_str());
+      if (errors) printf("  Socket errors: %llu\n", (unsigned long long)errors);
+      if (non2xx) printf("  Non-2xx or 3xx responses: %llu\n", (unsigned long long)non2xx);
+      printf("Requests/sec: %12.2f\nTransfer/sec: %10s\n", rps, human_bytes(double(bytes) / o.duration_s).c_str());
+      return 0;
+    }
     printf("{\"mode\":\"%s\",\"duration_s\":%.3f,\"connections\":%d,\"threads\":%d,\"targets\":%zu,\"target_rate\":%.1f,\"rps\":%.1f,\"latency\":%s}\n",
            o.rate > 0 ? "open-loop" : "duration", o.duration_s, o.connections, o.threads, o.targets.size(), o.rate, rps,
            s.c_str());

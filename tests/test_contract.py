@@ -355,3 +355,21 @@ def test_loadgen_pipelined_batches_counted(hola):
     out = run_duration([("127.0.0.1", s.port)], 4, 1, 0.5, 0.2, pipeline=8)
     lat = out["latency"]
     assert lat["errors"] == 0 and lat["non2xx"] == 0 and lat["count"] > 8 and lat["reconnects"] == 0
+
+
+def test_loadgen_wrk_style_invocation(hola):
+    """`hola_loadgen -t1 -c4 -d1s --latency http://host:port/path` as a drop-in for the wrk runs
+    of BASELINE configs 2-4: wrk's glued options and duration suffix, text summary."""
+    import subprocess
+
+    from hola_amd.native import binary
+
+    s = hola()
+    r = subprocess.run([str(binary("hola_loadgen")), "-t1", "-c4", "-d1s", "--latency",
+                        f"http://127.0.0.1:{s.port}/api/health"], capture_output=True, text=True, timeout=30)
+    assert r.returncode == 0, r.stderr
+    out = r.stdout
+    assert out.startswith("Running 1s test @ http://127.0.0.1:") and "1 threads and 4 connections" in out
+    assert "Latency Distribution" in out and "Requests/sec:" in out
+    assert "Socket errors" not in out and "Non-2xx" not in out
+    assert int(out.split(" requests in ")[0].split()[-1]) > 0
