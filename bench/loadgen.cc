@@ -170,23 +170,49 @@ bool send_req(Conn* c, int depth) {
 
 // Returns 1 when a full response starts at buf[from] (its size in *used), 0 if more is
 // needed, -1 on malformed input.
+// Case-insensitive prefix test against a lower-case literal.
+inline bool iprefix(const char* p, size_t n, std::string_view lower) {
+  if (n < lower.size()) return false;
+  for (size_t i = 0; i < lower.size(); ++i)
+    if ((p[i] | 0x20) != lower[i]) return false;
+  return true;
+}
+
+// Returns 1 when a full response starts at buf[from] (its size in *used), 0 if more is
+// needed, -1 on malformed input. One pass over the head's lines: the status line, then
+// Content-Length and Connection, up to the empty line.
 int response_complete(Conn* c, size_t from, int* status, bool* close, size_t* used) {
-  std::string_view s(c->buf + from, c->have - from);
-  const void* end = memmem(s.data(), s.size(), "\r\n\r\n", 4);
-  if (!end) return (from == 0 && c->have >= sizeof c->buf) ? -1 : 0;  // a head larger than buf
-  const size_t he = size_t(static_cast<const char*>(end) - s.data());
-  if (s.size() < 12 || s.substr(0, 5) != "HTTP/") return -1;
+  const char* s = c->buf + from;
+  const size_t n = c->have - from;
+  auto incomplete = [&] { return (from == 0 && c->have >= sizeof c->buf) ? -1 : 0; };  // head > buf
+  const char* nl = static_cast<const char*>(memchr(s, '\n', n));
+  if (!nl) return incomplete();
+  if (nl - s < 12 || memcmp(s, "HTTP/", 5) != 0) return -1;
   *status = (s[9] - '0') * 100 + (s[10] - '0') * 10 + (s[11] - '0');
-  std::string_view head = s.substr(0, he);
-  size_t cl = 0;
-  size_t p = head.find("Content-Length: ");
-  if (p == std::string_view::npos) p = head.find("content-length: ");
-  if (p != std::string_view::npos)
-    for (size_t i = p + 16; i < head.size() && head[i] >= '0' && head[i] <= '9'; ++i) cl = cl * 10 + size_t(head[i] - '0');
-  *close = head.find("Connection: close") != std::string_view::npos;
-  if (he + 4 + cl > sizeof c->buf) return -1;
-  *used = he + 4 + cl;
-  return s.size() >= *used ? 1 : 0;
+  *close = false;
+  size_t cl = 0, p = size_t(nl - s) + 1;
+  for (;;) {
+    const char* line = s + p;
+    const char* e = static_cast<const char*>(memchr(line, '\n', n - p));
+    if (!e) return incomplete();
+    size_t len = size_t(e - line);
+    p += len + 1;
+    if (len && line[len - 1] == '\r') --len;
+    if (len == 0) break;  // end of head
+    if ((line[0] | 0x20) != 'c') continue;
+    if (iprefix(line, len, "content-length:")) {
+      size_t i = 15;
+      while (i < len && line[i] == ' ') ++i;
+      for (; i < len && line[i] >= '0' && line[i] <= '9'; ++i) cl = cl * 10 + size_t(line[i] - '0');
+    } else if (iprefix(line, len, "connection:")) {
+      size_t i = 11;
+      while (i < len && line[i] == ' ') ++i;
+      *close = iprefix(line + i, len - i, "close");
+    }
+  }
+  if (p + cl > sizeof c->buf) return -1;
+  *used = p + cl;
+  return n >= *used ? 1 : 0;
 }
 
 void thread_main(ThreadState* ts, const Options* o) {
