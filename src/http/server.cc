@@ -135,8 +135,8 @@ bool Connection::process(const char* data, size_t len, size_t* consumed) {
   in_process_ = true;
   size_t off = 0;
   uint64_t handled = 0;
+  Request r;  // parse_request resets it for every request
   while (off < len && !parked_ && !streaming_ && !closed_ && !close_after_flush_) {
-    Request r;
     int status = 400;
     StageProfile* prof = worker_->profile();
     int64_t tp = prof ? mono_ns() : 0;
