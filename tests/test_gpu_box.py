@@ -53,3 +53,35 @@ def test_bench_two_ranks_on_host():
     assert out["requests"] == 2 * 64 * 500 * 3
     assert out["errors"] == 0 and out["non2xx"] == 0
     assert set(out["config"]["cpu_map"]) == {"rank0", "rank1"}
+
+
+@pytest.mark.gpu
+def test_pipelined_bench_on_host():
+    """`bench.py --pipeline 16` on the real host: 16 requests share each loopback segment."""
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--pipeline", "16", "--steps", "2", "--warmup", "1",
+                        "--reqs-per-conn", "16000"], capture_output=True, text=True, timeout=300,
+                       env={**os.environ, "HOLA_BENCH_PORT": "18780"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["errors"] == 0 and out["non2xx"] == 0 and out["requests"] == 64 * 16000 * 2
+    assert out["config"]["pipeline"] == 16
+    assert out["value"] > 1_000_000  # a loaded box still does several times this
+    if out["tcp_per_req"]:
+        assert out["tcp_per_req"]["OutSegs"] < 0.5
+
+
+@pytest.mark.gpu
+def test_proxy_front_on_host():
+    """The L4 round-robin proxy between the load generator and a replica, in the mirrored core
+    plan on the real host's L3 domains."""
+    import contextlib
+    import io
+
+    from hola_amd.parallel import scaling
+
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        scaling.main(["--replicas", "1", "--lb", "proxy", "--duration", "2", "--warmup", "0.5"])
+    row = json.loads(next(l for l in buf.getvalue().splitlines() if l.startswith("{")))
+    assert row["errors"] == 0 and row["non2xx"] == 0 and row["lb"] == "proxy"
+    assert row["rps"] > 100_000
