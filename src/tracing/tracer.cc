@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstring>
+#include <type_traits>
 
 #include "client/url.h"
 #include "core/clock.h"
@@ -23,7 +24,8 @@ namespace hola::tracing {
 SpanRing::SpanRing(size_t cap) {
   size_t c = 1;
   while (c < cap) c <<= 1;
-  buf_.resize(c);
+  static_assert(std::is_trivially_default_constructible_v<SpanRecord>);
+  buf_.reset(new SpanRecord[c]);
   mask_ = c - 1;
 }
 
@@ -56,7 +58,6 @@ Tracer::Tracer(TracerOptions o, int num_workers) : o_(std::move(o)) {
     }
     w->s0 = seed[0] | 1;
     w->s1 = seed[1] | 2;
-    w->ring = std::make_unique<SpanRing>(o_.ring_capacity);
     ws_.push_back(std::move(w));
   }
   client::Url u;
@@ -70,6 +71,9 @@ Tracer::Tracer(TracerOptions o, int num_workers) : o_(std::move(o)) {
       LOG_WARN("ZIPKIN_SERVER_URL '%s' is not an http:// URL; spans will be dropped", o_.collector_url.c_str());
     }
   }
+  // Without a collector, spans are counted and dropped at the source: no rings.
+  if (collecting_)
+    for (auto& w : ws_) w->ring = std::make_unique<SpanRing>(o_.ring_capacity);
 }
 
 Tracer::~Tracer() {
@@ -139,7 +143,7 @@ ServerSpan Tracer::begin_server(int worker, const http::Request& r) {
 
 void Tracer::push(int worker, const SpanRecord& r) {
   WorkerState& w = *ws_[size_t(worker)];
-  if (w.ring->push(r)) w.recorded.store(w.recorded.load(std::memory_order_relaxed) + 1, std::memory_order_relaxed);
+  if (w.ring && w.ring->push(r)) w.recorded.store(w.recorded.load(std::memory_order_relaxed) + 1, std::memory_order_relaxed);
   else w.dropped.store(w.dropped.load(std::memory_order_relaxed) + 1, std::memory_order_relaxed);
 }
 
@@ -305,7 +309,8 @@ bool Tracer::post(const std::string& body) {
 }
 
 void Tracer::drain_rings() {
-  for (auto& w : ws_) w->ring->drain(&pending_);
+  for (auto& w : ws_)
+    if (w->ring) w->ring->drain(&pending_);
 }
 
 void Tracer::post_pending() {

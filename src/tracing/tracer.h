@@ -61,7 +61,9 @@ class SpanRing {
   size_t drain(std::vector<SpanRecord>* out);
 
  private:
-  std::vector<SpanRecord> buf_;
+  // Left uninitialised (SpanRecord is trivial): the pages are first touched by the producing
+  // worker, on its own NUMA node.
+  std::unique_ptr<SpanRecord[]> buf_;
   size_t mask_;
   alignas(64) std::atomic<uint64_t> head_{0};  // consumer
   alignas(64) std::atomic<uint64_t> tail_{0};  // producer
