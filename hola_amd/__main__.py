@@ -96,6 +96,15 @@ def _info() -> int:
     print(f"cgroup quota   : {cgroup_cpu_quota() or 'unlimited'}  -> budget {cpu_budget()} CPUs")
     for n in (1, 2, 4, 8):
         print(f"plan x{n}: {[format_cpu_list(p) for p in plan_node(n, avoid_busy=False)]}")
+    # What bench.py would decide on this node (one replica per GPU slot, weak scaling).
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent))  # bench.py at the repo root
+    from bench import _gpu_slots
+    from hola_amd.utils.cpu import slot_cores, smt_fits
+
+    slots = max(1, _gpu_slots())
+    cores = slot_cores(slots)
+    print(f"gpu slots      : {slots} (KFD topology) -> {cores} physical cores per replica")
+    print(f"bench --smt auto: {'pair' if smt_fits(slots, cores) else 'off'}")
     return 0
 
 
