@@ -224,7 +224,9 @@ void thread_main(ThreadState* ts, const Options* o) {
     auto c = std::make_unique<Conn>();
     c->target = (i + o->target_offset) % int(o->targets.size());
     const Target& t = o->targets[size_t(c->target)];
-    c->req = o->method + " " + o->path + " HTTP/1.1\r\nHost: " + t.host + ":" + std::to_string(t.port) + "\r\n";
+    const bool v6 = t.host.find(':') != std::string::npos;  // RFC 3986 IP-literal in Host
+    c->req = o->method + " " + o->path + " HTTP/1.1\r\nHost: " + (v6 ? "[" + t.host + "]" : t.host) + ":" +
+             std::to_string(t.port) + "\r\n";
     for (auto& h : o->extra_headers) c->req += h + "\r\n";
     c->req += "\r\n";
     const std::string one = c->req;
