@@ -17,6 +17,7 @@
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -108,6 +109,7 @@ struct Session : EventLoop::Handler {
   bool connecting = false;  // backend handshake not confirmed yet
   int failovers = 0;
   bool closed = false;
+  int64_t last_active_ms = 0;  // for the idle timeout
   Session *prev = nullptr, *next = nullptr;  // the owning loop's list of open sessions
 
   Session(ProxyLoop* o, int c, int b) : owner(o), cfd(c), bfd(b) {
@@ -124,7 +126,8 @@ struct Session : EventLoop::Handler {
 
 class ProxyLoop {
  public:
-  ProxyLoop(int index, int cpu, int busy_poll_us, int busy_poll_pause) : index_(index), cpu_(cpu) {
+  ProxyLoop(int index, int cpu, int busy_poll_us, int busy_poll_pause, int idle_timeout_ms)
+      : index_(index), cpu_(cpu), idle_timeout_ms_(idle_timeout_ms) {
     loop_.set_busy_poll_us(busy_poll_us);
     loop_.set_busy_poll_pause(busy_poll_pause);
   }
@@ -163,18 +166,36 @@ class ProxyLoop {
     auto* s = new Session(this, cfd, bfd);
     s->backend = b;
     s->connecting = inprog;
+    s->last_active_ms = loop_.now_ms();
     link(s);
     loop_.add(bfd, kEvents, &s->bside);
     loop_.add(cfd, kEvents, &s->cside);
   }
   void run() {
     if (cpu_ >= 0) pin_current_thread(cpu_);
+    if (idle_timeout_ms_ > 0) schedule_sweep();
     loop_.run();
+  }
+  // Closes sessions with no traffic in either direction for the idle timeout (an L4 front's
+  // "timeout client/server"): e.g. a client that keeps a session open after the backend
+  // closed its side.
+  void schedule_sweep() {
+    const int period = std::max(50, std::min(1000, idle_timeout_ms_ / 4));
+    loop_.add_timer(period, [this] {
+      const int64_t now = loop_.now_ms();
+      for (Session* s = head_; s;) {
+        Session* next = s->next;
+        if (now - s->last_active_ms > idle_timeout_ms_) s->close();
+        s = next;
+      }
+      schedule_sweep();
+    });
   }
 
  private:
   EventLoop loop_;
   int index_, cpu_;
+  int idle_timeout_ms_;
   std::atomic<int64_t> sessions_{0};
   Session* head_ = nullptr;
 };
@@ -253,6 +274,7 @@ bool Session::backend_connected(uint32_t ev) {
 
 void Session::on_event(bool client_side, uint32_t ev) {
   if (closed) return;
+  last_active_ms = owner->loop().now_ms();
   if (connecting) {
     // The client is not read until the backend accepted, so a refusal can still fail over.
     if (client_side) {
@@ -366,7 +388,7 @@ void health_loop(int interval_ms) {
 }  // namespace
 
 int main(int argc, char** argv) {
-  int port = 8080, threads = 1, health_ms = 500, busy_poll_us = 0, busy_poll_pause = 0;
+  int port = 8080, threads = 1, health_ms = 500, busy_poll_us = 0, busy_poll_pause = 0, idle_timeout_ms = 60000;
   bool steer = true;
   std::string backends, cpu_list, host = "0.0.0.0", port_file;
   for (int i = 1; i < argc; ++i) {
@@ -385,10 +407,12 @@ int main(int argc, char** argv) {
     else if (a == "--busy-poll-us") busy_poll_us = atoi(val().c_str());
     else if (a == "--busy-poll-pause") busy_poll_pause = atoi(val().c_str());
     else if (a == "--no-steer") steer = false;
+    else if (a == "--idle-timeout-ms") idle_timeout_ms = atoi(val().c_str());
     else {
       fprintf(stderr,
               "usage: hola_rrproxy --backends h:p,h:p.. [--port N] [--host H] [--threads N] [--cpu-list L]\n"
-              "                    [--health-ms N] [--busy-poll-us N [--busy-poll-pause P]] [--no-steer] [--port-file F]\n");
+              "                    [--health-ms N] [--busy-poll-us N [--busy-poll-pause P]] [--no-steer] [--port-file F]\n"
+              "                    [--idle-timeout-ms N (default 60000, 0 = never)]\n");
       return 2;
     }
   }
@@ -445,7 +469,7 @@ int main(int argc, char** argv) {
   std::vector<std::unique_ptr<ProxyLoop>> loops;
   for (int t = 0; t < threads; ++t)
     loops.push_back(std::make_unique<ProxyLoop>(t, cpus.empty() ? -1 : cpus[size_t(t) % cpus.size()], busy_poll_us,
-                                                busy_poll_pause));
+                                                busy_poll_pause, idle_timeout_ms));
   acc.loops = &loops;
   acc.steer = steer && !cpus.empty();
   loops[0]->loop().add(acc.fd, EPOLLIN, &acc);

@@ -121,7 +121,7 @@ class RRProxy:
 
     def __init__(self, backends: list[tuple[str, int]], port: int = 0, threads: int = 1,
                  cpu_list: str | None = None, health_ms: int = 200, busy_poll_us: int = 0,
-                 exe: str | None = None, host: str = "127.0.0.1"):
+                 exe: str | None = None, host: str = "127.0.0.1", idle_timeout_ms: int | None = None):
         self._tmp = tempfile.TemporaryDirectory(prefix="rrproxy-")
         self.port_file = os.path.join(self._tmp.name, "port")
         cmd = [exe or str(binary("hola_rrproxy")), "--host", host, "--port", str(port),
@@ -131,6 +131,8 @@ class RRProxy:
             cmd += ["--cpu-list", cpu_list]
         if busy_poll_us:
             cmd += ["--busy-poll-us", str(busy_poll_us)]
+        if idle_timeout_ms is not None:
+            cmd += ["--idle-timeout-ms", str(idle_timeout_ms)]
         self.cmd = cmd
         self.proc: subprocess.Popen | None = None
         self.port = port

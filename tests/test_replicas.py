@@ -67,6 +67,26 @@ def test_proxy_half_close_and_backpressure():
         assert data.endswith(b"Hola de replica-0")
 
 
+def test_proxy_idle_timeout_closes_silent_sessions():
+    """A session with no traffic either way for --idle-timeout-ms is closed by the proxy; an
+    active one is not."""
+    import socket
+
+    with ReplicaSet(1, threads_per_replica=1, supervise=False) as rs, \
+            RRProxy(rs.targets, idle_timeout_ms=300) as px:
+        idle = socket.create_connection(("127.0.0.1", px.port), timeout=5)
+        busy = socket.create_connection(("127.0.0.1", px.port), timeout=5)
+        t0 = time.monotonic()
+        while time.monotonic() - t0 < 1.2:
+            busy.sendall(b"GET /api/health HTTP/1.1\r\nHost: x\r\n\r\n")
+            assert busy.recv(4096).startswith(b"HTTP/1.1 200")
+            time.sleep(0.1)
+        idle.settimeout(2)
+        assert idle.recv(16) == b""  # closed by the proxy
+        idle.close()
+        busy.close()
+
+
 def test_proxy_fails_over_on_refused_connect():
     """A backend that refuses is marked DOWN at once and the connection goes to the next one,
     before any health check has run."""
