@@ -11,7 +11,8 @@
 // IN|OUT|RDHUP: no epoll_ctl per message. A read that comes back short has drained the
 // socket (no extra EAGAIN read); a send that would block parks the bytes until the OUT edge
 // and stops reading the other side until they are gone (backpressure). Accepted sockets are
-// handed to a loop in the client's L3 domain (SO_INCOMING_CPU), as the server does.
+// handed to a loop in the client's L3 domain (SO_INCOMING_CPU), as the server does. A FIN
+// is passed on as a half-close; sessions silent for --idle-timeout-ms are closed.
 #include <errno.h>
 #include <signal.h>
 #include <sys/socket.h>
