@@ -373,3 +373,23 @@ def test_loadgen_wrk_style_invocation(hola):
     assert "Latency Distribution" in out and "Requests/sec:" in out
     assert "Socket errors" not in out and "Non-2xx" not in out
     assert int(out.split(" requests in ")[0].split()[-1]) > 0
+
+
+def test_loadgen_url_with_ipv6_literal(hola):
+    """wrk-style URL with a bracketed IPv6 literal; the Host header carries the brackets."""
+    import socket
+    import subprocess
+
+    from hola_amd.native import binary
+
+    try:
+        with socket.socket(socket.AF_INET6) as sk:
+            sk.bind(("::1", 0))
+    except OSError:
+        pytest.skip("no IPv6 loopback")
+    s = hola(args=["--host", "::1"])
+    r = subprocess.run([str(binary("hola_loadgen")), "-t1", "-c2", "-d1", "--json",
+                        f"http://[::1]:{s.port}/api/hola"], capture_output=True, text=True, timeout=30)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(r.stdout)
+    assert out["rps"] > 0 and out["latency"]["errors"] == 0 and out["latency"]["non2xx"] == 0
