@@ -97,3 +97,12 @@ def test_systemd_units_reuseport(tmp_path):
     assert "SO_REUSEPORT" in units["hola.target"]
     with pytest.raises(ValueError):
         render_units(replicas=1, lb="dns")
+
+
+def test_license_matches_swagger_document():
+    """C24: the project license is Apache-2.0, the one `SwaggerListener` advertises."""
+    import json
+    text = (ROOT / "LICENSE").read_text()
+    assert "Apache-2.0" in text and "http://www.apache.org/licenses/LICENSE-2.0" in text
+    lic = json.loads((ROOT / "assets" / "swagger.json").read_text())["info"]["license"]
+    assert lic["url"] == "http://www.apache.org/licenses/LICENSE-2.0.html"
