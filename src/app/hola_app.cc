@@ -302,6 +302,12 @@ void HolaApp::on_request(http::Connection& c, const http::Request& r) {
     size_t n = 0;
     if (path.size() <= sizeof decoded && http::percent_decode(path, decoded, &n)) path = std::string_view(decoded, n);
   }
+  char canonical[512];
+  if (__builtin_expect(path.find("/.") != std::string_view::npos, 0)) {
+    size_t n = 0;
+    if (path.size() <= sizeof canonical && http::remove_dot_segments(path, canonical, &n))
+      path = std::string_view(canonical, n);
+  }
   const int route = route_of(path);
   const Method m = method_of(r.method);
   const int head = m == Method::kHead ? 1 : 0;

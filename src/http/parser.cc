@@ -83,6 +83,36 @@ bool percent_decode(std::string_view in, char* out, size_t* out_len) {
   return true;
 }
 
+bool remove_dot_segments(std::string_view in, char* out, size_t* out_len) {
+  // RFC 3986 §5.2.4 on an absolute path, segment by segment: "." segments vanish, ".."
+  // drops the last output segment (never above the root). A trailing "." or ".." leaves
+  // the path ending in "/", as the RFC's "/." and "/.." rules do.
+  if (in.empty() || in[0] != '/') return false;
+  size_t o = 0;
+  size_t i = 0;
+  while (i < in.size()) {
+    size_t j = i + 1;  // in[i] == '/'
+    while (j < in.size() && in[j] != '/') ++j;
+    std::string_view seg = in.substr(i + 1, j - i - 1);
+    const bool last = j == in.size();
+    if (seg == ".") {
+      if (last) out[o++] = '/';
+    } else if (seg == "..") {
+      while (o > 0 && out[o - 1] != '/') --o;  // strip the last segment's text ...
+      if (o > 0) --o;                          // ... and its leading '/'
+      if (last) out[o++] = '/';
+    } else {
+      out[o++] = '/';
+      memcpy(out + o, seg.data(), seg.size());
+      o += seg.size();
+    }
+    i = j;
+  }
+  if (o == 0) out[o++] = '/';
+  *out_len = o;
+  return true;
+}
+
 Parse parse_request(const char* buf, size_t len, Request* req, int* status) {
   *req = Request();
   size_t pos = 0;

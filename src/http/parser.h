@@ -49,5 +49,9 @@ Parse decode_chunked_body(const char* buf, size_t len, size_t* consumed, std::st
 bool iequals(std::string_view a, std::string_view b);
 // Percent-decodes a path; false on malformed escapes. Output written to out (len <= in len).
 bool percent_decode(std::string_view in, char* out, size_t* out_len);
+// Removes "." and ".." segments from an absolute path (RFC 3986 §5.2.4), the way Undertow
+// canonicalises the request path before servlet/JAX-RS matching; false unless `in` starts
+// with '/'. Output written to out (len <= in len).
+bool remove_dot_segments(std::string_view in, char* out, size_t* out_len);
 
 }  // namespace hola::http

@@ -324,6 +324,12 @@ PYBIND11_MODULE(_native, m) {
     return http::accepts(accept, t, st);
   });
   m.def("parse_request", &parse_request_py);
+  m.def("remove_dot_segments", [](const std::string& p) -> py::object {
+    std::string out(p.size() + 1, '\0');
+    size_t n = 0;
+    if (!http::remove_dot_segments(p, out.data(), &n)) return py::none();
+    return py::str(out.substr(0, n));
+  });
   m.def("skip_chunked_body", &skip_chunked_py);
   m.def("decode_chunked_body", &decode_chunked_py);
   m.def("b3_extract", &b3_extract_py, py::arg("trace_id") = "", py::arg("span_id") = "", py::arg("parent_id") = "",

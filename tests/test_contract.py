@@ -133,6 +133,18 @@ def test_trailing_slash_and_percent_encoding(hola):
     assert s.get("/api/hola?x=1&y=2")[2] == b"Hola de h"
 
 
+def test_dot_segments_are_removed_before_matching(hola):
+    """Undertow canonicalises the request path before servlet/JAX-RS matching (parity
+    unpinned: no reference artefact covers it); RFC 3986 §5.2.4 gives the same result."""
+    s = hola(env={"HOSTNAME": "h"})
+    assert s.get("/api/../api/hola")[2] == b"Hola de h"
+    assert s.get("/api/./hola")[2] == b"Hola de h"
+    assert s.get("/../../api/health")[2] == b"I'm ok"
+    assert s.get("/api/%2e%2e/api/hola")[2] == b"Hola de h"  # decoded first, then canonicalised
+    assert s.get("/api/hola/x/..")[2] == b"Hola de h"       # -> /api/hola/ (one trailing slash)
+    assert s.get("/api/hola/..")[0] == 404                   # -> /api/
+
+
 def _raw(port, data: bytes, timeout=3.0) -> bytes:
     with socket.create_connection(("127.0.0.1", port), timeout=timeout) as c:
         c.sendall(data)

@@ -154,3 +154,50 @@ def test_json_roundtrip(native, items):
     assert json.loads(enc) == items
     dec = native.decode_string_list(enc)
     assert [None if x is None else x.decode() for x in dec] == items
+
+
+@pytest.mark.parametrize("path,want", [
+    ("/api/hola", "/api/hola"), ("/api/../api/hola", "/api/hola"), ("/api/./hola", "/api/hola"),
+    ("/../api/hola", "/api/hola"), ("/api/hola/.", "/api/hola/"), ("/api/hola/..", "/api/"),
+    ("/.", "/"), ("/..", "/"), ("/a/b/../../c", "/c"), ("/api/.hidden", "/api/.hidden"),
+    ("/api/..x/../hola", "/api/hola"), ("//a/../b", "//b"), ("rel/path", None),
+])
+def test_remove_dot_segments(native, path, want):
+    assert native.remove_dot_segments(path) == want
+
+
+def _rfc3986_remove_dot_segments(p: str) -> str:
+    """RFC 3986 §5.2.4, step by step, as the oracle."""
+    out = []
+    while p:
+        if p.startswith("../"):
+            p = p[3:]
+        elif p.startswith("./"):
+            p = p[2:]
+        elif p.startswith("/./"):
+            p = p[2:]
+        elif p == "/.":
+            p = "/"
+        elif p.startswith("/../"):
+            p = p[3:]
+            if out:
+                out.pop()
+        elif p == "/..":
+            p = "/"
+            if out:
+                out.pop()
+        elif p in (".", ".."):
+            p = ""
+        else:
+            j = p.find("/", 1)
+            j = len(p) if j < 0 else j
+            out.append(p[:j])
+            p = p[j:]
+    return "".join(out) or "/"
+
+
+@settings(max_examples=400, deadline=None)
+@given(st.lists(st.sampled_from(["a", "bc", ".", "..", "", "..x", ".y"]), min_size=1, max_size=8))
+def test_remove_dot_segments_matches_rfc_oracle(native, segs):
+    path = "/" + "/".join(segs)
+    assert native.remove_dot_segments(path) == _rfc3986_remove_dot_segments(path)
