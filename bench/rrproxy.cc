@@ -358,6 +358,16 @@ struct Acceptor : EventLoop::Handler {
       int c = ::accept4(fd, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
       if (c < 0) {
         if (errno == EINTR || errno == ECONNABORTED) continue;
+        if (errno == EMFILE || errno == ENFILE) {
+          // The listener is level-triggered: leaving it armed at the fd limit would spin
+          // loop 0. Disarm it and retry in 50 ms (hola's server does the same).
+          fprintf(stderr, "rrproxy: accept: %s (fd limit); pausing accepts\n", strerror(errno));
+          EventLoop& l = (*loops)[0]->loop();
+          l.del(fd);
+          l.add_timer(50, [this, &l] {
+            if (!g_stop.load()) l.add(fd, EPOLLIN, this);
+          });
+        }
         return;
       }
       set_nodelay(c);

@@ -206,3 +206,53 @@ def test_open_loop_rate_mode(hola):
     assert res["mode"] == "open-loop"
     assert 4500 <= res["rps"] <= 5500
     assert res["latency"]["errors"] == 0 and res["latency"]["p50_ns"] > 0
+
+
+def _cpu_s(pid: int) -> float:
+    import os
+    f = open(f"/proc/{pid}/stat").read().rsplit(")", 1)[1].split()
+    return (int(f[11]) + int(f[12])) / os.sysconf("SC_CLK_TCK")
+
+
+def _exhaust_fds_then_recover(pid: int, port: int, fd_limit: int):
+    """Lowers the process's RLIMIT_NOFILE, holds enough client connections to hit it, checks
+    that the process idles (a still-armed level-triggered listener would spin a core at
+    100 %), then frees the connections and checks that accepting resumes."""
+    import resource
+    import socket
+
+    soft, hard = resource.prlimit(pid, resource.RLIMIT_NOFILE)
+    resource.prlimit(pid, resource.RLIMIT_NOFILE, (fd_limit, hard))  # soft limit only: no privilege needed
+    held = []
+    try:
+        for _ in range(fd_limit + 8):
+            c = socket.create_connection(("127.0.0.1", port), timeout=5)
+            held.append(c)
+        time.sleep(0.3)  # every fd is in use and the rest wait in the backlog
+        c0 = _cpu_s(pid)
+        time.sleep(1.0)
+        assert _cpu_s(pid) - c0 < 0.3, "accept loop spins at the fd limit"
+    finally:
+        for c in held:
+            c.close()
+    resource.prlimit(pid, resource.RLIMIT_NOFILE, (soft, hard))
+    deadline = time.monotonic() + 5
+    while True:
+        try:
+            assert greeting_via(port).startswith("Hola de")
+            return
+        except (OSError, AssertionError):
+            if time.monotonic() > deadline:
+                raise
+            time.sleep(0.1)
+
+
+def test_proxy_backs_off_at_fd_limit():
+    with ReplicaSet(1, threads_per_replica=1, supervise=False) as rs, RRProxy(rs.targets) as px:
+        _exhaust_fds_then_recover(px.proc.pid, px.port, 48)
+        assert "fd limit" in px.log()
+
+
+def test_server_backs_off_at_fd_limit(hola):
+    s = hola(env={"HOSTNAME": "h"}, threads=1)
+    _exhaust_fds_then_recover(s.proc.pid, s.port, 48)
