@@ -79,6 +79,11 @@ int connect_backend(Backend** chosen, bool* in_progress) {
       *chosen = b;
       return fd;
     }
+    // Out of local fds, memory or ephemeral ports: the next backend would fail the same
+    // way, and none of them is at fault.
+    if (errno == EMFILE || errno == ENFILE || errno == ENOBUFS || errno == ENOMEM || errno == EAGAIN ||
+        errno == EADDRNOTAVAIL)
+      return -1;
     mark_down(b, errno);
   }
   return -1;
@@ -332,6 +337,7 @@ struct Acceptor : EventLoop::Handler {
   int fd = -1;
   std::vector<std::unique_ptr<ProxyLoop>>* loops = nullptr;
   bool steer = true;
+  bool paused = false;  // accepts are paused at the fd limit (logged once per episode)
   uint64_t rr = 0;
 
   ProxyLoop* choose(int cfd) {
@@ -361,7 +367,8 @@ struct Acceptor : EventLoop::Handler {
         if (errno == EMFILE || errno == ENFILE) {
           // The listener is level-triggered: leaving it armed at the fd limit would spin
           // loop 0. Disarm it and retry in 50 ms (hola's server does the same).
-          fprintf(stderr, "rrproxy: accept: %s (fd limit); pausing accepts\n", strerror(errno));
+          if (!paused) fprintf(stderr, "rrproxy: accept: %s (fd limit); pausing accepts\n", strerror(errno));
+          paused = true;
           EventLoop& l = (*loops)[0]->loop();
           l.del(fd);
           l.add_timer(50, [this, &l] {
@@ -370,6 +377,7 @@ struct Acceptor : EventLoop::Handler {
         }
         return;
       }
+      paused = false;
       set_nodelay(c);
       ProxyLoop* l = choose(c);
       l->sessions().fetch_add(1, std::memory_order_relaxed);
@@ -387,8 +395,11 @@ void health_loop(int interval_ms) {
       u.port = b->port;
       int fd = -1;
       client::BlockingResponse r;
+      errno = 0;
       bool ok = client::blocking_request(u, &fd, "GET", "/api/health", "", "", 1000, &r) && r.status == 200;
+      const int err = errno;
       if (fd >= 0) ::close(fd);
+      if (!ok && (err == EMFILE || err == ENFILE || err == ENOBUFS || err == ENOMEM)) continue;  // local, not the backend
       bool was = b->healthy.exchange(ok);
       if (was != ok) fprintf(stderr, "rrproxy: backend %s:%d is %s\n", b->host.c_str(), b->port, ok ? "UP" : "DOWN");
     }

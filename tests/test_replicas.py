@@ -251,6 +251,7 @@ def test_proxy_backs_off_at_fd_limit():
     with ReplicaSet(1, threads_per_replica=1, supervise=False) as rs, RRProxy(rs.targets) as px:
         _exhaust_fds_then_recover(px.proc.pid, px.port, 48)
         assert "fd limit" in px.log()
+        assert "is DOWN" not in px.log()  # running out of local fds says nothing about a backend
 
 
 def test_server_backs_off_at_fd_limit(hola):
