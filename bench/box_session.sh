@@ -1,0 +1,77 @@
+#!/bin/bash
+# One gpurun session on the MI355X host. Replaces the per-session box_*.sh scripts.
+#
+#   gpurun -- 'bash bench/box_session.sh MODE OUT [ARGS...]'
+#
+# MODE
+#   final              smoke(), pytest -m gpu, the default bench (the driver's round-end tiers)
+#   bench ARGS...      one bench.py run with ARGS
+#   ab REPS "label|args" ...   interleaved A/B of bench.py variants, REPS rounds
+#   rehearsal [Ns]     the driver's own N>1 command line (default N = 2 4 8) inside the box's
+#                      CPU slice, plus --profile-dir stage profiles for locality attribution
+#   latency            BASELINE config 2 (1 connection) and the open-loop latency curve
+#   chain              two-hop chaining bench (loadgen -> hola A -> hola B)
+#   tracing            headline with a native Zipkin sink attached vs. without a collector
+#   soak MINUTES       mixed-load soak sampling RSS and FDs
+#
+# Every GPU-box step runs under its own `timeout -k`, steps are chained with &&, and the
+# script stops at the first failure (no retries).
+set -o pipefail
+MODE=${1:?mode}; OUT=${2:?out dir}; shift 2
+mkdir -p "$OUT"
+info() { python -m hola_amd info > "$OUT/info.txt" 2>&1 || true; }
+
+case "$MODE" in
+final)
+  info
+  timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 &&
+  timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+    > "$OUT/pytest_gpu.log" 2>&1 &&
+  timeout -k 10 300 python bench.py > "$OUT/bench_default.json" 2>> "$OUT/err.log"
+  ;;
+bench)
+  timeout -k 10 400 python bench.py "$@" > "$OUT/bench.json" 2>> "$OUT/err.log"
+  ;;
+ab)
+  REPS=${1:?reps}; shift
+  for rep in $(seq 1 "$REPS"); do
+    for v in "$@"; do
+      label=${v%%|*}; args=${v#*|}
+      timeout -k 10 240 python bench.py --steps 15 --warmup 4 $args > "$OUT/${label}_${rep}.json" \
+        2>> "$OUT/err.log" || exit 1
+      python3 -c "import json; d=json.load(open('$OUT/${label}_${rep}.json')); print('$label', $rep, d['value'], d['p50_ms'], d['p99_ms'], d['server_cpu_us_per_req'], d['loadgen_cpu_us_per_req'])" \
+        >> "$OUT/summary.txt"
+    done
+  done
+  cat "$OUT/summary.txt"
+  ;;
+rehearsal)
+  NS=${*:-2 4 8}
+  for n in $NS; do
+    timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$n" \
+      --master-addr 127.0.0.1 --master-port $((29600 + n)) bench.py --gpus "$n" --steps 8 --warmup 2 \
+      --profile-dir "$OUT/prof_n$n" > "$OUT/n$n.json" 2> "$OUT/err_n$n.log" || exit $?
+  done
+  ;;
+latency)
+  timeout -k 10 150 python bench.py --connections 1 --cores 2 --smt off --steps 15 --warmup 3 \
+    --reqs-per-conn 200000 > "$OUT/config2_c1.json" 2>> "$OUT/err.log" &&
+  timeout -k 10 200 python bench/latency_curve.py --duration 6 --out "$OUT/latency_curve.json" \
+    > "$OUT/latency_curve.log" 2>&1
+  ;;
+chain)
+  timeout -k 10 120 python bench/chain_bench.py --duration 10 --out "$OUT/chain.json" > "$OUT/chain.log" 2>&1
+  ;;
+tracing)
+  timeout -k 10 300 python bench.py --steps 15 --warmup 3 > "$OUT/no_collector.json" 2>> "$OUT/err.log" &&
+  timeout -k 10 300 python bench.py --steps 15 --warmup 3 --zipkin-sink > "$OUT/sink.json" 2>> "$OUT/err.log"
+  ;;
+soak)
+  MIN=${1:-5}
+  timeout -k 10 $((MIN * 60 + 150)) python -u bench/soak.py --minutes "$MIN" --sample-s 30 \
+    --out "$OUT/soak.json" > "$OUT/soak.log" 2>&1
+  ;;
+*)
+  echo "unknown mode $MODE" >&2; exit 2
+  ;;
+esac
