@@ -2,8 +2,9 @@
 
 * :class:`FakeAloha`  — the `aloha` service hola chains to (AlohaService.java:25). Its mode can
   be switched at runtime: ``ok`` / ``slow`` / ``error`` (HTTP 500) / ``garbage`` (invalid
-  JSON) / ``chunked`` / ``chunked_lf`` (chunk lines ended by a bare LF) / ``close`` (drop the connection). Records every request's headers so
-  tests can check B3 propagation.
+  JSON) / ``chunked`` / ``chunked_lf`` (chunk lines ended by a bare LF) / ``close`` (drop the
+  connection) / ``unavailable`` (HTTP 503 with ``Retry-After: <retry_after>``). Records every
+  request's headers so tests can check B3 propagation.
 * :class:`FakeZipkin` — a span collector recording POST /api/v1/spans and /api/v2/spans.
 """
 from __future__ import annotations
@@ -72,12 +73,16 @@ class _AlohaHandler(BaseHTTPRequestHandler):
             body, status = b"not found", 404
         elif mode == "error":
             body, status = b"boom", 500
+        elif mode == "unavailable":  # 503 + Retry-After: Feign's ErrorDecoder makes it retryable
+            body, status = b"busy", 503
         elif mode == "garbage":
             body, status = b"{not json", 200
         else:
             body, status = json.dumps(payload).encode(), 200
         self.send_response(status)
         self.send_header("Content-Type", "application/json")
+        if mode == "unavailable":
+            self.send_header("Retry-After", owner.retry_after)
         if mode in ("chunked", "chunked_lf"):
             eol = b"\r\n" if mode == "chunked" else b"\n"  # bare LF: tolerated framing (RFC 9112 §2.2)
             self.send_header("Transfer-Encoding", "chunked")
@@ -98,6 +103,7 @@ class FakeAloha(_Base):
         self.requests: list[dict] = []
         self.mode = mode
         self.delay_s = delay_s
+        self.retry_after = "0"  # Retry-After value sent in mode "unavailable"
         self.payload = payload if payload is not None else ["Aloha mai aloha-1", "Bonjour de bonjour-1"]
         super().__init__(_AlohaHandler)
 

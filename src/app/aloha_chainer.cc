@@ -1,6 +1,8 @@
 #include "app/aloha_chainer.h"
 
 #include <algorithm>
+#include <cmath>
+#include <cstdio>
 
 #include "core/clock.h"
 
@@ -14,19 +16,47 @@ namespace hola::app {
 using resilience::Command;
 using resilience::Event;
 
+int64_t RetryPolicy::backoff_ms(int attempt) const {
+  // Retryer.Default.nextMaxInterval(): (long) (period * Math.pow(1.5, attempt - 1)) with the
+  // retryer's counter already post-incremented, i.e. 1.5^attempt here.
+  const double v = double(period_ms) * std::pow(1.5, double(attempt));
+  return v >= double(max_period_ms) ? int64_t(max_period_ms) : int64_t(v);
+}
+
+bool parse_retry_policy(const std::string& s, RetryPolicy* out) {
+  if (s == "default") {
+    *out = RetryPolicy();
+    return true;
+  }
+  if (s == "off" || s == "never") {
+    *out = RetryPolicy();
+    out->max_attempts = 1;
+    return true;
+  }
+  int p = 0, m = 0, n = 0;
+  char tail = 0;
+  if (sscanf(s.c_str(), "%d,%d,%d%c", &p, &m, &n, &tail) != 3 || p < 0 || m < 0 || n < 1) return false;
+  out->period_ms = p;
+  out->max_period_ms = m;
+  out->max_attempts = n;
+  return true;
+}
+
 AlohaChainer::AlohaChainer(AlohaOptions o, resilience::Settings s, int num_workers, tracing::Tracer* tracer,
                            const Clock& clock)
     : o_(std::move(o)), tracer_(tracer), clock_(clock) {
   url_ok_ = client::parse_url(o_.url, &target_);
   if (!url_ok_) LOG_ERROR("aloha url '%s' is not an http:// URL; every call will fall back", o_.url.c_str());
   full_url_ = "http://" + target_.host + ":" + std::to_string(target_.port) + target_.base_path + o_.path;
-  // HystrixFeign keys: command = Feign configKey, group (and pool) = target name (the URL).
+  // HystrixFeign keys: command = o_.command_key, group (and pool) = target name (the URL).
   cmd_ = std::make_unique<Command>(o_.command_key, o_.url, o_.url, s, clock_);
   timeout_ms_.store(s.timeout_enabled ? s.timeout_ms : 0);
   if (url_ok_) addr_ = std::make_unique<client::AddressCache>(target_.host, target_.port);
   pools_.resize(size_t(num_workers));
   calls_.resize(size_t(num_workers));
   req_path_ = target_.base_path + o_.path;
+  // feign.Logger.methodTag(): '[' + configKey up to '(' + "] ".
+  log_tag_ = "[" + o_.config_key.substr(0, o_.config_key.find('(')) + "] ";
 }
 
 AlohaChainer::~AlohaChainer() { stop(); }
@@ -54,10 +84,15 @@ client::ClientPool& AlohaChainer::pool(http::Worker& w) {
 struct AlohaChainer::Call {
   uint32_t gen = 0;
   bool live = false;
-  uint64_t req_id = 0;
-  int64_t start_ms = 0;
-  int64_t start_us = 0;
-  tracing::SpanContext ctx;
+  uint64_t req_id = 0;     // client request of the execution in flight (0 = none)
+  bool inflight = false;   // an HTTP execution is outstanding (not sleeping between retries)
+  int attempts = 0;        // HTTP executions started (Feign retries included)
+  int64_t start_ms = 0;    // command start (Hystrix latency, timeout)
+  int64_t attempt_ms = 0;  // start of the current execution (Feign's "(Nms)")
+  int64_t start_us = 0;    // wall clock of the current execution (client span)
+  tracing::SpanContext parent;
+  bool has_parent = false;
+  tracing::SpanContext ctx;  // client span of the current execution
   bool traced = false;
   std::function<void(const ChainResult&)> cb;
 };
@@ -96,7 +131,10 @@ uint32_t AlohaChainer::acquire(WorkerCalls& wc) {
   Call& c = *wc.slots[s];
   c.live = true;
   c.req_id = 0;
+  c.inflight = false;
+  c.attempts = 0;
   c.traced = false;
+  c.has_parent = false;
   c.ctx = tracing::SpanContext();
   return s;
 }
@@ -153,23 +191,14 @@ void AlohaChainer::call(http::Worker& w, const tracing::SpanContext* parent,
   const uint32_t gen = c.gen;
   c.cb = std::move(done);
   c.start_ms = start_ms;
-  std::string headers;
   if (tracer_ && tracer_->enabled() && parent && parent->sampled) {
-    c.ctx = tracer_->new_child(w.index(), *parent);
-    c.traced = true;
-    tracing::inject(c.ctx, &headers);
+    c.parent = *parent;
+    c.has_parent = true;
   }
-  c.start_us = wall_us();
-  if (o_.feign_log_basic) LOG_INFO("[%s] ---> GET %s HTTP/1.1", o_.command_key.c_str(), full_url_.c_str());
-
-  const int worker_index = w.index();
-  client::ClientPool& p = pool(w);
-  const uint64_t id = p.get(req_path_, headers, [this, &wc, slot, gen, worker_index](client::ClientResult&& r) {
-    on_response(wc, slot, gen, worker_index, std::move(r));
-  });
+  execute(w, wc, slot, gen);
   if (dead(wc, slot, gen)) return;  // answered (or failed) synchronously
-  c.req_id = id;
 
+  // One Hystrix execution timeout covers every Feign attempt and the sleeps between them.
   const int timeout_ms = timeout_ms_.load(std::memory_order_relaxed);
   if (timeout_ms <= 0) return;
   const WorkerCalls::Pending e{mono_ms() + timeout_ms, slot, gen};
@@ -181,38 +210,91 @@ void AlohaChainer::call(http::Worker& w, const tracing::SpanContext* parent,
                                [](int64_t d, const WorkerCalls::Pending& x) { return d < x.deadline_ms; });
     wc.fifo.insert(it, e);
   }
-  arm(w.loop(), wc, p, worker_index);
+  arm(w.loop(), wc, pool(w), w.index());
 }
 
-void AlohaChainer::on_response(WorkerCalls& wc, uint32_t slot, uint32_t gen, int worker_index,
+// One HTTP execution of the Feign method (SynchronousMethodHandler.executeAndDecode).
+void AlohaChainer::execute(http::Worker& w, WorkerCalls& wc, uint32_t slot, uint32_t gen) {
+  Call& c = *wc.slots[slot];
+  ++c.attempts;
+  c.inflight = true;
+  c.req_id = 0;
+  c.traced = false;
+  std::string headers;
+  if (c.has_parent && tracer_) {
+    // Brave's HttpClient interceptors open a client span per executed request.
+    c.ctx = tracer_->new_child(w.index(), c.parent);
+    c.traced = true;
+    tracing::inject(c.ctx, &headers);
+  }
+  c.start_us = wall_us();
+  c.attempt_ms = clock_.now_ms();
+  if (o_.feign_log_basic) Logger::instance().raw("%s---> GET %s HTTP/1.1", log_tag_.c_str(), full_url_.c_str());
+  http::Worker* wp = &w;
+  const uint64_t id = pool(w).get(req_path_, headers, [this, wp, &wc, slot, gen](client::ClientResult&& r) {
+    on_response(*wp, wc, slot, gen, std::move(r));
+  });
+  if (!dead(wc, slot, gen) && c.inflight) c.req_id = id;
+}
+
+void AlohaChainer::on_response(http::Worker& w, WorkerCalls& wc, uint32_t slot, uint32_t gen,
                                client::ClientResult&& r) {
   if (dead(wc, slot, gen)) return;
   Call& c = *wc.slots[slot];
+  c.inflight = false;
+  c.req_id = 0;
   Command* cmd = cmd_.get();
-  const int64_t elapsed = clock_.now_ms() - c.start_ms;
+  const int64_t now = clock_.now_ms();
+  if (o_.feign_log_basic) {
+    // Feign Logger BASIC: logAndRebufferResponse / logIOException (r.error is "Class: msg").
+    if (r.ok)
+      Logger::instance().raw("%s<--- HTTP/1.1 %d%s%s (%lldms)", log_tag_.c_str(), r.status,
+                             r.reason.empty() ? "" : " ", r.reason.c_str(), (long long)(now - c.attempt_ms));
+    else
+      Logger::instance().raw("%s<--- ERROR %s (%lldms)", log_tag_.c_str(), r.error.c_str(),
+                             (long long)(now - c.attempt_ms));
+  }
   ChainResult res;
   std::string err;
-  bool success = false;
+  bool success = false, retryable = false;
+  int64_t retry_after = 0;
+  bool has_retry_after = false;
   if (r.ok && r.status >= 200 && r.status < 300) {
     std::vector<std::optional<std::string>> items;
     if (json::decode_string_list(r.body, &items, &err)) {
       success = true;
       res.items = std::move(items);
     } else {
-      err = "DecodeException: " + err;
+      err = "DecodeException: " + err;  // a FeignException: never retried
     }
   } else if (r.ok) {
-    err = "FeignException: status " + std::to_string(r.status) + " reading AlohaService#aloha()";
+    // ErrorDecoder.Default: FeignException, retryable only with a Retry-After header.
+    err = "FeignException: status " + std::to_string(r.status) + " reading " + o_.config_key;
+    retryable = has_retry_after = r.has_retry_after;
+    retry_after = r.retry_after_ms;
   } else {
-    err = r.error;
-  }
-  if (o_.feign_log_basic) {
-    if (r.ok) LOG_INFO("[%s] <--- HTTP/1.1 %d (%lldms)", o_.command_key.c_str(), r.status, (long long)elapsed);
-    else LOG_INFO("[%s] <--- ERROR %s (%lldms)", o_.command_key.c_str(), r.error.c_str(), (long long)elapsed);
+    err = r.error;  // IOException before a response: RetryableException
+    retryable = r.retryable;
   }
   if (c.traced && tracer_)
-    tracer_->record_client(worker_index, c.ctx, c.start_us, wall_us(), full_url_, r.ok ? r.status : 0,
+    tracer_->record_client(w.index(), c.ctx, c.start_us, wall_us(), full_url_, r.ok ? r.status : 0,
                            success ? std::string_view() : std::string_view(err));
+  if (!success && retryable && c.attempts < o_.retry.max_attempts) {
+    // Retryer.Default.continueOrPropagate: sleep, then "---> RETRYING" and execute again.
+    // The sleep is a loop timer; if the Hystrix timeout fires first, the slot is released
+    // and the timer finds the call dead.
+    int64_t sleep_ms = has_retry_after ? std::min<int64_t>(retry_after, o_.retry.max_period_ms)
+                                       : o_.retry.backoff_ms(c.attempts);
+    if (sleep_ms < 0) sleep_ms = 0;
+    http::Worker* wp = &w;
+    w.loop().add_timer(sleep_ms, [this, wp, &wc, slot, gen] {
+      if (dead(wc, slot, gen)) return;
+      if (o_.feign_log_basic) Logger::instance().raw("%s---> RETRYING", log_tag_.c_str());
+      execute(*wp, wc, slot, gen);
+    });
+    return;
+  }
+  const int64_t elapsed = now - c.start_ms;
   if (success) {
     cmd->complete(Event::kSuccess, elapsed, false, clock_.now_ms() - c.start_ms);
   } else {
@@ -220,7 +302,11 @@ void AlohaChainer::on_response(WorkerCalls& wc, uint32_t slot, uint32_t gen, int
     res = fallback_result("failure");
     res.reason = err;
   }
-  auto cb = std::move(c.cb);
+  finish(wc, slot, res);
+}
+
+void AlohaChainer::finish(WorkerCalls& wc, uint32_t slot, const ChainResult& res) {
+  auto cb = std::move(wc.slots[slot]->cb);
   release(wc, slot);  // before the callback: it may start the next call on this worker
   cb(res);
 }
@@ -252,15 +338,17 @@ void AlohaChainer::expire(EventLoop& loop, WorkerCalls& wc, client::ClientPool& 
     if (e.deadline_ms > now) break;
     wc.fifo.pop_front();
     Call& c = *wc.slots[e.slot];
-    p.cancel(c.req_id);  // abandon the socket
+    if (c.inflight) {
+      p.cancel(c.req_id);  // abandon the socket
+      if (c.traced && tracer_)
+        tracer_->record_client(worker_index, c.ctx, c.start_us, wall_us(), full_url_, 0, "timeout");
+    }
     const int64_t elapsed = clock_.now_ms() - c.start_ms;
-    if (o_.feign_log_basic)
-      LOG_INFO("[%s] <--- ERROR HystrixTimeoutException (%lldms)", o_.command_key.c_str(), (long long)elapsed);
-    if (c.traced && tracer_) tracer_->record_client(worker_index, c.ctx, c.start_us, wall_us(), full_url_, 0, "timeout");
+    // Feign itself logs nothing when Hystrix times the command out.
+    LOG_DEBUG("%s HystrixTimeoutException after %lld ms (%d attempt(s))", log_tag_.c_str(), (long long)elapsed,
+              c.attempts);
     cmd_->complete(Event::kTimeout, elapsed, true, elapsed);
-    auto cb = std::move(c.cb);
-    release(wc, e.slot);
-    cb(fallback_result("timeout"));
+    finish(wc, e.slot, fallback_result("timeout"));
   }
   arm(loop, wc, p, worker_index);
 }

@@ -2,9 +2,14 @@
 // HolaResource.getNextService() (HolaResource.java:94-113) re-designed for an event loop.
 //
 //   Feign target      http://aloha:8080/ + GET /api/aloha-chaining  (AlohaService.java:25)
-//   Hystrix command   "AlohaService#aloha()", group = target URL     [lib-default keying]
+//   Hystrix command   "aloha" (method name), group = pool = target URL [lib-default keying,
+//                     feign-hystrix 8.15.1 HystrixInvocationHandler; see docs/PARITY.md]
+//   retries           Feign's default Retryer.Default(100 ms, 1 s, 5): IO errors and
+//                     Retry-After responses re-execute with 1.5x backoff, inside the Hystrix
+//                     timeout (HolaResource.java:104-112 configures no .retryer())
 //   fallback          ["Aloha response (fallback)"]                  (HolaResource.java:111-112)
-//   tracing           client span child of the server span + B3 headers (HolaResource.java:97-108)
+//   tracing           one client span per HTTP attempt, child of the server span, + B3
+//                     headers (HolaResource.java:97-108)
 //   logging           Feign Logger.ErrorLogger at Level.BASIC        (HolaResource.java:109)
 #pragma once
 #include <atomic>
@@ -23,11 +28,27 @@ class Tracer;
 
 namespace hola::app {
 
+// feign.Retryer.Default: after the n-th failed execution (n = 1, 2, ...) it sleeps
+// min(period * 1.5^n, max_period) and executes again, up to max_attempts executions; a
+// Retry-After date replaces the backoff (capped at max_period; in the past = no sleep).
+struct RetryPolicy {
+  int period_ms = 100;
+  int max_period_ms = 1000;
+  int max_attempts = 5;  // 1 = never retry (Retryer.NEVER_RETRY)
+  // Sleep before execution attempt `attempt` + 1, given `attempt` executions have failed.
+  int64_t backoff_ms(int attempt) const;
+};
+bool parse_retry_policy(const std::string& s, RetryPolicy* out);  // "default" | "off" | "P,MAX,N"
+
 struct AlohaOptions {
   std::string url = "http://aloha:8080/";  // HolaResource.java:103
   std::string path = "api/aloha-chaining";  // AlohaService.java:25
   bool feign_log_basic = true;
-  std::string command_key = "AlohaService#aloha()";
+  // Feign.configKey(AlohaService.class, aloha): the BASIC log tag ("[AlohaService#aloha] ")
+  // and the FeignException message.
+  std::string config_key = "AlohaService#aloha()";
+  std::string command_key = "aloha";  // Hystrix command key (--hystrix-command-key)
+  RetryPolicy retry;
 };
 
 class AlohaChainer final : public Chainer {
@@ -57,7 +78,9 @@ class AlohaChainer final : public Chainer {
   uint32_t acquire(WorkerCalls& wc);
   static void release(WorkerCalls& wc, uint32_t slot);
   static bool dead(const WorkerCalls& wc, uint32_t slot, uint32_t gen);
-  void on_response(WorkerCalls& wc, uint32_t slot, uint32_t gen, int worker_index, client::ClientResult&& r);
+  void execute(http::Worker& w, WorkerCalls& wc, uint32_t slot, uint32_t gen);
+  void on_response(http::Worker& w, WorkerCalls& wc, uint32_t slot, uint32_t gen, client::ClientResult&& r);
+  void finish(WorkerCalls& wc, uint32_t slot, const ChainResult& res);
   void expire(EventLoop& loop, WorkerCalls& wc, client::ClientPool& p, int worker_index);
   void arm(EventLoop& loop, WorkerCalls& wc, client::ClientPool& p, int worker_index);
   AlohaOptions o_;
@@ -69,6 +92,7 @@ class AlohaChainer final : public Chainer {
   std::vector<std::unique_ptr<client::ClientPool>> pools_;
   std::vector<std::unique_ptr<WorkerCalls>> calls_;
   std::string req_path_;  // target base path + aloha path
+  std::string log_tag_;   // "[AlohaService#aloha] "
   tracing::Tracer* tracer_;
   const Clock& clock_;
   std::atomic<int> timeout_ms_{0};  // 0 = execution timeout disabled (read per call, lock-free)

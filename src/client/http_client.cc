@@ -8,6 +8,9 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
+
+#include "core/clock.h"
 
 #include "core/net.h"
 #include "http/parser.h"
@@ -65,6 +68,8 @@ bool AddressCache::get(sockaddr_storage* out, socklen_t* len, std::string* err) 
 
 // ---------------------------------------------------------------- connection
 
+constexpr int kTransportRetries = 3;  // DefaultHttpRequestRetryHandler(3, false)
+
 struct ClientPool::Conn final : EventLoop::Handler {
   enum State { kConnecting, kWriting, kReading, kIdle, kDead };
   ClientPool* pool = nullptr;
@@ -75,7 +80,9 @@ struct ClientPool::Conn final : EventLoop::Handler {
   std::string in;
   uint64_t id = 0;
   Callback cb;
-  bool reused = false;  // the request goes out unchanged in `out` (kept for the silent retry)
+  bool reused = false;  // went out on a kept-alive socket
+  int tries = 0;        // transport re-executions so far (DefaultHttpRequestRetryHandler)
+  bool head_ok = false;  // a complete, well-formed status line + header block has arrived
   uint32_t interest = 0;
 
   void set_interest(uint32_t ev) {
@@ -83,7 +90,8 @@ struct ClientPool::Conn final : EventLoop::Handler {
     interest = ev;
     pool->loop_.mod(fd, ev, this);
   }
-  void fail(const std::string& why);
+  // io = an I/O error (not a connect failure or a protocol error).
+  void fail(const std::string& why, bool io = true);
   void on_event(uint32_t ev) override;
   void do_write();
   void do_read();
@@ -91,23 +99,29 @@ struct ClientPool::Conn final : EventLoop::Handler {
   int try_parse(ClientResult* r, bool* keep, bool eof);
 };
 
-void ClientPool::Conn::fail(const std::string& why) {
-  // A kept-alive socket the server had already closed: retry once on a fresh connection.
-  if (reused && in.empty() && st != kConnecting) {
+void ClientPool::Conn::fail(const std::string& why, bool io) {
+  // Apache HttpClient's DefaultHttpRequestRetryHandler (the default of the HttpClientBuilder
+  // in HolaResource.java:98-102): an idempotent GET that hit an I/O error before its response
+  // head (a stale kept-alive socket, a reset, EOF with no response) is re-executed at once
+  // on a fresh connection, up to 3 times. Connect failures and protocol errors are not.
+  if (io && !head_ok && st != kConnecting && tries < kTransportRetries) {
     ClientPool* p = pool;
     uint64_t rid = id;
     Callback c = std::move(cb);
     std::string r = std::move(out);
+    const int t = tries + 1;
     p->active_.erase(rid);
     p->destroy(this);
     auto* fresh = new Conn();
     fresh->pool = p;
+    fresh->tries = t;
     p->start_on(fresh, rid, std::move(r), std::move(c), false);
     return;
   }
   ClientResult res;
   res.ok = false;
   res.error = why;
+  res.retryable = !head_ok;
   pool->finish(this, std::move(res), false);
 }
 
@@ -124,7 +138,7 @@ void ClientPool::Conn::on_event(uint32_t ev) {
     socklen_t sl = sizeof soerr;
     getsockopt(fd, SOL_SOCKET, SO_ERROR, &soerr, &sl);
     if (soerr != 0 || (ev & (EPOLLERR | EPOLLHUP))) {
-      fail(std::string("ConnectException: ") + strerror(soerr ? soerr : ECONNREFUSED));
+      fail(pool->connect_error(soerr ? soerr : ECONNREFUSED), false);
       return;
     }
     st = kWriting;
@@ -166,6 +180,9 @@ int ClientPool::Conn::try_parse(ClientResult* r, bool* keep, bool eof) {
   }
   if (status < 100) return -1;
   bool http10 = head.substr(5, 3) == "1.0";
+  const size_t eol = std::min(head.find("\r\n"), head.size());
+  r->reason.assign(eol > 13 && head[12] == ' ' ? head.substr(13, eol - 13) : std::string_view());
+  r->has_retry_after = false;
   int64_t cl = -1;
   bool chunked = false, close = http10;
   size_t p = head.find("\r\n");
@@ -188,11 +205,14 @@ int ClientPool::Conn::try_parse(ClientResult* r, bool* keep, bool eof) {
       else if (http::iequals(k, "connection")) {
         if (http::iequals(v, "close")) close = true;
         else if (http::iequals(v, "keep-alive")) close = false;
+      } else if (http::iequals(k, "retry-after")) {
+        r->has_retry_after = parse_retry_after(v, wall_us() / 1000, &r->retry_after_ms);
       }
     }
     p = n;
   }
   size_t body = he + 4;
+  head_ok = true;
   if (status == 204 || status == 304 || (status >= 100 && status < 200)) {
     r->status = status;
     *keep = !close;
@@ -232,7 +252,7 @@ void ClientPool::Conn::do_read() {
     bool eof = false;
     if (n > 0) {
       in.append(buf, size_t(n));
-      reused = false;  // the server answered: no silent retry from here on
+      reused = false;
     } else if (n == 0) {
       eof = true;
     } else {
@@ -245,7 +265,7 @@ void ClientPool::Conn::do_read() {
     bool keep = false;
     int rc = try_parse(&r, &keep, eof);
     if (rc < 0) {
-      fail("ClientProtocolException: malformed response");
+      fail("ClientProtocolException: malformed response", false);
       return;
     }
     if (rc == 1) {
@@ -262,6 +282,36 @@ void ClientPool::Conn::do_read() {
 }
 
 // ---------------------------------------------------------------- pool
+
+bool parse_retry_after(std::string_view v, int64_t now_ms, int64_t* out_ms) {
+  while (!v.empty() && (v.back() == ' ' || v.back() == '\t')) v.remove_suffix(1);
+  if (v.empty()) return false;
+  bool digits = true;
+  int64_t secs = 0;
+  for (char d : v) {
+    if (d < '0' || d > '9') {
+      digits = false;
+      break;
+    }
+    secs = std::min<int64_t>(secs * 10 + (d - '0'), int64_t(1) << 40);
+  }
+  if (digits) {
+    *out_ms = secs * 1000;
+    return true;
+  }
+  // RFC 1123 date, e.g. "Wed, 21 Oct 2015 07:28:00 GMT" (Feign's RetryAfterDecoder format).
+  std::string s(v);
+  tm t{};
+  const char* end = strptime(s.c_str(), "%a, %d %b %Y %H:%M:%S GMT", &t);
+  if (!end || *end) return false;
+  *out_ms = int64_t(timegm(&t)) * 1000 - now_ms;
+  return true;
+}
+
+std::string ClientPool::connect_error(int err) const {
+  // Apache HttpClient 4.5 wraps a refused/failed connect as HttpHostConnectException.
+  return "HttpHostConnectException: Connect to " + target_.host + ":" + std::to_string(target_.port) + " failed: " + strerror(err);
+}
 
 ClientPool::ClientPool(EventLoop& loop, Url target, AddressCache* addr, size_t max_idle)
     : loop_(loop), target_(std::move(target)), addr_(addr), max_idle_(max_idle) {
@@ -318,6 +368,7 @@ void ClientPool::start_on(Conn* c, uint64_t id, std::string req, Callback cb, bo
   c->off = 0;
   c->in.clear();
   c->reused = reused;
+  c->head_ok = false;
   active_[id] = c;
   if (reused) {
     c->st = Conn::kWriting;
@@ -335,6 +386,7 @@ void ClientPool::start_on(Conn* c, uint64_t id, std::string req, Callback cb, bo
       if (it == active_.end()) return;
       ClientResult r;
       r.error = err;
+      r.retryable = true;  // UnknownHostException is an IOException
       finish(it->second, std::move(r), false);
     });
     return;
@@ -342,13 +394,14 @@ void ClientPool::start_on(Conn* c, uint64_t id, std::string req, Callback cb, bo
   bool inprog = false;
   c->fd = connect_nonblocking(ss, len, &inprog);
   if (c->fd < 0) {
-    std::string e = std::string("ConnectException: ") + strerror(errno);
+    std::string e = connect_error(errno);
     c->st = Conn::kDead;
     loop_.add_timer(0, [this, id, e] {
       auto it = active_.find(id);
       if (it == active_.end()) return;
       ClientResult r;
       r.error = e;
+      r.retryable = true;
       finish(it->second, std::move(r), false);
     });
     return;

@@ -12,6 +12,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <string_view>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -48,9 +49,24 @@ class AddressCache {
 struct ClientResult {
   bool ok = false;      // a complete HTTP response was received
   int status = 0;
+  std::string reason;   // reason phrase of the status line ("OK")
   std::string body;
-  std::string error;    // network error description when !ok
+  std::string error;    // "<ExceptionClass>: <message>" when !ok
+  // !ok only: the failure happened before a complete response head arrived (connect, write,
+  // or reading the status line/headers). Apache HttpClient throws an IOException from
+  // execute() there, which Feign turns into a RetryableException (SynchronousMethodHandler
+  // errorExecuting); a failure while reading the body is a non-retryable FeignException.
+  bool retryable = false;
+  // ok only: a parseable Retry-After header, as milliseconds from now (negative for a date
+  // in the past). Feign's ErrorDecoder.Default makes any non-2xx response carrying it a
+  // RetryableException.
+  bool has_retry_after = false;
+  int64_t retry_after_ms = 0;
 };
+
+// Retry-After value (delta-seconds or RFC 1123 date) as milliseconds from now_ms (wall
+// clock, negative for a date in the past); false when it cannot be parsed.
+bool parse_retry_after(std::string_view v, int64_t now_ms, int64_t* out_ms);
 
 class ClientPool {
  public:
@@ -72,6 +88,7 @@ class ClientPool {
   void finish(Conn* c, ClientResult&& r, bool reusable);
   void destroy(Conn* c);
   std::string build_request(const std::string& path, const std::string& extra) const;
+  std::string connect_error(int err) const;
 
   EventLoop& loop_;
   Url target_;

@@ -58,13 +58,30 @@ void Logger::vlog(LogLevel l, const char* fmt, va_list ap) {
   int m = snprintf(line, sizeof line, "%04d-%02d-%02dT%02d:%02d:%02d.%03dZ %-5s [%d] %.*s\n",
                    t.tm_year + 1900, t.tm_mon + 1, t.tm_mday, t.tm_hour, t.tm_min, t.tm_sec,
                    int(us / 1000 % 1000), level_name(l), int(getpid()), n, msg);
+  enqueue(line, size_t(m < int(sizeof line) ? m : sizeof line - 1));
+}
+
+void Logger::raw(const char* fmt, ...) {
+  if (level() == LogLevel::kOff) return;
+  char line[2048];
+  va_list ap;
+  va_start(ap, fmt);
+  int n = vsnprintf(line, sizeof line - 1, fmt, ap);
+  va_end(ap);
+  if (n < 0) return;
+  if (n > int(sizeof line) - 2) n = int(sizeof line) - 2;
+  line[n++] = '\n';
+  enqueue(line, size_t(n));
+}
+
+void Logger::enqueue(const char* line, size_t n) {
   {
     std::lock_guard<std::mutex> g(mu_);
     if (q_.size() >= kMaxQueued) {
       dropped_.fetch_add(1, std::memory_order_relaxed);
       return;
     }
-    q_.emplace_back(line, size_t(m < int(sizeof line) ? m : sizeof line - 1));
+    q_.emplace_back(line, n);
     ++enqueued_;
   }
   cv_.notify_one();

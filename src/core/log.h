@@ -23,6 +23,11 @@ class Logger {
   bool enabled(LogLevel l) const { return int(l) >= level_.load(std::memory_order_relaxed); }
   void log(LogLevel l, const char* fmt, ...) __attribute__((format(printf, 3, 4)));
   void vlog(LogLevel l, const char* fmt, va_list ap);
+  // One line exactly as formatted (a newline is appended), without the timestamp/level
+  // prefix: for output whose format belongs to the reference's libraries, e.g. Feign's
+  // Logger.ErrorLogger, which System.err.printf()s its lines (HolaResource.java:109).
+  // Suppressed only when the level is off.
+  void raw(const char* fmt, ...) __attribute__((format(printf, 2, 3)));
   // Blocks until every queued line has been written.
   void flush();
   uint64_t dropped() const { return dropped_.load(std::memory_order_relaxed); }
@@ -31,6 +36,7 @@ class Logger {
  private:
   Logger();
   void run();
+  void enqueue(const char* line, size_t n);
   std::atomic<int> level_{int(LogLevel::kInfo)};
   std::mutex mu_;
   std::condition_variable cv_, flushed_;

@@ -266,6 +266,7 @@ void Connection::flush() {
     }
     WorkerStats::bump(st.bytes_out, uint64_t(w));
     out_off_ += size_t(w);
+    sent_total_ += uint64_t(w);
   }
   out_.clear();
   out_off_ = 0;

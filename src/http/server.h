@@ -78,6 +78,10 @@ class Connection final : public EventLoop::Handler {
   // No response owed and nothing queued to send (a partial request may be buffered).
   bool quiet() const { return !parked_ && out_.size() == out_off_; }
   int64_t last_active_ms() const { return last_active_ms_; }
+  // Bytes queued for this connection that the socket has not taken yet.
+  size_t unsent() const { return out_.size() - out_off_; }
+  // Bytes the socket has taken over the connection's life.
+  uint64_t bytes_sent() const { return sent_total_; }
 
  private:
   void on_readable(bool peer_closed);
@@ -94,6 +98,7 @@ class Connection final : public EventLoop::Handler {
   std::string in_;   // unconsumed input carried across reads
   std::string out_;  // unsent output
   size_t out_off_ = 0;
+  uint64_t sent_total_ = 0;
   bool closed_ = false;
   bool parked_ = false;
   bool streaming_ = false;

@@ -51,7 +51,13 @@ void usage() {
           "  --aloha-url URL          downstream service (default http://aloha:8080/)\n"
           "  --aloha-path PATH        downstream path (default api/aloha-chaining)\n"
           "  --feign-log basic|none   outbound call logging (default basic)\n"
+          "  --feign-retry default|off|P,MAX,N   Feign Retryer on IO errors (default: Retryer.Default\n"
+          "                           = 100 ms period, 1000 ms max period, 5 attempts)\n"
+          "  --hystrix-command-key method|configkey|KEY   Hystrix command key of the aloha call\n"
+          "                           (default method = \"aloha\", feign-hystrix 8.x; configkey =\n"
+          "                           \"AlohaService#aloha()\", feign-hystrix 9.x SetterFactory.Default)\n"
           "  --hystrix-stream-max N   max /hystrix.stream subscribers (default 5)\n"
+          "  --hystrix-stream-stall-ms N   close a subscriber that has not read for N ms (default 30000)\n"
           "  --hystrix-timeout-ms N | --hystrix-request-volume N | --hystrix-error-pct N |\n"
           "  --hystrix-sleep-window-ms N | --hystrix-pool-size N\n"
           "                           shorthands for -Dhystrix.command.default.* / threadpool.default.*\n"
@@ -96,6 +102,7 @@ int main(int argc, char** argv) {
   const char* hn = getenv("HOSTNAME");
   if (hn) ao.hostname = hn;  // HolaResource.java:57 getOrDefault("HOSTNAME", "unknown")
   int threads = 0, drain_ms = 5000, stream_max = 5;
+  int64_t stream_stall_ms = 30000;
   std::string cpu_list, port_file, profile_out;
   bool auto_pin = true;
   bool no_tracing = false;
@@ -141,7 +148,19 @@ int main(int argc, char** argv) {
       while (!alo.path.empty() && alo.path.front() == '/') alo.path.erase(0, 1);
     }
     else if (a == "--feign-log") alo.feign_log_basic = val("--feign-log") == "basic";
+    else if (a == "--feign-retry") {
+      if (!app::parse_retry_policy(val("--feign-retry"), &alo.retry)) {
+        fprintf(stderr, "hola: --feign-retry default|off|PERIOD_MS,MAX_PERIOD_MS,MAX_ATTEMPTS\n");
+        return 2;
+      }
+    } else if (a == "--hystrix-command-key") {
+      std::string k = val("--hystrix-command-key");
+      if (k == "method") alo.command_key = "aloha";
+      else if (k == "configkey") alo.command_key = alo.config_key;
+      else if (!k.empty()) alo.command_key = k;
+    }
     else if (a == "--hystrix-stream-max") stream_max = atoi(val("--hystrix-stream-max").c_str());
+    else if (a == "--hystrix-stream-stall-ms") stream_stall_ms = atoll(val("--hystrix-stream-stall-ms").c_str());
     else if (a == "--config-poll-ms") mo.poll_ms = atoi(val("--config-poll-ms").c_str());
     else if (a == "--drain-ms") drain_ms = atoi(val("--drain-ms").c_str());
     else if (a == "--port-file") port_file = val("--port-file");
@@ -231,12 +250,14 @@ int main(int argc, char** argv) {
   app::AlohaChainer chainer(alo, hystrix_settings({}), threads, to.enabled ? &tracer : nullptr);
   app.set_chainer(&chainer);
   metrics::HystrixStream stream(stream_max);
+  stream.set_stall_close_ms(stream_stall_ms);
   stream.add_command(&chainer.command());
   app.set_hystrix_stream(&stream);
   metrics::Prometheus prom(threads, app::HolaApp::kNumRoutes);
   prom.set_tracer(to.enabled ? &tracer : nullptr);
   prom.set_command(&chainer.command());
   prom.set_config_reloads([&cfg] { return cfg.reloads(); });
+  prom.set_stream(&stream);
   app.set_prometheus(&prom);
 
   cfg.start([&](const config::Snapshot& s) {

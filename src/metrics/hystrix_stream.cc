@@ -1,10 +1,13 @@
 #include "metrics/hystrix_stream.h"
 
+#include <sys/socket.h>
+
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
 
+#include "core/clock.h"
 #include "http/server.h"
 #include "json/json.h"
 
@@ -141,6 +144,8 @@ struct Sub {
   bool alive = true;
   bool chunked = true;
   int delay_ms = 500;
+  int64_t stalled_since_ms = 0;  // first tick with bytes pending and no progress (0 = none)
+  uint64_t last_sent = 0;        // conn->bytes_sent() at the previous tick
 };
 
 std::string chunk(const std::string& data, bool chunked) {
@@ -161,7 +166,28 @@ struct HystrixStream::Ticker : std::enable_shared_from_this<HystrixStream::Ticke
       conn->release();  // balances the hold() taken at subscribe time
       return;
     }
-    conn->send(chunk(stream->render_events(), sub->chunked));
+    // Hystrix's servlet writes block, so a subscriber that stops reading stalls only its own
+    // servlet thread. Here writes are queued: past kMaxBacklog unsent bytes the frame is
+    // skipped (memory stays bounded), and a subscriber whose socket has taken no bytes for
+    // stall_close_ms while some are pending is closed, so that it does not hold one of the
+    // max_connections slots forever.
+    const uint64_t sent = conn->bytes_sent();
+    if (conn->unsent() > 0 && sent == sub->last_sent) {
+      const int64_t now = mono_ms();
+      if (sub->stalled_since_ms == 0) {
+        sub->stalled_since_ms = now;
+      } else if (now - sub->stalled_since_ms >= stream->stall_close_ms_) {
+        stream->stalled_closed_.fetch_add(1, std::memory_order_relaxed);
+        conn->close();
+        conn->release();
+        return;
+      }
+    } else {
+      sub->stalled_since_ms = 0;
+    }
+    sub->last_sent = sent;
+    if (conn->unsent() > kMaxBacklog) stream->skipped_.fetch_add(1, std::memory_order_relaxed);
+    else conn->send(chunk(stream->render_events(), sub->chunked));
     auto self = shared_from_this();
     loop->add_timer(sub->delay_ms, [self] { self->fire(); });
   }
@@ -170,9 +196,9 @@ struct HystrixStream::Ticker : std::enable_shared_from_this<HystrixStream::Ticke
 void HystrixStream::subscribe(http::Connection& c, const http::Request& r) {
   if (subscribers_.fetch_add(1) >= max_connections_) {
     subscribers_.fetch_sub(1);
-    const char* msg = "MaxConcurrentConnections reached: 5";
+    const std::string msg = "MaxConcurrentConnections reached: " + std::to_string(max_connections_);
     std::string resp = "HTTP/1.1 503 Service Unavailable\r\nConnection: close\r\nContent-Type: text/plain\r\nContent-Length: " +
-                       std::to_string(strlen(msg)) + "\r\n\r\n" + msg;
+                       std::to_string(msg.size()) + "\r\n\r\n" + msg;
     c.send(resp);
     c.close_after_response();
     return;
@@ -190,6 +216,10 @@ void HystrixStream::subscribe(http::Connection& c, const http::Request& r) {
   std::string head = "HTTP/1.1 200 OK\r\nContent-Type: text/event-stream;charset=UTF-8\r\n"
                      "Cache-Control: no-cache, no-store, max-age=0, must-revalidate\r\nPragma: no-cache\r\n";
   head += sub->chunked ? "Transfer-Encoding: chunked\r\n\r\n" : "Connection: close\r\n\r\n";
+  // A fixed socket send buffer (no autotuning up to tcp_wmem's max, megabytes) bounds what
+  // the kernel holds for a subscriber that stops reading; kMaxBacklog bounds the rest.
+  const int sndbuf = int(kMaxBacklog);
+  setsockopt(c.fd(), SOL_SOCKET, SO_SNDBUF, &sndbuf, sizeof sndbuf);
   c.send(head);
   HystrixStream* self = this;
   c.hold();

@@ -23,6 +23,13 @@ class HystrixStream {
   void add_command(resilience::Command* c) { commands_.push_back(c); }
   void subscribe(http::Connection& c, const http::Request& r);
   int subscribers() const { return subscribers_.load(); }
+  // Frames not queued because the subscriber had stopped reading, and subscribers closed
+  // after staying stalled for stall_close_ms (default 30 s; hola --hystrix-stream-stall-ms).
+  uint64_t frames_skipped() const { return skipped_.load(std::memory_order_relaxed); }
+  uint64_t stalled_closed() const { return stalled_closed_.load(std::memory_order_relaxed); }
+  // A subscriber with more than this many bytes unsent gets no new frame.
+  static constexpr size_t kMaxBacklog = 64 * 1024;
+  void set_stall_close_ms(int64_t ms) { stall_close_ms_ = ms; }
   // One SSE payload (all commands + pools), exposed for tests.
   std::string render_events();
   static std::string command_json(const resilience::CommandSnapshot& s);
@@ -32,8 +39,10 @@ class HystrixStream {
   struct Ticker;
   int max_connections_;
   int default_delay_ms_;
+  int64_t stall_close_ms_ = 30000;
   std::vector<resilience::Command*> commands_;
   std::atomic<int> subscribers_{0};
+  std::atomic<uint64_t> skipped_{0}, stalled_closed_{0};
 };
 
 }  // namespace hola::metrics

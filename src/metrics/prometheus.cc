@@ -4,6 +4,7 @@
 
 #include "app/hola_app.h"
 #include "http/server.h"
+#include "metrics/hystrix_stream.h"
 #include "resilience/hystrix.h"
 #include "tracing/tracer.h"
 
@@ -92,6 +93,14 @@ std::string Prometheus::render(http::Server* server) const {
          (s.circuit_open ? "1" : "0") + "\n";
   }
   if (reloads_) o += "# TYPE hola_config_reloads_total counter\nhola_config_reloads_total " + std::to_string(reloads_()) + "\n";
+  if (stream_) {
+    o += "# TYPE hola_hystrix_stream_subscribers gauge\nhola_hystrix_stream_subscribers " +
+         std::to_string(stream_->subscribers()) + "\n";
+    o += "# TYPE hola_hystrix_stream_frames_skipped_total counter\nhola_hystrix_stream_frames_skipped_total " +
+         std::to_string(stream_->frames_skipped()) + "\n";
+    o += "# TYPE hola_hystrix_stream_stalled_closed_total counter\nhola_hystrix_stream_stalled_closed_total " +
+         std::to_string(stream_->stalled_closed()) + "\n";
+  }
   return o;
 }
 

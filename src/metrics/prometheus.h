@@ -23,6 +23,8 @@ class Command;
 
 namespace hola::metrics {
 
+class HystrixStream;
+
 class Prometheus {
  public:
   Prometheus(int num_workers, int num_routes);
@@ -46,6 +48,7 @@ class Prometheus {
   void set_tracer(tracing::Tracer* t) { tracer_ = t; }
   void set_command(resilience::Command* c) { cmd_ = c; }
   void set_config_reloads(std::function<uint64_t()> f) { reloads_ = std::move(f); }
+  void set_stream(const HystrixStream* s) { stream_ = s; }
   std::string render(http::Server* server) const;
 
  private:
@@ -65,6 +68,7 @@ class Prometheus {
   tracing::Tracer* tracer_ = nullptr;
   resilience::Command* cmd_ = nullptr;
   std::function<uint64_t()> reloads_;
+  const HystrixStream* stream_ = nullptr;
 };
 
 }  // namespace hola::metrics

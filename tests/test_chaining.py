@@ -2,6 +2,7 @@
 back to ["Aloha response (fallback)"] (HolaResource.java:111-112), the 600 ms timeout
 (config.properties:17), the circuit breaker (config.properties:19) and the bulkhead."""
 import json
+import re
 import socket
 import threading
 import time
@@ -48,23 +49,136 @@ def test_chunked_response(hola, aloha, mode):
         assert chain(s)[1:] == ["Aloha mai aloha-1", "Bonjour de bonjour-1"]
 
 
-@pytest.mark.parametrize("mode", ["error", "garbage", "close"])
-def test_failures_fall_back(hola, aloha, mode):
+def _events(s) -> dict:
+    """Rolling Hystrix event counts of the aloha command from /metrics."""
+    _, _, body = s.get("/metrics")
+    out = {}
+    for line in body.decode().splitlines():
+        if line.startswith("hola_hystrix_events_total{"):
+            out[line.split('event="')[1].split('"')[0]] = int(float(line.rsplit(" ", 1)[1]))
+    return out
+
+
+def _wait_log(s, needle: str, count: int, timeout: float = 3.0) -> str:
+    deadline = time.monotonic() + timeout
+    while True:
+        log = s.log()
+        if log.count(needle) >= count or time.monotonic() > deadline:
+            return log
+        time.sleep(0.05)
+
+
+@pytest.mark.parametrize("mode", ["error", "garbage"])
+def test_response_failures_fall_back_fast_without_retry(hola, aloha, mode):
+    """A 500 (FeignException) or an undecodable body (DecodeException) is not retryable:
+    one HTTP execution, FAILURE at once."""
     aloha.set_mode(mode)
     s = hola(args=["--aloha-url", aloha.url])
+    t0 = time.monotonic()
     assert chain(s) == ["Hola de testhost", FALLBACK]
+    assert time.monotonic() - t0 < 0.3
+    assert len(aloha.requests) == 1
+    ev = _events(s)
+    assert ev.get("FAILURE") == 1 and ev.get("TIMEOUT", 0) == 0
 
 
-def test_connection_refused_falls_back(hola):
-    s = hola(args=["--aloha-url", f"http://127.0.0.1:{closed_port()}/"])
+def test_dropped_connection_is_retried_until_the_hystrix_timeout(hola, aloha):
+    """aloha closes without answering: NoHttpResponseException, an IOException. Apache
+    HttpClient re-executes the GET 3 times on fresh connections, then Feign's Retryer sleeps
+    150/225/... ms between attempts until the 600 ms Hystrix timeout wins (TIMEOUT)."""
+    aloha.set_mode("close")
+    s = hola(args=["--aloha-url", aloha.url])
+    t0 = time.monotonic()
+    assert chain(s) == ["Hola de testhost", FALLBACK]
+    assert 0.55 <= time.monotonic() - t0 < 1.0
+    # Feign attempts at ~0, 150, 375 ms, each 1 + 3 transport tries
+    assert len(aloha.requests) == 12
+    assert _events(s).get("TIMEOUT") == 1
+
+
+def test_connection_refused_retries_until_timeout_then_opens(hola):
+    """Feign's default Retryer (HolaResource.java:104-112 sets none) retries the refused
+    connect at +150 ms and +375 ms; the next sleep (337 ms) would end past the 600 ms Hystrix
+    timeout (config.properties:17), so the call is a TIMEOUT at ~600 ms. After
+    requestVolumeThreshold=5 (config.properties:19) such calls the breaker opens and
+    short-circuits at once."""
+    s = hola(args=["--aloha-url", f"http://127.0.0.1:{closed_port()}/",
+                   "-Dhystrix.command.default.metrics.healthSnapshot.intervalInMilliseconds=0"])
+    for _ in range(5):
+        t0 = time.monotonic()
+        assert chain(s)[1:] == [FALLBACK]
+        assert 0.55 <= time.monotonic() - t0 < 1.0
     t0 = time.monotonic()
     assert chain(s)[1:] == [FALLBACK]
-    assert time.monotonic() - t0 < 0.5
+    assert time.monotonic() - t0 < 0.3  # short-circuited
+    ev = _events(s)
+    assert ev.get("TIMEOUT") == 5 and ev.get("SHORT_CIRCUITED") == 1 and ev.get("FAILURE", 0) == 0
+    log = _wait_log(s, "---> GET", 15)
+    assert log.count("[AlohaService#aloha] ---> GET ") == 15  # 3 attempts x 5 calls
+    assert log.count("[AlohaService#aloha] ---> RETRYING") == 10
+    assert "[AlohaService#aloha] <--- ERROR HttpHostConnectException: Connect to 127.0.0.1:" in log
+    # The SSE stream shows the same rolling counts.
+    with socket.create_connection(("127.0.0.1", s.port), timeout=5) as c:
+        c.sendall(b"GET /hystrix.stream HTTP/1.1\r\nHost: x\r\n\r\n")
+        data = b""
+        while b'"type":"HystrixCommand"' not in data or not data.rstrip().endswith(b"}"):
+            data += c.recv(65536)
+    cmd = json.loads(next(l for l in data.decode().splitlines()
+                          if l.startswith("data:") and '"HystrixCommand"' in l)[5:])
+    assert cmd["rollingCountTimeout"] == 5 and cmd["isCircuitBreakerOpen"] is True
 
 
-def test_unknown_host_falls_back(hola):
-    s = hola(args=["--aloha-url", "http://aloha.invalid:8080/"])
+def test_feign_retry_off_fails_fast(hola):
+    s = hola(args=["--aloha-url", f"http://127.0.0.1:{closed_port()}/", "--feign-retry", "off"])
+    t0 = time.monotonic()
     assert chain(s)[1:] == [FALLBACK]
+    assert time.monotonic() - t0 < 0.3
+    assert _events(s).get("FAILURE") == 1
+
+
+def test_retries_exhaust_before_a_long_timeout(hola):
+    """With a generous Hystrix timeout the Retryer gives up after max_attempts executions and
+    the command is a FAILURE (RetryableException propagated)."""
+    s = hola(args=["--aloha-url", f"http://127.0.0.1:{closed_port()}/", "--hystrix-timeout-ms", "5000",
+                   "--feign-retry", "10,1000,5"])
+    t0 = time.monotonic()
+    assert chain(s)[1:] == [FALLBACK]
+    dt = time.monotonic() - t0
+    assert 0.1 <= dt < 0.5, dt  # sleeps 15 + 22 + 33 + 50 ms
+    assert _events(s).get("FAILURE") == 1
+    log = _wait_log(s, "---> GET", 5)
+    assert log.count("---> GET ") == 5 and log.count("---> RETRYING") == 4
+
+
+def test_retry_after_makes_an_error_status_retryable(hola, aloha):
+    """ErrorDecoder.Default: a non-2xx response with Retry-After is a RetryableException.
+    Retry-After: 0 retries at once (5 executions, then FAILURE); a 1 s Retry-After is capped
+    at the 1 s max period, so the 600 ms Hystrix timeout fires first."""
+    aloha.set_mode("unavailable")
+    s = hola(args=["--aloha-url", aloha.url, "--hystrix-request-volume", "100"])
+    t0 = time.monotonic()
+    assert chain(s)[1:] == [FALLBACK]
+    assert time.monotonic() - t0 < 0.3
+    assert len(aloha.requests) == 5
+    assert _events(s).get("FAILURE") == 1
+    aloha.retry_after = "1"
+    t0 = time.monotonic()
+    assert chain(s)[1:] == [FALLBACK]
+    assert 0.55 <= time.monotonic() - t0 < 1.0
+    assert len(aloha.requests) == 6
+    assert _events(s).get("TIMEOUT") == 1
+    log = _wait_log(s, "<--- HTTP/1.1 503", 6)
+    assert "[AlohaService#aloha] <--- HTTP/1.1 503 Service Unavailable (" in log
+
+
+def test_unknown_host_retries_until_timeout(hola):
+    s = hola(args=["--aloha-url", "http://aloha.invalid:8080/"])
+    t0 = time.monotonic()
+    assert chain(s)[1:] == [FALLBACK]
+    assert 0.55 <= time.monotonic() - t0 < 1.0
+    assert _events(s).get("TIMEOUT") == 1
+    log = _wait_log(s, "UnknownHostException", 1)
+    assert "[AlohaService#aloha] <--- ERROR UnknownHostException: " in log
 
 
 def test_timeout_600ms(hola, aloha):
@@ -97,7 +211,7 @@ def test_circuit_opens_after_volume_threshold(hola, aloha):
         assert chain(s)[1:] == [FALLBACK]
     assert len(aloha.requests) == n_before
     st, _, body = s.get("/metrics")
-    assert b'hola_hystrix_circuit_open{command="AlohaService#aloha()"} 1' in body
+    assert b'hola_hystrix_circuit_open{command="aloha"} 1' in body
     assert b'event="SHORT_CIRCUITED"' in body
 
 
@@ -176,12 +290,35 @@ def test_format_error_skips_downstream_call(hola, aloha, tmp_path):
 
 
 def test_feign_basic_logging(hola, aloha):
+    """Feign Logger.ErrorLogger at BASIC (HolaResource.java:109): raw stderr lines tagged with
+    the config key cut at '(' (Logger.methodTag), the reason phrase and the elapsed ms."""
     s = hola(args=["--aloha-url", aloha.url])
     chain(s)
-    time.sleep(0.2)
-    log = s.log()
-    assert "[AlohaService#aloha()] ---> GET " in log and "/api/aloha-chaining HTTP/1.1" in log
-    assert "<--- HTTP/1.1 200" in log
+    log = _wait_log(s, "<--- HTTP/1.1", 1)
+    lines = [l for l in log.splitlines() if l.startswith("[AlohaService#aloha] ")]
+    assert lines[0] == f"[AlohaService#aloha] ---> GET {aloha.url.rstrip('/')}/api/aloha-chaining HTTP/1.1"
+    assert re.fullmatch(r"\[AlohaService#aloha\] <--- HTTP/1\.1 200 OK \(\d+ms\)", lines[1]), lines[1]
+
+
+def test_hystrix_command_key_default_and_flag(hola, aloha):
+    """feign-hystrix 8.15.1 keys the command by the method name ("aloha"); the group and pool
+    are the target URL. --hystrix-command-key configkey gives the 9.x SetterFactory.Default
+    key; per-command properties follow the key."""
+    aloha.set_mode("slow", delay_s=1.0)
+    s = hola(args=["--aloha-url", aloha.url, "--feign-log", "none",
+                   "-Dhystrix.command.aloha.execution.isolation.thread.timeoutInMilliseconds=150"])
+    t0 = time.monotonic()
+    assert chain(s)[1:] == [FALLBACK]
+    assert time.monotonic() - t0 < 0.5
+    _, _, body = s.get("/metrics")
+    assert b'hola_hystrix_events_total{command="aloha",event="TIMEOUT"} 1' in body
+    s2 = hola(args=["--aloha-url", aloha.url, "--feign-log", "none", "--hystrix-command-key", "configkey",
+                    "-Dhystrix.command.AlohaService#aloha().execution.isolation.thread.timeoutInMilliseconds=150"])
+    t0 = time.monotonic()
+    assert chain(s2)[1:] == [FALLBACK]
+    assert time.monotonic() - t0 < 0.5
+    _, _, body = s2.get("/metrics")
+    assert b'command="AlohaService#aloha()",event="TIMEOUT"} 1' in body
 
 
 def test_hystrix_flag_shorthands(hola, aloha):

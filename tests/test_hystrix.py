@@ -169,7 +169,7 @@ def test_stream_reports_command_after_chaining(hola):
     types = {e["type"] for e in events}
     assert types == {"HystrixCommand", "HystrixThreadPool"}
     cmd = next(e for e in events if e["type"] == "HystrixCommand")
-    assert cmd["name"] == "AlohaService#aloha()" and cmd["rollingCountSuccess"] >= 1
+    assert cmd["name"] == "aloha" and cmd["group"] == aloha.url and cmd["rollingCountSuccess"] >= 1
 
 
 def test_stream_connection_limit(hola):
@@ -182,6 +182,58 @@ def test_stream_connection_limit(hola):
     time.sleep(0.2)
     out = _read_sse(s.port, seconds=0.3)
     assert b"200 OK" in out
+
+
+def test_stream_limit_message_uses_configured_max(hola):
+    """The 503 text names the configured limit, as HystrixMetricsStreamServlet does."""
+    s = hola(args=["--hystrix-stream-max", "2"])
+    subs = []
+    try:
+        for _ in range(2):
+            c = socket.create_connection(("127.0.0.1", s.port), timeout=3)
+            c.sendall(b"GET /hystrix.stream HTTP/1.1\r\nHost: x\r\n\r\n")
+            assert b"200 OK" in c.recv(100)
+            subs.append(c)
+        st, _, body = s.get("/hystrix.stream")
+        assert st == 503 and body == b"MaxConcurrentConnections reached: 2"
+    finally:
+        for c in subs:
+            c.close()
+
+
+def _metric(s, name: str) -> int:
+    _, _, body = s.get("/metrics")
+    line = next(l for l in body.decode().splitlines() if l.startswith(name + " "))
+    return int(float(line.split()[1]))
+
+
+def test_stalled_subscriber_is_bounded_then_closed(hola):
+    """A subscriber that never reads: frames stop being queued once 64 KB are unsent (memory
+    stays bounded), and after --hystrix-stream-stall-ms it is closed, freeing its slot."""
+    with FakeAloha() as aloha:
+        s = hola(args=["--aloha-url", aloha.url, "--feign-log", "none", "--hystrix-stream-max", "1",
+                       "--hystrix-stream-stall-ms", "1500"], threads=1)
+        s.get("/api/hola-chaining")  # the command has run: every frame carries its JSON
+    rss0 = s.memory_kb().get("VmRSS", 0)
+    c = socket.socket()
+    c.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 2048)
+    c.connect(("127.0.0.1", s.port))
+    try:
+        c.sendall(b"GET /hystrix.stream?delay=10 HTTP/1.1\r\nHost: x\r\n\r\n")
+        deadline = time.monotonic() + 10
+        while _metric(s, "hola_hystrix_stream_frames_skipped_total") == 0 and time.monotonic() < deadline:
+            time.sleep(0.1)
+        assert _metric(s, "hola_hystrix_stream_frames_skipped_total") > 0
+        assert s.get("/hystrix.stream")[0] == 503  # the stalled subscriber still holds the slot
+        while _metric(s, "hola_hystrix_stream_stalled_closed_total") == 0 and time.monotonic() < deadline:
+            time.sleep(0.1)
+        assert _metric(s, "hola_hystrix_stream_stalled_closed_total") == 1
+        assert _metric(s, "hola_hystrix_stream_subscribers") == 0
+        assert s.memory_kb().get("VmRSS", 0) - rss0 < 4096
+        out = _read_sse(s.port, seconds=0.3)  # the slot is free again
+        assert b"200 OK" in out
+    finally:
+        c.close()
 
 
 @pytest.mark.parametrize("fail_every", [0, 1, 3])
