@@ -79,6 +79,10 @@ def parse_args():
                     help="requests per connection sent back to back before waiting for their "
                          "responses (wrk's pipeline.lua, as in the TechEmpower plaintext test); "
                          "1 = wrk's default and the headline (BASELINE configs 2-4)")
+    ap.add_argument("--c1-reqs", type=int, default=150000,
+                    help="after the timed region, rank 0 drives its own replica over ONE connection for "
+                         "this many requests (BASELINE config 2) and reports c1_rps/c1_p50_ms/c1_p99_ms; "
+                         "0 = skip. Outside the timed region: `value` is untouched")
     ap.add_argument("--busy-poll-us", type=int, default=20,
                     help="spin this long in epoll before sleeping (server and load generator); "
                          "20 us measured best on the box (profiles/r11_box_session), 0 = off")
@@ -133,6 +137,10 @@ def main() -> int:
     targets = [(host, base_port + i) for i in range(local_world)]
 
     env = {"HOSTNAME": f"replica-{rank}"}
+    # Every response body is checked by the load generator (a mismatch is an error): the
+    # replica behind target i answers "Hola de replica-<node's first rank + i>".
+    first_rank = rank - local_rank
+    bodies = _expected_bodies(a.path, [first_rank + i for i in range(local_world)])
     args = ["--no-tracing"] if a.no_tracing else []
     if host != "127.0.0.1":
         args += ["--host", host]
@@ -156,7 +164,8 @@ def main() -> int:
         loadgen = ControlledLoadgen(targets, a.connections, len(load_cpus), cpu_list=",".join(map(str, load_cpus)),
                                     path=a.path, target_offset=local_rank, busy_poll_us=a.busy_poll_us,
                                     busy_poll_pause=a.busy_poll_pause, epoll_lt=a.epoll_lt,
-                                    per_conn_quota=a.per_conn_quota, pipeline=a.pipeline)
+                                    per_conn_quota=a.per_conn_quota, pipeline=a.pipeline,
+                                    expect_bodies=bodies, verify_body=bodies is None)
         for _ in range(a.warmup):
             loadgen.run(a.reqs_per_conn)
         loadgen.reset()
@@ -183,9 +192,12 @@ def main() -> int:
         thr1 = _cgroup_cpu_stat()
         st = loadgen.stats()
         mem = server.memory_kb()
+        c1 = _config2_subrun(a, host, port, load_cpus, bodies and [bodies[local_rank]]) if local_rank == 0 else None
 
         local = {"elapsed": elapsed, "requests": reqs, "errors": errs, "hist": st.get("hist", ""),
-                 "non2xx": st.get("non2xx", 0), "server_cpus": format_cpu_list(server_cpus),
+                 "non2xx": st.get("non2xx", 0), "body_checked": st.get("body_checked", 0),
+                 "body_mismatch": st.get("body_mismatch", 0), "c1": c1,
+                 "server_cpus": format_cpu_list(server_cpus),
                  "load_cpus": format_cpu_list(load_cpus),
                  "server_cpu_s": cpu1[0] - cpu0[0], "loadgen_cpu_s": cpu1[1] - cpu0[1],
                  "startup_ms": server.startup_ms, "rss_peak_kb": mem.get("VmHWM", 0),
@@ -243,6 +255,11 @@ def main() -> int:
                                 "throttled_ms": round(gathered[0]["cgroup"].get("throttled_usec", 0) / 1000.0, 1)},
             "errors": sum(g["errors"] for g in gathered),
             "non2xx": sum(g["non2xx"] for g in gathered),
+            # every 2xx body of the timed region compared byte for byte with the expected one
+            "body_checked": sum(g["body_checked"] for g in gathered),
+            "body_mismatch": sum(g["body_mismatch"] for g in gathered),
+            # BASELINE config 2 (1 connection, 1 replica), measured after the timed region
+            **_c1_keys(gathered[0]["c1"]),
             "config": {
                 "model": "hola GET /api/hola (native C++ replica, default greeting, "
                          + ("tracing off" if a.no_tracing else
@@ -278,6 +295,44 @@ def main() -> int:
             dist.barrier()
             dist.destroy_process_group()
     return 0
+
+
+def _expected_bodies(path: str, ranks: list[int]) -> list[str] | None:
+    """Exact body each target must answer, or None to learn it from the first response."""
+    if path.split("?")[0] in ("/api/hola", "/api/hola/"):
+        return [f"Hola de replica-{r}" for r in ranks]  # default greeting (HolaResource.java:60,65)
+    if path.split("?")[0] == "/api/health":
+        return ["I'm ok"] * len(ranks)
+    return None
+
+
+def _config2_subrun(a, host: str, port: int, load_cpus, bodies) -> dict | None:
+    """BASELINE config 2: one keep-alive connection against this rank's replica, run after
+    the timed region (so the headline is unaffected)."""
+    if a.c1_reqs <= 0:
+        return None
+    lg = ControlledLoadgen([(host, port)], 1, 1, cpu_list=str(load_cpus[0]), path=a.path,
+                           busy_poll_us=a.busy_poll_us, busy_poll_pause=a.busy_poll_pause, epoll_lt=a.epoll_lt,
+                           expect_bodies=bodies, verify_body=bodies is None)
+    try:
+        lg.run(max(1000, a.c1_reqs // 10))  # warm-up
+        lg.reset()
+        r = lg.run(a.c1_reqs)
+        st = lg.stats()
+    finally:
+        lg.close()
+    el = r["elapsed_ns"] / 1e9
+    return {"rps": r["requests"] / el if el > 0 else 0.0, "requests": r["requests"], "elapsed_s": el,
+            "p50_ns": st["p50_ns"], "p99_ns": st["p99_ns"], "errors": r["errors"],
+            "body_checked": st.get("body_checked", 0)}
+
+
+def _c1_keys(c1: dict | None) -> dict:
+    if not c1:
+        return {}
+    return {"c1_rps": round(c1["rps"], 1), "c1_p50_ms": round(c1["p50_ns"] / 1e6, 4),
+            "c1_p99_ms": round(c1["p99_ns"] / 1e6, 4), "c1_requests": c1["requests"],
+            "c1_errors": c1["errors"], "c1_body_checked": c1["body_checked"]}
 
 
 class _stdout_to_stderr:

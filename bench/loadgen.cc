@@ -18,6 +18,11 @@
 //        reset       clears the histogram
 //        quit
 //
+// Response bodies are verified against --expect-body (one per target in --targets order, or
+// one for all) and/or, with --verify-body, against the first 2xx body each thread sees from
+// each target; a mismatch counts as an error (and in "body_mismatch"), so a server that
+// answers fast with the wrong bytes cannot inflate req/s.
+//
 // wrk-style invocation: `hola_loadgen -t8 -c64 -d30s [--latency] http://host:port/path`
 // takes the target from the URL, accepts wrk's duration suffixes (s/m/h) and prints a
 // wrk-like text summary (`--json` keeps the JSON line).
@@ -83,6 +88,8 @@ struct Options {
   // a run waiting for a slower one); --per-conn-quota gives each connection exactly R.
   bool per_conn_quota = false;
   int pipeline = 1;  // requests per batch (closed loop only)
+  std::vector<std::string> expect_bodies;  // --expect-body: per target, or one for all
+  bool verify_body = false;                // --verify-body: learn the first 2xx body per target
 };
 
 struct Conn {
@@ -108,6 +115,9 @@ struct ThreadState {
   Histogram hist;
   std::mutex hist_mu;
   uint64_t completed = 0, errors = 0, non2xx = 0, reconnects = 0, bytes = 0;
+  uint64_t body_checked = 0, body_mismatch = 0;
+  std::vector<std::string> expected;  // per target: the body every response must carry
+  std::vector<bool> have_expected;
   std::atomic<int64_t> run_quota{0};  // control: batches per connection for the next run
   std::atomic<uint64_t> run_gen{0};
   std::atomic<uint64_t> done_gen{0};
@@ -181,7 +191,7 @@ inline bool iprefix(const char* p, size_t n, std::string_view lower) {
 // Returns 1 when a full response starts at buf[from] (its size in *used), 0 if more is
 // needed, -1 on malformed input. One pass over the head's lines: the status line, then
 // Content-Length and Connection, up to the empty line.
-int response_complete(Conn* c, size_t from, int* status, bool* close, size_t* used) {
+int response_complete(Conn* c, size_t from, int* status, bool* close, size_t* used, size_t* body_at) {
   const char* s = c->buf + from;
   const size_t n = c->have - from;
   auto incomplete = [&] { return (from == 0 && c->have >= sizeof c->buf) ? -1 : 0; };  // head > buf
@@ -212,6 +222,7 @@ int response_complete(Conn* c, size_t from, int* status, bool* close, size_t* us
   }
   if (p + cl > sizeof c->buf) return -1;
   *used = p + cl;
+  *body_at = from + p;
   return n >= *used ? 1 : 0;
 }
 
@@ -232,6 +243,15 @@ void thread_main(ThreadState* ts, const Options* o) {
     const std::string one = c->req;
     for (int k = 1; k < o->pipeline; ++k) c->req += one;
     ts->conns.push_back(std::move(c));
+  }
+  const bool verify = o->verify_body || !o->expect_bodies.empty();
+  ts->expected.assign(o->targets.size(), std::string());
+  ts->have_expected.assign(o->targets.size(), false);
+  for (size_t k = 0; k < o->targets.size(); ++k) {
+    const size_t e = o->expect_bodies.size() == 1 ? 0 : k;
+    if (e >= o->expect_bodies.size()) continue;  // learned with --verify-body, or unchecked
+    ts->expected[k] = o->expect_bodies[e];
+    ts->have_expected[k] = true;
   }
   for (auto& c : ts->conns) {
     if (!connect_once(c.get(), *o)) {
@@ -407,8 +427,8 @@ void thread_main(ThreadState* ts, const Options* o) {
       size_t at = 0;  // responses are consumed in place; what is left moves down once
       for (;;) {  // every complete response in the buffer (several when pipelining)
         int status = 0;
-        size_t used = 0;
-        int rc = response_complete(c, at, &status, &close, &used);
+        size_t used = 0, body_at = 0;
+        int rc = response_complete(c, at, &status, &close, &used, &body_at);
         if (rc == 0) break;
         if (rc < 0) {
           ++ts->errors;
@@ -422,7 +442,21 @@ void thread_main(ThreadState* ts, const Options* o) {
           ts->hist.add(uint64_t(lat));
           ++ts->completed;
         }
-        if (status < 200 || status > 299) ++ts->non2xx;
+        if (status < 200 || status > 299) {
+          ++ts->non2xx;
+        } else if (verify) {
+          const size_t t = size_t(c->target);
+          const size_t blen = at + used - body_at;
+          if (!ts->have_expected[t]) {
+            ts->expected[t].assign(c->buf + body_at, blen);
+            ts->have_expected[t] = true;
+          } else if (blen != ts->expected[t].size() || memcmp(c->buf + body_at, ts->expected[t].data(), blen) != 0) {
+            if (ts->recording) ++ts->body_mismatch;
+            ++ts->errors;
+            ++run_errors;
+          }
+          if (ts->recording) ++ts->body_checked;
+        }
         ++run_requests;
         --c->inflight;
         at += used;
@@ -491,22 +525,26 @@ bool parse_targets(const std::string& s, std::vector<Target>* out) {
 
 std::string stats_json(std::vector<std::unique_ptr<ThreadState>>& ts, bool with_hist) {
   Histogram h;
-  uint64_t errors = 0, non2xx = 0, reconnects = 0;
+  uint64_t errors = 0, non2xx = 0, reconnects = 0, checked = 0, mismatch = 0;
   for (auto& t : ts) {
     std::lock_guard<std::mutex> g(t->hist_mu);
     h.merge(t->hist);
     errors += t->errors;
     non2xx += t->non2xx;
     reconnects += t->reconnects;
+    checked += t->body_checked;
+    mismatch += t->body_mismatch;
   }
-  char buf[512];
+  char buf[640];
   snprintf(buf, sizeof buf,
            "{\"count\":%llu,\"mean_ns\":%.0f,\"p50_ns\":%llu,\"p90_ns\":%llu,\"p99_ns\":%llu,\"p999_ns\":%llu,"
-           "\"max_ns\":%llu,\"errors\":%llu,\"non2xx\":%llu,\"reconnects\":%llu",
+           "\"max_ns\":%llu,\"errors\":%llu,\"non2xx\":%llu,\"reconnects\":%llu,\"body_checked\":%llu,"
+           "\"body_mismatch\":%llu",
            (unsigned long long)h.count(), h.mean(), (unsigned long long)h.percentile(50),
            (unsigned long long)h.percentile(90), (unsigned long long)h.percentile(99),
            (unsigned long long)h.percentile(99.9), (unsigned long long)h.max(), (unsigned long long)errors,
-           (unsigned long long)non2xx, (unsigned long long)reconnects);
+           (unsigned long long)non2xx, (unsigned long long)reconnects, (unsigned long long)checked,
+           (unsigned long long)mismatch);
   std::string s = buf;
   if (with_hist) s += ",\"hist\":\"" + h.encode() + "\"";
   return s + "}";
@@ -540,6 +578,20 @@ bool parse_url_arg(const std::string& url, std::string* target, std::string* pat
   }
   *target = host + ":" + port;
   return !host.empty();
+}
+
+// --expect-body text with \n \r \t \\ escapes.
+std::string unescape(const std::string& s) {
+  std::string o;
+  for (size_t i = 0; i < s.size(); ++i) {
+    if (s[i] != '\\' || i + 1 == s.size()) {
+      o += s[i];
+      continue;
+    }
+    char n = s[++i];
+    o += n == 'n' ? '\n' : n == 'r' ? '\r' : n == 't' ? '\t' : n;
+  }
+  return o;
 }
 
 std::string human_ns(double ns) {
@@ -605,12 +657,14 @@ int main(int argc, char** argv) {
     else if (a == "--spin-us") o.spin_us = atoi(val().c_str());
     else if (a == "--per-conn-quota") o.per_conn_quota = true;
     else if (a == "--pipeline") o.pipeline = atoi(val().c_str());
+    else if (a == "--expect-body") o.expect_bodies.push_back(unescape(val()));
+    else if (a == "--verify-body") o.verify_body = true;
     else {
       fprintf(stderr,
               "usage: hola_loadgen --targets h:p[,h:p..] -c CONNS -t THREADS [--cpu-list L] [--path P]\n"
               "                    (--duration S [--warmup S] [--rate R [--spin-us N]] | --control [--per-conn-quota])\n"
               "                    [--target-offset K] [--busy-poll-us N [--busy-poll-pause P]] [--epoll-lt] [-H 'Name: v']\n"
-              "                    [--pipeline P]\n"
+              "                    [--pipeline P] [--expect-body B]... [--verify-body]\n"
               "       hola_loadgen -t T -c C -d 30s [--latency] [--json] [-H 'Name: v'] http://host:port/path   (wrk style)\n");
       return 2;
     }
@@ -685,7 +739,10 @@ int main(int argc, char** argv) {
       }
       printf("  %llu requests in %.2fs, %s read\n", (unsigned long long)completed, o.duration_s,
              human_bytes(double(bytes)).c_str());
+      uint64_t mismatch = 0;
+      for (auto& t : ts) mismatch += t->body_mismatch;
       if (errors) printf("  Socket errors: %llu\n", (unsigned long long)errors);
+      if (mismatch) printf("  Body mismatches: %llu\n", (unsigned long long)mismatch);
       if (non2xx) printf("  Non-2xx or 3xx responses: %llu\n", (unsigned long long)non2xx);
       printf("Requests/sec: %12.2f\nTransfer/sec: %10s\n", rps, human_bytes(double(bytes) / o.duration_s).c_str());
       return 0;
@@ -742,7 +799,7 @@ int main(int argc, char** argv) {
       for (auto& t : ts) {
         std::lock_guard<std::mutex> g(t->hist_mu);
         t->hist.reset();
-        t->errors = t->non2xx = t->reconnects = 0;
+        t->errors = t->non2xx = t->reconnects = t->body_checked = t->body_mismatch = 0;
       }
       printf("{\"reset\":true}\n");
       fflush(stdout);

@@ -36,6 +36,20 @@ def merge_hists(hists: list[dict[int, int]]) -> dict[int, int]:
     return out
 
 
+def escape_body(b: str) -> str:
+    """--expect-body argument form of a body (the loadgen unescapes \\n \\r \\t \\\\)."""
+    return b.replace("\\", "\\\\").replace("\n", "\\n").replace("\r", "\\r").replace("\t", "\\t")
+
+
+def body_args(expect_bodies: list[str] | None, verify_body: bool) -> list[str]:
+    out: list[str] = []
+    for b in expect_bodies or []:
+        out += ["--expect-body", escape_body(b)]
+    if verify_body:
+        out += ["--verify-body"]
+    return out
+
+
 def percentile(hist: dict[int, int], p: float) -> int:
     total = sum(hist.values())
     if not total:
@@ -51,15 +65,18 @@ def percentile(hist: dict[int, int], p: float) -> int:
 
 class ControlledLoadgen:
     """`hola_loadgen --control`: each run(R) completes R x connections requests, drawn by the
-    connections from one shared budget (or exactly R per connection with `per_conn_quota`)."""
+    connections from one shared budget (or exactly R per connection with `per_conn_quota`).
+    `expect_bodies` (one per target, or one for all) and `verify_body` (learn each target's
+    first 2xx body) make every response body checked; mismatches count as errors."""
 
     def __init__(self, targets: list[tuple[str, int]], connections: int, threads: int,
                  cpu_list: str | None = None, path: str = "/api/hola", target_offset: int = 0,
                  headers: list[str] | None = None, busy_poll_us: int = 0, per_conn_quota: bool = False,
-                 busy_poll_pause: int = 0, epoll_lt: bool = False, pipeline: int = 1):
+                 busy_poll_pause: int = 0, epoll_lt: bool = False, pipeline: int = 1,
+                 expect_bodies: list[str] | None = None, verify_body: bool = False):
         cmd = [str(binary("hola_loadgen")), "--targets", ",".join(f"{h}:{p}" for h, p in targets),
                "-c", str(connections), "-t", str(threads), "--path", path, "--control",
-               "--target-offset", str(target_offset)]
+               "--target-offset", str(target_offset)] + body_args(expect_bodies, verify_body)
         if cpu_list:
             cmd += ["--cpu-list", cpu_list]
         for h in headers or []:
@@ -116,7 +133,8 @@ class ControlledLoadgen:
 def run_duration(targets: list[tuple[str, int]], connections: int, threads: int, duration_s: float,
                  warmup_s: float = 1.0, cpu_list: str | None = None, path: str = "/api/hola",
                  timeout: float | None = None, rate: float = 0.0, busy_poll_us: int = 0,
-                 spin_us: int = 0, pipeline: int = 1) -> dict:
+                 spin_us: int = 0, pipeline: int = 1, expect_bodies: list[str] | None = None,
+                 verify_body: bool = False) -> dict:
     """wrk-style timed run (closed loop), or wrk2-style open loop at `rate` req/s with latency
     measured from intended send times; returns the loadgen's JSON summary. `busy_poll_us`
     spins in epoll after activity; `spin_us` (open loop) spins instead of sleeping when the
@@ -124,7 +142,7 @@ def run_duration(targets: list[tuple[str, int]], connections: int, threads: int,
     (closed loop only)."""
     cmd = [str(binary("hola_loadgen")), "--targets", ",".join(f"{h}:{p}" for h, p in targets),
            "-c", str(connections), "-t", str(threads), "--path", path, "--duration", str(duration_s),
-           "--warmup", str(warmup_s)]
+           "--warmup", str(warmup_s)] + body_args(expect_bodies, verify_body)
     if cpu_list:
         cmd += ["--cpu-list", cpu_list]
     if rate > 0:

@@ -20,12 +20,18 @@ def run(cmd, port):
 
 
 def test_bench_one_rank():
-    out = run([sys.executable, str(ROOT / "bench.py"), "--steps", "2", "--warmup", "1", "--reqs-per-conn", "100"], 18800)
+    out = run([sys.executable, str(ROOT / "bench.py"), "--steps", "2", "--warmup", "1", "--reqs-per-conn", "100",
+               "--c1-reqs", "3000"], 18800)
     for k in KEYS:
         assert k in out
     assert out["metric"] == json.loads((ROOT / "BASELINE.json").read_text())["metric"]
     assert out["n_gpus"] == 1 and out["steps"] == 2 and out["warmup"] == 1
     assert out["requests"] == 64 * 100 * 2 and out["errors"] == 0
+    # every timed response body was compared with "Hola de replica-0"
+    assert out["body_checked"] == out["requests"] and out["body_mismatch"] == 0
+    # BASELINE config 2 sub-run (1 connection), outside the timed region
+    assert out["c1_requests"] == 3000 and out["c1_errors"] == 0 and out["c1_body_checked"] == 3000
+    assert out["c1_rps"] > 0 and 0 < out["c1_p50_ms"] <= out["c1_p99_ms"]
     assert out["scaling"] == "weak" and out["higher_is_better"] is True and out["vs_baseline"] is None
     assert out["config"]["global_batch"] == 64 and out["config"]["parallelism"] == "replicas1"
     assert abs(out["value"] - out["requests"] / (out["ms_per_step"] * out["steps"] / 1000)) / out["value"] < 0.01
@@ -37,8 +43,11 @@ def test_bench_one_rank():
 def test_bench_two_ranks_gloo():
     out = run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                "--master-addr", "127.0.0.1", "--master-port", "29561", str(ROOT / "bench.py"), "--gpus", "2",
-               "--steps", "2", "--warmup", "1", "--reqs-per-conn", "100"], 18820)
+               "--steps", "2", "--warmup", "1", "--reqs-per-conn", "100", "--c1-reqs", "2000"], 18820)
     assert out["n_gpus"] == 2 and out["requests"] == 2 * 64 * 100 * 2
+    # connections are dealt over both replicas; each body must name the replica behind it
+    assert out["body_checked"] == out["requests"] and out["body_mismatch"] == 0 and out["errors"] == 0
+    assert out["c1_requests"] == 2000 and out["c1_errors"] == 0
     assert out["config"]["global_batch"] == 128
 
 
@@ -47,9 +56,10 @@ def test_bench_four_ranks_gloo():
     connections over all 4 replicas; the JSON line reports the node-wide total."""
     out = run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
                "--master-addr", "127.0.0.1", "--master-port", "29563", str(ROOT / "bench.py"), "--gpus", "4",
-               "--steps", "2", "--warmup", "1", "--reqs-per-conn", "50"], 18840)
+               "--steps", "2", "--warmup", "1", "--reqs-per-conn", "50", "--c1-reqs", "0"], 18840)
     assert out["n_gpus"] == 4 and out["requests"] == 4 * 64 * 50 * 2
     assert out["errors"] == 0 and out["non2xx"] == 0
+    assert out["body_checked"] == out["requests"] and "c1_rps" not in out
     assert out["config"]["global_batch"] == 256 and out["config"]["parallelism"] == "replicas4"
     from hola_amd.utils.cpu import parse_cpu_list
     cpus = [c for r in out["config"]["cpu_map"].values() for side in r.values() for c in parse_cpu_list(side)]
@@ -60,9 +70,25 @@ def test_bench_pipelined():
     """--pipeline 16 (wrk's pipeline.lua): a step still completes connections x reqs-per-conn
     requests, every response is counted and checked, and the setting is recorded."""
     out = run([sys.executable, str(ROOT / "bench.py"), "--steps", "2", "--warmup", "1", "--reqs-per-conn", "160",
-               "--pipeline", "16"], 18860)
+               "--pipeline", "16", "--c1-reqs", "0"], 18860)
     assert out["requests"] == 64 * 160 * 2 and out["errors"] == 0 and out["non2xx"] == 0
     assert out["config"]["pipeline"] == 16 and "16 pipelined" in out["data"]
     # 16 requests per segment each way: far fewer than 2 segments per request
     if out["tcp_per_req"]:
         assert out["tcp_per_req"]["OutSegs"] < 1.0
+
+
+def test_loadgen_counts_wrong_bodies_as_errors():
+    """A server answering 200 with the wrong bytes must not count as good throughput."""
+    from hola_amd.parallel.loadgen import run_duration
+    from hola_amd.server import HolaProcess
+
+    with HolaProcess(env={"HOSTNAME": "hx"}, threads=1) as s:
+        good = run_duration([("127.0.0.1", s.port)], 2, 1, 0.3, warmup_s=0.1, expect_bodies=["Hola de hx"])
+        bad = run_duration([("127.0.0.1", s.port)], 2, 1, 0.3, warmup_s=0.1, expect_bodies=["Hola de hy"])
+        learned = run_duration([("127.0.0.1", s.port)], 2, 1, 0.3, warmup_s=0.1, verify_body=True)
+    assert good["latency"]["body_mismatch"] == 0 and good["latency"]["errors"] == 0
+    assert good["latency"]["body_checked"] == good["latency"]["count"] > 0
+    assert bad["latency"]["body_mismatch"] == bad["latency"]["count"] > 0
+    assert bad["latency"]["errors"] >= bad["latency"]["body_mismatch"]
+    assert learned["latency"]["body_mismatch"] == 0 and learned["latency"]["body_checked"] > 0
