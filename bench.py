@@ -56,6 +56,14 @@ def parse_args():
                     help="loopback address of the replicas; auto = ::1 when IPv6 loopback works (2.6%% "
                          "more req/s than 127.0.0.1 on the box, profiles/r20_v6), else 127.0.0.1")
     ap.add_argument("--no-tracing", action="store_true", help="run replicas with tracing off")
+    ap.add_argument("--zipkin-sink", action="store_true",
+                    help="the deployed tracing configuration (ZIPKIN_SERVER_URL is set in the image, "
+                         "Dockerfile:6): start a native discard Zipkin collector (hola_zipkin_sink) and "
+                         "point every replica at it; the JSON gains a `tracing` block with spans "
+                         "recorded/reported/dropped per second and the reporter thread's CPU")
+    ap.add_argument("--trace-queue", type=int, default=-1,
+                    help="replicas' --trace-queue (spans exported per flush interval; -1 = server "
+                         "default 1000, Brave 3's collector queue; 0 = bounded only by the rings)")
     ap.add_argument("--profile-dir", default="",
                     help="run replicas with --profile and write their stage histograms here")
     ap.add_argument("--no-avoid-busy", action="store_true",
@@ -111,6 +119,9 @@ def main() -> int:
     # once on rank 0 and broadcast, since load measurements differ between processes);
     # within a rank, server worker t and loadgen thread t share an L3 domain. ----
     plan = [None]
+    sink = None
+    if rank == 0 and a.zipkin_sink and not a.no_tracing:
+        sink = _start_sink()
     if rank == 0:
         slots = max(local_world, _gpu_slots())
         cores = a.cores or slot_cores(slots)
@@ -123,7 +134,8 @@ def main() -> int:
                                                      avoid_busy=not a.no_avoid_busy, smt=smt),
                  "smt": smt, "gpu_slots": slots,
                  "host": host,
-                 "base_port": _free_port_block(a.base_port, local_world, host)}]
+                 "base_port": _free_port_block(a.base_port, local_world, host),
+                 "sink_port": sink[1] if sink else 0}]
     if dist:
         dist.broadcast_object_list(plan, src=0)
     server_cpus, load_cpus = plan[0]["cores"][local_rank]["server"], plan[0]["cores"][local_rank]["loadgen"]
@@ -142,6 +154,10 @@ def main() -> int:
     first_rank = rank - local_rank
     bodies = _expected_bodies(a.path, [first_rank + i for i in range(local_world)])
     args = ["--no-tracing"] if a.no_tracing else []
+    if plan[0]["sink_port"]:
+        args += ["--zipkin-url", f"http://127.0.0.1:{plan[0]['sink_port']}/"]
+    if a.trace_queue >= 0:
+        args += ["--trace-queue", str(a.trace_queue)]
     if host != "127.0.0.1":
         args += ["--host", host]
     if a.epoll_lt:
@@ -174,6 +190,9 @@ def main() -> int:
         if dist:
             dist.barrier()
         cuda()
+        span0 = _span_counters(host, port)
+        sink0 = _sink_stats(plan[0]["sink_port"]) if local_rank == 0 else {}
+        tracer0 = _thread_cpu_s(server.proc.pid, "hola-tracer")
         cpu0 = (_proc_cpu_s(server.proc.pid), _proc_cpu_s(loadgen.proc.pid))
         tcp0 = _tcp_counters()
         thr0 = _cgroup_cpu_stat()
@@ -188,6 +207,9 @@ def main() -> int:
         cuda()
         elapsed = time.perf_counter() - t0
         cpu1 = (_proc_cpu_s(server.proc.pid), _proc_cpu_s(loadgen.proc.pid))
+        tracer1 = _thread_cpu_s(server.proc.pid, "hola-tracer")
+        span1 = _span_counters(host, port)
+        sink1 = _sink_stats(plan[0]["sink_port"]) if local_rank == 0 else {}
         tcp1 = _tcp_counters()
         thr1 = _cgroup_cpu_stat()
         st = loadgen.stats()
@@ -197,6 +219,9 @@ def main() -> int:
         local = {"elapsed": elapsed, "requests": reqs, "errors": errs, "hist": st.get("hist", ""),
                  "non2xx": st.get("non2xx", 0), "body_checked": st.get("body_checked", 0),
                  "body_mismatch": st.get("body_mismatch", 0), "c1": c1,
+                 "spans": {k: span1[k] - span0.get(k, 0) for k in span1},
+                 "sink": {k: sink1[k] - sink0.get(k, 0) for k in sink1},
+                 "tracer_cpu_s": tracer1 - tracer0,
                  "server_cpus": format_cpu_list(server_cpus),
                  "load_cpus": format_cpu_list(load_cpus),
                  "server_cpu_s": cpu1[0] - cpu0[0], "loadgen_cpu_s": cpu1[1] - cpu0[1],
@@ -212,6 +237,9 @@ def main() -> int:
         if loadgen:
             loadgen.close()
         server.stop()
+        if sink:
+            sink[0].terminate()
+            sink[0].wait(timeout=10)
 
     if rank == 0:
         t = max(g["elapsed"] for g in gathered)
@@ -260,6 +288,8 @@ def main() -> int:
             "body_mismatch": sum(g["body_mismatch"] for g in gathered),
             # BASELINE config 2 (1 connection, 1 replica), measured after the timed region
             **_c1_keys(gathered[0]["c1"]),
+            # span accounting over the timed region, all replicas (per second)
+            "tracing": _tracing_block(a, gathered, t, plan[0]["sink_port"]),
             "config": {
                 "model": "hola GET /api/hola (native C++ replica, default greeting, "
                          + ("tracing off" if a.no_tracing else
@@ -295,6 +325,85 @@ def main() -> int:
             dist.barrier()
             dist.destroy_process_group()
     return 0
+
+
+def _start_sink():
+    """Native discard Zipkin collector on an ephemeral port: (process, port)."""
+    import subprocess
+    import tempfile
+
+    from hola_amd.native import binary
+
+    pf = Path(tempfile.mkdtemp(prefix="hola_sink_")) / "port"
+    proc = subprocess.Popen([str(binary("hola_zipkin_sink")), "--port", "0", "--port-file", str(pf)])
+    deadline = time.monotonic() + 10
+    while not pf.exists():
+        if proc.poll() is not None or time.monotonic() > deadline:
+            raise RuntimeError("hola_zipkin_sink did not start")
+        time.sleep(0.01)
+    return proc, int(pf.read_text())
+
+
+def _sink_stats(port: int) -> dict:
+    if not port:
+        return {}
+    from hola_amd.utils.net import http_get
+    st, _, body = http_get("127.0.0.1", port, "/stats")
+    return json.loads(body) if st == 200 else {}
+
+
+def _span_counters(host: str, port: int) -> dict:
+    """hola_spans_* counters from a replica's /metrics (empty with tracing off)."""
+    from hola_amd.utils.net import http_get
+    try:
+        st, _, body = http_get(host, port, "/metrics")
+    except OSError:
+        return {}
+    out = {}
+    for line in body.decode().splitlines() if st == 200 else []:
+        if line.startswith("hola_spans_recorded_total "):
+            out["recorded"] = int(float(line.split()[1]))
+        elif line.startswith("hola_spans_reported_total "):
+            out["reported"] = int(float(line.split()[1]))
+        elif line.startswith("hola_spans_dropped_total{reason="):
+            out["dropped_" + line.split('"')[1]] = int(float(line.rsplit(" ", 1)[1]))
+    return out
+
+
+def _thread_cpu_s(pid: int, name: str) -> float:
+    """user+system CPU seconds of the thread of `pid` whose comm is `name` (0 if none)."""
+    total = 0.0
+    for task in Path(f"/proc/{pid}/task").glob("*"):
+        try:
+            if (task / "comm").read_text().strip() != name:
+                continue
+            fields = (task / "stat").read_text().rsplit(")", 1)[1].split()
+            total += (int(fields[11]) + int(fields[12])) / os.sysconf("SC_CLK_TCK")
+        except (OSError, IndexError, ValueError):
+            pass
+    return total
+
+
+def _tracing_block(a, gathered: list[dict], t: float, sink_port: int) -> dict:
+    if a.no_tracing:
+        return {"mode": "off"}
+    spans: dict[str, int] = {}
+    for g in gathered:
+        for k, v in g["spans"].items():
+            spans[k] = spans.get(k, 0) + v
+    per_s = {k: round(v / t, 1) for k, v in sorted(spans.items())} if t > 0 else {}
+    out = {"mode": "collector: native discard sink (hola_zipkin_sink)" if sink_port else
+           "no collector (ZIPKIN_SERVER_URL unset): spans counted and dropped at the source",
+           "trace_queue_per_flush": a.trace_queue if a.trace_queue >= 0 else 1000,
+           "spans_per_s": per_s,
+           # reporter thread CPU (drain rings, encode Zipkin JSON, POST), % of one core, summed
+           "reporter_cpu_pct": round(100.0 * sum(g["tracer_cpu_s"] for g in gathered) / t, 2) if t > 0 else 0.0}
+    if sink_port and gathered[0]["sink"]:
+        s = gathered[0]["sink"]
+        out["sink_received_spans_per_s"] = round(s.get("spans", 0) / t, 1) if t > 0 else 0.0
+        out["sink_posts"] = s.get("posts", 0)
+        out["sink_bad"] = s.get("bad", 0)
+    return out
 
 
 def _expected_bodies(path: str, ranks: list[int]) -> list[str] | None:

@@ -81,9 +81,7 @@ int connect_backend(Backend** chosen, bool* in_progress) {
     }
     // Out of local fds, memory or ephemeral ports: the next backend would fail the same
     // way, and none of them is at fault.
-    if (errno == EMFILE || errno == ENFILE || errno == ENOBUFS || errno == ENOMEM || errno == EAGAIN ||
-        errno == EADDRNOTAVAIL)
-      return -1;
+    if (is_local_resource_error(errno)) return -1;
     mark_down(b, errno);
   }
   return -1;
@@ -399,7 +397,7 @@ void health_loop(int interval_ms) {
       bool ok = client::blocking_request(u, &fd, "GET", "/api/health", "", "", 1000, &r) && r.status == 200;
       const int err = errno;
       if (fd >= 0) ::close(fd);
-      if (!ok && (err == EMFILE || err == ENFILE || err == ENOBUFS || err == ENOMEM)) continue;  // local, not the backend
+      if (!ok && is_local_resource_error(err)) continue;  // local, not the backend
       bool was = b->healthy.exchange(ok);
       if (was != ok) fprintf(stderr, "rrproxy: backend %s:%d is %s\n", b->host.c_str(), b->port, ok ? "UP" : "DOWN");
     }

@@ -19,7 +19,7 @@ from pathlib import Path
 
 REPO = Path(__file__).resolve().parent.parent
 BUILD_ROOT = REPO / "build"
-BINARIES = ("hola", "hola_loadgen", "hola_rrproxy")
+BINARIES = ("hola", "hola_loadgen", "hola_rrproxy", "hola_zipkin_sink")
 
 # preset name -> extra CMake arguments
 PRESETS = {

@@ -300,7 +300,8 @@ void HolaApp::on_request(http::Connection& c, const http::Request& r) {
   char decoded[512];
   if (path.find('%') != std::string_view::npos) {
     size_t n = 0;
-    if (path.size() <= sizeof decoded && http::percent_decode(path, decoded, &n)) path = std::string_view(decoded, n);
+    if (path.size() <= sizeof decoded && http::percent_decode(path, decoded, &n, /*keep_encoded_slash=*/true))
+      path = std::string_view(decoded, n);
   }
   char canonical[512];
   if (__builtin_expect(path.find("/.") != std::string_view::npos, 0)) {
@@ -319,23 +320,37 @@ void HolaApp::on_request(http::Connection& c, const http::Request& r) {
     case kChaining:
     case kSwagger:
     case kSwaggerYaml: {
+      // ZipKinFilter maps BraveServletFilter to exactly /api/hola and /api/hola-chaining for
+      // every method (ZipKinFilter.java:43): OPTIONS, 405 and 406 answers get a server span,
+      // while /api/hola/ (which JAX-RS still serves) does not match the servlet pattern.
+      const bool traced = (route == kHola || route == kChaining) && path.back() != '/' && tracer_ &&
+                          tracer_->enabled();
+      auto send_traced = [&](std::string_view resp, int status) {
+        if (!traced) {
+          c.send(resp);
+          return;
+        }
+        tracing::ServerSpan span = tracer_->begin_server(w.index(), r);
+        c.send(resp);
+        tracer_->end_server(w.index(), span, status);
+      };
       if (m == Method::kOptions) {
-        c.send(wc.api_options[ka].view());
+        send_traced(wc.api_options[ka].view(), 200);
         return;
       }
       if (m == Method::kOther) {
-        c.send(wc.api_not_allowed[ka].view());
+        send_traced(wc.api_not_allowed[ka].view(), 405);
         return;
       }
       std::string_view subtype = route == kSwaggerYaml ? "yaml"
                                  : (route == kChaining || route == kSwagger) ? "json" : "plain";
       std::string_view type = (route == kChaining || route == kSwagger || route == kSwaggerYaml) ? "application" : "text";
       if (r.has_accept && !http::accepts(r.accept, type, subtype)) {
-        c.send(wc.not_acceptable[ka].view());
+        send_traced(wc.not_acceptable[ka].view(), 406);
         return;
       }
       if (route == kHola) {
-        if (tracer_ && tracer_->enabled()) {
+        if (traced) {
           tracing::ServerSpan span = tracer_->begin_server(w.index(), r);
           c.send(wc.hola[ka][head].view());
           tracer_->end_server(w.index(), span, wc.content && wc.content->ok ? 200 : 500);
@@ -349,7 +364,7 @@ void HolaApp::on_request(http::Connection& c, const http::Request& r) {
       } else if (route == kSwaggerYaml) {
         c.send(wc.swagger_yaml[ka][head].view());
       } else {
-        handle_chaining(c, r, wc, 0);
+        handle_chaining(c, r, wc, traced);
       }
       return;
     }
@@ -390,17 +405,17 @@ void HolaApp::on_request(http::Connection& c, const http::Request& r) {
   }
 }
 
-void HolaApp::handle_chaining(http::Connection& c, const http::Request& r, WorkerCache& wc, int64_t) {
+void HolaApp::handle_chaining(http::Connection& c, const http::Request& r, WorkerCache& wc, bool traced) {
   const int ka = r.keep_alive ? 1 : 0;
   const int head = r.method == "HEAD" ? 1 : 0;
+  tracing::ServerSpan span;
+  if (traced) span = tracer_->begin_server(c.worker().index(), r);
   if (!wc.content || !wc.content->ok) {
     // hola() throws before the downstream call is made (HolaResource.java:75)
     c.send(wc.server_error[ka][head].view());
+    if (traced) tracer_->end_server(c.worker().index(), span, 500);
     return;
   }
-  tracing::ServerSpan span;
-  bool traced = tracer_ && tracer_->enabled();
-  if (traced) span = tracer_->begin_server(c.worker().index(), r);
   const int64_t t0 = mono_ns();
   if (!chainer_) {
     c.send(wc.chaining_fallback[ka][head].view());

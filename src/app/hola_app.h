@@ -86,7 +86,8 @@ class HolaApp final : public http::RequestHandler {
   struct WorkerCache;
   WorkerCache& cache(http::Worker& w);
   void refresh(http::Worker& w, WorkerCache& wc);
-  void handle_chaining(http::Connection& c, const http::Request& r, WorkerCache& wc, int64_t start_us);
+  // `traced`: the request matched ZipKinFilter's servlet pattern (server span around it).
+  void handle_chaining(http::Connection& c, const http::Request& r, WorkerCache& wc, bool traced);
 
   AppOptions o_;
   http::Server* server_ = nullptr;

@@ -40,6 +40,10 @@ int listen_tcp(const ListenOptions& o, std::string* err) {
   return fd;
 }
 
+bool is_local_resource_error(int err) {
+  return err == EMFILE || err == ENFILE || err == ENOBUFS || err == ENOMEM || err == EAGAIN || err == EADDRNOTAVAIL;
+}
+
 int bound_port(int fd) {
   sockaddr_storage ss{};
   socklen_t len = sizeof ss;

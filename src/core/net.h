@@ -31,6 +31,10 @@ int connect_nonblocking(const sockaddr_storage& addr, socklen_t len, bool* in_pr
 // Blocking connect with a timeout in ms; returns fd or -1.
 int connect_blocking(const sockaddr_storage& addr, socklen_t len, int timeout_ms);
 
+// A connect/socket errno caused by this host running out of something (fds, memory,
+// ephemeral ports), not by the peer: it must never mark a backend DOWN.
+bool is_local_resource_error(int err);
+
 void set_nodelay(int fd);
 void set_nonblocking(int fd, bool on = true);
 

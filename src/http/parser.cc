@@ -60,7 +60,7 @@ bool iequals(std::string_view a, std::string_view b) {
   return true;
 }
 
-bool percent_decode(std::string_view in, char* out, size_t* out_len) {
+bool percent_decode(std::string_view in, char* out, size_t* out_len, bool keep_encoded_slash) {
   auto hex = [](char c) -> int {
     if (c >= '0' && c <= '9') return c - '0';
     c = lower(c);
@@ -73,7 +73,13 @@ bool percent_decode(std::string_view in, char* out, size_t* out_len) {
       if (i + 2 >= in.size()) return false;
       int h = hex(in[i + 1]), l = hex(in[i + 2]);
       if (h < 0 || l < 0) return false;
-      out[o++] = char(h * 16 + l);
+      const char d = char(h * 16 + l);
+      if (keep_encoded_slash && d == '/') {
+        memcpy(out + o, in.data() + i, 3);
+        o += 3;
+      } else {
+        out[o++] = d;
+      }
       i += 2;
     } else {
       out[o++] = in[i];

@@ -48,7 +48,9 @@ Parse decode_chunked_body(const char* buf, size_t len, size_t* consumed, std::st
 // Case-insensitive ASCII equality.
 bool iequals(std::string_view a, std::string_view b);
 // Percent-decodes a path; false on malformed escapes. Output written to out (len <= in len).
-bool percent_decode(std::string_view in, char* out, size_t* out_len);
+// With keep_encoded_slash, "%2F" stays encoded (Undertow's default allow-encoded-slash=false),
+// so an encoded slash never becomes a path separator.
+bool percent_decode(std::string_view in, char* out, size_t* out_len, bool keep_encoded_slash = false);
 // Removes "." and ".." segments from an absolute path (RFC 3986 §5.2.4), the way Undertow
 // canonicalises the request path before servlet/JAX-RS matching; false unless `in` starts
 // with '/'. Output written to out (len <= in len).

@@ -522,7 +522,8 @@ void Server::Acceptor::on_event(uint32_t) {
     if (c < 0) {
       if (errno == EINTR || errno == ECONNABORTED) continue;
       if (errno == EMFILE || errno == ENFILE) {
-        LOG_WARN("accept: %s (fd limit); pausing accepts", strerror(errno));
+        if (!paused) LOG_WARN("accept: %s (fd limit); pausing accepts", strerror(errno));
+        paused = true;
         // back off for a moment; the listener stays level-triggered
         worker->loop().del(fd);
         int lfd = fd;
@@ -532,6 +533,10 @@ void Server::Acceptor::on_event(uint32_t) {
         });
       }
       return;
+    }
+    if (paused) {
+      LOG_INFO("accept: resumed after the fd limit");
+      paused = false;
     }
     if (server->opts_.reuseport_accept && !server->steering()) {
       // The kernel already spread connections over the workers' listeners.

@@ -231,6 +231,7 @@ class Server {
     Server* server;
     Worker* worker;
     int fd;
+    bool paused = false;  // at the fd limit: logged once per episode, cleared by the next accept
     void on_event(uint32_t) override;
   };
   ServerOptions opts_;

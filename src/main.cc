@@ -48,6 +48,9 @@ void usage() {
           "  --zipkin-v2              POST /api/v2/spans instead of /api/v1/spans\n"
           "  --trace-sample-rate R    0..1 (default 1)\n"
           "  --no-tracing             disable tracing entirely\n"
+          "  --trace-queue N          spans exported per flush interval, the rest dropped and counted\n"
+          "                           (default 1000: Brave 3's collector queue; 0 = bounded by the rings)\n"
+          "  --trace-ring N           per-worker span ring capacity (default 2048)\n"
           "  --aloha-url URL          downstream service (default http://aloha:8080/)\n"
           "  --aloha-path PATH        downstream path (default api/aloha-chaining)\n"
           "  --feign-log basic|none   outbound call logging (default basic)\n"
@@ -133,6 +136,8 @@ int main(int argc, char** argv) {
     else if (a == "--zipkin-v2") to.v2 = true;
     else if (a == "--trace-sample-rate") to.sample_rate = atof(val("--trace-sample-rate").c_str());
     else if (a == "--no-tracing") no_tracing = true;
+    else if (a == "--trace-queue") to.queue_spans = size_t(atoll(val("--trace-queue").c_str()));
+    else if (a == "--trace-ring") to.ring_capacity = size_t(atoll(val("--trace-ring").c_str()));
     else if (a == "--hystrix-timeout-ms")
       sysprops["hystrix.command.default.execution.isolation.thread.timeoutInMilliseconds"] = val(a.c_str());
     else if (a == "--hystrix-request-volume")

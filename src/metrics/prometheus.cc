@@ -78,7 +78,8 @@ std::string Prometheus::render(http::Server* server) const {
     o += "# TYPE hola_spans_reported_total counter\nhola_spans_reported_total " + std::to_string(t.reported) + "\n";
     o += "# TYPE hola_spans_dropped_total counter\nhola_spans_dropped_total{reason=\"ring_full\"} " +
          std::to_string(t.dropped_ring) + "\nhola_spans_dropped_total{reason=\"collector\"} " +
-         std::to_string(t.dropped_no_collector) + "\n";
+         std::to_string(t.dropped_no_collector) + "\nhola_spans_dropped_total{reason=\"queue_full\"} " +
+         std::to_string(t.dropped_queue) + "\n";
     o += "# TYPE hola_span_post_failures_total counter\nhola_span_post_failures_total " + std::to_string(t.post_failures) + "\n";
   }
   if (cmd_) {

@@ -8,7 +8,10 @@
 #include <thread>
 
 
+#include "app/aloha_chainer.h"
+#include "client/http_client.h"
 #include "config/jformat.h"
+#include "core/net.h"
 #include "config/properties.h"
 #include "config/resolver.h"
 #include "http/negotiate.h"
@@ -344,6 +347,17 @@ PYBIND11_MODULE(_native, m) {
         py::arg("end_us") = 2000, py::arg("url") = "http://localhost/api/hola", py::arg("status") = 200,
         py::arg("shared") = false);
   m.def("histogram_percentiles", &histogram_percentiles);
+  m.def("is_local_resource_error", &is_local_resource_error);
+  m.def("parse_retry_after", [](const std::string& v, int64_t now_ms) -> py::object {
+    int64_t ms = 0;
+    if (!client::parse_retry_after(v, now_ms, &ms)) return py::none();
+    return py::int_(ms);
+  });
+  m.def("feign_backoff_ms", [](int attempt, const std::string& policy) -> py::object {
+    app::RetryPolicy p;
+    if (!app::parse_retry_policy(policy, &p)) return py::none();
+    return py::make_tuple(p.backoff_ms(attempt), p.max_attempts);
+  }, py::arg("attempt"), py::arg("policy") = "default");
   m.def("loop_timer_order", &loop_timer_order, py::arg("delays"), py::arg("cancel") = std::vector<int>{});
   m.def("span_ring", &span_ring);
   m.def("hystrix_stress", &hystrix_stress, py::arg("threads"), py::arg("iters"), py::arg("pool") = 10,

@@ -1,6 +1,7 @@
 #include "tracing/tracer.h"
 
 #include <arpa/inet.h>
+#include <pthread.h>
 #include <poll.h>
 #include <sys/eventfd.h>
 #include <sys/random.h>
@@ -74,6 +75,18 @@ Tracer::Tracer(TracerOptions o, int num_workers) : o_(std::move(o)) {
   // Without a collector, spans are counted and dropped at the source: no rings.
   if (collecting_)
     for (auto& w : ws_) w->ring = std::make_unique<SpanRing>(o_.ring_capacity);
+  budget_.store(o_.queue_spans ? int64_t(o_.queue_spans) : INT64_MAX);
+}
+
+bool Tracer::admit(int worker) {
+  if (o_.queue_spans == 0) return true;
+  // Read first: once the budget is spent, the line stays shared and the check costs a load.
+  if (budget_.load(std::memory_order_relaxed) <= 0 || budget_.fetch_sub(1, std::memory_order_relaxed) <= 0) {
+    auto& d = ws_[size_t(worker)]->over_budget;
+    d.store(d.load(std::memory_order_relaxed) + 1, std::memory_order_relaxed);
+    return false;
+  }
+  return true;
 }
 
 Tracer::~Tracer() {
@@ -123,6 +136,7 @@ ServerSpan Tracer::begin_server(int worker, const http::Request& r) {
     u.store(u.load(std::memory_order_relaxed) + 1, std::memory_order_relaxed);
     return s;
   }
+  if (!admit(worker)) return s;  // sampled (B3 flows on) but not exported this interval
   s.record = true;
   s.start_us = wall_us();
   s.method_len = uint8_t(r.method.size() < sizeof s.method ? r.method.size() : sizeof s.method);
@@ -185,6 +199,7 @@ void Tracer::record_client(int worker, const SpanContext& ctx, int64_t start_us,
     u.store(u.load(std::memory_order_relaxed) + 1, std::memory_order_relaxed);
     return;
   }
+  if (!admit(worker)) return;
   SpanRecord r;
   r.trace_hi = ctx.trace_hi;
   r.trace_id = ctx.trace_id;
@@ -356,6 +371,8 @@ void Tracer::run() {
     int64_t now = mono_ms();
     if (now - last_post >= o_.flush_interval_ms || pending_.size() >= 5000) {
       post_pending();
+      if (now - last_post >= o_.flush_interval_ms && o_.queue_spans)
+        budget_.store(int64_t(o_.queue_spans), std::memory_order_relaxed);  // next interval's queue
       last_post = now;
     }
   }
@@ -365,6 +382,7 @@ void Tracer::start() {
   if (!o_.enabled || running_) return;
   running_ = true;
   th_ = std::thread([this] { run(); });
+  pthread_setname_np(th_.native_handle(), "hola-tracer");  // bench.py reads its CPU time
 }
 
 void Tracer::stop() {
@@ -385,6 +403,7 @@ TracerStats Tracer::stats() const {
   for (auto& w : ws_) {
     s.recorded += w->recorded.load(std::memory_order_relaxed);
     s.dropped_ring += w->dropped.load(std::memory_order_relaxed);
+    s.dropped_queue += w->over_budget.load(std::memory_order_relaxed);
   }
   s.reported = reported_.load();
   s.dropped_no_collector = dropped_no_collector_.load();

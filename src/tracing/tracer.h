@@ -6,6 +6,13 @@
 // 50 ms (so they stay cache-resident) and POSTs Zipkin v1 JSON to
 // $ZIPKIN_SERVER_URL/api/v1/spans about every second (v2 optional). When the collector is
 // unset or down, spans are dropped and counted — never blocking a worker.
+//
+// Export budget (the explicit drop policy): at most `queue_spans` spans are admitted per
+// flush interval — Brave 3's AbstractSpanCollector queues at most 1000 spans between its
+// 1 s flushes and drops (and counts) the rest. The budget is one shared counter that the
+// reporter refills each flush; a worker reads it before recording, so once it is spent a
+// span costs one read of a cache line nobody writes, and is counted as dropped
+// ("queue_full"). Trace ids still propagate downstream in B3 headers either way.
 #pragma once
 #include <atomic>
 #include <cstdint>
@@ -80,10 +87,14 @@ struct TracerOptions {
   uint32_t ipv4 = 0;                  // endpoint address (network order)
   int port = 8080;
   size_t ring_capacity = 2048;
+  // Spans admitted for export per flush interval (Brave 3 AbstractSpanCollector: a 1000-span
+  // queue). 0 = unlimited (bounded only by the rings: ring_capacity per drain interval).
+  size_t queue_spans = 1000;
 };
 
 struct TracerStats {
-  uint64_t recorded = 0, dropped_ring = 0, dropped_no_collector = 0, reported = 0, post_failures = 0;
+  uint64_t recorded = 0, dropped_ring = 0, dropped_no_collector = 0, dropped_queue = 0, reported = 0,
+           post_failures = 0;
 };
 
 class Tracer {
@@ -112,6 +123,8 @@ class Tracer {
 
  private:
   uint64_t next_id(int worker);
+  // Takes one span from this flush interval's export budget; false (and counted) when spent.
+  bool admit(int worker);
   void push(int worker, const SpanRecord& r);
   void run();
   bool post(const std::string& body);
@@ -121,7 +134,7 @@ class Tracer {
   struct alignas(64) WorkerState {
     uint64_t s0, s1;  // xorshift128+
     std::unique_ptr<SpanRing> ring;
-    std::atomic<uint64_t> recorded{0}, dropped{0}, unreported{0};
+    std::atomic<uint64_t> recorded{0}, dropped{0}, unreported{0}, over_budget{0};
   };
   std::vector<std::unique_ptr<WorkerState>> ws_;
   std::thread th_;
@@ -130,6 +143,7 @@ class Tracer {
   bool running_ = false;  // start()/stop() are called from the owning (main) thread
   std::mutex flush_mu_;
   std::atomic<uint64_t> reported_{0}, dropped_no_collector_{0}, post_failures_{0};
+  alignas(64) std::atomic<int64_t> budget_{0};  // spans still admissible this flush interval
   bool collecting_ = false;            // a collector URL is configured
   std::vector<SpanRecord> pending_;    // drained, not yet posted (reporter thread / flush)
   void drain_rings();

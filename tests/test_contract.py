@@ -145,6 +145,17 @@ def test_dot_segments_are_removed_before_matching(hola):
     assert s.get("/api/hola/..")[0] == 404                   # -> /api/
 
 
+def test_encoded_slash_is_not_a_separator(hola):
+    """Undertow's default allow-encoded-slash=false leaves %2F encoded, so it never splits a
+    segment: /api%2Fhola and /api/x%2F..%2Fhola are 404 (parity unpinned: no reference
+    artefact covers it)."""
+    s = hola(env={"HOSTNAME": "h"})
+    assert s.get("/api%2Fhola")[0] == 404
+    assert s.get("/api%2fhola")[0] == 404
+    assert s.get("/api/x%2F..%2Fhola")[0] == 404
+    assert s.get("/api/hol%61")[2] == b"Hola de h"  # other escapes still decode
+
+
 def _raw(port, data: bytes, timeout=3.0) -> bytes:
     with socket.create_connection(("127.0.0.1", port), timeout=timeout) as c:
         c.sendall(data)

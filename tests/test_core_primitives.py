@@ -29,3 +29,37 @@ def test_span_ring_bounded_and_ordered(native):
     assert ok == 8 and drained == 8  # the ring drops (and the tracer counts) the rest
     ok, drained = native.span_ring(1024, 1000)
     assert ok == drained == 1000
+
+
+def test_local_resource_errors_never_blame_a_backend(native):
+    """rrproxy's connect path and health checker share one classification: running out of
+    fds, memory or ephemeral ports (EADDRNOTAVAIL) is local, a refusal is the backend's."""
+    import errno
+
+    for e in (errno.EMFILE, errno.ENFILE, errno.ENOBUFS, errno.ENOMEM, errno.EAGAIN, errno.EADDRNOTAVAIL):
+        assert native.is_local_resource_error(e)
+    for e in (errno.ECONNREFUSED, errno.ETIMEDOUT, errno.EHOSTUNREACH, errno.ECONNRESET):
+        assert not native.is_local_resource_error(e)
+
+
+def test_retry_after_parsing(native):
+    """Feign's RetryAfterDecoder formats: delta-seconds or an RFC 1123 date."""
+    import calendar
+
+    assert native.parse_retry_after("0", 0) == 0
+    assert native.parse_retry_after("3", 0) == 3000
+    now = calendar.timegm((2015, 10, 21, 7, 28, 0)) * 1000
+    assert native.parse_retry_after("Wed, 21 Oct 2015 07:28:02 GMT", now) == 2000
+    assert native.parse_retry_after("Wed, 21 Oct 2015 07:27:59 GMT", now) == -1000  # in the past
+    assert native.parse_retry_after("soon", now) is None
+    assert native.parse_retry_after("", now) is None
+
+
+def test_feign_retryer_default_backoff(native):
+    """Retryer.Default(100 ms, 1 s, 5): sleeps 150, 225, 337, 506 ms between 5 attempts,
+    capped at the 1 s max period."""
+    assert [native.feign_backoff_ms(n)[0] for n in (1, 2, 3, 4)] == [150, 225, 337, 506]
+    assert native.feign_backoff_ms(1)[1] == 5
+    assert native.feign_backoff_ms(9, "100,1000,12")[0] == 1000
+    assert native.feign_backoff_ms(1, "off")[1] == 1
+    assert native.feign_backoff_ms(1, "bogus") is None

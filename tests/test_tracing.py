@@ -179,3 +179,76 @@ def test_sample_rate_half(hola, zipkin):
         s.get("/api/hola")
     spans = zipkin.wait_for(lambda sp: len(sp) >= 120, timeout=5)
     assert 120 <= len(spans) <= 280
+
+
+def test_export_budget_drops_beyond_the_queue(hola, zipkin):
+    """At most --trace-queue spans are exported per flush interval (Brave 3's collector
+    queue holds 1000); the rest are counted as dropped with reason queue_full."""
+    s = hola(args=["--zipkin-url", zipkin.url, "--trace-queue", "5"], threads=1)
+    for _ in range(20):
+        assert s.get("/api/hola")[0] == 200
+    spans = zipkin.wait_for(lambda sp: len(sp) >= 5)
+    time.sleep(1.3)  # one more flush: nothing beyond the budget arrives
+    assert len(zipkin.spans()) == 5
+    st, _, body = s.get("/metrics")
+    assert b'hola_spans_dropped_total{reason="queue_full"} 15' in body
+    assert b"hola_spans_reported_total 5" in body
+    for _ in range(3):  # the next interval has a fresh budget
+        s.get("/api/hola")
+    assert len(zipkin.wait_for(lambda sp: len(sp) >= 8)) == 8
+
+
+def test_native_discard_sink_counts_spans(hola_bin):
+    """bench/zipkin_sink.cc (the bench's collector) answers 202 and counts every span of
+    v1 and v2 batches."""
+    import subprocess
+    import tempfile
+    from pathlib import Path
+
+    from hola_amd.native import binary
+    from hola_amd.server import HolaProcess
+    from hola_amd.utils.net import http_get
+
+    pf = Path(tempfile.mkdtemp()) / "port"
+    sink = subprocess.Popen([str(binary("hola_zipkin_sink")), "--port", "0", "--port-file", str(pf)])
+    try:
+        deadline = time.monotonic() + 10
+        while not pf.exists() and time.monotonic() < deadline:
+            time.sleep(0.01)
+        port = int(pf.read_text())
+        for extra in ([], ["--zipkin-v2"]):
+            s = HolaProcess(args=["--zipkin-url", f"http://127.0.0.1:{port}/", *extra]).start()
+            for _ in range(10):
+                s.get("/api/hola")
+            s.get("/api/health")  # not traced
+            s.stop()  # flushes
+        st, _, body = http_get("127.0.0.1", port, "/stats")
+        stats = json.loads(body)
+        assert st == 200 and stats["spans"] == 20 and stats["bad"] == 0 and stats["posts"] >= 2
+        assert http_get("127.0.0.1", port, "/api/v1/spans", method="POST", body=b"[]")[0] == 202
+    finally:
+        sink.terminate()
+        sink.wait(timeout=10)
+
+
+def test_filter_pattern_traces_every_method_on_exact_paths(hola, zipkin):
+    """BraveServletFilter is mapped to exactly /api/hola and /api/hola-chaining for all
+    methods (ZipKinFilter.java:43): OPTIONS, 405 and 406 answers there get a server span;
+    /api/hola/ is served (JAX-RS tolerates the slash) but does not match the pattern."""
+    s = hola(args=["--zipkin-url", zipkin.url], threads=1)
+    assert s.get("/api/hola", method="OPTIONS")[0] == 200
+    assert s.get("/api/hola", method="POST")[0] == 405
+    assert s.get("/api/hola", headers={"Accept": "application/json"})[0] == 406
+    assert s.get("/api/hola-chaining", method="DELETE")[0] == 405
+    assert s.get("/api/hola/")[0] == 200
+    assert s.get("/api/hola-chaining/", method="OPTIONS")[0] == 200
+    spans = zipkin.wait_for(lambda sp: len(sp) >= 4)
+    time.sleep(1.2)
+    spans = zipkin.spans()
+    assert len(spans) == 4
+    names = sorted(sp["name"] for sp in spans)
+    assert names == ["delete", "get", "options", "post"]
+    codes = sorted(b["value"] for sp in spans for b in sp["binaryAnnotations"] if b["key"] == "http.status_code")
+    assert codes == ["405", "405", "406"]
+    urls = [b["value"] for sp in spans for b in sp["binaryAnnotations"] if b["key"] == "http.url"]
+    assert not any(u.endswith("/") for u in urls)
