@@ -30,7 +30,8 @@ from hola_amd.native import ensure_built  # noqa: E402
 from hola_amd.parallel.loadgen import ControlledLoadgen, decode_hist, merge_hists, percentile  # noqa: E402
 from hola_amd.server import HolaProcess  # noqa: E402
 from hola_amd.utils.cpu import (  # noqa: E402
-    cgroup_cpu_quota, cpu_budget, format_cpu_list, plan_replicas_with_loadgen, siblings, slot_cores, smt_fits)
+    cgroup_cpu_quota, connection_targets, cpu_budget, format_cpu_list, plan_replicas_with_loadgen, siblings,
+    slot_cores, smt_fits)
 
 METRIC = "HTTP req/sec + p50/p99 latency, GET /api/hola at 1/2/4/8 replicas"
 BASELINE_VALUE = None  # the reference publishes no numbers
@@ -139,6 +140,10 @@ def main() -> int:
     if dist:
         dist.broadcast_object_list(plan, src=0)
     server_cpus, load_cpus = plan[0]["cores"][local_rank]["server"], plan[0]["cores"][local_rank]["loadgen"]
+    thread_targets = plan[0]["cores"][local_rank].get("thread_targets")
+    # Each load-generator thread drives only replicas in its own L3 (see
+    # plan_replicas_with_loadgen); None = plain (i + rank) % N dealing.
+    conn_targets = connection_targets(thread_targets, a.connections) if thread_targets else None
     s_threads = len(server_cpus)
     smt = plan[0]["smt"]
     if a.busy_poll_pause < 0:
@@ -181,7 +186,7 @@ def main() -> int:
                                     path=a.path, target_offset=local_rank, busy_poll_us=a.busy_poll_us,
                                     busy_poll_pause=a.busy_poll_pause, epoll_lt=a.epoll_lt,
                                     per_conn_quota=a.per_conn_quota, pipeline=a.pipeline,
-                                    expect_bodies=bodies, verify_body=bodies is None)
+                                    expect_bodies=bodies, verify_body=bodies is None, conn_targets=conn_targets)
         for _ in range(a.warmup):
             loadgen.run(a.reqs_per_conn)
         loadgen.reset()
@@ -209,6 +214,7 @@ def main() -> int:
         cpu1 = (_proc_cpu_s(server.proc.pid), _proc_cpu_s(loadgen.proc.pid))
         tracer1 = _thread_cpu_s(server.proc.pid, "hola-tracer")
         span1 = _span_counters(host, port)
+        locality = _accept_locality(host, port)
         sink1 = _sink_stats(plan[0]["sink_port"]) if local_rank == 0 else {}
         tcp1 = _tcp_counters()
         thr1 = _cgroup_cpu_stat()
@@ -222,6 +228,7 @@ def main() -> int:
                  "spans": {k: span1[k] - span0.get(k, 0) for k in span1},
                  "sink": {k: sink1[k] - sink0.get(k, 0) for k in sink1},
                  "tracer_cpu_s": tracer1 - tracer0,
+                 "locality": locality,
                  "server_cpus": format_cpu_list(server_cpus),
                  "load_cpus": format_cpu_list(load_cpus),
                  "server_cpu_s": cpu1[0] - cpu0[0], "loadgen_cpu_s": cpu1[1] - cpu0[1],
@@ -290,6 +297,8 @@ def main() -> int:
             **_c1_keys(gathered[0]["c1"]),
             # span accounting over the timed region, all replicas (per second)
             "tracing": _tracing_block(a, gathered, t, plan[0]["sink_port"]),
+            # client thread vs. serving worker placement of every accepted connection
+            "locality": _locality_block(gathered),
             "config": {
                 "model": "hola GET /api/hola (native C++ replica, default greeting, "
                          + ("tracing off" if a.no_tracing else
@@ -301,7 +310,8 @@ def main() -> int:
                 "connections_per_replica": a.connections,
                 "reqs_per_conn_per_step": a.reqs_per_conn,
                 "pipeline": a.pipeline,
-                "lb": "client-side round-robin over replica ports",
+                "lb": "client-side round-robin over replica ports" + (
+                    "" if world == 1 else ", each load-generator thread on the L3 of the replicas it drives"),
                 "loopback": host,
                 "cores_per_replica": len({min(siblings(c)) for c in list(server_cpus) + list(load_cpus)}),
                 "server_threads_per_replica": s_threads,
@@ -368,6 +378,37 @@ def _span_counters(host: str, port: int) -> dict:
         elif line.startswith("hola_spans_dropped_total{reason="):
             out["dropped_" + line.split('"')[1]] = int(float(line.rsplit(" ", 1)[1]))
     return out
+
+
+def _accept_locality(host: str, port: int) -> dict:
+    """hola_accept_locality_total from a replica's /metrics: where each accepted connection's
+    client thread ran relative to the worker serving it (same_core / same_l3 / same_socket /
+    cross_socket / unknown)."""
+    from hola_amd.utils.net import http_get
+    try:
+        st, _, body = http_get(host, port, "/metrics")
+    except OSError:
+        return {}
+    out = {}
+    for line in body.decode().splitlines() if st == 200 else []:
+        if line.startswith("hola_accept_locality_total{relation="):
+            out[line.split('"')[1]] = int(float(line.rsplit(" ", 1)[1]))
+    return out
+
+
+def _locality_block(gathered: list[dict]) -> dict:
+    """Node-wide and per-replica fractions of accepted connections by client/worker
+    relation. The bench's connections are all made before the timed region, so this is the
+    placement of every timed request's connection (minus the /metrics probes: 1-2 each)."""
+    def frac(d: dict) -> dict:
+        n = sum(d.values())
+        return {k: round(v / n, 4) for k, v in d.items()} if n else {}
+    total: dict[str, int] = {}
+    for g in gathered:
+        for k, v in g["locality"].items():
+            total[k] = total.get(k, 0) + v
+    return {"accepted": sum(total.values()), "fraction": frac(total),
+            "per_replica": [frac(g["locality"]) for g in gathered]}
 
 
 def _thread_cpu_s(pid: int, name: str) -> float:

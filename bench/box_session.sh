@@ -11,7 +11,8 @@
 #                      CPU slice, plus --profile-dir stage profiles for locality attribution
 #   latency            BASELINE config 2 (1 connection) and the open-loop latency curve
 #   chain              two-hop chaining bench (loadgen -> hola A -> hola B)
-#   tracing            headline with a native Zipkin sink attached vs. without a collector
+#   tracing            headline without a collector, with the native Zipkin sink (default 1000-span
+#                      export budget, and unbounded), and with tracing off
 #   soak MINUTES       mixed-load soak sampling RSS and FDs
 #
 # Every GPU-box step runs under its own `timeout -k`, steps are chained with &&, and the
@@ -63,8 +64,11 @@ chain)
   timeout -k 10 120 python bench/chain_bench.py --duration 10 --out "$OUT/chain.json" > "$OUT/chain.log" 2>&1
   ;;
 tracing)
-  timeout -k 10 300 python bench.py --steps 15 --warmup 3 > "$OUT/no_collector.json" 2>> "$OUT/err.log" &&
-  timeout -k 10 300 python bench.py --steps 15 --warmup 3 --zipkin-sink > "$OUT/sink.json" 2>> "$OUT/err.log"
+  timeout -k 10 300 python bench.py --steps 15 --warmup 3 --c1-reqs 0 > "$OUT/no_collector.json" 2>> "$OUT/err.log" &&
+  timeout -k 10 300 python bench.py --steps 15 --warmup 3 --c1-reqs 0 --zipkin-sink > "$OUT/sink.json" 2>> "$OUT/err.log" &&
+  timeout -k 10 300 python bench.py --steps 15 --warmup 3 --c1-reqs 0 --zipkin-sink --trace-queue 0 \
+    > "$OUT/sink_unbounded.json" 2>> "$OUT/err.log" &&
+  timeout -k 10 300 python bench.py --steps 15 --warmup 3 --c1-reqs 0 --no-tracing > "$OUT/tracing_off.json" 2>> "$OUT/err.log"
   ;;
 soak)
   MIN=${1:-5}

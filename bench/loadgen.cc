@@ -90,6 +90,7 @@ struct Options {
   int pipeline = 1;  // requests per batch (closed loop only)
   std::vector<std::string> expect_bodies;  // --expect-body: per target, or one for all
   bool verify_body = false;                // --verify-body: learn the first 2xx body per target
+  std::vector<int> conn_targets;           // --conn-targets: target index of connection i (cycled)
 };
 
 struct Conn {
@@ -233,7 +234,8 @@ void thread_main(ThreadState* ts, const Options* o) {
   // replica on the other socket from main()'s.
   for (int i : ts->conn_ids) {
     auto c = std::make_unique<Conn>();
-    c->target = (i + o->target_offset) % int(o->targets.size());
+    c->target = o->conn_targets.empty() ? (i + o->target_offset) % int(o->targets.size())
+                                        : o->conn_targets[size_t(i) % o->conn_targets.size()];
     const Target& t = o->targets[size_t(c->target)];
     const bool v6 = t.host.find(':') != std::string::npos;  // RFC 3986 IP-literal in Host
     c->req = o->method + " " + o->path + " HTTP/1.1\r\nHost: " + (v6 ? "[" + t.host + "]" : t.host) + ":" +
@@ -659,12 +661,18 @@ int main(int argc, char** argv) {
     else if (a == "--pipeline") o.pipeline = atoi(val().c_str());
     else if (a == "--expect-body") o.expect_bodies.push_back(unescape(val()));
     else if (a == "--verify-body") o.verify_body = true;
+    else if (a == "--conn-targets") {
+      if (!parse_cpu_list(val(), &o.conn_targets)) {  // same "0,1,1,0" / "0-3" syntax
+        fprintf(stderr, "loadgen: bad --conn-targets\n");
+        return 2;
+      }
+    }
     else {
       fprintf(stderr,
               "usage: hola_loadgen --targets h:p[,h:p..] -c CONNS -t THREADS [--cpu-list L] [--path P]\n"
               "                    (--duration S [--warmup S] [--rate R [--spin-us N]] | --control [--per-conn-quota])\n"
               "                    [--target-offset K] [--busy-poll-us N [--busy-poll-pause P]] [--epoll-lt] [-H 'Name: v']\n"
-              "                    [--pipeline P] [--expect-body B]... [--verify-body]\n"
+              "                    [--pipeline P] [--expect-body B]... [--verify-body] [--conn-targets i,j,..]\n"
               "       hola_loadgen -t T -c C -d 30s [--latency] [--json] [-H 'Name: v'] http://host:port/path   (wrk style)\n");
       return 2;
     }
@@ -677,6 +685,11 @@ int main(int argc, char** argv) {
   }
   const bool wrk_text = !url.empty() && !json && !o.control;
   if (!parse_targets(targets, &o.targets)) return 2;
+  for (int t : o.conn_targets)
+    if (t < 0 || size_t(t) >= o.targets.size()) {
+      fprintf(stderr, "loadgen: --conn-targets index %d out of range\n", t);
+      return 2;
+    }
   if (!cpu_list.empty() && !parse_cpu_list(cpu_list, &o.cpus)) {
     fprintf(stderr, "loadgen: bad --cpu-list\n");
     return 2;

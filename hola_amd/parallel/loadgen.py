@@ -73,7 +73,8 @@ class ControlledLoadgen:
                  cpu_list: str | None = None, path: str = "/api/hola", target_offset: int = 0,
                  headers: list[str] | None = None, busy_poll_us: int = 0, per_conn_quota: bool = False,
                  busy_poll_pause: int = 0, epoll_lt: bool = False, pipeline: int = 1,
-                 expect_bodies: list[str] | None = None, verify_body: bool = False):
+                 expect_bodies: list[str] | None = None, verify_body: bool = False,
+                 conn_targets: list[int] | None = None):
         cmd = [str(binary("hola_loadgen")), "--targets", ",".join(f"{h}:{p}" for h, p in targets),
                "-c", str(connections), "-t", str(threads), "--path", path, "--control",
                "--target-offset", str(target_offset)] + body_args(expect_bodies, verify_body)
@@ -91,6 +92,8 @@ class ControlledLoadgen:
             cmd += ["--epoll-lt"]
         if pipeline > 1:
             cmd += ["--pipeline", str(pipeline)]
+        if conn_targets:
+            cmd += ["--conn-targets", ",".join(map(str, conn_targets))]
         self.proc = subprocess.Popen(cmd, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, bufsize=1)
         ready = self._read()
         if not ready.get("ready"):

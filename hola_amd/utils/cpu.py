@@ -213,11 +213,18 @@ def plan_replicas_with_loadgen(local_world: int, per_rank: int | None = None, se
     """Core plan for `local_world` co-located (replica + load generator) ranks with
     client-side round-robin over all replicas.
 
-    Rank r's load-generator thread t drives replica (t + r) % N (connection i -> thread i % T,
-    target (i + r) % N, so with T % N == 0 each thread talks to exactly one replica). Its CPU
-    is therefore taken from the *target* replica's L3 domains, so every connection's client
-    and server ends share an L3 even though traffic crosses ranks. Returns, per rank,
-    {"server": [...], "loadgen": [... one CPU per thread, in thread order]}.
+    Connection i of a rank's load generator runs on thread t = i % T. Each thread drives only
+    the replicas in ``thread_targets[t]``, and its CPU is taken from *those* replicas' L3
+    domains, so every connection's client and server ends share an L3 even though traffic
+    crosses ranks:
+      * T % N == 0: thread t of rank r drives replica (t + r) % N alone;
+      * N % T == 0 (fewer threads than replicas, e.g. 2 threads and 4 replicas on a 16-CPU
+        slice): the replicas form T groups of N/T consecutive ranks (which plan_node puts in
+        one L3); thread t of rank r drives group (t + r) % T;
+      * otherwise ``thread_targets`` is None and connections are dealt (i + r) % N.
+    Every replica still receives the same number of connections from every rank (client-side
+    round-robin in aggregate). Returns, per rank, {"server": [...], "loadgen": [... one CPU
+    per thread, in thread order], "thread_targets": [[replica, ...] per thread] or None}.
 
     `smt` decides what happens to the SMT sibling of each planned physical core:
       * "off"   - left idle (one thread per physical core);
@@ -250,13 +257,34 @@ def plan_replicas_with_loadgen(local_world: int, per_rank: int | None = None, se
     uniform = all(len(sp[1]) == t_threads for sp in splits)
     plans = []
     for r in range(n):
-        if n > 1 and uniform and t_threads % n == 0:
+        targets = None
+        if n == 1:
+            load = splits[0][1]
+            targets = [[0] for _ in load]
+        elif uniform and t_threads % n == 0:
             per = t_threads // n
             load = [splits[(t + r) % n][1][r * per + t // n] for t in range(t_threads)]
+            targets = [[(t + r) % n] for t in range(t_threads)]
+        elif uniform and n % t_threads == 0:
+            per = n // t_threads  # replicas per group
+            load, targets = [], []
+            for t in range(t_threads):
+                g = (t + r) % t_threads
+                members = [g * per + j for j in range(per)]
+                pool = [c for m in members for c in splits[m][1]]  # per * T CPUs, one per rank
+                load.append(pool[r])
+                targets.append([members[(j + r) % per] for j in range(per)])
         else:
             load = splits[r][1]
-        plans.append({"server": splits[r][0], "loadgen": load})
+        plans.append({"server": splits[r][0], "loadgen": load, "thread_targets": targets})
     return plans
+
+
+def connection_targets(thread_targets: list[list[int]], connections: int) -> list[int]:
+    """Target replica of each connection (connection i runs on thread i % T)."""
+    t_threads = len(thread_targets)
+    return [thread_targets[i % t_threads][(i // t_threads) % len(thread_targets[i % t_threads])]
+            for i in range(connections)]
 
 
 def plan_mirrored(weights: dict[str, int], total: int | None = None, avoid_busy: bool = True) -> dict[str, list[int]]:

@@ -114,6 +114,26 @@ int core_of(int cpu) {
   return (cpu >= 0 && size_t(cpu) < table.size()) ? table[size_t(cpu)] : -1;
 }
 
+int package_of(int cpu) {
+  static const std::vector<int> table = [] {
+    std::vector<int> v;
+    for (int c = 0; c < CPU_SETSIZE; ++c) {
+      std::ifstream f("/sys/devices/system/cpu/cpu" + std::to_string(c) + "/topology/physical_package_id");
+      if (!f) {
+        std::ifstream online("/sys/devices/system/cpu/cpu" + std::to_string(c));
+        if (!online) break;  // past the last CPU
+        v.push_back(-1);
+        continue;
+      }
+      int id = -1;
+      if (!(f >> id)) id = -1;
+      v.push_back(id);
+    }
+    return v;
+  }();
+  return (cpu >= 0 && size_t(cpu) < table.size()) ? table[size_t(cpu)] : -1;
+}
+
 double cgroup_cpu_quota() {
   std::ifstream f("/sys/fs/cgroup/cpu.max");
   std::string q, p;

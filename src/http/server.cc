@@ -440,16 +440,42 @@ Server::Server(ServerOptions opts, RequestHandler* handler) : opts_(std::move(op
   }
 }
 
+const char* Server::locality_name(int l) {
+  static const char* const names[kNumLocality] = {"same_core", "same_l3", "same_socket", "cross_socket", "unknown"};
+  return (l >= 0 && l < kNumLocality) ? names[l] : "?";
+}
+
+int Server::incoming_cpu(int fd) {
+  int cpu = -1;
+  socklen_t len = sizeof cpu;
+  if (getsockopt(fd, SOL_SOCKET, SO_INCOMING_CPU, &cpu, &len) != 0) return -1;
+  return cpu;
+}
+
+void Server::note_locality(int client_cpu, size_t worker) {
+  int l = kUnknown;
+  if (client_cpu >= 0 && !opts_.cpus.empty()) {
+    const int wcpu = opts_.cpus[worker % opts_.cpus.size()];
+    const int cc = core_of(client_cpu), wc = core_of(wcpu);
+    const int cd = l3_domain_of(client_cpu), wd = l3_domain_of(wcpu);
+    const int cp = package_of(client_cpu), wp = package_of(wcpu);
+    if (client_cpu == wcpu || (cc >= 0 && cc == wc)) l = kSameCore;
+    else if (cd >= 0 && cd == wd) l = kSameL3;
+    else if (cp >= 0 && cp == wp) l = kSameSocket;
+    else if (cp >= 0 && wp >= 0) l = kCrossSocket;
+  }
+  locality_[l].fetch_add(1, std::memory_order_relaxed);
+}
+
 Worker* Server::pick_worker(int fd) {
   const size_t n = workers_.size();
   size_t k = rr_.fetch_add(1, std::memory_order_relaxed) % n;
+  // The CPU that processed this connection's latest packet: for loopback clients, the
+  // client thread's own CPU. Serving it from the same L3 keeps both socket buffers in
+  // one cache domain (cross-CCD hand-offs more than double the cost of send()).
+  const int cpu = incoming_cpu(fd);
   if (!domain_workers_.empty() || !core_workers_.empty()) {
-    // The CPU that processed this connection's latest packet: for loopback clients, the
-    // client thread's own CPU. Serving it from the same L3 keeps both socket buffers in
-    // one cache domain (cross-CCD hand-offs more than double the cost of send()).
-    int cpu = -1;
-    socklen_t len = sizeof cpu;
-    if (getsockopt(fd, SOL_SOCKET, SO_INCOMING_CPU, &cpu, &len) == 0 && cpu >= 0) {
+    if (cpu >= 0) {
       auto least_assigned = [&] {
         int32_t least = assigned_[0].load(std::memory_order_relaxed);
         for (size_t i = 1; i < n; ++i) least = std::min(least, assigned_[i].load(std::memory_order_relaxed));
@@ -462,6 +488,7 @@ Worker* Server::pick_worker(int fd) {
         if (assigned_[wi].load(std::memory_order_relaxed) <= least_assigned() + 8) {
           assigned_[wi].fetch_add(1, std::memory_order_relaxed);
           steered_core_.fetch_add(1, std::memory_order_relaxed);
+          note_locality(cpu, wi);
           return workers_[wi].get();
         }
         break;
@@ -483,6 +510,7 @@ Worker* Server::pick_worker(int fd) {
     }
   }
   assigned_[k].fetch_add(1, std::memory_order_relaxed);
+  note_locality(cpu, k);
   return workers_[k].get();
 }
 
@@ -541,6 +569,7 @@ void Server::Acceptor::on_event(uint32_t) {
     if (server->opts_.reuseport_accept && !server->steering()) {
       // The kernel already spread connections over the workers' listeners.
       server->assigned_[size_t(worker->index())].fetch_add(1, std::memory_order_relaxed);
+      server->note_locality(incoming_cpu(c), size_t(worker->index()));
       worker->adopt_here(c, t0);
     } else {
       // Round-robin accept, or reuseport with L3 steering: the kernel's hash ignores where
@@ -650,7 +679,11 @@ std::string Server::profile_json() const {
   snprintf(steer, sizeof steer, "\"steering\":{\"same_core\":%llu,\"same_l3\":%llu,\"unsteered\":%llu},",
            (unsigned long long)steered_core_.load(), (unsigned long long)steered_.load(),
            (unsigned long long)unsteered_.load());
-  return "{\"unit\":\"ns (batch: requests per recv)\"," + std::string(steer) + one("accept", all.accept) + "," + one("recv", all.recv) + "," + one("parse", all.parse) + "," +
+  std::string loc = "\"locality\":{";
+  for (int l = 0; l < kNumLocality; ++l)
+    loc += std::string(l ? "," : "") + "\"" + locality_name(l) + "\":" + std::to_string(locality(l));
+  loc += "},";
+  return "{\"unit\":\"ns (batch: requests per recv)\"," + std::string(steer) + loc + one("accept", all.accept) + "," + one("recv", all.recv) + "," + one("parse", all.parse) + "," +
          one("handle", all.handle) + "," + one("send", all.send) + "," + one("batch", all.batch) + "}";
 }
 

@@ -226,6 +226,12 @@ class Server {
   // JSON summary of the --profile histograms (call after join()).
   std::string profile_json() const;
 
+  // Where each accepted connection's client ran (SO_INCOMING_CPU: for loopback clients the
+  // CPU of the sending thread) relative to the pinned worker that serves it.
+  enum Locality { kSameCore = 0, kSameL3, kSameSocket, kCrossSocket, kUnknown, kNumLocality };
+  static const char* locality_name(int l);
+  uint64_t locality(int l) const { return locality_[l].load(std::memory_order_relaxed); }
+
  private:
   struct Acceptor : EventLoop::Handler {
     Server* server;
@@ -250,6 +256,10 @@ class Server {
   std::unique_ptr<std::atomic<uint32_t>[]> domain_rr_;
   std::unique_ptr<std::atomic<int32_t>[]> assigned_;  // live connections per worker
   std::atomic<uint64_t> steered_core_{0}, steered_{0}, unsteered_{0};  // accept steering outcomes
+  std::atomic<uint64_t> locality_[kNumLocality] = {};
+  // Counts the client/worker relation of an accepted connection (client_cpu -1 = unknown).
+  void note_locality(int client_cpu, size_t worker);
+  static int incoming_cpu(int fd);
   friend class Worker;
 };
 

@@ -94,6 +94,12 @@ std::string Prometheus::render(http::Server* server) const {
          (s.circuit_open ? "1" : "0") + "\n";
   }
   if (reloads_) o += "# TYPE hola_config_reloads_total counter\nhola_config_reloads_total " + std::to_string(reloads_()) + "\n";
+  if (server) {
+    o += "# TYPE hola_accept_locality_total counter\n";
+    for (int l = 0; l < http::Server::kNumLocality; ++l)
+      o += std::string("hola_accept_locality_total{relation=\"") + http::Server::locality_name(l) + "\"} " +
+           std::to_string(server->locality(l)) + "\n";
+  }
   if (stream_) {
     o += "# TYPE hola_hystrix_stream_subscribers gauge\nhola_hystrix_stream_subscribers " +
          std::to_string(stream_->subscribers()) + "\n";

@@ -60,6 +60,10 @@ def test_bench_four_ranks_gloo():
     assert out["n_gpus"] == 4 and out["requests"] == 4 * 64 * 50 * 2
     assert out["errors"] == 0 and out["non2xx"] == 0
     assert out["body_checked"] == out["requests"] and "c1_rps" not in out
+    # every accepted connection's client/worker placement is reported, per replica
+    loc = out["locality"]
+    assert loc["accepted"] >= 4 * 64 and len(loc["per_replica"]) == 4
+    assert abs(sum(loc["fraction"].values()) - 1.0) < 1e-3
     assert out["config"]["global_batch"] == 256 and out["config"]["parallelism"] == "replicas4"
     from hola_amd.utils.cpu import parse_cpu_list
     cpus = [c for r in out["config"]["cpu_map"].values() for side in r.values() for c in parse_cpu_list(side)]

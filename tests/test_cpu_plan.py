@@ -156,3 +156,30 @@ def test_slot_cores_per_node(epyc, monkeypatch):
     monkeypatch.setattr(cpu, "allowed_cpus", lambda: list(range(384)))
     monkeypatch.setattr(cpu, "physical_cores", lambda cpus=None: list(range(192)))
     assert cpu.slot_cores(8) == 24  # 2 x 96 cores
+
+
+def test_fewer_loadgen_threads_than_replicas_stay_in_l3(epyc):
+    """The 16-CPU rehearsal at N = 4: 4 cores per rank, 2 server workers + 2 load-generator
+    threads, so T = 2 < N = 4. Each thread drives one L3 group of replicas from a CPU in
+    that group's L3, and every replica still gets the same connections from every rank."""
+    n = 4
+    plans = cpu.plan_replicas_with_loadgen(n, 4)
+    used = [c for p in plans for c in p["server"] + p["loadgen"]]
+    assert len(used) == len(set(used)) == 16
+    per_replica = [0] * n
+    for r, p in enumerate(plans):
+        assert p["thread_targets"] is not None and len(p["thread_targets"]) == len(p["loadgen"]) == 2
+        for t, c in enumerate(p["loadgen"]):
+            for target in p["thread_targets"][t]:
+                assert cpu.l3_domain(c) in {cpu.l3_domain(x) for x in plans[target]["server"]}
+        conns = cpu.connection_targets(p["thread_targets"], 64)
+        for x in conns:
+            per_replica[x] += 1
+        assert sorted(set(conns)) == list(range(n)) and all(conns.count(x) == 16 for x in range(n))
+    assert per_replica == [64] * n
+
+
+def test_aligned_thread_targets_match_the_dealing(epyc):
+    plans = cpu.plan_replicas_with_loadgen(2, per_rank=16)
+    for r, p in enumerate(plans):
+        assert p["thread_targets"] == [[(t + r) % 2] for t in range(len(p["loadgen"]))]
