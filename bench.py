@@ -67,6 +67,10 @@ def parse_args():
                          "default 1000, Brave 3's collector queue; 0 = bounded only by the rings)")
     ap.add_argument("--profile-dir", default="",
                     help="run replicas with --profile and write their stage histograms here")
+    ap.add_argument("--plain-dealing", action="store_true",
+                    help="deal every rank's connections (i + rank) %% N over all replicas from its own "
+                         "cores, instead of giving each load-generator thread the replicas of its L3 "
+                         "(A/B of the planner's locality)")
     ap.add_argument("--no-avoid-busy", action="store_true",
                     help="take cores in id order instead of the quietest L3 domains first")
     ap.add_argument("--per-conn-quota", action="store_true",
@@ -137,6 +141,8 @@ def main() -> int:
                  "host": host,
                  "base_port": _free_port_block(a.base_port, local_world, host),
                  "sink_port": sink[1] if sink else 0}]
+        # the rank's own load-generator cores, for --plain-dealing (the r42 layout)
+        plan[0]["own_loadgen"] = _own_loadgen(plan[0]["cores"])
     if dist:
         dist.broadcast_object_list(plan, src=0)
     server_cpus, load_cpus = plan[0]["cores"][local_rank]["server"], plan[0]["cores"][local_rank]["loadgen"]
@@ -144,6 +150,9 @@ def main() -> int:
     # Each load-generator thread drives only replicas in its own L3 (see
     # plan_replicas_with_loadgen); None = plain (i + rank) % N dealing.
     conn_targets = connection_targets(thread_targets, a.connections) if thread_targets else None
+    if a.plain_dealing:
+        conn_targets = None
+        load_cpus = plan[0]["own_loadgen"][local_rank]
     s_threads = len(server_cpus)
     smt = plan[0]["smt"]
     if a.busy_poll_pause < 0:
@@ -335,6 +344,21 @@ def main() -> int:
             dist.barrier()
             dist.destroy_process_group()
     return 0
+
+
+def _own_loadgen(cores: list[dict]) -> list[list[int]]:
+    """Load-generator CPUs regrouped so that each rank runs on the CPUs planned next to its
+    own replica (no cross-rank swap): rank r takes the CPUs whose L3 is its server's."""
+    from hola_amd.utils.cpu import l3_domain
+    pool = sorted({c for p in cores for c in p["loadgen"]})
+    out = []
+    for p in cores:
+        doms = {l3_domain(c) for c in p["server"]}
+        mine = [c for c in pool if l3_domain(c) in doms][:len(p["loadgen"])]
+        for c in mine:
+            pool.remove(c)
+        out.append(mine if len(mine) == len(p["loadgen"]) else p["loadgen"])
+    return out
 
 
 def _start_sink():

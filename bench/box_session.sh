@@ -9,6 +9,7 @@
 #   ab REPS "label|args" ...   interleaved A/B of bench.py variants, REPS rounds
 #   rehearsal [Ns]     the driver's own N>1 command line (default N = 2 4 8) inside the box's
 #                      CPU slice, plus --profile-dir stage profiles for locality attribution
+#   locality           N = 1, 2, 4, 8 in the box's slice, L3-grouped vs. plain connection dealing
 #   latency            BASELINE config 2 (1 connection) and the open-loop latency curve
 #   chain              two-hop chaining bench (loadgen -> hola A -> hola B)
 #   tracing            headline without a collector, with the native Zipkin sink (default 1000-span
@@ -52,6 +53,16 @@ rehearsal)
     timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$n" \
       --master-addr 127.0.0.1 --master-port $((29600 + n)) bench.py --gpus "$n" --steps 8 --warmup 2 \
       --profile-dir "$OUT/prof_n$n" > "$OUT/n$n.json" 2> "$OUT/err_n$n.log" || exit $?
+  done
+  ;;
+locality)
+  # N>1 layouts inside the box's CPU slice: the planner's L3-grouped load generators vs. the
+  # plain (i + rank) % N dealing from each rank's own cores, with stage profiles.
+  for spec in "1|" "2|" "4|" "4|--plain-dealing" "8|" "8|--plain-dealing"; do
+    n=${spec%%|*}; extra=${spec#*|}; tag=n$n${extra:+_plain}
+    timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$n" \
+      --master-addr 127.0.0.1 --master-port $((29700 + n)) bench.py --gpus "$n" --steps 8 --warmup 2 \
+      --c1-reqs 0 --profile-dir "$OUT/prof_$tag" $extra > "$OUT/$tag.json" 2> "$OUT/err_$tag.log" || exit $?
   done
   ;;
 latency)
