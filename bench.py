@@ -319,8 +319,8 @@ def main() -> int:
                 "connections_per_replica": a.connections,
                 "reqs_per_conn_per_step": a.reqs_per_conn,
                 "pipeline": a.pipeline,
-                "lb": "client-side round-robin over replica ports" + (
-                    "" if world == 1 else ", each load-generator thread on the L3 of the replicas it drives"),
+                "lb": "client-side " + ("round-robin over all replicas from the rank's own cores" if a.plain_dealing
+                                        else plan[0]["cores"][local_rank].get("dealing", "round-robin")),
                 "loopback": host,
                 "cores_per_replica": len({min(siblings(c)) for c in list(server_cpus) + list(load_cpus)}),
                 "server_threads_per_replica": s_threads,

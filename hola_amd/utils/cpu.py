@@ -219,11 +219,15 @@ def plan_replicas_with_loadgen(local_world: int, per_rank: int | None = None, se
     crosses ranks:
       * T % N == 0: thread t of rank r drives replica (t + r) % N alone;
       * N % T == 0 (fewer threads than replicas, e.g. 2 threads and 4 replicas on a 16-CPU
-        slice): the replicas form T groups of N/T consecutive ranks (which plan_node puts in
-        one L3); thread t of rank r drives group (t + r) % T;
-      * otherwise ``thread_targets`` is None and connections are dealt (i + r) % N.
-    Every replica still receives the same number of connections from every rank (client-side
-    round-robin in aggregate). Returns, per rank, {"server": [...], "loadgen": [... one CPU
+        slice) and each group of N/T consecutive ranks sits in one L3: thread t of rank r
+        drives group (t + r) % T;
+      * otherwise each thread stays on its own rank's cores and drives the replicas whose
+        servers share its L3 (topology-aware round-robin: every replica still gets the same
+        number of connections in aggregate, but a rank no longer reaches every replica);
+        ``thread_targets`` is None (plain (i + r) % N dealing) only when no such replica
+        exists.
+    In the first two cases every replica receives the same number of connections from every
+    rank (client-side round-robin). Returns, per rank, {"server": [...], "loadgen": [... one CPU
     per thread, in thread order], "thread_targets": [[replica, ...] per thread] or None}.
 
     `smt` decides what happens to the SMT sibling of each planned physical core:
@@ -258,6 +262,7 @@ def plan_replicas_with_loadgen(local_world: int, per_rank: int | None = None, se
     plans = []
     for r in range(n):
         targets = None
+        dealing = "round-robin over all replicas, each thread on the L3 of the replica it drives"
         if n == 1:
             load = splits[0][1]
             targets = [[0] for _ in load]
@@ -265,7 +270,7 @@ def plan_replicas_with_loadgen(local_world: int, per_rank: int | None = None, se
             per = t_threads // n
             load = [splits[(t + r) % n][1][r * per + t // n] for t in range(t_threads)]
             targets = [[(t + r) % n] for t in range(t_threads)]
-        elif uniform and n % t_threads == 0:
+        elif uniform and n % t_threads == 0 and _groups_share_l3(splits, n // t_threads):
             per = n // t_threads  # replicas per group
             load, targets = [], []
             for t in range(t_threads):
@@ -274,10 +279,29 @@ def plan_replicas_with_loadgen(local_world: int, per_rank: int | None = None, se
                 pool = [c for m in members for c in splits[m][1]]  # per * T CPUs, one per rank
                 load.append(pool[r])
                 targets.append([members[(j + r) % per] for j in range(per)])
+            dealing = "round-robin over all replicas, each thread on the L3 of the replica group it drives"
         else:
             load = splits[r][1]
-        plans.append({"server": splits[r][0], "loadgen": load, "thread_targets": targets})
+            dealing = "topology-aware round-robin over the replicas in each thread's L3"
+            targets = []
+            for c in load:
+                local = [m for m in range(n) if l3_domain(c) in {l3_domain(x) for x in splits[m][0]}]
+                targets.append([local[(j + r) % len(local)] for j in range(len(local))] if local else None)
+            if any(x is None for x in targets):
+                targets = None
+                dealing = "round-robin over all replicas from the rank's own cores"
+        plans.append({"server": splits[r][0], "loadgen": load, "thread_targets": targets, "dealing": dealing})
     return plans
+
+
+def _groups_share_l3(splits: list[tuple[list[int], list[int]]], per: int) -> bool:
+    """True when every group of `per` consecutive replicas has its servers and load-generator
+    CPUs in one L3 domain."""
+    for g in range(0, len(splits), per):
+        doms = {l3_domain(c) for sv, ld in splits[g:g + per] for c in sv + ld}
+        if len(doms) != 1:
+            return False
+    return True
 
 
 def connection_targets(thread_targets: list[list[int]], connections: int) -> list[int]:

@@ -183,3 +183,21 @@ def test_aligned_thread_targets_match_the_dealing(epyc):
     plans = cpu.plan_replicas_with_loadgen(2, per_rank=16)
     for r, p in enumerate(plans):
         assert p["thread_targets"] == [[(t + r) % 2] for t in range(len(p["loadgen"]))]
+
+
+def test_one_thread_per_rank_drives_same_l3_replicas(epyc):
+    """N = 8 in a 16-CPU slice: 1 server worker + 1 load-generator thread per rank, 4 ranks
+    per L3. One thread cannot reach all 8 replicas inside its L3, so each drives the 4
+    replicas of its own L3; every replica still gets 64 connections in total."""
+    n = 8
+    plans = cpu.plan_replicas_with_loadgen(n, 2)
+    per_replica = [0] * n
+    for r, p in enumerate(plans):
+        (c,) = p["loadgen"]
+        (targets,) = p["thread_targets"]
+        assert len(targets) == 4
+        for m in targets:
+            assert cpu.l3_domain(c) == cpu.l3_domain(plans[m]["server"][0])
+        for x in cpu.connection_targets(p["thread_targets"], 64):
+            per_replica[x] += 1
+    assert per_replica == [64] * n
