@@ -10,8 +10,8 @@ ROOT = Path(__file__).resolve().parent.parent
 OS = ROOT / "deploy" / "openshift"
 
 
-def items():
-    doc = yaml.safe_load((OS / "hola.yaml").read_text())
+def items(name: str = "hola.yaml"):
+    doc = yaml.safe_load((OS / name).read_text())
     return {i["kind"]: i for i in doc["items"]}
 
 
@@ -106,3 +106,51 @@ def test_license_matches_swagger_document():
     assert "Apache-2.0" in text and "http://www.apache.org/licenses/LICENSE-2.0" in text
     lic = json.loads((ROOT / "assets" / "swagger.json").read_text())["info"]["license"]
     assert lic["url"] == "http://www.apache.org/licenses/LICENSE-2.0.html"
+
+
+def test_deploymentconfig_flavour_for_oc_env_dc():
+    """`oc env dc/hola JAVA_OPTIONS=...` (Readme.md:18-24) needs a DeploymentConfig named
+    hola: hola-dc.yaml ships one, with the same Service and the same container spec as the
+    apps/v1 Deployment in hola.yaml."""
+    dc_items = items("hola-dc.yaml")
+    assert set(dc_items) == {"Service", "DeploymentConfig"}
+    assert dc_items["Service"] == items()["Service"]
+    dc = dc_items["DeploymentConfig"]
+    assert dc["apiVersion"] == "apps.openshift.io/v1" and dc["metadata"]["name"] == "hola"
+    assert dc["metadata"]["labels"]["group"] == "msa" and dc["metadata"]["labels"]["hystrix.enabled"] == "true"
+    tpl = dc["spec"]["template"]
+    # DC selectors are plain label maps (no matchLabels), matching the pod template and Service
+    assert set(dc["spec"]["selector"].items()) <= set(tpl["metadata"]["labels"].items())
+    assert set(dc_items["Service"]["spec"]["selector"].items()) <= set(tpl["metadata"]["labels"].items())
+    assert {"type": "ConfigChange"} in dc["spec"]["triggers"]
+    assert tpl == items()["Deployment"]["spec"]["template"]  # the two flavours never drift
+    (c,) = tpl["spec"]["containers"]
+    assert c["image"] == "redhatmsa/hola:0.0.1-SNAPSHOT"  # pom.xml:71-72
+    env = {e["name"]: e.get("value") for e in c["env"]}
+    assert env["JAVA_OPTIONS"] == "-Xmx512m" and env["AB_OFF"] == "true"
+    rp = c["readinessProbe"]
+    assert rp["httpGet"] == {"path": "/api/health", "port": 8080}
+    assert rp["initialDelaySeconds"] == 5 and rp["timeoutSeconds"] == 30
+
+
+def test_configmap_patch_applies_to_the_deploymentconfig(native):
+    """`oc patch dc/hola -p "$(cat translation-patch.yaml)"`: a strategic merge by container
+    name that mounts the ConfigMap and points -Dconf at it."""
+    dc = items("hola-dc.yaml")["DeploymentConfig"]
+    patch = yaml.safe_load((OS / "translation-patch.yaml").read_text())
+    (pc,) = patch["spec"]["template"]["spec"]["containers"]
+    (c,) = dc["spec"]["template"]["spec"]["containers"]
+    assert pc["name"] == c["name"]
+    merged_env = {e["name"]: e.get("value") for e in c["env"]}
+    merged_env.update({e["name"]: e["value"] for e in pc["env"]})
+    conf = native.parse_java_options(merged_env["JAVA_OPTIONS"])["conf"]
+    (vol,) = patch["spec"]["template"]["spec"]["volumes"]
+    cm = yaml.safe_load((OS / "translation-configmap.yaml").read_text())
+    assert vol["configMap"]["name"] == cm["metadata"]["name"]
+    assert conf == pc["volumeMounts"][0]["mountPath"] + "/translation.properties"
+    assert "-Xmx512m" in merged_env["JAVA_OPTIONS"]
+
+
+def test_dockerfile_offers_the_reference_image_name():
+    df = (ROOT / "deploy" / "Dockerfile").read_text()
+    assert "-t redhatmsa/hola:0.0.1-SNAPSHOT" in df
