@@ -5,10 +5,6 @@ The service itself is the ``hola`` executable (epoll event loops pinned to the E
 cores). This Python package is the tooling around it:
 
 * :mod:`hola_amd.native`   — build / locate / load the native artefacts
-* :mod:`hola_amd.ops`      — Python API over the native core operations (Properties parser,
-  String.format, Accept negotiation, B3, JSON) — the code the server itself runs
-* :mod:`hola_amd.models`   — the service's HTTP contract as data (routes, media types, CORS,
-  tracing), checked against the running server by the tests
 * :mod:`hola_amd.server`   — run a ``hola`` process (tests, smoke, bench)
 * :mod:`hola_amd.parallel` — replica scale-out: pinned replica sets, round-robin proxy,
   the 1/2/4/8 scaling harness (the service's analogue of data parallelism)
