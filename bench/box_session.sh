@@ -6,7 +6,7 @@
 # MODE
 #   final              smoke(), pytest -m gpu, the default bench (the driver's round-end tiers)
 #   bench ARGS...      one bench.py run with ARGS
-#   ab REPS "label|args" ...   interleaved A/B of bench.py variants, REPS rounds
+#   ab REPS "label|args[|VAR=value]" ...   interleaved A/B of bench.py variants, REPS rounds
 #   rehearsal [Ns]     the driver's own N>1 command line (default N = 2 4 8) inside the box's
 #                      CPU slice, plus --profile-dir stage profiles for locality attribution
 #   locality           N = 1, 2, 4, 8 in the box's slice, L3-grouped vs. plain connection dealing
@@ -38,8 +38,10 @@ ab)
   REPS=${1:?reps}; shift
   for rep in $(seq 1 "$REPS"); do
     for v in "$@"; do
-      label=${v%%|*}; args=${v#*|}
-      timeout -k 10 240 python bench.py --steps 15 --warmup 4 $args > "$OUT/${label}_${rep}.json" \
+      # "label|bench args" or "label|bench args|VAR=value ..." (environment for that variant)
+      label=${v%%|*}; rest=${v#*|}; args=${rest%%|*}; envs=""
+      [ "$rest" != "$args" ] && envs=${rest#*|}
+      env $envs timeout -k 10 240 python bench.py --steps 15 --warmup 4 $args > "$OUT/${label}_${rep}.json" \
         2>> "$OUT/err.log" || exit 1
       python3 -c "import json; d=json.load(open('$OUT/${label}_${rep}.json')); print('$label', $rep, d['value'], d['p50_ms'], d['p99_ms'], d['server_cpu_us_per_req'], d['loadgen_cpu_us_per_req'])" \
         >> "$OUT/summary.txt"

@@ -27,6 +27,11 @@ PRESETS = {
     "debug": ["-DCMAKE_BUILD_TYPE=Debug"],
     "tsan": ["-DCMAKE_BUILD_TYPE=RelWithDebInfo", "-DHOLA_SANITIZE=thread", "-DHOLA_BUILD_PYTHON=OFF"],
     "asan": ["-DCMAKE_BUILD_TYPE=RelWithDebInfo", "-DHOLA_SANITIZE=address,undefined", "-DHOLA_BUILD_PYTHON=OFF"],
+    # compile-flag A/B variants of the release build (server binary via HOLA_SERVER_BIN)
+    "release-v4": ["-DCMAKE_BUILD_TYPE=Release", "-DHOLA_MARCH=x86-64-v4", "-DHOLA_BUILD_PYTHON=OFF"],
+    "release-o3lto": ["-DCMAKE_BUILD_TYPE=Release", "-DHOLA_OPT=-O3", "-DHOLA_LTO=ON", "-DHOLA_BUILD_PYTHON=OFF"],
+    "release-v4-o3lto": ["-DCMAKE_BUILD_TYPE=Release", "-DHOLA_MARCH=x86-64-v4", "-DHOLA_OPT=-O3", "-DHOLA_LTO=ON",
+                         "-DHOLA_BUILD_PYTHON=OFF"],
 }
 
 
@@ -112,7 +117,16 @@ def ensure_built(preset: str = "release") -> Path:
 
 
 def binary(name: str = "hola", preset: str = "release", build_if_missing: bool = True) -> Path:
-    """Absolute path of a native executable (``HOLA_BIN_DIR`` overrides the build dir)."""
+    """Absolute path of a native executable (``HOLA_BIN_DIR`` overrides the build dir;
+    ``HOLA_SERVER_BIN`` overrides the ``hola`` server alone, for compile-flag A/B runs)."""
+    server = os.environ.get("HOLA_SERVER_BIN")
+    if name == "hola" and server:
+        p = Path(server)
+        if not p.is_absolute():
+            p = REPO / p
+        if not p.exists():
+            raise NativeBuildError(f"HOLA_SERVER_BIN {p} is missing")
+        return p
     override = os.environ.get("HOLA_BIN_DIR")
     bdir = Path(override) if override else build_dir(preset)
     p = bdir / name
