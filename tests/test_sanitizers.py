@@ -65,7 +65,7 @@ def _workload(s: HolaProcess, aloha: FakeAloha, conf):
                     pass
 
     def modes():
-        for m in ("ok", "error", "slow", "garbage", "ok", "close", "ok"):
+        for m in ("ok", "error", "slow", "garbage", "ok", "close", "unavailable", "ok"):
             aloha.set_mode(m, delay_s=0.3)
             time.sleep(0.25)
 
