@@ -6,7 +6,8 @@ Load mix, all running concurrently:
   * closed-loop GET /api/hola from the native load generator (most of the traffic);
   * GET /api/hola-chaining against a fake aloha that cycles ok / slow / 500 / garbage /
     connection-drop, so the breaker opens and closes and timeouts fire;
-  * two /hystrix.stream subscribers; /metrics scrapes;
+  * two /hystrix.stream subscribers, plus one that never reads (its backlog must stay
+    bounded and the server must close it after --hystrix-stream-stall-ms); /metrics scrapes;
   * a config hot reload every few seconds.
 
     python bench/soak.py --minutes 5 --out soak.json
@@ -43,12 +44,13 @@ samples, errors = [], []
 
 with FakeAloha() as aloha, HolaProcess(
         args=["--aloha-url", aloha.url, "--feign-log", "none", f"-Dconf={conf}",
-              "-Dhystrix.command.default.circuitBreaker.sleepWindowInMilliseconds=1000"],
+              "-Dhystrix.command.default.circuitBreaker.sleepWindowInMilliseconds=1000",
+              "--hystrix-stream-stall-ms", "5000"],
         env={"HOSTNAME": "soak"}, threads=len(srv), cpu_list=format_cpu_list(srv), log_level="warn") as s:
     pid = s.proc.pid
 
     def chaining():
-        modes = ["ok", "slow", "error", "ok", "garbage", "close", "ok"]
+        modes = ["ok", "slow", "error", "ok", "garbage", "close", "unavailable", "ok"]
         i = 0
         while not stop.is_set():
             aloha.set_mode(modes[i % len(modes)], delay_s=1.0)
@@ -75,6 +77,20 @@ with FakeAloha() as aloha, HolaProcess(
                     except socket.timeout:
                         pass
 
+    def stalled_stream():
+        import socket
+        while not stop.is_set():
+            c = socket.socket()
+            c.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 4096)
+            try:
+                c.connect(("127.0.0.1", s.port))
+                c.sendall(b"GET /hystrix.stream?delay=10 HTTP/1.1\r\nHost: x\r\n\r\n")
+                stop.wait(8)  # never reads; the server gives up after 5 s without progress
+            except OSError:
+                pass
+            finally:
+                c.close()
+
     def reload():
         v = 0
         while not stop.wait(3):
@@ -96,7 +112,8 @@ with FakeAloha() as aloha, HolaProcess(
                 errors.append(("sampler", repr(e)))
             stop.wait(a.sample_s)
 
-    threads = [threading.Thread(target=f, daemon=True) for f in (chaining, stream, stream, reload, sampler)]
+    threads = [threading.Thread(target=f, daemon=True)
+               for f in (chaining, stream, stream, stalled_stream, reload, sampler)]
     for t in threads:
         t.start()
     res = run_duration([("127.0.0.1", s.port)], 64, len(lg), duration, 1.0, cpu_list=",".join(map(str, lg)))
@@ -104,6 +121,14 @@ with FakeAloha() as aloha, HolaProcess(
     for t in threads:
         t.join(timeout=30)
     alive = s.proc.poll() is None
+    stream_stats = {}
+    try:
+        _, _, m = http_get("127.0.0.1", s.port, "/metrics", timeout=5)
+        for l in m.decode().splitlines():
+            if l.startswith(("hola_hystrix_stream_frames_skipped_total ", "hola_hystrix_stream_stalled_closed_total ")):
+                stream_stats[l.split()[0]] = int(float(l.split()[1]))
+    except OSError as e:
+        errors.append(("metrics", repr(e)))
 conf.unlink()
 
 first, last = samples[1] if len(samples) > 1 else samples[0], samples[-1]
@@ -111,7 +136,7 @@ out = {
     "minutes": a.minutes, "hola_rps": res["rps"], "hola_p99_ms": res["latency"]["p99_ns"] / 1e6,
     "hola_errors": res["latency"]["errors"], "other_errors": errors[:20], "alive_at_end": alive,
     "rss_kb_first": first["rss_kb"], "rss_kb_last": last["rss_kb"], "rss_kb_max": max(x["rss_kb"] for x in samples),
-    "fds_first": first["fds"], "fds_last": last["fds"], "samples": samples,
+    "fds_first": first["fds"], "fds_last": last["fds"], "stream": stream_stats, "samples": samples,
 }
 print(json.dumps({k: v for k, v in out.items() if k != "samples"}))
 if a.out:
