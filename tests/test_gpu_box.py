@@ -34,6 +34,11 @@ def test_bench_json_contract_on_host():
     assert out["errors"] == 0 and out["non2xx"] == 0
     assert out["value"] > 10000  # a pinned native replica on EPYC cores does far more than this
     assert out["p50_ms"] > 0 and out["p99_ms"] >= out["p50_ms"]
+    # every timed response body was compared with the replica's greeting
+    assert out["body_checked"] == out["requests"] and out["body_mismatch"] == 0
+    # BASELINE config 2 ran after the timed region, and placement was reported
+    assert out["c1_errors"] == 0 and out["c1_rps"] > 10000 and out["c1_body_checked"] == out["c1_requests"]
+    assert abs(sum(out["locality"]["fraction"].values()) - 1.0) < 1e-3
 
 
 @pytest.mark.gpu
@@ -53,6 +58,27 @@ def test_bench_two_ranks_on_host():
     assert out["requests"] == 2 * 64 * 500 * 3
     assert out["errors"] == 0 and out["non2xx"] == 0
     assert set(out["config"]["cpu_map"]) == {"rank0", "rank1"}
+    assert out["body_checked"] == out["requests"] and out["body_mismatch"] == 0
+    # the planner keeps each load-generator thread in the L3 of the replica it drives
+    loc = out["locality"]["fraction"]
+    assert loc["same_core"] + loc["same_l3"] > 0.8, loc
+
+
+@pytest.mark.gpu
+def test_tracing_as_deployed_on_host():
+    """`bench.py --zipkin-sink`: a native collector attached, as ZIPKIN_SERVER_URL is in the
+    reference image. Spans beyond the Brave-parity budget are dropped and counted, the rest
+    reach the collector, and the request path does not slow down."""
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--steps", "4", "--warmup", "1",
+                        "--reqs-per-conn", "20000", "--c1-reqs", "0", "--zipkin-sink"],
+                       capture_output=True, text=True, timeout=600, env={**os.environ, "HOLA_BENCH_PORT": "18720"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    tr = out["tracing"]
+    assert out["errors"] == 0 and tr["mode"].startswith("collector")
+    assert tr["sink_bad"] == 0 and tr["spans_per_s"]["reported"] > 0
+    assert tr["spans_per_s"]["dropped_queue_full"] > 0
+    assert out["value"] > 10000
 
 
 @pytest.mark.gpu
