@@ -105,6 +105,23 @@ def _info() -> int:
     cores = slot_cores(slots)
     print(f"gpu slots      : {slots} (KFD topology) -> {cores} physical cores per replica")
     print(f"bench --smt auto: {'pair' if smt_fits(slots, cores) else 'off'}")
+    # The bench's per-N layout: server and load-generator CPUs, and which replicas each
+    # load-generator thread drives (connection dealing), as bench.py would plan them.
+    from hola_amd.utils.cpu import plan_replicas_with_loadgen
+
+    budget = cpu_budget()
+    for n in (1, 2, 4, 8):
+        per_rank = min(cores, max(1, budget // n))
+        smt = "pair" if smt_fits(slots, per_rank) else "off"
+        try:
+            plans = plan_replicas_with_loadgen(n, per_rank, avoid_busy=False, smt=smt)
+        except (IndexError, ValueError) as e:
+            print(f"bench N={n}: no plan ({e})")
+            continue
+        print(f"bench N={n}: {per_rank} cores/replica, smt {smt}, {plans[0]['dealing']}")
+        for r, p in enumerate(plans):
+            print(f"  rank{r}: server {format_cpu_list(p['server'])} loadgen {format_cpu_list(p['loadgen'])} "
+                  f"threads->replicas {p['thread_targets']}")
     return 0
 
 
