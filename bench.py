@@ -368,14 +368,28 @@ def _start_sink():
 
     from hola_amd.native import binary
 
-    pf = Path(tempfile.mkdtemp(prefix="hola_sink_")) / "port"
+    import atexit
+    import shutil
+
+    tmp = Path(tempfile.mkdtemp(prefix="hola_sink_"))
+    pf = tmp / "port"
     proc = subprocess.Popen([str(binary("hola_zipkin_sink")), "--port", "0", "--port-file", str(pf)])
-    deadline = time.monotonic() + 10
-    while not pf.exists():
-        if proc.poll() is not None or time.monotonic() > deadline:
-            raise RuntimeError("hola_zipkin_sink did not start")
-        time.sleep(0.01)
-    return proc, int(pf.read_text())
+
+    def stop():
+        if proc.poll() is None:
+            proc.terminate()
+            proc.wait(timeout=10)
+
+    atexit.register(stop)  # also on an exception before main()'s cleanup runs
+    try:
+        deadline = time.monotonic() + 10
+        while not pf.exists():
+            if proc.poll() is not None or time.monotonic() > deadline:
+                raise RuntimeError("hola_zipkin_sink did not start")
+            time.sleep(0.01)
+        return proc, int(pf.read_text())
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
 
 
 def _sink_stats(port: int) -> dict:
