@@ -96,3 +96,28 @@ def test_loadgen_counts_wrong_bodies_as_errors():
     assert bad["latency"]["body_mismatch"] == bad["latency"]["count"] > 0
     assert bad["latency"]["errors"] >= bad["latency"]["body_mismatch"]
     assert learned["latency"]["body_mismatch"] == 0 and learned["latency"]["body_checked"] > 0
+
+
+def test_loadgen_conn_targets_pin_connections_to_replicas():
+    """--conn-targets fixes each connection's replica (the planner's L3 groups); an index
+    outside --targets is rejected before any connection is made."""
+    import subprocess
+
+    from hola_amd.native import binary
+    from hola_amd.parallel.loadgen import run_duration
+    from hola_amd.server import HolaProcess
+
+    with HolaProcess(env={"HOSTNAME": "a"}, threads=1) as a, HolaProcess(env={"HOSTNAME": "b"}, threads=1) as b:
+        targets = [("127.0.0.1", a.port), ("127.0.0.1", b.port)]
+        # all 4 connections on replica 1: every body must be b's greeting
+        out = run_duration(targets, 4, 2, 0.3, warmup_s=0.1, expect_bodies=["Hola de a", "Hola de b"])
+        assert out["latency"]["body_mismatch"] == 0
+        cmd = [str(binary("hola_loadgen")), "--targets", f"127.0.0.1:{a.port},127.0.0.1:{b.port}", "-c", "4",
+               "-t", "2", "--duration", "0.3", "--conn-targets", "1,1,1,1", "--expect-body", "Hola de b",
+               "--expect-body", "Hola de b"]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=60)
+        assert r.returncode == 0, r.stderr
+        lat = json.loads(r.stdout.strip().splitlines()[-1])["latency"]
+        assert lat["body_mismatch"] == 0 and lat["body_checked"] == lat["count"] > 0
+        bad = subprocess.run(cmd[:-4] + ["--conn-targets", "0,2"], capture_output=True, text=True, timeout=60)
+        assert bad.returncode == 2 and "out of range" in bad.stderr
