@@ -383,3 +383,22 @@ def test_shortened_timeout_does_not_wait_behind_older_calls(hola, aloha, tmp_pat
     assert time.monotonic() - t0 < 0.8  # its own 150 ms deadline, not the older 3000 ms one
     t.join()
     assert first and first[0][1:] != [FALLBACK]  # the older call still completed normally
+
+
+def test_retry_sleeps_hold_the_bulkhead_slot(hola):
+    """Feign's retry sleeps run on the Hystrix thread, so a retrying call keeps its bulkhead
+    slot until the timeout: with coreSize=1, a second concurrent call is rejected."""
+    s = hola(args=["--aloha-url", f"http://127.0.0.1:{closed_port()}/", "--feign-log", "none",
+                   "-Dhystrix.threadpool.default.coreSize=1",
+                   "-Dhystrix.command.default.circuitBreaker.enabled=false"], threads=1)
+    first = []
+    t = threading.Thread(target=lambda: first.append(chain(s)))
+    t.start()
+    time.sleep(0.2)  # the first call is sleeping between Feign attempts
+    t0 = time.monotonic()
+    assert chain(s)[1:] == [FALLBACK]
+    assert time.monotonic() - t0 < 0.3  # rejected at once, not retried
+    t.join()
+    assert first and first[0][1:] == [FALLBACK]
+    ev = _events(s)
+    assert ev.get("THREAD_POOL_REJECTED") == 1 and ev.get("TIMEOUT") == 1
