@@ -252,3 +252,26 @@ def test_filter_pattern_traces_every_method_on_exact_paths(hola, zipkin):
     assert codes == ["405", "405", "406"]
     urls = [b["value"] for sp in spans for b in sp["binaryAnnotations"] if b["key"] == "http.url"]
     assert not any(u.endswith("/") for u in urls)
+
+
+def test_one_client_span_per_feign_attempt(hola, zipkin):
+    """Brave's HttpClient interceptors run once per executed request: a call Feign retries
+    5 times (503 + Retry-After: 0) records 5 client spans, children of the server span."""
+    with FakeAloha() as aloha:
+        aloha.set_mode("unavailable")
+        s = hola(args=["--zipkin-url", zipkin.url, "--aloha-url", aloha.url, "--feign-log", "none"])
+        st, _, body = s.get("/api/hola-chaining")
+        assert st == 200 and json.loads(body)[1:] == ["Aloha response (fallback)"]
+        spans = zipkin.wait_for(lambda sp: len(sp) >= 6)
+    server = [sp for sp in spans if _annotations(sp) == {"sr", "ss"}]
+    client = [sp for sp in spans if _annotations(sp) == {"cs", "cr"}]
+    assert len(server) == 1 and len(client) == 5
+    assert {sp["traceId"] for sp in spans} == {server[0]["traceId"]}
+    assert all(sp["parentId"] == server[0]["id"] for sp in client)
+    assert len({sp["id"] for sp in client}) == 5
+    for sp in client:
+        codes = [b["value"] for b in sp["binaryAnnotations"] if b["key"] == "http.status_code"]
+        assert codes == ["503"]
+    # each attempt carried its own B3 span id downstream
+    sent = [r["headers"].get("x-b3-spanid") for r in aloha.requests]
+    assert sorted(sent) == sorted(sp["id"] for sp in client)
