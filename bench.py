@@ -92,10 +92,13 @@ def parse_args():
                     help="requests per connection sent back to back before waiting for their "
                          "responses (wrk's pipeline.lua, as in the TechEmpower plaintext test); "
                          "1 = wrk's default and the headline (BASELINE configs 2-4)")
-    ap.add_argument("--c1-reqs", type=int, default=150000,
+    ap.add_argument("--c1-seconds", type=float, default=3.0,
                     help="after the timed region, rank 0 drives its own replica over ONE connection for "
-                         "this many requests (BASELINE config 2) and reports c1_rps/c1_p50_ms/c1_p99_ms; "
+                         "about this long (BASELINE config 2) and reports c1_rps/c1_p50_ms/c1_p99_ms; "
                          "0 = skip. Outside the timed region: `value` is untouched")
+    ap.add_argument("--c1-reqs", type=int, default=0,
+                    help="config-2 request count instead of --c1-seconds (0 = sized from a warm-up "
+                         "run to last --c1-seconds)")
     ap.add_argument("--busy-poll-us", type=int, default=20,
                     help="spin this long in epoll before sleeping (server and load generator); "
                          "20 us measured best on the box (profiles/r11_box_session), 0 = off")
@@ -497,15 +500,19 @@ def _expected_bodies(path: str, ranks: list[int]) -> list[str] | None:
 def _config2_subrun(a, host: str, port: int, load_cpus, bodies) -> dict | None:
     """BASELINE config 2: one keep-alive connection against this rank's replica, run after
     the timed region (so the headline is unaffected)."""
-    if a.c1_reqs <= 0:
+    if a.c1_reqs <= 0 and a.c1_seconds <= 0:
         return None
     lg = ControlledLoadgen([(host, port)], 1, 1, cpu_list=str(load_cpus[0]), path=a.path,
                            busy_poll_us=a.busy_poll_us, busy_poll_pause=a.busy_poll_pause, epoll_lt=a.epoll_lt,
                            expect_bodies=bodies, verify_body=bodies is None)
     try:
-        lg.run(max(1000, a.c1_reqs // 10))  # warm-up
+        warm = lg.run(max(1000, a.c1_reqs // 10) if a.c1_reqs > 0 else 20000)
+        n = a.c1_reqs
+        if n <= 0:  # size the run from the warm-up rate: about --c1-seconds, within bounds
+            rate = warm["requests"] / max(1e-9, warm["elapsed_ns"] / 1e9)
+            n = int(min(5_000_000, max(20_000, rate * a.c1_seconds)))
         lg.reset()
-        r = lg.run(a.c1_reqs)
+        r = lg.run(n)
         st = lg.stats()
     finally:
         lg.close()

@@ -64,7 +64,7 @@ locality)
     n=${spec%%|*}; extra=${spec#*|}; tag=n$n${extra:+_plain}
     timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$n" \
       --master-addr 127.0.0.1 --master-port $((29700 + n)) bench.py --gpus "$n" --steps 8 --warmup 2 \
-      --c1-reqs 0 --profile-dir "$OUT/prof_$tag" $extra > "$OUT/$tag.json" 2> "$OUT/err_$tag.log" || exit $?
+      --c1-seconds 0 --profile-dir "$OUT/prof_$tag" $extra > "$OUT/$tag.json" 2> "$OUT/err_$tag.log" || exit $?
   done
   ;;
 latency)
@@ -77,11 +77,11 @@ chain)
   timeout -k 10 120 python bench/chain_bench.py --duration 10 --out "$OUT/chain.json" > "$OUT/chain.log" 2>&1
   ;;
 tracing)
-  timeout -k 10 300 python bench.py --steps 15 --warmup 3 --c1-reqs 0 > "$OUT/no_collector.json" 2>> "$OUT/err.log" &&
-  timeout -k 10 300 python bench.py --steps 15 --warmup 3 --c1-reqs 0 --zipkin-sink > "$OUT/sink.json" 2>> "$OUT/err.log" &&
-  timeout -k 10 300 python bench.py --steps 15 --warmup 3 --c1-reqs 0 --zipkin-sink --trace-queue 0 \
+  timeout -k 10 300 python bench.py --steps 15 --warmup 3 --c1-seconds 0 > "$OUT/no_collector.json" 2>> "$OUT/err.log" &&
+  timeout -k 10 300 python bench.py --steps 15 --warmup 3 --c1-seconds 0 --zipkin-sink > "$OUT/sink.json" 2>> "$OUT/err.log" &&
+  timeout -k 10 300 python bench.py --steps 15 --warmup 3 --c1-seconds 0 --zipkin-sink --trace-queue 0 \
     > "$OUT/sink_unbounded.json" 2>> "$OUT/err.log" &&
-  timeout -k 10 300 python bench.py --steps 15 --warmup 3 --c1-reqs 0 --no-tracing > "$OUT/tracing_off.json" 2>> "$OUT/err.log"
+  timeout -k 10 300 python bench.py --steps 15 --warmup 3 --c1-seconds 0 --no-tracing > "$OUT/tracing_off.json" 2>> "$OUT/err.log"
   ;;
 soak)
   MIN=${1:-5}

@@ -56,7 +56,7 @@ def test_bench_four_ranks_gloo():
     connections over all 4 replicas; the JSON line reports the node-wide total."""
     out = run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
                "--master-addr", "127.0.0.1", "--master-port", "29563", str(ROOT / "bench.py"), "--gpus", "4",
-               "--steps", "2", "--warmup", "1", "--reqs-per-conn", "50", "--c1-reqs", "0"], 18840)
+               "--steps", "2", "--warmup", "1", "--reqs-per-conn", "50", "--c1-seconds", "0"], 18840)
     assert out["n_gpus"] == 4 and out["requests"] == 4 * 64 * 50 * 2
     assert out["errors"] == 0 and out["non2xx"] == 0
     assert out["body_checked"] == out["requests"] and "c1_rps" not in out
@@ -74,7 +74,7 @@ def test_bench_pipelined():
     """--pipeline 16 (wrk's pipeline.lua): a step still completes connections x reqs-per-conn
     requests, every response is counted and checked, and the setting is recorded."""
     out = run([sys.executable, str(ROOT / "bench.py"), "--steps", "2", "--warmup", "1", "--reqs-per-conn", "160",
-               "--pipeline", "16", "--c1-reqs", "0"], 18860)
+               "--pipeline", "16", "--c1-seconds", "0"], 18860)
     assert out["requests"] == 64 * 160 * 2 and out["errors"] == 0 and out["non2xx"] == 0
     assert out["config"]["pipeline"] == 16 and "16 pipelined" in out["data"]
     # 16 requests per segment each way: far fewer than 2 segments per request

@@ -70,7 +70,7 @@ def test_tracing_as_deployed_on_host():
     reference image. Spans beyond the Brave-parity budget are dropped and counted, the rest
     reach the collector, and the request path does not slow down."""
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--steps", "4", "--warmup", "1",
-                        "--reqs-per-conn", "20000", "--c1-reqs", "0", "--zipkin-sink"],
+                        "--reqs-per-conn", "20000", "--c1-seconds", "0", "--zipkin-sink"],
                        capture_output=True, text=True, timeout=600, env={**os.environ, "HOLA_BENCH_PORT": "18720"})
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads(r.stdout.strip().splitlines()[-1])
