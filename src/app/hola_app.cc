@@ -425,8 +425,7 @@ void HolaApp::handle_chaining(http::Connection& c, const http::Request& r, Worke
   }
   // Async: the connection is parked until aloha answers, times out or is short-circuited.
   c.park();
-  c.hold();
-  http::Connection* conn = &c;
+  http::ConnRef conn(&c);  // held until the callback is gone, run or not
   std::shared_ptr<const Content> content = wc.content;
   HolaApp* self = this;
   chainer_->call(c.worker(), traced ? &span.ctx : nullptr,
@@ -490,7 +489,6 @@ void HolaApp::handle_chaining(http::Connection& c, const http::Request& r, Worke
                    }
                    if (traced) self->tracer_->end_server(w.index(), span, 200);
                    if (self->prom_) self->prom_->observe_chaining_us(w.index(), uint64_t(mono_ns() - t0) / 1000);
-                   conn->release();
                  });
 }
 

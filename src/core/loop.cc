@@ -24,6 +24,18 @@ EventLoop::EventLoop() {
 }
 
 EventLoop::~EventLoop() {
+  // Callbacks that never ran may own references that hand handlers back to this loop when
+  // destroyed (a ConnRef releasing its connection retires it): drop them first, then free
+  // every retired handler.
+  {
+    auto timers = std::move(timers_);
+    timers.clear();
+    std::vector<std::function<void()>> posted;
+    {
+      std::lock_guard<std::mutex> g(post_mu_);
+      posted.swap(posted_);
+    }
+  }
   for (Handler* h : retired_) delete h;
   if (wakefd_ >= 0) ::close(wakefd_);
   if (epfd_ >= 0) ::close(epfd_);

@@ -332,6 +332,10 @@ Worker::Worker(Server* s, int index) : server_(s), index_(index) {
   loop_.set_busy_poll_pause(s->options().busy_poll_pause);
 }
 
+Worker::~Worker() {
+  while (conns_) conns_->close_silently();  // unlinks itself from conns_
+}
+
 RequestHandler& Worker::handler() { return server_->handler(); }
 
 void Worker::tick() {
@@ -517,6 +521,8 @@ Worker* Server::pick_worker(int fd) {
 Server::~Server() {
   for (auto& a : acceptors_)
     if (a->fd >= 0) ::close(a->fd);
+  // Workers first, while the per-worker counters their connections update still exist.
+  workers_.clear();
 }
 
 bool Server::bind(std::string* err) {

@@ -65,11 +65,18 @@ class Connection final : public EventLoop::Handler {
   void start_streaming(std::function<void()> on_close);
   bool streaming() const { return streaming_; }
 
-  // Keeps the object alive across async callbacks even if the socket closes meanwhile.
+  // Keeps the object alive across async callbacks even if the socket closes meanwhile
+  // (prefer ConnRef, which cannot forget the release).
   void hold() { ++holds_; }
   void release();
 
   void close();
+  // close() without running the on_close callback: for tearing a worker down after the
+  // objects such callbacks point at may already be gone.
+  void close_silently() {
+    on_close_ = nullptr;
+    close();
+  }
 
   // Remote address (for tracing / logs).
   std::string peer() const;
@@ -160,6 +167,9 @@ struct StageProfile {
 class Worker {
  public:
   Worker(Server* s, int index);
+  // Runs after the worker's thread has stopped: connections still open (a drain that timed
+  // out) are closed without their callbacks and freed with the loop.
+  ~Worker();
   EventLoop& loop() { return loop_; }
   int index() const { return index_; }
   Server& server() { return *server_; }
@@ -201,6 +211,32 @@ class Worker {
   Connection* conns_ = nullptr;
   std::unique_ptr<StageProfile> profile_;
   std::shared_ptr<std::function<void()>> sweep_;  // idle-timeout sweeper (owned here)
+};
+
+// Counted reference to a Connection for asynchronous callbacks (aloha calls, SSE tickers):
+// holds it while any copy exists, so a callback that is destroyed without running — a
+// timer dropped at shutdown, say — still releases it. Copies and destruction happen on the
+// connection's worker thread, or after the worker has stopped.
+class ConnRef {
+ public:
+  ConnRef() = default;
+  explicit ConnRef(Connection* c) : c_(c) {
+    if (c_) c_->hold();
+  }
+  ConnRef(const ConnRef& o) : c_(o.c_) {
+    if (c_) c_->hold();
+  }
+  ConnRef(ConnRef&& o) noexcept : c_(o.c_) { o.c_ = nullptr; }
+  ConnRef& operator=(const ConnRef&) = delete;
+  ConnRef& operator=(ConnRef&&) = delete;
+  ~ConnRef() {
+    if (c_) c_->release();
+  }
+  Connection* operator->() const { return c_; }
+  Connection* get() const { return c_; }
+
+ private:
+  Connection* c_ = nullptr;
 };
 
 class Server {

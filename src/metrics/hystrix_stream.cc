@@ -156,16 +156,17 @@ std::string chunk(const std::string& data, bool chunked) {
 }
 }  // namespace
 
+// The pending timer owns the ticker, and the ticker holds the connection (ConnRef): when a
+// tick does not re-arm, or the loop drops its timers at shutdown, the connection is released.
 struct HystrixStream::Ticker : std::enable_shared_from_this<HystrixStream::Ticker> {
+  Ticker(std::shared_ptr<Sub> s, HystrixStream* st, http::Connection* c)
+      : sub(std::move(s)), stream(st), conn(c), loop(&c->worker().loop()) {}
   std::shared_ptr<Sub> sub;
-  HystrixStream* stream = nullptr;
-  http::Connection* conn = nullptr;
-  EventLoop* loop = nullptr;
+  HystrixStream* stream;
+  http::ConnRef conn;
+  EventLoop* loop;
   void fire() {
-    if (!sub->alive || conn->closed()) {
-      conn->release();  // balances the hold() taken at subscribe time
-      return;
-    }
+    if (!sub->alive || conn->closed()) return;
     // Hystrix's servlet writes block, so a subscriber that stops reading stalls only its own
     // servlet thread. Here writes are queued: past kMaxBacklog unsent bytes the frame is
     // skipped (memory stays bounded), and a subscriber whose socket has taken no bytes for
@@ -179,7 +180,6 @@ struct HystrixStream::Ticker : std::enable_shared_from_this<HystrixStream::Ticke
       } else if (now - sub->stalled_since_ms >= stream->stall_close_ms_) {
         stream->stalled_closed_.fetch_add(1, std::memory_order_relaxed);
         conn->close();
-        conn->release();
         return;
       }
     } else {
@@ -222,18 +222,12 @@ void HystrixStream::subscribe(http::Connection& c, const http::Request& r) {
   setsockopt(c.fd(), SOL_SOCKET, SO_SNDBUF, &sndbuf, sizeof sndbuf);
   c.send(head);
   HystrixStream* self = this;
-  c.hold();
   c.start_streaming([sub, self] {
     sub->alive = false;
     self->subscribers_.fetch_sub(1);
   });
-  auto t = std::make_shared<Ticker>();
-  t->sub = sub;
-  t->stream = this;
-  t->conn = &c;
-  t->loop = &c.worker().loop();
-  // Emit immediately, then every delay_ms until the subscriber goes away. The pending timer
-  // owns the ticker; when it is not re-armed the ticker is freed.
+  auto t = std::make_shared<Ticker>(sub, this, &c);
+  // Emit immediately, then every delay_ms until the subscriber goes away.
   t->loop->add_timer(0, [t] { t->fire(); });
 }
 

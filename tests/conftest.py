@@ -64,5 +64,15 @@ def hola(hola_bin):
         return p
 
     yield start
+    reports = []
     for p in procs:
-        p.stop()
+        rc = p.stop()
+        if os.environ.get("HOLA_SANITIZER"):
+            # Under a sanitizer build every server must exit cleanly and report nothing,
+            # including leaks found at exit (after the test's own assertions ran).
+            log = p.log()
+            if rc != 0 or "Sanitizer" in log or "runtime error" in log:
+                reports.append((rc, log[-4000:]))
+                with open(os.path.join(os.environ.get("TMPDIR", "/tmp"), "hola_sanitizer_report.log"), "a") as f:
+                    f.write(log)
+    assert not reports, reports[0]

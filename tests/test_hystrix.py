@@ -1,6 +1,7 @@
 """Hystrix 1.5.1 circuit-breaker state machine on a fake clock (native Command), the
 properties that tune it (config.properties:16-19) and /hystrix.stream (HystrixServlet.java)."""
 import json
+import os
 import socket
 import time
 
@@ -229,7 +230,8 @@ def test_stalled_subscriber_is_bounded_then_closed(hola):
             time.sleep(0.1)
         assert _metric(s, "hola_hystrix_stream_stalled_closed_total") == 1
         assert _metric(s, "hola_hystrix_stream_subscribers") == 0
-        assert s.memory_kb().get("VmRSS", 0) - rss0 < 4096
+        if not os.environ.get("HOLA_SANITIZER"):  # sanitizer allocators grow RSS on their own
+            assert s.memory_kb().get("VmRSS", 0) - rss0 < 4096
         out = _read_sse(s.port, seconds=0.3)  # the slot is free again
         assert b"200 OK" in out
     finally:

@@ -182,3 +182,38 @@ def test_sanitized_proxy(preset, tmp_path):
     assert rc == 0, (rc, text[-3000:])
     # only requests in flight on the killed replica may fail
     assert len(errors) <= 12, errors[:5]
+
+
+@pytest.mark.parametrize("preset", ["asan", "tsan"])
+def test_shutdown_with_parked_calls_and_streams_frees_everything(preset, tmp_path):
+    """SIGTERM while a chaining call is parked on a slow aloha (past a short drain), an SSE
+    subscriber is open and another never reads: every connection, ticker and pending callback
+    must be freed (LeakSanitizer at exit) without touching freed objects."""
+    build(preset)
+    exe = build_dir(preset) / "hola"
+    with FakeAloha() as aloha:
+        aloha.set_mode("slow", delay_s=3.0)
+        s = HolaProcess(args=["--aloha-url", aloha.url, "--feign-log", "none", "--drain-ms", "100",
+                              "--hystrix-timeout-ms", "5000"],
+                        env={"HOSTNAME": "san", **SAN_ENV[preset]}, threads=2, exe=exe, log_level="warn",
+                        wrapper=tsan_wrapper() if preset == "tsan" else None)
+        s.start(timeout=60)
+        socks = []
+        try:
+            t = threading.Thread(target=lambda: s.get("/api/hola-chaining", timeout=10), daemon=True)
+            t.start()
+            for rcvbuf in (None, 2048):
+                c = socket.socket()
+                if rcvbuf:
+                    c.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, rcvbuf)
+                c.connect(("127.0.0.1", s.port))
+                c.sendall(b"GET /hystrix.stream?delay=10 HTTP/1.1\r\nHost: x\r\n\r\n")
+                socks.append(c)
+            time.sleep(0.5)  # the call is parked, the streams are ticking
+        finally:
+            rc = s.stop(signal.SIGTERM, timeout=60)
+            for c in socks:
+                c.close()
+        log = s.log()
+    assert "Sanitizer" not in log and "runtime error" not in log, log[-6000:]
+    assert rc == 0, (rc, log[-3000:])
