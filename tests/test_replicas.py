@@ -2,6 +2,7 @@
 native round-robin proxy, greeting rotation, failure of a replica under load, supervisor
 restarts, graceful shutdown."""
 import json
+import os
 import signal
 import subprocess
 import threading
@@ -254,6 +255,10 @@ def test_proxy_backs_off_at_fd_limit():
         assert "is DOWN" not in px.log()  # running out of local fds says nothing about a backend
 
 
+@pytest.mark.skipif(bool(os.environ.get("HOLA_SANITIZER")),
+                    reason="UBSan's vptr check tests vtable readability through a pipe(2); at "
+                           "RLIMIT_NOFILE that pipe cannot be created and every virtual call is "
+                           "reported as 'invalid vptr' (a sanitizer false positive)")
 def test_server_backs_off_at_fd_limit(hola):
     s = hola(env={"HOSTNAME": "h"}, threads=1)
     _exhaust_fds_then_recover(s.proc.pid, s.port, 48)
