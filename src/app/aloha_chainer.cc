@@ -74,7 +74,7 @@ void AlohaChainer::stop() {
 
 client::ClientPool& AlohaChainer::pool(http::Worker& w) {
   auto& p = pools_[size_t(w.index())];
-  if (!p) p = std::make_unique<client::ClientPool>(w.loop(), target_, addr_.get());
+  if (!p) p = std::make_unique<client::ClientPool>(w.loop(), target_, addr_.get(), 64, &transport_retries_);
   return *p;
 }
 
@@ -289,6 +289,7 @@ void AlohaChainer::on_response(http::Worker& w, WorkerCalls& wc, uint32_t slot, 
     http::Worker* wp = &w;
     w.loop().add_timer(sleep_ms, [this, wp, &wc, slot, gen] {
       if (dead(wc, slot, gen)) return;
+      feign_retries_.fetch_add(1, std::memory_order_relaxed);
       if (o_.feign_log_basic) Logger::instance().raw("%s---> RETRYING", log_tag_.c_str());
       execute(*wp, wc, slot, gen);
     });

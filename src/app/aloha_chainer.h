@@ -69,6 +69,9 @@ class AlohaChainer final : public Chainer {
     timeout_ms_.store(s.timeout_enabled ? s.timeout_ms : 0, std::memory_order_relaxed);
   }
   const std::string& full_url() const { return full_url_; }
+  // Feign re-executions (Retryer) and HttpClient re-sends on a fresh connection, since start.
+  uint64_t feign_retries() const { return feign_retries_.load(std::memory_order_relaxed); }
+  uint64_t transport_retries() const { return transport_retries_.load(std::memory_order_relaxed); }
 
  private:
   struct Call;
@@ -96,6 +99,7 @@ class AlohaChainer final : public Chainer {
   tracing::Tracer* tracer_;
   const Clock& clock_;
   std::atomic<int> timeout_ms_{0};  // 0 = execution timeout disabled (read per call, lock-free)
+  std::atomic<uint64_t> feign_retries_{0}, transport_retries_{0};
 };
 
 }  // namespace hola::app

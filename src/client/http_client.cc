@@ -110,6 +110,7 @@ void ClientPool::Conn::fail(const std::string& why, bool io) {
     Callback c = std::move(cb);
     std::string r = std::move(out);
     const int t = tries + 1;
+    if (p->transport_retries_) p->transport_retries_->fetch_add(1, std::memory_order_relaxed);
     p->active_.erase(rid);
     p->destroy(this);
     auto* fresh = new Conn();
@@ -313,8 +314,9 @@ std::string ClientPool::connect_error(int err) const {
   return "HttpHostConnectException: Connect to " + target_.host + ":" + std::to_string(target_.port) + " failed: " + strerror(err);
 }
 
-ClientPool::ClientPool(EventLoop& loop, Url target, AddressCache* addr, size_t max_idle)
-    : loop_(loop), target_(std::move(target)), addr_(addr), max_idle_(max_idle) {
+ClientPool::ClientPool(EventLoop& loop, Url target, AddressCache* addr, size_t max_idle,
+                       std::atomic<uint64_t>* transport_retries)
+    : loop_(loop), target_(std::move(target)), addr_(addr), max_idle_(max_idle), transport_retries_(transport_retries) {
   host_header_ = target_.host;
   if (target_.port != 80) host_header_ += ":" + std::to_string(target_.port);
 }

@@ -71,7 +71,10 @@ bool parse_retry_after(std::string_view v, int64_t now_ms, int64_t* out_ms);
 class ClientPool {
  public:
   using Callback = std::function<void(ClientResult&&)>;
-  ClientPool(EventLoop& loop, Url target, AddressCache* addr, size_t max_idle = 64);
+  // `transport_retries` (optional, shared by the pools of all workers) counts requests
+  // re-sent on a fresh connection after an I/O error (DefaultHttpRequestRetryHandler role).
+  ClientPool(EventLoop& loop, Url target, AddressCache* addr, size_t max_idle = 64,
+             std::atomic<uint64_t>* transport_retries = nullptr);
   ~ClientPool();
   // Starts GET <path>; `cb` runs exactly once on the loop thread unless cancel() is called
   // first. Returns a request id.
@@ -99,6 +102,7 @@ class ClientPool {
   uint64_t next_id_ = 1;
   uint64_t opened_ = 0;
   std::string host_header_;
+  std::atomic<uint64_t>* transport_retries_;
 };
 
 }  // namespace hola::client

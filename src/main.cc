@@ -263,6 +263,7 @@ int main(int argc, char** argv) {
   prom.set_command(&chainer.command());
   prom.set_config_reloads([&cfg] { return cfg.reloads(); });
   prom.set_stream(&stream);
+  prom.set_retries([&chainer] { return chainer.feign_retries(); }, [&chainer] { return chainer.transport_retries(); });
   app.set_prometheus(&prom);
 
   cfg.start([&](const config::Snapshot& s) {

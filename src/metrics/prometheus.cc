@@ -94,6 +94,11 @@ std::string Prometheus::render(http::Server* server) const {
          (s.circuit_open ? "1" : "0") + "\n";
   }
   if (reloads_) o += "# TYPE hola_config_reloads_total counter\nhola_config_reloads_total " + std::to_string(reloads_()) + "\n";
+  if (feign_retries_ && transport_retries_) {
+    o += "# TYPE hola_aloha_retries_total counter\nhola_aloha_retries_total{kind=\"feign\"} " +
+         std::to_string(feign_retries_()) + "\nhola_aloha_retries_total{kind=\"transport\"} " +
+         std::to_string(transport_retries_()) + "\n";
+  }
   if (server) {
     o += "# TYPE hola_accept_locality_total counter\n";
     for (int l = 0; l < http::Server::kNumLocality; ++l)

@@ -49,6 +49,11 @@ class Prometheus {
   void set_command(resilience::Command* c) { cmd_ = c; }
   void set_config_reloads(std::function<uint64_t()> f) { reloads_ = std::move(f); }
   void set_stream(const HystrixStream* s) { stream_ = s; }
+  // Outbound retry counters (Feign Retryer, HttpClient re-sends).
+  void set_retries(std::function<uint64_t()> feign, std::function<uint64_t()> transport) {
+    feign_retries_ = std::move(feign);
+    transport_retries_ = std::move(transport);
+  }
   std::string render(http::Server* server) const;
 
  private:
@@ -69,6 +74,7 @@ class Prometheus {
   resilience::Command* cmd_ = nullptr;
   std::function<uint64_t()> reloads_;
   const HystrixStream* stream_ = nullptr;
+  std::function<uint64_t()> feign_retries_, transport_retries_;
 };
 
 }  // namespace hola::metrics

@@ -94,6 +94,9 @@ def test_dropped_connection_is_retried_until_the_hystrix_timeout(hola, aloha):
     # Feign attempts at ~0, 150, 375 ms, each 1 + 3 transport tries
     assert len(aloha.requests) == 12
     assert _events(s).get("TIMEOUT") == 1
+    _, _, body = s.get("/metrics")
+    assert b'hola_aloha_retries_total{kind="feign"} 2' in body
+    assert b'hola_aloha_retries_total{kind="transport"} 9' in body
 
 
 def test_connection_refused_retries_until_timeout_then_opens(hola):
