@@ -1,6 +1,7 @@
 """Command line entry point: ``python -m hola_amd <command>``.
 
-  build [--preset release|debug|tsan|asan]   compile the native artefacts in-tree
+  build [--preset P]                         compile the native artefacts in-tree (P: release,
+                                             debug, tsan, asan, or a release-* flag variant)
   serve [hola args...]                       run the service (same flags as the binary)
   cluster --replicas N [--port P] [--lb L]   N pinned replicas on P: behind the round-robin
                                              proxy (--lb proxy) or one SO_REUSEPORT group
