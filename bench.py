@@ -278,8 +278,9 @@ def main() -> int:
             "vs_baseline": None if BASELINE_VALUE is None else round(value / BASELINE_VALUE, 4),
             "dtype": "n/a (host-CPU HTTP service; no tensor compute)",
             "data": "synthetic closed-loop HTTP load (native loadgen, keep-alive, "
-                    + ("1 request in flight per connection)" if a.pipeline == 1 else
-                       f"{a.pipeline} pipelined requests in flight per connection)"),
+                    + ("1 request in flight per connection" if a.pipeline == 1 else
+                       f"{a.pipeline} pipelined requests in flight per connection")
+                    + ", every response body verified)",
             "p50_ms": round(percentile(hist, 50) / 1e6, 4),
             "p99_ms": round(percentile(hist, 99) / 1e6, 4),
             "p999_ms": round(percentile(hist, 99.9) / 1e6, 4),
