@@ -6,6 +6,7 @@
 # MODE
 #   final              smoke(), pytest -m gpu, the default bench (the driver's round-end tiers)
 #   bench ARGS...      one bench.py run with ARGS
+#   repeat REPS [ARGS] the default bench REPS times (run-to-run spread)
 #   ab REPS "label|args[|VAR=value]" ...   interleaved A/B of bench.py variants, REPS rounds
 #   rehearsal [Ns]     the driver's own N>1 command line (default N = 2 4 8) inside the box's
 #                      CPU slice, plus --profile-dir stage profiles for locality attribution
@@ -33,6 +34,13 @@ final)
   ;;
 bench)
   timeout -k 10 400 python bench.py "$@" > "$OUT/bench.json" 2>> "$OUT/err.log"
+  ;;
+repeat)
+  # the default bench REPS times back to back: run-to-run spread of the headline on this host
+  REPS=${1:-5}; shift
+  for rep in $(seq 1 "$REPS"); do
+    timeout -k 10 300 python bench.py "$@" > "$OUT/bench_$rep.json" 2>> "$OUT/err.log" || exit 1
+  done
   ;;
 ab)
   REPS=${1:?reps}; shift
