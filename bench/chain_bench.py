@@ -44,9 +44,11 @@ def cpu_s(pid: int) -> float:
 plan = plan_mirrored({"A": 2, "B": 1, "loadgen": 1})
 cores = [plan["A"], plan["B"], plan["loadgen"]]
 # B answers /api/hola-chaining itself with its own fallback (its aloha is unreachable and its
-# breaker opens), so A decodes ["Hola de B", "Aloha response (fallback)"].
+# breaker opens), so A decodes ["Hola de B", "Aloha response (fallback)"]. B does not retry
+# its refused aloha (--feign-retry off): a retrying B would answer only at its 600 ms
+# timeout until its breaker opens, and A's equal timeout would fall back first.
 with HolaProcess(args=["--aloha-url", "http://127.0.0.1:1/", "--feign-log", "none", "--no-tracing",
-                       "--log-level", "warn"], env={"HOSTNAME": "B"}, threads=len(cores[1]),
+                       "--feign-retry", "off", "--log-level", "warn"], env={"HOSTNAME": "B"}, threads=len(cores[1]),
                  cpu_list=format_cpu_list(cores[1])) as b:
     with HolaProcess(args=["--aloha-url", f"http://127.0.0.1:{b.port}/", "--aloha-path", "api/hola-chaining",
                            "--feign-log", "none", "--hystrix-pool-size", str(a.pool)],
@@ -55,16 +57,21 @@ with HolaProcess(args=["--aloha-url", "http://127.0.0.1:1/", "--feign-log", "non
         st, _, body = s.get("/api/hola-chaining")
         assert st == 200, body
         sample = json.loads(body)
+        assert sample[1:] == ["Hola de B", "Aloha response (fallback)"], sample  # two hops, no fallback at A
         c0, w0 = (cpu_s(s.proc.pid), cpu_s(b.proc.pid)), time.perf_counter()
+        # every response must be the two-hop body seen above (a fallback would differ)
         res = run_duration([("127.0.0.1", s.port)], a.connections, len(cores[2]), a.duration, 2.0,
-                           cpu_list=format_cpu_list(cores[2]), path="/api/hola-chaining")
+                           cpu_list=format_cpu_list(cores[2]), path="/api/hola-chaining",
+                           expect_bodies=[body.decode()])
         wall = time.perf_counter() - w0
         busy = {"A": (cpu_s(s.proc.pid) - c0[0]) / wall, "B": (cpu_s(b.proc.pid) - c0[1]) / wall}
         _, _, metrics = s.get("/metrics")
 events = {l.split('event="')[1].split('"')[0]: int(l.split()[-1]) for l in metrics.decode().splitlines()
           if l.startswith("hola_hystrix_events_total")}
 out = {"sample": sample, "rps": res["rps"], "p50_ms": res["latency"]["p50_ns"] / 1e6,
-       "p99_ms": res["latency"]["p99_ns"] / 1e6, "errors": res["latency"]["errors"], "hystrix_events": events,
+       "p99_ms": res["latency"]["p99_ns"] / 1e6, "errors": res["latency"]["errors"],
+       "body_checked": res["latency"].get("body_checked", 0), "body_mismatch": res["latency"].get("body_mismatch", 0),
+       "hystrix_events": events,
        # cores kept busy (warmup included) and CPU µs per request at the measured rate
        "cpus_busy": {k: round(v, 2) for k, v in busy.items()},
        "cpu_us_per_req": {k: round(v / res["rps"] * 1e6, 2) for k, v in busy.items()},

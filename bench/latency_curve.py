@@ -43,7 +43,7 @@ with HolaProcess(args=server_args, env={"HOSTNAME": "h"}, threads=len(srv), cpu_
         s0 = server_cpu()
         r = run_duration([("127.0.0.1", s.port)], a.connections, len(lg), a.duration, 2.0,
                          cpu_list=",".join(map(str, lg)), rate=rate, busy_poll_us=a.busy_poll_us,
-                         spin_us=a.spin_us)
+                         spin_us=a.spin_us, verify_body=True)
         c1 = resource.getrusage(resource.RUSAGE_CHILDREN)
         s1 = server_cpu()
         wall = a.duration + 2.0  # warmup included in both CPU figures

@@ -88,13 +88,15 @@ def run_point(n: int, args) -> dict:
                 res = run_duration(targets, conns, len(p["loadgen"]), args.duration, args.warmup,
                                    cpu_list=",".join(map(str, p["loadgen"])), busy_poll_us=args.busy_poll_us)
         else:
+            # client-side round-robin: one target per replica, so each target's body is fixed
             res = run_duration(rs.targets, conns, len(p["loadgen"]), args.duration, args.warmup,
-                               cpu_list=",".join(map(str, p["loadgen"])), busy_poll_us=args.busy_poll_us)
+                               cpu_list=",".join(map(str, p["loadgen"])), busy_poll_us=args.busy_poll_us,
+                               verify_body=args.lb == "client")
     lat = res["latency"]
     return {
         "replicas": n, "connections": conns, "lb": args.lb, "rps": res["rps"],
         "p50_ms": lat["p50_ns"] / 1e6, "p99_ms": lat["p99_ns"] / 1e6, "p999_ms": lat["p999_ns"] / 1e6,
-        "errors": lat["errors"], "non2xx": lat["non2xx"],
+        "errors": lat["errors"], "non2xx": lat["non2xx"], "body_mismatch": lat.get("body_mismatch", 0),
         "cpu_map": {"replicas": [format_cpu_list(c) for c in p["replicas"]], "proxy": format_cpu_list(p["proxy"]),
                     "loadgen": format_cpu_list(p["loadgen"])},
         "budget": budget, "quota": cgroup_cpu_quota(), "duration_s": args.duration,
