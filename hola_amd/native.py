@@ -43,13 +43,18 @@ def build_dir(preset: str = "release") -> Path:
     return BUILD_ROOT / preset
 
 
+# Inputs of the native build: C++ sources and headers, embedded assets, CMake files. Python
+# and shell tooling under bench/ is not one (editing it must not trigger a rebuild).
+_NATIVE_SUFFIXES = {".cc", ".h", ".cpp", ".hpp", ".cmake", ".html", ".json", ".yaml"}
+
+
 def _sources_newer_than(target: Path) -> bool:
     if not target.exists():
         return True
     t = target.stat().st_mtime
     for sub in ("src", "bench", "assets", "cmake"):
         for p in (REPO / sub).rglob("*"):
-            if p.is_file() and p.stat().st_mtime > t:
+            if p.suffix in _NATIVE_SUFFIXES and p.is_file() and p.stat().st_mtime > t:
                 return True
     return (REPO / "CMakeLists.txt").stat().st_mtime > t
 
