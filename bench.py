@@ -520,7 +520,7 @@ def _config2_subrun(a, host: str, port: int, load_cpus, bodies) -> dict | None:
     el = r["elapsed_ns"] / 1e9
     return {"rps": r["requests"] / el if el > 0 else 0.0, "requests": r["requests"], "elapsed_s": el,
             "p50_ns": st["p50_ns"], "p99_ns": st["p99_ns"], "errors": r["errors"],
-            "body_checked": st.get("body_checked", 0)}
+            "body_checked": st.get("body_checked", 0), "client_cpu": load_cpus[0]}
 
 
 def _c1_keys(c1: dict | None) -> dict:
@@ -528,7 +528,10 @@ def _c1_keys(c1: dict | None) -> dict:
         return {}
     return {"c1_rps": round(c1["rps"], 1), "c1_p50_ms": round(c1["p50_ns"] / 1e6, 4),
             "c1_p99_ms": round(c1["p99_ns"] / 1e6, 4), "c1_requests": c1["requests"],
-            "c1_errors": c1["errors"], "c1_body_checked": c1["body_checked"]}
+            "c1_errors": c1["errors"], "c1_body_checked": c1["body_checked"],
+            # the client's CPU: with --smt pair it is the SMT sibling of a server worker, and the
+            # connection is served on that same physical core (r18: slower for one connection)
+            "c1_client_cpu": c1["client_cpu"]}
 
 
 class _stdout_to_stderr:
