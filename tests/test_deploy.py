@@ -154,3 +154,34 @@ def test_configmap_patch_applies_to_the_deploymentconfig(native):
 def test_dockerfile_offers_the_reference_image_name():
     df = (ROOT / "deploy" / "Dockerfile").read_text()
     assert "-t redhatmsa/hola:0.0.1-SNAPSHOT" in df
+
+
+def test_dockerfile_build_stage_compiles_from_its_copy_set(tmp_path):
+    """No docker daemon here, so replay the image's build stage: copy exactly what the
+    Dockerfile COPYs into an empty tree and run its cmake commands. Catches a source the
+    image would miss (e.g. a new directory that is not COPY'd)."""
+    import shutil
+    import subprocess
+
+    df = (ROOT / "deploy" / "Dockerfile").read_text().split("\nFROM ", 2)[1]  # build stage only
+    copies = [l.split()[1:] for l in df.splitlines() if l.startswith("COPY ") and "--from" not in l]
+    assert copies
+    for srcs in copies:
+        *items, dest = srcs
+        for item in items:
+            src = ROOT / item
+            dst = tmp_path / (item if dest.endswith("/") or dest == "./" else dest)
+            if src.is_dir():
+                shutil.copytree(src, dst, ignore=shutil.ignore_patterns("__pycache__"))
+            else:
+                dst.parent.mkdir(parents=True, exist_ok=True)
+                shutil.copy2(src, dst)
+    gen = ["-G", "Ninja"] if shutil.which("ninja") else []
+    bdir = tmp_path / "build"
+    r = subprocess.run(["cmake", "-S", str(tmp_path), "-B", str(bdir), *gen, "-DCMAKE_BUILD_TYPE=Release",
+                        "-DHOLA_BUILD_PYTHON=OFF"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    r = subprocess.run(["cmake", "--build", str(bdir), "--target", "hola", "-j", "8"],
+                       capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert (bdir / "hola").exists()
