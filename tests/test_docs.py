@@ -1,0 +1,33 @@
+"""Docs that name code must stay true to it: every metric docs/OPERATIONS.md tells operators
+to watch is exported by /metrics, and every flag it lists is accepted by `hola`."""
+import re
+from pathlib import Path
+
+from hola_amd.testing.fakes import FakeAloha, FakeZipkin
+
+ROOT = Path(__file__).resolve().parent.parent
+OPS = (ROOT / "docs" / "OPERATIONS.md").read_text()
+
+
+def test_operations_metrics_are_exported(hola):
+    names = set(re.findall(r"`(hola_[a-z_]+)", OPS)) - {"hola_amd"}
+    with FakeAloha() as aloha, FakeZipkin() as zipkin:
+        s = hola(args=["--aloha-url", aloha.url, "--zipkin-url", zipkin.url, "--feign-log", "none"])
+        s.get("/api/hola")
+        s.get("/api/hola-chaining")
+        _, _, body = s.get("/metrics")
+    exported = set(re.findall(r"^(hola_[a-z_]+)", body.decode(), re.M))
+    exported |= {n[:-len("_bucket")] for n in exported if n.endswith("_bucket")}
+    missing = sorted(n for n in names if n not in exported)
+    assert not missing, missing
+
+
+def test_operations_flags_are_accepted(hola_bin):
+    import subprocess
+
+    help_text = subprocess.run([str(hola_bin), "--help"], capture_output=True, text=True).stdout + \
+        subprocess.run([str(hola_bin), "--help"], capture_output=True, text=True).stderr
+    flags = set(re.findall(r"`(--[a-z][a-z0-9-]+)", OPS)) - {"--replicas", "--out", "--lb", "--minutes", "--zipkin-sink",
+                                                              "--profile-out"}
+    missing = sorted(f for f in flags if f not in help_text)
+    assert not missing, missing
