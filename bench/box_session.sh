@@ -11,6 +11,7 @@
 #   rehearsal [Ns]     the driver's own N>1 command line (default N = 2 4 8) inside the box's
 #                      CPU slice, plus --profile-dir stage profiles for locality attribution
 #   locality           N = 1, 2, 4, 8 in the box's slice, L3-grouped vs. plain connection dealing
+#   pairmode           N = 1, 2, 4 with --smt pair (the 8-GPU node's per-replica layout shape)
 #   latency            BASELINE config 2 (1 connection) and the open-loop latency curve
 #   chain              two-hop chaining bench (loadgen -> hola A -> hola B)
 #   tracing            headline without a collector, with the native Zipkin sink (default 1000-span
@@ -73,6 +74,16 @@ locality)
     timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$n" \
       --master-addr 127.0.0.1 --master-port $((29700 + n)) bench.py --gpus "$n" --steps 8 --warmup 2 \
       --c1-seconds 0 --profile-dir "$OUT/prof_$tag" $extra > "$OUT/$tag.json" 2> "$OUT/err_$tag.log" || exit $?
+  done
+  ;;
+pairmode)
+  # the 8-GPU node's layout shape (--smt pair: each server worker with its client thread on
+  # one physical core) at N = 1, 2, 4 inside the box's 16-CPU quota
+  for spec in "1|8" "2|4" "4|2"; do
+    n=${spec%%|*}; cores=${spec#*|}
+    timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$n" \
+      --master-addr 127.0.0.1 --master-port $((29750 + n)) bench.py --gpus "$n" --cores "$cores" --smt pair \
+      --steps 8 --warmup 2 --profile-dir "$OUT/prof_n$n" > "$OUT/pair_n$n.json" 2> "$OUT/err_n$n.log" || exit $?
   done
   ;;
 latency)
