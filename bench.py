@@ -27,6 +27,9 @@ from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parent))
 
 from hola_amd.native import ensure_built  # noqa: E402
+from hola_amd.parallel.hostmetrics import (  # noqa: E402
+    accept_locality, cgroup_cpu_stat, proc_cpu_s, sink_stats, span_counters, start_zipkin_sink, tcp_counters,
+    thread_cpu_s)
 from hola_amd.parallel.loadgen import ControlledLoadgen, decode_hist, merge_hists, percentile  # noqa: E402
 from hola_amd.server import HolaProcess  # noqa: E402
 from hola_amd.utils.cpu import (  # noqa: E402
@@ -129,7 +132,7 @@ def main() -> int:
     plan = [None]
     sink = None
     if rank == 0 and a.zipkin_sink and not a.no_tracing:
-        sink = _start_sink()
+        sink = start_zipkin_sink()
     if rank == 0:
         slots = max(local_world, _gpu_slots())
         cores = a.cores or slot_cores(slots)
@@ -207,12 +210,12 @@ def main() -> int:
         if dist:
             dist.barrier()
         cuda()
-        span0 = _span_counters(host, port)
-        sink0 = _sink_stats(plan[0]["sink_port"]) if local_rank == 0 else {}
-        tracer0 = _thread_cpu_s(server.proc.pid, "hola-tracer")
-        cpu0 = (_proc_cpu_s(server.proc.pid), _proc_cpu_s(loadgen.proc.pid))
-        tcp0 = _tcp_counters()
-        thr0 = _cgroup_cpu_stat()
+        span0 = span_counters(host, port)
+        sink0 = sink_stats(plan[0]["sink_port"]) if local_rank == 0 else {}
+        tracer0 = thread_cpu_s(server.proc.pid, "hola-tracer")
+        cpu0 = (proc_cpu_s(server.proc.pid), proc_cpu_s(loadgen.proc.pid))
+        tcp0 = tcp_counters()
+        thr0 = cgroup_cpu_stat()
         t0 = time.perf_counter()
         reqs = errs = 0
         for _ in range(a.steps):
@@ -223,13 +226,13 @@ def main() -> int:
             dist.barrier()
         cuda()
         elapsed = time.perf_counter() - t0
-        cpu1 = (_proc_cpu_s(server.proc.pid), _proc_cpu_s(loadgen.proc.pid))
-        tracer1 = _thread_cpu_s(server.proc.pid, "hola-tracer")
-        span1 = _span_counters(host, port)
-        locality = _accept_locality(host, port)
-        sink1 = _sink_stats(plan[0]["sink_port"]) if local_rank == 0 else {}
-        tcp1 = _tcp_counters()
-        thr1 = _cgroup_cpu_stat()
+        cpu1 = (proc_cpu_s(server.proc.pid), proc_cpu_s(loadgen.proc.pid))
+        tracer1 = thread_cpu_s(server.proc.pid, "hola-tracer")
+        span1 = span_counters(host, port)
+        locality = accept_locality(host, port)
+        sink1 = sink_stats(plan[0]["sink_port"]) if local_rank == 0 else {}
+        tcp1 = tcp_counters()
+        thr1 = cgroup_cpu_stat()
         st = loadgen.stats()
         mem = server.memory_kb()
         c1 = _config2_subrun(a, host, port, load_cpus, bodies and [bodies[local_rank]]) if local_rank == 0 else None
@@ -365,79 +368,6 @@ def _own_loadgen(cores: list[dict]) -> list[list[int]]:
     return out
 
 
-def _start_sink():
-    """Native discard Zipkin collector on an ephemeral port: (process, port)."""
-    import subprocess
-    import tempfile
-
-    from hola_amd.native import binary
-
-    import atexit
-    import shutil
-
-    tmp = Path(tempfile.mkdtemp(prefix="hola_sink_"))
-    pf = tmp / "port"
-    proc = subprocess.Popen([str(binary("hola_zipkin_sink")), "--port", "0", "--port-file", str(pf)])
-
-    def stop():
-        if proc.poll() is None:
-            proc.terminate()
-            proc.wait(timeout=10)
-
-    atexit.register(stop)  # also on an exception before main()'s cleanup runs
-    try:
-        deadline = time.monotonic() + 10
-        while not pf.exists():
-            if proc.poll() is not None or time.monotonic() > deadline:
-                raise RuntimeError("hola_zipkin_sink did not start")
-            time.sleep(0.01)
-        return proc, int(pf.read_text())
-    finally:
-        shutil.rmtree(tmp, ignore_errors=True)
-
-
-def _sink_stats(port: int) -> dict:
-    if not port:
-        return {}
-    from hola_amd.utils.net import http_get
-    st, _, body = http_get("127.0.0.1", port, "/stats")
-    return json.loads(body) if st == 200 else {}
-
-
-def _span_counters(host: str, port: int) -> dict:
-    """hola_spans_* counters from a replica's /metrics (empty with tracing off)."""
-    from hola_amd.utils.net import http_get
-    try:
-        st, _, body = http_get(host, port, "/metrics")
-    except OSError:
-        return {}
-    out = {}
-    for line in body.decode().splitlines() if st == 200 else []:
-        if line.startswith("hola_spans_recorded_total "):
-            out["recorded"] = int(float(line.split()[1]))
-        elif line.startswith("hola_spans_reported_total "):
-            out["reported"] = int(float(line.split()[1]))
-        elif line.startswith("hola_spans_dropped_total{reason="):
-            out["dropped_" + line.split('"')[1]] = int(float(line.rsplit(" ", 1)[1]))
-    return out
-
-
-def _accept_locality(host: str, port: int) -> dict:
-    """hola_accept_locality_total from a replica's /metrics: where each accepted connection's
-    client thread ran relative to the worker serving it (same_core / same_l3 / same_socket /
-    cross_socket / unknown)."""
-    from hola_amd.utils.net import http_get
-    try:
-        st, _, body = http_get(host, port, "/metrics")
-    except OSError:
-        return {}
-    out = {}
-    for line in body.decode().splitlines() if st == 200 else []:
-        if line.startswith("hola_accept_locality_total{relation="):
-            out[line.split('"')[1]] = int(float(line.rsplit(" ", 1)[1]))
-    return out
-
-
 def _locality_block(gathered: list[dict]) -> dict:
     """Node-wide and per-replica fractions of accepted connections by client/worker
     relation. The bench's connections are all made before the timed region, so this is the
@@ -451,20 +381,6 @@ def _locality_block(gathered: list[dict]) -> dict:
             total[k] = total.get(k, 0) + v
     return {"accepted": sum(total.values()), "fraction": frac(total),
             "per_replica": [frac(g["locality"]) for g in gathered]}
-
-
-def _thread_cpu_s(pid: int, name: str) -> float:
-    """user+system CPU seconds of the thread of `pid` whose comm is `name` (0 if none)."""
-    total = 0.0
-    for task in Path(f"/proc/{pid}/task").glob("*"):
-        try:
-            if (task / "comm").read_text().strip() != name:
-                continue
-            fields = (task / "stat").read_text().rsplit(")", 1)[1].split()
-            total += (int(fields[11]) + int(fields[12])) / os.sysconf("SC_CLK_TCK")
-        except (OSError, IndexError, ValueError):
-            pass
-    return total
 
 
 def _tracing_block(a, gathered: list[dict], t: float, sink_port: int) -> dict:
@@ -582,16 +498,6 @@ def _free_port_block(start: int, n: int, host: str = "127.0.0.1") -> int:
     return start
 
 
-def _proc_cpu_s(pid: int) -> float:
-    """user+system CPU seconds of a process (all threads) from /proc/<pid>/stat."""
-    try:
-        with open(f"/proc/{pid}/stat") as f:
-            fields = f.read().rsplit(")", 1)[1].split()
-        return (int(fields[11]) + int(fields[12])) / os.sysconf("SC_CLK_TCK")
-    except (OSError, IndexError, ValueError):
-        return 0.0
-
-
 def _gpu_slots() -> int:
     """GPUs on this node (one replica slot each), visible to this process or not: the KFD
     topology lists every GPU agent (gpu_id != 0), whatever HIP_VISIBLE_DEVICES says; falls
@@ -609,42 +515,6 @@ def _gpu_slots() -> int:
         return int(torch.cuda.device_count())
     except Exception:
         return 0
-
-
-def _cgroup_cpu_stat() -> dict[str, int]:
-    """cgroup v2 cpu.stat counters of this process's cgroup (empty when unavailable)."""
-    try:
-        rel = next((l[3:] for l in Path("/proc/self/cgroup").read_text().splitlines() if l.startswith("0::")), "/")
-        for path in (Path("/sys/fs/cgroup") / rel.lstrip("/") / "cpu.stat", Path("/sys/fs/cgroup/cpu.stat")):
-            if path.exists():
-                return {k: int(v) for k, v in (l.split() for l in path.read_text().splitlines() if l.strip())}
-    except (OSError, IndexError, ValueError):
-        pass
-    return {}
-
-
-def _tcp_counters() -> dict[str, int]:
-    """Network-namespace-wide TCP counters (/proc/net/snmp `Tcp:`, /proc/net/netstat
-    `TcpExt:`): segments, and the ACK counts that show whether ACKs ride on the request and
-    response segments or travel as extra pure-ACK packets through the loopback path."""
-    want = {"Tcp": ("OutSegs", "InSegs", "RetransSegs"),
-            "TcpExt": ("DelayedACKs", "TCPPureAcks", "TCPHPAcks", "TCPAutoCorking")}
-    out: dict[str, int] = {}
-    for path in ("/proc/net/snmp", "/proc/net/netstat"):
-        try:
-            with open(path) as f:
-                lines = f.read().splitlines()
-        except OSError:
-            continue
-        for names, vals in zip(lines[::2], lines[1::2]):
-            group = names.split(":", 1)[0]
-            if group not in want:
-                continue
-            row = dict(zip(names.split()[1:], vals.split()[1:]))
-            for field in want[group]:
-                if row.get(field, "").lstrip("-").isdigit():
-                    out[field] = int(row[field])
-    return out
 
 
 def _cuda_sync_fn(local_rank: int):

@@ -1,0 +1,146 @@
+"""Host-side measurements for bench.py (BASELINE configs 2-4 on the MI355X node's EPYC cores).
+
+Process and thread CPU time from /proc, cgroup v2 CPU throttling, namespace-wide TCP segment
+counters, a replica's own /metrics counters (spans, connection placement), and the native
+discard Zipkin collector used by `bench.py --zipkin-sink`. Everything here reads the host;
+nothing touches a GPU.
+"""
+from __future__ import annotations
+
+import json
+import os
+import time
+from pathlib import Path
+
+
+def start_zipkin_sink():
+    """Native discard Zipkin collector on an ephemeral port: (process, port)."""
+    import subprocess
+    import tempfile
+
+    from hola_amd.native import binary
+
+    import atexit
+    import shutil
+
+    tmp = Path(tempfile.mkdtemp(prefix="hola_sink_"))
+    pf = tmp / "port"
+    proc = subprocess.Popen([str(binary("hola_zipkin_sink")), "--port", "0", "--port-file", str(pf)])
+
+    def stop():
+        if proc.poll() is None:
+            proc.terminate()
+            proc.wait(timeout=10)
+
+    atexit.register(stop)  # also on an exception before main()'s cleanup runs
+    try:
+        deadline = time.monotonic() + 10
+        while not pf.exists():
+            if proc.poll() is not None or time.monotonic() > deadline:
+                raise RuntimeError("hola_zipkin_sink did not start")
+            time.sleep(0.01)
+        return proc, int(pf.read_text())
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+def sink_stats(port: int) -> dict:
+    if not port:
+        return {}
+    from hola_amd.utils.net import http_get
+    st, _, body = http_get("127.0.0.1", port, "/stats")
+    return json.loads(body) if st == 200 else {}
+
+
+def span_counters(host: str, port: int) -> dict:
+    """hola_spans_* counters from a replica's /metrics (empty with tracing off)."""
+    from hola_amd.utils.net import http_get
+    try:
+        st, _, body = http_get(host, port, "/metrics")
+    except OSError:
+        return {}
+    out = {}
+    for line in body.decode().splitlines() if st == 200 else []:
+        if line.startswith("hola_spans_recorded_total "):
+            out["recorded"] = int(float(line.split()[1]))
+        elif line.startswith("hola_spans_reported_total "):
+            out["reported"] = int(float(line.split()[1]))
+        elif line.startswith("hola_spans_dropped_total{reason="):
+            out["dropped_" + line.split('"')[1]] = int(float(line.rsplit(" ", 1)[1]))
+    return out
+
+
+def accept_locality(host: str, port: int) -> dict:
+    """hola_accept_locality_total from a replica's /metrics: where each accepted connection's
+    client thread ran relative to the worker serving it (same_core / same_l3 / same_socket /
+    cross_socket / unknown)."""
+    from hola_amd.utils.net import http_get
+    try:
+        st, _, body = http_get(host, port, "/metrics")
+    except OSError:
+        return {}
+    out = {}
+    for line in body.decode().splitlines() if st == 200 else []:
+        if line.startswith("hola_accept_locality_total{relation="):
+            out[line.split('"')[1]] = int(float(line.rsplit(" ", 1)[1]))
+    return out
+
+
+def thread_cpu_s(pid: int, name: str) -> float:
+    """user+system CPU seconds of the thread of `pid` whose comm is `name` (0 if none)."""
+    total = 0.0
+    for task in Path(f"/proc/{pid}/task").glob("*"):
+        try:
+            if (task / "comm").read_text().strip() != name:
+                continue
+            fields = (task / "stat").read_text().rsplit(")", 1)[1].split()
+            total += (int(fields[11]) + int(fields[12])) / os.sysconf("SC_CLK_TCK")
+        except (OSError, IndexError, ValueError):
+            pass
+    return total
+
+
+def proc_cpu_s(pid: int) -> float:
+    """user+system CPU seconds of a process (all threads) from /proc/<pid>/stat."""
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            fields = f.read().rsplit(")", 1)[1].split()
+        return (int(fields[11]) + int(fields[12])) / os.sysconf("SC_CLK_TCK")
+    except (OSError, IndexError, ValueError):
+        return 0.0
+
+
+def cgroup_cpu_stat() -> dict[str, int]:
+    """cgroup v2 cpu.stat counters of this process's cgroup (empty when unavailable)."""
+    try:
+        rel = next((l[3:] for l in Path("/proc/self/cgroup").read_text().splitlines() if l.startswith("0::")), "/")
+        for path in (Path("/sys/fs/cgroup") / rel.lstrip("/") / "cpu.stat", Path("/sys/fs/cgroup/cpu.stat")):
+            if path.exists():
+                return {k: int(v) for k, v in (l.split() for l in path.read_text().splitlines() if l.strip())}
+    except (OSError, IndexError, ValueError):
+        pass
+    return {}
+
+
+def tcp_counters() -> dict[str, int]:
+    """Network-namespace-wide TCP counters (/proc/net/snmp `Tcp:`, /proc/net/netstat
+    `TcpExt:`): segments, and the ACK counts that show whether ACKs ride on the request and
+    response segments or travel as extra pure-ACK packets through the loopback path."""
+    want = {"Tcp": ("OutSegs", "InSegs", "RetransSegs"),
+            "TcpExt": ("DelayedACKs", "TCPPureAcks", "TCPHPAcks", "TCPAutoCorking")}
+    out: dict[str, int] = {}
+    for path in ("/proc/net/snmp", "/proc/net/netstat"):
+        try:
+            with open(path) as f:
+                lines = f.read().splitlines()
+        except OSError:
+            continue
+        for names, vals in zip(lines[::2], lines[1::2]):
+            group = names.split(":", 1)[0]
+            if group not in want:
+                continue
+            row = dict(zip(names.split()[1:], vals.split()[1:]))
+            for field in want[group]:
+                if row.get(field, "").lstrip("-").isdigit():
+                    out[field] = int(row[field])
+    return out
