@@ -27,6 +27,8 @@ PRESETS = {
     "debug": ["-DCMAKE_BUILD_TYPE=Debug"],
     "tsan": ["-DCMAKE_BUILD_TYPE=RelWithDebInfo", "-DHOLA_SANITIZE=thread", "-DHOLA_BUILD_PYTHON=OFF"],
     "asan": ["-DCMAKE_BUILD_TYPE=RelWithDebInfo", "-DHOLA_SANITIZE=address,undefined", "-DHOLA_BUILD_PYTHON=OFF"],
+    # gcov line coverage of the native code under the test suite (HOLA_SANITIZER=coverage)
+    "coverage": ["-DCMAKE_BUILD_TYPE=Debug", "-DHOLA_COVERAGE=ON", "-DHOLA_BUILD_PYTHON=OFF"],
     # compile-flag A/B variants of the release build (server binary via HOLA_SERVER_BIN)
     "release-v4": ["-DCMAKE_BUILD_TYPE=Release", "-DHOLA_MARCH=x86-64-v4", "-DHOLA_BUILD_PYTHON=OFF"],
     "release-o3lto": ["-DCMAKE_BUILD_TYPE=Release", "-DHOLA_OPT=-O3", "-DHOLA_LTO=ON", "-DHOLA_BUILD_PYTHON=OFF"],
