@@ -3,8 +3,11 @@
 * :class:`FakeAloha`  — the `aloha` service hola chains to (AlohaService.java:25). Its mode can
   be switched at runtime: ``ok`` / ``slow`` / ``error`` (HTTP 500) / ``garbage`` (invalid
   JSON) / ``chunked`` / ``chunked_lf`` (chunk lines ended by a bare LF) / ``close`` (drop the
-  connection) / ``unavailable`` (HTTP 503 with ``Retry-After: <retry_after>``). Records every
-  request's headers so tests can check B3 propagation.
+  connection) / ``unavailable`` (HTTP 503 with ``Retry-After: <retry_after>``) / ``empty``
+  (200, empty body) / ``json_null`` (200, ``null``) / ``no_content`` (204) /
+  ``close_delimited`` (no Content-Length, body ends at EOF) / ``drop_idle`` (keep-alive
+  response, then the socket closes while idle). Records every request's headers so tests can
+  check B3 propagation.
 * :class:`FakeZipkin` — a span collector recording POST /api/v1/spans and /api/v2/spans.
 """
 from __future__ import annotations
@@ -75,6 +78,12 @@ class _AlohaHandler(BaseHTTPRequestHandler):
             body, status = b"boom", 500
         elif mode == "unavailable":  # 503 + Retry-After: Feign's ErrorDecoder makes it retryable
             body, status = b"busy", 503
+        elif mode == "empty":
+            body, status = b"", 200
+        elif mode == "json_null":
+            body, status = b"null", 200
+        elif mode == "no_content":
+            body, status = b"", 204
         elif mode == "garbage":
             body, status = b"{not json", 200
         else:
@@ -83,6 +92,13 @@ class _AlohaHandler(BaseHTTPRequestHandler):
         self.send_header("Content-Type", "application/json")
         if mode == "unavailable":
             self.send_header("Retry-After", owner.retry_after)
+        if mode == "close_delimited":  # no Content-Length: the body ends with the connection
+            self.close_connection = True
+            self.end_headers()
+            self.wfile.write(body)
+            self.wfile.flush()
+            self.connection.shutdown(socket.SHUT_WR)
+            return
         if mode in ("chunked", "chunked_lf"):
             eol = b"\r\n" if mode == "chunked" else b"\n"  # bare LF: tolerated framing (RFC 9112 §2.2)
             self.send_header("Transfer-Encoding", "chunked")
@@ -92,9 +108,13 @@ class _AlohaHandler(BaseHTTPRequestHandler):
                 self.wfile.write(b"%x%s%s%s" % (len(part), eol, part, eol))
             self.wfile.write(b"0" + eol + eol)
         else:
-            self.send_header("Content-Length", str(len(body)))
+            if status != 204:
+                self.send_header("Content-Length", str(len(body)))
             self.end_headers()
             self.wfile.write(body)
+            if mode == "drop_idle":  # a kept-alive response, then the socket closes while idle
+                self.wfile.flush()
+                self.close_connection = True
 
 
 class FakeAloha(_Base):

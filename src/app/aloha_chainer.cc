@@ -155,6 +155,17 @@ bool AlohaChainer::dead(const WorkerCalls& wc, uint32_t slot, uint32_t gen) {
 }
 
 namespace {
+// feign-jackson's JacksonDecoder returns null for an empty body (before asking Jackson) and
+// Jackson maps a JSON `null` to null; a body of only whitespace is a decode error instead.
+bool decodes_to_null(std::string_view body) {
+  if (body.empty()) return true;
+  size_t b = 0, e = body.size();
+  auto ws = [](char c) { return c == ' ' || c == '\t' || c == '\r' || c == '\n'; };
+  while (b < e && ws(body[b])) ++b;
+  while (e > b && ws(body[e - 1])) --e;
+  return body.substr(b, e - b) == "null";
+}
+
 ChainResult fallback_result(const char* why) {
   ChainResult r;
   r.fallback = true;
@@ -259,7 +270,10 @@ void AlohaChainer::on_response(http::Worker& w, WorkerCalls& wc, uint32_t slot, 
   bool success = false, retryable = false;
   int64_t retry_after = 0;
   bool has_retry_after = false;
-  if (r.ok && r.status >= 200 && r.status < 300) {
+  if (r.ok && r.status >= 200 && r.status < 300 && decodes_to_null(r.body)) {
+    success = true;
+    res.null_list = true;
+  } else if (r.ok && r.status >= 200 && r.status < 300) {
     std::vector<std::optional<std::string>> items;
     if (json::decode_string_list(r.body, &items, &err)) {
       success = true;

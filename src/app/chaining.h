@@ -22,6 +22,10 @@ constexpr std::string_view kFallbackGreeting = "Aloha response (fallback)";
 struct ChainResult {
   std::vector<std::optional<std::string>> items;
   bool fallback = false;
+  // aloha answered 2xx without a list (empty body, or JSON null): Feign's JacksonDecoder
+  // returns null, the command succeeds, and greetings.addAll(null) then throws in
+  // HolaResource.holaChaining() (HolaResource.java:76), so the request fails with a 500.
+  bool null_list = false;
   std::string reason;  // why the fallback was used (timeout, short-circuited, ...)
 };
 

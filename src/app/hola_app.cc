@@ -433,6 +433,15 @@ void HolaApp::handle_chaining(http::Connection& c, const http::Request& r, Worke
                    http::Worker& w = conn->worker();
                    WorkerCache& wc = self->cache(w);
                    bool answered = false;
+                   if (!conn->closed() && res.null_list) {
+                     // greetings.addAll(null) throws after a successful command: a 500.
+                     if (wc.gen != self->gen_.load(std::memory_order_relaxed) || wc.date_version != w.date_version())
+                       self->refresh(w, wc);
+                     conn->complete(wc.server_error[ka][head].view(), ka);
+                     if (traced) self->tracer_->end_server(w.index(), span, 500);
+                     if (self->prom_) self->prom_->observe_chaining_us(w.index(), uint64_t(mono_ns() - t0) / 1000);
+                     return;
+                   }
                    if (!conn->closed() && res.fallback) {
                      // The prepared ["<greeting>","Aloha response (fallback)"] response, if the
                      // configuration has not changed since the request arrived.

@@ -405,3 +405,33 @@ def test_retry_sleeps_hold_the_bulkhead_slot(hola):
     assert first and first[0][1:] == [FALLBACK]
     ev = _events(s)
     assert ev.get("THREAD_POOL_REJECTED") == 1 and ev.get("TIMEOUT") == 1
+
+
+@pytest.mark.parametrize("mode", ["empty", "json_null", "no_content"])
+def test_list_decoding_to_null_is_a_500(hola, aloha, mode):
+    """feign-jackson's JacksonDecoder returns null for an empty body, and Jackson maps JSON
+    null to null: the Hystrix command succeeds, then greetings.addAll(null) throws in
+    holaChaining() (HolaResource.java:76), which the container answers with a 500."""
+    aloha.set_mode(mode)
+    s = hola(args=["--aloha-url", aloha.url, "--feign-log", "none"])
+    st, h, _ = s.get("/api/hola-chaining", timeout=10)
+    assert st == 500 and "access-control-allow-origin" not in h
+    assert _events(s).get("SUCCESS") == 1 and len(aloha.requests) == 1
+
+
+def test_close_delimited_aloha_body(hola, aloha):
+    aloha.set_mode("close_delimited")
+    s = hola(args=["--aloha-url", aloha.url, "--feign-log", "none"], env={"HOSTNAME": "h"})
+    for _ in range(3):  # a fresh connection each time
+        assert chain(s) == ["Hola de h", "Aloha mai aloha-1", "Bonjour de bonjour-1"]
+
+
+def test_idle_connection_closed_by_aloha_is_dropped(hola, aloha):
+    """aloha closes a kept-alive connection while it sits idle in the pool: the pool drops it
+    when the close arrives (or, if the next call races it, re-sends on a fresh connection)."""
+    aloha.set_mode("drop_idle")
+    s = hola(args=["--aloha-url", aloha.url, "--feign-log", "none"], env={"HOSTNAME": "h"}, threads=1)
+    for _ in range(5):
+        assert chain(s)[1:] == ["Aloha mai aloha-1", "Bonjour de bonjour-1"]
+        time.sleep(0.05)
+    assert _events(s).get("SUCCESS") == 5
