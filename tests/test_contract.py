@@ -416,3 +416,20 @@ def test_loadgen_url_with_ipv6_literal(hola):
     assert r.returncode == 0, r.stderr
     out = json.loads(r.stdout)
     assert out["rps"] > 0 and out["latency"]["errors"] == 0 and out["latency"]["non2xx"] == 0
+
+
+def test_request_body_over_limit_is_413_and_closes(hola):
+    """Request bodies are read and discarded (no route takes one); beyond 1 MiB the server
+    answers 413 and closes, for Content-Length and for chunked bodies. WildFly's listener
+    default is a 10 MB max-post-size; the lower bound here caps buffered bytes per
+    connection (docs/PARITY.md)."""
+    s = hola()
+    out = _raw(s.port, b"POST /api/hola HTTP/1.1\r\nHost: x\r\nContent-Length: 2000000\r\n\r\n" + b"x" * 1000)
+    assert out.startswith(b"HTTP/1.1 413") and b"Connection: close" in out
+    chunk = b"%x\r\n%s\r\n" % (600000, b"y" * 600000)
+    out = _raw(s.port, b"POST /api/hola HTTP/1.1\r\nHost: x\r\nTransfer-Encoding: chunked\r\n\r\n" + chunk * 2 + b"0\r\n\r\n")
+    assert out.startswith(b"HTTP/1.1 413")
+    # under the limit the body is skipped and the connection stays usable
+    small = b"POST /api/hola HTTP/1.1\r\nHost: x\r\nContent-Length: 5\r\n\r\nhello"
+    out = _raw(s.port, small + b"GET /api/health HTTP/1.1\r\nHost: x\r\nConnection: close\r\n\r\n")
+    assert out.startswith(b"HTTP/1.1 405") and out.count(b"HTTP/1.1 200 OK") == 1 and out.endswith(b"I'm ok")
