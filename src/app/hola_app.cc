@@ -297,6 +297,12 @@ void HolaApp::on_request(http::Connection& c, const http::Request& r) {
   if (!ka) c.close_after_response();
 
   std::string_view path = r.path;
+  char unparam[512];
+  if (__builtin_expect(path.find(';') != std::string_view::npos, 0) && path.size() <= sizeof unparam) {
+    size_t n = 0;
+    http::strip_path_parameters(path, unparam, &n);  // before decoding: %3B is not a delimiter
+    path = std::string_view(unparam, n);
+  }
   char decoded[512];
   if (path.find('%') != std::string_view::npos) {
     size_t n = 0;

@@ -89,6 +89,17 @@ bool percent_decode(std::string_view in, char* out, size_t* out_len, bool keep_e
   return true;
 }
 
+void strip_path_parameters(std::string_view in, char* out, size_t* out_len) {
+  size_t o = 0;
+  bool skipping = false;
+  for (char ch : in) {
+    if (ch == '/') skipping = false;
+    else if (ch == ';') skipping = true;
+    if (!skipping) out[o++] = ch;
+  }
+  *out_len = o;
+}
+
 bool remove_dot_segments(std::string_view in, char* out, size_t* out_len) {
   // RFC 3986 §5.2.4 on an absolute path, segment by segment: "." segments vanish, ".."
   // drops the last output segment (never above the root). A trailing "." or ".." leaves

@@ -55,5 +55,9 @@ bool percent_decode(std::string_view in, char* out, size_t* out_len, bool keep_e
 // canonicalises the request path before servlet/JAX-RS matching; false unless `in` starts
 // with '/'. Output written to out (len <= in len).
 bool remove_dot_segments(std::string_view in, char* out, size_t* out_len);
+// Drops path parameters (";name=value" up to the next '/') from every segment of a raw,
+// still percent-encoded path, as Undertow does before servlet and JAX-RS matching
+// ("/api/hola;jsessionid=x" -> "/api/hola"). Output written to out (len <= in len).
+void strip_path_parameters(std::string_view in, char* out, size_t* out_len);
 
 }  // namespace hola::http

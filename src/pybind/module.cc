@@ -348,6 +348,13 @@ PYBIND11_MODULE(_native, m) {
         py::arg("shared") = false);
   m.def("histogram_percentiles", &histogram_percentiles);
   m.def("is_local_resource_error", &is_local_resource_error);
+  m.def("strip_path_parameters", [](const std::string& p) {
+    std::string out(p.size(), '\0');
+    size_t n = 0;
+    http::strip_path_parameters(p, out.data(), &n);
+    out.resize(n);
+    return out;
+  });
   m.def("parse_retry_after", [](const std::string& v, int64_t now_ms) -> py::object {
     int64_t ms = 0;
     if (!client::parse_retry_after(v, now_ms, &ms)) return py::none();

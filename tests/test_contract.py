@@ -433,3 +433,17 @@ def test_request_body_over_limit_is_413_and_closes(hola):
     small = b"POST /api/hola HTTP/1.1\r\nHost: x\r\nContent-Length: 5\r\n\r\nhello"
     out = _raw(s.port, small + b"GET /api/health HTTP/1.1\r\nHost: x\r\nConnection: close\r\n\r\n")
     assert out.startswith(b"HTTP/1.1 405") and out.count(b"HTTP/1.1 200 OK") == 1 and out.endswith(b"I'm ok")
+
+
+def test_path_parameters_are_ignored_for_matching(hola, native):
+    """Undertow parses ";name=value" path parameters out of every segment before servlet and
+    JAX-RS matching (a ;jsessionid, a matrix parameter), so they never change the route; an
+    encoded %3B is not a delimiter (parity unpinned: no reference artefact covers it)."""
+    assert native.strip_path_parameters("/api/hola;jsessionid=abc") == "/api/hola"
+    assert native.strip_path_parameters("/api;v=1/hola;x;y=2/") == "/api/hola/"
+    assert native.strip_path_parameters("/api/hola%3Bx") == "/api/hola%3Bx"
+    s = hola(env={"HOSTNAME": "h"})
+    assert s.get("/api/hola;jsessionid=abc")[2] == b"Hola de h"
+    assert s.get("/api;v=1/hola")[2] == b"Hola de h"
+    assert s.get("/api/health;x")[2] == b"I'm ok"
+    assert s.get("/api/hola%3Bx")[0] == 404
