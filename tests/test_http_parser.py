@@ -201,3 +201,30 @@ def _rfc3986_remove_dot_segments(p: str) -> str:
 def test_remove_dot_segments_matches_rfc_oracle(native, segs):
     path = "/" + "/".join(segs)
     assert native.remove_dot_segments(path) == _rfc3986_remove_dot_segments(path)
+
+
+_seg = st.text(alphabet="abc/;=%3B.", max_size=12)
+
+
+@given(st.lists(_seg, max_size=6))
+@settings(max_examples=300, deadline=None)
+def test_strip_path_parameters_properties(native, parts):
+    """Against a Python oracle: every ';...' run up to the next '/' goes, '/' never does,
+    and stripping is idempotent."""
+    p = "/" + "/".join(parts)
+    out = native.strip_path_parameters(p)
+    oracle = "/".join(seg.split(";", 1)[0] for seg in p.split("/"))
+    assert out == oracle
+    assert ";" not in out and out.count("/") == p.count("/")
+    assert native.strip_path_parameters(out) == out
+
+
+@given(st.integers(min_value=0, max_value=10**6), st.integers(min_value=-10**6, max_value=10**6))
+@settings(max_examples=200, deadline=None)
+def test_retry_after_seconds_and_dates(native, secs, skew_s):
+    import email.utils
+
+    assert native.parse_retry_after(str(secs), 12345) == secs * 1000
+    now_ms = 1_700_000_000_000
+    date = email.utils.formatdate(now_ms / 1000 + skew_s, usegmt=True)
+    assert native.parse_retry_after(date, now_ms) == skew_s * 1000
