@@ -104,7 +104,7 @@ int main(int argc, char** argv) {
   if (zu) to.collector_url = zu;
   const char* hn = getenv("HOSTNAME");
   if (hn) ao.hostname = hn;  // HolaResource.java:57 getOrDefault("HOSTNAME", "unknown")
-  int threads = 0, drain_ms = 5000, stream_max = 5;
+  int threads = 0, drain_ms = 5000, stream_max = -1;
   int64_t stream_stall_ms = 30000;
   std::string cpu_list, port_file, profile_out;
   bool auto_pin = true;
@@ -254,6 +254,12 @@ int main(int argc, char** argv) {
   };
   app::AlohaChainer chainer(alo, hystrix_settings({}), threads, to.enabled ? &tracer : nullptr);
   app.set_chainer(&chainer);
+  if (stream_max < 0) {
+    // HystrixMetricsStreamServlet reads the Archaius property
+    // hystrix.stream.maxConcurrentConnections (default 5) [lib-default].
+    auto it = sysprops.find("hystrix.stream.maxConcurrentConnections");
+    stream_max = it != sysprops.end() && !it->second.empty() ? atoi(it->second.c_str()) : 5;
+  }
   metrics::HystrixStream stream(stream_max);
   stream.set_stall_close_ms(stream_stall_ms);
   stream.add_command(&chainer.command());

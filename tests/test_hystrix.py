@@ -185,9 +185,11 @@ def test_stream_connection_limit(hola):
     assert b"200 OK" in out
 
 
-def test_stream_limit_message_uses_configured_max(hola):
-    """The 503 text names the configured limit, as HystrixMetricsStreamServlet does."""
-    s = hola(args=["--hystrix-stream-max", "2"])
+@pytest.mark.parametrize("args", [["--hystrix-stream-max", "2"], ["-Dhystrix.stream.maxConcurrentConnections=2"]])
+def test_stream_limit_message_uses_configured_max(hola, args):
+    """The 503 text names the configured limit, as HystrixMetricsStreamServlet does; the limit
+    comes from --hystrix-stream-max or the servlet's Archaius property."""
+    s = hola(args=args)
     subs = []
     try:
         for _ in range(2):
