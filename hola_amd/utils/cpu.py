@@ -148,7 +148,9 @@ def plan_node(local_world: int, per_rank: int | None = None, avoid_busy: bool = 
     if len(phys) < per_rank * local_world:
         phys = allowed_cpus()
         per_rank = max(1, min(per_rank, len(phys) // max(1, local_world)))
-    busy = cpu_busy() if avoid_busy else {}
+    # 1 s of /proc/stat: other tenants' load on a shared host comes in bursts, and a short
+    # sample can rank a busy L3 domain as quiet
+    busy = cpu_busy(1.0) if avoid_busy else {}
     load = {c: sum(busy.get(x, 0.0) for x in siblings(c)) for c in phys}
     domains: dict[int, list[int]] = {}
     for c in phys:
