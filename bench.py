@@ -5,13 +5,19 @@ One rank per "GPU slot" of the node = one hola replica. Every rank:
   * starts a `hola` replica pinned to its own share of the host cores (the GPUs stay idle:
     the reference has no tensor work — SURVEY.md §0),
   * drives it with the native closed-loop load generator on disjoint cores; the generator's
-    64 keep-alive connections per replica are dealt round-robin over ALL replicas of the
+    64 keep-alive connections per replica are dealt round-robin over the replicas of the
     node (client-side round-robin, BASELINE.json config 4: "512 connections against 8
-    replicas behind round-robin"; N=1 is config 3: 64 connections, 1 replica).
+    replicas behind round-robin"; N=1 is config 3: 64 connections, 1 replica), each
+    load-generator thread on the L3 (or SMT sibling core) of the replicas it drives.
 A step = connections x `--reqs-per-conn` requests per replica, drawn by the connections from
-a shared budget (weak scaling: the work per replica is fixed). W warmup steps, then exactly K timed steps between barriers; the elapsed
-time is the MAX over ranks, `value` is the node-wide total req/s, and p50/p99 come from the
-merged latency histograms of all ranks.
+a shared budget (weak scaling: the work per replica is fixed). W warmup steps, then exactly
+K timed steps between barriers; the elapsed time is the MAX over ranks, `value` is the
+node-wide total req/s, and p50/p99 come from the merged latency histograms of all ranks.
+Every response body in the timed region is compared with the greeting of the replica behind
+its connection (a mismatch is an error). After the timed region rank 0 runs BASELINE config
+2 (one connection, ~3 s) and reports it as c1_* keys; the JSON also carries span accounting
+(`tracing`, with a native collector under --zipkin-sink) and connection placement
+(`locality`).
 
   python bench.py --gpus N --steps K --warmup W
 """
