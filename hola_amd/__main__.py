@@ -112,8 +112,11 @@ def _info() -> int:
 
     budget = cpu_budget()
     for n in (1, 2, 4, 8):
-        per_rank = min(cores, max(1, budget // n))
-        smt = "pair" if smt_fits(slots, per_rank) else "off"
+        # bench.py plans N ranks as max(N, GPU slots) slots, so a node with fewer GPUs than
+        # ranks (a rehearsal on the 1-GPU box) splits its budget further
+        s = max(n, slots)
+        per_rank = min(slot_cores(s), max(1, budget // n))
+        smt = "pair" if smt_fits(s, per_rank) else "off"
         try:
             plans = plan_replicas_with_loadgen(n, per_rank, avoid_busy=False, smt=smt)
         except (IndexError, ValueError) as e:
