@@ -35,8 +35,9 @@ namespace {
 void usage() {
   fprintf(stderr,
           "usage: hola [options] [-Dkey=value ...]\n"
-          "  --port N                 listen port (default 8080)\n"
-          "  --host ADDR              listen address (default 0.0.0.0)\n"
+          "  --port N                 listen port (default: -Dswarm.http.port, 8080, plus\n"
+          "                           -Dswarm.port.offset)\n"
+          "  --host ADDR              listen address (default: -Dswarm.bind.address, 0.0.0.0)\n"
           "  --threads N              event-loop workers (default: one per allowed CPU, capped by cgroup quota)\n"
           "  --cpu-list LIST          pin workers to these CPUs, e.g. 0-3,8\n"
           "  --accept rr|reuseport    connection distribution (default rr)\n"
@@ -109,6 +110,7 @@ int main(int argc, char** argv) {
   std::string cpu_list, port_file, profile_out;
   bool auto_pin = true;
   bool no_tracing = false;
+  bool port_flag = false, host_flag = false;
 
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
@@ -120,8 +122,13 @@ int main(int argc, char** argv) {
       size_t eq = a.find('=');
       if (eq == std::string::npos) sysprops[a.substr(2)] = "";
       else sysprops[a.substr(2, eq - 2)] = a.substr(eq + 1);
-    } else if (a == "--port") so.port = atoi(val("--port").c_str());
-    else if (a == "--host") so.host = val("--host");
+    } else if (a == "--port") {
+      so.port = atoi(val("--port").c_str());
+      port_flag = true;
+    } else if (a == "--host") {
+      so.host = val("--host");
+      host_flag = true;
+    }
     else if (a == "--threads") threads = atoi(val("--threads").c_str());
     else if (a == "--cpu-list") cpu_list = val("--cpu-list");
     else if (a == "--accept") {
@@ -191,6 +198,40 @@ int main(int argc, char** argv) {
       usage();
       return 2;
     }
+  }
+
+  // ---- listen address ----
+  // WildFly Swarm 1.0's socket-binding properties (on the command line or in JAVA_OPTIONS, as
+  // `java -Dswarm.http.port=8081 -jar hola-swarm.jar` takes them): swarm.http.port (8080),
+  // swarm.port.offset added to it, swarm.bind.address (0.0.0.0). An explicit --port / --host
+  // wins and takes no offset.
+  if (!port_flag) {
+    auto prop_int = [&](const char* k, int dflt, int* out) {
+      auto it = sysprops.find(k);
+      if (it == sysprops.end() || it->second.empty()) {
+        *out = dflt;
+        return true;
+      }
+      char* end = nullptr;
+      long v = strtol(it->second.c_str(), &end, 10);
+      if (*end || v < -65535 || v > 65535) {
+        fprintf(stderr, "hola: bad -D%s=%s\n", k, it->second.c_str());
+        return false;
+      }
+      *out = int(v);
+      return true;
+    };
+    int port = 0, offset = 0;
+    if (!prop_int("swarm.http.port", so.port, &port) || !prop_int("swarm.port.offset", 0, &offset)) return 2;
+    if (port + offset < 0 || port + offset > 65535) {
+      fprintf(stderr, "hola: swarm.http.port %d + swarm.port.offset %d is not a port\n", port, offset);
+      return 2;
+    }
+    so.port = port + offset;
+  }
+  if (!host_flag) {
+    auto it = sysprops.find("swarm.bind.address");
+    if (it != sysprops.end() && !it->second.empty()) so.host = it->second;
   }
 
   // ---- CPUs / workers ----

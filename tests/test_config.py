@@ -58,6 +58,74 @@ def test_conf_from_java_options(hola, tmp_path):
     assert s.get("/api/hola")[2] == b"Hi from h"
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run_until_port(hola_bin, tmp_path, args, env=None, timeout=10.0):
+    """Starts the binary without --port/--host and returns (proc, bound port)."""
+    import subprocess
+
+    pf = tmp_path / "port"
+    p = subprocess.Popen([str(hola_bin), "--threads", "1", "--port-file", str(pf), "--log-level", "warn", *args],
+                         env={**os.environ, "HOSTNAME": "h", **(env or {})},
+                         stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+    deadline = time.monotonic() + timeout
+    while time.monotonic() < deadline and p.poll() is None:
+        if pf.exists() and pf.read_text().strip():
+            return p, int(pf.read_text())
+        time.sleep(0.02)
+    p.kill()
+    raise AssertionError(f"no port (rc {p.wait()}): {p.stderr.read().decode()}")
+
+
+def _get(port, host="127.0.0.1"):
+    import http.client
+
+    c = http.client.HTTPConnection(host, port, timeout=5)
+    c.request("GET", "/api/hola")
+    r = c.getresponse()
+    return r.status, r.read()
+
+
+@pytest.mark.parametrize("via", ["argv", "java_options"])
+def test_swarm_socket_binding_properties(hola_bin, tmp_path, via):
+    """`java -Dswarm.http.port=P -Dswarm.port.offset=K -jar hola-swarm.jar` listens on P + K
+    (WildFly Swarm 1.0 socket bindings), on swarm.bind.address; JAVA_OPTIONS works too."""
+    port = _free_port()
+    props = [f"-Dswarm.http.port={port - 1}", "-Dswarm.port.offset=1", "-Dswarm.bind.address=127.0.0.1"]
+    args, env = (props, None) if via == "argv" else ([], {"JAVA_OPTIONS": "-Xmx512m " + " ".join(props)})
+    p, bound = _run_until_port(hola_bin, tmp_path, args, env)
+    try:
+        assert bound == port
+        assert _get(bound) == (200, b"Hola de h")
+    finally:
+        p.terminate()
+        assert p.wait(timeout=10) == 0
+
+
+def test_explicit_port_flag_wins_over_swarm_properties(hola_bin, tmp_path):
+    p, bound = _run_until_port(hola_bin, tmp_path, ["--host", "127.0.0.1", "--port", "0",
+                                                     "-Dswarm.http.port=1", "-Dswarm.port.offset=5"])
+    try:
+        assert bound not in (1, 6) and _get(bound)[0] == 200
+    finally:
+        p.terminate()
+        p.wait(timeout=10)
+
+
+@pytest.mark.parametrize("bad", [["-Dswarm.http.port=http"], ["-Dswarm.http.port=65535", "-Dswarm.port.offset=1"]])
+def test_bad_swarm_port_is_a_usage_error(hola_bin, bad):
+    import subprocess
+
+    r = subprocess.run([str(hola_bin), "--threads", "1", *bad], capture_output=True, text=True, timeout=10)
+    assert r.returncode == 2 and "swarm" in r.stderr
+
+
 def test_missing_or_broken_conf_uses_default(hola, tmp_path):
     s = hola(args=[f"-Dconf={tmp_path / 'absent.properties'}"], env={"HOSTNAME": "h"})
     assert s.get("/api/hola")[2] == b"Hola de h"
