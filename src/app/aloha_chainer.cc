@@ -62,10 +62,10 @@ AlohaChainer::AlohaChainer(AlohaOptions o, resilience::Settings s, int num_worke
 AlohaChainer::~AlohaChainer() { stop(); }
 
 void AlohaChainer::start() {
-  if (addr_) {
-    addr_->resolve_now();
-    addr_->start();
-  }
+  // Resolution runs on the cache's thread; start-up waits for it only briefly, so /api/hola
+  // serves at once even when the DNS server for aloha's name does not answer. Until then an
+  // aloha call fails as UnknownHostException (retried by Feign inside the Hystrix timeout).
+  if (addr_) addr_->start();
 }
 
 void AlohaChainer::stop() {

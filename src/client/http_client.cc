@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
 #include <ctime>
@@ -19,50 +20,101 @@ namespace hola::client {
 
 // ---------------------------------------------------------------- AddressCache
 
+struct AddressCache::State {
+  State(std::string h, int p) : host(std::move(h)), port(p) {}
+  const std::string host;
+  const int port;
+  std::mutex mu;
+  std::condition_variable cv;
+  bool ok = false;
+  bool answered = false;  // the first resolution has finished (either way)
+  bool stop = false;
+  bool done = false;  // the thread has left its loop
+  sockaddr_storage addr{};
+  socklen_t len = 0;
+  std::string err;
+};
+
+namespace {
+// Bounded wait against the system clock: libstdc++ implements steady-clock waits with
+// pthread_cond_clockwait, which the toolchain's ThreadSanitizer does not intercept (it then
+// reports a false "double lock"); pthread_cond_timedwait is intercepted.
+template <class Pred>
+bool wait_ms(std::condition_variable& cv, std::unique_lock<std::mutex>& g, int ms, Pred p) {
+  return cv.wait_until(g, std::chrono::system_clock::now() + std::chrono::milliseconds(ms), p);
+}
+}  // namespace
+
 AddressCache::AddressCache(std::string host, int port, int refresh_ms)
-    : host_(std::move(host)), port_(port), refresh_ms_(refresh_ms) {}
+    : st_(std::make_shared<State>(std::move(host), port)), refresh_ms_(refresh_ms) {
+  // Java's UnknownHostException message is the host name.
+  st_->err = "UnknownHostException: " + st_->host;
+}
 
 AddressCache::~AddressCache() { stop(); }
 
-void AddressCache::resolve_now() {
+void AddressCache::resolve(State& s) {
   sockaddr_storage ss{};
   socklen_t len = 0;
   std::string err;
-  bool ok = resolve_host(host_, port_, &ss, &len, &err);
-  std::lock_guard<std::mutex> g(mu_);
-  ok_ = ok;
+  bool ok = resolve_host(s.host, s.port, &ss, &len, &err);
+  std::lock_guard<std::mutex> g(s.mu);
+  s.ok = ok;
+  s.answered = true;
   if (ok) {
-    addr_ = ss;
-    len_ = len;
-    err_.clear();
+    s.addr = ss;
+    s.len = len;
+    s.err.clear();
   } else {
-    err_ = "UnknownHostException: " + err;
+    s.err = "UnknownHostException: " + err;
   }
+  s.cv.notify_all();
 }
 
-void AddressCache::start() {
-  th_ = std::thread([this] {
-    while (!stop_.load()) {
-      resolve_now();
-      for (int waited = 0; waited < refresh_ms_ && !stop_.load(); waited += 50)
-        std::this_thread::sleep_for(std::chrono::milliseconds(50));
+void AddressCache::resolve_now() { resolve(*st_); }
+
+void AddressCache::start(int first_wait_ms) {
+  std::shared_ptr<State> st = st_;
+  const int refresh = refresh_ms_;
+  th_ = std::thread([st, refresh] {
+    std::unique_lock<std::mutex> g(st->mu);
+    while (!st->stop) {
+      g.unlock();
+      resolve(*st);
+      g.lock();
+      wait_ms(st->cv, g, refresh, [&] { return st->stop; });
     }
+    st->done = true;
+    st->cv.notify_all();
   });
+  std::unique_lock<std::mutex> g(st_->mu);
+  wait_ms(st_->cv, g, first_wait_ms, [&] { return st_->answered; });
 }
 
 void AddressCache::stop() {
-  stop_.store(true);
-  if (th_.joinable()) th_.join();
+  if (!th_.joinable()) return;
+  bool done;
+  {
+    std::unique_lock<std::mutex> g(st_->mu);
+    st_->stop = true;
+    st_->cv.notify_all();
+    done = wait_ms(st_->cv, g, 200, [&] { return st_->done; });
+  }
+  // A thread inside getaddrinfo() cannot be interrupted, and joining it would make shutdown
+  // wait for a DNS timeout: it holds its own reference to the state, sees `stop` when the
+  // call returns and exits.
+  if (done) th_.join();
+  else th_.detach();
 }
 
 bool AddressCache::get(sockaddr_storage* out, socklen_t* len, std::string* err) const {
-  std::lock_guard<std::mutex> g(mu_);
-  if (!ok_) {
-    if (err) *err = err_;
+  std::lock_guard<std::mutex> g(st_->mu);
+  if (!st_->ok) {
+    if (err) *err = st_->err;
     return false;
   }
-  *out = addr_;
-  *len = len_;
+  *out = st_->addr;
+  *len = st_->len;
   return true;
 }
 

@@ -27,23 +27,23 @@ class AddressCache {
  public:
   AddressCache(std::string host, int port, int refresh_ms = 5000);
   ~AddressCache();
-  void start();
+  // Starts the resolver thread and waits up to first_wait_ms for its first answer: a name
+  // that resolves at once (an IP literal, /etc/hosts, a healthy DNS) is ready before the
+  // first call, while an unreachable DNS server delays start-up by at most that long.
+  void start(int first_wait_ms = 1000);
+  // Does not wait for a getaddrinfo() that is stuck: the thread is left to finish on its own
+  // (it shares the state it writes, so it outlives this object safely).
   void stop();
   // false when the host has not (yet) resolved.
   bool get(sockaddr_storage* out, socklen_t* len, std::string* err) const;
-  void resolve_now();  // synchronous (tests / startup)
+  void resolve_now();  // synchronous (tests)
 
  private:
-  std::string host_;
-  int port_;
+  struct State;
+  static void resolve(State& s);
+  std::shared_ptr<State> st_;
   int refresh_ms_;
-  mutable std::mutex mu_;
-  bool ok_ = false;
-  sockaddr_storage addr_{};
-  socklen_t len_ = 0;
-  std::string err_ = "not resolved yet";
   std::thread th_;
-  std::atomic<bool> stop_{false};
 };
 
 struct ClientResult {
