@@ -122,15 +122,22 @@ bool read_response(int fd, BlockingResponse* out, bool* close_delimited) {
   return true;
 }
 
-bool blocking_request(const Url& u, int* fd, std::string_view method, std::string_view path,
-                      std::string_view extra_headers, std::string_view body, int timeout_ms,
-                      BlockingResponse* out) {
+namespace {
+bool request_on(const Url& u, const sockaddr_storage* addr, socklen_t addr_len, int* fd, std::string_view method,
+                std::string_view path, std::string_view extra_headers, std::string_view body, int timeout_ms,
+                BlockingResponse* out) {
   for (int attempt = 0; attempt < 2; ++attempt) {
     bool reused = *fd >= 0;
     if (*fd < 0) {
       sockaddr_storage ss{};
       socklen_t len = 0;
-      if (!resolve_host(u.host, u.port, &ss, &len, nullptr)) return false;
+      if (addr) {
+        if (addr_len == 0) return false;  // no address known: only a kept-alive socket will do
+        ss = *addr;
+        len = addr_len;
+      } else if (!resolve_host(u.host, u.port, &ss, &len, nullptr)) {
+        return false;
+      }
       *fd = connect_blocking(ss, len, timeout_ms);
       if (*fd < 0) return false;
       timeval tv{timeout_ms / 1000, (timeout_ms % 1000) * 1000};
@@ -158,6 +165,19 @@ bool blocking_request(const Url& u, int* fd, std::string_view method, std::strin
     if (!reused) return false;  // a stale kept-alive socket gets one retry
   }
   return false;
+}
+}  // namespace
+
+bool blocking_request(const Url& u, int* fd, std::string_view method, std::string_view path,
+                      std::string_view extra_headers, std::string_view body, int timeout_ms,
+                      BlockingResponse* out) {
+  return request_on(u, nullptr, 0, fd, method, path, extra_headers, body, timeout_ms, out);
+}
+
+bool blocking_request(const Url& u, const sockaddr_storage& addr, socklen_t addr_len, int* fd,
+                      std::string_view method, std::string_view path, std::string_view extra_headers,
+                      std::string_view body, int timeout_ms, BlockingResponse* out) {
+  return request_on(u, &addr, addr_len, fd, method, path, extra_headers, body, timeout_ms, out);
 }
 
 }  // namespace hola::client

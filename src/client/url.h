@@ -1,6 +1,8 @@
 // http:// URL parsing and a small blocking HTTP/1.1 client (used off the request path: the
 // Zipkin reporter thread, the load generator's sanity check and the proxy health checks).
 #pragma once
+#include <sys/socket.h>
+
 #include <string>
 #include <string_view>
 
@@ -26,6 +28,12 @@ struct BlockingResponse {
 bool blocking_request(const Url& u, int* fd, std::string_view method, std::string_view path,
                       std::string_view extra_headers, std::string_view body, int timeout_ms,
                       BlockingResponse* out);
+// The same, connecting to an address resolved beforehand (e.g. by an AddressCache) when a new
+// connection is needed (addr_len 0: none known, so only a kept-alive *fd can be used); u.host
+// still names the Host header.
+bool blocking_request(const Url& u, const sockaddr_storage& addr, socklen_t addr_len, int* fd,
+                      std::string_view method, std::string_view path, std::string_view extra_headers,
+                      std::string_view body, int timeout_ms, BlockingResponse* out);
 
 // Reads one HTTP/1.1 response (Content-Length / chunked / close-delimited) from a blocking fd.
 bool read_response(int fd, BlockingResponse* out, bool* close_delimited);

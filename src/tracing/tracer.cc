@@ -12,6 +12,7 @@
 #include <cstring>
 #include <type_traits>
 
+#include "client/http_client.h"
 #include "client/url.h"
 #include "core/clock.h"
 #include "core/log.h"
@@ -68,6 +69,7 @@ Tracer::Tracer(TracerOptions o, int num_workers) : o_(std::move(o)) {
       cport_ = u.port;
       cpath_ = u.base_path + (o_.v2 ? "api/v2/spans" : "api/v1/spans");
       collecting_ = true;
+      caddr_ = std::make_unique<client::AddressCache>(chost_, cport_);
     } else {
       LOG_WARN("ZIPKIN_SERVER_URL '%s' is not an http:// URL; spans will be dropped", o_.collector_url.c_str());
     }
@@ -319,7 +321,17 @@ bool Tracer::post(const std::string& body) {
   u.host = chost_;
   u.port = cport_;
   client::BlockingResponse resp;
-  bool ok = client::blocking_request(u, &cfd_, "POST", cpath_, "Content-Type: application/json\r\n", body, 2000, &resp);
+  const char* hdr = "Content-Type: application/json\r\n";
+  bool ok;
+  if (running_) {
+    // the reporter is up, so is the resolver thread: never resolve here
+    sockaddr_storage ss{};
+    socklen_t len = 0;
+    if (!caddr_->get(&ss, &len, nullptr)) len = 0;
+    ok = client::blocking_request(u, ss, len, &cfd_, "POST", cpath_, hdr, body, 2000, &resp);
+  } else {
+    ok = client::blocking_request(u, &cfd_, "POST", cpath_, hdr, body, 2000, &resp);  // tests: flush() alone
+  }
   return ok && resp.status >= 200 && resp.status < 300;
 }
 
@@ -337,14 +349,17 @@ void Tracer::post_pending() {
   }
   constexpr size_t kChunk = 500;
   for (size_t i = 0; i < pending_.size(); i += kChunk) {
-    std::vector<SpanRecord> part(pending_.begin() + long(i),
-                                 pending_.begin() + long(std::min(pending_.size(), i + kChunk)));
+    const size_t end = std::min(pending_.size(), i + kChunk);
+    std::vector<SpanRecord> part(pending_.begin() + long(i), pending_.begin() + long(end));
     std::string body = o_.v2 ? encode_v2(part) : encode_v1(part);
     if (post(body)) {
       reported_.fetch_add(part.size());
     } else {
+      // One failed POST drops the rest of the batch too: a collector that is down or times
+      // out costs one connect timeout per flush, not one per 500 spans.
       post_failures_.fetch_add(1);
-      dropped_no_collector_.fetch_add(part.size());
+      dropped_no_collector_.fetch_add(pending_.size() - i);
+      break;
     }
   }
   pending_.clear();
@@ -380,6 +395,7 @@ void Tracer::run() {
 
 void Tracer::start() {
   if (!o_.enabled || running_) return;
+  if (caddr_) caddr_->start(0);
   running_ = true;
   th_ = std::thread([this] { run(); });
   pthread_setname_np(th_.native_handle(), "hola-tracer");  // bench.py reads its CPU time
@@ -396,6 +412,7 @@ void Tracer::stop() {
   if (cfd_ >= 0) ::close(cfd_);
   cfd_ = -1;
   running_ = false;
+  if (caddr_) caddr_->stop();
 }
 
 TracerStats Tracer::stats() const {

@@ -27,6 +27,9 @@
 namespace hola::http {
 struct Request;
 }
+namespace hola::client {
+class AddressCache;
+}
 
 namespace hola::tracing {
 
@@ -148,7 +151,10 @@ class Tracer {
   std::vector<SpanRecord> pending_;    // drained, not yet posted (reporter thread / flush)
   void drain_rings();
   void post_pending();
-  // collector connection (reporter thread only)
+  // collector connection (reporter thread only); the collector's name is resolved on the
+  // cache's own thread while the reporter runs, so a DNS server that does not answer never
+  // holds up a flush or shutdown
+  std::unique_ptr<client::AddressCache> caddr_;
   int cfd_ = -1;
   std::string chost_, cpath_;
   int cport_ = 0;

@@ -1,5 +1,6 @@
-"""aloha's name is resolved off the request path (client/http_client.cc AddressCache): a DNS
-server that never answers must neither delay start-up by its timeouts nor hold up SIGTERM.
+"""aloha's and the Zipkin collector's names are resolved off the request path and off the
+span reporter (client/http_client.cc AddressCache): a DNS server that never answers must
+neither delay start-up by its timeouts, nor stall span export, nor hold up SIGTERM.
 
 The reference resolves inside each Hystrix thread (HttpClient -> InetAddress), so a hung DNS
 costs it one 600 ms timeout per chaining call and nothing else; these tests pin the same.
@@ -42,7 +43,8 @@ if not os.access(hola, os.X_OK):
 t0 = time.monotonic()
 p = subprocess.Popen([hola, "--host", "127.0.0.1", "--port", "0", "--port-file", pf, "--threads", "1",
                       "--log-level", "warn", "--aloha-url", "http://aloha-unanswered:8080/"],
-                     env={**os.environ, "HOSTNAME": "h"}, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
+                     env={**os.environ, "HOSTNAME": "h", "ZIPKIN_SERVER_URL": "http://zipkin-unanswered:9411"},
+                     stdout=subprocess.DEVNULL, stderr=subprocess.PIPE)
 while not (os.path.exists(pf) and open(pf).read().strip()):
     if p.poll() is not None or time.monotonic() - t0 > 20:
         p.kill()
@@ -61,6 +63,10 @@ def get(path):
 
 out["hola"] = get("/api/hola")[:2]
 out["chaining"] = get("/api/hola-chaining")
+time.sleep(1.2)  # a span flush falls due: the reporter must not be stuck resolving the collector
+metrics = get("/metrics")[1]
+out["dropped"] = sum(float(l.split()[-1]) for l in metrics.splitlines()
+                     if l.startswith("hola_spans_dropped_total") and 'reason="collector"' in l)
 t = time.monotonic()
 p.send_signal(signal.SIGTERM)
 out["rc"] = p.wait(timeout=30)
@@ -96,7 +102,9 @@ def test_unanswered_dns_neither_delays_startup_nor_shutdown(hola_bin, tmp_path):
     status, body, secs = res["chaining"]
     assert status == 200 and json.loads(body) == ["Hola de h", "Aloha response (fallback)"]
     assert 0.5 <= secs < 2.0, res  # the Hystrix timeout, not a DNS timeout
-    # SIGTERM does not wait for the stuck getaddrinfo()
+    # the spans recorded so far went to the unresolvable collector and were counted as dropped
+    assert res["dropped"] >= 2, res
+    # SIGTERM waits for neither stuck getaddrinfo() (aloha's, the collector's)
     assert res["rc"] == 0 and res["stop_s"] < 3.0, res
     # leaving the resolver thread behind is clean under the sanitizer builds too
     assert "Sanitizer" not in res["stderr"] and "runtime error" not in res["stderr"], res["stderr"]
