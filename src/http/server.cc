@@ -281,7 +281,13 @@ void Connection::flush() {
   }
 }
 
-void Connection::on_writable() { flush(); }
+void Connection::on_writable() {
+  // The slow path (the socket was full): progress here counts as activity for the idle sweep,
+  // so only a peer that has stopped reading its responses is timed out.
+  const uint64_t before = sent_total_;
+  flush();
+  if (sent_total_ != before) last_active_ms_ = worker_->loop().now_ms();
+}
 
 void Connection::update_interest() {
   if (closed_) return;
@@ -371,8 +377,11 @@ void Worker::sweep_idle() {
   for (Connection* c = conns_; c;) {
     Connection* next = c->next_;
     // Includes connections holding a partial request (slow-loris): nothing arrived for the
-    // whole timeout, so the request will not complete.
-    if (!c->streaming() && c->quiet() && now - c->last_active_ms() > limit) c->close();
+    // whole timeout, so the request will not complete; and connections whose peer stopped
+    // reading its responses: nothing was read or written for the whole timeout (the output
+    // backlog stays bounded by kMaxBufferedOutput meanwhile). A parked request has its own
+    // deadline (the Hystrix timeout), and SSE streams have theirs.
+    if (!c->streaming() && !c->parked_ && now - c->last_active_ms() > limit) c->close();
     c = next;
   }
 }

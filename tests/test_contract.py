@@ -297,6 +297,57 @@ def test_slowloris_partial_request_times_out(hola):
         assert c.recv(4096) == b""
 
 
+def test_peer_that_stops_reading_responses_times_out(hola):
+    """A client that pipelines requests but never reads the answers fills the socket, then the
+    server's bounded backlog (reading stops at 1 MiB unsent); with nothing read or written for
+    --idle-timeout-ms the connection is closed, freeing its buffers, while a slow reader that
+    makes progress is kept."""
+    s = hola(args=["--idle-timeout-ms", "300"], threads=1)
+    req = b"GET /api/hola HTTP/1.1\r\nHost: x\r\n\r\n"
+    stalled = socket.socket()
+    stalled.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 4096)
+    stalled.connect(("127.0.0.1", s.port))
+    stalled.setblocking(False)
+    sent = 0
+    t0 = time.monotonic()
+    while time.monotonic() - t0 < 3:  # until the server stops reading (our sends block)
+        try:
+            sent += stalled.send(req * 256)
+        except BlockingIOError:
+            time.sleep(0.05)
+            try:
+                sent += stalled.send(req * 256)
+            except BlockingIOError:
+                break
+    assert sent > len(req) * 10000
+    # a slow reader: one small read every 100 ms keeps its connection alive past the timeout
+    slow = socket.create_connection(("127.0.0.1", s.port), timeout=3)
+    slow.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 4096)
+    slow.sendall(req * 20000)
+    got = 0
+    for _ in range(10):
+        time.sleep(0.1)
+        got += len(slow.recv(65536))
+    assert got > 0
+    # the stalled connection is gone: its unread responses end in EOF or a reset
+    stalled.setblocking(True)
+    stalled.settimeout(3)
+    end = None
+    try:
+        while True:
+            chunk = stalled.recv(1 << 20)
+            if not chunk:
+                end = "eof"
+                break
+    except ConnectionResetError:
+        end = "reset"
+    assert end in ("eof", "reset")
+    slow.settimeout(0.5)
+    assert slow.recv(65536)  # still served
+    stalled.close()
+    slow.close()
+
+
 def test_profile_stage_histograms(hola, tmp_path):
     """`--profile`: per-stage latency histograms dumped at exit."""
     import signal
