@@ -6,7 +6,7 @@
 //   aloha chainer + Hystrix     (HolaResource.getNextService, config.properties:17,19)
 //   /hystrix.stream             (HystrixServlet.java)
 //   HTTP server on :8080        (Dockerfile:8, pom.xml:74)
-// SIGTERM/SIGINT: stop accepting, drain in-flight requests, flush spans, exit 0.
+// SIGTERM/SIGINT/SIGHUP: stop accepting, drain in-flight requests, flush spans, exit 0.
 #include <signal.h>
 #include <unistd.h>
 
@@ -70,7 +70,8 @@ void usage() {
           "  --port-file PATH         write the bound port here once listening\n"
           "  --busy-poll-us N         spin up to N us in epoll before sleeping (default 0)\n"
           "  --busy-poll-pause N      PAUSE instructions between empty polls (SMT-friendly spin)\n"
-          "  --idle-timeout-ms N      close keep-alive connections idle this long (default 60000, 0 = never)\n"
+          "  --idle-timeout-ms N      close connections with nothing read or written this long\n"
+          "                           (default 60000, 0 = never)\n"
           "  --max-connections N      refuse connections beyond N per replica (default unlimited)\n"
           "  --no-steer               plain round-robin accept (default: L3-domain steering when pinned)\n"
           "  --epoll-lt               level-triggered connection sockets (default: edge-triggered)\n"
@@ -260,6 +261,10 @@ int main(int argc, char** argv) {
   sigemptyset(&sigs);
   sigaddset(&sigs, SIGTERM);
   sigaddset(&sigs, SIGINT);
+  // The JVM runs its shutdown hooks on SIGHUP too, unless the signal was ignored at start-up
+  // (nohup); the same here.
+  struct sigaction hup {};
+  if (sigaction(SIGHUP, nullptr, &hup) == 0 && hup.sa_handler != SIG_IGN) sigaddset(&sigs, SIGHUP);
   pthread_sigmask(SIG_BLOCK, &sigs, nullptr);
   signal(SIGPIPE, SIG_IGN);
 
@@ -339,7 +344,8 @@ int main(int argc, char** argv) {
 
   int sig = 0;
   sigwait(&sigs, &sig);
-  LOG_INFO("received %s: draining (up to %d ms)", sig == SIGTERM ? "SIGTERM" : "SIGINT", drain_ms);
+  LOG_INFO("received %s: draining (up to %d ms)",
+           sig == SIGTERM ? "SIGTERM" : sig == SIGINT ? "SIGINT" : "SIGHUP", drain_ms);
   server.shutdown(drain_ms);
   server.join();
   if (so.profile) {

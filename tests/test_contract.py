@@ -348,6 +348,18 @@ def test_peer_that_stops_reading_responses_times_out(hola):
     slow.close()
 
 
+@pytest.mark.parametrize("sig", ["SIGTERM", "SIGINT", "SIGHUP"])
+def test_termination_signals_drain_and_exit_zero(hola, sig):
+    """The JVM runs its shutdown hooks on SIGTERM, SIGINT and SIGHUP alike: each one drains
+    and exits 0 here."""
+    import signal
+
+    s = hola()
+    assert s.get("/api/hola")[0] == 200
+    assert s.stop(getattr(signal, sig), timeout=10) == 0
+    assert f"received {sig}: draining" in s.log()
+
+
 def test_profile_stage_histograms(hola, tmp_path):
     """`--profile`: per-stage latency histograms dumped at exit."""
     import signal
