@@ -32,12 +32,16 @@ class ReplicaSet:
 
     HOSTNAME is set to ``replica-<i>`` so responses identify the replica (the k8s pod name
     plays that role in the reference). With ``supervise=True`` a background thread restarts
-    any replica that exits (the platform's restart policy).
+    any replica that exits (the platform's restart policy), with kubelet's CrashLoopBackOff
+    shape: a replica that dies (or fails to come up) within ``stable_s`` of its start waits
+    0.1 s, then twice as long after each further quick death, up to ``max_backoff_s``; one
+    that ran for longer is restarted at once and its delay is reset.
     """
 
     def __init__(self, n: int, cpu_plan: list[list[int]] | None = None, threads_per_replica: int = 1,
                  args: list[str] | None = None, env: dict | None = None, supervise: bool = True,
-                 base_port: int = 0, log_level: str = "warn", shared_port: int | None = None):
+                 base_port: int = 0, log_level: str = "warn", shared_port: int | None = None,
+                 stable_s: float = 10.0, max_backoff_s: float = 10.0):
         self.n = n
         self.cpu_plan = cpu_plan
         self.threads = threads_per_replica
@@ -54,6 +58,12 @@ class ReplicaSet:
             self.ports = [base_port + i if base_port else free_port() for i in range(n)]
         self.procs: list[HolaProcess | None] = [None] * n
         self.restarts = [0] * n
+        self.failed_restarts = [0] * n  # respawns that did not come up (counted towards back-off)
+        self.stable_s = stable_s
+        self.max_backoff_s = max_backoff_s
+        self._started = [0.0] * n
+        self._backoff = [0.0] * n
+        self._next = [0.0] * n  # when a dead replica may be respawned (0 = death not seen yet)
         self._stop = threading.Event()
         self._lock = threading.Lock()
         self._sup: threading.Thread | None = None
@@ -68,6 +78,7 @@ class ReplicaSet:
     def start(self, timeout: float = 30.0) -> "ReplicaSet":
         for i in range(self.n):
             self.procs[i] = self._spawn(i)
+            self._started[i] = time.monotonic()
         for i in range(self.n):
             if not wait_http("127.0.0.1", self.ports[i], timeout=timeout):
                 raise RuntimeError(f"replica {i} not ready")
@@ -76,19 +87,36 @@ class ReplicaSet:
             self._sup.start()
         return self
 
+    def _next_backoff(self, i: int, ran_s: float) -> float:
+        if ran_s >= self.stable_s:
+            return 0.0
+        return min(self.max_backoff_s, max(0.1, self._backoff[i] * 2))
+
     def _supervise(self) -> None:
-        while not self._stop.wait(0.1):
+        while not self._stop.wait(0.05):
             for i, p in enumerate(self.procs):
                 if p is None or p.proc is None or p.proc.poll() is None:
+                    continue
+                now = time.monotonic()
+                if self._next[i] == 0.0:  # the death is new: schedule the restart
+                    self._backoff[i] = self._next_backoff(i, now - self._started[i])
+                    self._next[i] = now + self._backoff[i]
+                if now < self._next[i]:
                     continue
                 with self._lock:
                     if self._stop.is_set():
                         return
+                    self._started[i] = time.monotonic()
                     try:
                         self.procs[i] = self._spawn(i)
-                        self.restarts[i] += 1
                     except Exception:
-                        time.sleep(0.2)
+                        # did not come up: a quick death, so the next try waits longer
+                        self.failed_restarts[i] += 1
+                        self._backoff[i] = self._next_backoff(i, 0.0)
+                        self._next[i] = time.monotonic() + self._backoff[i]
+                        continue
+                    self.restarts[i] += 1
+                    self._next[i] = 0.0
 
     def kill(self, i: int, sig: int = signal.SIGKILL) -> None:
         p = self.procs[i]

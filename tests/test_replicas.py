@@ -116,6 +116,35 @@ def test_supervisor_restarts_crashed_replica():
         assert greeting_via(rs.ports[0]) == "Hola de replica-0"
 
 
+def test_supervisor_backs_off_a_crash_looping_replica():
+    """A replica that cannot come back (its port is taken) is retried with growing delays,
+    0.1 s doubling up to the cap, like kubelet's CrashLoopBackOff, not every poll; once the
+    port is free again it is back within one capped delay."""
+    import socket
+
+    with ReplicaSet(1, threads_per_replica=1, supervise=True, max_backoff_s=1.0) as rs:
+        port = rs.ports[0]
+        rs.kill(0)
+        blocker = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+        blocker.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+        blocker.bind(("0.0.0.0", port))
+        blocker.listen(1)
+        try:
+            time.sleep(2.5)
+            fails = rs.failed_restarts[0]
+            # delays 0.1, 0.2, 0.4, 0.8, 1.0 s: about 4 tries in 2.5 s (polling every 50 ms
+            # without back-off would make dozens)
+            assert 2 <= fails <= 6, fails
+            assert rs.restarts[0] == 0
+        finally:
+            blocker.close()
+        deadline = time.time() + 5
+        while time.time() < deadline and rs.restarts[0] == 0:
+            time.sleep(0.05)
+        assert rs.restarts[0] == 1
+        assert greeting_via(port) == "Hola de replica-0"
+
+
 def test_kill_replica_under_load_client_rr():
     """Chaos: SIGKILL one replica mid-run; the other keeps answering, the loadgen reconnects."""
     from hola_amd.parallel.loadgen import ControlledLoadgen
