@@ -29,15 +29,26 @@ from pathlib import Path
 from hola_amd import native
 
 
+_STOP_SIGNALS = (signal.SIGTERM, signal.SIGINT, signal.SIGHUP)
+
+
 def _serve(argv: list[str]) -> int:
     exe = native.binary("hola")
-    # Runs as a child (never exec from a process that might have touched a GPU).
+    # Runs as a child (never exec from a process that might have touched a GPU). Termination
+    # signals sent to this wrapper (systemd, a container runtime, Ctrl-C) go to the server, which
+    # drains and exits; the wrapper then exits with its status.
     p = subprocess.Popen([str(exe), *argv])
-    try:
-        return p.wait()
-    except KeyboardInterrupt:
-        p.send_signal(signal.SIGINT)
-        return p.wait()
+    for s in _STOP_SIGNALS:
+        signal.signal(s, lambda sig, _frame: p.send_signal(sig))
+    return p.wait()
+
+
+class _Stop(Exception):
+    pass
+
+
+def _raise_stop(sig, _frame):
+    raise _Stop(sig)
 
 
 def _cluster(argv: list[str]) -> int:
@@ -60,11 +71,17 @@ def _cluster(argv: list[str]) -> int:
     a = ap.parse_args(argv)
 
     def wait():
+        # SIGTERM/SIGHUP/SIGINT unwind the `with` blocks below, which stop the proxy and every
+        # replica (each drains); otherwise they would outlive this process.
         try:
             while True:
                 time.sleep(1)
-        except KeyboardInterrupt:
-            pass
+        except (KeyboardInterrupt, _Stop):
+            for s in _STOP_SIGNALS:  # a second signal must not interrupt the teardown
+                signal.signal(s, signal.SIG_IGN)
+
+    for s in _STOP_SIGNALS:
+        signal.signal(s, _raise_stop)
 
     if a.lb == "reuseport":
         plan = plan_node(a.replicas, a.cores_per_replica or None)

@@ -138,7 +138,11 @@ class ReplicaSet:
                     p.stop()
 
     def __enter__(self) -> "ReplicaSet":
-        return self.start()
+        try:
+            return self.start()
+        except BaseException:  # a failed or interrupted start leaves no replica behind
+            self.stop()
+            raise
 
     def __exit__(self, *exc) -> None:
         self.stop()
@@ -192,13 +196,19 @@ class RRProxy:
                 self.proc.wait(timeout=10)
             except subprocess.TimeoutExpired:
                 self.proc.kill()
+                self.proc.wait()
         try:
             self._log.close()
         except Exception:
             pass
 
     def __enter__(self) -> "RRProxy":
-        return self.start()
+        try:
+            return self.start()
+        except BaseException:
+            self.stop()
+            self._tmp.cleanup()
+            raise
 
     def __exit__(self, *exc) -> None:
         self.stop()
