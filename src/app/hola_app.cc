@@ -286,6 +286,28 @@ int route_of(std::string_view p) {
   return HolaApp::kNotFound;
 }
 
+// The path as Undertow and RESTEasy match it: path parameters dropped (before decoding, so
+// %3B is not a delimiter), escapes decoded except %2F, dot segments removed. Each step's
+// output is no longer than its input. Only paths containing ';', '%' or "/." get here.
+std::string_view canonical_path(std::string_view path, std::string* storage) {
+  std::string a(path.size(), '\0'), b;
+  size_t n = 0;
+  http::strip_path_parameters(path, a.data(), &n);
+  a.resize(n);
+  b.resize(a.size());
+  if (http::percent_decode(a, b.data(), &n, /*keep_encoded_slash=*/true)) {
+    b.resize(n);
+    a.swap(b);
+  }
+  b.resize(a.size());
+  if (http::remove_dot_segments(a, b.data(), &n)) {
+    b.resize(n);
+    a.swap(b);
+  }
+  *storage = std::move(a);
+  return *storage;
+}
+
 }  // namespace
 
 void HolaApp::on_request(http::Connection& c, const http::Request& r) {
@@ -297,24 +319,10 @@ void HolaApp::on_request(http::Connection& c, const http::Request& r) {
   if (!ka) c.close_after_response();
 
   std::string_view path = r.path;
-  char unparam[512];
-  if (__builtin_expect(path.find(';') != std::string_view::npos, 0) && path.size() <= sizeof unparam) {
-    size_t n = 0;
-    http::strip_path_parameters(path, unparam, &n);  // before decoding: %3B is not a delimiter
-    path = std::string_view(unparam, n);
-  }
-  char decoded[512];
-  if (path.find('%') != std::string_view::npos) {
-    size_t n = 0;
-    if (path.size() <= sizeof decoded && http::percent_decode(path, decoded, &n, /*keep_encoded_slash=*/true))
-      path = std::string_view(decoded, n);
-  }
-  char canonical[512];
-  if (__builtin_expect(path.find("/.") != std::string_view::npos, 0)) {
-    size_t n = 0;
-    if (path.size() <= sizeof canonical && http::remove_dot_segments(path, canonical, &n))
-      path = std::string_view(canonical, n);
-  }
+  std::string canonical;  // stays empty (no allocation) for plain paths
+  if (__builtin_expect(path.find_first_of(";%") != std::string_view::npos ||
+                       path.find("/.") != std::string_view::npos, 0))
+    path = canonical_path(path, &canonical);
   const int route = route_of(path);
   const Method m = method_of(r.method);
   const int head = m == Method::kHead ? 1 : 0;

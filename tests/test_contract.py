@@ -510,3 +510,13 @@ def test_path_parameters_are_ignored_for_matching(hola, native):
     assert s.get("/api;v=1/hola")[2] == b"Hola de h"
     assert s.get("/api/health;x")[2] == b"I'm ok"
     assert s.get("/api/hola%3Bx")[0] == 404
+
+
+def test_long_paths_are_canonicalised_too(hola):
+    """Path parameters, escapes and dot segments are handled for paths of any length the
+    request line allows, not only short ones."""
+    s = hola(env={"HOSTNAME": "h"})
+    assert s.get("/api/hola;jsessionid=" + "x" * 1500)[2] == b"Hola de h"
+    assert s.get("/api/" + "a/../" * 300 + "hola")[2] == b"Hola de h"
+    assert s.get("/api/" + "%7A/../" * 200 + "hola")[2] == b"Hola de h"
+    assert s.get("/api/" + "%7A" * 600)[0] == 404
