@@ -86,6 +86,7 @@ struct AlohaChainer::Call {
   bool live = false;
   uint64_t req_id = 0;     // client request of the execution in flight (0 = none)
   bool inflight = false;   // an HTTP execution is outstanding (not sleeping between retries)
+  bool queued = false;     // waiting in the Hystrix pool queue for a bulkhead slot
   int attempts = 0;        // HTTP executions started (Feign retries included)
   int64_t start_ms = 0;    // command start (Hystrix latency, timeout)
   int64_t attempt_ms = 0;  // start of the current execution (Feign's "(Nms)")
@@ -111,11 +112,15 @@ struct AlohaChainer::WorkerCalls {
   std::deque<Pending> fifo;
   EventLoop::TimerId timer = 0;
   int64_t timer_at = 0;  // deadline the armed timer fires for (0 = none armed)
+  http::Worker* worker = nullptr;
 };
 
 AlohaChainer::WorkerCalls& AlohaChainer::calls(http::Worker& w) {
   auto& c = calls_[size_t(w.index())];
-  if (!c) c = std::make_unique<WorkerCalls>();
+  if (!c) {
+    c = std::make_unique<WorkerCalls>();
+    c->worker = &w;
+  }
   return *c;
 }
 
@@ -132,6 +137,7 @@ uint32_t AlohaChainer::acquire(WorkerCalls& wc) {
   c.live = true;
   c.req_id = 0;
   c.inflight = false;
+  c.queued = false;
   c.attempts = 0;
   c.traced = false;
   c.has_parent = false;
@@ -186,30 +192,37 @@ void AlohaChainer::call(http::Worker& w, const tracing::SpanContext* parent,
                         std::function<void(const ChainResult&)> done) {
   const int64_t start_ms = clock_.now_ms();
   Command* cmd = cmd_.get();
-  Command::Admit a = url_ok_ ? cmd->try_start() : Command::Admit::kRun;
-  if (a != Command::Admit::kRun) {
-    cmd->rejected(clock_.now_ms() - start_ms);
-    done(static_fallback(a));
-    return;
-  }
   if (!url_ok_) {
     done(fallback_result("bad-url"));
     return;
   }
   WorkerCalls& wc = calls(w);
   const uint32_t slot = acquire(wc);
+  const uint32_t gen = wc.slots[slot]->gen;
+  const Command::Queued ref = queued_ref(w, slot, gen);
+  const Command::Admit a = cmd->try_start(&ref);
+  if (a == Command::Admit::kShortCircuited || a == Command::Admit::kRejected) {
+    release(wc, slot);
+    cmd->rejected(clock_.now_ms() - start_ms);
+    done(static_fallback(a));
+    return;
+  }
   Call& c = *wc.slots[slot];
-  const uint32_t gen = c.gen;
   c.cb = std::move(done);
   c.start_ms = start_ms;
   if (tracer_ && tracer_->enabled() && parent && parent->sampled) {
     c.parent = *parent;
     c.has_parent = true;
   }
-  execute(w, wc, slot, gen);
-  if (dead(wc, slot, gen)) return;  // answered (or failed) synchronously
+  if (a == Command::Admit::kQueued) {
+    c.queued = true;  // started by pump() when a slot frees up, or timed out by expire()
+  } else {
+    execute(w, wc, slot, gen);
+    if (dead(wc, slot, gen)) return;  // answered (or failed) synchronously
+  }
 
-  // One Hystrix execution timeout covers every Feign attempt and the sleeps between them.
+  // One Hystrix execution timeout covers the queue wait, every Feign attempt and the sleeps
+  // between them.
   const int timeout_ms = timeout_ms_.load(std::memory_order_relaxed);
   if (timeout_ms <= 0) return;
   const WorkerCalls::Pending e{mono_ms() + timeout_ms, slot, gen};
@@ -222,6 +235,27 @@ void AlohaChainer::call(http::Worker& w, const tracing::SpanContext* parent,
     wc.fifo.insert(it, e);
   }
   arm(w.loop(), wc, pool(w), w.index());
+}
+
+void AlohaChainer::pump() {
+  Command::Queued q;
+  while (cmd_->next_queued(&q)) {
+    auto* w = reinterpret_cast<http::Worker*>(uintptr_t(q.a));
+    const uint32_t slot = uint32_t(q.b >> 32), gen = uint32_t(q.b);
+    w->loop().post([this, w, slot, gen] { start_queued(*w, slot, gen); });
+  }
+}
+
+void AlohaChainer::start_queued(http::Worker& w, uint32_t slot, uint32_t gen) {
+  WorkerCalls& wc = calls(w);
+  if (dead(wc, slot, gen) || !wc.slots[slot]->queued) {
+    // timed out between leaving the queue and getting here: the slot goes to the next call
+    cmd_->release_slot();
+    pump();
+    return;
+  }
+  wc.slots[slot]->queued = false;
+  execute(w, wc, slot, gen);
 }
 
 // One HTTP execution of the Feign method (SynchronousMethodHandler.executeAndDecode).
@@ -318,6 +352,7 @@ void AlohaChainer::on_response(http::Worker& w, WorkerCalls& wc, uint32_t slot, 
     res.reason = err;
   }
   finish(wc, slot, res);
+  pump();
 }
 
 void AlohaChainer::finish(WorkerCalls& wc, uint32_t slot, const ChainResult& res) {
@@ -353,6 +388,15 @@ void AlohaChainer::expire(EventLoop& loop, WorkerCalls& wc, client::ClientPool& 
     if (e.deadline_ms > now) break;
     wc.fifo.pop_front();
     Call& c = *wc.slots[e.slot];
+    if (c.queued) {
+      // Timed out waiting for a bulkhead slot: it never executed. If pump() has already
+      // popped it, start_queued() finds it dead and hands the slot on.
+      const int64_t elapsed = clock_.now_ms() - c.start_ms;
+      cmd_->cancel_queued(queued_ref(*wc.worker, e.slot, e.gen));
+      cmd_->queued_timeout(elapsed);
+      finish(wc, e.slot, fallback_result("timeout"));
+      continue;
+    }
     if (c.inflight) {
       p.cancel(c.req_id);  // abandon the socket
       if (c.traced && tracer_)
@@ -364,6 +408,7 @@ void AlohaChainer::expire(EventLoop& loop, WorkerCalls& wc, client::ClientPool& 
               c.attempts);
     cmd_->complete(Event::kTimeout, elapsed, true, elapsed);
     finish(wc, e.slot, fallback_result("timeout"));
+    pump();
   }
   arm(loop, wc, p, worker_index);
 }

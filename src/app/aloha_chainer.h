@@ -84,6 +84,13 @@ class AlohaChainer final : public Chainer {
   void execute(http::Worker& w, WorkerCalls& wc, uint32_t slot, uint32_t gen);
   void on_response(http::Worker& w, WorkerCalls& wc, uint32_t slot, uint32_t gen, client::ClientResult&& r);
   void finish(WorkerCalls& wc, uint32_t slot, const ChainResult& res);
+  // Pool queue (hystrix.threadpool.*.maxQueueSize > 0): after a bulkhead slot is released,
+  // start the calls that were waiting for one, each on its own worker's loop.
+  void pump();
+  void start_queued(http::Worker& w, uint32_t slot, uint32_t gen);
+  static resilience::Command::Queued queued_ref(http::Worker& w, uint32_t slot, uint32_t gen) {
+    return {uint64_t(reinterpret_cast<uintptr_t>(&w)), (uint64_t(slot) << 32) | gen};
+  }
   void expire(EventLoop& loop, WorkerCalls& wc, client::ClientPool& p, int worker_index);
   void arm(EventLoop& loop, WorkerCalls& wc, client::ClientPool& p, int worker_index);
   AlohaOptions o_;

@@ -116,8 +116,8 @@ std::string HystrixStream::threadpool_json(const CommandSnapshot& s) {
   kv(&o, "currentLargestPoolSize", s.pool_largest);
   kv(&o, "currentMaximumPoolSize", int64_t(s.settings.pool_core_size));
   kv(&o, "currentPoolSize", s.pool_largest);
-  kv(&o, "currentQueueSize", int64_t(0));
-  kv(&o, "currentTaskCount", s.pool_completed + s.pool_active);
+  kv(&o, "currentQueueSize", s.pool_queue_size);
+  kv(&o, "currentTaskCount", s.pool_completed + s.pool_active + s.pool_queue_size);
   kv(&o, "rollingCountThreadsExecuted", s.pool_rolling_executed);
   kv(&o, "rollingMaxActiveThreads", s.pool_rolling_max_active);
   kv(&o, "rollingCountCommandRejections", s.pool_rolling_rejected);

@@ -92,6 +92,11 @@ std::string Prometheus::render(http::Server* server) const {
     }
     o += "# TYPE hola_hystrix_circuit_open gauge\nhola_hystrix_circuit_open{command=\"" + s.name + "\"} " +
          (s.circuit_open ? "1" : "0") + "\n";
+    // the bulkhead: calls holding a pool slot, and calls waiting in the pool queue
+    o += "# TYPE hola_hystrix_pool_active gauge\nhola_hystrix_pool_active{command=\"" + s.name + "\"} " +
+         std::to_string(s.pool_active) + "\n";
+    o += "# TYPE hola_hystrix_pool_queued gauge\nhola_hystrix_pool_queued{command=\"" + s.name + "\"} " +
+         std::to_string(s.pool_queue_size) + "\n";
   }
   if (reloads_) o += "# TYPE hola_config_reloads_total counter\nhola_config_reloads_total " + std::to_string(reloads_()) + "\n";
   if (feign_retries_ && transport_retries_) {

@@ -148,13 +148,26 @@ struct PyCommand {
     resilience::Settings s = resilience::settings_from(props, "AlohaService#aloha()", "aloha");
     cmd = std::make_unique<resilience::Command>("AlohaService#aloha()", "aloha", "aloha", s, clock);
   }
-  std::string try_start() {
-    switch (cmd->try_start()) {
+  // `ticket` >= 0 offers the call to the pool queue under that id (maxQueueSize > 0).
+  std::string try_start(int64_t ticket) {
+    resilience::Command::Queued q{uint64_t(ticket), 0};
+    switch (cmd->try_start(ticket >= 0 ? &q : nullptr)) {
       case resilience::Command::Admit::kRun: return "run";
+      case resilience::Command::Admit::kQueued: return "queued";
       case resilience::Command::Admit::kShortCircuited: return "short_circuited";
       default: return "rejected";
     }
   }
+  // The ticket of the queued call that takes a released slot, or None.
+  py::object next_queued() {
+    resilience::Command::Queued q;
+    if (!cmd->next_queued(&q)) return py::none();
+    return py::int_(int64_t(q.a));
+  }
+  bool cancel_queued(int64_t ticket) { return cmd->cancel_queued({uint64_t(ticket), 0}); }
+  void release_slot() { cmd->release_slot(); }
+  void queued_timeout(int64_t ms) { cmd->queued_timeout(ms); }
+  int64_t queue_size() { return cmd->queue_size(); }
   void finish(const std::string& outcome, int64_t ms) {
     resilience::Event e = outcome == "success" ? resilience::Event::kSuccess
                           : outcome == "timeout" ? resilience::Event::kTimeout
@@ -371,7 +384,12 @@ PYBIND11_MODULE(_native, m) {
         py::arg("fail_every") = 0, py::arg("volume") = 20);
   py::class_<PyCommand>(m, "HystrixCommand")
       .def(py::init<const std::map<std::string, std::string>&>(), py::arg("props") = std::map<std::string, std::string>{})
-      .def("try_start", &PyCommand::try_start)
+      .def("try_start", &PyCommand::try_start, py::arg("ticket") = -1)
+      .def("next_queued", &PyCommand::next_queued)
+      .def("cancel_queued", &PyCommand::cancel_queued)
+      .def("release_slot", &PyCommand::release_slot)
+      .def("queued_timeout", &PyCommand::queued_timeout)
+      .def("queue_size", &PyCommand::queue_size)
       .def("finish", &PyCommand::finish)
       .def("advance", &PyCommand::advance)
       .def("is_open", &PyCommand::is_open)

@@ -238,6 +238,7 @@ struct alignas(64) Command::Shard {
 
 Command::Command(std::string name, std::string group, std::string pool, Settings s, const Clock& clock)
     : name_(std::move(name)), group_(std::move(group)), pool_(std::move(pool)), clock_(clock), s_(s) {
+  max_queue_.store(s.pool_max_queue, std::memory_order_relaxed);
   apply_hot(s);
   for (int i = 0; i < kShards; ++i) shards_.push_back(std::make_unique<Shard>(s));
 }
@@ -252,6 +253,7 @@ void Command::apply_hot(const Settings& s) {
   error_pct_.store(s.error_threshold_pct, std::memory_order_relaxed);
   sleep_window_ms_.store(s.sleep_window_ms, std::memory_order_relaxed);
   pool_core_.store(s.pool_core_size, std::memory_order_relaxed);
+  queue_threshold_.store(s.pool_queue_reject_threshold, std::memory_order_relaxed);
   health_ms_.store(s.health_snapshot_ms, std::memory_order_relaxed);
 }
 
@@ -320,7 +322,26 @@ bool Command::allow_request(int64_t now) {
   return false;
 }
 
-Command::Admit Command::try_start() {
+bool Command::try_acquire_slot() {
+  int64_t a = active_.load(std::memory_order_relaxed);
+  const int64_t core = pool_core_.load(std::memory_order_relaxed);
+  while (a < core)
+    if (active_.compare_exchange_weak(a, a + 1, std::memory_order_acq_rel)) return true;
+  return false;
+}
+
+void Command::slot_started(int64_t now, int64_t active) {
+  int64_t largest = largest_.load(std::memory_order_relaxed);
+  while (active > largest && !largest_.compare_exchange_weak(largest, active, std::memory_order_relaxed)) {
+  }
+  Shard& sh = shard();
+  std::lock_guard<std::mutex> g(sh.mu);
+  sh.counter.update_max_concurrency(now, active);
+  sh.pool_counter.update_max_concurrency(now, active);
+  sh.pool_counter.add(now, Event::kSuccess);  // "threads executed"
+}
+
+Command::Admit Command::try_start(const Queued* q) {
   int64_t now = clock_.now_ms();
   if (!executed_.load(std::memory_order_relaxed)) executed_.store(true, std::memory_order_relaxed);
   if (!allow_request(now)) {
@@ -330,23 +351,76 @@ Command::Admit Command::try_start() {
     return Admit::kShortCircuited;
   }
   int64_t active = active_.fetch_add(1, std::memory_order_acq_rel) + 1;
-  if (active > pool_core_.load(std::memory_order_relaxed)) {  // SynchronousQueue: no waiting room
-    active_.fetch_sub(1, std::memory_order_acq_rel);
-    Shard& sh = shard();
-    std::lock_guard<std::mutex> g(sh.mu);
-    sh.counter.add(now, Event::kThreadPoolRejected);
-    sh.pool_counter.add(now, Event::kThreadPoolRejected);
-    return Admit::kRejected;
+  if (active <= pool_core_.load(std::memory_order_relaxed)) {
+    slot_started(now, active);
+    return Admit::kRun;
   }
-  int64_t largest = largest_.load(std::memory_order_relaxed);
-  while (active > largest && !largest_.compare_exchange_weak(largest, active, std::memory_order_relaxed)) {
+  active_.fetch_sub(1, std::memory_order_acq_rel);
+  const int max_queue = max_queue_.load(std::memory_order_relaxed);
+  if (q && max_queue > 0) {
+    // HystrixThreadPool.isQueueSpaceAvailable() (queue size < queueSizeRejectionThreshold),
+    // then the LinkedBlockingQueue(maxQueueSize) offer. Under the queue lock, retry the slot
+    // first: one released since the check above would otherwise find an empty queue and
+    // leave this call waiting beside a free slot.
+    std::lock_guard<std::mutex> g(queue_mu_);
+    if (try_acquire_slot()) {
+      slot_started(now, active_.load(std::memory_order_relaxed));
+      return Admit::kRun;
+    }
+    const size_t cap = size_t(std::max(0, std::min(max_queue, queue_threshold_.load(std::memory_order_relaxed))));
+    if (queue_.size() < cap) {
+      queue_.push_back(*q);
+      return Admit::kQueued;
+    }
   }
+  // SynchronousQueue (no waiting room), or the queue is at its limit
   Shard& sh = shard();
   std::lock_guard<std::mutex> g(sh.mu);
-  sh.counter.update_max_concurrency(now, active);
-  sh.pool_counter.update_max_concurrency(now, active);
-  sh.pool_counter.add(now, Event::kSuccess);  // "threads executed"
-  return Admit::kRun;
+  sh.counter.add(now, Event::kThreadPoolRejected);
+  sh.pool_counter.add(now, Event::kThreadPoolRejected);
+  return Admit::kRejected;
+}
+
+bool Command::next_queued(Queued* out) {
+  {
+    std::lock_guard<std::mutex> g(queue_mu_);
+    if (queue_.empty() || !try_acquire_slot()) return false;
+    *out = queue_.front();
+    queue_.pop_front();
+  }
+  slot_started(clock_.now_ms(), active_.load(std::memory_order_relaxed));
+  return true;
+}
+
+bool Command::cancel_queued(const Queued& q) {
+  std::lock_guard<std::mutex> g(queue_mu_);
+  for (auto it = queue_.begin(); it != queue_.end(); ++it) {
+    if (*it == q) {
+      queue_.erase(it);
+      return true;
+    }
+  }
+  return false;
+}
+
+void Command::release_slot() {
+  int64_t a = active_.load(std::memory_order_relaxed);
+  while (a > 0 && !active_.compare_exchange_weak(a, a - 1, std::memory_order_acq_rel)) {
+  }
+}
+
+void Command::queued_timeout(int64_t total_ms) {
+  int64_t now = clock_.now_ms();
+  Shard& sh = shard();
+  std::lock_guard<std::mutex> g(sh.mu);
+  sh.counter.add(now, Event::kTimeout);
+  sh.counter.add(now, Event::kFallbackSuccess);
+  sh.total_lat.add(now, total_ms);
+}
+
+int64_t Command::queue_size() {
+  std::lock_guard<std::mutex> g(queue_mu_);
+  return int64_t(queue_.size());
 }
 
 void Command::finish_in(Shard& sh, int64_t now, Event outcome, int64_t execute_ms) {
@@ -431,6 +505,7 @@ void Command::update_settings(const Settings& s) {
   s_.percentile_window_ms = pw;
   s_.percentile_buckets = pb;
   apply_hot(s_);
+  if (!executed_.load(std::memory_order_relaxed)) max_queue_.store(s.pool_max_queue, std::memory_order_relaxed);
 }
 
 Settings Command::settings() {
@@ -479,6 +554,7 @@ CommandSnapshot Command::snapshot() {
   s.pool_largest = largest_.load(std::memory_order_relaxed);
   s.pool_rolling_executed = pc[size_t(Event::kSuccess)];
   s.pool_rolling_rejected = pc[size_t(Event::kThreadPoolRejected)];
+  s.pool_queue_size = queue_size();
   s.has_executed = executed_.load(std::memory_order_relaxed);
   return s;
 }

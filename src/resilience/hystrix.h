@@ -11,13 +11,17 @@
 //  * while open, one trial request is let through every sleepWindow (5 s); a success closes
 //    the circuit and resets the counts;
 //  * bulkhead = thread pool of coreSize 10 with no queue (maxQueueSize -1): the 11th
-//    concurrent call is rejected straight to the fallback;
+//    concurrent call is rejected straight to the fallback. With maxQueueSize > 0 (fixed when
+//    the pool is created) calls beyond coreSize wait in a FIFO while it holds fewer than
+//    min(maxQueueSize, queueSizeRejectionThreshold) (the threshold is dynamic), and are
+//    rejected beyond that; a queued call's timeout runs from its start, queue wait included;
 //  * execution timeout 1000 ms by default, 600 ms per config.properties:17.
 // All time comes from an injectable Clock so tests can drive the state machine.
 #pragma once
 #include <array>
 #include <atomic>
 #include <cstdint>
+#include <deque>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -138,7 +142,7 @@ struct CommandSnapshot {
   Settings settings;
   // thread pool view
   int64_t pool_active = 0, pool_largest = 0, pool_completed = 0, pool_rolling_executed = 0,
-          pool_rolling_max_active = 0, pool_rolling_rejected = 0;
+          pool_rolling_max_active = 0, pool_rolling_rejected = 0, pool_queue_size = 0;
   bool has_executed = false;
 };
 
@@ -152,9 +156,27 @@ class Command {
   Command(std::string name, std::string group, std::string pool, Settings s, const Clock& clock);
   ~Command();
 
-  enum class Admit { kRun, kShortCircuited, kRejected };
-  // Breaker + bulkhead admission. kRun takes a bulkhead slot that finish() releases.
-  Admit try_start();
+  // The caller's handle for a call waiting in the pool queue (opaque to the command).
+  struct Queued {
+    uint64_t a = 0, b = 0;
+    bool operator==(const Queued& o) const { return a == o.a && b == o.b; }
+  };
+  enum class Admit { kRun, kQueued, kShortCircuited, kRejected };
+  // Breaker + bulkhead admission. kRun takes a bulkhead slot that finish()/complete()
+  // releases. kQueued (only with a queue handle and maxQueueSize > 0) parks `q` in the pool
+  // queue: it gets a slot through next_queued().
+  Admit try_start(const Queued* q = nullptr);
+  // After a slot is released: if a call waits, takes a slot for it and pops it (the caller
+  // starts it, or hands the slot back with release_slot()). Call until it returns false.
+  bool next_queued(Queued* out);
+  // Removes a call from the queue (its timeout fired first); false if it was already popped.
+  bool cancel_queued(const Queued& q);
+  // Hands back a slot taken by next_queued() for a call that can no longer run.
+  void release_slot();
+  // A queued call that timed out before getting a slot: TIMEOUT + fallback + total latency,
+  // no slot to release.
+  void queued_timeout(int64_t total_ms);
+  int64_t queue_size();
   // Outcome of an admitted execution: kSuccess, kFailure, kTimeout or kBadRequest.
   void finish(Event outcome, int64_t execute_ms);
   // After a short-circuit/rejection/failure/timeout the fallback runs; record its result
@@ -199,8 +221,17 @@ class Command {
   std::mutex health_mu_;
   std::atomic<int64_t> health_at_{-1};
   std::atomic<uint64_t> health_packed_{0};
-  // bulkhead (thread pool of pool_core_ threads, no queue)
+  // bulkhead (thread pool of pool_core_ threads, and a queue when max_queue_ > 0)
   std::atomic<int64_t> active_{0}, largest_{0};
+  bool try_acquire_slot();
+  void slot_started(int64_t now, int64_t active);
+  // maxQueueSize: Hystrix sizes the pool's queue once, when the pool is created at the first
+  // execution, so later property changes do not resize it (update_settings() before the
+  // first call still does: the start-up configuration arrives after construction)
+  std::atomic<int> max_queue_{-1};
+  std::atomic<int> queue_threshold_{5};
+  std::mutex queue_mu_;
+  std::deque<Queued> queue_;
   std::atomic<bool> executed_{false};
 };
 

@@ -253,6 +253,74 @@ def test_bulkhead_rejects_beyond_pool(hola, aloha):
     assert b'event="THREAD_POOL_REJECTED"' in body
 
 
+def _gauge(s, name: str) -> int:
+    body = s.get("/metrics")[2].decode()
+    return int(next(l.rsplit(" ", 1)[1] for l in body.splitlines() if l.startswith(name + "{")))
+
+
+def test_pool_queue_serves_waiting_calls_in_order(hola, aloha):
+    """-Dhystrix.threadpool.default.maxQueueSize=2: with one pool slot and a slow aloha, the
+    next two calls wait in the queue and are served one after another within the timeout;
+    a fourth is rejected to the fallback at once."""
+    aloha.set_mode("slow", delay_s=0.3)
+    s = hola(args=["--aloha-url", aloha.url, "--feign-log", "none", "--no-tracing",
+                   "-Dhystrix.threadpool.default.coreSize=1", "-Dhystrix.threadpool.default.maxQueueSize=2",
+                   "-Dhystrix.threadpool.default.queueSizeRejectionThreshold=2",
+                   "-Dhystrix.command.default.execution.isolation.thread.timeoutInMilliseconds=3000",
+                   "-Dhystrix.command.default.circuitBreaker.enabled=false"], threads=2)
+    results = {}
+
+    def one(i):
+        t0 = time.monotonic()
+        results[i] = (chain(s), time.monotonic() - t0)
+
+    ts = []
+    for i in range(4):
+        ts.append(threading.Thread(target=one, args=(i,)))
+        ts[-1].start()
+        time.sleep(0.05)  # arrival order 0, 1, 2, 3
+    assert _gauge(s, "hola_hystrix_pool_queued") == 2 and _gauge(s, "hola_hystrix_pool_active") == 1
+    for t in ts:
+        t.join()
+    assert results[3][0][1] == FALLBACK and results[3][1] < 0.25  # queue full: rejected
+    served = [results[i] for i in range(3)]
+    assert all(r[0][1] != FALLBACK for r in served), served
+    # one at a time through the single slot: ~0.3, ~0.6, ~0.9 s after arrival
+    assert served[0][1] < served[1][1] < served[2][1] and served[2][1] >= 0.75, served
+    assert _gauge(s, "hola_hystrix_pool_queued") == 0 and _gauge(s, "hola_hystrix_pool_active") == 0
+    assert b'event="THREAD_POOL_REJECTED"} 1' in s.get("/metrics")[2]
+
+
+def test_pool_queue_under_timeouts_leaks_no_slot(hola, aloha):
+    """Queue, timeouts and rejections racing across two workers: afterwards no slot is held
+    and nothing waits, and the next call goes straight through."""
+    aloha.set_mode("slow", delay_s=0.08)
+    s = hola(args=["--aloha-url", aloha.url, "--feign-log", "none", "--no-tracing",
+                   "-Dhystrix.threadpool.default.coreSize=2", "-Dhystrix.threadpool.default.maxQueueSize=4",
+                   "-Dhystrix.threadpool.default.queueSizeRejectionThreshold=4",
+                   "-Dhystrix.command.default.execution.isolation.thread.timeoutInMilliseconds=150",
+                   "-Dhystrix.command.default.circuitBreaker.enabled=false"], threads=2)
+    outcomes = []
+
+    def burst():
+        for _ in range(6):
+            outcomes.append(chain(s)[1])
+
+    ts = [threading.Thread(target=burst) for _ in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert len(outcomes) == 48
+    assert FALLBACK in outcomes and any(o != FALLBACK for o in outcomes)
+    time.sleep(0.3)
+    assert _gauge(s, "hola_hystrix_pool_active") == 0 and _gauge(s, "hola_hystrix_pool_queued") == 0
+    aloha.set_mode("ok")
+    assert chain(s)[1] != FALLBACK
+    body = s.get("/metrics")[2].decode()
+    assert 'event="TIMEOUT"' in body and 'event="SUCCESS"' in body
+
+
 def _histogram(body: bytes, name: str) -> tuple[dict, float, int]:
     buckets, total, count = {}, None, None
     for line in body.decode().splitlines():

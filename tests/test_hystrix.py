@@ -105,6 +105,58 @@ def test_bulkhead(native):
     assert c.try_start() == "run"
 
 
+QUEUE = {**TUNED, "hystrix.threadpool.default.coreSize": "1", "hystrix.threadpool.default.maxQueueSize": "3",
+         "hystrix.threadpool.default.queueSizeRejectionThreshold": "2"}
+
+
+def test_pool_queue_admission_and_fifo(native):
+    """maxQueueSize > 0: beyond coreSize, calls wait in a FIFO holding fewer than
+    min(maxQueueSize, queueSizeRejectionThreshold); a released slot goes to the oldest."""
+    c = native.HystrixCommand(QUEUE)
+    assert [c.try_start(t) for t in range(5)] == ["run", "queued", "queued", "rejected", "rejected"]
+    assert c.queue_size() == 2
+    assert c.next_queued() is None          # no slot free yet
+    c.finish("success", 1)
+    assert c.next_queued() == 1             # oldest first, and it holds the slot now
+    assert c.next_queued() is None
+    assert c.try_start(7) == "queued"       # room again behind ticket 2
+    c.finish("success", 1)
+    assert c.next_queued() == 2
+    c.finish("success", 1)
+    assert c.next_queued() == 7
+    pool = json.loads(c.pool_json())
+    assert pool["currentQueueSize"] == 0 and pool["currentActiveCount"] == 1
+    assert pool["rollingCountThreadsExecuted"] == 4 and pool["rollingCountCommandRejections"] == 2
+
+
+def test_pool_queue_threshold_and_default(native):
+    # the smaller of maxQueueSize and the rejection threshold bounds the queue
+    c = native.HystrixCommand({**QUEUE, "hystrix.threadpool.default.maxQueueSize": "1",
+                               "hystrix.threadpool.default.queueSizeRejectionThreshold": "5"})
+    assert [c.try_start(t) for t in range(3)] == ["run", "queued", "rejected"]
+    # default maxQueueSize -1 (SynchronousQueue): never queued, even when offered
+    c = native.HystrixCommand({**TUNED, "hystrix.threadpool.default.coreSize": "1"})
+    assert [c.try_start(t) for t in range(2)] == ["run", "rejected"] and c.queue_size() == 0
+
+
+def test_pool_queue_timeout_and_cancel(native):
+    """A queued call that times out leaves the queue and counts as a TIMEOUT (an error for
+    the breaker); a call popped after its timeout hands its slot back."""
+    c = native.HystrixCommand(QUEUE)
+    assert [c.try_start(t) for t in range(3)] == ["run", "queued", "queued"]
+    assert c.cancel_queued(1) and not c.cancel_queued(1)
+    c.queued_timeout(600)
+    assert c.queue_size() == 1
+    c.finish("success", 1)
+    assert c.next_queued() == 2
+    c.release_slot()                         # ticket 2 timed out meanwhile: slot handed back
+    assert c.try_start(9) == "run"
+    cmd = json.loads(c.stream_json())
+    assert cmd["rollingCountTimeout"] == 1 and cmd["rollingCountFallbackSuccess"] == 1
+    c.advance(600)
+    assert c.health()["errors"] == 1
+
+
 def test_force_open_and_closed(native):
     c = native.HystrixCommand({"hystrix.command.default.circuitBreaker.forceOpen": "true"})
     assert c.try_start() == "short_circuited"
