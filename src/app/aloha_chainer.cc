@@ -51,6 +51,7 @@ AlohaChainer::AlohaChainer(AlohaOptions o, resilience::Settings s, int num_worke
   // HystrixFeign keys: command = o_.command_key, group (and pool) = target name (the URL).
   cmd_ = std::make_unique<Command>(o_.command_key, o_.url, o_.url, s, clock_);
   timeout_ms_.store(s.timeout_enabled ? s.timeout_ms : 0);
+  fallback_enabled_.store(s.fallback_enabled);
   if (url_ok_) addr_ = std::make_unique<client::AddressCache>(target_.host, target_.port);
   pools_.resize(size_t(num_workers));
   calls_.resize(size_t(num_workers));
@@ -188,6 +189,14 @@ const ChainResult& static_fallback(Command::Admit a) {
 }
 }  // namespace
 
+ChainResult AlohaChainer::failed_result(const char* why) const {
+  if (fallback_enabled_.load(std::memory_order_relaxed)) return fallback_result(why);
+  ChainResult r;
+  r.error = true;
+  r.reason = why;
+  return r;
+}
+
 void AlohaChainer::call(http::Worker& w, const tracing::SpanContext* parent,
                         std::function<void(const ChainResult&)> done) {
   const int64_t start_ms = clock_.now_ms();
@@ -203,8 +212,10 @@ void AlohaChainer::call(http::Worker& w, const tracing::SpanContext* parent,
   const Command::Admit a = cmd->try_start(&ref);
   if (a == Command::Admit::kShortCircuited || a == Command::Admit::kRejected) {
     release(wc, slot);
-    cmd->rejected(clock_.now_ms() - start_ms);
-    done(static_fallback(a));
+    const bool fb = fallback_enabled_.load(std::memory_order_relaxed);
+    cmd->rejected(clock_.now_ms() - start_ms, fb);
+    if (fb) done(static_fallback(a));
+    else done(failed_result(a == Command::Admit::kShortCircuited ? "short-circuited" : "rejected"));
     return;
   }
   Call& c = *wc.slots[slot];
@@ -347,8 +358,9 @@ void AlohaChainer::on_response(http::Worker& w, WorkerCalls& wc, uint32_t slot, 
   if (success) {
     cmd->complete(Event::kSuccess, elapsed, false, clock_.now_ms() - c.start_ms);
   } else {
-    cmd->complete(Event::kFailure, elapsed, true, clock_.now_ms() - c.start_ms);
-    res = fallback_result("failure");
+    const bool fb = fallback_enabled_.load(std::memory_order_relaxed);
+    cmd->complete(Event::kFailure, elapsed, fb, clock_.now_ms() - c.start_ms);
+    res = failed_result("failure");
     res.reason = err;
   }
   finish(wc, slot, res);
@@ -393,8 +405,8 @@ void AlohaChainer::expire(EventLoop& loop, WorkerCalls& wc, client::ClientPool& 
       // popped it, start_queued() finds it dead and hands the slot on.
       const int64_t elapsed = clock_.now_ms() - c.start_ms;
       cmd_->cancel_queued(queued_ref(*wc.worker, e.slot, e.gen));
-      cmd_->queued_timeout(elapsed);
-      finish(wc, e.slot, fallback_result("timeout"));
+      cmd_->queued_timeout(elapsed, fallback_enabled_.load(std::memory_order_relaxed));
+      finish(wc, e.slot, failed_result("timeout"));
       continue;
     }
     if (c.inflight) {
@@ -406,8 +418,8 @@ void AlohaChainer::expire(EventLoop& loop, WorkerCalls& wc, client::ClientPool& 
     // Feign itself logs nothing when Hystrix times the command out.
     LOG_DEBUG("%s HystrixTimeoutException after %lld ms (%d attempt(s))", log_tag_.c_str(), (long long)elapsed,
               c.attempts);
-    cmd_->complete(Event::kTimeout, elapsed, true, elapsed);
-    finish(wc, e.slot, fallback_result("timeout"));
+    cmd_->complete(Event::kTimeout, elapsed, fallback_enabled_.load(std::memory_order_relaxed), elapsed);
+    finish(wc, e.slot, failed_result("timeout"));
     pump();
   }
   arm(loop, wc, p, worker_index);

@@ -67,6 +67,7 @@ class AlohaChainer final : public Chainer {
   void update_settings(const resilience::Settings& s) {
     cmd_->update_settings(s);
     timeout_ms_.store(s.timeout_enabled ? s.timeout_ms : 0, std::memory_order_relaxed);
+    fallback_enabled_.store(s.fallback_enabled, std::memory_order_relaxed);
   }
   const std::string& full_url() const { return full_url_; }
   // Feign re-executions (Retryer) and HttpClient re-sends on a fresh connection, since start.
@@ -107,6 +108,10 @@ class AlohaChainer final : public Chainer {
   const Clock& clock_;
   std::atomic<int> timeout_ms_{0};  // 0 = execution timeout disabled (read per call, lock-free)
   std::atomic<uint64_t> feign_retries_{0}, transport_retries_{0};
+  // hystrix.command.*.fallback.enabled: false turns every failed call into an error (500)
+  std::atomic<bool> fallback_enabled_{true};
+  // The fallback, or the escaped HystrixRuntimeException when fallbacks are disabled.
+  ChainResult failed_result(const char* why) const;
 };
 
 }  // namespace hola::app

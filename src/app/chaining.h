@@ -26,6 +26,9 @@ struct ChainResult {
   // returns null, the command succeeds, and greetings.addAll(null) then throws in
   // HolaResource.holaChaining() (HolaResource.java:76), so the request fails with a 500.
   bool null_list = false;
+  // The command failed with hystrix.command.*.fallback.enabled=false: HystrixRuntimeException
+  // escapes aloha() and holaChaining() answers a 500, like null_list.
+  bool error = false;
   std::string reason;  // why the fallback was used (timeout, short-circuited, ...)
 };
 

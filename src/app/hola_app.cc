@@ -447,8 +447,9 @@ void HolaApp::handle_chaining(http::Connection& c, const http::Request& r, Worke
                    http::Worker& w = conn->worker();
                    WorkerCache& wc = self->cache(w);
                    bool answered = false;
-                   if (!conn->closed() && res.null_list) {
-                     // greetings.addAll(null) throws after a successful command: a 500.
+                   if (!conn->closed() && (res.null_list || res.error)) {
+                     // greetings.addAll(null) throws after a successful command, and with
+                     // fallbacks disabled HystrixRuntimeException escapes aloha(): a 500.
                      if (wc.gen != self->gen_.load(std::memory_order_relaxed) || wc.date_version != w.date_version())
                        self->refresh(w, wc);
                      conn->complete(wc.server_error[ka][head].view(), ka);

@@ -133,7 +133,9 @@ std::string HystrixStream::render_events() {
     CommandSnapshot s = c->snapshot();
     if (!s.has_executed) continue;  // Hystrix only knows commands that have run
     out += "data: " + command_json(s) + "\n\n";
-    out += "data: " + threadpool_json(s) + "\n\n";
+    // HystrixMetricsPoller publishes a pool only once a task has completed on it
+    // (hasExecutedCommandsOnThread): never for SEMAPHORE isolation
+    if (s.pool_completed > 0) out += "data: " + threadpool_json(s) + "\n\n";
   }
   if (out.empty()) out = "ping: \n\n";
   return out;

@@ -254,6 +254,8 @@ void Command::apply_hot(const Settings& s) {
   sleep_window_ms_.store(s.sleep_window_ms, std::memory_order_relaxed);
   pool_core_.store(s.pool_core_size, std::memory_order_relaxed);
   queue_threshold_.store(s.pool_queue_reject_threshold, std::memory_order_relaxed);
+  semaphore_.store(s.isolation == "SEMAPHORE", std::memory_order_relaxed);
+  sem_max_.store(s.semaphore_max_concurrent, std::memory_order_relaxed);
   health_ms_.store(s.health_snapshot_ms, std::memory_order_relaxed);
 }
 
@@ -350,7 +352,22 @@ Command::Admit Command::try_start(const Queued* q) {
     sh.counter.add(now, Event::kShortCircuited);
     return Admit::kShortCircuited;
   }
+  const bool sem = semaphore_.load(std::memory_order_relaxed);
   int64_t active = active_.fetch_add(1, std::memory_order_acq_rel) + 1;
+  if (sem) {
+    // TryableSemaphoreActual.tryAcquire(): the caller's own thread runs the command
+    if (active <= sem_max_.load(std::memory_order_relaxed)) {
+      Shard& sh = shard();
+      std::lock_guard<std::mutex> g(sh.mu);
+      sh.counter.update_max_concurrency(now, active);
+      return Admit::kRun;
+    }
+    active_.fetch_sub(1, std::memory_order_acq_rel);
+    Shard& sh = shard();
+    std::lock_guard<std::mutex> g(sh.mu);
+    sh.counter.add(now, Event::kSemaphoreRejected);
+    return Admit::kRejected;
+  }
   if (active <= pool_core_.load(std::memory_order_relaxed)) {
     slot_started(now, active);
     return Admit::kRun;
@@ -409,12 +426,12 @@ void Command::release_slot() {
   }
 }
 
-void Command::queued_timeout(int64_t total_ms) {
+void Command::queued_timeout(int64_t total_ms, bool with_fallback) {
   int64_t now = clock_.now_ms();
   Shard& sh = shard();
   std::lock_guard<std::mutex> g(sh.mu);
   sh.counter.add(now, Event::kTimeout);
-  sh.counter.add(now, Event::kFallbackSuccess);
+  if (with_fallback) sh.counter.add(now, Event::kFallbackSuccess);
   sh.total_lat.add(now, total_ms);
 }
 
@@ -427,7 +444,7 @@ void Command::finish_in(Shard& sh, int64_t now, Event outcome, int64_t execute_m
   int64_t a = active_.load(std::memory_order_relaxed);
   while (a > 0 && !active_.compare_exchange_weak(a, a - 1, std::memory_order_acq_rel)) {
   }
-  ++sh.completed;
+  if (!semaphore_.load(std::memory_order_relaxed)) ++sh.completed;  // tasks run on the pool
   sh.counter.add(now, outcome);
   if (outcome == Event::kSuccess || outcome == Event::kFailure) sh.exec_lat.add(now, execute_ms);
 }
@@ -469,11 +486,11 @@ void Command::complete(Event outcome, int64_t execute_ms, bool with_fallback, in
   if (outcome == Event::kSuccess) mark_success(now);
 }
 
-void Command::rejected(int64_t total_ms) {
+void Command::rejected(int64_t total_ms, bool with_fallback) {
   int64_t now = clock_.now_ms();
   Shard& sh = shard();
   std::lock_guard<std::mutex> g(sh.mu);
-  sh.counter.add(now, Event::kFallbackSuccess);
+  if (with_fallback) sh.counter.add(now, Event::kFallbackSuccess);
   sh.total_lat.add(now, total_ms);
 }
 

@@ -15,6 +15,9 @@
 //    the pool is created) calls beyond coreSize wait in a FIFO while it holds fewer than
 //    min(maxQueueSize, queueSizeRejectionThreshold) (the threshold is dynamic), and are
 //    rejected beyond that; a queued call's timeout runs from its start, queue wait included;
+//  * execution.isolation.strategy=SEMAPHORE swaps the pool for a semaphore of
+//    semaphore.maxConcurrentRequests (10): rejections are SEMAPHORE_REJECTED, nothing queues,
+//    and the pool reports no tasks (so the stream shows no HystrixThreadPool frame);
 //  * execution timeout 1000 ms by default, 600 ms per config.properties:17.
 // All time comes from an injectable Clock so tests can drive the state machine.
 #pragma once
@@ -175,7 +178,7 @@ class Command {
   void release_slot();
   // A queued call that timed out before getting a slot: TIMEOUT + fallback + total latency,
   // no slot to release.
-  void queued_timeout(int64_t total_ms);
+  void queued_timeout(int64_t total_ms, bool with_fallback = true);
   int64_t queue_size();
   // Outcome of an admitted execution: kSuccess, kFailure, kTimeout or kBadRequest.
   void finish(Event outcome, int64_t execute_ms);
@@ -185,8 +188,8 @@ class Command {
   void total_latency(int64_t total_ms);
   // finish() + optional fallback() + total_latency() in one shard visit.
   void complete(Event outcome, int64_t execute_ms, bool with_fallback, int64_t total_ms);
-  // Short-circuit / rejection path: fallback + total latency in one shard visit.
-  void rejected(int64_t total_ms);
+  // Short-circuit / rejection path: fallback (unless disabled) + total latency in one shard visit.
+  void rejected(int64_t total_ms, bool with_fallback = true);
 
   bool circuit_open();            // evaluates health like HystrixCircuitBreaker.isOpen()
   HealthCounts health();
@@ -212,7 +215,9 @@ class Command {
   Settings s_;
   // Settings read on every call, updated by config reloads.
   std::atomic<bool> circuit_enabled_{true}, force_open_{false}, force_closed_{false};
-  std::atomic<int> volume_{20}, error_pct_{50}, sleep_window_ms_{5000}, pool_core_{10}, health_ms_{500};
+  std::atomic<int> volume_{20}, error_pct_{50}, sleep_window_ms_{5000}, pool_core_{10}, health_ms_{500},
+      sem_max_{10};
+  std::atomic<bool> semaphore_{false};  // execution.isolation.strategy=SEMAPHORE
   std::vector<std::unique_ptr<Shard>> shards_;
   // breaker (HystrixCircuitBreakerImpl)
   std::atomic<bool> open_{false};

@@ -253,6 +253,38 @@ def test_bulkhead_rejects_beyond_pool(hola, aloha):
     assert b'event="THREAD_POOL_REJECTED"' in body
 
 
+def test_semaphore_isolation_rejects_beyond_max_concurrent(hola, aloha):
+    aloha.set_mode("slow", delay_s=0.4)
+    s = hola(args=["--aloha-url", aloha.url, "--feign-log", "none", "--no-tracing",
+                   "-Dhystrix.command.default.execution.isolation.strategy=SEMAPHORE",
+                   "-Dhystrix.command.default.execution.isolation.semaphore.maxConcurrentRequests=1",
+                   "-Dhystrix.command.default.circuitBreaker.enabled=false"], threads=2)
+    results = []
+    ts = [threading.Thread(target=lambda: results.append(chain(s))) for _ in range(3)]
+    for t in ts:
+        t.start()
+        time.sleep(0.05)
+    for t in ts:
+        t.join()
+    assert sorted(r[1] == FALLBACK for r in results) == [False, True, True]
+    body = s.get("/metrics")[2]
+    assert b'event="SEMAPHORE_REJECTED"} 2' in body and b"THREAD_POOL_REJECTED" not in body
+
+
+def test_fallback_disabled_turns_failures_into_500(hola):
+    """hystrix.command.default.fallback.enabled=false: a failed aloha call raises
+    HystrixRuntimeException out of aloha(), so holaChaining() fails with a 500 and no
+    fallback is counted."""
+    s = hola(args=["--aloha-url", f"http://127.0.0.1:{closed_port()}/", "--feign-retry", "off", "--feign-log", "none",
+                   "-Dhystrix.command.default.fallback.enabled=false"])
+    st, h, body = s.get("/api/hola-chaining")
+    assert st == 500 and "access-control-allow-origin" not in h
+    m = s.get("/metrics")[2]
+    assert b'event="FAILURE"} 1' in m and b"FALLBACK_SUCCESS" not in m
+    # /api/hola is unaffected
+    assert s.get("/api/hola")[0] == 200
+
+
 def _gauge(s, name: str) -> int:
     body = s.get("/metrics")[2].decode()
     return int(next(l.rsplit(" ", 1)[1] for l in body.splitlines() if l.startswith(name + "{")))

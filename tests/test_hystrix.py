@@ -225,6 +225,34 @@ def test_stream_reports_command_after_chaining(hola):
     assert cmd["name"] == "aloha" and cmd["group"] == aloha.url and cmd["rollingCountSuccess"] >= 1
 
 
+def test_semaphore_isolation(native):
+    """execution.isolation.strategy=SEMAPHORE: semaphore.maxConcurrentRequests bounds the
+    calls, rejections are SEMAPHORE_REJECTED, nothing queues and no pool task is counted."""
+    c = native.HystrixCommand({**QUEUE, "hystrix.command.default.execution.isolation.strategy": "SEMAPHORE",
+                               "hystrix.command.default.execution.isolation.semaphore.maxConcurrentRequests": "2"})
+    assert [c.try_start(t) for t in range(3)] == ["run", "run", "rejected"]
+    assert c.queue_size() == 0
+    c.finish("success", 1)
+    assert c.try_start() == "run"
+    cmd = json.loads(c.stream_json())
+    assert cmd["rollingCountSemaphoreRejected"] == 1 and cmd["rollingCountThreadPoolRejected"] == 0
+    assert cmd["propertyValue_executionIsolationStrategy"] == "SEMAPHORE"
+    pool = json.loads(c.pool_json())
+    assert pool["currentCompletedTaskCount"] == 0 and pool["rollingCountThreadsExecuted"] == 0
+
+
+def test_stream_has_no_pool_frame_for_semaphore_commands(hola):
+    """HystrixMetricsPoller publishes a thread pool only after a task completed on it."""
+    with FakeAloha() as aloha:
+        s = hola(args=["--aloha-url", aloha.url, "--feign-log", "none",
+                       "-Dhystrix.command.default.execution.isolation.strategy=SEMAPHORE"])
+        s.get("/api/hola-chaining")
+        out = _read_sse(s.port)
+    events = [json.loads(l[6:]) for l in out.decode(errors="replace").splitlines() if l.startswith("data: {")]
+    assert {e["type"] for e in events} == {"HystrixCommand"}
+    assert events[0]["rollingCountSuccess"] >= 1
+
+
 def test_stream_connection_limit(hola):
     s = hola(args=["--hystrix-stream-max", "1"])
     with socket.create_connection(("127.0.0.1", s.port), timeout=3) as first:
