@@ -399,6 +399,7 @@ Command::Admit Command::try_start(const Queued* q) {
 }
 
 bool Command::next_queued(Queued* out) {
+  if (max_queue_.load(std::memory_order_relaxed) <= 0) return false;  // no queue: no lock per call
   {
     std::lock_guard<std::mutex> g(queue_mu_);
     if (queue_.empty() || !try_acquire_slot()) return false;
