@@ -52,6 +52,7 @@ AlohaChainer::AlohaChainer(AlohaOptions o, resilience::Settings s, int num_worke
   cmd_ = std::make_unique<Command>(o_.command_key, o_.url, o_.url, s, clock_);
   timeout_ms_.store(s.timeout_enabled ? s.timeout_ms : 0);
   fallback_enabled_.store(s.fallback_enabled);
+  read_timeout_armed_.store(read_timeout_for(s));
   if (url_ok_) addr_ = std::make_unique<client::AddressCache>(target_.host, target_.port);
   pools_.resize(size_t(num_workers));
   calls_.resize(size_t(num_workers));
@@ -75,7 +76,10 @@ void AlohaChainer::stop() {
 
 client::ClientPool& AlohaChainer::pool(http::Worker& w) {
   auto& p = pools_[size_t(w.index())];
-  if (!p) p = std::make_unique<client::ClientPool>(w.loop(), target_, addr_.get(), 64, &transport_retries_);
+  if (!p) {
+    p = std::make_unique<client::ClientPool>(w.loop(), target_, addr_.get(), 64, &transport_retries_);
+    p->set_timeouts(o_.connect_timeout_ms, &read_timeout_armed_);
+  }
   return *p;
 }
 

@@ -7,6 +7,8 @@
 //   retries           Feign's default Retryer.Default(100 ms, 1 s, 5): IO errors and
 //                     Retry-After responses re-execute with 1.5x backoff, inside the Hystrix
 //                     timeout (HolaResource.java:104-112 configures no .retryer())
+//   timeouts          Feign Request.Options defaults, 10 s connect / 60 s read; the read
+//                     timeout is armed only when the Hystrix timeout would not come first
 //   fallback          ["Aloha response (fallback)"]                  (HolaResource.java:111-112)
 //   tracing           one client span per HTTP attempt, child of the server span, + B3
 //                     headers (HolaResource.java:97-108)
@@ -49,6 +51,11 @@ struct AlohaOptions {
   std::string config_key = "AlohaService#aloha()";
   std::string command_key = "aloha";  // Hystrix command key (--hystrix-command-key)
   RetryPolicy retry;
+  // Feign 8 Request.Options defaults (the reference builds none): 10 s to connect, 60 s to
+  // read. They matter only when the Hystrix timeout is disabled or longer: the read timeout
+  // is armed per request only then (--feign-timeouts CONNECT_MS,READ_MS).
+  int connect_timeout_ms = 10000;
+  int read_timeout_ms = 60000;
 };
 
 class AlohaChainer final : public Chainer {
@@ -68,6 +75,7 @@ class AlohaChainer final : public Chainer {
     cmd_->update_settings(s);
     timeout_ms_.store(s.timeout_enabled ? s.timeout_ms : 0, std::memory_order_relaxed);
     fallback_enabled_.store(s.fallback_enabled, std::memory_order_relaxed);
+    read_timeout_armed_.store(read_timeout_for(s), std::memory_order_relaxed);
   }
   const std::string& full_url() const { return full_url_; }
   // Feign re-executions (Retryer) and HttpClient re-sends on a fresh connection, since start.
@@ -110,6 +118,12 @@ class AlohaChainer final : public Chainer {
   std::atomic<uint64_t> feign_retries_{0}, transport_retries_{0};
   // hystrix.command.*.fallback.enabled: false turns every failed call into an error (500)
   std::atomic<bool> fallback_enabled_{true};
+  // Feign's read timeout, armed per request only when the Hystrix timeout would not end the
+  // call first (0 = not armed).
+  std::atomic<int> read_timeout_armed_{0};
+  int read_timeout_for(const resilience::Settings& s) const {
+    return (!s.timeout_enabled || s.timeout_ms > o_.read_timeout_ms) ? o_.read_timeout_ms : 0;
+  }
   // The fallback, or the escaped HystrixRuntimeException when fallbacks are disabled.
   ChainResult failed_result(const char* why) const;
 };

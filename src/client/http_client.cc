@@ -131,6 +131,7 @@ struct ClientPool::Conn final : EventLoop::Handler {
   size_t off = 0;
   std::string in;
   uint64_t id = 0;
+  uint64_t serial = 0;
   Callback cb;
   bool reused = false;  // went out on a kept-alive socket
   int tries = 0;        // transport re-executions so far (DefaultHttpRequestRetryHandler)
@@ -415,8 +416,29 @@ uint64_t ClientPool::get(const std::string& path, const std::string& extra_heade
   return id;
 }
 
+void ClientPool::arm_timeout(int ms, uint64_t id, uint64_t serial, bool connect_phase) {
+  loop_.add_timer(ms, [this, id, serial, connect_phase] {
+    auto it = active_.find(id);
+    if (it == active_.end() || it->second->serial != serial) return;  // answered, or a new connection
+    Conn* c = it->second;
+    if (connect_phase) {
+      if (c->st != Conn::kConnecting) return;
+      c->fail("ConnectTimeoutException: Connect to " + target_.host + ":" + std::to_string(target_.port) +
+                  " failed: connect timed out",
+              false);
+    } else if (c->st == Conn::kWriting || c->st == Conn::kReading) {
+      c->fail("SocketTimeoutException: Read timed out", false);
+    }
+  });
+}
+
 void ClientPool::start_on(Conn* c, uint64_t id, std::string req, Callback cb, bool reused) {
   c->id = id;
+  c->serial = next_serial_++;
+  if (read_timeout_ms_) {
+    const int rt = read_timeout_ms_->load(std::memory_order_relaxed);
+    if (rt > 0) arm_timeout(rt, id, c->serial, false);
+  }
   c->cb = std::move(cb);
   c->out = std::move(req);
   c->off = 0;
@@ -464,6 +486,7 @@ void ClientPool::start_on(Conn* c, uint64_t id, std::string req, Callback cb, bo
   c->interest = EPOLLOUT;
   loop_.add(c->fd, EPOLLOUT, c);
   c->st = inprog ? Conn::kConnecting : Conn::kWriting;
+  if (inprog && connect_timeout_ms_ > 0) arm_timeout(connect_timeout_ms_, id, c->serial, true);
   if (!inprog) c->do_write();
 }
 

@@ -81,6 +81,14 @@ class ClientPool {
   uint64_t get(const std::string& path, const std::string& extra_headers, Callback cb);
   // Abandons a request (e.g. on timeout): its connection is closed, its callback dropped.
   void cancel(uint64_t id);
+  // Feign's Request.Options on this pool: a connect that has not completed after
+  // `connect_ms` fails as ConnectTimeoutException, and, while *read_ms > 0, a request without
+  // a complete response *read_ms after it started fails as SocketTimeoutException. Both are
+  // IOExceptions to Feign (retried by its Retryer) but not to HttpClient's retry handler.
+  void set_timeouts(int connect_ms, const std::atomic<int>* read_ms) {
+    connect_timeout_ms_ = connect_ms;
+    read_timeout_ms_ = read_ms;
+  }
   size_t idle_connections() const { return idle_.size(); }
   uint64_t connections_opened() const { return opened_; }
 
@@ -103,6 +111,11 @@ class ClientPool {
   uint64_t opened_ = 0;
   std::string host_header_;
   std::atomic<uint64_t>* transport_retries_;
+  int connect_timeout_ms_ = 0;
+  const std::atomic<int>* read_timeout_ms_ = nullptr;
+  uint64_t next_serial_ = 1;  // tells a Conn from a later one at the same address
+  // Fails request `id` if it is still on connection `serial` in one of `states` after `ms`.
+  void arm_timeout(int ms, uint64_t id, uint64_t serial, bool connect_phase);
 };
 
 }  // namespace hola::client

@@ -57,6 +57,9 @@ void usage() {
           "  --feign-log basic|none   outbound call logging (default basic)\n"
           "  --feign-retry default|off|P,MAX,N   Feign Retryer on IO errors (default: Retryer.Default\n"
           "                           = 100 ms period, 1000 ms max period, 5 attempts)\n"
+          "  --feign-timeouts C,R     Feign Request.Options: connect / read timeout in ms (default\n"
+          "                           10000,60000; the read timeout applies when the Hystrix timeout\n"
+          "                           is disabled or longer)\n"
           "  --hystrix-command-key method|configkey|KEY   Hystrix command key of the aloha call\n"
           "                           (default method = \"aloha\", feign-hystrix 8.x; configkey =\n"
           "                           \"AlohaService#aloha()\", feign-hystrix 9.x SetterFactory.Default)\n"
@@ -166,6 +169,15 @@ int main(int argc, char** argv) {
         fprintf(stderr, "hola: --feign-retry default|off|PERIOD_MS,MAX_PERIOD_MS,MAX_ATTEMPTS\n");
         return 2;
       }
+    } else if (a == "--feign-timeouts") {
+      int c = 0, r = 0;
+      char tail = 0;
+      if (sscanf(val("--feign-timeouts").c_str(), "%d,%d%c", &c, &r, &tail) != 2 || c < 0 || r < 0) {
+        fprintf(stderr, "hola: --feign-timeouts CONNECT_MS,READ_MS\n");
+        return 2;
+      }
+      alo.connect_timeout_ms = c;
+      alo.read_timeout_ms = r;
     } else if (a == "--hystrix-command-key") {
       std::string k = val("--hystrix-command-key");
       if (k == "method") alo.command_key = "aloha";

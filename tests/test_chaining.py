@@ -271,6 +271,26 @@ def test_semaphore_isolation_rejects_beyond_max_concurrent(hola, aloha):
     assert b'event="SEMAPHORE_REJECTED"} 2' in body and b"THREAD_POOL_REJECTED" not in body
 
 
+def test_feign_read_timeout_when_hystrix_timeout_is_disabled(hola, aloha):
+    """With execution.timeout.enabled=false nothing but Feign's Request.Options ends a call to
+    an aloha that never answers: each attempt fails as SocketTimeoutException after the read
+    timeout (an IOException, so Feign retries), then the command fails to the fallback. The
+    bulkhead slot is released instead of being held for good."""
+    aloha.set_mode("slow", delay_s=3.0)
+    s = hola(args=["--aloha-url", aloha.url, "--feign-timeouts", "10000,300", "--feign-retry", "100,1000,2",
+                   "-Dhystrix.command.default.execution.timeout.enabled=false",
+                   "-Dhystrix.threadpool.default.coreSize=1"], threads=1)
+    t0 = time.monotonic()
+    assert chain(s)[1] == FALLBACK
+    took = time.monotonic() - t0
+    assert 0.65 <= took < 1.5, took  # 300 ms, 150 ms sleep, 300 ms
+    m = s.get("/metrics")[2]
+    assert b'event="FAILURE"} 1' in m and b"TIMEOUT" not in m
+    assert b'hola_aloha_retries_total{kind="feign"} 1' in m
+    assert b'hola_hystrix_pool_active{command="aloha"} 0' in m
+    assert "<--- ERROR SocketTimeoutException: Read timed out" in s.log()
+
+
 def test_fallback_disabled_turns_failures_into_500(hola):
     """hystrix.command.default.fallback.enabled=false: a failed aloha call raises
     HystrixRuntimeException out of aloha(), so holaChaining() fails with a 500 and no
