@@ -568,6 +568,12 @@ CommandSnapshot Command::snapshot() {
   s.latency_execute_mean = exec_n ? exec_sum / exec_n : 0;
   s.latency_total_mean = total_n ? total_sum / total_n : 0;
   s.settings = settings();
+  if (!s.settings.percentile_enabled) {
+    // HystrixRollingPercentile with metrics.rollingPercentile.enabled=false reports -1
+    s.latency_execute.fill(-1);
+    s.latency_total.fill(-1);
+    s.latency_execute_mean = s.latency_total_mean = -1;
+  }
   s.pool_active = s.concurrent;
   s.pool_largest = largest_.load(std::memory_order_relaxed);
   s.pool_rolling_executed = pc[size_t(Event::kSuccess)];

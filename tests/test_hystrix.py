@@ -253,6 +253,15 @@ def test_stream_has_no_pool_frame_for_semaphore_commands(hola):
     assert events[0]["rollingCountSuccess"] >= 1
 
 
+def test_rolling_percentile_disabled_reports_minus_one(native):
+    c = native.HystrixCommand({**TUNED, "hystrix.command.default.metrics.rollingPercentile.enabled": "false"})
+    assert c.try_start() == "run"
+    c.finish("success", 12)
+    cmd = json.loads(c.stream_json())
+    assert set(cmd["latencyExecute"].values()) == {-1} and cmd["latencyExecute_mean"] == -1
+    assert set(cmd["latencyTotal"].values()) == {-1} and cmd["latencyTotal_mean"] == -1
+
+
 def test_stream_connection_limit(hola):
     s = hola(args=["--hystrix-stream-max", "1"])
     with socket.create_connection(("127.0.0.1", s.port), timeout=3) as first:
