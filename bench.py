@@ -34,8 +34,8 @@ sys.path.insert(0, str(Path(__file__).resolve().parent))
 
 from hola_amd.native import ensure_built  # noqa: E402
 from hola_amd.parallel.hostmetrics import (  # noqa: E402
-    accept_locality, cgroup_cpu_stat, proc_cpu_s, sink_stats, span_counters, start_zipkin_sink, tcp_counters,
-    thread_cpu_s)
+    MetricsProbe, accept_locality, cgroup_cpu_stat, proc_cpu_s, sink_stats, span_counters, start_zipkin_sink,
+    tcp_counters, thread_cpu_s)
 from hola_amd.parallel.loadgen import ControlledLoadgen, decode_hist, merge_hists, percentile  # noqa: E402
 from hola_amd.server import HolaProcess  # noqa: E402
 from hola_amd.utils.cpu import (  # noqa: E402
@@ -200,6 +200,10 @@ def main() -> int:
                          log_level="warn")
     server.start()
     loadgen = None
+    # /metrics over one kept-alive connection: the placement counters before the load
+    # generator connects and after the timed region then differ by exactly its connections
+    probe = MetricsProbe(host, port)
+    locality0 = accept_locality(host, port, probe)
     try:
         if dist:
             dist.barrier()  # every replica is listening before any connection is made
@@ -216,7 +220,7 @@ def main() -> int:
         if dist:
             dist.barrier()
         cuda()
-        span0 = span_counters(host, port)
+        span0 = span_counters(host, port, probe)
         sink0 = sink_stats(plan[0]["sink_port"]) if local_rank == 0 else {}
         tracer0 = thread_cpu_s(server.proc.pid, "hola-tracer")
         cpu0 = (proc_cpu_s(server.proc.pid), proc_cpu_s(loadgen.proc.pid))
@@ -234,8 +238,9 @@ def main() -> int:
         elapsed = time.perf_counter() - t0
         cpu1 = (proc_cpu_s(server.proc.pid), proc_cpu_s(loadgen.proc.pid))
         tracer1 = thread_cpu_s(server.proc.pid, "hola-tracer")
-        span1 = span_counters(host, port)
-        locality = accept_locality(host, port)
+        span1 = span_counters(host, port, probe)
+        locality1 = accept_locality(host, port, probe)
+        locality = {k: v - locality0.get(k, 0) for k, v in locality1.items()}
         sink1 = sink_stats(plan[0]["sink_port"]) if local_rank == 0 else {}
         tcp1 = tcp_counters()
         thr1 = cgroup_cpu_stat()
@@ -262,6 +267,7 @@ def main() -> int:
         else:
             gathered = [local]
     finally:
+        probe.close()
         if loadgen:
             loadgen.close()
         server.stop()
@@ -376,8 +382,8 @@ def _own_loadgen(cores: list[dict]) -> list[list[int]]:
 
 def _locality_block(gathered: list[dict]) -> dict:
     """Node-wide and per-replica fractions of accepted connections by client/worker
-    relation. The bench's connections are all made before the timed region, so this is the
-    placement of every timed request's connection (minus the /metrics probes: 1-2 each)."""
+    relation, counted over the load generator's own connections (made before the timed
+    region): the placement of every timed request's connection."""
     def frac(d: dict) -> dict:
         n = sum(d.values())
         return {k: round(v / n, 4) for k, v in d.items()} if n else {}

@@ -52,15 +52,46 @@ def sink_stats(port: int) -> dict:
     return json.loads(body) if st == 200 else {}
 
 
-def span_counters(host: str, port: int) -> dict:
-    """hola_spans_* counters from a replica's /metrics (empty with tracing off)."""
+class MetricsProbe:
+    """One kept-alive connection to a replica's /metrics. Probing over it adds no accepted
+    connection after the first, so the accept-placement counters taken before and after a
+    run differ by exactly the run's own connections."""
+
+    def __init__(self, host: str, port: int, timeout: float = 5.0):
+        import http.client
+
+        self._conn = http.client.HTTPConnection(host, port, timeout=timeout)
+
+    def text(self) -> str:
+        import http.client
+
+        for _ in range(2):  # the replica may have closed the idle connection: reconnect once
+            try:
+                self._conn.request("GET", "/metrics")
+                r = self._conn.getresponse()
+                body = r.read()
+                return body.decode() if r.status == 200 else ""
+            except (OSError, http.client.HTTPException):
+                self._conn.close()
+        return ""
+
+    def close(self) -> None:
+        self._conn.close()
+
+
+def _metrics_text(host: str, port: int) -> str:
     from hola_amd.utils.net import http_get
     try:
         st, _, body = http_get(host, port, "/metrics")
     except OSError:
-        return {}
+        return ""
+    return body.decode() if st == 200 else ""
+
+
+def span_counters(host: str, port: int, probe: MetricsProbe | None = None) -> dict:
+    """hola_spans_* counters from a replica's /metrics (empty with tracing off)."""
     out = {}
-    for line in body.decode().splitlines() if st == 200 else []:
+    for line in (probe.text() if probe else _metrics_text(host, port)).splitlines():
         if line.startswith("hola_spans_recorded_total "):
             out["recorded"] = int(float(line.split()[1]))
         elif line.startswith("hola_spans_reported_total "):
@@ -70,17 +101,12 @@ def span_counters(host: str, port: int) -> dict:
     return out
 
 
-def accept_locality(host: str, port: int) -> dict:
+def accept_locality(host: str, port: int, probe: MetricsProbe | None = None) -> dict:
     """hola_accept_locality_total from a replica's /metrics: where each accepted connection's
     client thread ran relative to the worker serving it (same_core / same_l3 / same_socket /
     cross_socket / unknown)."""
-    from hola_amd.utils.net import http_get
-    try:
-        st, _, body = http_get(host, port, "/metrics")
-    except OSError:
-        return {}
     out = {}
-    for line in body.decode().splitlines() if st == 200 else []:
+    for line in (probe.text() if probe else _metrics_text(host, port)).splitlines():
         if line.startswith("hola_accept_locality_total{relation="):
             out[line.split('"')[1]] = int(float(line.rsplit(" ", 1)[1]))
     return out
