@@ -345,6 +345,9 @@ int main(int argc, char** argv) {
                                : (server.steering() ? "rr+l3-steering" : "rr"),
            !to.enabled ? "off" : (to.collector_url.empty() ? "on (no collector: spans dropped)" : to.collector_url.c_str()),
            chainer.full_url().c_str());
+  // The start-up lines are on stderr before anyone is told the port (supervisors and tests
+  // read them as soon as the port file appears).
+  Logger::instance().flush();
   if (!port_file.empty()) {
     std::string tmp = port_file + ".tmp";
     {
