@@ -292,6 +292,29 @@ def test_feign_read_timeout_when_hystrix_timeout_is_disabled(hola, aloha):
     assert "<--- ERROR SocketTimeoutException: Read timed out" in s.log()
 
 
+def test_feign_connect_timeout(hola):
+    """A connect that never completes (aloha's accept queue is full, so its SYNs are dropped)
+    fails as ConnectTimeoutException after Feign's connect timeout, and is retried by Feign."""
+    srv = socket.socket()
+    srv.bind(("127.0.0.1", 0))
+    srv.listen(0)
+    filler = socket.create_connection(srv.getsockname())  # the one queued connection
+    try:
+        s = hola(args=["--aloha-url", "http://127.0.0.1:%d/" % srv.getsockname()[1], "--feign-timeouts", "300,60000",
+                       "--feign-retry", "100,1000,2", "-Dhystrix.command.default.execution.timeout.enabled=false"],
+                 threads=1)
+        t0 = time.monotonic()
+        assert chain(s)[1] == FALLBACK
+        took = time.monotonic() - t0
+        assert 0.65 <= took < 1.5, took  # 300 ms, 150 ms sleep, 300 ms
+        assert "<--- ERROR ConnectTimeoutException: Connect to 127.0.0.1:%d failed: connect timed out" % srv.getsockname()[1] \
+            in s.log(), s.log()
+        assert b'hola_aloha_retries_total{kind="feign"} 1' in s.get("/metrics")[2]
+    finally:
+        filler.close()
+        srv.close()
+
+
 def test_fallback_disabled_turns_failures_into_500(hola):
     """hystrix.command.default.fallback.enabled=false: a failed aloha call raises
     HystrixRuntimeException out of aloha(), so holaChaining() fails with a 500 and no
