@@ -112,6 +112,13 @@ def _info() -> int:
     print(f"allowed cpus   : {format_cpu_list(allowed_cpus())}")
     print(f"physical cores : {len(phys)} in {len(doms)} L3 domains")
     print(f"cgroup quota   : {cgroup_cpu_quota() or 'unlimited'}  -> budget {cpu_budget()} CPUs")
+    # Host load per L3 domain (both SMT threads of its cores, other tenants included): what
+    # the bench's planner ranks when it takes the quietest domains first.
+    from hola_amd.utils.cpu import cpu_busy, siblings
+
+    busy = cpu_busy(0.5)
+    dom_load = {d: sum(busy.get(x, 0.0) for c in cs for x in siblings(c)) for d, cs in doms.items()}
+    print("L3 load (CPUs busy, 0.5 s): " + ", ".join(f"{d}:{v:.1f}" for d, v in sorted(dom_load.items())))
     for n in (1, 2, 4, 8):
         print(f"plan x{n}: {[format_cpu_list(p) for p in plan_node(n, avoid_busy=False)]}")
     # What bench.py would decide on this node (one replica per GPU slot, weak scaling).
