@@ -34,8 +34,8 @@ sys.path.insert(0, str(Path(__file__).resolve().parent))
 
 from hola_amd.native import ensure_built  # noqa: E402
 from hola_amd.parallel.hostmetrics import (  # noqa: E402
-    MetricsProbe, accept_locality, cgroup_cpu_stat, proc_cpu_s, sink_stats, span_counters, start_zipkin_sink,
-    tcp_counters, thread_cpu_s)
+    MetricsProbe, accept_locality, busy_fraction, cgroup_cpu_stat, cpu_times, proc_cpu_s, sink_stats, span_counters,
+    start_zipkin_sink, tcp_counters, thread_cpu_s)
 from hola_amd.parallel.loadgen import ControlledLoadgen, decode_hist, merge_hists, percentile  # noqa: E402
 from hola_amd.server import HolaProcess  # noqa: E402
 from hola_amd.utils.cpu import (  # noqa: E402
@@ -226,6 +226,7 @@ def main() -> int:
         cpu0 = (proc_cpu_s(server.proc.pid), proc_cpu_s(loadgen.proc.pid))
         tcp0 = tcp_counters()
         thr0 = cgroup_cpu_stat()
+        times0 = cpu_times()
         t0 = time.perf_counter()
         reqs = errs = 0
         for _ in range(a.steps):
@@ -244,6 +245,9 @@ def main() -> int:
         sink1 = sink_stats(plan[0]["sink_port"]) if local_rank == 0 else {}
         tcp1 = tcp_counters()
         thr1 = cgroup_cpu_stat()
+        times1 = cpu_times()
+        own = set(server_cpus) | set(load_cpus)
+        sibs = {x for c in own for x in siblings(c)} - own
         st = loadgen.stats()
         mem = server.memory_kb()
         c1 = _config2_subrun(a, host, port, load_cpus, bodies and [bodies[local_rank]]) if local_rank == 0 else None
@@ -260,7 +264,11 @@ def main() -> int:
                  "server_cpu_s": cpu1[0] - cpu0[0], "loadgen_cpu_s": cpu1[1] - cpu0[1],
                  "startup_ms": server.startup_ms, "rss_peak_kb": mem.get("VmHWM", 0),
                  "tcp": {k: tcp1[k] - tcp0[k] for k in tcp1 if k in tcp0},
-                 "cgroup": {k: thr1[k] - thr0[k] for k in thr1 if k in thr0}}
+                 "cgroup": {k: thr1[k] - thr0[k] for k in thr1 if k in thr0},
+                 # host-wide busy share over the timed region of this rank's CPUs and of their
+                 # SMT siblings that it leaves idle (busy there = another tenant sharing our cores)
+                 "host_load": {"own": busy_fraction(times0, times1, own),
+                               "siblings": busy_fraction(times0, times1, sibs)}}
         if dist:
             gathered = [None] * world
             dist.all_gather_object(gathered, local)
@@ -327,6 +335,9 @@ def main() -> int:
             "tracing": _tracing_block(a, gathered, t, plan[0]["sink_port"]),
             # client thread vs. serving worker placement of every accepted connection
             "locality": _locality_block(gathered),
+            # busy share of the replicas' CPUs and of the SMT siblings they leave idle, per rank,
+            # over the timed region: siblings kept busy by other tenants slow our threads
+            "host_load": [g["host_load"] for g in gathered],
             "config": {
                 "model": "hola GET /api/hola (native C++ replica, default greeting, "
                          + ("tracing off" if a.no_tracing else

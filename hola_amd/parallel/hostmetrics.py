@@ -136,6 +136,31 @@ def proc_cpu_s(pid: int) -> float:
         return 0.0
 
 
+def cpu_times() -> dict[int, tuple[int, int]]:
+    """Per-CPU (total, idle+iowait) jiffies from /proc/stat, host-wide (other tenants included)."""
+    out = {}
+    try:
+        with open("/proc/stat") as f:
+            for line in f:
+                if line.startswith("cpu") and line[3].isdigit():
+                    parts = line.split()
+                    v = list(map(int, parts[1:]))
+                    out[int(parts[0][3:])] = (sum(v), v[3] + v[4])
+    except (OSError, ValueError, IndexError):
+        pass
+    return out
+
+
+def busy_fraction(t0: dict, t1: dict, cpus) -> float | None:
+    """Busy share of `cpus` between two cpu_times() snapshots (None when unknown)."""
+    tot = idle = 0
+    for c in cpus:
+        if c in t0 and c in t1:
+            tot += t1[c][0] - t0[c][0]
+            idle += t1[c][1] - t0[c][1]
+    return round(1.0 - idle / tot, 4) if tot > 0 else None
+
+
 def cgroup_cpu_stat() -> dict[str, int]:
     """cgroup v2 cpu.stat counters of this process's cgroup (empty when unavailable)."""
     try:
