@@ -16,8 +16,9 @@ node-wide total req/s, and p50/p99 come from the merged latency histograms of al
 Every response body in the timed region is compared with the greeting of the replica behind
 its connection (a mismatch is an error). After the timed region rank 0 runs BASELINE config
 2 (one connection, ~3 s) and reports it as c1_* keys; the JSON also carries span accounting
-(`tracing`, with a native collector under --zipkin-sink) and connection placement
-(`locality`).
+(`tracing`, with a native collector under --zipkin-sink), connection placement (`locality`)
+and how busy the replicas' cores and their idle SMT siblings were (`host_load`: other
+tenants on the siblings are what moves the number between runs on a shared host).
 
   python bench.py --gpus N --steps K --warmup W
 """
