@@ -1,6 +1,12 @@
 #include "metrics/prometheus.h"
 
+#include <dirent.h>
+#include <sys/resource.h>
+#include <unistd.h>
+
 #include <cstdio>
+#include <cstdlib>
+#include <cstring>
 
 #include "app/hola_app.h"
 #include "http/server.h"
@@ -9,6 +15,62 @@
 #include "tracing/tracer.h"
 
 namespace hola::metrics {
+
+namespace {
+// The standard process_* metrics of Prometheus client libraries, from /proc/self.
+void process_metrics(std::string* o) {
+  const double tck = double(sysconf(_SC_CLK_TCK));
+  const double page = double(sysconf(_SC_PAGESIZE));
+  char buf[1024];
+  char num[64];
+  if (FILE* f = fopen("/proc/self/stat", "r")) {
+    size_t n = fread(buf, 1, sizeof buf - 1, f);
+    fclose(f);
+    buf[n] = 0;
+    // After the parenthesised comm: v[0] is field 3 (state), so field N is v[N - 3]:
+    // utime 14, stime 15, starttime 22, vsize 23, rss 24 (pages).
+    if (const char* p = strrchr(buf, ')')) {
+      unsigned long long v[22] = {};
+      const char* q = p + 1;
+      for (int k = 0; k < 22 && *q; ++k) {
+        while (*q == ' ') ++q;
+        v[k] = strtoull(q, nullptr, 10);
+        while (*q && *q != ' ') ++q;
+      }
+      snprintf(num, sizeof num, "%.2f", double(v[11] + v[12]) / tck);
+      *o += "# TYPE process_cpu_seconds_total counter\nprocess_cpu_seconds_total ";
+      *o += num;
+      *o += "\n# TYPE process_virtual_memory_bytes gauge\nprocess_virtual_memory_bytes " + std::to_string(v[20]);
+      *o += "\n# TYPE process_resident_memory_bytes gauge\nprocess_resident_memory_bytes " +
+            std::to_string((unsigned long long)(double(v[21]) * page)) + "\n";
+      if (FILE* st = fopen("/proc/stat", "r")) {
+        unsigned long long btime = 0;
+        char line[256];
+        while (fgets(line, sizeof line, st))
+          if (sscanf(line, "btime %llu", &btime) == 1) break;
+        fclose(st);
+        if (btime) {
+          snprintf(num, sizeof num, "%.2f", double(btime) + double(v[19]) / tck);
+          *o += "# TYPE process_start_time_seconds gauge\nprocess_start_time_seconds ";
+          *o += num;
+          *o += "\n";
+        }
+      }
+    }
+  }
+  if (DIR* d = opendir("/proc/self/fd")) {
+    long n = 0;
+    while (dirent* e = readdir(d))
+      if (e->d_name[0] != '.') ++n;
+    closedir(d);
+    // minus the descriptor the directory stream itself held
+    *o += "# TYPE process_open_fds gauge\nprocess_open_fds " + std::to_string(n - 1) + "\n";
+  }
+  rlimit rl{};
+  if (getrlimit(RLIMIT_NOFILE, &rl) == 0)
+    *o += "# TYPE process_max_fds gauge\nprocess_max_fds " + std::to_string((unsigned long long)rl.rlim_cur) + "\n";
+}
+}  // namespace
 
 Prometheus::Prometheus(int num_workers, int num_routes)
     : nworkers_(num_workers), nroutes_(num_routes), counts_(new Counter[size_t(num_workers) * size_t(num_routes)]),
@@ -98,6 +160,7 @@ std::string Prometheus::render(http::Server* server) const {
     o += "# TYPE hola_hystrix_pool_queued gauge\nhola_hystrix_pool_queued{command=\"" + s.name + "\"} " +
          std::to_string(s.pool_queue_size) + "\n";
   }
+  process_metrics(&o);
   if (reloads_) o += "# TYPE hola_config_reloads_total counter\nhola_config_reloads_total " + std::to_string(reloads_()) + "\n";
   if (feign_retries_ && transport_retries_) {
     o += "# TYPE hola_aloha_retries_total counter\nhola_aloha_retries_total{kind=\"feign\"} " +

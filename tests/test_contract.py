@@ -269,6 +269,27 @@ def test_many_concurrent_connections(hola):
             c.close()
 
 
+def test_metrics_process_collector(hola):
+    """/metrics carries the standard process_* metrics of Prometheus client libraries."""
+    import resource
+
+    s = hola()
+    t0 = time.time()
+    m = {}
+    for line in s.get("/metrics")[2].decode().splitlines():
+        if line.startswith("process_"):
+            k, v = line.split()
+            m[k] = float(v)
+    assert set(m) == {"process_cpu_seconds_total", "process_virtual_memory_bytes", "process_resident_memory_bytes",
+                      "process_start_time_seconds", "process_open_fds", "process_max_fds"}
+    assert 1 << 20 < m["process_resident_memory_bytes"] < 512 << 20
+    assert m["process_virtual_memory_bytes"] > m["process_resident_memory_bytes"]
+    assert abs(m["process_start_time_seconds"] - t0) < 120
+    assert 3 <= m["process_open_fds"] < 200
+    assert m["process_max_fds"] == resource.getrlimit(resource.RLIMIT_NOFILE)[0]
+    assert m["process_cpu_seconds_total"] >= 0
+
+
 def test_expect_100_continue(hola):
     s = hola()
     with socket.create_connection(("127.0.0.1", s.port), timeout=3) as c:
