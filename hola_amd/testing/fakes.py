@@ -154,11 +154,25 @@ class _ZipkinHandler(BaseHTTPRequestHandler):
 
 
 class FakeZipkin(_Base):
-    def __init__(self, status: int = 202):
+    """Zipkin collector stand-in. With ``tls=(certfile, keyfile)`` it serves HTTPS (the URL
+    becomes https://127.0.0.1:PORT/)."""
+
+    def __init__(self, status: int = 202, tls: tuple[str, str] | None = None):
         self.lock = threading.Lock()
         self.posts: list[dict] = []
         self.status = status
         super().__init__(_ZipkinHandler)
+        self.tls = tls
+        if tls:
+            import ssl
+
+            ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
+            ctx.load_cert_chain(*tls)
+            self.server.socket = ctx.wrap_socket(self.server.socket, server_side=True)
+
+    @property
+    def url(self) -> str:
+        return f"{'https' if self.tls else 'http'}://127.0.0.1:{self.port}/"
 
     def spans(self) -> list[dict]:
         with self.lock:

@@ -45,7 +45,9 @@ bool parse_retry_policy(const std::string& s, RetryPolicy* out) {
 AlohaChainer::AlohaChainer(AlohaOptions o, resilience::Settings s, int num_workers, tracing::Tracer* tracer,
                            const Clock& clock)
     : o_(std::move(o)), tracer_(tracer), clock_(clock) {
-  url_ok_ = client::parse_url(o_.url, &target_);
+  // The reference's target is http://aloha:8080/ (HolaResource.java:103); the event-loop client
+  // speaks plain HTTP only.
+  url_ok_ = client::parse_url(o_.url, &target_) && !target_.tls;
   if (!url_ok_) LOG_ERROR("aloha url '%s' is not an http:// URL; every call will fall back", o_.url.c_str());
   full_url_ = "http://" + target_.host + ":" + std::to_string(target_.port) + target_.base_path + o_.path;
   // HystrixFeign keys: command = o_.command_key, group (and pool) = target name (the URL).

@@ -10,6 +10,7 @@
 
 #include "app/aloha_chainer.h"
 #include "client/http_client.h"
+#include "client/url.h"
 #include "config/jformat.h"
 #include "core/net.h"
 #include "config/properties.h"
@@ -361,6 +362,11 @@ PYBIND11_MODULE(_native, m) {
         py::arg("shared") = false);
   m.def("histogram_percentiles", &histogram_percentiles);
   m.def("is_local_resource_error", &is_local_resource_error);
+  m.def("parse_url", [](const std::string& s) -> py::object {
+    client::Url u;
+    if (!client::parse_url(s, &u)) return py::none();
+    return py::make_tuple(u.host, u.port, u.base_path, u.tls);
+  });
   m.def("strip_path_parameters", [](const std::string& p) {
     std::string out(p.size(), '\0');
     size_t n = 0;

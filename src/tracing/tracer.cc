@@ -67,11 +67,13 @@ Tracer::Tracer(TracerOptions o, int num_workers) : o_(std::move(o)) {
     if (client::parse_url(o_.collector_url, &u)) {
       chost_ = u.host;
       cport_ = u.port;
+      ctls_ = u.tls;
       cpath_ = u.base_path + (o_.v2 ? "api/v2/spans" : "api/v1/spans");
       collecting_ = true;
       caddr_ = std::make_unique<client::AddressCache>(chost_, cport_);
     } else {
-      LOG_WARN("ZIPKIN_SERVER_URL '%s' is not an http:// URL; spans will be dropped", o_.collector_url.c_str());
+      LOG_WARN("ZIPKIN_SERVER_URL '%s' is not an http:// or https:// URL; spans will be dropped",
+               o_.collector_url.c_str());
     }
   }
   // Without a collector, spans are counted and dropped at the source: no rings.
@@ -320,6 +322,7 @@ bool Tracer::post(const std::string& body) {
   client::Url u;
   u.host = chost_;
   u.port = cport_;
+  u.tls = ctls_;
   client::BlockingResponse resp;
   const char* hdr = "Content-Type: application/json\r\n";
   bool ok;
@@ -328,9 +331,10 @@ bool Tracer::post(const std::string& body) {
     sockaddr_storage ss{};
     socklen_t len = 0;
     if (!caddr_->get(&ss, &len, nullptr)) len = 0;
-    ok = client::blocking_request(u, ss, len, &cfd_, "POST", cpath_, hdr, body, 2000, &resp);
+    ok = client::blocking_request(u, &cconn_, &ss, len, "POST", cpath_, hdr, body, 2000, &resp);
   } else {
-    ok = client::blocking_request(u, &cfd_, "POST", cpath_, hdr, body, 2000, &resp);  // tests: flush() alone
+    // tests: flush() without start()
+    ok = client::blocking_request(u, &cconn_, nullptr, 0, "POST", cpath_, hdr, body, 2000, &resp);
   }
   return ok && resp.status >= 200 && resp.status < 300;
 }
@@ -409,8 +413,7 @@ void Tracer::stop() {
   (void)w;
   if (th_.joinable()) th_.join();
   flush();
-  if (cfd_ >= 0) ::close(cfd_);
-  cfd_ = -1;
+  cconn_.close();
   running_ = false;
   if (caddr_) caddr_->stop();
 }

@@ -22,6 +22,7 @@
 #include <thread>
 #include <vector>
 
+#include "client/url.h"
 #include "tracing/b3.h"
 
 namespace hola::http {
@@ -155,9 +156,10 @@ class Tracer {
   // cache's own thread while the reporter runs, so a DNS server that does not answer never
   // holds up a flush or shutdown
   std::unique_ptr<client::AddressCache> caddr_;
-  int cfd_ = -1;
+  client::BlockingConn cconn_;
   std::string chost_, cpath_;
   int cport_ = 0;
+  bool ctls_ = false;  // https:// collector
 };
 
 }  // namespace hola::tracing

@@ -114,6 +114,56 @@ def test_collector_down_never_blocks(hola):
     assert b"hola_span_post_failures_total" in body
 
 
+def _self_signed(tmp_path, name: str, san: str) -> tuple[str, str]:
+    import shutil
+    import subprocess
+
+    if not shutil.which("openssl"):
+        pytest.skip("openssl CLI not installed")
+    cert, key = tmp_path / f"{name}.pem", tmp_path / f"{name}.key"
+    subprocess.run(["openssl", "req", "-x509", "-newkey", "rsa:2048", "-nodes", "-days", "1", "-keyout", str(key),
+                    "-out", str(cert), "-subj", f"/CN={name}", "-addext", f"subjectAltName={san}"],
+                   check=True, capture_output=True)
+    return str(cert), str(key)
+
+
+def _post_failures(s) -> int:
+    body = s.get("/metrics")[2].decode()
+    return int(next(l.split()[1] for l in body.splitlines() if l.startswith("hola_span_post_failures_total ")))
+
+
+def test_https_collector_verified_against_the_trust_store(hola, tmp_path):
+    """ZIPKIN_SERVER_URL=https://...: spans go over TLS once the collector's certificate
+    chains to a trusted CA ($SSL_CERT_FILE here) and names the host; otherwise nothing is
+    sent and the failed POSTs are counted."""
+    cert, key = _self_signed(tmp_path, "collector", "DNS:localhost,IP:127.0.0.1")
+    with FakeZipkin(tls=(cert, key)) as z:
+        assert z.url.startswith("https://")
+        s = hola(env={"ZIPKIN_SERVER_URL": z.url.rstrip("/"), "SSL_CERT_FILE": cert})
+        assert s.get("/api/hola")[0] == 200
+        spans = z.wait_for(lambda sp: len(sp) >= 1)
+        assert len(spans) == 1 and spans[0]["name"] == "get"
+        # not trusted: the self-signed certificate is not in the store
+        s2 = hola(env={"ZIPKIN_SERVER_URL": z.url.rstrip("/"), "SSL_CERT_FILE": str(tmp_path / "none.pem")})
+        assert s2.get("/api/hola")[0] == 200
+        time.sleep(1.5)
+        assert len(z.spans()) == 1 and _post_failures(s2) >= 1
+    # trusted, but issued for another name
+    other_cert, other_key = _self_signed(tmp_path, "other", "DNS:other.example")
+    with FakeZipkin(tls=(other_cert, other_key)) as z:
+        s3 = hola(env={"ZIPKIN_SERVER_URL": z.url.rstrip("/"), "SSL_CERT_FILE": other_cert})
+        assert s3.get("/api/hola")[0] == 200
+        time.sleep(1.5)
+        assert z.spans() == [] and _post_failures(s3) >= 1
+
+
+def test_https_urls_parse(native):
+    assert native.parse_url("https://zipkin:9411") == ("zipkin", 9411, "/", True)
+    assert native.parse_url("https://zipkin/") == ("zipkin", 443, "/", True)
+    assert native.parse_url("http://zipkin-query:9411") == ("zipkin-query", 9411, "/", False)
+    assert native.parse_url("ftp://x") is None
+
+
 def test_spans_flushed_on_shutdown(hola_bin, zipkin):
     from hola_amd.server import HolaProcess
 
