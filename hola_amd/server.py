@@ -32,7 +32,7 @@ class HolaProcess:
         self.cpu_list = cpu_list
         self.exe = exe or binary("hola", preset)
         keep = ("PATH", "LANG", "LC_ALL", "TMPDIR", "LD_LIBRARY_PATH", "TSAN_OPTIONS", "ASAN_OPTIONS",
-                "UBSAN_OPTIONS", "LSAN_OPTIONS")
+                "UBSAN_OPTIONS", "LSAN_OPTIONS", "SSL_CERT_FILE", "SSL_CERT_DIR")
         base = dict(os.environ) if inherit_env else {k: v for k, v in os.environ.items() if k in keep}
         if not inherit_env:
             base.pop("HOSTNAME", None)
