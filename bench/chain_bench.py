@@ -33,10 +33,16 @@ a = ap.parse_args()
 
 
 
+def cpu_split(pid: int) -> tuple[float, float]:
+    """(utime, stime) of a process, in seconds."""
+    f = Path(f"/proc/{pid}/stat").read_text().rsplit(")", 1)[1].split()
+    tck = os.sysconf("SC_CLK_TCK")
+    return int(f[11]) / tck, int(f[12]) / tck
+
+
 def cpu_s(pid: int) -> float:
     """utime + stime of a process, in seconds."""
-    f = Path(f"/proc/{pid}/stat").read_text().rsplit(")", 1)[1].split()
-    return (int(f[11]) + int(f[12])) / os.sysconf("SC_CLK_TCK")
+    return sum(cpu_split(pid))
 
 
 # Every L3 domain holds a share of A, B and the load generator (A does two hops' work), so
@@ -59,12 +65,17 @@ with HolaProcess(args=["--aloha-url", "http://127.0.0.1:1/", "--feign-log", "non
         sample = json.loads(body)
         assert sample[1:] == ["Hola de B", "Aloha response (fallback)"], sample  # two hops, no fallback at A
         c0, w0 = (cpu_s(s.proc.pid), cpu_s(b.proc.pid)), time.perf_counter()
+        u0 = (cpu_split(s.proc.pid), cpu_split(b.proc.pid))
         # every response must be the two-hop body seen above (a fallback would differ)
         res = run_duration([("127.0.0.1", s.port)], a.connections, len(cores[2]), a.duration, 2.0,
                            cpu_list=format_cpu_list(cores[2]), path="/api/hola-chaining",
                            expect_bodies=[body.decode()])
         wall = time.perf_counter() - w0
         busy = {"A": (cpu_s(s.proc.pid) - c0[0]) / wall, "B": (cpu_s(b.proc.pid) - c0[1]) / wall}
+        u1 = (cpu_split(s.proc.pid), cpu_split(b.proc.pid))
+        # user-space share of each process's CPU (the rest is the kernel: sockets, epoll)
+        user_share = {k: round((u1[i][0] - u0[i][0]) / max(1e-9, sum(u1[i]) - sum(u0[i])), 3)
+                      for i, k in enumerate(("A", "B"))}
         _, _, metrics = s.get("/metrics")
 events = {l.split('event="')[1].split('"')[0]: int(l.split()[-1]) for l in metrics.decode().splitlines()
           if l.startswith("hola_hystrix_events_total")}
@@ -75,6 +86,7 @@ out = {"sample": sample, "rps": res["rps"], "p50_ms": res["latency"]["p50_ns"] /
        # cores kept busy (warmup included) and CPU µs per request at the measured rate
        "cpus_busy": {k: round(v, 2) for k, v in busy.items()},
        "cpu_us_per_req": {k: round(v / res["rps"] * 1e6, 2) for k, v in busy.items()},
+       "user_share": user_share,
        "cpu_map": {"A": format_cpu_list(cores[0]), "B": format_cpu_list(cores[1]), "loadgen": format_cpu_list(cores[2])}}
 print(json.dumps(out))
 if a.out:
