@@ -375,6 +375,7 @@ ClientPool::ClientPool(EventLoop& loop, Url target, AddressCache* addr, size_t m
 }
 
 ClientPool::~ClientPool() {
+  if (read_timer_) loop_.cancel_timer(read_timer_);
   for (Conn* c : idle_) {
     if (c->fd >= 0) ::close(c->fd);
     delete c;
@@ -416,20 +417,68 @@ uint64_t ClientPool::get(const std::string& path, const std::string& extra_heade
   return id;
 }
 
-void ClientPool::arm_timeout(int ms, uint64_t id, uint64_t serial, bool connect_phase) {
-  loop_.add_timer(ms, [this, id, serial, connect_phase] {
+void ClientPool::arm_connect_timeout(int ms, uint64_t id, uint64_t serial) {
+  loop_.add_timer(ms, [this, id, serial] {
     auto it = active_.find(id);
     if (it == active_.end() || it->second->serial != serial) return;  // answered, or a new connection
     Conn* c = it->second;
-    if (connect_phase) {
-      if (c->st != Conn::kConnecting) return;
-      c->fail("ConnectTimeoutException: Connect to " + target_.host + ":" + std::to_string(target_.port) +
-                  " failed: connect timed out",
-              false);
-    } else if (c->st == Conn::kWriting || c->st == Conn::kReading) {
-      c->fail("SocketTimeoutException: Read timed out", false);
-    }
+    if (c->st != Conn::kConnecting) return;
+    c->fail("ConnectTimeoutException: Connect to " + target_.host + ":" + std::to_string(target_.port) +
+                " failed: connect timed out",
+            false);
   });
+}
+
+bool ClientPool::live(const ReadDeadline& d) const {
+  auto it = active_.find(d.id);
+  return it != active_.end() && it->second->serial == d.serial;
+}
+
+void ClientPool::push_read_deadline(int ms, uint64_t id, uint64_t serial) {
+  const ReadDeadline d{mono_ms() + ms, id, serial};
+  if (read_fifo_.empty() || read_fifo_.back().at_ms <= d.at_ms) {
+    read_fifo_.push_back(d);
+  } else {
+    // The read timeout was shortened by a config reload: keep the FIFO in deadline order.
+    auto it = std::upper_bound(read_fifo_.begin(), read_fifo_.end(), d.at_ms,
+                               [](int64_t at, const ReadDeadline& x) { return at < x.at_ms; });
+    read_fifo_.insert(it, d);
+  }
+  arm_read_timer();
+}
+
+void ClientPool::arm_read_timer() {
+  if (read_fifo_.empty()) return;
+  const int64_t at = read_fifo_.front().at_ms;
+  if (read_timer_at_ != 0 && read_timer_at_ <= at) return;
+  if (read_timer_) loop_.cancel_timer(read_timer_);
+  read_timer_at_ = at;
+  read_timer_ = loop_.add_timer(at - mono_ms(), [this] {
+    read_timer_ = 0;
+    read_timer_at_ = 0;
+    expire_reads();
+  });
+}
+
+void ClientPool::expire_reads() {
+  const int64_t now = mono_ms();
+  while (!read_fifo_.empty()) {
+    const ReadDeadline d = read_fifo_.front();
+    if (!live(d)) {
+      read_fifo_.pop_front();
+      continue;
+    }
+    if (d.at_ms > now) break;
+    read_fifo_.pop_front();
+    Conn* c = active_.find(d.id)->second;
+    // fail() runs the callback, which may start (and push deadlines for) further requests
+    if (c->st == Conn::kWriting || c->st == Conn::kReading) c->fail("SocketTimeoutException: Read timed out", false);
+  }
+  arm_read_timer();
+}
+
+void ClientPool::pop_finished_reads() {
+  while (!read_fifo_.empty() && !live(read_fifo_.front())) read_fifo_.pop_front();
 }
 
 void ClientPool::start_on(Conn* c, uint64_t id, std::string req, Callback cb, bool reused) {
@@ -437,7 +486,7 @@ void ClientPool::start_on(Conn* c, uint64_t id, std::string req, Callback cb, bo
   c->serial = next_serial_++;
   if (read_timeout_ms_) {
     const int rt = read_timeout_ms_->load(std::memory_order_relaxed);
-    if (rt > 0) arm_timeout(rt, id, c->serial, false);
+    if (rt > 0) push_read_deadline(rt, id, c->serial);
   }
   c->cb = std::move(cb);
   c->out = std::move(req);
@@ -486,12 +535,13 @@ void ClientPool::start_on(Conn* c, uint64_t id, std::string req, Callback cb, bo
   c->interest = EPOLLOUT;
   loop_.add(c->fd, EPOLLOUT, c);
   c->st = inprog ? Conn::kConnecting : Conn::kWriting;
-  if (inprog && connect_timeout_ms_ > 0) arm_timeout(connect_timeout_ms_, id, c->serial, true);
+  if (inprog && connect_timeout_ms_ > 0) arm_connect_timeout(connect_timeout_ms_, id, c->serial);
   if (!inprog) c->do_write();
 }
 
 void ClientPool::finish(Conn* c, ClientResult&& r, bool reusable) {
   active_.erase(c->id);
+  if (!read_fifo_.empty()) pop_finished_reads();
   Callback cb = std::move(c->cb);
   c->cb = nullptr;
   if (reusable && c->fd >= 0 && idle_.size() < max_idle_) {
@@ -522,6 +572,7 @@ void ClientPool::cancel(uint64_t id) {
   Conn* c = it->second;
   active_.erase(it);
   destroy(c);
+  if (!read_fifo_.empty()) pop_finished_reads();
 }
 
 }  // namespace hola::client

@@ -8,6 +8,7 @@
 
 #include <atomic>
 #include <cstdint>
+#include <deque>
 #include <functional>
 #include <memory>
 #include <mutex>
@@ -114,8 +115,25 @@ class ClientPool {
   int connect_timeout_ms_ = 0;
   const std::atomic<int>* read_timeout_ms_ = nullptr;
   uint64_t next_serial_ = 1;  // tells a Conn from a later one at the same address
-  // Fails request `id` if it is still on connection `serial` in one of `states` after `ms`.
-  void arm_timeout(int ms, uint64_t id, uint64_t serial, bool connect_phase);
+  // Fails request `id` as a connect timeout if it is still connecting on `serial` after `ms`.
+  void arm_connect_timeout(int ms, uint64_t id, uint64_t serial);
+  // Read timeouts all have the same delay, so their deadlines come due in the order they
+  // were armed: a FIFO with one loop timer for its front replaces a timer per request (which
+  // would hold rate x timeout entries, since a timer outlives the request it guards).
+  // Entries of finished requests are dropped from the front as requests finish, so the FIFO
+  // holds about as many entries as there are requests in flight.
+  struct ReadDeadline {
+    int64_t at_ms;
+    uint64_t id, serial;
+  };
+  std::deque<ReadDeadline> read_fifo_;
+  EventLoop::TimerId read_timer_ = 0;
+  int64_t read_timer_at_ = 0;  // deadline the armed timer fires for (0 = none armed)
+  bool live(const ReadDeadline& d) const;
+  void push_read_deadline(int ms, uint64_t id, uint64_t serial);
+  void arm_read_timer();
+  void expire_reads();
+  void pop_finished_reads();
 };
 
 }  // namespace hola::client

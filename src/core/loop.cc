@@ -61,10 +61,14 @@ EventLoop::TimerId EventLoop::add_timer(int64_t delay_ms, std::function<void()> 
   TimerId id = next_timer_++;
   heap_.push({mono_ms() + (delay_ms < 0 ? 0 : delay_ms), id});
   timers_.emplace(id, std::move(cb));
+  pending_.store(timers_.size(), std::memory_order_relaxed);
   return id;
 }
 
-void EventLoop::cancel_timer(TimerId id) { timers_.erase(id); }
+void EventLoop::cancel_timer(TimerId id) {
+  timers_.erase(id);
+  pending_.store(timers_.size(), std::memory_order_relaxed);
+}
 
 void EventLoop::post(std::function<void()> fn) {
   {
@@ -107,6 +111,7 @@ void EventLoop::run_timers() {
     if (it == timers_.end()) continue;  // cancelled
     auto cb = std::move(it->second);
     timers_.erase(it);
+    pending_.store(timers_.size(), std::memory_order_relaxed);
     cb();
   }
   // Drop cancelled entries at the top so they do not cause spurious wakeups.

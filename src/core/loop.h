@@ -37,6 +37,9 @@ class EventLoop {
   // One-shot timer; callback runs on the loop thread. Returns an id usable with cancel_timer.
   TimerId add_timer(int64_t delay_ms, std::function<void()> cb);
   void cancel_timer(TimerId id);
+  // Timers armed and not yet fired or cancelled; readable from any thread (a leak detector:
+  // the /metrics gauge hola_event_loop_timers).
+  size_t pending_timers() const { return pending_.load(std::memory_order_relaxed); }
 
   // Thread-safe: run fn on the loop thread soon.
   void post(std::function<void()> fn);
@@ -83,6 +86,7 @@ class EventLoop {
   int64_t now_ms_ = 0;
   std::priority_queue<TimerEntry, std::vector<TimerEntry>, std::greater<TimerEntry>> heap_;
   std::unordered_map<TimerId, std::function<void()>> timers_;
+  std::atomic<size_t> pending_{0};  // timers_.size(), published for other threads
   TimerId next_timer_ = 1;
   std::mutex post_mu_;
   std::vector<std::function<void()>> posted_;

@@ -171,6 +171,7 @@ class Worker {
   // out) are closed without their callbacks and freed with the loop.
   ~Worker();
   EventLoop& loop() { return loop_; }
+  const EventLoop& loop() const { return loop_; }
   int index() const { return index_; }
   Server& server() { return *server_; }
   WorkerStats& stats() { return stats_; }

@@ -133,6 +133,10 @@ std::string Prometheus::render(http::Server* server) const {
     o += "# TYPE hola_bytes_in_total counter\nhola_bytes_in_total " + std::to_string(bin) + "\n";
     o += "# TYPE hola_bytes_out_total counter\nhola_bytes_out_total " + std::to_string(bout) + "\n";
     o += "# TYPE hola_workers gauge\nhola_workers " + std::to_string(server->num_workers()) + "\n";
+    // Loop timers armed and not yet fired: tracks the calls in flight, never the call rate.
+    size_t timers = 0;
+    for (size_t i = 0; i < server->num_workers(); ++i) timers += server->worker(i).loop().pending_timers();
+    o += "# TYPE hola_event_loop_timers gauge\nhola_event_loop_timers " + std::to_string(timers) + "\n";
   }
   if (tracer_) {
     tracing::TracerStats t = tracer_->stats();

@@ -292,6 +292,34 @@ def test_feign_read_timeout_when_hystrix_timeout_is_disabled(hola, aloha):
     assert "<--- ERROR SocketTimeoutException: Read timed out" in s.log()
 
 
+def _metric(s, name) -> int:
+    for line in s.get("/metrics")[2].decode().splitlines():
+        if line.startswith(name + " "):
+            return int(float(line.split()[1]))
+    raise AssertionError(f"{name} missing from /metrics")
+
+
+def test_read_timeouts_do_not_pile_up_timers(hola, aloha):
+    """With the Hystrix timeout disabled, every aloha request is guarded by Feign's 60 s read
+    timeout. Finished requests must not leave their timeout behind: the loop's pending timers
+    follow the calls in flight, not calls x 60 s (a timer per request would reach millions at
+    the chaining rate)."""
+    s = hola(args=["--aloha-url", aloha.url, "--no-tracing", "--feign-log", "none",
+                   "-Dhystrix.command.default.execution.timeout.enabled=false"], threads=1)
+    idle = _metric(s, "hola_event_loop_timers")
+    for _ in range(200):
+        assert chain(s)[1] == "Aloha mai aloha-1"
+    assert _metric(s, "hola_event_loop_timers") <= idle + 4  # a timer each: read FIFO, sweep, ticks
+    # the read timeout still fires for a request that gets no answer
+    aloha.set_mode("slow", delay_s=3.0)
+    s2 = hola(args=["--aloha-url", aloha.url, "--no-tracing", "--feign-timeouts", "10000,200", "--feign-retry", "off",
+                    "-Dhystrix.command.default.execution.timeout.enabled=false"], threads=1)
+    t0 = time.monotonic()
+    assert chain(s2)[1] == FALLBACK
+    assert 0.15 <= time.monotonic() - t0 < 1.0
+    assert "<--- ERROR SocketTimeoutException: Read timed out" in s2.log()
+
+
 def test_feign_connect_timeout(hola):
     """A connect that never completes (aloha's accept queue is full, so its SYNs are dropped)
     fails as ConnectTimeoutException after Feign's connect timeout, and is retried by Feign."""
