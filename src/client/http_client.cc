@@ -370,12 +370,14 @@ std::string ClientPool::connect_error(int err) const {
 ClientPool::ClientPool(EventLoop& loop, Url target, AddressCache* addr, size_t max_idle,
                        std::atomic<uint64_t>* transport_retries)
     : loop_(loop), target_(std::move(target)), addr_(addr), max_idle_(max_idle), transport_retries_(transport_retries) {
+  connect_fifo_.connect = true;
   host_header_ = target_.host;
   if (target_.port != 80) host_header_ += ":" + std::to_string(target_.port);
 }
 
 ClientPool::~ClientPool() {
-  if (read_timer_) loop_.cancel_timer(read_timer_);
+  for (DeadlineFifo* f : {&connect_fifo_, &read_fifo_})
+    if (f->timer) loop_.cancel_timer(f->timer);
   for (Conn* c : idle_) {
     if (c->fd >= 0) ::close(c->fd);
     delete c;
@@ -417,68 +419,64 @@ uint64_t ClientPool::get(const std::string& path, const std::string& extra_heade
   return id;
 }
 
-void ClientPool::arm_connect_timeout(int ms, uint64_t id, uint64_t serial) {
-  loop_.add_timer(ms, [this, id, serial] {
-    auto it = active_.find(id);
-    if (it == active_.end() || it->second->serial != serial) return;  // answered, or a new connection
-    Conn* c = it->second;
-    if (c->st != Conn::kConnecting) return;
-    c->fail("ConnectTimeoutException: Connect to " + target_.host + ":" + std::to_string(target_.port) +
-                " failed: connect timed out",
-            false);
-  });
-}
-
-bool ClientPool::live(const ReadDeadline& d) const {
+bool ClientPool::live(const Deadline& d) const {
   auto it = active_.find(d.id);
   return it != active_.end() && it->second->serial == d.serial;
 }
 
-void ClientPool::push_read_deadline(int ms, uint64_t id, uint64_t serial) {
-  const ReadDeadline d{mono_ms() + ms, id, serial};
-  if (read_fifo_.empty() || read_fifo_.back().at_ms <= d.at_ms) {
-    read_fifo_.push_back(d);
+void ClientPool::push_deadline(DeadlineFifo& f, int ms, uint64_t id, uint64_t serial) {
+  const Deadline d{mono_ms() + ms, id, serial};
+  if (f.q.empty() || f.q.back().at_ms <= d.at_ms) {
+    f.q.push_back(d);
   } else {
-    // The read timeout was shortened by a config reload: keep the FIFO in deadline order.
-    auto it = std::upper_bound(read_fifo_.begin(), read_fifo_.end(), d.at_ms,
-                               [](int64_t at, const ReadDeadline& x) { return at < x.at_ms; });
-    read_fifo_.insert(it, d);
+    // The timeout was shortened (a config reload): keep the FIFO in deadline order.
+    auto it = std::upper_bound(f.q.begin(), f.q.end(), d.at_ms,
+                               [](int64_t at, const Deadline& x) { return at < x.at_ms; });
+    f.q.insert(it, d);
   }
-  arm_read_timer();
+  arm(f);
 }
 
-void ClientPool::arm_read_timer() {
-  if (read_fifo_.empty()) return;
-  const int64_t at = read_fifo_.front().at_ms;
-  if (read_timer_at_ != 0 && read_timer_at_ <= at) return;
-  if (read_timer_) loop_.cancel_timer(read_timer_);
-  read_timer_at_ = at;
-  read_timer_ = loop_.add_timer(at - mono_ms(), [this] {
-    read_timer_ = 0;
-    read_timer_at_ = 0;
-    expire_reads();
+void ClientPool::arm(DeadlineFifo& f) {
+  if (f.q.empty()) return;
+  const int64_t at = f.q.front().at_ms;
+  if (f.timer_at != 0 && f.timer_at <= at) return;
+  if (f.timer) loop_.cancel_timer(f.timer);
+  f.timer_at = at;
+  DeadlineFifo* fp = &f;
+  f.timer = loop_.add_timer(at - mono_ms(), [this, fp] {
+    fp->timer = 0;
+    fp->timer_at = 0;
+    expire(*fp);
   });
 }
 
-void ClientPool::expire_reads() {
+void ClientPool::expire(DeadlineFifo& f) {
   const int64_t now = mono_ms();
-  while (!read_fifo_.empty()) {
-    const ReadDeadline d = read_fifo_.front();
+  while (!f.q.empty()) {
+    const Deadline d = f.q.front();
     if (!live(d)) {
-      read_fifo_.pop_front();
+      f.q.pop_front();
       continue;
     }
     if (d.at_ms > now) break;
-    read_fifo_.pop_front();
+    f.q.pop_front();
     Conn* c = active_.find(d.id)->second;
     // fail() runs the callback, which may start (and push deadlines for) further requests
-    if (c->st == Conn::kWriting || c->st == Conn::kReading) c->fail("SocketTimeoutException: Read timed out", false);
+    if (f.connect) {
+      if (c->st == Conn::kConnecting)
+        c->fail("ConnectTimeoutException: Connect to " + target_.host + ":" + std::to_string(target_.port) +
+                    " failed: connect timed out",
+                false);
+    } else if (c->st == Conn::kWriting || c->st == Conn::kReading) {
+      c->fail("SocketTimeoutException: Read timed out", false);
+    }
   }
-  arm_read_timer();
+  arm(f);
 }
 
-void ClientPool::pop_finished_reads() {
-  while (!read_fifo_.empty() && !live(read_fifo_.front())) read_fifo_.pop_front();
+void ClientPool::pop_finished(DeadlineFifo& f) {
+  while (!f.q.empty() && !live(f.q.front())) f.q.pop_front();
 }
 
 void ClientPool::start_on(Conn* c, uint64_t id, std::string req, Callback cb, bool reused) {
@@ -486,7 +484,7 @@ void ClientPool::start_on(Conn* c, uint64_t id, std::string req, Callback cb, bo
   c->serial = next_serial_++;
   if (read_timeout_ms_) {
     const int rt = read_timeout_ms_->load(std::memory_order_relaxed);
-    if (rt > 0) push_read_deadline(rt, id, c->serial);
+    if (rt > 0) push_deadline(read_fifo_, rt, id, c->serial);
   }
   c->cb = std::move(cb);
   c->out = std::move(req);
@@ -535,13 +533,14 @@ void ClientPool::start_on(Conn* c, uint64_t id, std::string req, Callback cb, bo
   c->interest = EPOLLOUT;
   loop_.add(c->fd, EPOLLOUT, c);
   c->st = inprog ? Conn::kConnecting : Conn::kWriting;
-  if (inprog && connect_timeout_ms_ > 0) arm_connect_timeout(connect_timeout_ms_, id, c->serial);
+  if (inprog && connect_timeout_ms_ > 0) push_deadline(connect_fifo_, connect_timeout_ms_, id, c->serial);
   if (!inprog) c->do_write();
 }
 
 void ClientPool::finish(Conn* c, ClientResult&& r, bool reusable) {
   active_.erase(c->id);
-  if (!read_fifo_.empty()) pop_finished_reads();
+  if (!read_fifo_.q.empty()) pop_finished(read_fifo_);
+  if (!connect_fifo_.q.empty()) pop_finished(connect_fifo_);
   Callback cb = std::move(c->cb);
   c->cb = nullptr;
   if (reusable && c->fd >= 0 && idle_.size() < max_idle_) {
@@ -572,7 +571,8 @@ void ClientPool::cancel(uint64_t id) {
   Conn* c = it->second;
   active_.erase(it);
   destroy(c);
-  if (!read_fifo_.empty()) pop_finished_reads();
+  if (!read_fifo_.q.empty()) pop_finished(read_fifo_);
+  if (!connect_fifo_.q.empty()) pop_finished(connect_fifo_);
 }
 
 }  // namespace hola::client

@@ -115,25 +115,27 @@ class ClientPool {
   int connect_timeout_ms_ = 0;
   const std::atomic<int>* read_timeout_ms_ = nullptr;
   uint64_t next_serial_ = 1;  // tells a Conn from a later one at the same address
-  // Fails request `id` as a connect timeout if it is still connecting on `serial` after `ms`.
-  void arm_connect_timeout(int ms, uint64_t id, uint64_t serial);
-  // Read timeouts all have the same delay, so their deadlines come due in the order they
-  // were armed: a FIFO with one loop timer for its front replaces a timer per request (which
-  // would hold rate x timeout entries, since a timer outlives the request it guards).
-  // Entries of finished requests are dropped from the front as requests finish, so the FIFO
-  // holds about as many entries as there are requests in flight.
-  struct ReadDeadline {
+  // Connect and read timeouts each have one delay, so deadlines of one kind come due in the
+  // order they were armed: a FIFO per kind with one loop timer for its front replaces a timer
+  // per request (which would hold rate x timeout entries, since a timer outlives the request
+  // it guards). Entries of finished requests are dropped from the front as requests finish,
+  // so a FIFO holds about as many entries as there are requests in flight.
+  struct Deadline {
     int64_t at_ms;
     uint64_t id, serial;
   };
-  std::deque<ReadDeadline> read_fifo_;
-  EventLoop::TimerId read_timer_ = 0;
-  int64_t read_timer_at_ = 0;  // deadline the armed timer fires for (0 = none armed)
-  bool live(const ReadDeadline& d) const;
-  void push_read_deadline(int ms, uint64_t id, uint64_t serial);
-  void arm_read_timer();
-  void expire_reads();
-  void pop_finished_reads();
+  struct DeadlineFifo {
+    std::deque<Deadline> q;
+    EventLoop::TimerId timer = 0;
+    int64_t timer_at = 0;  // deadline the armed timer fires for (0 = none armed)
+    bool connect = false;  // connect timeouts (else read timeouts)
+  };
+  DeadlineFifo connect_fifo_, read_fifo_;
+  bool live(const Deadline& d) const;
+  void push_deadline(DeadlineFifo& f, int ms, uint64_t id, uint64_t serial);
+  void arm(DeadlineFifo& f);
+  void expire(DeadlineFifo& f);
+  void pop_finished(DeadlineFifo& f);
 };
 
 }  // namespace hola::client
