@@ -27,6 +27,9 @@ ap = argparse.ArgumentParser(description=__doc__)
 ap.add_argument("--duration", type=float, default=10)
 ap.add_argument("--connections", type=int, default=64)
 ap.add_argument("--pool", type=int, default=128, help="hystrix thread-pool (bulkhead) size on A")
+ap.add_argument("--feign-log", default="none", choices=("none", "basic"),
+                help="A's Feign logging; basic = the reference's ErrorLogger at Level.BASIC (two stderr "
+                     "lines per call, the server's default)")
 ap.add_argument("--out", default="")
 ap.add_argument("--exe-a", default="", help="alternative hola binary for A (A/B runs)")
 a = ap.parse_args()
@@ -57,7 +60,7 @@ with HolaProcess(args=["--aloha-url", "http://127.0.0.1:1/", "--feign-log", "non
                        "--feign-retry", "off", "--log-level", "warn"], env={"HOSTNAME": "B"}, threads=len(cores[1]),
                  cpu_list=format_cpu_list(cores[1])) as b:
     with HolaProcess(args=["--aloha-url", f"http://127.0.0.1:{b.port}/", "--aloha-path", "api/hola-chaining",
-                           "--feign-log", "none", "--hystrix-pool-size", str(a.pool)],
+                           "--feign-log", a.feign_log, "--hystrix-pool-size", str(a.pool)],
                      env={"HOSTNAME": "A"}, threads=len(cores[0]), cpu_list=format_cpu_list(cores[0]),
                      exe=Path(a.exe_a) if a.exe_a else None) as s:
         st, _, body = s.get("/api/hola-chaining")
@@ -82,7 +85,7 @@ events = {l.split('event="')[1].split('"')[0]: int(l.split()[-1]) for l in metri
 out = {"sample": sample, "rps": res["rps"], "p50_ms": res["latency"]["p50_ns"] / 1e6,
        "p99_ms": res["latency"]["p99_ns"] / 1e6, "errors": res["latency"]["errors"],
        "body_checked": res["latency"].get("body_checked", 0), "body_mismatch": res["latency"].get("body_mismatch", 0),
-       "hystrix_events": events,
+       "hystrix_events": events, "feign_log": a.feign_log,
        # cores kept busy (warmup included) and CPU µs per request at the measured rate
        "cpus_busy": {k: round(v, 2) for k, v in busy.items()},
        "cpu_us_per_req": {k: round(v / res["rps"] * 1e6, 2) for k, v in busy.items()},

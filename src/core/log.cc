@@ -2,7 +2,10 @@
 
 #include <unistd.h>
 
+#include <algorithm>
+#include <chrono>
 #include <cstdio>
+#include <cstring>
 #include <ctime>
 
 #include "core/clock.h"
@@ -10,7 +13,6 @@
 namespace hola {
 
 namespace {
-constexpr size_t kMaxQueued = 65536;  // beyond this, lines are dropped and counted
 const char* level_name(LogLevel l) {
   switch (l) {
     case LogLevel::kDebug: return "DEBUG";
@@ -26,6 +28,42 @@ Logger& Logger::instance() {
   static Logger* l = new Logger();  // intentionally leaked: usable during static destruction
   return *l;
 }
+
+// A single-producer / single-consumer byte ring of length-prefixed lines. head and tail
+// count bytes ever written / consumed; the producer publishes a line by advancing head.
+struct Logger::Ring {
+  static constexpr size_t kSize = 128 * 1024;  // power of two
+  alignas(64) std::atomic<uint64_t> head{0};
+  alignas(64) std::atomic<uint64_t> tail{0};
+  std::atomic<bool> orphan{false};  // its thread has exited: free for the next new thread
+  char buf[kSize];
+
+  void put(uint64_t pos, const void* p, size_t n) {
+    const size_t at = size_t(pos & (kSize - 1)), first = std::min(n, kSize - at);
+    memcpy(buf + at, p, first);
+    memcpy(buf, static_cast<const char*>(p) + first, n - first);
+  }
+  void get(uint64_t pos, void* p, size_t n) const {
+    const size_t at = size_t(pos & (kSize - 1)), first = std::min(n, kSize - at);
+    memcpy(p, buf + at, first);
+    memcpy(static_cast<char*>(p) + first, buf, n - first);
+  }
+};
+
+namespace {
+struct ThreadRing {
+  Logger::Ring* r = nullptr;
+  ~ThreadRing() {
+    if (r) r->orphan.store(true, std::memory_order_release);
+  }
+};
+thread_local ThreadRing tls_ring;
+
+// Bounded waits against the system clock: libstdc++ implements steady-clock waits with
+// pthread_cond_clockwait, which the toolchain's ThreadSanitizer does not intercept.
+constexpr auto kPoll = std::chrono::milliseconds(1);
+constexpr int kIdlePolls = 10;  // empty polls in a row before the writer sleeps until woken
+}  // namespace
 
 Logger::Logger() : th_([this] { run(); }) {}
 
@@ -74,49 +112,131 @@ void Logger::raw(const char* fmt, ...) {
   enqueue(line, size_t(n));
 }
 
+Logger::Ring* Logger::ring_for_this_thread() {
+  if (tls_ring.r) return tls_ring.r;
+  std::lock_guard<std::mutex> g(reg_mu_);
+  const int n = nrings_.load(std::memory_order_relaxed);
+  for (int i = 0; i < n; ++i) {
+    Ring* r = rings_[i].load(std::memory_order_relaxed);
+    // A ring whose thread has exited is reused once the writer has emptied it.
+    if (r->orphan.load(std::memory_order_acquire) &&
+        r->head.load(std::memory_order_acquire) == r->tail.load(std::memory_order_acquire)) {
+      r->orphan.store(false, std::memory_order_relaxed);
+      return tls_ring.r = r;
+    }
+  }
+  if (n == kMaxRings) return nullptr;
+  Ring* r = new Ring();
+  rings_[n].store(r, std::memory_order_release);
+  nrings_.store(n + 1, std::memory_order_release);
+  return tls_ring.r = r;
+}
+
 void Logger::enqueue(const char* line, size_t n) {
+  Ring* r = ring_for_this_thread();
+  const uint32_t len = uint32_t(n);
+  const uint64_t h = r ? r->head.load(std::memory_order_relaxed) : 0;
+  if (!r || Ring::kSize - (h - r->tail.load(std::memory_order_acquire)) < sizeof len + n) {
+    dropped_.fetch_add(1, std::memory_order_relaxed);
+    return;
+  }
+  r->put(h, &len, sizeof len);
+  r->put(h + sizeof len, line, n);
+  // seq_cst pairs with the writer's store of sleeping_ before its last look at the rings:
+  // either it sees this line, or this thread sees it asleep and wakes it.
+  r->head.store(h + sizeof len + n, std::memory_order_seq_cst);
+  if (sleeping_.load(std::memory_order_seq_cst)) wake();
+}
+
+void Logger::wake() {
   {
     std::lock_guard<std::mutex> g(mu_);
-    if (q_.size() >= kMaxQueued) {
-      dropped_.fetch_add(1, std::memory_order_relaxed);
-      return;
-    }
-    q_.emplace_back(line, n);
-    ++enqueued_;
+    sleeping_.store(false, std::memory_order_seq_cst);
   }
   cv_.notify_one();
 }
 
+bool Logger::rings_empty() const {
+  const int n = nrings_.load(std::memory_order_acquire);
+  for (int i = 0; i < n; ++i) {
+    const Ring* r = rings_[i].load(std::memory_order_acquire);
+    if (r->head.load(std::memory_order_seq_cst) != r->tail.load(std::memory_order_relaxed)) return false;
+  }
+  return true;
+}
+
+size_t Logger::drain(std::string* out) {
+  size_t lines = 0;
+  const int n = nrings_.load(std::memory_order_acquire);
+  for (int i = 0; i < n; ++i) {
+    Ring* r = rings_[i].load(std::memory_order_acquire);
+    uint64_t t = r->tail.load(std::memory_order_relaxed);
+    const uint64_t h = r->head.load(std::memory_order_acquire);
+    if (t == h) continue;
+    while (t < h) {
+      uint32_t len;
+      r->get(t, &len, sizeof len);
+      const size_t old = out->size();
+      out->resize(old + len);
+      r->get(t + sizeof len, &(*out)[old], len);
+      t += sizeof len + len;
+      ++lines;
+    }
+    r->tail.store(t, std::memory_order_release);
+  }
+  return lines;
+}
+
 void Logger::flush() {
   std::unique_lock<std::mutex> g(mu_);
-  uint64_t target = enqueued_;
-  flushed_.wait(g, [&] { return written_ >= target || stop_; });
+  const uint64_t ticket = ++flush_req_;
+  cv_.notify_one();
+  flushed_.wait(g, [&] { return flush_done_ >= ticket || stop_; });
 }
 
 void Logger::run() {
-  std::deque<std::string> batch;
+  std::string out;
+  int idle = 0;
   for (;;) {
+    uint64_t req;
+    bool stop;
     {
-      std::unique_lock<std::mutex> g(mu_);
-      cv_.wait(g, [&] { return stop_ || !q_.empty(); });
-      if (q_.empty() && stop_) break;
-      batch.swap(q_);
+      std::lock_guard<std::mutex> g(mu_);
+      req = flush_req_;
+      stop = stop_;
     }
-    std::string out;
-    for (auto& s : batch) out += s;
+    out.clear();
+    const size_t got = drain(&out);
     size_t off = 0;
     while (off < out.size()) {
       ssize_t w = ::write(2, out.data() + off, out.size() - off);
       if (w <= 0) break;
       off += size_t(w);
     }
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      written_ += batch.size();
+    std::unique_lock<std::mutex> g(mu_);
+    if (flush_done_ < req) {
+      flush_done_ = req;  // every line logged before those flush() calls is written
+      flushed_.notify_all();
     }
-    batch.clear();
-    flushed_.notify_all();
+    if (stop && got == 0) break;
+    if (stop_ || flush_req_ != flush_done_) continue;
+    auto woken = [&] { return stop_ || flush_req_ != flush_done_; };
+    if (got) idle = 0;
+    if (got || ++idle < kIdlePolls) {
+      cv_.wait_until(g, std::chrono::system_clock::now() + kPoll, woken);
+      continue;
+    }
+    sleeping_.store(true, std::memory_order_seq_cst);
+    if (!rings_empty()) {
+      sleeping_.store(false, std::memory_order_relaxed);
+      continue;
+    }
+    cv_.wait(g, [&] { return !sleeping_.load(std::memory_order_relaxed) || woken(); });
+    sleeping_.store(false, std::memory_order_relaxed);
+    idle = 0;
   }
+  std::lock_guard<std::mutex> g(mu_);
+  flush_done_ = flush_req_;
   flushed_.notify_all();
 }
 

@@ -1,5 +1,7 @@
 #include "metrics/prometheus.h"
 
+#include "core/log.h"
+
 #include <dirent.h>
 #include <sys/resource.h>
 #include <unistd.h>
@@ -165,6 +167,8 @@ std::string Prometheus::render(http::Server* server) const {
          std::to_string(s.pool_queue_size) + "\n";
   }
   process_metrics(&o);
+  o += "# TYPE hola_log_lines_dropped_total counter\nhola_log_lines_dropped_total " +
+       std::to_string(Logger::instance().dropped()) + "\n";
   if (reloads_) o += "# TYPE hola_config_reloads_total counter\nhola_config_reloads_total " + std::to_string(reloads_()) + "\n";
   if (feign_retries_ && transport_retries_) {
     o += "# TYPE hola_aloha_retries_total counter\nhola_aloha_retries_total{kind=\"feign\"} " +

@@ -2,6 +2,7 @@
 // the exact code the server runs (properties parser, String.format subset, B3 codec, Accept
 // negotiation, HTTP parser, JSON codec, Hystrix state machine on a fake clock, span encoding).
 #include <pybind11/pybind11.h>
+
 #include <pybind11/stl.h>
 
 #include <atomic>
@@ -25,6 +26,7 @@
 #include "core/histogram.h"
 #include "core/loop.h"
 #include "core/clock.h"
+#include "core/log.h"
 
 namespace py = pybind11;
 using namespace hola;
@@ -321,6 +323,23 @@ std::pair<size_t, size_t> span_ring(size_t capacity, size_t pushes) {
   return {ok, out.size()};
 }
 
+// Logs `lines` raw lines "<tag> <thread> <i>" from each of `threads` threads (each a new
+// thread, so rings of exited threads are reused across calls), then flushes; returns the
+// lines dropped meanwhile (ring full).
+uint64_t log_stress(int threads, int lines, const std::string& tag) {
+  py::gil_scoped_release nogil;
+  Logger& l = Logger::instance();
+  const uint64_t d0 = l.dropped();
+  std::vector<std::thread> ts;
+  for (int t = 0; t < threads; ++t)
+    ts.emplace_back([&l, t, lines, &tag] {
+      for (int i = 0; i < lines; ++i) l.raw("%s %d %d", tag.c_str(), t, i);
+    });
+  for (auto& t : ts) t.join();
+  l.flush();
+  return l.dropped() - d0;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_native, m) {
@@ -386,6 +405,7 @@ PYBIND11_MODULE(_native, m) {
   }, py::arg("attempt"), py::arg("policy") = "default");
   m.def("loop_timer_order", &loop_timer_order, py::arg("delays"), py::arg("cancel") = std::vector<int>{});
   m.def("span_ring", &span_ring);
+  m.def("log_stress", &log_stress, py::arg("threads"), py::arg("lines"), py::arg("tag") = "stress");
   m.def("hystrix_stress", &hystrix_stress, py::arg("threads"), py::arg("iters"), py::arg("pool") = 10,
         py::arg("fail_every") = 0, py::arg("volume") = 20);
   py::class_<PyCommand>(m, "HystrixCommand")

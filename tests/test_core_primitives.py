@@ -63,3 +63,31 @@ def test_feign_retryer_default_backoff(native):
     assert native.feign_backoff_ms(9, "100,1000,12")[0] == 1000
     assert native.feign_backoff_ms(1, "off")[1] == 1
     assert native.feign_backoff_ms(1, "bogus") is None
+
+
+def test_logger_per_thread_rings_keep_every_line_in_order(native, capfd):
+    """Lines from many threads at once all reach stderr, each thread's in its own order, and
+    flush() returns only after they are written. Threads exit between the two calls, so the
+    second reuses their rings."""
+    for tag in ("first", "second"):
+        dropped = native.log_stress(8, 2000, tag)
+        err = capfd.readouterr().err
+        assert dropped == 0
+        seen = {}
+        for line in err.splitlines():
+            parts = line.split()
+            if len(parts) == 3 and parts[0] == tag:
+                t, i = int(parts[1]), int(parts[2])
+                assert i == seen.get(t, -1) + 1, (t, i)
+                seen[t] = i
+        assert seen == {t: 1999 for t in range(8)}
+
+
+def test_logger_drops_and_counts_when_a_ring_overflows(native, capfd):
+    """One thread logging far faster than the writer drains: the excess is dropped and
+    counted instead of growing memory, and what is written stays in order."""
+    dropped = native.log_stress(1, 200000, "burst")
+    err = capfd.readouterr().err
+    got = [int(l.split()[2]) for l in err.splitlines() if l.startswith("burst 0 ")]
+    assert len(got) + dropped == 200000
+    assert got == sorted(got)
