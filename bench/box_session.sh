@@ -14,6 +14,7 @@
 #   pairmode           N = 1, 2, 4 with --smt pair (the 8-GPU node's per-replica layout shape)
 #   latency            BASELINE config 2 (1 connection) and the open-loop latency curve
 #   chain              two-hop chaining bench (loadgen -> hola A -> hola B)
+#   chainab [REPS]     chaining with Feign BASIC logging on/off, this server vs. PREV_BIN
 #   tracing            headline without a collector, with the native Zipkin sink (default 1000-span
 #                      export budget, and unbounded), and with tracing off
 #   soak MINUTES       mixed-load soak sampling RSS and FDs
@@ -94,6 +95,21 @@ latency)
   ;;
 chain)
   timeout -k 10 120 python bench/chain_bench.py --duration 10 --out "$OUT/chain.json" > "$OUT/chain.log" 2>&1
+  ;;
+chainab)
+  # chaining with A's Feign BASIC logging on (the server default) and off, this tree's server
+  # against PREV_BIN (a server built from an earlier commit), REPS interleaved rounds
+  REPS=${1:-3}; PREV=${PREV_BIN:-build/prev/hola}
+  for rep in $(seq 1 "$REPS"); do
+    for v in "new_basic|basic|" "prev_basic|basic|$PREV" "new_none|none|"; do
+      label=${v%%|*}; rest=${v#*|}; log=${rest%%|*}; exe=${rest#*|}
+      timeout -k 10 120 python bench/chain_bench.py --duration 8 --feign-log "$log" ${exe:+--exe-a "$exe"} \
+        --out "$OUT/${label}_${rep}.json" > "$OUT/${label}_${rep}.log" 2>&1 || exit 1
+      python3 -c "import json; d=json.load(open('$OUT/${label}_${rep}.json')); print('$label', $rep, d['rps'], d['p50_ms'], d['p99_ms'], d['cpu_us_per_req']['A'], d['user_share']['A'])" \
+        >> "$OUT/summary.txt"
+    done
+  done
+  cat "$OUT/summary.txt"
   ;;
 tracing)
   timeout -k 10 300 python bench.py --steps 15 --warmup 3 --c1-seconds 0 > "$OUT/no_collector.json" 2>> "$OUT/err.log" &&

@@ -62,6 +62,9 @@ with HolaProcess(args=["--aloha-url", "http://127.0.0.1:1/", "--feign-log", "non
     with HolaProcess(args=["--aloha-url", f"http://127.0.0.1:{b.port}/", "--aloha-path", "api/hola-chaining",
                            "--feign-log", a.feign_log, "--hystrix-pool-size", str(a.pool)],
                      env={"HOSTNAME": "A"}, threads=len(cores[0]), cpu_list=format_cpu_list(cores[0]),
+                     # BASIC logging writes ~150 bytes per call: at 1.5 M calls/s that would be
+                     # gigabytes of log file per run, so A's stderr goes to /dev/null
+                     stderr_path=os.devnull if a.feign_log == "basic" else None,
                      exe=Path(a.exe_a) if a.exe_a else None) as s:
         st, _, body = s.get("/api/hola-chaining")
         assert st == 200, body
