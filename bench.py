@@ -77,6 +77,9 @@ def parse_args():
                          "default 1000, Brave 3's collector queue; 0 = bounded only by the rings)")
     ap.add_argument("--profile-dir", default="",
                     help="run replicas with --profile and write their stage histograms here")
+    ap.add_argument("--cpu-profile-dir", default="",
+                    help="run replicas with --cpu-profile (sampled call stacks of every server thread, "
+                         "bench/cpuprof_report.py symbolises them) and write them here")
     ap.add_argument("--plain-dealing", action="store_true",
                     help="deal every rank's connections (i + rank) %% N over all replicas from its own "
                          "cores, instead of giving each load-generator thread the replicas of its L3 "
@@ -197,6 +200,9 @@ def main() -> int:
         os.makedirs(a.profile_dir, exist_ok=True)
         args += ["--profile", "--profile-out", os.path.join(os.path.abspath(a.profile_dir),
                                                             f"server_profile_rank{rank}.json")]
+    if a.cpu_profile_dir:
+        os.makedirs(a.cpu_profile_dir, exist_ok=True)
+        args += ["--cpu-profile", os.path.join(os.path.abspath(a.cpu_profile_dir), f"server_cpu_rank{rank}.prof")]
     server = HolaProcess(args=args, env=env, port=port, threads=s_threads, cpu_list=format_cpu_list(server_cpus),
                          log_level="warn")
     server.start()

@@ -15,6 +15,7 @@
 #   latency            BASELINE config 2 (1 connection) and the open-loop latency curve
 #   chain              two-hop chaining bench (loadgen -> hola A -> hola B)
 #   chainab [REPS]     chaining with Feign BASIC logging on/off, this server vs. PREV_BIN
+#   cpuprof            sampled CPU profiles (hola --cpu-profile) of the headline and of chaining
 #   tracing            headline without a collector, with the native Zipkin sink (default 1000-span
 #                      export budget, and unbounded), and with tracing off
 #   soak MINUTES       mixed-load soak sampling RSS and FDs
@@ -110,6 +111,18 @@ chainab)
     done
   done
   cat "$OUT/summary.txt"
+  ;;
+cpuprof)
+  # sampled call stacks of the server's threads: the headline (1 replica, 64 connections) and
+  # the chaining path with Feign BASIC logging, each symbolised on the box
+  timeout -k 10 200 python bench.py --steps 10 --warmup 2 --c1-seconds 0 --cpu-profile-dir "$OUT/headline" \
+    > "$OUT/headline.json" 2>> "$OUT/err.log" &&
+  python bench/cpuprof_report.py "$OUT/headline/server_cpu_rank0.prof" --top 40 --json "$OUT/headline_report.json" \
+    > "$OUT/headline_report.txt" 2>> "$OUT/err.log" &&
+  timeout -k 10 120 python bench/chain_bench.py --duration 8 --feign-log basic --cpu-profile "$OUT/chain_a.prof" \
+    --out "$OUT/chain.json" > "$OUT/chain.log" 2>&1 &&
+  python bench/cpuprof_report.py "$OUT/chain_a.prof" --top 40 --json "$OUT/chain_report.json" \
+    > "$OUT/chain_report.txt" 2>> "$OUT/err.log"
   ;;
 tracing)
   timeout -k 10 300 python bench.py --steps 15 --warmup 3 --c1-seconds 0 > "$OUT/no_collector.json" 2>> "$OUT/err.log" &&

@@ -30,6 +30,8 @@ ap.add_argument("--pool", type=int, default=128, help="hystrix thread-pool (bulk
 ap.add_argument("--feign-log", default="none", choices=("none", "basic"),
                 help="A's Feign logging; basic = the reference's ErrorLogger at Level.BASIC (two stderr "
                      "lines per call, the server's default)")
+ap.add_argument("--cpu-profile", default="",
+                help="run A with --cpu-profile here (sampled call stacks; bench/cpuprof_report.py reads it)")
 ap.add_argument("--out", default="")
 ap.add_argument("--exe-a", default="", help="alternative hola binary for A (A/B runs)")
 a = ap.parse_args()
@@ -60,7 +62,8 @@ with HolaProcess(args=["--aloha-url", "http://127.0.0.1:1/", "--feign-log", "non
                        "--feign-retry", "off", "--log-level", "warn"], env={"HOSTNAME": "B"}, threads=len(cores[1]),
                  cpu_list=format_cpu_list(cores[1])) as b:
     with HolaProcess(args=["--aloha-url", f"http://127.0.0.1:{b.port}/", "--aloha-path", "api/hola-chaining",
-                           "--feign-log", a.feign_log, "--hystrix-pool-size", str(a.pool)],
+                           "--feign-log", a.feign_log, "--hystrix-pool-size", str(a.pool)]
+                          + (["--cpu-profile", os.path.abspath(a.cpu_profile)] if a.cpu_profile else []),
                      env={"HOSTNAME": "A"}, threads=len(cores[0]), cpu_list=format_cpu_list(cores[0]),
                      # BASIC logging writes ~150 bytes per call: at 1.5 M calls/s that would be
                      # gigabytes of log file per run, so A's stderr goes to /dev/null

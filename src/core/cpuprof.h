@@ -1,0 +1,26 @@
+// Sampling CPU profiler for the server's own threads (`hola --cpu-profile FILE`).
+//
+// The GPU boxes have no perf and rocprofv3 sees no kernels here (the service dispatches none),
+// so this is the host-side profile: each registered thread arms a timer on its own CPU-time
+// clock (timer_create(CLOCK_THREAD_CPUTIME_ID) delivering SIGPROF to that thread), and the
+// handler records a short call stack (_Unwind_Backtrace, which walks .eh_frame, so frames of
+// libc and of code built without frame pointers are found too) into a preallocated buffer.
+// Time spent inside a syscall is charged to the libc wrapper the thread returns to (send,
+// recv, epoll_wait), so the profile also splits kernel time by call. At exit the samples and
+// the executable mappings are written as text; `bench/cpuprof_report.py` symbolises them.
+#pragma once
+#include <string>
+
+namespace hola::cpuprof {
+
+// Allocates the sample buffer and installs the SIGPROF handler; `hz` samples per second of
+// each thread's CPU time. Returns false (and profiles nothing) on failure.
+bool start(const std::string& path, int hz = 4000);
+// Arms the calling thread's CPU-time timer (a no-op unless start() succeeded).
+void register_thread();
+// Disarms the calling thread's timer.
+void unregister_thread();
+// Disarms every timer and writes the profile file. Call once, after the threads have stopped.
+bool write();
+
+}  // namespace hola::cpuprof

@@ -1,5 +1,6 @@
 #include "core/log.h"
 
+#include <pthread.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -9,6 +10,7 @@
 #include <ctime>
 
 #include "core/clock.h"
+#include "core/cpuprof.h"
 
 namespace hola {
 
@@ -65,7 +67,7 @@ constexpr auto kPoll = std::chrono::milliseconds(1);
 constexpr int kIdlePolls = 10;  // empty polls in a row before the writer sleeps until woken
 }  // namespace
 
-Logger::Logger() : th_([this] { run(); }) {}
+Logger::Logger() : th_([this] { run(); }) { pthread_setname_np(th_.native_handle(), "hola-log"); }
 
 Logger::~Logger() {
   {
@@ -198,6 +200,7 @@ void Logger::run() {
   std::string out;
   int idle = 0;
   for (;;) {
+    cpuprof::register_thread();  // no-op once armed (or when not profiling)
     uint64_t req;
     bool stop;
     {

@@ -2,6 +2,7 @@
 
 #include <errno.h>
 #include <netinet/in.h>
+#include <pthread.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -12,6 +13,7 @@
 
 #include "core/affinity.h"
 #include "core/clock.h"
+#include "core/cpuprof.h"
 #include "core/log.h"
 #include "core/net.h"
 
@@ -79,10 +81,15 @@ void Connection::on_readable(bool peer_closed) {
       if (n < ssize_t(sizeof buf)) return;
     }
   }
+  if (parked_) {
+    read_pending_ = true;
+    peer_closed_pending_ |= peer_closed;
+    return;
+  }
   StageProfile* prof = worker_->profile();
+  bool more = false;
   while (!parked_ && reading_ && !streaming_ && !closed_) {
     int64_t t0 = prof ? mono_ns() : 0;
-    bool more;
     if (in_.empty()) {
       char* buf = worker_->scratch();
       const size_t cap = worker_->scratch_size();
@@ -125,6 +132,11 @@ void Connection::on_readable(bool peer_closed) {
       if (consumed < buf.size()) in_.assign(buf, consumed, std::string::npos);
     }
     if (!more) break;
+  }
+  if (parked_ && more) {
+    // parked with input possibly still in the socket: no new edge will announce it
+    read_pending_ = true;
+    peer_closed_pending_ |= peer_closed;
   }
   if (!closed_) flush();
 }
@@ -202,7 +214,7 @@ bool Connection::process(const char* data, size_t len, size_t* consumed) {
   if (StageProfile* prof = worker_->profile(); prof && handled) prof->batch.add(handled);
   *consumed = off;
   if (closed_) return false;
-  if (parked_ || streaming_) update_interest();
+  if (streaming_ || (parked_ && !worker_->server().options().edge_triggered)) update_interest();
   return true;
 }
 
@@ -236,7 +248,14 @@ void Connection::complete(std::string_view response, bool keep_alive) {
     if (consumed < buf.size()) in_.assign(buf, consumed, std::string::npos);
   }
   flush();
-  if (!closed_) update_interest();
+  if (closed_) return;
+  if (!worker_->server().options().edge_triggered) {
+    update_interest();  // level-triggered: input interest was dropped while parked
+  } else if (read_pending_ && !parked_) {
+    const bool pc = peer_closed_pending_;
+    read_pending_ = peer_closed_pending_ = false;
+    on_readable(pc);
+  }
 }
 
 void Connection::start_streaming(std::function<void()> on_close) {
@@ -293,7 +312,9 @@ void Connection::update_interest() {
   if (closed_) return;
   uint32_t ev = worker_->server().options().edge_triggered ? uint32_t(EPOLLET) : 0u;
   if (streaming_) ev |= EPOLLIN | EPOLLRDHUP;
-  else if (reading_ && !parked_) ev |= EPOLLIN | EPOLLRDHUP;
+  // level-triggered input interest is dropped while a request is parked, edge-triggered
+  // interest is kept (see read_pending_)
+  else if (reading_ && (!parked_ || (ev & EPOLLET))) ev |= EPOLLIN | EPOLLRDHUP;
   if (want_write_) ev |= EPOLLOUT;
   worker_->loop().mod(fd_, ev, this);
 }
@@ -605,6 +626,10 @@ void Server::start() {
         int cpu = opts_.cpus[size_t(wp->index()) % opts_.cpus.size()];
         if (!pin_current_thread(cpu)) LOG_WARN("worker %d: could not pin to cpu %d", wp->index(), cpu);
       }
+      char name[16];
+      snprintf(name, sizeof name, "hola-w%d", wp->index());
+      pthread_setname_np(pthread_self(), name);
+      cpuprof::register_thread();
       wp->scratch_.assign(opts_.read_chunk, 0);
       handler_->on_worker_start(*wp);
       if (opts_.idle_timeout_ms > 0) {
@@ -621,6 +646,7 @@ void Server::start() {
       }
       wp->loop().run();
       handler_->on_worker_stop(*wp);
+      cpuprof::unregister_thread();
     });
   }
 }

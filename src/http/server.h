@@ -114,6 +114,11 @@ class Connection final : public EventLoop::Handler {
   bool reading_ = true;
   bool in_process_ = false;  // inside process(): batch writes instead of sending eagerly
   bool continue_sent_ = false;  // "100 Continue" already sent for the pending request
+  // Edge-triggered sockets stay registered for input while a request is parked (no
+  // epoll_ctl per parked request): an edge that arrives meanwhile, or input left unread when
+  // the request parked, is remembered here and read when the response completes.
+  bool read_pending_ = false;
+  bool peer_closed_pending_ = false;
   int holds_ = 0;
   int64_t last_active_ms_ = 0;
   std::function<void()> on_close_;

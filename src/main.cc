@@ -21,6 +21,7 @@
 #include "config/manager.h"
 #include "config/resolver.h"
 #include "core/affinity.h"
+#include "core/cpuprof.h"
 #include "core/log.h"
 #include "core/net.h"
 #include "http/server.h"
@@ -82,6 +83,9 @@ void usage() {
           "                           one CPU per worker (e.g. a kubelet static-CPU-manager cpuset)\n"
           "  --profile                per-stage latency histograms (accept/recv/parse/handle/send), dumped at exit\n"
           "  --profile-out PATH       write the --profile JSON here (default: stderr)\n"
+          "  --cpu-profile PATH       sample the server's threads' call stacks on their CPU time and write\n"
+          "                           them here at exit (bench/cpuprof_report.py symbolises them)\n"
+          "  --cpu-profile-hz N       samples per CPU-second of each thread (default 1000)\n"
           "  --log-level L            debug|info|warn|error|off (default info)\n"
           "  --no-metrics             disable the /metrics endpoint\n");
 }
@@ -111,7 +115,8 @@ int main(int argc, char** argv) {
   if (hn) ao.hostname = hn;  // HolaResource.java:57 getOrDefault("HOSTNAME", "unknown")
   int threads = 0, drain_ms = 5000, stream_max = -1;
   int64_t stream_stall_ms = 30000;
-  std::string cpu_list, port_file, profile_out;
+  std::string cpu_list, port_file, profile_out, cpu_profile;
+  int cpu_profile_hz = 1000;
   bool auto_pin = true;
   bool no_tracing = false;
   bool port_flag = false, host_flag = false;
@@ -198,6 +203,8 @@ int main(int argc, char** argv) {
     else if (a == "--idle-timeout-ms") so.idle_timeout_ms = atoi(val("--idle-timeout-ms").c_str());
     else if (a == "--max-connections") so.max_connections = size_t(atol(val("--max-connections").c_str()));
     else if (a == "--profile-out") profile_out = val("--profile-out");
+    else if (a == "--cpu-profile") cpu_profile = val("--cpu-profile");
+    else if (a == "--cpu-profile-hz") cpu_profile_hz = atoi(val("--cpu-profile-hz").c_str());
     else if (a == "--no-metrics") ao.enable_metrics_endpoint = false;
     else if (a == "--log-level") {
       LogLevel l;
@@ -335,6 +342,10 @@ int main(int argc, char** argv) {
     chainer.update_settings(hystrix_settings(s.hystrix));
   });
 
+  if (!cpu_profile.empty() && !cpuprof::start(cpu_profile, cpu_profile_hz)) {
+    fprintf(stderr, "hola: cannot start the CPU profiler\n");
+    return 1;
+  }
   chainer.start();
   tracer.start();
   server.start();
@@ -375,6 +386,7 @@ int main(int argc, char** argv) {
   cfg.stop();
   chainer.stop();
   tracer.stop();
+  if (!cpu_profile.empty() && !cpuprof::write()) LOG_WARN("could not write the CPU profile to %s", cpu_profile.c_str());
   LOG_INFO("shutdown complete (%llu requests served)", (unsigned long long)server.total_requests());
   Logger::instance().flush();
   return 0;

@@ -15,6 +15,7 @@
 #include "client/http_client.h"
 #include "client/url.h"
 #include "core/clock.h"
+#include "core/cpuprof.h"
 #include "core/log.h"
 #include "http/parser.h"
 #include "json/json.h"
@@ -380,11 +381,13 @@ void Tracer::run() {
   // batches are POSTed every flush_interval_ms, or earlier when large. The wait is a poll()
   // on an eventfd rather than a timed condition variable (gcc 11's TSan does not intercept
   // pthread_cond_clockwait, which turns timed cv waits into false race reports).
+  cpuprof::register_thread();
   int64_t last_post = mono_ms();
   for (;;) {
     pollfd p{stopfd_, POLLIN, 0};
     ::poll(&p, 1, o_.drain_interval_ms);
     if (stopping_.load(std::memory_order_acquire)) break;
+    cpuprof::register_thread();  // no-op once armed (or when not profiling)
     std::lock_guard<std::mutex> f(flush_mu_);
     drain_rings();
     int64_t now = mono_ms();

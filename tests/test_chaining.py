@@ -609,3 +609,42 @@ def test_idle_connection_closed_by_aloha_is_dropped(hola, aloha):
         assert chain(s)[1:] == ["Aloha mai aloha-1", "Bonjour de bonjour-1"]
         time.sleep(0.05)
     assert _events(s).get("SUCCESS") == 5
+
+
+@pytest.mark.parametrize("epoll", ["et", "lt"])
+def test_input_arriving_while_a_request_is_parked(hola, aloha, epoll):
+    """A parked /api/hola-chaining keeps its connection's input registered (edge-triggered)
+    or not (level-triggered). Either way, requests pipelined behind it, requests sent while
+    it waits, and a FIN sent while it waits are all handled, in order, once it completes."""
+    aloha.set_mode("slow", delay_s=0.2)
+    args = ["--aloha-url", aloha.url, "--no-tracing", "--feign-log", "none"] + (["--epoll-lt"] if epoll == "lt" else [])
+    s = hola(args=args, env={"HOSTNAME": "h"}, threads=1)
+    chain_req = b"GET /api/hola-chaining HTTP/1.1\r\nHost: x\r\n\r\n"
+    hola_req = b"GET /api/hola HTTP/1.1\r\nHost: x\r\n\r\n"
+
+    def read_until_closed(c):
+        out = b""
+        c.settimeout(5)
+        while True:
+            b = c.recv(65536)
+            if not b:
+                return out
+            out += b
+
+    # 1) pipelined behind the parked request, in one write
+    with socket.create_connection(("127.0.0.1", s.port)) as c:
+        c.sendall(chain_req + hola_req + chain_req.replace(b"\r\n\r\n", b"\r\nConnection: close\r\n\r\n"))
+        out = read_until_closed(c)
+    assert out.count(b"HTTP/1.1 200 OK") == 3
+    first, mid, last = out.find(b"Aloha mai"), out.find(b"\r\n\r\nHola de h"), out.rfind(b"Aloha mai")
+    assert 0 < first < mid < last, out
+    # 2) a second request and then a FIN, both sent while the first is parked
+    with socket.create_connection(("127.0.0.1", s.port)) as c:
+        c.sendall(chain_req)
+        time.sleep(0.05)
+        c.sendall(hola_req)
+        time.sleep(0.05)
+        c.shutdown(socket.SHUT_WR)
+        out = read_until_closed(c)
+    assert out.count(b"HTTP/1.1 200 OK") == 2
+    assert 0 < out.find(b"Aloha mai") < out.rfind(b"Hola de h"), out

@@ -1,0 +1,33 @@
+"""`hola --cpu-profile`: per-thread CPU-time sampling of the server, symbolised by
+bench/cpuprof_report.py (the host-side profile on boxes without perf)."""
+import subprocess
+import sys
+from pathlib import Path
+
+from hola_amd.parallel.loadgen import run_duration
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def test_cpu_profile_samples_workers_under_load(hola, tmp_path):
+    prof = tmp_path / "cpu.prof"
+    s = hola(args=["--cpu-profile", str(prof), "--cpu-profile-hz", "2000"], threads=2)
+    res = run_duration([("127.0.0.1", s.port)], 8, 2, 1.5, 0.2)
+    assert res["latency"]["errors"] == 0
+    assert s.stop() == 0
+    text = prof.read_text()
+    assert "period_ns 500000" in text
+    assert " hola-w0\n" in text and " hola-log\n" in text and "map " in text
+    out = subprocess.run([sys.executable, str(ROOT / "bench/cpuprof_report.py"), str(prof), "--top", "40",
+                          "--json", str(tmp_path / "rep.json")], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    import json
+    rep = json.loads((tmp_path / "rep.json").read_text())
+    # the workers spent a good part of 1.5 s each on the CPU: 2 samples per CPU-ms
+    assert rep["samples"] > 100, rep["samples"]
+    assert set(rep["threads"]) >= {"hola-w0", "hola-w1"}
+    names = [fn for _, fn in rep["total"]]
+    # the stacks reach from the syscall wrappers up into the server's own code
+    assert any("send" in fn for fn in names), names
+    assert any("hola::EventLoop::run" in fn for fn in names), names
+    assert any("hola::http::Connection::" in fn for fn in names), names
