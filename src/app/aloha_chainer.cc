@@ -1,6 +1,8 @@
 #include "app/aloha_chainer.h"
 
 #include <algorithm>
+#include <charconv>
+#include <cstring>
 #include <cmath>
 #include <cstdio>
 
@@ -61,6 +63,7 @@ AlohaChainer::AlohaChainer(AlohaOptions o, resilience::Settings s, int num_worke
   req_path_ = target_.base_path + o_.path;
   // feign.Logger.methodTag(): '[' + configKey up to '(' + "] ".
   log_tag_ = "[" + o_.config_key.substr(0, o_.config_key.find('(')) + "] ";
+  log_request_line_ = log_tag_ + "---> GET " + full_url_ + " HTTP/1.1";
 }
 
 AlohaChainer::~AlohaChainer() { stop(); }
@@ -291,7 +294,7 @@ void AlohaChainer::execute(http::Worker& w, WorkerCalls& wc, uint32_t slot, uint
   }
   c.start_us = wall_us();
   c.attempt_ms = clock_.now_ms();
-  if (o_.feign_log_basic) Logger::instance().raw("%s---> GET %s HTTP/1.1", log_tag_.c_str(), full_url_.c_str());
+  if (o_.feign_log_basic) Logger::instance().raw_line(log_request_line_);
   http::Worker* wp = &w;
   const uint64_t id = pool(w).get(req_path_, headers, [this, wp, &wc, slot, gen](client::ClientResult&& r) {
     on_response(*wp, wc, slot, gen, std::move(r));
@@ -309,10 +312,30 @@ void AlohaChainer::on_response(http::Worker& w, WorkerCalls& wc, uint32_t slot, 
   const int64_t now = clock_.now_ms();
   if (o_.feign_log_basic) {
     // Feign Logger BASIC: logAndRebufferResponse / logIOException (r.error is "Class: msg").
-    if (r.ok)
-      Logger::instance().raw("%s<--- HTTP/1.1 %d%s%s (%lldms)", log_tag_.c_str(), r.status,
-                             r.reason.empty() ? "" : " ", r.reason.c_str(), (long long)(now - c.attempt_ms));
-    else
+    if (r.ok) {
+      // "<tag><--- HTTP/1.1 <status>[ <reason>] (<N>ms)", built without printf (every call)
+      char line[512];
+      char* p = line;
+      char* const end = line + sizeof line - 32;  // room for the status and the timing
+      auto put = [&](std::string_view v) {
+        const size_t k = p < end ? std::min(v.size(), size_t(end - p)) : 0;
+        memcpy(p, v.data(), k);
+        p += k;
+      };
+      put(log_tag_);
+      put("<--- HTTP/1.1 ");
+      p = std::to_chars(p, end + 32, r.status).ptr;
+      if (!r.reason.empty()) {
+        put(" ");
+        put(r.reason);
+      }
+      put(" (");
+      p = std::to_chars(p, end + 32, (long long)(now - c.attempt_ms)).ptr;
+      *p++ = 'm';
+      *p++ = 's';
+      *p++ = ')';
+      Logger::instance().raw_line(std::string_view(line, size_t(p - line)));
+    } else
       Logger::instance().raw("%s<--- ERROR %s (%lldms)", log_tag_.c_str(), r.error.c_str(),
                              (long long)(now - c.attempt_ms));
   }

@@ -112,6 +112,7 @@ class AlohaChainer final : public Chainer {
   std::vector<std::unique_ptr<WorkerCalls>> calls_;
   std::string req_path_;  // target base path + aloha path
   std::string log_tag_;   // "[AlohaService#aloha] "
+  std::string log_request_line_;  // Feign BASIC request line (constant per target)
   tracing::Tracer* tracer_;
   const Clock& clock_;
   std::atomic<int> timeout_ms_{0};  // 0 = execution timeout disabled (read per call, lock-free)

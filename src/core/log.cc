@@ -114,6 +114,15 @@ void Logger::raw(const char* fmt, ...) {
   enqueue(line, size_t(n));
 }
 
+void Logger::raw_line(std::string_view line) {
+  if (level() == LogLevel::kOff) return;
+  char buf[2048];
+  const size_t n = std::min(line.size(), sizeof buf - 1);
+  memcpy(buf, line.data(), n);
+  buf[n] = '\n';
+  enqueue(buf, n + 1);
+}
+
 Logger::Ring* Logger::ring_for_this_thread() {
   if (tls_ring.r) return tls_ring.r;
   std::lock_guard<std::mutex> g(reg_mu_);

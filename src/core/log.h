@@ -16,6 +16,7 @@
 #include <cstdint>
 #include <mutex>
 #include <string>
+#include <string_view>
 #include <thread>
 
 namespace hola {
@@ -35,6 +36,8 @@ class Logger {
   // Logger.ErrorLogger, which System.err.printf()s its lines (HolaResource.java:109).
   // Suppressed only when the level is off.
   void raw(const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+  // raw() for a line that is already built (no printf); a newline is appended.
+  void raw_line(std::string_view line);
   // Blocks until every line logged before the call (by any thread) has been written.
   void flush();
   // Lines dropped because their thread's ring was full (the writer fell behind).

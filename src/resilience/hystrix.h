@@ -219,21 +219,25 @@ class Command {
       sem_max_{10};
   std::atomic<bool> semaphore_{false};  // execution.isolation.strategy=SEMAPHORE
   std::vector<std::unique_ptr<Shard>> shards_;
+  // Cache lines: the breaker state and health snapshot are read by every call and written
+  // rarely; the bulkhead count is written by every call from every worker. They sit on
+  // separate lines so that the count's traffic does not evict the read-mostly state.
   // breaker (HystrixCircuitBreakerImpl)
-  std::atomic<bool> open_{false};
+  alignas(64) std::atomic<bool> open_{false};
   std::atomic<int64_t> opened_or_tested_{0};
   // health snapshot: (total << 32 | errors), refreshed at most every health_ms_
   std::mutex health_mu_;
   std::atomic<int64_t> health_at_{-1};
   std::atomic<uint64_t> health_packed_{0};
   // bulkhead (thread pool of pool_core_ threads, and a queue when max_queue_ > 0)
-  std::atomic<int64_t> active_{0}, largest_{0};
+  alignas(64) std::atomic<int64_t> active_{0};
+  std::atomic<int64_t> largest_{0};
   bool try_acquire_slot();
   void slot_started(int64_t now, int64_t active);
   // maxQueueSize: Hystrix sizes the pool's queue once, when the pool is created at the first
   // execution, so later property changes do not resize it (update_settings() before the
   // first call still does: the start-up configuration arrives after construction)
-  std::atomic<int> max_queue_{-1};
+  alignas(64) std::atomic<int> max_queue_{-1};
   std::atomic<int> queue_threshold_{5};
   std::mutex queue_mu_;
   std::deque<Queued> queue_;
