@@ -385,10 +385,10 @@ void AlohaChainer::on_response(http::Worker& w, WorkerCalls& wc, uint32_t slot, 
   }
   const int64_t elapsed = now - c.start_ms;
   if (success) {
-    cmd->complete(Event::kSuccess, elapsed, false, clock_.now_ms() - c.start_ms);
+    cmd->complete(Event::kSuccess, elapsed, false, elapsed);
   } else {
     const bool fb = fallback_enabled_.load(std::memory_order_relaxed);
-    cmd->complete(Event::kFailure, elapsed, fb, clock_.now_ms() - c.start_ms);
+    cmd->complete(Event::kFailure, elapsed, fb, elapsed);
     res = failed_result("failure");
     res.reason = err;
   }

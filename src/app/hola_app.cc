@@ -115,7 +115,11 @@ void HolaApp::refresh(http::Worker& w, WorkerCache& wc) {
   uint64_t g = gen_.load(std::memory_order_acquire);
   if (g != wc.gen) {
     wc.gen = g;
-    wc.content = content();
+    // A private copy per worker: every chaining call holds a reference to its worker's
+    // content while it waits, and one control block shared by all workers would bounce its
+    // reference count between their cores on every call.
+    if (auto shared = content()) wc.content = std::make_shared<const Content>(*shared);
+    else wc.content = nullptr;
     const Content* c = wc.content.get();
     const char* date = w.date();
     wc.all.clear();
