@@ -78,8 +78,8 @@ def parse_args():
     ap.add_argument("--profile-dir", default="",
                     help="run replicas with --profile and write their stage histograms here")
     ap.add_argument("--cpu-profile-dir", default="",
-                    help="run replicas with --cpu-profile (sampled call stacks of every server thread, "
-                         "bench/cpuprof_report.py symbolises them) and write them here")
+                    help="run replicas and load generators with --cpu-profile (sampled call stacks of "
+                         "their threads; bench/cpuprof_report.py symbolises them) and write them here")
     ap.add_argument("--plain-dealing", action="store_true",
                     help="deal every rank's connections (i + rank) %% N over all replicas from its own "
                          "cores, instead of giving each load-generator thread the replicas of its L3 "
@@ -218,7 +218,9 @@ def main() -> int:
                                     path=a.path, target_offset=local_rank, busy_poll_us=a.busy_poll_us,
                                     busy_poll_pause=a.busy_poll_pause, epoll_lt=a.epoll_lt,
                                     per_conn_quota=a.per_conn_quota, pipeline=a.pipeline,
-                                    expect_bodies=bodies, verify_body=bodies is None, conn_targets=conn_targets)
+                                    expect_bodies=bodies, verify_body=bodies is None, conn_targets=conn_targets,
+                                    cpu_profile=os.path.join(os.path.abspath(a.cpu_profile_dir),
+                                                             f"loadgen_cpu_rank{rank}.prof") if a.cpu_profile_dir else None)
         for _ in range(a.warmup):
             loadgen.run(a.reqs_per_conn)
         loadgen.reset()

@@ -119,6 +119,8 @@ cpuprof)
     > "$OUT/headline.json" 2>> "$OUT/err.log" &&
   python bench/cpuprof_report.py "$OUT/headline/server_cpu_rank0.prof" --top 40 --json "$OUT/headline_report.json" \
     > "$OUT/headline_report.txt" 2>> "$OUT/err.log" &&
+  python bench/cpuprof_report.py "$OUT/headline/loadgen_cpu_rank0.prof" --threads hola-lg --top 40 \
+    --json "$OUT/loadgen_report.json" > "$OUT/loadgen_report.txt" 2>> "$OUT/err.log" &&
   timeout -k 10 120 python bench/chain_bench.py --duration 8 --feign-log basic --cpu-profile "$OUT/chain_a.prof" \
     --out "$OUT/chain.json" > "$OUT/chain.log" 2>&1 &&
   python bench/cpuprof_report.py "$OUT/chain_a.prof" --top 40 --json "$OUT/chain_report.json" \

@@ -28,6 +28,7 @@
 // wrk-like text summary (`--json` keeps the JSON line).
 #include <errno.h>
 #include <netinet/in.h>
+#include <pthread.h>
 #include <sys/epoll.h>
 #include <sys/prctl.h>
 #include <sys/eventfd.h>
@@ -48,6 +49,7 @@
 #include <thread>
 #include <vector>
 
+#include "core/cpuprof.h"
 #include "core/histogram.h"
 #include "core/affinity.h"
 #include "core/clock.h"
@@ -229,6 +231,12 @@ int response_complete(Conn* c, size_t from, int* status, bool* close, size_t* us
 
 void thread_main(ThreadState* ts, const Options* o) {
   if (!o->cpus.empty()) pin_current_thread(o->cpus[size_t(ts->index) % o->cpus.size()]);
+  {
+    char name[16];
+    snprintf(name, sizeof name, "hola-lg%d", ts->index);
+    pthread_setname_np(pthread_self(), name);
+  }
+  hola::cpuprof::register_thread();
   // Connections (and their receive buffers) are built here, after pinning, so their pages
   // are first touched on this thread's NUMA node: on a 2-socket node a thread may drive a
   // replica on the other socket from main()'s.
@@ -621,7 +629,7 @@ std::string human_bytes(double b) {
 
 int main(int argc, char** argv) {
   Options o;
-  std::string targets = "127.0.0.1:8080", cpu_list, url;
+  std::string targets = "127.0.0.1:8080", cpu_list, url, cpu_profile;
   bool json = false, latency = false;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
@@ -661,6 +669,7 @@ int main(int argc, char** argv) {
     else if (a == "--pipeline") o.pipeline = atoi(val().c_str());
     else if (a == "--expect-body") o.expect_bodies.push_back(unescape(val()));
     else if (a == "--verify-body") o.verify_body = true;
+    else if (a == "--cpu-profile") cpu_profile = val();
     else if (a == "--conn-targets") {
       if (!parse_cpu_list(val(), &o.conn_targets)) {  // same "0,1,1,0" / "0-3" syntax
         fprintf(stderr, "loadgen: bad --conn-targets\n");
@@ -673,6 +682,7 @@ int main(int argc, char** argv) {
               "                    (--duration S [--warmup S] [--rate R [--spin-us N]] | --control [--per-conn-quota])\n"
               "                    [--target-offset K] [--busy-poll-us N [--busy-poll-pause P]] [--epoll-lt] [-H 'Name: v']\n"
               "                    [--pipeline P] [--expect-body B]... [--verify-body] [--conn-targets i,j,..]\n"
+              "                    [--cpu-profile FILE]  (sampled call stacks, bench/cpuprof_report.py --threads hola-lg)\n"
               "       hola_loadgen -t T -c C -d 30s [--latency] [--json] [-H 'Name: v'] http://host:port/path   (wrk style)\n");
       return 2;
     }
@@ -702,6 +712,10 @@ int main(int argc, char** argv) {
   }
   if (!o.control && o.duration_s <= 0) o.duration_s = 10;
   signal(SIGPIPE, SIG_IGN);
+  if (!cpu_profile.empty() && !hola::cpuprof::start(cpu_profile)) {
+    fprintf(stderr, "loadgen: cannot start the CPU profiler\n");
+    return 2;
+  }
   g_donefd = eventfd(0, EFD_SEMAPHORE | EFD_CLOEXEC);
 
   std::vector<std::unique_ptr<ThreadState>> ts;
@@ -729,6 +743,7 @@ int main(int argc, char** argv) {
 
   if (!o.control) {
     for (auto& t : th) t.join();
+    if (!cpu_profile.empty()) hola::cpuprof::write();
     std::string s = stats_json(ts, false);
     uint64_t completed = 0;
     for (auto& t : ts) completed += t->completed;
@@ -827,5 +842,6 @@ int main(int argc, char** argv) {
     (void)w;
   }
   for (auto& t : th) t.join();
+  if (!cpu_profile.empty()) hola::cpuprof::write();
   return 0;
 }

@@ -74,7 +74,7 @@ class ControlledLoadgen:
                  headers: list[str] | None = None, busy_poll_us: int = 0, per_conn_quota: bool = False,
                  busy_poll_pause: int = 0, epoll_lt: bool = False, pipeline: int = 1,
                  expect_bodies: list[str] | None = None, verify_body: bool = False,
-                 conn_targets: list[int] | None = None):
+                 conn_targets: list[int] | None = None, cpu_profile: str | None = None):
         cmd = [str(binary("hola_loadgen")), "--targets", ",".join(f"{h}:{p}" for h, p in targets),
                "-c", str(connections), "-t", str(threads), "--path", path, "--control",
                "--target-offset", str(target_offset)] + body_args(expect_bodies, verify_body)
@@ -94,6 +94,8 @@ class ControlledLoadgen:
             cmd += ["--pipeline", str(pipeline)]
         if conn_targets:
             cmd += ["--conn-targets", ",".join(map(str, conn_targets))]
+        if cpu_profile:
+            cmd += ["--cpu-profile", cpu_profile]  # written when the generator quits
         self.proc = subprocess.Popen(cmd, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, bufsize=1)
         ready = self._read()
         if not ready.get("ready"):

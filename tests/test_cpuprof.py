@@ -31,3 +31,18 @@ def test_cpu_profile_samples_workers_under_load(hola, tmp_path):
     assert any("send" in fn for fn in names), names
     assert any("hola::EventLoop::run" in fn for fn in names), names
     assert any("hola::http::Connection::" in fn for fn in names), names
+
+
+def test_loadgen_cpu_profile(hola, tmp_path):
+    from hola_amd.parallel.loadgen import ControlledLoadgen
+
+    s = hola(threads=1)
+    prof = tmp_path / "lg.prof"
+    lg = ControlledLoadgen([("127.0.0.1", s.port)], 4, 2, cpu_profile=str(prof))
+    try:
+        r = lg.run(20000)
+        assert r["errors"] == 0
+    finally:
+        lg.close()
+    text = prof.read_text()
+    assert " hola-lg0\n" in text and " hola-lg1\n" in text and "\nstack " in text
