@@ -31,6 +31,8 @@ from hola_amd.utils.net import http_get  # noqa: E402
 ap = argparse.ArgumentParser(description=__doc__)
 ap.add_argument("--minutes", type=float, default=5)
 ap.add_argument("--sample-s", type=float, default=10)
+ap.add_argument("--feign-log", default="basic", choices=("basic", "none"),
+                help="the replica's Feign logging (basic = the default, two log-ring lines per aloha call)")
 ap.add_argument("--out", default="")
 a = ap.parse_args()
 
@@ -43,10 +45,12 @@ stop = threading.Event()
 samples, errors = [], []
 
 with FakeAloha() as aloha, HolaProcess(
-        args=["--aloha-url", aloha.url, "--feign-log", "none", f"-Dconf={conf}",
+        args=["--aloha-url", aloha.url, "--feign-log", a.feign_log, f"-Dconf={conf}",
               "-Dhystrix.command.default.circuitBreaker.sleepWindowInMilliseconds=1000",
               "--hystrix-stream-stall-ms", "5000"],
-        env={"HOSTNAME": "soak"}, threads=len(srv), cpu_list=format_cpu_list(srv), log_level="warn") as s:
+        env={"HOSTNAME": "soak"}, threads=len(srv), cpu_list=format_cpu_list(srv), log_level="warn",
+        # BASIC logging writes two lines per aloha call: kept off the disk
+        stderr_path=os.devnull if a.feign_log == "basic" else None) as s:
     pid = s.proc.pid
 
     def chaining():
@@ -104,11 +108,16 @@ with FakeAloha() as aloha, HolaProcess(
                 rss = next(int(l.split()[1]) for l in open(f"/proc/{pid}/status") if l.startswith("VmRSS:"))
                 fds = len(os.listdir(f"/proc/{pid}/fd"))
                 _, _, m = http_get("127.0.0.1", s.port, "/metrics", timeout=5)
-                reqs = next(int(l.split()[-1]) for l in m.decode().splitlines()
-                            if l.startswith("hola_http_requests_total "))
-                samples.append({"t_s": round(time.monotonic() - t0, 1), "rss_kb": rss, "fds": fds, "requests": reqs})
+                metric = {l.split()[0]: int(float(l.split()[-1])) for l in m.decode().splitlines()
+                          if l.startswith(("hola_http_requests_total ", "hola_event_loop_timers ",
+                                           "hola_log_lines_dropped_total "))}
+                samples.append({"t_s": round(time.monotonic() - t0, 1), "rss_kb": rss, "fds": fds,
+                                "requests": metric["hola_http_requests_total"],
+                                # pending loop timers follow the calls in flight (a leak grows them)
+                                "timers": metric.get("hola_event_loop_timers", -1),
+                                "log_dropped": metric.get("hola_log_lines_dropped_total", -1)})
                 print(json.dumps(samples[-1]), flush=True)
-            except (OSError, StopIteration) as e:
+            except (OSError, StopIteration, KeyError) as e:
                 errors.append(("sampler", repr(e)))
             stop.wait(a.sample_s)
 
@@ -136,7 +145,9 @@ out = {
     "minutes": a.minutes, "hola_rps": res["rps"], "hola_p99_ms": res["latency"]["p99_ns"] / 1e6,
     "hola_errors": res["latency"]["errors"], "other_errors": errors[:20], "alive_at_end": alive,
     "rss_kb_first": first["rss_kb"], "rss_kb_last": last["rss_kb"], "rss_kb_max": max(x["rss_kb"] for x in samples),
-    "fds_first": first["fds"], "fds_last": last["fds"], "stream": stream_stats, "samples": samples,
+    "fds_first": first["fds"], "fds_last": last["fds"], "stream": stream_stats,
+    "timers_max": max(x.get("timers", -1) for x in samples), "timers_last": last.get("timers", -1),
+    "log_dropped_last": last.get("log_dropped", -1), "feign_log": a.feign_log, "samples": samples,
 }
 print(json.dumps({k: v for k, v in out.items() if k != "samples"}))
 if a.out:
