@@ -123,6 +123,7 @@ struct AlohaChainer::WorkerCalls {
   EventLoop::TimerId timer = 0;
   int64_t timer_at = 0;  // deadline the armed timer fires for (0 = none armed)
   http::Worker* worker = nullptr;
+  AlohaChainer* owner = nullptr;
 };
 
 AlohaChainer::WorkerCalls& AlohaChainer::calls(http::Worker& w) {
@@ -130,6 +131,7 @@ AlohaChainer::WorkerCalls& AlohaChainer::calls(http::Worker& w) {
   if (!c) {
     c = std::make_unique<WorkerCalls>();
     c->worker = &w;
+    c->owner = this;
   }
   return *c;
 }
@@ -295,9 +297,11 @@ void AlohaChainer::execute(http::Worker& w, WorkerCalls& wc, uint32_t slot, uint
   c.start_us = wall_us();
   c.attempt_ms = clock_.now_ms();
   if (o_.feign_log_basic) Logger::instance().raw_line(log_request_line_);
-  http::Worker* wp = &w;
-  const uint64_t id = pool(w).get(req_path_, headers, [this, wp, &wc, slot, gen](client::ClientResult&& r) {
-    on_response(*wp, wc, slot, gen, std::move(r));
+  // Two words of captures: std::function keeps them inline (no allocation per call).
+  WorkerCalls* wcp = &wc;
+  const uint64_t sg = (uint64_t(slot) << 32) | gen;
+  const uint64_t id = pool(w).get(req_path_, headers, [wcp, sg](client::ClientResult&& r) {
+    wcp->owner->on_response(*wcp->worker, *wcp, uint32_t(sg >> 32), uint32_t(sg), std::move(r));
   });
   if (!dead(wc, slot, gen) && c.inflight) c.req_id = id;
 }
