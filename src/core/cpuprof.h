@@ -8,6 +8,10 @@
 // Time spent inside a syscall is charged to the libc wrapper the thread returns to (send,
 // recv, epoll_wait), so the profile also splits kernel time by call. At exit the samples and
 // the executable mappings are written as text; `bench/cpuprof_report.py` symbolises them.
+//
+// The unwinder is not async-signal-safe in general: it may take the loader's lock (glibc's
+// dl_iterate_phdr). That lock is recursive, and the profiled threads load no libraries after
+// start-up, so a sample cannot deadlock them; still, this is a diagnostic mode, off by default.
 #pragma once
 #include <string>
 
@@ -15,7 +19,7 @@ namespace hola::cpuprof {
 
 // Allocates the sample buffer and installs the SIGPROF handler; `hz` samples per second of
 // each thread's CPU time. Returns false (and profiles nothing) on failure.
-bool start(const std::string& path, int hz = 4000);
+bool start(const std::string& path, int hz = 1000);
 // Arms the calling thread's CPU-time timer (a no-op unless start() succeeded).
 void register_thread();
 // Disarms the calling thread's timer.
