@@ -30,6 +30,8 @@ ap.add_argument("--pool", type=int, default=128, help="hystrix thread-pool (bulk
 ap.add_argument("--feign-log", default="none", choices=("none", "basic"),
                 help="A's Feign logging; basic = the reference's ErrorLogger at Level.BASIC (two stderr "
                      "lines per call, the server's default)")
+ap.add_argument("--aloha-pipeline", type=int, default=1,
+                help="A's --aloha-pipeline (HTTP/1.1 pipelining of concurrent calls to B; 1 = off)")
 ap.add_argument("--cpu-profile", default="",
                 help="run A with --cpu-profile here (sampled call stacks; bench/cpuprof_report.py reads it)")
 ap.add_argument("--out", default="")
@@ -63,7 +65,8 @@ with HolaProcess(args=["--aloha-url", "http://127.0.0.1:1/", "--feign-log", "non
                  cpu_list=format_cpu_list(cores[1])) as b:
     with HolaProcess(args=["--aloha-url", f"http://127.0.0.1:{b.port}/", "--aloha-path", "api/hola-chaining",
                            "--feign-log", a.feign_log, "--hystrix-pool-size", str(a.pool)]
-                          + (["--cpu-profile", os.path.abspath(a.cpu_profile)] if a.cpu_profile else []),
+                          + (["--cpu-profile", os.path.abspath(a.cpu_profile)] if a.cpu_profile else [])
+                          + (["--aloha-pipeline", str(a.aloha_pipeline)] if a.aloha_pipeline > 1 else []),
                      env={"HOSTNAME": "A"}, threads=len(cores[0]), cpu_list=format_cpu_list(cores[0]),
                      # BASIC logging writes ~150 bytes per call: at 1.5 M calls/s that would be
                      # gigabytes of log file per run, so A's stderr goes to /dev/null
@@ -91,7 +94,7 @@ events = {l.split('event="')[1].split('"')[0]: int(l.split()[-1]) for l in metri
 out = {"sample": sample, "rps": res["rps"], "p50_ms": res["latency"]["p50_ns"] / 1e6,
        "p99_ms": res["latency"]["p99_ns"] / 1e6, "errors": res["latency"]["errors"],
        "body_checked": res["latency"].get("body_checked", 0), "body_mismatch": res["latency"].get("body_mismatch", 0),
-       "hystrix_events": events, "feign_log": a.feign_log,
+       "hystrix_events": events, "feign_log": a.feign_log, "aloha_pipeline": a.aloha_pipeline,
        # cores kept busy (warmup included) and CPU µs per request at the measured rate
        "cpus_busy": {k: round(v, 2) for k, v in busy.items()},
        "cpu_us_per_req": {k: round(v / res["rps"] * 1e6, 2) for k, v in busy.items()},

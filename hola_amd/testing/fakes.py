@@ -64,7 +64,8 @@ class _AlohaHandler(BaseHTTPRequestHandler):
     def do_GET(self):
         owner: FakeAloha = self.server.owner  # type: ignore[attr-defined]
         with owner.lock:
-            owner.requests.append({"path": self.path, "headers": {k.lower(): v for k, v in self.headers.items()}})
+            owner.requests.append({"path": self.path, "headers": {k.lower(): v for k, v in self.headers.items()},
+                                   "peer_port": self.client_address[1]})
             mode, delay, payload = owner.mode, owner.delay_s, owner.payload
         if mode == "slow":
             time.sleep(delay)

@@ -84,6 +84,7 @@ client::ClientPool& AlohaChainer::pool(http::Worker& w) {
   if (!p) {
     p = std::make_unique<client::ClientPool>(w.loop(), target_, addr_.get(), 64, &transport_retries_);
     p->set_timeouts(o_.connect_timeout_ms, &read_timeout_armed_);
+    p->set_pipeline(o_.pipeline);
   }
   return *p;
 }

@@ -56,6 +56,10 @@ struct AlohaOptions {
   // is armed per request only then (--feign-timeouts CONNECT_MS,READ_MS).
   int connect_timeout_ms = 10000;
   int read_timeout_ms = 60000;
+  // HTTP/1.1 pipelining of concurrent aloha calls over each pooled connection
+  // (--aloha-pipeline N, opt-in: the reference's HttpClient sends one request per
+  // connection at a time). 1 = off.
+  int pipeline = 1;
 };
 
 class AlohaChainer final : public Chainer {

@@ -152,6 +152,34 @@ struct ClientPool::Conn final : EventLoop::Handler {
   int try_parse(ClientResult* r, bool* keep, bool eof);
 };
 
+// A pipelined connection (ClientPool::set_pipeline): requests queue in order, responses
+// complete them in order.
+struct ClientPool::PConn final : EventLoop::Handler {
+  struct Pending {
+    uint64_t id, serial;
+    std::string req;  // kept for a re-send if the connection fails before the response
+    Callback cb;
+    int tries = 0;
+    bool abandoned = false;  // cancelled (timed out): its response is read and dropped
+  };
+  ClientPool* pool = nullptr;
+  int fd = -1;
+  bool connecting = false, dead = false, dirty = false;
+  std::string out, in;
+  size_t off = 0;
+  std::deque<Pending> q;
+  uint32_t interest = 0;
+
+  void set_interest(uint32_t ev) {
+    if (ev == interest) return;
+    interest = ev;
+    pool->loop_.mod(fd, ev, this);
+  }
+  void on_event(uint32_t ev) override;
+  void do_write();
+  void do_read();
+};
+
 void ClientPool::Conn::fail(const std::string& why, bool io) {
   // Apache HttpClient's DefaultHttpRequestRetryHandler (the default of the HttpClientBuilder
   // in HolaResource.java:98-102): an idempotent GET that hit an I/O error before its response
@@ -222,9 +250,13 @@ void ClientPool::Conn::do_write() {
   set_interest(EPOLLIN | EPOLLRDHUP);
 }
 
-int ClientPool::Conn::try_parse(ClientResult* r, bool* keep, bool eof) {
+namespace {
+// One response from the front of `in`: 1 = complete (*consumed bytes; *close when the
+// connection cannot carry another response), 0 = need more, -1 = malformed. *head_ok is set
+// once a well-formed status line and header block have arrived.
+int parse_response(std::string_view in, bool eof, ClientResult* r, bool* close, size_t* consumed, bool* head_ok) {
   size_t he = in.find("\r\n\r\n");
-  if (he == std::string::npos) return in.size() > 64 * 1024 ? -1 : 0;
+  if (he == std::string_view::npos) return in.size() > 64 * 1024 ? -1 : 0;
   std::string_view head(in.data(), he);
   if (head.size() < 12 || head.substr(0, 5) != "HTTP/") return -1;
   int status = 0;
@@ -238,7 +270,8 @@ int ClientPool::Conn::try_parse(ClientResult* r, bool* keep, bool eof) {
   r->reason.assign(eol > 13 && head[12] == ' ' ? head.substr(13, eol - 13) : std::string_view());
   r->has_retry_after = false;
   int64_t cl = -1;
-  bool chunked = false, close = http10;
+  bool chunked = false;
+  *close = http10;
   size_t p = head.find("\r\n");
   while (p != std::string_view::npos && p + 2 <= head.size()) {
     size_t n = head.find("\r\n", p + 2);
@@ -257,8 +290,8 @@ int ClientPool::Conn::try_parse(ClientResult* r, bool* keep, bool eof) {
       }
       else if (http::iequals(k, "transfer-encoding") && v.find("chunked") != std::string_view::npos) chunked = true;
       else if (http::iequals(k, "connection")) {
-        if (http::iequals(v, "close")) close = true;
-        else if (http::iequals(v, "keep-alive")) close = false;
+        if (http::iequals(v, "close")) *close = true;
+        else if (http::iequals(v, "keep-alive")) *close = false;
       } else if (http::iequals(k, "retry-after")) {
         r->has_retry_after = parse_retry_after(v, wall_us() / 1000, &r->retry_after_ms);
       }
@@ -266,37 +299,48 @@ int ClientPool::Conn::try_parse(ClientResult* r, bool* keep, bool eof) {
     p = n;
   }
   size_t body = he + 4;
-  head_ok = true;
+  *head_ok = true;
   if (status == 204 || status == 304 || (status >= 100 && status < 200)) {
     r->status = status;
-    *keep = !close;
+    *consumed = body;
     return 1;
   }
   if (chunked) {
-    size_t consumed = 0;
+    size_t used = 0;
     std::string out;
-    http::Parse q = http::decode_chunked_body(in.data() + body, in.size() - body, &consumed, &out);
+    http::Parse q = http::decode_chunked_body(in.data() + body, in.size() - body, &used, &out);
     if (q == http::Parse::kError) return -1;
     if (q == http::Parse::kIncomplete) return in.size() > (1 << 20) ? -1 : 0;
     r->status = status;
     r->body = std::move(out);
-    *keep = !close && body + consumed == in.size();
+    *consumed = body + used;
     return 1;
   }
   if (cl >= 0) {
     if (cl > (1 << 20)) return -1;
     if (in.size() - body < size_t(cl)) return 0;
     r->status = status;
-    r->body = in.substr(body, size_t(cl));
-    *keep = !close && body + size_t(cl) == in.size();
+    r->body.assign(in.substr(body, size_t(cl)));
+    *consumed = body + size_t(cl);
     return 1;
   }
   // close-delimited body
   if (!eof) return in.size() > (1 << 20) ? -1 : 0;
   r->status = status;
-  r->body = in.substr(body);
-  *keep = false;
+  r->body.assign(in.substr(body));
+  *consumed = in.size();
+  *close = true;
   return 1;
+}
+}  // namespace
+
+int ClientPool::Conn::try_parse(ClientResult* r, bool* keep, bool eof) {
+  bool close = false;
+  size_t consumed = 0;
+  const int rc = parse_response(in, eof, r, &close, &consumed, &head_ok);
+  // a response followed by stray bytes leaves a connection that cannot be reused
+  if (rc == 1) *keep = !close && consumed == in.size();
+  return rc;
 }
 
 void ClientPool::Conn::do_read() {
@@ -376,6 +420,13 @@ ClientPool::ClientPool(EventLoop& loop, Url target, AddressCache* addr, size_t m
 }
 
 ClientPool::~ClientPool() {
+  for (PConn* c : pconns_) {
+    if (c->fd >= 0) {
+      loop_.del(c->fd);
+      ::close(c->fd);
+    }
+    delete c;
+  }
   for (DeadlineFifo* f : {&connect_fifo_, &read_fifo_})
     if (f->timer) loop_.cancel_timer(f->timer);
   for (Conn* c : idle_) {
@@ -407,6 +458,7 @@ std::string ClientPool::build_request(const std::string& path, const std::string
 uint64_t ClientPool::get(const std::string& path, const std::string& extra_headers, Callback cb) {
   uint64_t id = next_id_++;
   std::string req = build_request(path, extra_headers);
+  if (pipeline_ > 1 && get_pipelined(id, req, cb)) return id;
   if (!idle_.empty()) {
     Conn* c = idle_.back();
     idle_.pop_back();
@@ -421,7 +473,9 @@ uint64_t ClientPool::get(const std::string& path, const std::string& extra_heade
 
 bool ClientPool::live(const Deadline& d) const {
   auto it = active_.find(d.id);
-  return it != active_.end() && it->second->serial == d.serial;
+  if (it != active_.end()) return it->second->serial == d.serial;
+  auto pt = pactive_.find(d.id);
+  return pt != pactive_.end() && pt->second.serial == d.serial;
 }
 
 void ClientPool::push_deadline(DeadlineFifo& f, int ms, uint64_t id, uint64_t serial) {
@@ -461,6 +515,17 @@ void ClientPool::expire(DeadlineFifo& f) {
     }
     if (d.at_ms > now) break;
     f.q.pop_front();
+    if (auto pt = pactive_.find(d.id); pt != pactive_.end()) {
+      // Pipelined: the responses behind this one cannot overtake it, so the connection ends;
+      // this request fails with the timeout, the others are re-sent on fresh connections.
+      PConn* pc = pt->second.conn;
+      if (!f.connect)
+        pfail(pc, "SocketTimeoutException: Read timed out", d.id);
+      else if (pc->connecting)
+        pfail(pc, "ConnectTimeoutException: Connect to " + target_.host + ":" + std::to_string(target_.port) +
+                      " failed: connect timed out", d.id);
+      continue;
+    }
     Conn* c = active_.find(d.id)->second;
     // fail() runs the callback, which may start (and push deadlines for) further requests
     if (f.connect) {
@@ -566,6 +631,18 @@ void ClientPool::destroy(Conn* c) {
 }
 
 void ClientPool::cancel(uint64_t id) {
+  if (auto pt = pactive_.find(id); pt != pactive_.end()) {
+    // Its response will still arrive in order on the shared connection: read and dropped.
+    for (auto& p : pt->second.conn->q)
+      if (p.id == id) {
+        p.abandoned = true;
+        p.cb = nullptr;
+      }
+    pactive_.erase(pt);
+    if (!read_fifo_.q.empty()) pop_finished(read_fifo_);
+    if (!connect_fifo_.q.empty()) pop_finished(connect_fifo_);
+    return;
+  }
   auto it = active_.find(id);
   if (it == active_.end()) return;
   Conn* c = it->second;
@@ -573,6 +650,213 @@ void ClientPool::cancel(uint64_t id) {
   destroy(c);
   if (!read_fifo_.q.empty()) pop_finished(read_fifo_);
   if (!connect_fifo_.q.empty()) pop_finished(connect_fifo_);
+}
+
+// ---------------------------------------------------------------- pipelined connections
+
+
+ClientPool::PConn* ClientPool::open_pconn() {
+  sockaddr_storage ss{};
+  socklen_t len = 0;
+  if (!addr_ || !addr_->get(&ss, &len, nullptr)) return nullptr;  // the plain path reports it
+  bool inprog = false;
+  const int fd = connect_nonblocking(ss, len, &inprog);
+  if (fd < 0) return nullptr;
+  auto* c = new PConn();
+  c->pool = this;
+  c->fd = fd;
+  c->connecting = inprog;
+  c->interest = inprog ? uint32_t(EPOLLOUT) : uint32_t(EPOLLIN | EPOLLRDHUP);
+  loop_.add(fd, c->interest, c);
+  pconns_.push_back(c);
+  ++opened_;
+  return c;
+}
+
+bool ClientPool::get_pipelined(uint64_t id, std::string& req, Callback& cb) {
+  // Fill the connection this batch already writes to, then any other with room, then a new
+  // one: requests of one batch share a send() and a TCP segment.
+  const size_t depth = size_t(pipeline_);
+  PConn* c = nullptr;
+  for (PConn* p : dirty_)
+    if (!p->dead && p->q.size() < depth) {
+      c = p;
+      break;
+    }
+  if (!c)
+    for (PConn* p : pconns_)
+      if (!p->dead && p->q.size() < depth) {
+        c = p;
+        break;
+      }
+  if (!c && !(c = open_pconn())) return false;
+  const uint64_t serial = next_serial_++;
+  c->out += req;
+  c->q.push_back({id, serial, std::move(req), std::move(cb)});
+  pactive_[id] = {c, serial};
+  if (read_timeout_ms_) {
+    const int rt = read_timeout_ms_->load(std::memory_order_relaxed);
+    if (rt > 0) push_deadline(read_fifo_, rt, id, serial);
+  }
+  if (c->connecting && connect_timeout_ms_ > 0) push_deadline(connect_fifo_, connect_timeout_ms_, id, serial);
+  if (!c->dirty) {
+    c->dirty = true;
+    dirty_.push_back(c);
+  }
+  if (!flush_scheduled_) {
+    flush_scheduled_ = true;
+    loop_.defer([this] { flush_dirty(); });
+  }
+  return true;
+}
+
+void ClientPool::flush_dirty() {
+  flush_scheduled_ = false;
+  std::vector<PConn*> batch;
+  batch.swap(dirty_);
+  for (PConn* c : batch) {
+    c->dirty = false;
+    if (!c->dead && !c->connecting) c->do_write();
+  }
+}
+
+void ClientPool::PConn::on_event(uint32_t ev) {
+  if (dead) return;
+  if (connecting) {
+    int soerr = 0;
+    socklen_t sl = sizeof soerr;
+    getsockopt(fd, SOL_SOCKET, SO_ERROR, &soerr, &sl);
+    if (soerr != 0 || (ev & (EPOLLERR | EPOLLHUP))) {
+      pool->pfail(this, pool->connect_error(soerr ? soerr : ECONNREFUSED));
+      return;
+    }
+    connecting = false;
+    set_interest(EPOLLIN | EPOLLRDHUP);
+    do_write();
+    return;
+  }
+  if (ev & EPOLLOUT) {
+    do_write();
+    if (dead) return;
+  }
+  if (ev & (EPOLLIN | EPOLLRDHUP | EPOLLHUP | EPOLLERR)) do_read();
+}
+
+void ClientPool::PConn::do_write() {
+  while (off < out.size()) {
+    ssize_t w = ::send(fd, out.data() + off, out.size() - off, MSG_NOSIGNAL);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      if (errno == EAGAIN) {
+        set_interest(EPOLLIN | EPOLLRDHUP | EPOLLOUT);
+        return;
+      }
+      pool->pfail(this, std::string("SocketException: ") + strerror(errno));
+      return;
+    }
+    off += size_t(w);
+  }
+  out.clear();
+  off = 0;
+  set_interest(EPOLLIN | EPOLLRDHUP);
+}
+
+void ClientPool::PConn::do_read() {
+  char buf[16384];
+  for (;;) {
+    ssize_t n = ::recv(fd, buf, sizeof buf, 0);
+    bool eof = false;
+    if (n > 0) {
+      in.append(buf, size_t(n));
+    } else if (n == 0) {
+      eof = true;
+    } else {
+      if (errno == EINTR) continue;
+      if (errno == EAGAIN) return;
+      pool->pfail(this, std::string("SocketException: ") + strerror(errno));
+      return;
+    }
+    // Responses arrive in request order: each completes the oldest request.
+    size_t used = 0;
+    while (!q.empty()) {
+      ClientResult r;
+      bool close = false, head_ok = false;
+      size_t consumed = 0;
+      const int rc = parse_response(std::string_view(in).substr(used), eof, &r, &close, &consumed, &head_ok);
+      if (rc < 0) {
+        pool->pfail(this, "ClientProtocolException: malformed response");
+        return;
+      }
+      if (rc == 0) break;
+      used += consumed;
+      Pending p = std::move(q.front());
+      q.pop_front();
+      pool->pactive_.erase(p.id);
+      r.ok = true;
+      if (!p.abandoned && p.cb) p.cb(std::move(r));
+      if (dead) return;  // the callback's work ended this connection
+      if (close) {
+        in.clear();
+        pool->pfail(this, "NoHttpResponseException: connection closed");
+        return;
+      }
+    }
+    if (used) in.erase(0, used);
+    if (eof || (q.empty() && !in.empty())) {
+      // the peer closed, or sent bytes nobody asked for: the connection is done
+      pool->pfail(this, in.empty() || q.empty() ? "NoHttpResponseException: connection closed"
+                                                : "TruncatedChunkException: premature EOF");
+      return;
+    }
+    if (size_t(n) < sizeof buf) return;
+  }
+}
+
+void ClientPool::pdestroy(PConn* c) {
+  if (c->dead) return;
+  c->dead = true;
+  loop_.del(c->fd);
+  ::close(c->fd);
+  c->fd = -1;
+  pconns_.erase(std::remove(pconns_.begin(), pconns_.end(), c), pconns_.end());
+  dirty_.erase(std::remove(dirty_.begin(), dirty_.end(), c), dirty_.end());
+  loop_.retire(c);
+}
+
+void ClientPool::pfail(PConn* c, const std::string& why, uint64_t timed_out) {
+  std::deque<PConn::Pending> q;
+  q.swap(c->q);
+  pdestroy(c);
+  for (auto& p : q) {
+    pactive_.erase(p.id);
+    if (p.abandoned || !p.cb) continue;
+    if (p.id == timed_out) {
+      ClientResult r;
+      r.error = why;
+      r.retryable = true;  // an IOException to Feign
+      p.cb(std::move(r));
+    } else {
+      resubmit(p.id, std::move(p.req), std::move(p.cb), p.tries + 1, why);
+    }
+  }
+  if (!read_fifo_.q.empty()) pop_finished(read_fifo_);
+  if (!connect_fifo_.q.empty()) pop_finished(connect_fifo_);
+}
+
+void ClientPool::resubmit(uint64_t id, std::string req, Callback cb, int tries, const std::string& why) {
+  if (tries > kTransportRetries) {
+    ClientResult r;
+    r.error = why;
+    r.retryable = true;
+    cb(std::move(r));
+    return;
+  }
+  if (transport_retries_) transport_retries_->fetch_add(1, std::memory_order_relaxed);
+  // DefaultHttpRequestRetryHandler: the idempotent GET goes out again on a fresh connection
+  auto* fresh = new Conn();
+  fresh->pool = this;
+  fresh->tries = tries;
+  start_on(fresh, id, std::move(req), std::move(cb), false);
 }
 
 }  // namespace hola::client

@@ -92,10 +92,16 @@ class ClientPool {
   }
   size_t idle_connections() const { return idle_.size(); }
   uint64_t connections_opened() const { return opened_; }
+  // HTTP/1.1 pipelining (opt-in; Apache HttpClient, the reference's transport, never
+  // pipelines): up to `depth` requests in flight per connection, and the requests queued on a
+  // connection during one event-loop batch go out in one send(). depth 1 = off.
+  void set_pipeline(int depth) { pipeline_ = depth < 1 ? 1 : depth; }
 
  private:
   struct Conn;
   friend struct Conn;
+  struct PConn;
+  friend struct PConn;
   void start_on(Conn* c, uint64_t id, std::string req, Callback cb, bool reused);
   void finish(Conn* c, ClientResult&& r, bool reusable);
   void destroy(Conn* c);
@@ -131,6 +137,24 @@ class ClientPool {
     bool connect = false;  // connect timeouts (else read timeouts)
   };
   DeadlineFifo connect_fifo_, read_fifo_;
+  // pipelined connections (pipeline_ > 1)
+  struct PRef {
+    PConn* conn;
+    uint64_t serial;
+  };
+  int pipeline_ = 1;
+  std::vector<PConn*> pconns_;
+  std::unordered_map<uint64_t, PRef> pactive_;  // request id -> its pipelined connection
+  std::vector<PConn*> dirty_;                   // requests queued this batch, not yet sent
+  bool flush_scheduled_ = false;
+  bool get_pipelined(uint64_t id, std::string& req, Callback& cb);
+  PConn* open_pconn();
+  void flush_dirty();
+  void pdestroy(PConn* c);
+  // Ends a pipelined connection: `timed_out` (if any) fails with `why`, every other request
+  // still waiting on it is re-sent on a fresh connection (HttpClient's transport retry).
+  void pfail(PConn* c, const std::string& why, uint64_t timed_out = 0);
+  void resubmit(uint64_t id, std::string req, Callback cb, int tries, const std::string& why);
   bool live(const Deadline& d) const;
   void push_deadline(DeadlineFifo& f, int ms, uint64_t id, uint64_t serial);
   void arm(DeadlineFifo& f);

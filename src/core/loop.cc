@@ -30,6 +30,8 @@ EventLoop::~EventLoop() {
   {
     auto timers = std::move(timers_);
     timers.clear();
+    deferred_.clear();
+    deferred_run_.clear();
     std::vector<std::function<void()>> posted;
     {
       std::lock_guard<std::mutex> g(post_mu_);
@@ -147,6 +149,11 @@ void EventLoop::run() {
     now_ms_ = mono_ms();
     for (int i = 0; i < n; ++i) static_cast<Handler*>(evs[i].data.ptr)->on_event(evs[i].events);
     if (!heap_.empty()) run_timers();
+    while (!deferred_.empty()) {
+      deferred_run_.swap(deferred_);
+      for (auto& f : deferred_run_) f();
+      deferred_run_.clear();
+    }
     if (!retired_.empty()) {
       for (Handler* h : retired_) delete h;
       retired_.clear();

@@ -45,6 +45,9 @@ class EventLoop {
   void post(std::function<void()> fn);
   // Handlers whose lifetime ends inside an event batch are deleted after the batch.
   void retire(Handler* h) { retired_.push_back(h); }
+  // Loop thread only: run fn once the current batch of events and timers has been handled
+  // (before the loop polls again), e.g. to send what a batch queued in one write.
+  void defer(std::function<void()> fn) { deferred_.push_back(std::move(fn)); }
 
   void run();
   void stop();  // thread-safe
@@ -91,6 +94,7 @@ class EventLoop {
   std::mutex post_mu_;
   std::vector<std::function<void()>> posted_;
   std::vector<Handler*> retired_;
+  std::vector<std::function<void()>> deferred_, deferred_run_;
   std::function<void()> tick_, on_exit_;
   int64_t busy_poll_ns_ = 0;
   int busy_poll_pause_ = 0;

@@ -61,6 +61,8 @@ void usage() {
           "  --feign-timeouts C,R     Feign Request.Options: connect / read timeout in ms (default\n"
           "                           10000,60000; the read timeout applies when the Hystrix timeout\n"
           "                           is disabled or longer)\n"
+          "  --aloha-pipeline N       pipeline up to N concurrent aloha calls per kept-alive connection,\n"
+          "                           a batch's requests in one send (default 1 = off, as HttpClient)\n"
           "  --hystrix-command-key method|configkey|KEY   Hystrix command key of the aloha call\n"
           "                           (default method = \"aloha\", feign-hystrix 8.x; configkey =\n"
           "                           \"AlohaService#aloha()\", feign-hystrix 9.x SetterFactory.Default)\n"
@@ -183,6 +185,12 @@ int main(int argc, char** argv) {
       }
       alo.connect_timeout_ms = c;
       alo.read_timeout_ms = r;
+    } else if (a == "--aloha-pipeline") {
+      alo.pipeline = atoi(val("--aloha-pipeline").c_str());
+      if (alo.pipeline < 1 || alo.pipeline > 256) {
+        fprintf(stderr, "hola: --aloha-pipeline takes 1..256\n");
+        return 2;
+      }
     } else if (a == "--hystrix-command-key") {
       std::string k = val("--hystrix-command-key");
       if (k == "method") alo.command_key = "aloha";

@@ -648,3 +648,52 @@ def test_input_arriving_while_a_request_is_parked(hola, aloha, epoll):
         out = read_until_closed(c)
     assert out.count(b"HTTP/1.1 200 OK") == 2
     assert 0 < out.find(b"Aloha mai") < out.rfind(b"Hola de h"), out
+
+
+def _concurrent_chains(s, n):
+    out = [None] * n
+
+    def one(i):
+        st, _, body = s.get("/api/hola-chaining", timeout=10)
+        out[i] = (st, json.loads(body))
+
+    ts = [threading.Thread(target=one, args=(i,)) for i in range(n)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    return out
+
+
+def test_pipelined_aloha_calls_share_connections(hola, aloha):
+    """--aloha-pipeline N: concurrent aloha calls of a worker go out over shared kept-alive
+    connections, several requests per connection in flight, and every call still gets its
+    own answer in order."""
+    s = hola(args=["--aloha-url", aloha.url, "--no-tracing", "--feign-log", "none", "--aloha-pipeline", "8",
+                   "-Dhystrix.threadpool.default.coreSize=64"], env={"HOSTNAME": "h"}, threads=1)
+    for _ in range(3):
+        res = _concurrent_chains(s, 24)
+        assert all(st == 200 and body == ["Hola de h", "Aloha mai aloha-1", "Bonjour de bonjour-1"]
+                   for st, body in res), res
+    peers = {r["peer_port"] for r in aloha.requests}
+    assert len(aloha.requests) == 72
+    assert len(peers) < 24, peers  # fewer connections than concurrent calls
+    m = s.get("/metrics")[2]
+    assert b'event="SUCCESS"} 72' in m
+
+
+@pytest.mark.parametrize("mode,expect_fallback", [("close", True), ("slow", True), ("error", True)])
+def test_pipelined_failures(hola, aloha, mode, expect_fallback):
+    """A dropped connection, a timeout and an error status on a pipelined connection: each
+    call falls back on its own, and the next calls succeed on fresh connections."""
+    aloha.set_mode(mode, delay_s=1.0)
+    s = hola(args=["--aloha-url", aloha.url, "--no-tracing", "--feign-log", "none", "--aloha-pipeline", "4",
+                   "--feign-retry", "off", "-Dhystrix.threadpool.default.coreSize=64",
+                   "-Dhystrix.command.default.circuitBreaker.enabled=false"], env={"HOSTNAME": "h"}, threads=1)
+    t0 = time.monotonic()
+    res = _concurrent_chains(s, 8)
+    assert all(st == 200 and body == ["Hola de h", FALLBACK] for st, body in res), res
+    assert time.monotonic() - t0 < 3.0
+    aloha.set_mode("ok")
+    res = _concurrent_chains(s, 8)
+    assert all(st == 200 and body[1] == "Aloha mai aloha-1" for st, body in res), res
