@@ -15,6 +15,7 @@
 #   latency            BASELINE config 2 (1 connection) and the open-loop latency curve
 #   chain              two-hop chaining bench (loadgen -> hola A -> hola B)
 #   chainab [REPS]     chaining with Feign BASIC logging on/off, this server vs. PREV_BIN
+#   chainpipe [REPS]   chaining with --aloha-pipeline 8 vs. one request per connection
 #   cpuprof            sampled CPU profiles (hola --cpu-profile) of the headline and of chaining
 #   tracing            headline without a collector, with the native Zipkin sink (default 1000-span
 #                      export budget, and unbounded), and with tracing off
@@ -107,6 +108,20 @@ chainab)
       timeout -k 10 120 python bench/chain_bench.py --duration 8 --feign-log "$log" ${exe:+--exe-a "$exe"} \
         --out "$OUT/${label}_${rep}.json" > "$OUT/${label}_${rep}.log" 2>&1 || exit 1
       python3 -c "import json; d=json.load(open('$OUT/${label}_${rep}.json')); print('$label', $rep, d['rps'], d['p50_ms'], d['p99_ms'], d['cpu_us_per_req']['A'], d['user_share']['A'])" \
+        >> "$OUT/summary.txt"
+    done
+  done
+  cat "$OUT/summary.txt"
+  ;;
+chainpipe)
+  # chaining with A's aloha calls pipelined (--aloha-pipeline 8) vs one request per connection
+  # (the default), Feign BASIC logging on, REPS interleaved rounds
+  REPS=${1:-3}
+  for rep in $(seq 1 "$REPS"); do
+    for pl in 1 8; do
+      timeout -k 10 120 python bench/chain_bench.py --duration 8 --feign-log basic --aloha-pipeline $pl \
+        --out "$OUT/pipe${pl}_${rep}.json" > "$OUT/pipe${pl}_${rep}.log" 2>&1 || exit 1
+      python3 -c "import json; d=json.load(open('$OUT/pipe${pl}_${rep}.json')); print('pipe$pl', $rep, d['rps'], d['p50_ms'], d['p99_ms'], d['cpu_us_per_req']['A'], d['cpu_us_per_req']['B'], d['errors'], d['body_mismatch'])" \
         >> "$OUT/summary.txt"
     done
   done
