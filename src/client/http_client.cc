@@ -632,15 +632,17 @@ void ClientPool::destroy(Conn* c) {
 
 void ClientPool::cancel(uint64_t id) {
   if (auto pt = pactive_.find(id); pt != pactive_.end()) {
-    // Its response will still arrive in order on the shared connection: read and dropped.
-    for (auto& p : pt->second.conn->q)
+    // Abandoned (timed out) on a shared connection: its answer may never come, and every call
+    // queued behind it would wait for it. The socket is given up, as on the plain path, and
+    // the other calls waiting on it are re-sent on fresh connections.
+    PConn* c = pt->second.conn;
+    for (auto& p : c->q)
       if (p.id == id) {
         p.abandoned = true;
         p.cb = nullptr;
       }
     pactive_.erase(pt);
-    if (!read_fifo_.q.empty()) pop_finished(read_fifo_);
-    if (!connect_fifo_.q.empty()) pop_finished(connect_fifo_);
+    pfail(c, "SocketException: connection abandoned");
     return;
   }
   auto it = active_.find(id);

@@ -697,3 +697,18 @@ def test_pipelined_failures(hola, aloha, mode, expect_fallback):
     aloha.set_mode("ok")
     res = _concurrent_chains(s, 8)
     assert all(st == 200 and body[1] == "Aloha mai aloha-1" for st, body in res), res
+
+
+def test_pipelined_connection_is_not_reused_after_a_timeout(hola, aloha):
+    """A call that times out on a pipelined connection gives the connection up: calls made
+    afterwards do not queue behind the answer that never came."""
+    s = hola(args=["--aloha-url", aloha.url, "--no-tracing", "--feign-log", "none", "--aloha-pipeline", "8",
+                   "--feign-retry", "off", "-Dhystrix.command.default.circuitBreaker.enabled=false"],
+             env={"HOSTNAME": "h"}, threads=1)
+    assert chain(s)[1] == "Aloha mai aloha-1"
+    aloha.set_mode("slow", delay_s=5.0)
+    assert chain(s)[1] == FALLBACK  # 600 ms
+    aloha.set_mode("ok")
+    t0 = time.monotonic()
+    assert chain(s)[1] == "Aloha mai aloha-1"
+    assert time.monotonic() - t0 < 0.5
