@@ -289,7 +289,7 @@ def test_feign_read_timeout_when_hystrix_timeout_is_disabled(hola, aloha):
     assert b'event="FAILURE"} 1' in m and b"TIMEOUT" not in m
     assert b'hola_aloha_retries_total{kind="feign"} 1' in m
     assert b'hola_hystrix_pool_active{command="aloha"} 0' in m
-    assert "<--- ERROR SocketTimeoutException: Read timed out" in s.log()
+    assert "<--- ERROR SocketTimeoutException: Read timed out" in _wait_log(s, "<--- ERROR SocketTimeoutException", 1)
 
 
 def _metric(s, name) -> int:
@@ -317,7 +317,7 @@ def test_read_timeouts_do_not_pile_up_timers(hola, aloha):
     t0 = time.monotonic()
     assert chain(s2)[1] == FALLBACK
     assert 0.15 <= time.monotonic() - t0 < 1.0
-    assert "<--- ERROR SocketTimeoutException: Read timed out" in s2.log()
+    assert "<--- ERROR SocketTimeoutException: Read timed out" in _wait_log(s2, "<--- ERROR SocketTimeoutException", 1)
 
 
 def test_feign_connect_timeout(hola):
@@ -335,8 +335,9 @@ def test_feign_connect_timeout(hola):
         assert chain(s)[1] == FALLBACK
         took = time.monotonic() - t0
         assert 0.65 <= took < 1.5, took  # 300 ms, 150 ms sleep, 300 ms
-        assert "<--- ERROR ConnectTimeoutException: Connect to 127.0.0.1:%d failed: connect timed out" % srv.getsockname()[1] \
-            in s.log(), s.log()
+        line = "<--- ERROR ConnectTimeoutException: Connect to 127.0.0.1:%d failed: connect timed out" % srv.getsockname()[1]
+        log = _wait_log(s, line, 1)
+        assert line in log, log
         assert b'hola_aloha_retries_total{kind="feign"} 1' in s.get("/metrics")[2]
     finally:
         filler.close()

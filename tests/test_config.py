@@ -151,6 +151,9 @@ def test_hot_reload_in_place_edit(hola, tmp_path):
     assert s.get("/api/hola")[2] == b"one h"
     conf.write_text("hello=two %s\n")
     assert wait_body(s, b"two h") == b"two h"
+    deadline = time.monotonic() + 3  # the log writer thread may lag the response
+    while "New value two %s for key hello" not in s.log() and time.monotonic() < deadline:
+        time.sleep(0.05)
     assert "New value two %s for key hello" in s.log()
 
 

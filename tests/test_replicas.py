@@ -14,6 +14,16 @@ from hola_amd.parallel.replicas import ReplicaSet, RRProxy
 from hola_amd.utils.net import http_get
 
 
+
+def _log_has(proc, text: str, timeout: float = 3.0) -> bool:
+    """The log writer thread may lag the event that logged: wait for the line."""
+    deadline = time.monotonic() + timeout
+    while text not in proc.log():
+        if time.monotonic() > deadline:
+            return False
+        time.sleep(0.05)
+    return True
+
 def greeting_via(port):
     st, _, body = http_get("127.0.0.1", port, "/api/hola")
     assert st == 200
@@ -35,7 +45,7 @@ def test_proxy_skips_dead_replica_and_recovers():
             time.sleep(0.3)  # health checker marks it DOWN
             seen = {greeting_via(px.port) for _ in range(8)}
             assert seen == {"Hola de replica-0"}
-            assert "is DOWN" in px.log()
+            assert _log_has(px, "is DOWN")
             rs.procs[1] = rs._spawn(1)  # platform restarts the pod
             time.sleep(0.3)
             seen = {greeting_via(px.port) for _ in range(8)}
@@ -100,7 +110,7 @@ def test_proxy_fails_over_on_refused_connect():
             time.sleep(0.1)
             seen = {greeting_via(px.port) for _ in range(6)}
             assert seen == {"Hola de replica-1"}
-            assert "is DOWN" in px.log()
+            assert _log_has(px, "is DOWN")
     finally:
         rs.stop()
 
@@ -280,7 +290,7 @@ def _exhaust_fds_then_recover(pid: int, port: int, fd_limit: int):
 def test_proxy_backs_off_at_fd_limit():
     with ReplicaSet(1, threads_per_replica=1, supervise=False) as rs, RRProxy(rs.targets) as px:
         _exhaust_fds_then_recover(px.proc.pid, px.port, 48)
-        assert "fd limit" in px.log()
+        assert _log_has(px, "fd limit")
         assert "is DOWN" not in px.log()  # running out of local fds says nothing about a backend
 
 
