@@ -19,7 +19,7 @@
 #   cpuprof            sampled CPU profiles (hola --cpu-profile) of the headline and of chaining
 #   tracing            headline without a collector, with the native Zipkin sink (default 1000-span
 #                      export budget, and unbounded), and with tracing off
-#   soak MINUTES       mixed-load soak sampling RSS and FDs
+#   soak MINUTES [ARGS] mixed-load soak sampling RSS and FDs (ARGS go to bench/soak.py)
 #
 # Every GPU-box step runs under its own `timeout -k`, steps are chained with &&, and the
 # script stops at the first failure (no retries).
@@ -149,8 +149,8 @@ tracing)
   timeout -k 10 300 python bench.py --steps 15 --warmup 3 --c1-seconds 0 --no-tracing > "$OUT/tracing_off.json" 2>> "$OUT/err.log"
   ;;
 soak)
-  MIN=${1:-5}
-  timeout -k 10 $((MIN * 60 + 150)) python -u bench/soak.py --minutes "$MIN" --sample-s 30 \
+  MIN=${1:-5}; shift || true
+  timeout -k 10 $((MIN * 60 + 150)) python -u bench/soak.py --minutes "$MIN" --sample-s 30 "$@" \
     --out "$OUT/soak.json" > "$OUT/soak.log" 2>&1
   ;;
 *)

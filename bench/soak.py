@@ -33,6 +33,9 @@ ap.add_argument("--minutes", type=float, default=5)
 ap.add_argument("--sample-s", type=float, default=10)
 ap.add_argument("--feign-log", default="basic", choices=("basic", "none"),
                 help="the replica's Feign logging (basic = the default, two log-ring lines per aloha call)")
+ap.add_argument("--aloha-pipeline", type=int, default=1, help="the replica's --aloha-pipeline")
+ap.add_argument("--chain-clients", type=int, default=1,
+                help="concurrent /api/hola-chaining clients (several keep pipelined connections busy)")
 ap.add_argument("--out", default="")
 a = ap.parse_args()
 
@@ -46,6 +49,7 @@ samples, errors = [], []
 
 with FakeAloha() as aloha, HolaProcess(
         args=["--aloha-url", aloha.url, "--feign-log", a.feign_log, f"-Dconf={conf}",
+              "--aloha-pipeline", str(a.aloha_pipeline),
               "-Dhystrix.command.default.circuitBreaker.sleepWindowInMilliseconds=1000",
               "--hystrix-stream-stall-ms", "5000"],
         env={"HOSTNAME": "soak"}, threads=len(srv), cpu_list=format_cpu_list(srv), log_level="warn",
@@ -53,8 +57,20 @@ with FakeAloha() as aloha, HolaProcess(
         stderr_path=os.devnull if a.feign_log == "basic" else None) as s:
     pid = s.proc.pid
 
+    def chaining_client():
+        while not stop.is_set():
+            try:
+                st, _, _ = http_get("127.0.0.1", s.port, "/api/hola-chaining", timeout=5)
+                if st != 200:
+                    errors.append(("chaining", st))
+            except OSError as e:
+                errors.append(("chaining", repr(e)))
+
     def chaining():
         modes = ["ok", "slow", "error", "ok", "garbage", "close", "unavailable", "ok"]
+        extra = [threading.Thread(target=chaining_client, daemon=True) for _ in range(a.chain_clients - 1)]
+        for t in extra:
+            t.start()
         i = 0
         while not stop.is_set():
             aloha.set_mode(modes[i % len(modes)], delay_s=1.0)
@@ -147,7 +163,8 @@ out = {
     "rss_kb_first": first["rss_kb"], "rss_kb_last": last["rss_kb"], "rss_kb_max": max(x["rss_kb"] for x in samples),
     "fds_first": first["fds"], "fds_last": last["fds"], "stream": stream_stats,
     "timers_max": max(x.get("timers", -1) for x in samples), "timers_last": last.get("timers", -1),
-    "log_dropped_last": last.get("log_dropped", -1), "feign_log": a.feign_log, "samples": samples,
+    "log_dropped_last": last.get("log_dropped", -1), "feign_log": a.feign_log,
+    "aloha_pipeline": a.aloha_pipeline, "chain_clients": a.chain_clients, "samples": samples,
 }
 print(json.dumps({k: v for k, v in out.items() if k != "samples"}))
 if a.out:
