@@ -608,7 +608,9 @@ void ClientPool::finish(Conn* c, ClientResult&& r, bool reusable) {
   if (!connect_fifo_.q.empty()) pop_finished(connect_fifo_);
   Callback cb = std::move(c->cb);
   c->cb = nullptr;
-  if (reusable && c->fd >= 0 && idle_.size() < max_idle_) {
+  // With pipelining on, new requests never take plain idle connections (only re-sends use
+  // plain ones), so keeping them would only hold sockets open.
+  if (reusable && c->fd >= 0 && idle_.size() < max_idle_ && pipeline_ <= 1) {
     c->st = Conn::kIdle;
     c->in.clear();
     c->set_interest(EPOLLIN | EPOLLRDHUP);

@@ -713,3 +713,25 @@ def test_pipelined_connection_is_not_reused_after_a_timeout(hola, aloha):
     t0 = time.monotonic()
     assert chain(s)[1] == "Aloha mai aloha-1"
     assert time.monotonic() - t0 < 0.5
+
+
+def test_pipelined_mode_keeps_no_idle_plain_connections(hola, aloha):
+    """Calls re-sent after a pipelined connection is given up run on plain connections; with
+    pipelining on nothing would reuse those afterwards, so they are closed, not pooled."""
+    import os
+    s = hola(args=["--aloha-url", aloha.url, "--no-tracing", "--feign-log", "none", "--aloha-pipeline", "4",
+                   "--feign-retry", "off", "-Dhystrix.threadpool.default.coreSize=64",
+                   "-Dhystrix.command.default.circuitBreaker.enabled=false"], threads=1)
+    fds = lambda: len(os.listdir(f"/proc/{s.proc.pid}/fd"))  # noqa: E731
+    _concurrent_chains(s, 8)
+    base = fds()
+    for _ in range(4):
+        # one slow answer at the head of a pipelined connection: its call times out and the
+        # calls behind it are re-sent on fresh plain connections, where they succeed
+        aloha.set_mode("slow", delay_s=0.8)
+        threading.Thread(target=lambda: s.get("/api/hola-chaining", timeout=10), daemon=True).start()
+        time.sleep(0.05)
+        aloha.set_mode("ok")
+        _concurrent_chains(s, 8)
+        time.sleep(0.8)
+    assert fds() <= base + 4, (base, fds())
