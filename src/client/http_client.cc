@@ -805,7 +805,12 @@ void ClientPool::PConn::do_read() {
         return;
       }
     }
-    if (used) in.erase(0, used);
+    if (used) {
+      in.erase(0, used);
+      // answered requests leave the deadline FIFOs (as ClientPool::finish does for plain ones)
+      if (!pool->read_fifo_.q.empty()) pool->pop_finished(pool->read_fifo_);
+      if (!pool->connect_fifo_.q.empty()) pool->pop_finished(pool->connect_fifo_);
+    }
     if (eof || (q.empty() && !in.empty())) {
       // the peer closed, or sent bytes nobody asked for: the connection is done
       pool->pfail(this, in.empty() || q.empty() ? "NoHttpResponseException: connection closed"

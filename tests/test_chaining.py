@@ -700,6 +700,19 @@ def test_pipelined_failures(hola, aloha, mode, expect_fallback):
     assert all(st == 200 and body[1] == "Aloha mai aloha-1" for st, body in res), res
 
 
+def test_pipelined_read_timeouts_do_not_pile_up(hola, aloha):
+    """Pipelined calls with the Hystrix timeout disabled are guarded by Feign's read timeout
+    (one FIFO of deadlines, one loop timer): answered calls leave the FIFO, and the pending
+    loop timers do not grow with the call count."""
+    s = hola(args=["--aloha-url", aloha.url, "--no-tracing", "--feign-log", "none", "--aloha-pipeline", "4",
+                   "-Dhystrix.command.default.execution.timeout.enabled=false",
+                   "-Dhystrix.threadpool.default.coreSize=64"], threads=1)
+    idle = _metric(s, "hola_event_loop_timers")
+    for _ in range(10):
+        assert all(st == 200 for st, _ in _concurrent_chains(s, 8))
+    assert _metric(s, "hola_event_loop_timers") <= idle + 4
+
+
 def test_pipelined_connection_is_not_reused_after_a_timeout(hola, aloha):
     """A call that times out on a pipelined connection gives the connection up: calls made
     afterwards do not queue behind the answer that never came."""
