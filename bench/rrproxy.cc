@@ -13,7 +13,16 @@
 // and stops reading the other side until they are gone (backpressure). Accepted sockets are
 // handed to a loop in the client's L3 domain (SO_INCOMING_CPU), as the server does. A FIN
 // is passed on as a half-close; sessions silent for --idle-timeout-ms are closed.
+//
+// Service mode (`python -m hola_amd apply`, the local manifest executor): --endpoints-file F
+// takes the backend set from F (one host:port per line), re-read whenever it changes; the
+// executor writes the Ready pods there, the role of the Endpoints object that kube-proxy
+// follows. --health-ms 0 turns the proxy's own probing off (kube-proxy does not probe), and
+// --no-failover makes a connection to a backend that refuses fail as it does through
+// kube-proxy's DNAT rules, instead of being retried on the next backend. Sessions keep their
+// backend when it leaves the set (conntrack keeps established flows).
 #include <errno.h>
+#include <sys/stat.h>
 #include <signal.h>
 #include <sys/socket.h>
 #include <unistd.h>
@@ -24,7 +33,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <fstream>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -47,17 +58,100 @@ struct Backend {
   std::atomic<uint64_t> picked{0};
 };
 
+// Every backend ever named, never freed (sessions and the current set point into it).
 std::vector<std::unique_ptr<Backend>> g_backends;
+std::mutex g_backends_mu;  // guards g_backends growth (the endpoints reloader)
+// The set new connections are dealt over. Replaced whole on an endpoints change; an old set
+// is kept (a few pointers) because a loop thread may still be reading it.
+struct BackendSet {
+  std::vector<Backend*> list;
+};
+std::atomic<const BackendSet*> g_set{nullptr};
+std::vector<std::unique_ptr<BackendSet>> g_sets;  // owner of every set published
 std::atomic<uint64_t> g_rr{0};
 std::atomic<bool> g_stop{false};
+bool g_failover = true;
+
+const BackendSet& current_set() { return *g_set.load(std::memory_order_acquire); }
 
 Backend* pick() {
-  const size_t n = g_backends.size();
+  const BackendSet& set = current_set();
+  const size_t n = set.list.size();
   for (size_t k = 0; k < n; ++k) {
-    Backend* b = g_backends[g_rr.fetch_add(1, std::memory_order_relaxed) % n].get();
+    Backend* b = set.list[g_rr.fetch_add(1, std::memory_order_relaxed) % n];
     if (b->healthy.load(std::memory_order_relaxed)) return b;
   }
   return nullptr;
+}
+
+Backend* backend_for(const std::string& host, int port) {
+  std::lock_guard<std::mutex> g(g_backends_mu);
+  for (auto& b : g_backends)
+    if (b->host == host && b->port == port) return b.get();
+  auto b = std::make_unique<Backend>();
+  b->host = host;
+  b->port = port;
+  std::string err;
+  if (!resolve_host(host, port, &b->addr, &b->len, &err)) {
+    fprintf(stderr, "rrproxy: %s\n", err.c_str());
+    return nullptr;
+  }
+  g_backends.push_back(std::move(b));
+  return g_backends.back().get();
+}
+
+// "h:p,h:p" or one h:p per line (IPv6 as [addr]:port or addr:port split at the last colon).
+bool parse_backends(const std::string& text, std::vector<Backend*>* out) {
+  size_t i = 0;
+  while (i < text.size()) {
+    size_t j = text.find_first_of(",\n", i);
+    if (j == std::string::npos) j = text.size();
+    std::string t = text.substr(i, j - i);
+    i = j + 1;
+    while (!t.empty() && (t.back() == ' ' || t.back() == '\r')) t.pop_back();
+    while (!t.empty() && t.front() == ' ') t.erase(0, 1);
+    if (t.empty() || t[0] == '#') continue;
+    size_t colon = t.rfind(':');
+    if (colon == std::string::npos) return false;
+    std::string host = t.substr(0, colon);
+    if (host.size() > 2 && host.front() == '[' && host.back() == ']') host = host.substr(1, host.size() - 2);
+    Backend* b = backend_for(host, atoi(t.substr(colon + 1).c_str()));
+    if (!b) return false;
+    if (std::find(out->begin(), out->end(), b) == out->end()) out->push_back(b);
+  }
+  return true;
+}
+
+void publish_set(std::vector<Backend*> list) {
+  auto set = std::make_unique<BackendSet>();
+  set->list = std::move(list);
+  for (Backend* b : set->list) b->healthy.store(true);  // listed = Ready (the executor probed it)
+  g_set.store(set.get(), std::memory_order_release);
+  g_sets.push_back(std::move(set));
+}
+
+// Follows --endpoints-file: re-read when its inode, size or mtime changes (the writer
+// replaces it with a rename, so a reader never sees half a file).
+void endpoints_loop(std::string path) {
+  struct stat last {};
+  bool have = false;
+  while (!g_stop.load()) {
+    struct stat st {};
+    if (stat(path.c_str(), &st) == 0 &&
+        (!have || st.st_ino != last.st_ino || st.st_size != last.st_size || st.st_mtim.tv_sec != last.st_mtim.tv_sec ||
+         st.st_mtim.tv_nsec != last.st_mtim.tv_nsec)) {
+      std::ifstream f(path);
+      std::string text((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+      std::vector<Backend*> list;
+      if (parse_backends(text, &list)) {
+        publish_set(std::move(list));
+        fprintf(stderr, "rrproxy: endpoints now %zu backends\n", current_set().list.size());
+        last = st;
+        have = true;
+      }
+    }
+    std::this_thread::sleep_for(std::chrono::milliseconds(10));
+  }
 }
 
 void mark_down(Backend* b, int err) {
@@ -70,7 +164,8 @@ void mark_down(Backend* b, int err) {
 // before it completes wait for the socket's OUT edge, and a refusal reported then fails over
 // from Session::on_event.
 int connect_backend(Backend** chosen, bool* in_progress) {
-  for (size_t tries = 0; tries < g_backends.size(); ++tries) {
+  const size_t n = g_failover ? current_set().list.size() : 1;
+  for (size_t tries = 0; tries < n; ++tries) {
     Backend* b = pick();
     if (!b) return -1;
     int fd = connect_nonblocking(b->addr, b->len, in_progress);
@@ -82,6 +177,7 @@ int connect_backend(Backend** chosen, bool* in_progress) {
     // Out of local fds, memory or ephemeral ports: the next backend would fail the same
     // way, and none of them is at fault.
     if (is_local_resource_error(errno)) return -1;
+    if (!g_failover) return -1;  // kube-proxy: the client's connection fails with the backend's
     mark_down(b, errno);
   }
   return -1;
@@ -262,12 +358,12 @@ bool Session::backend_connected(uint32_t ev) {
     connecting = false;
     return true;
   }
-  mark_down(backend, soerr ? soerr : ECONNRESET);
+  if (g_failover) mark_down(backend, soerr ? soerr : ECONNRESET);
   EventLoop& l = owner->loop();
   l.del(bfd);
   ::close(bfd);
   bfd = -1;
-  if (++failovers > int(g_backends.size())) return false;
+  if (!g_failover || ++failovers > int(current_set().list.size())) return false;
   bool inprog = false;
   bfd = connect_backend(&backend, &inprog);
   if (bfd < 0) return false;
@@ -387,7 +483,7 @@ struct Acceptor : EventLoop::Handler {
 
 void health_loop(int interval_ms) {
   while (!g_stop.load()) {
-    for (auto& b : g_backends) {
+    for (Backend* b : current_set().list) {
       client::Url u;
       u.host = b->host;
       u.port = b->port;
@@ -410,7 +506,7 @@ void health_loop(int interval_ms) {
 int main(int argc, char** argv) {
   int port = 8080, threads = 1, health_ms = 500, busy_poll_us = 0, busy_poll_pause = 0, idle_timeout_ms = 60000;
   bool steer = true;
-  std::string backends, cpu_list, host = "0.0.0.0", port_file;
+  std::string backends, cpu_list, host = "0.0.0.0", port_file, endpoints_file;
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     auto val = [&]() -> std::string {
@@ -428,37 +524,26 @@ int main(int argc, char** argv) {
     else if (a == "--busy-poll-pause") busy_poll_pause = atoi(val().c_str());
     else if (a == "--no-steer") steer = false;
     else if (a == "--idle-timeout-ms") idle_timeout_ms = atoi(val().c_str());
+    else if (a == "--endpoints-file") endpoints_file = val();
+    else if (a == "--no-failover") g_failover = false;
     else {
       fprintf(stderr,
               "usage: hola_rrproxy --backends h:p,h:p.. [--port N] [--host H] [--threads N] [--cpu-list L]\n"
               "                    [--health-ms N] [--busy-poll-us N [--busy-poll-pause P]] [--no-steer] [--port-file F]\n"
-              "                    [--idle-timeout-ms N (default 60000, 0 = never)]\n");
+              "                    [--idle-timeout-ms N (default 60000, 0 = never)]\n"
+              "                    [--endpoints-file F (backend set re-read on change)] [--no-failover]\n"
+              "                    (--health-ms 0: no probing of backends)\n");
       return 2;
     }
   }
   signal(SIGPIPE, SIG_IGN);
-  size_t i = 0;
-  while (i < backends.size()) {
-    size_t j = backends.find(',', i);
-    if (j == std::string::npos) j = backends.size();
-    std::string t = backends.substr(i, j - i);
-    i = j + 1;
-    size_t colon = t.rfind(':');
-    if (colon == std::string::npos) return 2;
-    auto b = std::make_unique<Backend>();
-    b->host = t.substr(0, colon);
-    b->port = atoi(t.substr(colon + 1).c_str());
-    std::string err;
-    if (!resolve_host(b->host, b->port, &b->addr, &b->len, &err)) {
-      fprintf(stderr, "rrproxy: %s\n", err.c_str());
-      return 2;
-    }
-    g_backends.push_back(std::move(b));
-  }
-  if (g_backends.empty()) {
-    fprintf(stderr, "rrproxy: --backends required\n");
+  std::vector<Backend*> initial;
+  if (!parse_backends(backends, &initial)) return 2;
+  if (initial.empty() && endpoints_file.empty()) {
+    fprintf(stderr, "rrproxy: --backends or --endpoints-file required\n");
     return 2;
   }
+  publish_set(std::move(initial));
   if (threads < 1) threads = 1;
   std::vector<int> cpus;
   if (!cpu_list.empty() && !parse_cpu_list(cpu_list, &cpus)) {
@@ -484,7 +569,7 @@ int main(int argc, char** argv) {
     rename((port_file + ".tmp").c_str(), port_file.c_str());
   }
   fprintf(stderr, "rrproxy: listening on %s:%d -> %zu backends, %d threads\n", host.c_str(), lo.port,
-          g_backends.size(), threads);
+          current_set().list.size(), threads);
 
   std::vector<std::unique_ptr<ProxyLoop>> loops;
   for (int t = 0; t < threads; ++t)
@@ -499,7 +584,10 @@ int main(int argc, char** argv) {
   sigaddset(&sigs, SIGTERM);
   sigaddset(&sigs, SIGINT);
   pthread_sigmask(SIG_BLOCK, &sigs, nullptr);
-  std::thread hc(health_loop, health_ms);
+  std::thread hc;
+  if (health_ms > 0) hc = std::thread(health_loop, health_ms);
+  std::thread ep;
+  if (!endpoints_file.empty()) ep = std::thread(endpoints_loop, endpoints_file);
   std::vector<std::thread> ws;
   for (auto& l : loops) ws.emplace_back([p = l.get()] { p->run(); });
   int sig;
@@ -507,7 +595,8 @@ int main(int argc, char** argv) {
   g_stop.store(true);
   for (auto& l : loops) l->loop().stop();
   for (auto& w : ws) w.join();
-  hc.join();
+  if (hc.joinable()) hc.join();
+  if (ep.joinable()) ep.join();
   for (auto& l : loops) l->close_all();
   ::close(acc.fd);
   for (auto& b : g_backends)

@@ -6,8 +6,9 @@
   connection) / ``unavailable`` (HTTP 503 with ``Retry-After: <retry_after>``) / ``empty``
   (200, empty body) / ``json_null`` (200, ``null``) / ``no_content`` (204) /
   ``close_delimited`` (no Content-Length, body ends at EOF) / ``drop_idle`` (keep-alive
-  response, then the socket closes while idle). Records every request's headers so tests can
-  check B3 propagation.
+  response, then the socket closes while idle) / ``bad_status`` (an invalid HTTP status line:
+  no valid response head) / ``bad_chunk`` (a valid 200 head, then a malformed chunk size).
+  Records every request's headers so tests can check B3 propagation.
 * :class:`FakeZipkin` — a span collector recording POST /api/v1/spans and /api/v2/spans.
 """
 from __future__ import annotations
@@ -72,6 +73,15 @@ class _AlohaHandler(BaseHTTPRequestHandler):
         if mode == "close":
             self.close_connection = True
             self.connection.shutdown(socket.SHUT_RDWR)
+            return
+        if mode == "bad_status":  # HTTP-level fault: no parseable status line
+            self.wfile.write(b"HTTP/1.1 2x0 Broken\r\nContent-Length: 2\r\n\r\n[]")
+            self.wfile.flush()
+            return
+        if mode == "bad_chunk":  # a valid head, then framing no HTTP/1.1 parser accepts
+            self.wfile.write(b"HTTP/1.1 200 OK\r\nContent-Type: application/json\r\n"
+                             b"Transfer-Encoding: chunked\r\n\r\nzz\r\n[]\r\n0\r\n\r\n")
+            self.wfile.flush()
             return
         if self.path != "/api/aloha-chaining":
             body, status = b"not found", 404

@@ -38,7 +38,7 @@ struct HolaApp::WorkerCache {
   uint64_t date_version = ~0ull;
   std::shared_ptr<const Content> content;
   // [keep_alive][head]
-  Prepared hola[2][2], health[2][2], swagger[2][2], swagger_yaml[2][2], index[2][2], viewer[2][2];
+  Prepared hola[2][2], health[2][2], health_unready[2][2], swagger[2][2], swagger_yaml[2][2], index[2][2], viewer[2][2];
   Prepared chaining_fallback[2][2];
   Prepared api_not_found[2], not_found[2][2], api_not_allowed[2], not_allowed[2], not_acceptable[2],
       api_options[2], static_options[2], server_error[2][2];
@@ -180,6 +180,10 @@ void HolaApp::refresh(http::Worker& w, WorkerCache& wc) {
         h.content_type = kTextPlain;
         h.body = "I'm ok";  // HolaResource.java:85
         wc.health[ka][head] = build_response(h, date);
+        ResponseSpec hu = h;  // readiness failing while the replica terminates
+        hu.status = 503;
+        hu.body = "shutting down";
+        wc.health_unready[ka][head] = build_response(hu, date);
         ResponseSpec sw = h;
         sw.content_type = kJson;
         sw.body = swagger ? swagger->view() : std::string_view("{}");
@@ -202,7 +206,7 @@ void HolaApp::refresh(http::Worker& w, WorkerCache& wc) {
         nf.body = kUndertowNotFound;
         wc.not_found[ka][head] = build_response(nf, date);
         for (auto* p : {&wc.hola[ka][head], &wc.server_error[ka][head], &wc.chaining_fallback[ka][head],
-                        &wc.health[ka][head], &wc.swagger[ka][head], &wc.swagger_yaml[ka][head], &wc.index[ka][head],
+                        &wc.health[ka][head], &wc.health_unready[ka][head], &wc.swagger[ka][head], &wc.swagger_yaml[ka][head], &wc.index[ka][head],
                         &wc.viewer[ka][head],
                         &wc.not_found[ka][head]})
           wc.all.push_back(p);
@@ -319,7 +323,9 @@ void HolaApp::on_request(http::Connection& c, const http::Request& r) {
   WorkerCache& wc = cache(w);
   if (__builtin_expect(wc.gen != gen_.load(std::memory_order_relaxed) || wc.date_version != w.date_version(), 0))
     refresh(w, wc);
-  const int ka = r.keep_alive ? 1 : 0;
+  // While the server terminates or drains, every response closes its connection
+  // (`Connection: close`), so kept-alive clients reconnect elsewhere between requests.
+  const int ka = r.keep_alive && !w.server().closing() ? 1 : 0;
   if (!ka) c.close_after_response();
 
   std::string_view path = r.path;
@@ -376,7 +382,9 @@ void HolaApp::on_request(http::Connection& c, const http::Request& r) {
           c.send(wc.hola[ka][head].view());
         }
       } else if (route == kHealth) {
-        c.send(wc.health[ka][head].view());
+        // Readiness fails from the first termination signal on (--shutdown-delay-ms): the
+        // Service stops routing new connections here while this replica still serves.
+        c.send((w.server().terminating() ? wc.health_unready : wc.health)[ka][head].view());
       } else if (route == kSwagger) {
         c.send(wc.swagger[ka][head].view());
       } else if (route == kSwaggerYaml) {
@@ -424,7 +432,7 @@ void HolaApp::on_request(http::Connection& c, const http::Request& r) {
 }
 
 void HolaApp::handle_chaining(http::Connection& c, const http::Request& r, WorkerCache& wc, bool traced) {
-  const int ka = r.keep_alive ? 1 : 0;
+  const int ka = r.keep_alive && !c.worker().server().closing() ? 1 : 0;
   const int head = r.method == "HEAD" ? 1 : 0;
   tracing::ServerSpan span;
   if (traced) span = tracer_->begin_server(c.worker().index(), r);
@@ -447,8 +455,10 @@ void HolaApp::handle_chaining(http::Connection& c, const http::Request& r, Worke
   std::shared_ptr<const Content> content = wc.content;
   HolaApp* self = this;
   chainer_->call(c.worker(), traced ? &span.ctx : nullptr,
-                 [self, conn, content, ka, head, traced, span, t0](const ChainResult& res) {
+                 [self, conn, content, ka_req = ka, head, traced, span, t0](const ChainResult& res) {
                    http::Worker& w = conn->worker();
+                   // termination may have begun while the call was parked
+                   const int ka = ka_req && !w.server().closing() ? 1 : 0;
                    WorkerCache& wc = self->cache(w);
                    bool answered = false;
                    if (!conn->closed() && (res.null_list || res.error)) {

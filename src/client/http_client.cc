@@ -224,6 +224,7 @@ void ClientPool::Conn::on_event(uint32_t ev) {
       return;
     }
     st = kWriting;
+    pool->arm_read_deadline(id, serial);
   }
   if (st == kWriting) {
     do_write();
@@ -523,7 +524,7 @@ void ClientPool::expire(DeadlineFifo& f) {
         pfail(pc, "SocketTimeoutException: Read timed out", d.id);
       else if (pc->connecting)
         pfail(pc, "ConnectTimeoutException: Connect to " + target_.host + ":" + std::to_string(target_.port) +
-                      " failed: connect timed out", d.id);
+                      " failed: connect timed out", 0, true, false);
       continue;
     }
     Conn* c = active_.find(d.id)->second;
@@ -547,10 +548,6 @@ void ClientPool::pop_finished(DeadlineFifo& f) {
 void ClientPool::start_on(Conn* c, uint64_t id, std::string req, Callback cb, bool reused) {
   c->id = id;
   c->serial = next_serial_++;
-  if (read_timeout_ms_) {
-    const int rt = read_timeout_ms_->load(std::memory_order_relaxed);
-    if (rt > 0) push_deadline(read_fifo_, rt, id, c->serial);
-  }
   c->cb = std::move(cb);
   c->out = std::move(req);
   c->off = 0;
@@ -560,6 +557,7 @@ void ClientPool::start_on(Conn* c, uint64_t id, std::string req, Callback cb, bo
   active_[id] = c;
   if (reused) {
     c->st = Conn::kWriting;
+    arm_read_deadline(id, c->serial);
     c->do_write();
     return;
   }
@@ -599,7 +597,19 @@ void ClientPool::start_on(Conn* c, uint64_t id, std::string req, Callback cb, bo
   loop_.add(c->fd, EPOLLOUT, c);
   c->st = inprog ? Conn::kConnecting : Conn::kWriting;
   if (inprog && connect_timeout_ms_ > 0) push_deadline(connect_fifo_, connect_timeout_ms_, id, c->serial);
-  if (!inprog) c->do_write();
+  if (!inprog) {
+    arm_read_deadline(id, c->serial);
+    c->do_write();
+  }
+}
+
+void ClientPool::arm_read_deadline(uint64_t id, uint64_t serial) {
+  // Feign's read timeout runs once the socket is connected (a connect has its own timeout):
+  // armed when the request starts going out, never while the connect is still pending, so a
+  // slow connect cannot leave the request unguarded afterwards.
+  if (!read_timeout_ms_) return;
+  const int rt = read_timeout_ms_->load(std::memory_order_relaxed);
+  if (rt > 0) push_deadline(read_fifo_, rt, id, serial);
 }
 
 void ClientPool::finish(Conn* c, ClientResult&& r, bool reusable) {
@@ -698,10 +708,7 @@ bool ClientPool::get_pipelined(uint64_t id, std::string& req, Callback& cb) {
   c->out += req;
   c->q.push_back({id, serial, std::move(req), std::move(cb)});
   pactive_[id] = {c, serial};
-  if (read_timeout_ms_) {
-    const int rt = read_timeout_ms_->load(std::memory_order_relaxed);
-    if (rt > 0) push_deadline(read_fifo_, rt, id, serial);
-  }
+  if (!c->connecting) arm_read_deadline(id, serial);
   if (c->connecting && connect_timeout_ms_ > 0) push_deadline(connect_fifo_, connect_timeout_ms_, id, serial);
   if (!c->dirty) {
     c->dirty = true;
@@ -731,10 +738,13 @@ void ClientPool::PConn::on_event(uint32_t ev) {
     socklen_t sl = sizeof soerr;
     getsockopt(fd, SOL_SOCKET, SO_ERROR, &soerr, &sl);
     if (soerr != 0 || (ev & (EPOLLERR | EPOLLHUP))) {
-      pool->pfail(this, pool->connect_error(soerr ? soerr : ECONNREFUSED));
+      // Nothing was sent: every call fails with the connect error, as each would on its own
+      // connection (HttpHostConnectException: no transport retry; Feign may retry it).
+      pool->pfail(this, pool->connect_error(soerr ? soerr : ECONNREFUSED), 0, true, false);
       return;
     }
     connecting = false;
+    for (const Pending& p : q) pool->arm_read_deadline(p.id, p.serial);
     set_interest(EPOLLIN | EPOLLRDHUP);
     do_write();
     return;
@@ -782,16 +792,23 @@ void ClientPool::PConn::do_read() {
     }
     // Responses arrive in request order: each completes the oldest request.
     size_t used = 0;
+    bool front_head = false;  // the oldest request's response head has arrived (body pending)
     while (!q.empty()) {
       ClientResult r;
       bool close = false, head_ok = false;
       size_t consumed = 0;
       const int rc = parse_response(std::string_view(in).substr(used), eof, &r, &close, &consumed, &head_ok);
       if (rc < 0) {
-        pool->pfail(this, "ClientProtocolException: malformed response");
+        // The oldest call got a bad answer: it fails alone, as on the plain path (a protocol
+        // error is never re-sent; Feign may retry it only if no valid head arrived). The calls
+        // behind it got no answer at all, so they are re-sent.
+        pool->pfail(this, "ClientProtocolException: malformed response", q.front().id, !head_ok);
         return;
       }
-      if (rc == 0) break;
+      if (rc == 0) {
+        front_head = head_ok;
+        break;
+      }
       used += consumed;
       Pending p = std::move(q.front());
       q.pop_front();
@@ -812,7 +829,13 @@ void ClientPool::PConn::do_read() {
       if (!pool->connect_fifo_.q.empty()) pool->pop_finished(pool->connect_fifo_);
     }
     if (eof || (q.empty() && !in.empty())) {
-      // the peer closed, or sent bytes nobody asked for: the connection is done
+      // The peer closed, or sent bytes nobody asked for: the connection is done. A call whose
+      // response head had arrived fails for good (HttpClient re-sends only before a response);
+      // the calls with nothing received yet are re-sent.
+      if (eof && front_head && !q.empty()) {
+        pool->pfail(this, "TruncatedChunkException: premature EOF", q.front().id, false);
+        return;
+      }
       pool->pfail(this, in.empty() || q.empty() ? "NoHttpResponseException: connection closed"
                                                 : "TruncatedChunkException: premature EOF");
       return;
@@ -832,17 +855,18 @@ void ClientPool::pdestroy(PConn* c) {
   loop_.retire(c);
 }
 
-void ClientPool::pfail(PConn* c, const std::string& why, uint64_t timed_out) {
+void ClientPool::pfail(PConn* c, const std::string& why, uint64_t failed, bool failed_retryable, bool resend_others) {
   std::deque<PConn::Pending> q;
   q.swap(c->q);
   pdestroy(c);
   for (auto& p : q) {
     pactive_.erase(p.id);
     if (p.abandoned || !p.cb) continue;
-    if (p.id == timed_out) {
+    if (p.id == failed || !resend_others) {
       ClientResult r;
       r.error = why;
-      r.retryable = true;  // an IOException to Feign
+      // retryable = an IOException before a response head (Feign's RetryableException)
+      r.retryable = p.id == failed ? failed_retryable : true;
       p.cb(std::move(r));
     } else {
       resubmit(p.id, std::move(p.req), std::move(p.cb), p.tries + 1, why);

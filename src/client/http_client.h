@@ -151,9 +151,14 @@ class ClientPool {
   PConn* open_pconn();
   void flush_dirty();
   void pdestroy(PConn* c);
-  // Ends a pipelined connection: `timed_out` (if any) fails with `why`, every other request
-  // still waiting on it is re-sent on a fresh connection (HttpClient's transport retry).
-  void pfail(PConn* c, const std::string& why, uint64_t timed_out = 0);
+  // Ends a pipelined connection. The request `failed` (if any: timed out, or answered with a
+  // malformed or truncated response) fails with `why` (`failed_retryable` = no valid response
+  // head arrived, so Feign may retry it). Every other request still waiting on the connection
+  // is re-sent on a fresh one (HttpClient's transport retry: nothing came back for it), or,
+  // with !resend_others (the connect failed, so nothing was sent), fails with `why` too.
+  void pfail(PConn* c, const std::string& why, uint64_t failed = 0, bool failed_retryable = true,
+             bool resend_others = true);
+  void arm_read_deadline(uint64_t id, uint64_t serial);
   void resubmit(uint64_t id, std::string req, Callback cb, int tries, const std::string& why);
   bool live(const Deadline& d) const;
   void push_deadline(DeadlineFifo& f, int ms, uint64_t id, uint64_t serial);

@@ -21,6 +21,7 @@ namespace hola::http {
 
 namespace {
 constexpr size_t kMaxBufferedOutput = 1 << 20;  // stop reading while this much is unsent
+constexpr int64_t kDrainIdleGraceMs = 100;       // see Server::shutdown
 constexpr int64_t kMaxBody = 1 << 20;           // request bodies are read and discarded
 
 const char* reason_phrase(int status) {
@@ -208,7 +209,7 @@ bool Connection::process(const char* data, size_t len, size_t* consumed) {
     } else {
       h.on_request(*this, r);
     }
-    if (worker_->server().draining()) close_after_flush_ = true;
+    if (worker_->server().closing()) close_after_flush_ = true;
   }
   in_process_ = false;
   if (StageProfile* prof = worker_->profile(); prof && handled) prof->batch.add(handled);
@@ -236,7 +237,7 @@ void Connection::complete(std::string_view response, bool keep_alive) {
     return;
   }
   parked_ = false;
-  if (!keep_alive || worker_->server().draining()) close_after_flush_ = true;
+  if (!keep_alive || worker_->server().closing()) close_after_flush_ = true;
   out_.append(response.data(), response.size());
   if (in_process_) return;
   // Continue with pipelined requests that arrived while parked.
@@ -384,10 +385,11 @@ void Worker::on_connection_closed(Connection* c) {
   c->prev_ = c->next_ = nullptr;
 }
 
-void Worker::close_idle_connections() {
+void Worker::close_idle_connections(int64_t grace_ms) {
+  const int64_t now = loop_.now_ms();
   for (Connection* c = conns_; c;) {
     Connection* next = c->next_;
-    if (c->streaming() || c->idle()) c->close();
+    if (c->streaming() || (c->idle() && now - c->last_active_ms() >= grace_ms)) c->close();
     c = next;
   }
 }
@@ -658,6 +660,7 @@ uint64_t Server::total_requests() const {
 }
 
 void Server::shutdown(int drain_ms) {
+  closing_.store(true);
   draining_.store(true);
   for (auto& a : acceptors_) {
     Acceptor* ap = a.get();
@@ -670,12 +673,13 @@ void Server::shutdown(int drain_ms) {
     });
     while (!done.load()) std::this_thread::sleep_for(std::chrono::milliseconds(1));
   }
-  // Idle keep-alive and streaming connections close now; busy ones close after their
-  // current response (process() sets close_after_flush_ while draining).
-  for (auto& w : workers_) {
-    Worker* wp = w.get();
-    wp->loop().post([wp] { wp->close_idle_connections(); });
-  }
+  // Streaming connections close now, and kept-alive ones that have been idle for the grace
+  // period; busy ones close after their current response (process() sets close_after_flush_
+  // while closing). A connection active just before the drain is given until it has been
+  // idle for the grace period to send one more request, answered with `Connection: close`:
+  // a closed-loop client has its next request on the way within microseconds, and closing
+  // under it would fail that request.
+  const int64_t grace_ms = std::min<int64_t>(kDrainIdleGraceMs, drain_ms);
   auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(drain_ms);
   for (;;) {
     size_t open = 0;
@@ -683,7 +687,8 @@ void Server::shutdown(int drain_ms) {
       std::atomic<size_t> n{0};
       std::atomic<bool> done{false};
       Worker* wp = w.get();
-      wp->loop().post([wp, &n, &done] {
+      wp->loop().post([wp, &n, &done, grace_ms] {
+        wp->close_idle_connections(grace_ms);
         n.store(wp->open_connections());
         done.store(true);
       });

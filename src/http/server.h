@@ -193,8 +193,11 @@ class Worker {
   void adopt_here(int fd, int64_t accepted_ns = 0);
   size_t open_connections() const { return nconns_; }
   void on_connection_closed(Connection* c);
-  // Closes idle and streaming connections (shutdown drain); runs on the worker thread.
-  void close_idle_connections();
+  // Shutdown drain, on the worker thread: closes streaming connections, and idle ones (no
+  // request in progress, nothing buffered) with nothing read or written for grace_ms. A
+  // connection used just before the drain began is likely to carry one more request, which
+  // is answered with `Connection: close` instead of racing a close against it.
+  void close_idle_connections(int64_t grace_ms = 0);
   // Closes keep-alive connections idle for longer than the idle timeout.
   void sweep_idle();
   // Per-worker slot for the application.
@@ -254,7 +257,17 @@ class Server {
   int port() const { return port_; }
   // Starts worker threads (returns immediately).
   void start();
-  // Stops accepting, lets workers finish in-flight responses for up to drain_ms, then stops.
+  // Termination, phase 1 (hola --shutdown-delay-ms): readiness fails (the application
+  // answers its health route with 503) and every response closes its connection, while the
+  // listener still accepts, so a client routed here before the endpoint removal has
+  // propagated is still served, and kept-alive clients reconnect elsewhere one response at
+  // a time instead of racing a close.
+  void begin_termination() {
+    terminating_.store(true);
+    closing_.store(true);
+  }
+  // Phase 2: stops accepting, lets workers finish in-flight responses for up to drain_ms
+  // (each kept-alive connection's next response says `Connection: close`), then stops.
   void shutdown(int drain_ms);
   void join();
   size_t num_workers() const { return workers_.size(); }
@@ -262,6 +275,9 @@ class Server {
   RequestHandler& handler() { return *handler_; }
   const ServerOptions& options() const { return opts_; }
   bool draining() const { return draining_.load(std::memory_order_relaxed); }
+  bool terminating() const { return terminating_.load(std::memory_order_relaxed); }
+  // Responses close their connections (terminating or draining).
+  bool closing() const { return closing_.load(std::memory_order_relaxed); }
   uint64_t total_requests() const;
   bool steering() const { return !domain_workers_.empty() || !core_workers_.empty(); }
   size_t open_connections() const { return open_.load(std::memory_order_relaxed); }
@@ -288,6 +304,8 @@ class Server {
   std::vector<std::unique_ptr<Acceptor>> acceptors_;
   std::vector<std::thread> threads_;
   std::atomic<bool> draining_{false};
+  std::atomic<bool> terminating_{false};
+  std::atomic<bool> closing_{false};
   std::atomic<uint64_t> rr_{0};
   std::atomic<size_t> open_{0};
   int port_ = 0;

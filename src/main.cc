@@ -10,6 +10,7 @@
 #include <signal.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -73,6 +74,11 @@ void usage() {
           "                           shorthands for -Dhystrix.command.default.* / threadpool.default.*\n"
           "  --config-poll-ms N       config re-check interval (default 1000)\n"
           "  --drain-ms N             graceful shutdown drain budget (default 5000)\n"
+          "  --shutdown-delay-ms N    on SIGTERM/SIGINT/SIGHUP, first keep serving and accepting for N ms\n"
+          "                           with /api/health answering 503 and every response closing its\n"
+          "                           connection, then drain (default 0; the manifests set it so a\n"
+          "                           rolling update outlasts endpoint propagation). A second signal\n"
+          "                           ends the delay early\n"
           "  --port-file PATH         write the bound port here once listening\n"
           "  --busy-poll-us N         spin up to N us in epoll before sleeping (default 0)\n"
           "  --busy-poll-pause N      PAUSE instructions between empty polls (SMT-friendly spin)\n"
@@ -115,7 +121,7 @@ int main(int argc, char** argv) {
   if (zu) to.collector_url = zu;
   const char* hn = getenv("HOSTNAME");
   if (hn) ao.hostname = hn;  // HolaResource.java:57 getOrDefault("HOSTNAME", "unknown")
-  int threads = 0, drain_ms = 5000, stream_max = -1;
+  int threads = 0, drain_ms = 5000, stream_max = -1, shutdown_delay_ms = 0;
   int64_t stream_stall_ms = 30000;
   std::string cpu_list, port_file, profile_out, cpu_profile;
   int cpu_profile_hz = 1000;
@@ -201,6 +207,7 @@ int main(int argc, char** argv) {
     else if (a == "--hystrix-stream-stall-ms") stream_stall_ms = atoll(val("--hystrix-stream-stall-ms").c_str());
     else if (a == "--config-poll-ms") mo.poll_ms = atoi(val("--config-poll-ms").c_str());
     else if (a == "--drain-ms") drain_ms = atoi(val("--drain-ms").c_str());
+    else if (a == "--shutdown-delay-ms") shutdown_delay_ms = std::max(0, atoi(val("--shutdown-delay-ms").c_str()));
     else if (a == "--port-file") port_file = val("--port-file");
     else if (a == "--busy-poll-us") so.busy_poll_us = atoi(val("--busy-poll-us").c_str());
     else if (a == "--busy-poll-pause") so.busy_poll_pause = atoi(val("--busy-poll-pause").c_str());
@@ -378,8 +385,19 @@ int main(int argc, char** argv) {
 
   int sig = 0;
   sigwait(&sigs, &sig);
-  LOG_INFO("received %s: draining (up to %d ms)",
-           sig == SIGTERM ? "SIGTERM" : sig == SIGINT ? "SIGINT" : "SIGHUP", drain_ms);
+  const char* sig_name = sig == SIGTERM ? "SIGTERM" : sig == SIGINT ? "SIGINT" : "SIGHUP";
+  if (shutdown_delay_ms > 0) {
+    // Phase 1: fail readiness, keep accepting, close connections between responses. The
+    // pod's endpoint removal takes a while to reach every proxy (kube-proxy's sync); new
+    // connections routed here meanwhile are still served.
+    LOG_INFO("received %s: readiness failing, still serving for %d ms", sig_name, shutdown_delay_ms);
+    Logger::instance().flush();
+    server.begin_termination();
+    timespec ts{shutdown_delay_ms / 1000, long(shutdown_delay_ms % 1000) * 1000000L};
+    siginfo_t si;
+    if (sigtimedwait(&sigs, &si, &ts) > 0) LOG_INFO("second termination signal: ending the delay early");
+  }
+  LOG_INFO("received %s: draining (up to %d ms)", sig_name, drain_ms);
   server.shutdown(drain_ms);
   server.join();
   if (so.profile) {

@@ -50,10 +50,10 @@ Settings settings_from(const std::map<std::string, std::string>& p, const std::s
   auto pi = [&](const std::string& key, int* dst) {
     if (pool_str(key, &v)) *dst = atoi(v.c_str());
   };
-  // execution.timeout.* is the 1.5 name; execution.isolation.thread.timeoutInMilliseconds the
-  // original one still honoured (and the one config.properties:17 uses).
+  // Hystrix 1.5.1 reads the timeout from this key only (config.properties:17 sets it); the
+  // execution.timeout.* namespace holds just `enabled`. Each key is resolved command-first,
+  // then default (cmd_str), which is Archaius' precedence.
   ci("execution.isolation.thread.timeoutInMilliseconds", &s.timeout_ms);
-  ci("execution.timeout.timeoutInMilliseconds", &s.timeout_ms);
   cb("execution.timeout.enabled", &s.timeout_enabled);
   if (cmd_str("execution.isolation.strategy", &v)) s.isolation = v;
   ci("execution.isolation.semaphore.maxConcurrentRequests", &s.semaphore_max_concurrent);

@@ -499,6 +499,34 @@ def test_hystrix_command_key_default_and_flag(hola, aloha):
     assert b'command="AlohaService#aloha()",event="TIMEOUT"} 1' in body
 
 
+def test_hystrix_command_key_beats_default_for_timeout(hola, aloha):
+    """Archaius precedence: hystrix.command.<key>.* wins over hystrix.command.default.* for the
+    same property, and the timeout is read from execution.isolation.thread.timeoutInMilliseconds
+    only (Hystrix 1.5.1 has no execution.timeout.timeoutInMilliseconds; config.properties:17)."""
+    aloha.set_mode("slow", delay_s=3.0)
+    s = hola(args=["--aloha-url", aloha.url, "--feign-log", "none",
+                   "-Dhystrix.command.default.execution.isolation.thread.timeoutInMilliseconds=100",
+                   "-Dhystrix.command.default.execution.timeout.timeoutInMilliseconds=100",
+                   "-Dhystrix.command.aloha.execution.isolation.thread.timeoutInMilliseconds=900"])
+    t0 = time.monotonic()
+    assert chain(s)[1:] == [FALLBACK]
+    dt = time.monotonic() - t0
+    assert 0.85 <= dt < 1.6, dt
+    _, _, body = s.get("/metrics")
+    assert b'hola_hystrix_events_total{command="aloha",event="TIMEOUT"} 1' in body
+
+
+def test_hystrix_invented_timeout_key_is_ignored(hola, aloha):
+    """execution.timeout.timeoutInMilliseconds is not a Hystrix key: setting it alone leaves the
+    600 ms default (config.properties:17) in force."""
+    aloha.set_mode("slow", delay_s=3.0)
+    s = hola(args=["--aloha-url", aloha.url, "--feign-log", "none",
+                   "-Dhystrix.command.default.execution.timeout.timeoutInMilliseconds=100"])
+    t0 = time.monotonic()
+    assert chain(s)[1:] == [FALLBACK]
+    assert 0.55 <= time.monotonic() - t0 < 1.4
+
+
 def test_hystrix_flag_shorthands(hola, aloha):
     aloha.set_mode("slow", delay_s=1.0)
     s = hola(args=["--aloha-url", aloha.url, "--hystrix-timeout-ms", "120", "--feign-log", "none"])
@@ -748,3 +776,69 @@ def test_pipelined_mode_keeps_no_idle_plain_connections(hola, aloha):
         _concurrent_chains(s, 8)
         time.sleep(0.8)
     assert fds() <= base + 4, (base, fds())
+
+
+def _retries(s) -> dict:
+    out = {}
+    for line in s.get("/metrics")[2].decode().splitlines():
+        if line.startswith("hola_aloha_retries_total{"):
+            out[line.split('kind="')[1].split('"')[0]] = int(float(line.rsplit(" ", 1)[1]))
+    return out
+
+
+_PIPE = ["--aloha-pipeline", "4", "-Dhystrix.threadpool.default.coreSize=64"]
+
+
+@pytest.mark.parametrize("pipelined", [False, True], ids=["plain", "pipelined"])
+def test_malformed_framing_after_a_valid_head_fails_once(hola, aloha, pipelined):
+    """A valid 200 head followed by a malformed chunk: HttpClient never re-sends it (a protocol
+    error after the response) and Feign does not retry it (the failure is in the body, after
+    execute() returned). Both client modes: one aloha request, one FAILURE, no transport
+    retry."""
+    aloha.set_mode("bad_chunk")
+    s = hola(args=["--aloha-url", aloha.url, "--no-tracing", "--feign-log", "none"] + (_PIPE if pipelined else []),
+             threads=1)
+    t0 = time.monotonic()
+    assert chain(s)[1:] == [FALLBACK]
+    assert time.monotonic() - t0 < 0.3
+    assert len(aloha.requests) == 1
+    assert _events(s).get("FAILURE") == 1
+    assert _retries(s).get("transport", 0) == 0
+
+
+@pytest.mark.parametrize("pipelined", [False, True], ids=["plain", "pipelined"])
+def test_malformed_status_line_is_not_resent_by_the_transport(hola, aloha, pipelined):
+    """No parseable status line: ClientProtocolException from execute() is an IOException, so
+    Feign's Retryer may retry the call, but the transport never re-sends it. With Feign retries
+    off: one request, one FAILURE. With the default Retryer: every aloha request is a Feign
+    attempt (transport retries stay 0) until the 600 ms Hystrix timeout."""
+    aloha.set_mode("bad_status")
+    base = ["--aloha-url", aloha.url, "--no-tracing"] + (_PIPE if pipelined else [])
+    s = hola(args=base + ["--feign-log", "none", "--feign-retry", "off"], threads=1)
+    assert chain(s)[1:] == [FALLBACK]
+    assert len(aloha.requests) == 1
+    assert _events(s).get("FAILURE") == 1
+    assert _retries(s).get("transport", 0) == 0
+    s2 = hola(args=base, threads=1)
+    n0 = len(aloha.requests)
+    assert chain(s2)[1:] == [FALLBACK]
+    assert _events(s2).get("TIMEOUT") == 1
+    r = _retries(s2)
+    assert r.get("transport", 0) == 0
+    assert r.get("feign", 0) >= 2
+    assert len(aloha.requests) - n0 == r["feign"] + 1
+    assert "<--- ERROR ClientProtocolException: malformed response" in _wait_log(s2, "ClientProtocolException", 1)
+
+
+@pytest.mark.parametrize("pipelined", [False, True], ids=["plain", "pipelined"])
+def test_refused_aloha_costs_no_transport_retry(hola, pipelined):
+    """A refused connect is HttpHostConnectException: HttpClient's retry handler never re-sends
+    it, in either client mode (before this fix a pipelined connection re-sent every call queued
+    on it, one more connect each)."""
+    s = hola(args=["--aloha-url", f"http://127.0.0.1:{closed_port()}/", "--no-tracing", "--feign-log", "none",
+                   "--feign-retry", "off", "-Dhystrix.command.default.circuitBreaker.enabled=false"]
+             + (_PIPE if pipelined else []), threads=1)
+    res = _concurrent_chains(s, 6)
+    assert all(st == 200 and body[1:] == [FALLBACK] for st, body in res), res
+    assert _retries(s).get("transport", 0) == 0
+    assert _events(s).get("FAILURE") == 6

@@ -541,3 +541,105 @@ def test_long_paths_are_canonicalised_too(hola):
     assert s.get("/api/" + "a/../" * 300 + "hola")[2] == b"Hola de h"
     assert s.get("/api/" + "%7A/../" * 200 + "hola")[2] == b"Hola de h"
     assert s.get("/api/" + "%7A" * 600)[0] == 404
+
+
+def _raw_exchange(sock, path: str = "/api/hola") -> tuple[int, dict, bytes]:
+    """One request on a kept-alive socket; returns (status, headers, body)."""
+    sock.sendall(f"GET {path} HTTP/1.1\r\nHost: x\r\n\r\n".encode())
+    data = b""
+    while b"\r\n\r\n" not in data:
+        chunk = sock.recv(65536)
+        if not chunk:
+            raise ConnectionError("EOF before a response")
+        data += chunk
+    head, _, body = data.partition(b"\r\n\r\n")
+    lines = head.decode().split("\r\n")
+    hdrs = {k.lower(): v for k, v in (l.split(": ", 1) for l in lines[1:])}
+    n = int(hdrs.get("content-length", "0"))
+    while len(body) < n:
+        chunk = sock.recv(65536)
+        if not chunk:
+            raise ConnectionError("EOF inside a body")
+        body += chunk
+    return int(lines[0].split()[1]), hdrs, body
+
+
+def test_shutdown_delay_fails_readiness_but_keeps_serving(hola):
+    """--shutdown-delay-ms: after SIGTERM the replica keeps accepting and serving for the delay,
+    /api/health answers 503 (the readiness probe of pom.xml:90-94 fails, so the Service stops
+    routing here), and every response carries `Connection: close` so kept-alive clients move
+    elsewhere between requests. Then it drains and exits 0."""
+    import signal
+
+    s = hola(args=["--shutdown-delay-ms", "1500"])
+    ka = socket.create_connection(("127.0.0.1", s.port), timeout=5)
+    assert _raw_exchange(ka)[0] == 200
+    t0 = time.monotonic()
+    s.proc.send_signal(signal.SIGTERM)
+    deadline = time.monotonic() + 5
+    while "readiness failing" not in s.log() and time.monotonic() < deadline:
+        time.sleep(0.01)
+    st, h, body = _raw_exchange(ka)  # the kept-alive connection: served once more, then closed
+    assert st == 200 and body == b"Hola de testhost" and h["connection"] == "close"
+    assert ka.recv(10) == b""
+    st, h, body = s.get("/api/health")  # a new connection is still accepted
+    assert st == 503 and body == b"shutting down"
+    st, h, body = s.get("/api/hola")
+    assert st == 200 and body == b"Hola de testhost"
+    assert s.proc.poll() is None
+    assert s.proc.wait(timeout=10) == 0
+    assert time.monotonic() - t0 >= 1.4
+    log = s.log()
+    assert "received SIGTERM: readiness failing, still serving for 1500 ms" in log
+    assert "received SIGTERM: draining" in log
+
+
+def test_second_signal_ends_the_shutdown_delay(hola):
+    import signal
+
+    s = hola(args=["--shutdown-delay-ms", "30000"])
+    s.proc.send_signal(signal.SIGTERM)
+    deadline = time.monotonic() + 5
+    while "readiness failing" not in s.log() and time.monotonic() < deadline:
+        time.sleep(0.01)
+    t0 = time.monotonic()
+    s.proc.send_signal(signal.SIGTERM)
+    assert s.proc.wait(timeout=10) == 0
+    assert time.monotonic() - t0 < 5
+    assert "ending the delay early" in s.log()
+
+
+def test_drain_closes_busy_keepalive_connections_between_responses(hola):
+    """Without a delay: SIGTERM while clients loop on kept-alive connections. Each client gets
+    a complete response carrying `Connection: close` and then EOF; no request is left without
+    a response (no close racing a request that was already on its way)."""
+    import signal
+    import threading
+
+    s = hola(threads=2)
+    results = []
+
+    def client():
+        c = socket.create_connection(("127.0.0.1", s.port), timeout=5)
+        n, last = 0, None
+        try:
+            while True:
+                st, h, _ = _raw_exchange(c)
+                assert st == 200
+                n += 1
+                last = h.get("connection")
+                if last == "close":
+                    break
+            results.append(("ok", n, c.recv(10)))
+        except Exception as e:  # noqa: BLE001
+            results.append(("error", n, repr(e)))
+
+    ts = [threading.Thread(target=client) for _ in range(4)]
+    for t in ts:
+        t.start()
+    time.sleep(0.3)
+    s.proc.send_signal(signal.SIGTERM)
+    for t in ts:
+        t.join(timeout=10)
+    assert s.proc.wait(timeout=10) == 0
+    assert len(results) == 4 and all(r[0] == "ok" and r[1] > 0 and r[2] == b"" for r in results), results
