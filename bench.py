@@ -15,7 +15,9 @@ K timed steps between barriers; the elapsed time is the MAX over ranks, `value` 
 node-wide total req/s, and p50/p99 come from the merged latency histograms of all ranks.
 Every response body in the timed region is compared with the greeting of the replica behind
 its connection (a mismatch is an error). After the timed region rank 0 runs BASELINE config
-2 (one connection, ~3 s) and reports it as c1_* keys; the JSON also carries span accounting
+2 (one connection, ~3 s) and reports it as c1_* keys, then the as-deployed replica (the
+image's exact ENTRYPOINT + the manifests' args and env: no busy-polling; deployed_* keys);
+the JSON also carries span accounting
 (`tracing`, with a native collector under --zipkin-sink), connection placement (`locality`)
 and how busy the replicas' cores and their idle SMT siblings were (`host_load`: other
 tenants on the siblings are what moves the number between runs on a shared host).
@@ -112,6 +114,11 @@ def parse_args():
     ap.add_argument("--c1-reqs", type=int, default=0,
                     help="config-2 request count instead of --c1-seconds (0 = sized from a warm-up "
                          "run to last --c1-seconds)")
+    ap.add_argument("--deployed-seconds", type=float, default=3.0,
+                    help="after the timed region, rank 0 also drives a replica started exactly as the image "
+                         "and manifests start it (deploy/Dockerfile ENTRYPOINT + deploy/openshift args and "
+                         "env: no --busy-poll-us) on its server CPUs, with the same load generator, for about "
+                         "this long; reported as deployed_*. 0 = skip. `value` is untouched")
     ap.add_argument("--busy-poll-us", type=int, default=20,
                     help="spin this long in epoll before sleeping (server and load generator); "
                          "20 us measured best on the box (profiles/r11_box_session), 0 = off")
@@ -288,6 +295,12 @@ def main() -> int:
         if loadgen:
             loadgen.close()
         server.stop()
+    # The as-deployed replica, on the same CPUs once the headline replica is gone (rank 0).
+    deployed = _deployed_subrun(a, server_cpus, load_cpus) if local_rank == 0 and a.deployed_seconds > 0 else None
+    if dist:
+        both = [None] * world
+        dist.all_gather_object(both, deployed)
+        deployed = both[0]
         if sink:
             sink[0].terminate()
             sink[0].wait(timeout=10)
@@ -340,6 +353,8 @@ def main() -> int:
             "body_mismatch": sum(g["body_mismatch"] for g in gathered),
             # BASELINE config 2 (1 connection, 1 replica), measured after the timed region
             **_c1_keys(gathered[0]["c1"]),
+            # the replica as the image and manifests run it (no busy-polling), same load generator
+            **_deployed_keys(deployed),
             # span accounting over the timed region, all replicas (per second)
             "tracing": _tracing_block(a, gathered, t, plan[0]["sink_port"]),
             # client thread vs. serving worker placement of every accepted connection
@@ -350,8 +365,11 @@ def main() -> int:
             "config": {
                 "model": "hola GET /api/hola (native C++ replica, default greeting, "
                          + ("tracing off" if a.no_tracing else
+                            "B3 tracing on, spans posted to a native discard Zipkin collector "
+                            "(hola_zipkin_sink) as the deployed ZIPKIN_SERVER_URL does" if plan[0]["sink_port"] else
                             "B3 tracing on without a collector: spans counted and dropped, as Brave "
-                            "does with ZIPKIN_SERVER_URL unset") + ")",
+                            "does with ZIPKIN_SERVER_URL unset")
+                         + (f", --busy-poll-us {a.busy_poll_us}" if a.busy_poll_us else "") + ")",
                 "global_batch": a.connections * world,
                 "seq_len": 1,
                 "parallelism": f"replicas{world}",
@@ -368,6 +386,7 @@ def main() -> int:
                 "busy_poll_pause": a.busy_poll_pause,
                 "epoll": "level" if a.epoll_lt else "edge",
                 "smt": smt,
+                "layout_note": _layout_note(plan[0]["gpu_slots"], smt, server_cpus, load_cpus),
                 "gpu_slots_on_node": plan[0]["gpu_slots"],
                 "cpus_per_replica": len(set(server_cpus) | set(load_cpus)),
                 "step_budget": "per-connection" if a.per_conn_quota else "shared",
@@ -469,6 +488,101 @@ def _config2_subrun(a, host: str, port: int, load_cpus, bodies) -> dict | None:
     return {"rps": r["requests"] / el if el > 0 else 0.0, "requests": r["requests"], "elapsed_s": el,
             "p50_ns": st["p50_ns"], "p99_ns": st["p99_ns"], "errors": r["errors"],
             "body_checked": st.get("body_checked", 0), "client_cpu": load_cpus[0]}
+
+
+def _layout_note(slots: int, smt: str, server_cpus, load_cpus) -> str:
+    """One line that tells a SCALE_rNN.json reader why its N=1 point differs from BENCH."""
+    phys = len({min(siblings(c)) for c in list(server_cpus) + list(load_cpus)})
+    how = ("each physical core runs a server worker on one SMT thread and its load-generator "
+           "thread on the other (--smt pair)" if smt == "pair" else
+           "server workers and load-generator threads on separate physical cores, SMT siblings idle")
+    return (f"{slots} GPU slot(s) on this node: each replica's share is {phys} physical cores "
+            f"({len(set(server_cpus) | set(load_cpus))} CPUs); {how}. The 1-GPU box (16-CPU quota) runs "
+            f"smt=off and an unconstrained 8-GPU node smt=pair, so BENCH and SCALE's N=1 differ by layout, "
+            f"not by code; compare config.smt before reading a difference as a regression.")
+
+
+def _deployed_subrun(a, server_cpus, load_cpus) -> dict | None:
+    """The replica exactly as deployed: deploy/Dockerfile's ENTRYPOINT (its /app paths mapped
+    to this tree) + the container args and env of deploy/openshift/hola-dc.yaml, in a cpuset of
+    this rank's server CPUs (a Guaranteed pod under the static CPU manager), HOSTNAME = a pod
+    name. Only the listen port differs (a free one instead of 8080). Same load generator as the
+    headline, about --deployed-seconds long."""
+    import socket
+    import subprocess
+
+    from hola_amd import native
+    from hola_amd.kube import manifests as km
+    from hola_amd.kube.image import Image
+
+    img = Image.from_dockerfile()
+    dc = next(o for o in km.load_objects([Path(__file__).resolve().parent / "deploy/openshift/hola-dc.yaml"])
+              if o["kind"] == "DeploymentConfig")
+    cont = dc["spec"]["template"]["spec"]["containers"][0]
+    argv = [str(img.files.get(x, x)) for x in img.entrypoint] + [str(x) for x in cont.get("args") or []]
+    argv[0] = str(native.binary("hola"))
+    port = _free_port_block(18900, 1)
+    argv += ["--port", str(port)]
+    env = {k: v for k, v in os.environ.items() if k in ("PATH", "LANG", "LD_LIBRARY_PATH")}
+    env.update(img.env)
+    env.update({e["name"]: str(e["value"]) for e in cont.get("env") or [] if "value" in e})
+    env["HOSTNAME"] = "hola-1-deplo"  # fieldRef metadata.name
+    cpus = list(server_cpus)
+    proc = subprocess.Popen(argv, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                            preexec_fn=lambda: os.sched_setaffinity(0, cpus))
+    try:
+        deadline = time.monotonic() + 10
+        while True:
+            try:
+                socket.create_connection(("127.0.0.1", port), timeout=1).close()
+                break
+            except OSError:
+                if proc.poll() is not None or time.monotonic() > deadline:
+                    return {"error": f"deployed replica did not start (rc {proc.poll()})"}
+                time.sleep(0.02)
+        body = ["Hola de hola-1-deplo"] if a.path == "/api/hola" else None
+        lg = ControlledLoadgen([("127.0.0.1", port)], a.connections, len(load_cpus),
+                               cpu_list=",".join(map(str, load_cpus)), path=a.path, busy_poll_us=a.busy_poll_us,
+                               busy_poll_pause=a.busy_poll_pause, epoll_lt=a.epoll_lt,
+                               expect_bodies=body, verify_body=body is None)
+        try:
+            warm = lg.run(2000)
+            rate = warm["requests"] / max(1e-9, warm["elapsed_ns"] / 1e9)
+            per_conn = int(min(200_000, max(2_000, rate * a.deployed_seconds / a.connections)))
+            lg.reset()
+            c0 = proc_cpu_s(proc.pid)
+            r = lg.run(per_conn)
+            c1 = proc_cpu_s(proc.pid)
+            st = lg.stats()
+        finally:
+            lg.close()
+    finally:
+        proc.terminate()
+        try:
+            proc.wait(timeout=15)
+        except subprocess.TimeoutExpired:
+            proc.kill()
+    el = r["elapsed_ns"] / 1e9
+    return {"rps": r["requests"] / el if el > 0 else 0.0, "p50_ns": st["p50_ns"], "p99_ns": st["p99_ns"],
+            "requests": r["requests"], "errors": r["errors"], "non2xx": st.get("non2xx", 0),
+            "cpu_us_per_req": 1e6 * (c1 - c0) / max(1, r["requests"]),
+            "args": " ".join(["hola"] + argv[1:-2]), "cpus": format_cpu_list(cpus),
+            "env": " ".join(f"{k}={v}" for k, v in sorted(env.items()) if k in img.env or k == "HOSTNAME")}
+
+
+def _deployed_keys(d: dict | None) -> dict:
+    if not d:
+        return {}
+    if "error" in d:
+        return {"deployed_error": d["error"]}
+    return {"deployed_rps": round(d["rps"], 1), "deployed_p50_ms": round(d["p50_ns"] / 1e6, 4),
+            "deployed_p99_ms": round(d["p99_ns"] / 1e6, 4), "deployed_requests": d["requests"],
+            "deployed_errors": d["errors"], "deployed_non2xx": d["non2xx"],
+            "deployed_server_cpu_us_per_req": round(d["cpu_us_per_req"], 3),
+            "deployed_args": d["args"], "deployed_cpus": d["cpus"],
+            # ZIPKIN_SERVER_URL names the cluster's zipkin-query Service, which does not resolve
+            # on a bare host: spans are recorded and dropped, as Brave does without a collector
+            "deployed_env": d["env"]}
 
 
 def _c1_keys(c1: dict | None) -> dict:

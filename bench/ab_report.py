@@ -1,0 +1,97 @@
+#!/usr/bin/env python3
+"""Gated A/B of interleaved bench.py runs (`bench/box_session.sh ab REPS "a|..." "b|..."`).
+
+Pairs run i of the baseline with run i of the candidate. A pair is kept only when neither
+side's `host_load.siblings` (busy share of the SMT siblings of the replica's cores: other
+tenants on our physical cores) exceeds --max-sibling-load. For the kept pairs it reports the
+paired difference of server CPU µs per request (the primary metric: the server's own cost,
+which sibling load and client jitter move least) and of req/s, with a 95 % t-interval.
+
+  python bench/ab_report.py DIR --baseline r1 --candidate final [--max-sibling-load 0.02]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import statistics
+import sys
+from pathlib import Path
+
+# two-sided 95 % t quantiles by degrees of freedom
+_T95 = {1: 12.706, 2: 4.303, 3: 3.182, 4: 2.776, 5: 2.571, 6: 2.447, 7: 2.365, 8: 2.306, 9: 2.262, 10: 2.228,
+        12: 2.179, 15: 2.131, 20: 2.086, 30: 2.042}
+
+
+def t95(df: int) -> float:
+    if df in _T95:
+        return _T95[df]
+    return next((v for k, v in sorted(_T95.items()) if k >= df), 1.96)
+
+
+def ci(diffs: list[float]) -> tuple[float, float, float]:
+    m = statistics.fmean(diffs)
+    if len(diffs) < 2:
+        return m, float("nan"), float("nan")
+    h = t95(len(diffs) - 1) * statistics.stdev(diffs) / math.sqrt(len(diffs))
+    return m, m - h, m + h
+
+
+def load(d: Path, label: str) -> dict[int, dict]:
+    out = {}
+    for p in d.glob(f"{label}_*.json"):
+        try:
+            out[int(p.stem.rsplit("_", 1)[1])] = json.loads(p.read_text().strip().splitlines()[-1])
+        except (ValueError, IndexError, json.JSONDecodeError):
+            pass
+    return out
+
+
+def sib(r: dict) -> float:
+    return max(h.get("siblings", 0.0) for h in r.get("host_load", [{}]))
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("dir")
+    ap.add_argument("--baseline", required=True)
+    ap.add_argument("--candidate", required=True)
+    ap.add_argument("--max-sibling-load", type=float, default=0.02)
+    ap.add_argument("--json", default="")
+    a = ap.parse_args()
+    d = Path(a.dir)
+    base, cand = load(d, a.baseline), load(d, a.candidate)
+    rows, kept = [], []
+    for i in sorted(set(base) & set(cand)):
+        b, c = base[i], cand[i]
+        ok = sib(b) <= a.max_sibling_load and sib(c) <= a.max_sibling_load
+        rows.append({"pair": i, "kept": ok, "sib_base": round(sib(b), 4), "sib_cand": round(sib(c), 4),
+                     "us_base": b["server_cpu_us_per_req"], "us_cand": c["server_cpu_us_per_req"],
+                     "rps_base": b["value"], "rps_cand": c["value"]})
+        if ok:
+            kept.append(rows[-1])
+    print(f"{'pair':>4} {'kept':>5} {'sib A':>7} {'sib B':>7} {'us/req A':>9} {'us/req B':>9} {'req/s A':>11} {'req/s B':>11}")
+    for r in rows:
+        print(f"{r['pair']:>4} {str(r['kept']):>5} {r['sib_base']:>7.3f} {r['sib_cand']:>7.3f} {r['us_base']:>9.3f} "
+              f"{r['us_cand']:>9.3f} {r['rps_base']:>11.0f} {r['rps_cand']:>11.0f}")
+    res = {"baseline": a.baseline, "candidate": a.candidate, "pairs": len(rows), "kept": len(kept),
+           "max_sibling_load": a.max_sibling_load, "rows": rows}
+    if kept:
+        us = [100.0 * (r["us_cand"] - r["us_base"]) / r["us_base"] for r in kept]
+        rps = [100.0 * (r["rps_cand"] - r["rps_base"]) / r["rps_base"] for r in kept]
+        m, lo, hi = ci(us)
+        res["server_us_per_req_delta_pct"] = {"mean": round(m, 2), "ci95": [round(lo, 2), round(hi, 2)]}
+        m2, lo2, hi2 = ci(rps)
+        res["rps_delta_pct"] = {"mean": round(m2, 2), "ci95": [round(lo2, 2), round(hi2, 2)]}
+        print(f"\n{a.candidate} vs {a.baseline}, {len(kept)} kept pairs (siblings <= {a.max_sibling_load:.0%}):")
+        print(f"  server us/req: {m:+.2f} % (95 % CI {lo:+.2f} .. {hi:+.2f})")
+        print(f"  req/s        : {m2:+.2f} % (95 % CI {lo2:+.2f} .. {hi2:+.2f})")
+    else:
+        print("\nno pair passed the sibling-load gate")
+    if a.json:
+        Path(a.json).write_text(json.dumps(res, indent=1) + "\n")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -20,6 +20,9 @@
 #   tracing            headline without a collector, with the native Zipkin sink (default 1000-span
 #                      export budget, and unbounded), and with tracing off
 #   soak MINUTES [ARGS] mixed-load soak sampling RSS and FDs (ARGS go to bench/soak.py)
+#   kube [ARGS]        BASELINE config 5: deploy/openshift applied by the local executor at real
+#                      timings (8 pods, probes, rollouts under 512-connection load, SIGKILL,
+#                      ConfigMap edit; ARGS go to bench/kube_rollout.py)
 #
 # Every GPU-box step runs under its own `timeout -k`, steps are chained with &&, and the
 # script stops at the first failure (no retries).
@@ -38,6 +41,9 @@ final)
   ;;
 bench)
   timeout -k 10 400 python bench.py "$@" > "$OUT/bench.json" 2>> "$OUT/err.log"
+  ;;
+kube)
+  timeout -k 10 540 python -u bench/kube_rollout.py --out "$OUT/run" "$@" > "$OUT/kube.json" 2> "$OUT/kube.log"
   ;;
 repeat)
   # the default bench REPS times back to back: run-to-run spread of the headline on this host

@@ -712,6 +712,14 @@ int main(int argc, char** argv) {
   }
   if (!o.control && o.duration_s <= 0) o.duration_s = 10;
   signal(SIGPIPE, SIG_IGN);
+  if (!o.control) {
+    // SIGINT/SIGTERM end a timed run early: the summary covers the time actually run (a
+    // harness can run the load "until the rollout is over").
+    struct sigaction sa {};
+    sa.sa_handler = [](int) { g_stop.store(true, std::memory_order_relaxed); };
+    sigaction(SIGINT, &sa, nullptr);
+    sigaction(SIGTERM, &sa, nullptr);
+  }
   if (!cpu_profile.empty() && !hola::cpuprof::start(cpu_profile)) {
     fprintf(stderr, "loadgen: cannot start the CPU profiler\n");
     return 2;
@@ -742,11 +750,16 @@ int main(int argc, char** argv) {
   }
 
   if (!o.control) {
+    const int64_t t_start = mono_ns();
     for (auto& t : th) t.join();
     if (!cpu_profile.empty()) hola::cpuprof::write();
     std::string s = stats_json(ts, false);
     uint64_t completed = 0;
     for (auto& t : ts) completed += t->completed;
+    if (g_stop.load()) {  // stopped by a signal: the measured part is what ran after the warm-up
+      const double ran = double(mono_ns() - t_start) / 1e9 - o.warmup_s;
+      o.duration_s = std::max(1e-3, std::min(o.duration_s, ran));
+    }
     double rps = double(completed) / o.duration_s;
     if (wrk_text) {
       Histogram h;

@@ -11,10 +11,14 @@
   info                                       host CPU topology / quota / plan for this node
   units --replicas N --out DIR [--lb L]      systemd units: N pinned replicas + proxy on :8080
                                              (or --lb reuseport: replicas share :8080)
+  apply -f MANIFEST... [--replicas N]        run deploy/openshift/*.yaml on this node: pods from
+                                             the image's ENTRYPOINT, probe-gated Service, ConfigMaps
+  oc get|scale|set env|patch|apply|delete|rollout ...   control a running `apply`
 
 The local equivalents of the reference's `mvn wildfly-swarm:run` (Readme.md:13) and
 `mvn clean package docker:build fabric8:json fabric8:apply` (Readme.md:24) are
-`python -m hola_amd serve` and deploy/Dockerfile + deploy/openshift/*.yaml.
+`python -m hola_amd serve` and deploy/Dockerfile + deploy/openshift/*.yaml, which
+`python -m hola_amd apply` executes on one node (hola_amd/kube).
 """
 from __future__ import annotations
 
@@ -179,6 +183,14 @@ def main(argv: list[str] | None = None) -> int:
         return subprocess.call([sys.executable, str(root / "bench.py"), *rest])
     if cmd == "info":
         return _info()
+    if cmd == "apply":
+        from hola_amd.kube.cli import apply_main
+
+        return apply_main(rest)
+    if cmd == "oc":
+        from hola_amd.kube.cli import oc_main
+
+        return oc_main(rest)
     if cmd == "units":
         from hola_amd.deploy import write_units
 

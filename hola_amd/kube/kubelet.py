@@ -1,0 +1,385 @@
+"""Pods on one node: what the kubelet does for the hola container, as host processes.
+
+A pod is one `hola` process started from the image's ENTRYPOINT with the container's env
+(`HOSTNAME` from `fieldRef: metadata.name`, as `deploy/openshift/hola-dc.yaml:78-81` asks),
+its args, and its own pod IP on the loopback network (127.a.b.n: every pod binds :8080 on its
+own address, the part of a network namespace the service contract needs). Around it:
+
+* volumes: ConfigMaps are projected the way the kubelet's atomic writer does it: the files
+  live in a `..<timestamp>` directory, `..data` links to it, and each key is a link through
+  `..data`; an update writes a new directory and swaps `..data` with one rename (the case
+  hola's parent-directory watcher exists for);
+* the readiness probe with its real parameters (`initialDelaySeconds`, `periodSeconds`,
+  `timeoutSeconds`, `successThreshold`, `failureThreshold`; k8s defaults where the manifest
+  has none), run off the control loop in a small thread pool;
+* restartPolicy Always with CrashLoopBackOff (immediate first restart, then 10 s doubling to
+  300 s, reset after 10 min of running);
+* termination: the pod leaves the Service endpoints at once, its preStop hook (if any) runs,
+  then SIGTERM, and SIGKILL once `terminationGracePeriodSeconds` (30 s) have passed;
+* resources: under the static CPU manager policy a Guaranteed pod with integer CPUs gets an
+  exclusive cpuset (its process affinity); everything else runs on the shared pool. CPU and
+  memory limits are recorded but not enforced (that needs cgroup writes, i.e. root).
+
+Delays (probe delay and period, restart back-off, ConfigMap sync) are multiplied by the
+cluster's `time_scale` so tests can run the same state machine faster; deadlines
+(probe timeout, grace period) are not.
+"""
+from __future__ import annotations
+
+import http.client
+import os
+import re
+import shutil
+import signal
+import subprocess
+import time
+from concurrent.futures import Future, ThreadPoolExecutor
+from dataclasses import dataclass, field
+from pathlib import Path
+
+PROBE_DEFAULTS = {"initialDelaySeconds": 0, "periodSeconds": 10, "timeoutSeconds": 1, "successThreshold": 1,
+                  "failureThreshold": 3}
+BACKOFF_INITIAL_S, BACKOFF_MAX_S, BACKOFF_RESET_S = 10.0, 300.0, 600.0
+DEFAULT_GRACE_S = 30.0
+
+
+def project_configmap(vol_dir: Path, data: dict[str, str], items: list[dict] | None = None) -> None:
+    """Writes (or updates) a ConfigMap volume with the kubelet's layout and atomic swap."""
+    vol_dir.mkdir(parents=True, exist_ok=True)
+    files = {it["path"]: data[it["key"]] for it in items if it.get("key") in data} if items else dict(data)
+    ts = time.strftime("..%Y_%m_%d_%H_%M_%S", time.gmtime()) + f".{time.time_ns() % 10**9:09d}"
+    new = vol_dir / ts
+    new.mkdir()
+    for rel, content in files.items():
+        p = new / rel
+        p.parent.mkdir(parents=True, exist_ok=True)
+        p.write_text(content)
+    old = os.readlink(vol_dir / "..data") if (vol_dir / "..data").is_symlink() else None
+    tmp = vol_dir / "..data_tmp"
+    if tmp.is_symlink():
+        tmp.unlink()
+    tmp.symlink_to(ts)
+    os.rename(tmp, vol_dir / "..data")  # the one atomic step readers can observe
+    for rel in {r.split("/")[0] for r in files}:
+        link = vol_dir / rel
+        if not link.is_symlink():
+            link.symlink_to(Path("..data") / rel)
+    for entry in vol_dir.iterdir():  # keys that disappeared
+        if entry.is_symlink() and not entry.name.startswith("..") and entry.name not in {r.split("/")[0] for r in files}:
+            entry.unlink()
+    if old and old != ts:
+        shutil.rmtree(vol_dir / old, ignore_errors=True)
+
+
+def http_probe(host: str, port: int, path: str, timeout_s: float, headers: dict | None = None) -> tuple[bool, str]:
+    """kubelet httpGet: success is a status in [200, 400)."""
+    try:
+        conn = http.client.HTTPConnection(host, port, timeout=timeout_s)
+        try:
+            conn.request("GET", path, headers={"User-Agent": "kube-probe/1.29", **(headers or {})})
+            r = conn.getresponse()
+            r.read()
+            return 200 <= r.status < 400, f"HTTP {r.status}"
+        finally:
+            conn.close()
+    except OSError as e:
+        return False, f"{type(e).__name__}: {e}"
+
+
+@dataclass
+class Pod:
+    name: str
+    owner: str  # ReplicationController / ReplicaSet name
+    revision: int
+    template: dict
+    ip: str
+    dir: Path
+    labels: dict = field(default_factory=dict)
+    cpus: list[int] | None = None  # exclusive cpuset (static CPU manager) or None (shared pool)
+    cpu_request: float = 0.0
+    created: float = field(default_factory=time.monotonic)
+    scheduled: bool = False
+    pending_reason: str = ""
+    # container state
+    proc: subprocess.Popen | None = None
+    started_at: float = 0.0
+    restarts: int = 0
+    next_start_at: float = 0.0
+    backoff_s: float = 0.0
+    last_exit: int | None = None
+    # readiness
+    ready: bool = False
+    ready_since: float = 0.0
+    probe_ok: int = 0
+    probe_fail: int = 0
+    next_probe_at: float = 0.0
+    probe_future: Future | None = None
+    last_probe: str = ""
+    # termination
+    terminating: bool = False
+    deletion_at: float = 0.0
+    grace_deadline: float = 0.0
+    prestop: subprocess.Popen | None = None
+    term_sent: bool = False
+    gone: bool = False
+
+    @property
+    def container(self) -> dict:
+        return self.template["spec"]["containers"][0]
+
+    @property
+    def running(self) -> bool:
+        return self.proc is not None and self.proc.poll() is None
+
+    @property
+    def log_path(self) -> Path:
+        return self.dir / "container.log"
+
+    def status(self) -> str:
+        if self.terminating:
+            return "Terminating"
+        if not self.scheduled:
+            return "Pending"
+        if self.running:
+            return "Running"
+        if self.last_exit is not None and self.restarts and self.backoff_s >= BACKOFF_INITIAL_S:
+            return "CrashLoopBackOff"
+        return "ContainerCreating" if self.proc is None else "Error"
+
+    def summary(self) -> dict:
+        return {"name": self.name, "ip": self.ip, "status": self.status(), "ready": self.ready,
+                "restarts": self.restarts, "revision": self.revision, "owner": self.owner,
+                "cpus": self.cpus, "pid": self.proc.pid if self.running else None,
+                "last_probe": self.last_probe, "pending_reason": self.pending_reason}
+
+
+class Kubelet:
+    """Runs the pods' containers, probes, volumes and terminations; driven by ticks from the
+    cluster's control loop (every state change happens on that thread)."""
+
+    def __init__(self, cluster, probe_workers: int = 16):
+        self.cluster = cluster
+        self.pool = ThreadPoolExecutor(max_workers=probe_workers, thread_name_prefix="kube-probe")
+
+    # ------------------------------------------------------------------ container start
+    def _probe_spec(self, pod: Pod) -> dict | None:
+        rp = pod.container.get("readinessProbe")
+        if not rp:
+            return None
+        return {**PROBE_DEFAULTS, **rp}
+
+    def _env(self, pod: Pod) -> dict[str, str]:
+        c = self.cluster
+        env = {"PATH": os.environ.get("PATH", "/usr/bin:/bin"), "HOME": str(pod.dir)}
+        for k in ("LANG", "LC_ALL", "TMPDIR", "LD_LIBRARY_PATH", "SSL_CERT_FILE", "SSL_CERT_DIR"):
+            if k in os.environ:
+                env[k] = os.environ[k]
+        env.update(c.image.env)
+        # Service links the kubelet injects (<NAME>_SERVICE_HOST/_PORT) for the cluster's Services
+        for svc, (host, port) in c.service_addresses().items():
+            key = re.sub(r"[^A-Z0-9]", "_", svc.upper())
+            env[f"{key}_SERVICE_HOST"] = host
+            env[f"{key}_SERVICE_PORT"] = str(port)
+        for e in pod.container.get("env") or []:
+            name = e["name"]
+            if "value" in e:
+                env[name] = _expand(str(e["value"]), env)
+            elif "valueFrom" in e:
+                vf = e["valueFrom"]
+                if "fieldRef" in vf:
+                    fp = vf["fieldRef"]["fieldPath"]
+                    env[name] = {"metadata.name": pod.name, "metadata.namespace": c.namespace,
+                                 "status.podIP": pod.ip, "spec.nodeName": c.node_name}.get(fp, "")
+                elif "configMapKeyRef" in vf:
+                    ref = vf["configMapKeyRef"]
+                    env[name] = c.configmaps.get(ref["name"], {}).get(ref["key"], "")
+        # cluster DNS: a URL naming a Service of this cluster reaches that Service's address
+        return {k: c.rewrite_service_urls(self.map_paths(pod, v)) for k, v in env.items()}
+
+    def map_paths(self, pod: Pod, value: str) -> str:
+        """Container paths inside a value (whitespace-separated tokens: `/x`, `-Dk=/x`,
+        `--f=/x`) resolved to the host files that back them: a volume mount first, then the
+        image's root filesystem."""
+        def one(tok: str) -> str:
+            m = re.match(r"^((?:-D[^=]+=)|(?:--[^=]+=))?(/.*)$", tok)
+            if not m:
+                return tok
+            host = self.host_path(pod, m.group(2))
+            return (m.group(1) or "") + host if host else tok
+        return " ".join(one(t) for t in value.split(" "))
+
+    def host_path(self, pod: Pod, cpath: str) -> str | None:
+        best = None
+        for vm in pod.container.get("volumeMounts") or []:
+            mp = vm["mountPath"].rstrip("/")
+            if cpath == mp or cpath.startswith(mp + "/"):
+                if best is None or len(mp) > len(best[0]):
+                    best = (mp, pod.dir / "volumes" / vm["name"])
+        if best:
+            return str(best[1]) + cpath[len(best[0]):]
+        root = pod.dir.parent.parent / "rootfs"
+        norm = os.path.normpath(cpath)
+        if norm in self.cluster.image.files or any(f.startswith(norm + "/") for f in self.cluster.image.files):
+            return str(root) + norm
+        return None
+
+    def _argv(self, pod: Pod) -> list[str]:
+        c, img = pod.container, self.cluster.image
+        if c.get("command"):
+            argv = list(c["command"]) + list(c.get("args") or [])
+        else:
+            argv = list(img.entrypoint) + list(c.get("args") if c.get("args") is not None else img.cmd)
+        argv = [self.map_paths(pod, a) for a in argv]
+        # the pod's own network namespace, reduced to what the contract needs: its address
+        return argv + ["--host", pod.ip]
+
+    def setup_volumes(self, pod: Pod) -> None:
+        for v in pod.template["spec"].get("volumes") or []:
+            d = pod.dir / "volumes" / v["name"]
+            if "configMap" in v:
+                cm = v["configMap"]
+                project_configmap(d, self.cluster.configmaps.get(cm["name"], {}), cm.get("items"))
+            else:  # emptyDir and anything else: a plain directory
+                d.mkdir(parents=True, exist_ok=True)
+
+    def start_container(self, pod: Pod, now: float) -> None:
+        pod.dir.mkdir(parents=True, exist_ok=True)
+        if pod.proc is None and pod.restarts == 0:
+            self.setup_volumes(pod)
+        argv, env = self._argv(pod), self._env(pod)
+        workdir = self.host_path(pod, self.cluster.image.workdir) or str(pod.dir)
+        if not os.path.isdir(workdir):
+            workdir = str(pod.dir)
+        cpus = pod.cpus if pod.cpus is not None else self.cluster.shared_pool()
+        log = open(pod.log_path, "ab")
+        log.write(f"--- start {time.strftime('%H:%M:%S')} restart={pod.restarts} argv={argv}\n".encode())
+        log.flush()
+        pod.proc = subprocess.Popen(argv, env=env, cwd=workdir, stdout=log, stderr=log,
+                                    preexec_fn=(lambda: os.sched_setaffinity(0, cpus)) if cpus else None,
+                                    start_new_session=True)
+        log.close()
+        pod.started_at = now
+        pod.ready = False
+        pod.probe_ok = pod.probe_fail = 0
+        ps = self._probe_spec(pod)
+        pod.next_probe_at = now + (ps["initialDelaySeconds"] * self.cluster.time_scale if ps else 0.0)
+        self.cluster.event(pod.name, "Started", f"pid {pod.proc.pid} on {pod.ip}, cpus {cpus}")
+
+    # ------------------------------------------------------------------ the tick
+    def tick(self, pod: Pod, now: float) -> None:
+        if pod.gone or not pod.scheduled:
+            return
+        ts = self.cluster.time_scale
+        if pod.terminating:
+            self._tick_terminating(pod, now)
+            return
+        if pod.proc is not None and pod.proc.poll() is not None and pod.last_exit is None:
+            # the container died: NotReady at once, restart with back-off
+            pod.last_exit = pod.proc.returncode
+            pod.ready = False
+            ran = now - pod.started_at
+            if ran >= BACKOFF_RESET_S * ts:
+                pod.backoff_s = 0.0
+            delay = pod.backoff_s
+            pod.backoff_s = BACKOFF_INITIAL_S if pod.backoff_s == 0 else min(BACKOFF_MAX_S, pod.backoff_s * 2)
+            pod.next_start_at = now + delay * ts
+            self.cluster.event(pod.name, "BackOff" if delay else "Died",
+                               f"container exited {pod.last_exit}; restart in {delay * ts:.1f}s")
+        if pod.proc is None or (pod.last_exit is not None and now >= pod.next_start_at):
+            if pod.proc is not None:
+                pod.restarts += 1
+            pod.last_exit = None
+            self.start_container(pod, now)
+            return
+        if pod.last_exit is not None or not pod.running:
+            return
+        self._tick_probe(pod, now)
+
+    def _tick_probe(self, pod: Pod, now: float) -> None:
+        ps = self._probe_spec(pod)
+        if ps is None:
+            if not pod.ready:
+                pod.ready, pod.ready_since = True, now
+            return
+        f = pod.probe_future
+        if f is not None:
+            if not f.done():
+                return
+            pod.probe_future = None
+            ok, detail = f.result()
+            pod.last_probe = detail
+            if ok:
+                pod.probe_ok += 1
+                pod.probe_fail = 0
+                if not pod.ready and pod.probe_ok >= int(ps["successThreshold"]):
+                    pod.ready, pod.ready_since = True, now
+                    self.cluster.event(pod.name, "Ready", detail)
+            else:
+                pod.probe_fail += 1
+                pod.probe_ok = 0
+                if pod.ready and pod.probe_fail >= int(ps["failureThreshold"]):
+                    pod.ready = False
+                    self.cluster.event(pod.name, "Unhealthy", f"Readiness probe failed: {detail}")
+        if now >= pod.next_probe_at:
+            hg = ps.get("httpGet") or {}
+            port = _port_number(pod.container, hg.get("port", 8080))
+            headers = {h["name"]: h["value"] for h in hg.get("httpHeaders") or []}
+            pod.probe_future = self.pool.submit(http_probe, pod.ip, port, hg.get("path", "/"),
+                                                float(ps["timeoutSeconds"]), headers)
+            pod.next_probe_at = now + float(ps["periodSeconds"]) * self.cluster.time_scale
+
+    # ------------------------------------------------------------------ termination
+    def begin_delete(self, pod: Pod, now: float, grace_s: float | None = None) -> None:
+        if pod.terminating:
+            return
+        pod.terminating = True
+        pod.ready = False
+        pod.deletion_at = now
+        spec_grace = pod.template["spec"].get("terminationGracePeriodSeconds", DEFAULT_GRACE_S)
+        pod.grace_deadline = now + float(spec_grace if grace_s is None else grace_s)
+        pre = ((pod.container.get("lifecycle") or {}).get("preStop") or {})
+        if pod.running and "exec" in pre:
+            cmd = [self.map_paths(pod, a) for a in pre["exec"]["command"]]
+            pod.prestop = subprocess.Popen(cmd, env=self._env(pod), stdout=subprocess.DEVNULL,
+                                           stderr=subprocess.DEVNULL, start_new_session=True)
+        elif pod.running and "httpGet" in pre:
+            hg = pre["httpGet"]
+            http_probe(pod.ip, _port_number(pod.container, hg.get("port", 8080)), hg.get("path", "/"), 5.0)
+        self.cluster.event(pod.name, "Killing", f"grace {pod.grace_deadline - now:.0f}s")
+
+    def _tick_terminating(self, pod: Pod, now: float) -> None:
+        if not pod.running:
+            pod.gone = True
+            if pod.prestop and pod.prestop.poll() is None:
+                pod.prestop.kill()
+            self.cluster.event(pod.name, "Deleted",
+                               f"exit {pod.proc.returncode if pod.proc else None} after {now - pod.deletion_at:.2f}s")
+            return
+        if not pod.term_sent and (pod.prestop is None or pod.prestop.poll() is not None or now >= pod.grace_deadline):
+            pod.proc.send_signal(signal.SIGTERM)
+            pod.term_sent = True
+        if now >= pod.grace_deadline:
+            pod.proc.kill()
+            self.cluster.event(pod.name, "Killed", "grace period expired: SIGKILL")
+
+    def kill_container(self, pod: Pod, sig: int = signal.SIGKILL) -> None:
+        if pod.running:
+            pod.proc.send_signal(sig)
+
+    def shutdown(self) -> None:
+        self.pool.shutdown(wait=False, cancel_futures=True)
+
+
+def _port_number(container: dict, port) -> int:
+    if isinstance(port, int) or str(port).isdigit():
+        return int(port)
+    for p in container.get("ports") or []:
+        if p.get("name") == port:
+            return int(p["containerPort"])
+    raise ValueError(f"unknown named port {port!r}")
+
+
+def _expand(value: str, env: dict[str, str]) -> str:
+    """$(VAR) references to earlier variables, as the kubelet expands them ($$ escapes)."""
+    return re.sub(r"\$\$|\$\(([A-Za-z_][A-Za-z0-9_]*)\)",
+                  lambda m: "$" if m.group(0) == "$$" else env.get(m.group(1), m.group(0)), value)

@@ -32,6 +32,7 @@ PRESETS = {
     # compile-flag A/B variants of the release build (server binary via HOLA_SERVER_BIN)
     "release-v4": ["-DCMAKE_BUILD_TYPE=Release", "-DHOLA_MARCH=x86-64-v4", "-DHOLA_BUILD_PYTHON=OFF"],
     "release-o3lto": ["-DCMAKE_BUILD_TYPE=Release", "-DHOLA_OPT=-O3", "-DHOLA_LTO=ON", "-DHOLA_BUILD_PYTHON=OFF"],
+    "release-nofp": ["-DCMAKE_BUILD_TYPE=Release", "-DHOLA_FRAME_POINTERS=OFF", "-DHOLA_BUILD_PYTHON=OFF"],
     "release-v4-o3lto": ["-DCMAKE_BUILD_TYPE=Release", "-DHOLA_MARCH=x86-64-v4", "-DHOLA_OPT=-O3", "-DHOLA_LTO=ON",
                          "-DHOLA_BUILD_PYTHON=OFF"],
 }

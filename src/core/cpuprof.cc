@@ -7,7 +7,6 @@
 #include <time.h>
 #include <ucontext.h>
 #include <unistd.h>
-#include <unwind.h>
 
 #include <algorithm>
 #include <atomic>
@@ -43,20 +42,43 @@ std::vector<timer_t> g_timers;
 thread_local int t_index = -1;
 thread_local timer_t t_timer;
 thread_local bool t_armed = false;
+// The sampled thread's stack, for bounds-checking the frame-pointer walk.
+thread_local uintptr_t t_stack_lo = 0, t_stack_hi = 0;
 
-struct Walk {
-  uintptr_t* out;
-  int n;
-};
+// Executable mappings at start(): a return address must fall in one of them. Read-only while
+// sampling (the handler takes no lock and calls nothing).
+constexpr int kMaxRanges = 512;
+uintptr_t g_exec_lo[kMaxRanges], g_exec_hi[kMaxRanges];
+int g_nexec = 0;
 
-_Unwind_Reason_Code walk_frame(_Unwind_Context* ctx, void* arg) {
-  auto* w = static_cast<Walk*>(arg);
-  const uintptr_t ip = _Unwind_GetIP(ctx);
-  if (!ip || w->n >= 2 * kDepth + 8) return _URC_END_OF_STACK;
-  w->out[w->n++] = ip;
-  return _URC_NO_REASON;
+int exec_range(uintptr_t pc) {
+  for (int i = 0; i < g_nexec; ++i)
+    if (pc >= g_exec_lo[i] && pc < g_exec_hi[i]) return i;
+  return -1;
+}
+bool executable(uintptr_t pc) { return exec_range(pc) >= 0; }
+int g_own_range = -1;  // the mapping holding this file's code (built with frame pointers)
+
+void load_exec_ranges() {
+  std::ifstream maps("/proc/self/maps");
+  g_nexec = 0;
+  for (std::string line; std::getline(maps, line) && g_nexec < kMaxRanges;) {
+    unsigned long lo = 0, hi = 0;
+    char perms[5] = {};
+    if (sscanf(line.c_str(), "%lx-%lx %4s", &lo, &hi, perms) == 3 && perms[2] == 'x') {
+      g_exec_lo[g_nexec] = lo;
+      g_exec_hi[g_nexec] = hi;
+      ++g_nexec;
+    }
+  }
 }
 
+// Async-signal-safe: walks the interrupted thread's frame-pointer chain from the ucontext's
+// RBP (the native code is built with -fno-omit-frame-pointer), reading only inside the
+// thread's own stack and stopping at the first address that is not code. No unwinder, no
+// locks, no allocation. When the sample lands in code from another object (libc's syscall
+// wrappers: send, recv, epoll_wait), which keeps no frame pointer, the caller is found by
+// scanning the top of the stack for the first return address into a different mapping.
 void on_prof(int, siginfo_t*, void* ucv) {
   if (!g_on.load(std::memory_order_relaxed) || t_index < 0) return;
   const size_t i = g_next.fetch_add(1, std::memory_order_relaxed);
@@ -66,17 +88,48 @@ void on_prof(int, siginfo_t*, void* ucv) {
   s.thread = uint16_t(t_index);
   const auto* uc = static_cast<const ucontext_t*>(ucv);
   const uintptr_t pc = uintptr_t(uc->uc_mcontext.gregs[REG_RIP]);
+  const uintptr_t sp = uintptr_t(uc->uc_mcontext.gregs[REG_RSP]);
+  uintptr_t fp = uintptr_t(uc->uc_mcontext.gregs[REG_RBP]);
   s.pc[0] = pc;
   s.depth = 1;
-  // The unwinder starts in this handler, passes the signal trampoline, then reaches the
-  // interrupted frame (its IP is `pc`); the frames after it are the callers.
-  uintptr_t frames[2 * kDepth + 8];
-  Walk w{frames, 0};
-  _Unwind_Backtrace(walk_frame, &w);
-  int k = 0;
-  while (k < w.n && frames[k] != pc) ++k;
-  for (++k; k < w.n && s.depth < kDepth; ++k) s.pc[s.depth++] = frames[k];
+  const bool bounded = t_stack_hi > t_stack_lo;
+  auto in_stack = [&](uintptr_t a) { return bounded && a >= t_stack_lo && a + 16 <= t_stack_hi && !(a & 7); };
+  const int pc_range = exec_range(pc);
+  uintptr_t caller = 0;
+  if (pc_range != g_own_range) {
+    for (int k = 0; k < 16 && in_stack(sp + 8 * uintptr_t(k)); ++k) {
+      const uintptr_t w = *reinterpret_cast<const uintptr_t*>(sp + 8 * uintptr_t(k));
+      const int r = exec_range(w);
+      if (r >= 0 && r != pc_range) {
+        caller = w;
+        s.pc[s.depth++] = w;
+        break;
+      }
+    }
+  }
+  bool first = true;
+  while (s.depth < kDepth && in_stack(fp)) {
+    const uintptr_t ret = *reinterpret_cast<const uintptr_t*>(fp + 8);
+    const uintptr_t next = *reinterpret_cast<const uintptr_t*>(fp);
+    if (!executable(ret)) break;
+    if (!(first && ret == caller)) s.pc[s.depth++] = ret;
+    first = false;
+    if (next <= fp) break;  // the chain must climb the stack
+    fp = next;
+  }
   errno = saved_errno;
+}
+
+void note_stack_bounds() {
+  pthread_attr_t attr;
+  if (pthread_getattr_np(pthread_self(), &attr) != 0) return;
+  void* addr = nullptr;
+  size_t size = 0;
+  if (pthread_attr_getstack(&attr, &addr, &size) == 0) {
+    t_stack_lo = uintptr_t(addr);
+    t_stack_hi = uintptr_t(addr) + size;
+  }
+  pthread_attr_destroy(&attr);
 }
 }  // namespace
 
@@ -85,11 +138,8 @@ bool start(const std::string& path, int hz) {
   g_path = path;
   g_period_ns = 1000000000L / hz;
   g_samples.reset(new Sample[kCapacity]);
-  {
-    uintptr_t warm[4];
-    Walk w{warm, 0};
-    _Unwind_Backtrace(walk_frame, &w);  // first use initialises the unwinder outside a handler
-  }
+  load_exec_ranges();
+  g_own_range = exec_range(uintptr_t(&on_prof));
   struct sigaction sa {};
   sa.sa_sigaction = on_prof;
   sa.sa_flags = SA_SIGINFO | SA_RESTART;
@@ -107,6 +157,7 @@ void register_thread() {
   sev.sigev_notify = SIGEV_THREAD_ID;
   sev.sigev_signo = SIGPROF;
   sev._sigev_un._tid = pid_t(syscall(SYS_gettid));
+  note_stack_bounds();
   if (timer_create(CLOCK_THREAD_CPUTIME_ID, &sev, &t_timer) != 0) return;
   {
     std::lock_guard<std::mutex> g(g_mu);

@@ -1,0 +1,312 @@
+"""BASELINE config 5, executed: `deploy/openshift/*.yaml` applied to a local one-node cluster
+(hola_amd/kube) — 8 probe-gated pods behind the LoadBalancer Service, pod-name HOSTNAMEs, a
+ConfigMap mounted through the kubelet's `..data` layout, `oc scale` and `oc set env` rollouts
+(`/root/reference/pom.xml:65-94`, `/root/reference/Readme.md:18-24`,
+`/root/reference/Dockerfile:3-8`).
+
+Probe delays and periods run at `time_scale` of their manifest values (0.1: the 5 s initial
+delay is 0.5 s); deadlines (probe timeout, grace period) are unscaled. The node is declared
+with 64 CPUs (`node_cpus`) so 8 pods requesting 2 CPUs each schedule on this 8-CPU
+container; their processes share its CPUs (CPU manager policy "none").
+"""
+from __future__ import annotations
+
+import json
+import os
+import signal
+import subprocess
+import threading
+import time
+from pathlib import Path
+
+import pytest
+import yaml
+
+from hola_amd import native
+from hola_amd.kube import Cluster
+from hola_amd.kube import manifests as m
+from hola_amd.kube.image import Image
+from hola_amd.kube.kubelet import project_configmap
+from hola_amd.utils.net import http_get
+
+ROOT = Path(__file__).resolve().parent.parent
+DC = ROOT / "deploy/openshift/hola-dc.yaml"
+DEPLOY = ROOT / "deploy/openshift/hola.yaml"
+CM = ROOT / "deploy/openshift/translation-configmap.yaml"
+PATCH = ROOT / "deploy/openshift/translation-patch.yaml"
+TS = 0.1
+
+
+@pytest.fixture
+def cluster(tmp_path, hola_bin):
+    made = []
+
+    def make(files=(DC,), **kw):
+        kw.setdefault("time_scale", TS)
+        kw.setdefault("node_cpus", 64)
+        kw.setdefault("service_port", 0)
+        c = Cluster([*files], state_dir=tmp_path / f"c{len(made)}", **kw).start()
+        made.append(c)
+        return c
+
+    yield make
+    for c in made:
+        c.close(grace_s=5)
+
+
+def _greet(c: Cluster, path: str = "/api/hola") -> tuple[int, str]:
+    host, port = c.service_ports["hola"]
+    st, _, body = http_get(host, port, path, timeout=5)
+    return st, body.decode()
+
+
+# ---------------------------------------------------------------------------- units
+def test_strategic_merge_patch_merges_containers_env_and_volumes():
+    dc = next(o for o in m.load_objects([DC]) if o["kind"] == "DeploymentConfig")
+    patch = yaml.safe_load(PATCH.read_text())
+    out = m.strategic_merge(dc, patch)
+    c = out["spec"]["template"]["spec"]["containers"][0]
+    env = {e["name"]: e.get("value") for e in c["env"]}
+    assert env["JAVA_OPTIONS"] == "-Xmx512m -Dconf=/etc/config/translation.properties"
+    assert env["ZIPKIN_SERVER_URL"] == "http://zipkin-query:9411"  # untouched entries stay
+    assert "HOSTNAME" in env and c["readinessProbe"]["httpGet"]["path"] == "/api/health"
+    assert c["volumeMounts"] == [{"name": "translation", "mountPath": "/etc/config", "readOnly": True}]
+    assert out["spec"]["template"]["spec"]["volumes"][0]["configMap"]["name"] == "translation"
+    # oc set env: replace one, add one, remove one
+    t = m.set_env(out["spec"]["template"], None, {"JAVA_OPTIONS": "-Xmx1g", "NEW": "1", "AB_OFF": None})
+    env2 = {e["name"]: e.get("value") for e in t["spec"]["containers"][0]["env"]}
+    assert env2["JAVA_OPTIONS"] == "-Xmx1g" and env2["NEW"] == "1" and "AB_OFF" not in env2
+
+
+def test_quantities_and_qos():
+    assert m.parse_cpu("2") == 2 and m.parse_cpu("500m") == 0.5
+    assert m.parse_memory("64Mi") == 64 << 20 and m.parse_memory("1G") == 10**9
+    assert m.resolve_int_or_percent("25%", 8, True) == 2 and m.resolve_int_or_percent("25%", 3, True) == 1
+    assert m.resolve_int_or_percent("25%", 3, False) == 0 and m.resolve_int_or_percent(1, 8, False) == 1
+    dc = next(o for o in m.load_objects([DC]) if o["kind"] == "DeploymentConfig")
+    assert m.qos_class(dc["spec"]["template"]["spec"]["containers"][0]) == "Guaranteed"
+    assert m.qos_class({"resources": {"requests": {"cpu": "1"}}}) == "Burstable"
+    assert m.qos_class({}) == "BestEffort"
+
+
+def test_image_is_read_from_the_dockerfile():
+    img = Image.from_dockerfile()
+    assert img.entrypoint == ["/app/hola", "--port", "8080", "--hystrix-config", "/app/conf/config.properties"]
+    assert img.env == {"AB_OFF": "true", "JAVA_OPTIONS": "-Xmx512m", "ZIPKIN_SERVER_URL": "http://zipkin-query:9411"}
+    assert img.exposed == [8080]
+    assert img.files["/app/hola"] == native.build_dir("release") / "hola"
+    assert img.files["/app/conf/config.properties"] == ROOT / "conf/config.properties"
+    assert img.files["/app/translation.properties"] == ROOT / "translation.properties"
+
+
+def test_configmap_projection_layout_and_atomic_update(tmp_path):
+    """The kubelet's atomic writer: files in `..<timestamp>/`, `..data` -> it, each key a link
+    through `..data`; an update swaps `..data` with one rename and removes the old directory."""
+    d = tmp_path / "vol"
+    project_configmap(d, {"translation.properties": "hello=A\n"})
+    assert os.readlink(d / "translation.properties") == "..data/translation.properties"
+    first = os.readlink(d / "..data")
+    assert first.startswith("..") and (d / first / "translation.properties").read_text() == "hello=A\n"
+    project_configmap(d, {"translation.properties": "hello=B\n", "extra": "x"})
+    second = os.readlink(d / "..data")
+    assert second != first and not (d / first).exists()
+    assert (d / "translation.properties").read_text() == "hello=B\n" and (d / "extra").read_text() == "x"
+    project_configmap(d, {"translation.properties": "hello=C\n"})
+    assert not (d / "extra").exists() and (d / "translation.properties").read_text() == "hello=C\n"
+
+
+# ---------------------------------------------------------------------------- the cluster
+def test_apply_scale_to_8_and_reach_8_pods_through_the_service(cluster):
+    """`oc apply -f hola-dc.yaml; oc scale dc/hola --replicas=8`: 8 pods named hola-1-xxxxx,
+    each answering with its own name (HOSTNAME from fieldRef metadata.name), all reached through
+    the Service once their readiness probe passed."""
+    c = cluster()
+    c.wait_ready(1, timeout=30)
+    c.scale(8)
+    c.wait_ready(8, timeout=60)
+    pods = c.get_pods()
+    assert len(pods) == 8 and all(p["name"].startswith("hola-1-") and len(p["name"]) == len("hola-1-abcde")
+                                  for p in pods)
+    names = {p["name"] for p in pods}
+    seen = set()
+    for _ in range(64):
+        st, body = _greet(c)
+        assert st == 200
+        seen.add(body)
+    assert seen == {f"Hola de {n}" for n in names}
+    # the Service gets the image's env and args: tracing to the zipkin-query stand-in
+    log = (c.state / "pods" / pods[0]["name"] / "container.log").read_text()
+    assert "--hystrix-config" in log and "--shutdown-delay-ms" in log
+    assert f"tracing=http://{c.subnet}.1:" in log
+    # scale down: the surplus pods terminate and leave the endpoints
+    c.scale(3)
+    c.wait_ready(3, timeout=30)
+    assert sum(p["status"] == "Terminating" for p in c.get_pods()) == 5  # serving out the shutdown delay
+    c.wait(lambda: len(c.get_pods()) == 3, 20, "terminated pods gone")
+
+
+def test_readiness_gates_endpoints_on_probe_timing(cluster):
+    """No pod is an endpoint before initialDelaySeconds (5 s x time_scale) has passed and its
+    first probe succeeded; a SIGKILLed container leaves the endpoints at once (NotReady),
+    restarts, and rejoins only after the initial delay again."""
+    c = cluster(replicas=2)
+    t0 = time.monotonic()
+    c.wait(lambda: len(c.endpoints(published=False)) == 2, 30, "2 ready pods")
+    assert time.monotonic() - t0 >= 5 * TS - 0.05
+    c.wait_ready(2, timeout=30)
+    victim = c.get_pods()[0]
+    ip = victim["ip"]
+    c.kill_container(victim["name"])
+    t_kill = time.monotonic()
+    c.wait(lambda: all(not e.startswith(ip + ":") for e in c.endpoints(published=False)), 5, "endpoint removal")
+    c.wait(lambda: all(not e.startswith(ip + ":") for e in c.endpoints()), 5, "published removal")
+    removed_after = time.monotonic() - t_kill
+    assert removed_after < 1.0
+    for _ in range(10):  # the Service only routes to the survivor meanwhile
+        assert _greet(c)[0] == 200
+    c.wait(lambda: any(e.startswith(ip + ":") for e in c.endpoints()), 30, "rejoin")
+    rejoined_after = time.monotonic() - t_kill
+    assert rejoined_after >= 5 * TS
+    p = next(p for p in c.get_pods() if p["name"] == victim["name"])
+    assert p["restarts"] == 1 and p["ready"]
+    reasons = [e[2] for e in c.events if e[1] == victim["name"]]
+    assert "Died" in reasons and reasons.count("Started") == 2
+
+
+def test_configmap_edit_reaches_every_pod(cluster):
+    """The demo's i18n flow: ConfigMap `translation` mounted at /etc/config (translation-patch),
+    selected by JAVA_OPTIONS -Dconf; an edit of the ConfigMap reaches all 8 pods through the
+    kubelet's `..data` swap without a restart."""
+    c = cluster(files=(DC, CM), patches=[PATCH], replicas=8, configmap_sync_s=10.0)
+    c.wait_ready(8, timeout=60)
+    pods = {p["name"] for p in c.get_pods()}
+    seen = {_greet(c)[1] for _ in range(48)}
+    assert seen == {f"Hola de {n} mediante el archivo de configuraciones\n" for n in pods}
+    c.apply_configmap("translation", {"translation.properties": "hello=Aloha de %s desde el ConfigMap\n"})
+    want = {f"Aloha de {n} desde el ConfigMap" for n in pods}
+
+    def all_updated():
+        return {_greet(c)[1] for _ in range(48)} == want
+    c.wait(all_updated, 20, "every pod serving the edited greeting")
+    assert all(p["restarts"] == 0 for p in c.get_pods())
+    assert sum(1 for e in c.events if e[2] == "ConfigMapSynced") == 8
+
+
+def test_unschedulable_pods_stay_pending(cluster):
+    """CPU requests against node capacity: on a 4-CPU node (1 reserved) only one pod asking
+    for 2 CPUs fits; the second is Pending with the scheduler's reason, never started."""
+    c = cluster(replicas=2, node_cpus=4)
+    c.wait(lambda: len(c.endpoints()) == 1, 30, "one endpoint")
+    time.sleep(0.3)
+    pods = c.get_pods()
+    pending = [p for p in pods if p["status"] == "Pending"]
+    assert len(pending) == 1 and "Insufficient cpu" in pending[0]["pending_reason"] and pending[0]["pid"] is None
+
+
+def test_static_cpu_manager_gives_exclusive_cpusets(cluster):
+    """cpu_manager_policy=static: a Guaranteed pod with integer CPUs gets its own cpuset (its
+    process affinity), disjoint from other pods and from the reserved CPU; hola then pins one
+    worker per CPU of it."""
+    if len(os.sched_getaffinity(0)) < 5:
+        pytest.skip("needs 5 CPUs")
+    c = cluster(replicas=2, node_cpus=None, cpu_manager_policy="static")
+    c.wait_ready(2, timeout=30)
+    pods = c.get_pods()
+    a, b = (set(p["cpus"]) for p in pods)
+    assert len(a) == len(b) == 2 and not a & b and min(os.sched_getaffinity(0)) not in a | b
+    for p in pods:
+        assert set(os.sched_getaffinity(p["pid"])) == set(p["cpus"])
+        log = (c.state / "pods" / p["name"] / "container.log").read_text()
+        assert "workers=2" in log
+
+
+def _loadgen(url: str, seconds: float, conns: int = 512, threads: int = 4) -> subprocess.Popen:
+    return subprocess.Popen([str(native.binary("hola_loadgen")), "-t", str(threads), "-c", str(conns),
+                             "-d", f"{seconds}s", "--json", url + "/api/hola"],
+                            stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+
+
+def _rollout_under_load(cluster, delay_ms: int) -> tuple[dict, Cluster]:
+    patch = {"spec": {"template": {"spec": {"containers": [
+        {"name": "hola", "args": ["--shutdown-delay-ms", str(delay_ms)]}]}}}}
+    c = cluster(replicas=8, endpoint_sync_s=5.0)  # kube-proxy applies changes 0.5 s late
+    c.patch(patch)
+    c.wait_ready(8, timeout=60)
+    lg = _loadgen(c.service_url(), 14.0)
+    time.sleep(2.0)
+    c.set_env({"JAVA_OPTIONS": "-Xmx512m -Drollout=2"})  # `oc set env dc/hola ...`: revision 3
+    c.wait(lambda: c.rollout_status()["complete"], 60, "rollout")
+    out, err = lg.communicate(timeout=60)
+    assert lg.returncode == 0, err
+    return json.loads(out.strip().splitlines()[-1]), c
+
+
+def test_rolling_update_under_load_has_no_errors_with_the_shutdown_delay(cluster):
+    """`oc set env` rolls 8 pods (maxSurge 25 %, maxUnavailable 25 %) while 512 kept-alive
+    connections load the Service. With the manifests' --shutdown-delay-ms, a terminating pod
+    fails readiness but keeps serving until kube-proxy has dropped it, and closes its
+    connections between responses: no connection error, no non-2xx."""
+    r, c = _rollout_under_load(cluster, 1500)
+    lat = r["latency"]
+    assert lat["count"] > 1000
+    assert lat["errors"] == 0 and lat["non2xx"] == 0, r
+    assert lat["reconnects"] > 0  # clients did move off the terminating pods
+    st = c.rollout_status()
+    assert st["revision"] == 3 and st["ready"] == 8
+    assert all(p["revision"] == 3 for p in c.get_pods())
+
+
+def test_rolling_update_without_the_delay_drops_connections(cluster):
+    """The same rollout with --shutdown-delay-ms 0: a terminating pod stops listening at once,
+    while kube-proxy still routes new connections to it for the sync delay, so clients see
+    refused/reset connections."""
+    r, _ = _rollout_under_load(cluster, 0)
+    assert r["latency"]["errors"] > 0, r
+
+
+def test_deployment_flavour_rolls_out_by_template_hash(cluster):
+    """hola.yaml (apps/v1 Deployment): ReplicaSets named by the pod-template hash; a template
+    change rolls out a new one and the old one scales to 0."""
+    c = cluster(files=(DEPLOY,), replicas=3)
+    c.wait_ready(3, timeout=30)
+    first = {p["owner"] for p in c.get_pods()}
+    assert len(first) == 1 and next(iter(first)).startswith("hola-")
+    c.set_env({"hello": "Hi from %s"})  # env `hello` is the ordinal-300 source of the greeting
+    c.wait(lambda: c.rollout_status()["complete"], 60, "rollout")
+    owners = {p["owner"] for p in c.get_pods()}
+    assert len(owners) == 1 and owners != first
+    c.wait_ready(3, timeout=30)
+    assert {_greet(c)[1] for _ in range(24)} == {f"Hi from {p['name']}" for p in c.get_pods()}
+
+
+def test_oc_command_line(tmp_path, hola_bin):
+    """`python -m hola_amd apply` in the foreground, driven by `python -m hola_amd oc`."""
+    state = tmp_path / "state"
+    env = {**os.environ, "PYTHONPATH": str(ROOT)}
+    ap = subprocess.Popen(["python", "-m", "hola_amd", "apply", "-f", str(DC), "--replicas", "2", "--state-dir",
+                           str(state), "--time-scale", str(TS), "--service-port", "0", "--node-cpus", "64"],
+                          cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+
+    def oc(*args):
+        return subprocess.run(["python", "-m", "hola_amd", "oc", "--state-dir", str(state), *args], cwd=ROOT,
+                              env=env, capture_output=True, text=True, timeout=60)
+    try:
+        deadline = time.monotonic() + 30
+        while not (state / "control.sock").exists() and time.monotonic() < deadline:
+            time.sleep(0.05)
+        assert oc("rollout", "status", "dc/hola", "--timeout", "30").returncode == 0
+        out = oc("get", "pods").stdout
+        assert out.count("1/1") == 2 and "Running" in out
+        assert oc("scale", "dc/hola", "--replicas=3").returncode == 0
+        assert oc("set", "env", "dc/hola", "hello=Hey %s").returncode == 0
+        assert oc("rollout", "status", "dc/hola", "--timeout", "60").returncode == 0
+        url = oc("url").stdout.strip()
+        time.sleep(5 * TS * 2)
+        host, port = url.split("//")[1].split(":")
+        bodies = {http_get(host, int(port), "/api/hola")[2].decode() for _ in range(20)}
+        assert all(b.startswith("Hey hola-2-") for b in bodies), bodies
+        assert "Synced" in oc("get", "events").stdout
+    finally:
+        oc("stop")
+        ap.wait(timeout=30)
+    assert ap.returncode == 0
