@@ -20,6 +20,7 @@
 #   tracing            headline without a collector, with the native Zipkin sink (default 1000-span
 #                      export budget, and unbounded), and with tracing off
 #   soak MINUTES [ARGS] mixed-load soak sampling RSS and FDs (ARGS go to bench/soak.py)
+#   uringchain         io_uring vs epoll on the chaining hop's four syscalls (bench/probes/uring_chain.cc)
 #   kube [ARGS]        BASELINE config 5: deploy/openshift applied by the local executor at real
 #                      timings (8 pods, probes, rollouts under 512-connection load, SIGKILL,
 #                      ConfigMap edit; ARGS go to bench/kube_rollout.py)
@@ -41,6 +42,12 @@ final)
   ;;
 bench)
   timeout -k 10 400 python bench.py "$@" > "$OUT/bench.json" 2>> "$OUT/err.log"
+  ;;
+uringchain)
+  # the chaining hop's four syscalls per request: epoll vs one io_uring batch per loop pass
+  g++ -O2 -std=c++20 -pthread bench/probes/uring_chain.cc -o /tmp/uring_chain &&
+  timeout -k 10 200 /tmp/uring_chain --hop-cpu 8 --aloha-cpu 9 --client-cpus 10,11 --connections 64 \
+    --rounds 6 --seconds 3 > "$OUT/uring_chain.jsonl" 2>> "$OUT/err.log"
   ;;
 kube)
   timeout -k 10 540 python -u bench/kube_rollout.py --out "$OUT/run" "$@" > "$OUT/kube.json" 2> "$OUT/kube.log"
