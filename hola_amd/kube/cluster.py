@@ -75,7 +75,8 @@ class Cluster:
             raise ValueError("cpu_manager_policy is 'none' or 'static'")
         self.objects = m.load_objects(files)
         self.patches = [o for p in patches for o in m.load_objects([p])]
-        self.state = Path(state_dir) if state_dir else Path(tempfile.mkdtemp(prefix="hola-cluster-"))
+        # absolute: pods run with their own working directory
+        self.state = Path(state_dir).resolve() if state_dir else Path(tempfile.mkdtemp(prefix="hola-cluster-"))
         self.state.mkdir(parents=True, exist_ok=True)
         self.namespace, self.node_name = namespace, "mi355x-node"
         self.time_scale = float(time_scale)

@@ -254,9 +254,19 @@ class Kubelet:
         log = open(pod.log_path, "ab")
         log.write(f"--- start {time.strftime('%H:%M:%S')} restart={pod.restarts} argv={argv}\n".encode())
         log.flush()
-        pod.proc = subprocess.Popen(argv, env=env, cwd=workdir, stdout=log, stderr=log,
-                                    preexec_fn=(lambda: os.sched_setaffinity(0, cpus)) if cpus else None,
-                                    start_new_session=True)
+        try:
+            pod.proc = subprocess.Popen(argv, env=env, cwd=workdir, stdout=log, stderr=log,
+                                        preexec_fn=(lambda: os.sched_setaffinity(0, cpus)) if cpus else None,
+                                        start_new_session=True)
+        except OSError as e:
+            # CreateContainerError / RunContainerError: retried with the restart back-off
+            log.write(f"--- cannot start the container: {e}\n".encode())
+            log.close()
+            pod.proc = subprocess.Popen(["/bin/false"])  # an exited container, for the back-off
+            pod.proc.wait()
+            pod.started_at = now
+            self.cluster.event(pod.name, "Failed", f"cannot start the container: {e}")
+            return
         log.close()
         pod.started_at = now
         pod.ready = False
