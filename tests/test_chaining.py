@@ -842,3 +842,43 @@ def test_refused_aloha_costs_no_transport_retry(hola, pipelined):
     assert all(st == 200 and body[1:] == [FALLBACK] for st, body in res), res
     assert _retries(s).get("transport", 0) == 0
     assert _events(s).get("FAILURE") == 6
+
+
+def test_read_timeout_runs_after_a_slow_connect(hola):
+    """Feign's read timeout is armed once the connect completes: a connect that takes longer
+    than the read timeout (its SYN dropped by a full accept queue and retransmitted ~1 s later)
+    followed by a server that never answers still ends with SocketTimeoutException, instead of
+    the deadline expiring unused while the connect was pending and the call hanging."""
+    lsock = socket.socket()
+    lsock.bind(("127.0.0.1", 0))
+    lsock.listen(0)  # one pending connection fills the accept queue
+    port = lsock.getsockname()[1]
+    filler = socket.create_connection(("127.0.0.1", port))
+    filler2 = socket.socket()
+    filler2.setblocking(False)
+    filler2.connect_ex(("127.0.0.1", port))
+    accepted = []
+
+    def drain_later():
+        time.sleep(0.5)  # after hola's SYN was dropped: make room for its retransmission
+        deadline = time.monotonic() + 5
+        lsock.settimeout(0.2)
+        while time.monotonic() < deadline:
+            try:
+                accepted.append(lsock.accept()[0])  # accepted, never answered
+            except OSError:
+                pass
+
+    s = hola(args=["--aloha-url", f"http://127.0.0.1:{port}/", "--no-tracing", "--feign-log", "basic",
+                   "--feign-retry", "off", "--feign-timeouts", "5000,300",
+                   "-Dhystrix.command.default.execution.timeout.enabled=false"], threads=1)
+    t = threading.Thread(target=drain_later, daemon=True)
+    t.start()
+    t0 = time.monotonic()
+    assert chain(s)[1:] == [FALLBACK]
+    dt = time.monotonic() - t0
+    assert dt < 4.5, dt
+    assert "<--- ERROR SocketTimeoutException: Read timed out" in _wait_log(s, "SocketTimeoutException", 1)
+    t.join()
+    for c in accepted + [filler, filler2, lsock]:
+        c.close()
