@@ -38,8 +38,15 @@ def log(msg: str) -> None:
 
 
 def greetings(c: Cluster, n: int = 64) -> list[str]:
+    """n GETs through the Service; a failed one is recorded as an "ERROR ..." entry."""
     host, port = c.service_ports["hola"]
-    return [http_get(host, port, "/api/hola", timeout=5)[2].decode() for _ in range(n)]
+    out = []
+    for _ in range(n):
+        try:
+            out.append(http_get(host, port, "/api/hola", timeout=5)[2].decode())
+        except OSError as e:
+            out.append(f"ERROR {type(e).__name__}: {e}")
+    return out
 
 
 def rollout_under_load(c: Cluster, env: dict, conns: int, threads: int, settle_s: float) -> dict:

@@ -17,7 +17,8 @@
 // Service mode (`python -m hola_amd apply`, the local manifest executor): --endpoints-file F
 // takes the backend set from F (one host:port per line), re-read whenever it changes; the
 // executor writes the Ready pods there, the role of the Endpoints object that kube-proxy
-// follows. --health-ms 0 turns the proxy's own probing off (kube-proxy does not probe), and
+// follows. After applying a file whose first line is `# gen N`, the proxy writes N to
+// F.applied, so the writer knows when new connections follow the new set. --health-ms 0 turns the proxy's own probing off (kube-proxy does not probe), and
 // --no-failover makes a connection to a backend that refuses fail as it does through
 // kube-proxy's DNAT rules, instead of being retried on the next backend. Sessions keep their
 // backend when it leaves the set (conntrack keeps established flows).
@@ -148,6 +149,15 @@ void endpoints_loop(std::string path) {
         fprintf(stderr, "rrproxy: endpoints now %zu backends\n", current_set().list.size());
         last = st;
         have = true;
+        unsigned long long gen = 0;
+        if (sscanf(text.c_str(), "# gen %llu", &gen) == 1) {
+          const std::string tmp = path + ".applied.tmp";
+          if (FILE* f = fopen(tmp.c_str(), "w")) {
+            fprintf(f, "%llu\n", gen);
+            fclose(f);
+            rename(tmp.c_str(), (path + ".applied").c_str());
+          }
+        }
       }
     }
     std::this_thread::sleep_for(std::chrono::milliseconds(10));

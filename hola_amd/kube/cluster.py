@@ -129,6 +129,7 @@ class Cluster:
         self._cm_due: list[tuple[float, str, str]] = []  # (due, pod, configmap)
         self._ep_desired: dict[str, list[str]] = {}
         self._ep_published: dict[str, list[str]] = {}
+        self._ep_written: dict[str, tuple[int, list[str]]] = {}  # (generation, endpoints) in the file
         self._ep_pending_since: dict[str, float] = {}
         self.endpoint_history: dict[str, list[tuple[float, list[str]]]] = {}
         self._last_rollout_step = 0.0
@@ -415,10 +416,20 @@ class Cluster:
             if since is not None and now - since >= self.endpoint_sync_s * self.time_scale:
                 del self._ep_pending_since[name]
                 cur = self._ep_desired[name]
-                if cur != self._ep_published.get(name):
+                if cur != self._ep_written.get(name, (0, None))[1]:
+                    gen = self._ep_written.get(name, (0, None))[0] + 1
                     tmp = self.state / "endpoints" / f".{name}.tmp"
-                    tmp.write_text("".join(e + "\n" for e in cur))
+                    tmp.write_text(f"# gen {gen}\n" + "".join(e + "\n" for e in cur))
                     os.replace(tmp, self.state / "endpoints" / name)  # rrproxy re-reads on change
+                    self._ep_written[name] = (gen, list(cur))
+            # published = what the proxy routes new connections to (it acknowledges each file)
+            gen, cur = self._ep_written.get(name, (0, None))
+            if cur is not None and cur != self._ep_published.get(name):
+                try:
+                    applied = int((self.state / "endpoints" / f"{name}.applied").read_text().strip() or 0)
+                except (OSError, ValueError):
+                    applied = 0
+                if applied >= gen:
                     self._ep_published[name] = list(cur)
                     self.endpoint_history.setdefault(name, []).append((now - self.t0, list(cur)))
                     self.event(f"endpoints/{name}", "Synced", f"{len(cur)} ready: {' '.join(cur)}")
