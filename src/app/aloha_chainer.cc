@@ -248,7 +248,7 @@ void AlohaChainer::call(http::Worker& w, const tracing::SpanContext* parent,
   // between them.
   const int timeout_ms = timeout_ms_.load(std::memory_order_relaxed);
   if (timeout_ms <= 0) return;
-  const WorkerCalls::Pending e{mono_ms() + timeout_ms, slot, gen};
+  const WorkerCalls::Pending e{start_ms + timeout_ms, slot, gen};
   if (wc.fifo.empty() || wc.fifo.back().deadline_ms <= e.deadline_ms) {
     wc.fifo.push_back(e);
   } else {

@@ -65,7 +65,7 @@ struct AlohaOptions {
 class AlohaChainer final : public Chainer {
  public:
   AlohaChainer(AlohaOptions o, resilience::Settings s, int num_workers, tracing::Tracer* tracer,
-               const Clock& clock = SystemClock::instance());
+               const Clock& clock = LoopClock::instance());
   ~AlohaChainer() override;
   bool ok() const { return url_ok_; }
   void start();  // DNS refresher

@@ -43,6 +43,23 @@ class SystemClock final : public Clock {
   }
 };
 
+// The time of the event loop running on this thread, read once per loop pass (EventLoop::run
+// publishes it here): millisecond bookkeeping on the request path (Hystrix windows and
+// timeouts, Feign timings) costs no clock read per call. Off a loop thread, mono_ms().
+inline thread_local const int64_t* t_loop_now_ms = nullptr;
+
+class LoopClock final : public Clock {
+ public:
+  int64_t now_ms() const override {
+    const int64_t* p = t_loop_now_ms;
+    return p ? *p : mono_ms();
+  }
+  static LoopClock& instance() {
+    static LoopClock c;
+    return c;
+  }
+};
+
 class FakeClock final : public Clock {
  public:
   explicit FakeClock(int64_t start = 1000000) : t_(start) {}

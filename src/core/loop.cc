@@ -130,23 +130,31 @@ int EventLoop::next_timeout_ms() {
 void EventLoop::run() {
   constexpr int kMaxEvents = 256;
   epoll_event evs[kMaxEvents];
+  t_loop_now_ms = &now_ms_;  // LoopClock on this thread reads the pass's time
   while (!stop_.load(std::memory_order_relaxed)) {
     if (tick_) tick_();
     int n = 0;
+    int64_t t = 0;  // mono_ns() at (or just before) the moment events were found
     if (busy_poll_ns_ > 0) {
-      int64_t until = mono_ns() + busy_poll_ns_;
+      t = mono_ns();
+      const int64_t until = t + busy_poll_ns_;
       for (;;) {
         n = epoll_wait(epfd_, evs, kMaxEvents, 0);
-        if (n != 0 || mono_ns() >= until || stop_.load(std::memory_order_relaxed)) break;
+        if (n != 0 || stop_.load(std::memory_order_relaxed)) break;
+        t = mono_ns();
+        if (t >= until) break;
         for (int i = 0; i < busy_poll_pause_; ++i) __builtin_ia32_pause();
       }
     }
-    if (n == 0) n = epoll_wait(epfd_, evs, kMaxEvents, next_timeout_ms());
+    if (n == 0) {
+      n = epoll_wait(epfd_, evs, kMaxEvents, next_timeout_ms());
+      t = mono_ns();
+    }
     if (n < 0 && errno != EINTR) {
       perror("epoll_wait");
       break;
     }
-    now_ms_ = mono_ms();
+    now_ms_ = t / 1000000;
     for (int i = 0; i < n; ++i) static_cast<Handler*>(evs[i].data.ptr)->on_event(evs[i].events);
     if (!heap_.empty()) run_timers();
     while (!deferred_.empty()) {
@@ -159,6 +167,7 @@ void EventLoop::run() {
       retired_.clear();
     }
   }
+  t_loop_now_ms = nullptr;
   drain_posted();
   if (on_exit_) on_exit_();
 }

@@ -38,6 +38,10 @@ def test_bench_json_contract_on_host():
     assert out["body_checked"] == out["requests"] and out["body_mismatch"] == 0
     # BASELINE config 2 ran after the timed region, and placement was reported
     assert out["c1_errors"] == 0 and out["c1_rps"] > 10000 and out["c1_body_checked"] == out["c1_requests"]
+    # ... and the replica exactly as the image and manifests start it (no busy-polling)
+    assert out["deployed_errors"] == 0 and out["deployed_non2xx"] == 0 and out["deployed_rps"] > 10000
+    assert "--shutdown-delay-ms 5000" in out["deployed_args"] and "--busy-poll" not in out["deployed_args"]
+    assert out["config"]["smt"] in ("off", "split", "pair") and "GPU slot" in out["config"]["layout_note"]
     assert abs(sum(out["locality"]["fraction"].values()) - 1.0) < 1e-3
 
 
@@ -111,3 +115,23 @@ def test_proxy_front_on_host():
     row = json.loads(next(l for l in buf.getvalue().splitlines() if l.startswith("{")))
     assert row["errors"] == 0 and row["non2xx"] == 0 and row["lb"] == "proxy"
     assert row["rps"] > 100_000
+
+
+@pytest.mark.gpu
+def test_manifests_execute_on_host():
+    """BASELINE config 5 on the real host, at 0.1x the probe timings: hola-dc.yaml + the
+    translation ConfigMap + patch as 8 pods behind the Service, a rollout under 512
+    connections with the manifests' shutdown delay (0 errors), a SIGKILLed pod rejoining, a
+    ConfigMap edit reaching every pod (bench/kube_rollout.py; profiles/round3/01_kube has the
+    run at real timings)."""
+    out_dir = ROOT / "gpurun_out" / "pytest_kube"
+    r = subprocess.run([sys.executable, str(ROOT / "bench" / "kube_rollout.py"), "--out", str(out_dir),
+                        "--time-scale", "0.1", "--configmap-sync-s", "5", "--policy", "none"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["greetings_seen"] == 8 and res["greetings_match_pods"]
+    assert res["rollout_with_delay"]["errors"] == 0 and res["rollout_with_delay"]["non2xx"] == 0
+    assert res["rollout_with_delay"]["requests"] > 10000
+    assert res["sigkill"]["restarts"] == 1
+    assert res["configmap_edit_all_pods_s"] < 60
