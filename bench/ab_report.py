@@ -6,6 +6,9 @@ side's `host_load.siblings` (busy share of the SMT siblings of the replica's cor
 tenants on our physical cores) exceeds --max-sibling-load. For the kept pairs it reports the
 paired difference of server CPU µs per request (the primary metric: the server's own cost,
 which sibling load and client jitter move least) and of req/s, with a 95 % t-interval.
+Because the sibling load moves every run's cost, it also fits one line through all runs of
+both variants, server µs/request = a + d * [candidate] + b * sibling load, and reports d (the
+candidate's cost at equal sibling load) with its 95 % interval: a gate that keeps every run.
 
   python bench/ab_report.py DIR --baseline r1 --candidate final [--max-sibling-load 0.02]
 """
@@ -51,6 +54,30 @@ def sib(r: dict) -> float:
     return max(h.get("siblings", 0.0) for h in r.get("host_load", [{}]))
 
 
+def adjusted(rows: list[dict]) -> dict | None:
+    """Least squares us = a + d*cand + b*sib over both variants' runs; d with a 95 % interval."""
+    import numpy as np
+
+    ys, xs = [], []
+    for r in rows:
+        ys += [r["us_base"], r["us_cand"]]
+        xs += [[1.0, 0.0, r["sib_base"]], [1.0, 1.0, r["sib_cand"]]]
+    if len(ys) < 5:
+        return None
+    X, y = np.array(xs), np.array(ys)
+    coef, *_ = np.linalg.lstsq(X, y, rcond=None)
+    resid = y - X @ coef
+    dof = len(y) - 3
+    s2 = float(resid @ resid) / dof
+    cov = s2 * np.linalg.inv(X.T @ X)
+    se = math.sqrt(cov[1, 1])
+    base = coef[0] + coef[2] * statistics.fmean([r["sib_base"] for r in rows])
+    h = t95(dof) * se
+    return {"delta_us": round(float(coef[1]), 4), "delta_pct": round(100 * float(coef[1]) / base, 2),
+            "ci95_pct": [round(100 * float(coef[1] - h) / base, 2), round(100 * float(coef[1] + h) / base, 2)],
+            "us_per_sibling_pct": round(float(coef[2]) / 100, 4), "runs": len(y)}
+
+
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("dir")
@@ -88,6 +115,12 @@ def main() -> int:
         print(f"  req/s        : {m2:+.2f} % (95 % CI {lo2:+.2f} .. {hi2:+.2f})")
     else:
         print("\nno pair passed the sibling-load gate")
+    adj = adjusted(rows)
+    if adj:
+        res["server_us_per_req_adjusted"] = adj
+        print(f"  adjusted for sibling load (all {len(rows)} pairs): candidate {adj['delta_pct']:+.2f} % server us/req "
+              f"(95 % CI {adj['ci95_pct'][0]:+.2f} .. {adj['ci95_pct'][1]:+.2f}); "
+              f"+{adj['us_per_sibling_pct']:.3f} us per sibling-load percent")
     if a.json:
         Path(a.json).write_text(json.dumps(res, indent=1) + "\n")
     return 0
