@@ -390,9 +390,9 @@ int main(int argc, char** argv) {
     // Phase 1: fail readiness, keep accepting, close connections between responses. The
     // pod's endpoint removal takes a while to reach every proxy (kube-proxy's sync); new
     // connections routed here meanwhile are still served.
+    server.begin_termination();  // before the log line: the line says it has happened
     LOG_INFO("received %s: readiness failing, still serving for %d ms", sig_name, shutdown_delay_ms);
     Logger::instance().flush();
-    server.begin_termination();
     timespec ts{shutdown_delay_ms / 1000, long(shutdown_delay_ms % 1000) * 1000000L};
     siginfo_t si;
     if (sigtimedwait(&sigs, &si, &ts) > 0) LOG_INFO("second termination signal: ending the delay early");
