@@ -34,7 +34,6 @@ Everything runs on one control-loop thread (`_loop`); the public methods take th
 from __future__ import annotations
 
 import copy
-import itertools
 import os
 import random
 import signal
@@ -95,10 +94,13 @@ class Cluster:
         self.events: list[tuple[float, str, str, str]] = []
         self._events_f = open(self.state / "events.log", "a")
         self.t0 = time.monotonic()
-        # pod network: 127.<a>.<b>.0/24 per cluster (.1 = stand-in Services, .2.. = pods)
+        # pod network: 127.<a>.0.0/16 per cluster (127.<a>.0.1 = stand-in Services, pods from
+        # 127.<a>.0.2 on; .0 and .255 host parts are skipped): room for 65 k pods over the
+        # executor's life, so rollouts never exhaust it
         rnd = random.Random()
-        self.subnet = f"127.{rnd.randrange(100, 250)}.{rnd.randrange(0, 256)}"
-        self._ips = itertools.count(2)
+        self.net = f"127.{rnd.randrange(100, 250)}"
+        self.subnet = f"{self.net}.0"
+        self._ips = (f"{self.net}.{b}.{c}" for b in range(256) for c in range(1, 255) if (b, c) != (0, 1))
         self.services: dict[str, dict] = {}
         self.configmaps: dict[str, dict[str, str]] = {}
         self.workload: dict | None = None
@@ -358,8 +360,8 @@ class Cluster:
             labels.update({"deployment": rc.name, "deploymentconfig": self.name})
         else:
             labels["pod-template-hash"] = rc.name.rsplit("-", 1)[-1]
-        ip = f"{self.subnet}.{next(self._ips)}"
-        if ip.endswith(".255"):
+        ip = next(self._ips, None)
+        if ip is None:
             raise ClusterError("pod network exhausted")
         c = rc.template["spec"]["containers"][0]
         res = c.get("resources") or {}

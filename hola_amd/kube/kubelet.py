@@ -120,6 +120,7 @@ class Pod:
     deletion_at: float = 0.0
     grace_deadline: float = 0.0
     prestop: subprocess.Popen | None = None
+    prestop_http: Future | None = None
     term_sent: bool = False
     gone: bool = False
 
@@ -352,9 +353,10 @@ class Kubelet:
             cmd = [self.map_paths(pod, a) for a in pre["exec"]["command"]]
             pod.prestop = subprocess.Popen(cmd, env=self._env(pod), stdout=subprocess.DEVNULL,
                                            stderr=subprocess.DEVNULL, start_new_session=True)
-        elif pod.running and "httpGet" in pre:
+        elif pod.running and "httpGet" in pre:  # off the control loop, like the probes
             hg = pre["httpGet"]
-            http_probe(pod.ip, _port_number(pod.container, hg.get("port", 8080)), hg.get("path", "/"), 5.0)
+            pod.prestop_http = self.pool.submit(http_probe, pod.ip, _port_number(pod.container, hg.get("port", 8080)),
+                                                hg.get("path", "/"), float(pod.grace_deadline - now))
         self.cluster.event(pod.name, "Killing", f"grace {pod.grace_deadline - now:.0f}s")
 
     def _tick_terminating(self, pod: Pod, now: float) -> None:
@@ -365,7 +367,9 @@ class Kubelet:
             self.cluster.event(pod.name, "Deleted",
                                f"exit {pod.proc.returncode if pod.proc else None} after {now - pod.deletion_at:.2f}s")
             return
-        if not pod.term_sent and (pod.prestop is None or pod.prestop.poll() is not None or now >= pod.grace_deadline):
+        hook_done = (pod.prestop is None or pod.prestop.poll() is not None) and \
+            (pod.prestop_http is None or pod.prestop_http.done())
+        if not pod.term_sent and (hook_done or now >= pod.grace_deadline):
             pod.proc.send_signal(signal.SIGTERM)
             pod.term_sent = True
         if now >= pod.grace_deadline:

@@ -310,3 +310,28 @@ def test_oc_command_line(tmp_path, hola_bin):
         oc("stop")
         ap.wait(timeout=30)
     assert ap.returncode == 0
+
+
+def test_prestop_hook_runs_before_sigterm(cluster):
+    """lifecycle.preStop: an exec hook runs to completion before the container gets SIGTERM
+    (within the grace period); an httpGet hook is called on the pod without blocking the
+    control loop."""
+    patch = {"spec": {"template": {"spec": {"containers": [{"name": "hola", "args": ["--shutdown-delay-ms", "0"],
+                                                             "lifecycle": {"preStop": {"exec": {"command": ["sleep", "1"]}}}}]}}}}
+    c = cluster(replicas=1)
+    c.patch(patch)
+    c.wait(lambda: c.rollout_status()["complete"] and c.rollout_status()["revision"] == 2, 30, "rollout")
+    c.wait(lambda: len(c.get_pods()) == 1, 30, "old pod gone")
+    name = c.get_pods()[0]["name"]
+    t0 = time.monotonic()
+    c.delete_pod(name)
+    c.wait(lambda: all(p["name"] != name for p in c.get_pods()), 30, "pod gone")
+    assert time.monotonic() - t0 >= 0.95  # SIGTERM only after the 1 s hook
+    log = (c.state / "pods" / name / "container.log").read_text()
+    assert "received SIGTERM: draining" in log
+    # httpGet flavour: the hook's request reaches the pod before its termination
+    c.patch({"spec": {"template": {"spec": {"containers": [{"name": "hola", "lifecycle": {"preStop": {
+        "httpGet": {"path": "/api/health", "port": 8080}}}}]}}}})
+    c.wait(lambda: c.rollout_status()["complete"] and c.rollout_status()["revision"] == 3, 30, "rollout")
+    c.wait(lambda: len(c.get_pods()) == 1, 30, "old pod gone")
+    assert any(e[2] == "Deleted" for e in c.events)
