@@ -125,6 +125,7 @@ struct AlohaChainer::WorkerCalls {
   int64_t timer_at = 0;  // deadline the armed timer fires for (0 = none armed)
   http::Worker* worker = nullptr;
   AlohaChainer* owner = nullptr;
+  std::string headers;  // the B3 headers of the execution being started (capacity reused)
 };
 
 AlohaChainer::WorkerCalls& AlohaChainer::calls(http::Worker& w) {
@@ -288,7 +289,8 @@ void AlohaChainer::execute(http::Worker& w, WorkerCalls& wc, uint32_t slot, uint
   c.inflight = true;
   c.req_id = 0;
   c.traced = false;
-  std::string headers;
+  std::string& headers = wc.headers;
+  headers.clear();
   if (c.has_parent && tracer_) {
     // Brave's HttpClient interceptors open a client span per executed request.
     c.ctx = tracer_->new_child(w.index(), c.parent);

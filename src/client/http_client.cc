@@ -197,7 +197,7 @@ void ClientPool::Conn::fail(const std::string& why, bool io) {
     auto* fresh = new Conn();
     fresh->pool = p;
     fresh->tries = t;
-    p->start_on(fresh, rid, std::move(r), std::move(c), false);
+    p->start_on(fresh, rid, &r, std::move(c), false);
     return;
   }
   ClientResult res;
@@ -445,6 +445,15 @@ ClientPool::~ClientPool() {
 
 std::string ClientPool::build_request(const std::string& path, const std::string& extra) const {
   std::string r;
+  build_request_into(&r, path, extra);
+  return r;
+}
+
+void ClientPool::build_request_into(std::string* out, const std::string& path, const std::string& extra) const {
+  // Into a connection's own buffer: a kept-alive connection reuses its capacity, so the
+  // request costs no allocation.
+  std::string& r = *out;
+  r.clear();
   r.reserve(128 + extra.size());
   r += "GET ";
   r += path;
@@ -453,22 +462,25 @@ std::string ClientPool::build_request(const std::string& path, const std::string
   r += "\r\nAccept: application/json\r\nConnection: keep-alive\r\n";
   r += extra;
   r += "\r\n";
-  return r;
 }
 
 uint64_t ClientPool::get(const std::string& path, const std::string& extra_headers, Callback cb) {
   uint64_t id = next_id_++;
-  std::string req = build_request(path, extra_headers);
-  if (pipeline_ > 1 && get_pipelined(id, req, cb)) return id;
-  if (!idle_.empty()) {
-    Conn* c = idle_.back();
-    idle_.pop_back();
-    start_on(c, id, std::move(req), std::move(cb), true);
-  } else {
-    auto* c = new Conn();
-    c->pool = this;
-    start_on(c, id, std::move(req), std::move(cb), false);
+  if (pipeline_ > 1) {
+    std::string req = build_request(path, extra_headers);
+    if (get_pipelined(id, req, cb)) return id;
   }
+  const bool reused = !idle_.empty();
+  Conn* c;
+  if (reused) {
+    c = idle_.back();
+    idle_.pop_back();
+  } else {
+    c = new Conn();
+    c->pool = this;
+  }
+  build_request_into(&c->out, path, extra_headers);
+  start_on(c, id, nullptr, std::move(cb), reused);
   return id;
 }
 
@@ -545,11 +557,11 @@ void ClientPool::pop_finished(DeadlineFifo& f) {
   while (!f.q.empty() && !live(f.q.front())) f.q.pop_front();
 }
 
-void ClientPool::start_on(Conn* c, uint64_t id, std::string req, Callback cb, bool reused) {
+void ClientPool::start_on(Conn* c, uint64_t id, std::string* req, Callback cb, bool reused) {
   c->id = id;
   c->serial = next_serial_++;
   c->cb = std::move(cb);
-  c->out = std::move(req);
+  if (req) c->out = std::move(*req);  // else the caller built it in c->out
   c->off = 0;
   c->in.clear();
   c->reused = reused;
@@ -889,7 +901,7 @@ void ClientPool::resubmit(uint64_t id, std::string req, Callback cb, int tries, 
   auto* fresh = new Conn();
   fresh->pool = this;
   fresh->tries = tries;
-  start_on(fresh, id, std::move(req), std::move(cb), false);
+  start_on(fresh, id, &req, std::move(cb), false);
 }
 
 }  // namespace hola::client

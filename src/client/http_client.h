@@ -102,10 +102,12 @@ class ClientPool {
   friend struct Conn;
   struct PConn;
   friend struct PConn;
-  void start_on(Conn* c, uint64_t id, std::string req, Callback cb, bool reused);
+  // `req` (moved in) is the request, or null when it is already in c->out.
+  void start_on(Conn* c, uint64_t id, std::string* req, Callback cb, bool reused);
   void finish(Conn* c, ClientResult&& r, bool reusable);
   void destroy(Conn* c);
   std::string build_request(const std::string& path, const std::string& extra) const;
+  void build_request_into(std::string* out, const std::string& path, const std::string& extra) const;
   std::string connect_error(int err) const;
 
   EventLoop& loop_;
