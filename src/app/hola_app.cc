@@ -47,6 +47,9 @@ struct HolaApp::WorkerCache {
   // "Content-Length: " per keep-alive mode, and the body's `["<greeting>"` prefix.
   std::string chain_head[2];
   std::string chain_json_prefix;
+  // Success responses of /api/hola-chaining are assembled here (capacity kept between calls;
+  // Connection::complete copies the bytes before anything else can run on this worker).
+  std::string chain_resp;
 };
 
 const char* HolaApp::route_name(int r) {
@@ -488,7 +491,8 @@ void HolaApp::handle_chaining(http::Connection& c, const http::Request& r, Worke
                      if (wc.content == content) {
                        size_t body_len = wc.chain_json_prefix.size() + 1;
                        for (auto& it : res.items) body_len += 1 + (it ? it->size() + 2 : 4);
-                       std::string resp;
+                       std::string& resp = wc.chain_resp;
+                       resp.clear();
                        resp.reserve(wc.chain_head[ka].size() + 48 + body_len + 16);
                        resp += wc.chain_head[ka];
                        const size_t len_at = resp.size();
