@@ -126,6 +126,10 @@ struct AlohaChainer::WorkerCalls {
   http::Worker* worker = nullptr;
   AlohaChainer* owner = nullptr;
   std::string headers;  // the B3 headers of the execution being started (capacity reused)
+  // The result handed to the finished call's callback. Reused, so aloha's list is decoded
+  // into strings that keep their capacity; callbacks read it before they can start another
+  // call on this worker.
+  ChainResult result;
 };
 
 AlohaChainer::WorkerCalls& AlohaChainer::calls(http::Worker& w) {
@@ -346,7 +350,9 @@ void AlohaChainer::on_response(http::Worker& w, WorkerCalls& wc, uint32_t slot, 
       Logger::instance().raw("%s<--- ERROR %s (%lldms)", log_tag_.c_str(), r.error.c_str(),
                              (long long)(now - c.attempt_ms));
   }
-  ChainResult res;
+  ChainResult& res = wc.result;
+  res.fallback = res.null_list = res.error = false;
+  res.reason.clear();
   std::string err;
   bool success = false, retryable = false;
   int64_t retry_after = 0;
@@ -354,11 +360,10 @@ void AlohaChainer::on_response(http::Worker& w, WorkerCalls& wc, uint32_t slot, 
   if (r.ok && r.status >= 200 && r.status < 300 && decodes_to_null(r.body)) {
     success = true;
     res.null_list = true;
+    res.items.clear();
   } else if (r.ok && r.status >= 200 && r.status < 300) {
-    std::vector<std::optional<std::string>> items;
-    if (json::decode_string_list(r.body, &items, &err)) {
+    if (json::decode_string_list(r.body, &res.items, &err)) {
       success = true;
-      res.items = std::move(items);
     } else {
       err = "DecodeException: " + err;  // a FeignException: never retried
     }

@@ -250,10 +250,30 @@ bool parse(std::string_view in, Value* out, std::string* err) {
 
 bool decode_string_list(std::string_view in, std::vector<std::optional<std::string>>* out,
                         std::string* err) {
-  // Streams straight into *out (no DOM): this runs once per aloha response.
+  // Streams straight into *out (no DOM): this runs once per aloha response. The elements
+  // already in *out are reused (a string keeps its capacity), so a caller that decodes into
+  // the same vector every time allocates nothing in the steady state.
   Parser p;
   p.s = in;
-  out->clear();
+  size_t n = 0;
+  auto next_str = [&]() -> std::string* {
+    if (n < out->size()) {
+      auto& o = (*out)[n++];
+      if (!o) o.emplace();
+      o->clear();
+      return &*o;
+    }
+    out->emplace_back(std::string());
+    ++n;
+    return &*out->back();
+  };
+  auto next_null = [&] {
+    if (n < out->size()) (*out)[n++].reset();
+    else {
+      out->emplace_back(std::nullopt);
+      ++n;
+    }
+  };
   auto fail = [&](const std::string& m) {
     if (err) *err = p.err.empty() ? m : p.err;
     return false;
@@ -276,20 +296,19 @@ bool decode_string_list(std::string_view in, std::vector<std::optional<std::stri
       if (p.i >= in.size()) return fail("unexpected end at offset " + std::to_string(p.i));
       char c = in[p.i];
       if (c == '"') {
-        out->emplace_back(std::string());
-        if (!p.str(&**(out->end() - 1))) return fail("bad string");
+        if (!p.str(next_str())) return fail("bad string");
       } else if (c == 'n') {
         if (!p.lit("null")) return fail("bad literal");
-        out->emplace_back(std::nullopt);
+        next_null();
       } else if (c == 't' || c == 'f') {
         if (!p.lit(c == 't' ? "true" : "false")) return fail("bad literal");
-        out->emplace_back(std::string(c == 't' ? "true" : "false"));
+        next_str()->assign(c == 't' ? "true" : "false");
       } else if (c == '[' || c == '{') {
         return fail("cannot deserialize java.lang.String out of a nested array/object");
       } else {
         Value v;
         if (!p.num(&v)) return fail("bad number");
-        out->emplace_back(std::move(v.text));
+        *next_str() = std::move(v.text);
       }
       p.ws();
       if (p.i < in.size() && in[p.i] == ',') {
@@ -305,6 +324,7 @@ bool decode_string_list(std::string_view in, std::vector<std::optional<std::stri
   }
   p.ws();
   if (p.i != in.size()) return fail("trailing characters at offset " + std::to_string(p.i));
+  out->resize(n);
   return true;
 }
 

@@ -34,7 +34,9 @@ struct Value {
 bool parse(std::string_view in, Value* out, std::string* err);
 
 // Jackson's List<String> binding: array of scalars; numbers/booleans coerce to their text,
-// null stays null; objects/arrays inside are a mismatch. false with *err on failure.
+// null stays null; objects/arrays inside are a mismatch. false with *err on failure (then
+// *out holds a partial result). Elements already in *out are reused, so decoding into the
+// same vector again allocates nothing once its strings are large enough.
 bool decode_string_list(std::string_view in, std::vector<std::optional<std::string>>* out,
                         std::string* err);
 

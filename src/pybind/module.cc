@@ -139,6 +139,19 @@ py::object decode_string_list_py(py::bytes data) {
   return l;
 }
 
+// Decodes each document into the same vector, as the chainer does per worker; returns the
+// last result (a list) or ("error", message).
+py::object decode_string_list_reusing_py(const std::vector<std::string>& docs) {
+  std::vector<std::optional<std::string>> out;
+  std::string err;
+  bool ok = true;
+  for (const auto& d : docs) ok = json::decode_string_list(d, &out, &err);
+  if (!ok) return py::make_tuple("error", err);
+  py::list l;
+  for (auto& o : out) l.append(o ? py::object(py::bytes(*o)) : py::object(py::none()));
+  return l;
+}
+
 py::bytes string_array_py(const std::vector<std::optional<std::string>>& items) {
   return py::bytes(json::string_array(items));
 }
@@ -373,6 +386,7 @@ PYBIND11_MODULE(_native, m) {
   m.def("b3_inject", &b3_inject_py, py::arg("trace_id"), py::arg("span_id"), py::arg("parent") = py::none(),
         py::arg("sampled") = true, py::arg("debug") = false);
   m.def("decode_string_list", &decode_string_list_py);
+  m.def("decode_string_list_reusing", &decode_string_list_reusing_py);
   m.def("string_array", &string_array_py);
   m.def("json_quote", [](const std::string& s) { return py::bytes(json::quote(s)); });
   m.def("encode_span", &encode_spans_py, py::arg("v2"), py::arg("trace_id"), py::arg("span_id"),

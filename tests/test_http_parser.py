@@ -148,6 +148,16 @@ def test_decode_string_list(native):
 
 
 @settings(max_examples=300, deadline=None)
+@given(st.lists(st.lists(st.one_of(st.none(), st.text(max_size=40)), max_size=6), min_size=1, max_size=4))
+def test_decode_into_a_reused_vector(native, docs):
+    """The chainer decodes every aloha answer into the same per-worker vector: each decode
+    must give exactly its own document's list, whatever the previous ones held."""
+    encoded = [native.string_array(d) for d in docs]
+    got = native.decode_string_list_reusing(encoded)
+    assert [None if x is None else x.decode() for x in got] == docs[-1]
+
+
+@settings(max_examples=300, deadline=None)
 @given(st.lists(st.one_of(st.none(), st.text(max_size=20)), max_size=8))
 def test_json_roundtrip(native, items):
     enc = native.string_array(items)
