@@ -127,7 +127,7 @@ def _dispatch(c, req: dict, stop: threading.Event):
     if op == "get-endpoints":
         return {"published": c.endpoints(req.get("service")), "desired": c.endpoints(req.get("service"), False)}
     if op == "get-events":
-        return [list(e) for e in c.events[-int(req.get("n", 200)):]]
+        return [list(e) for e in list(c.events)[-int(req.get("n", 200)):]]
     if op == "scale":
         return c.scale(int(req["replicas"]))
     if op == "set-env":

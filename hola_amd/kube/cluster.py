@@ -33,6 +33,7 @@ Everything runs on one control-loop thread (`_loop`); the public methods take th
 """
 from __future__ import annotations
 
+import collections
 import copy
 import os
 import random
@@ -91,7 +92,8 @@ class Cluster:
         self.image = Image.from_dockerfile(dockerfile) if dockerfile else Image.from_dockerfile()
         self.image.materialize(self.state / "rootfs")
         self.lock = threading.RLock()
-        self.events: list[tuple[float, str, str, str]] = []
+        # the latest events (the full stream is in events.log)
+        self.events: collections.deque[tuple[float, str, str, str]] = collections.deque(maxlen=20000)
         self._events_f = open(self.state / "events.log", "a")
         self.t0 = time.monotonic()
         # pod network: 127.<a>.0.0/16 per cluster (127.<a>.0.1 = stand-in Services, pods from
@@ -136,15 +138,20 @@ class Cluster:
         self.endpoint_history: dict[str, list[tuple[float, list[str]]]] = {}
         self._last_rollout_step = 0.0
         self._completed_rev = 0
-        self.proxy: subprocess.Popen | None = None
+        self.proxies: list[subprocess.Popen] = []  # one hola_rrproxy per Service
         self.sink: subprocess.Popen | None = None
+        self._logs: list = []  # stderr files of the helper processes
         self.service_ports: dict[str, tuple[str, int]] = {}
         self._stop = threading.Event()
         self._thread: threading.Thread | None = None
 
     # ------------------------------------------------------------------ lifecycle
     def start(self) -> "Cluster":
-        self._start_services()
+        try:
+            self._start_services()
+        except BaseException:
+            self._stop_services()
+            raise
         with self.lock:
             self._new_revision(self.workload["spec"]["template"], initial=True)
         self._thread = threading.Thread(target=self._loop, name="kube-control", daemon=True)
@@ -170,15 +177,22 @@ class Cluster:
             if p.running:
                 p.proc.kill()
                 p.proc.wait()
-        for proc in (self.proxy, self.sink):
+        self._stop_services()
+        self.kubelet.shutdown()
+        self._events_f.close()
+
+    def _stop_services(self) -> None:
+        for proc in [*self.proxies, self.sink]:
             if proc and proc.poll() is None:
                 proc.send_signal(signal.SIGTERM)
                 try:
                     proc.wait(timeout=5)
                 except subprocess.TimeoutExpired:
                     proc.kill()
-        self.kubelet.shutdown()
-        self._events_f.close()
+                    proc.wait()
+        for f in self._logs:
+            f.close()
+        self._logs.clear()
 
     def __enter__(self) -> "Cluster":
         return self.start()
@@ -193,9 +207,9 @@ class Cluster:
         if self.want_zipkin:
             ip = f"{self.subnet}.1"
             pf = self.state / "zipkin.port"
+            self._logs.append(open(self.state / "zipkin.log", "ab"))
             self.sink = subprocess.Popen([str(native.binary("hola_zipkin_sink")), "--host", ip, "--port", "9411",
-                                          "--port-file", str(pf)], stdout=subprocess.DEVNULL,
-                                         stderr=open(self.state / "zipkin.log", "ab"))
+                                          "--port-file", str(pf)], stdout=subprocess.DEVNULL, stderr=self._logs[-1])
             self.service_ports["zipkin-query"] = (ip, self._wait_port(pf, self.sink))
         for name, svc in self.services.items():
             port = svc["spec"]["ports"][0]
@@ -208,9 +222,10 @@ class Cluster:
                    "--threads", str(self.proxy_threads), "--port-file", str(pf)]
             if self.proxy_cpus:
                 cmd += ["--cpu-list", self.proxy_cpus]
-            self.proxy = subprocess.Popen(cmd, stdout=subprocess.DEVNULL,
-                                          stderr=open(self.state / f"service-{name}.log", "ab"))
-            self.service_ports[name] = (self.service_host, self._wait_port(pf, self.proxy))
+            self._logs.append(open(self.state / f"service-{name}.log", "ab"))
+            proxy = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=self._logs[-1])
+            self.proxies.append(proxy)
+            self.service_ports[name] = (self.service_host, self._wait_port(pf, proxy))
             self.event(f"service/{name}", "Listening",
                        f"{svc['spec'].get('type', 'ClusterIP')} {self.service_host}:{self.service_ports[name][1]}")
 
