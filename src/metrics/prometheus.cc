@@ -135,6 +135,9 @@ std::string Prometheus::render(http::Server* server) const {
     o += "# TYPE hola_bytes_in_total counter\nhola_bytes_in_total " + std::to_string(bin) + "\n";
     o += "# TYPE hola_bytes_out_total counter\nhola_bytes_out_total " + std::to_string(bout) + "\n";
     o += "# TYPE hola_workers gauge\nhola_workers " + std::to_string(server->num_workers()) + "\n";
+    // 1 from the termination signal on (readiness failing, --shutdown-delay-ms), 2 while draining
+    o += "# TYPE hola_server_terminating gauge\nhola_server_terminating " +
+         std::to_string(server->draining() ? 2 : server->terminating() ? 1 : 0) + "\n";
     // Loop timers armed and not yet fired: tracks the calls in flight, never the call rate.
     size_t timers = 0;
     for (size_t i = 0; i < server->num_workers(); ++i) timers += server->worker(i).loop().pending_timers();

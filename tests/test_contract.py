@@ -584,6 +584,7 @@ def test_shutdown_delay_fails_readiness_but_keeps_serving(hola):
     assert ka.recv(10) == b""
     st, h, body = s.get("/api/health")  # a new connection is still accepted
     assert st == 503 and body == b"shutting down"
+    assert b"hola_server_terminating 1" in s.get("/metrics")[2]
     st, h, body = s.get("/api/hola")
     assert st == 200 and body == b"Hola de testhost"
     assert s.proc.poll() is None
