@@ -306,6 +306,20 @@ def test_oc_command_line(tmp_path, hola_bin):
         bodies = {http_get(host, int(port), "/api/hola")[2].decode() for _ in range(20)}
         assert all(b.startswith("Hey hola-2-") for b in bodies), bodies
         assert "Synced" in oc("get", "events").stdout
+        # `oc delete pod`: the replication controller replaces it
+        pods = json.loads(oc("get", "pods", "-o", "json").stdout)
+        victim = pods[0]["name"]
+        assert oc("delete", "pod", victim).stdout.strip() == f'pod "{victim}" deleted'
+        deadline = time.monotonic() + 30
+        while time.monotonic() < deadline:
+            now = json.loads(oc("get", "pods", "-o", "json").stdout)
+            if victim not in {p["name"] for p in now} and sum(p["ready"] for p in now) == 3:
+                break
+            time.sleep(0.2)
+        else:
+            raise AssertionError(now)
+        eps = oc("get", "endpoints").stdout.strip().split(",")
+        assert len(eps) == 3 and all(e.endswith(":8080") for e in eps)
     finally:
         oc("stop")
         ap.wait(timeout=30)
