@@ -296,7 +296,12 @@ def main() -> int:
             loadgen.close()
         server.stop()
     # The as-deployed replica, on the same CPUs once the headline replica is gone (rank 0).
-    deployed = _deployed_subrun(a, server_cpus, load_cpus) if local_rank == 0 and a.deployed_seconds > 0 else None
+    deployed = None
+    if local_rank == 0 and a.deployed_seconds > 0:
+        try:
+            deployed = _deployed_subrun(a, server_cpus, load_cpus)
+        except Exception as e:  # noqa: BLE001 - reported in the JSON; the other ranks must not hang
+            deployed = {"error": f"{type(e).__name__}: {e}"}
     if dist:
         both = [None] * world
         dist.all_gather_object(both, deployed)
