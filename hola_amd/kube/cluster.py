@@ -381,8 +381,9 @@ class Cluster:
         c = rc.template["spec"]["containers"][0]
         res = c.get("resources") or {}
         req = m.parse_cpu((res.get("requests") or {}).get("cpu", (res.get("limits") or {}).get("cpu")))
+        mem = m.parse_memory((res.get("limits") or {}).get("memory"))
         pod = Pod(name=name, owner=rc.name, revision=rc.revision, template=rc.template, ip=ip,
-                  dir=self.state / "pods" / name, labels=labels, cpu_request=req, created=now)
+                  dir=self.state / "pods" / name, labels=labels, cpu_request=req, mem_limit=mem, created=now)
         self.pods[name] = pod
         self.event(name, "Created", f"{rc.name}, ip {ip}, cpu request {req:g}")
         return pod

@@ -17,8 +17,10 @@ own address, the part of a network namespace the service contract needs). Around
 * termination: the pod leaves the Service endpoints at once, its preStop hook (if any) runs,
   then SIGTERM, and SIGKILL once `terminationGracePeriodSeconds` (30 s) have passed;
 * resources: under the static CPU manager policy a Guaranteed pod with integer CPUs gets an
-  exclusive cpuset (its process affinity); everything else runs on the shared pool. CPU and
-  memory limits are recorded but not enforced (that needs cgroup writes, i.e. root).
+  exclusive cpuset (its process affinity); everything else runs on the shared pool. A memory
+  limit is enforced the way the cgroup OOM killer would: resident memory above it gets the
+  container SIGKILLed (OOMKilled) and restarted. CPU quotas (CFS) are not enforced: that
+  needs cgroup writes, i.e. root.
 
 Delays (probe delay and period, restart back-off, ConfigMap sync) are multiplied by the
 cluster's `time_scale` so tests can run the same state machine faster; deadlines
@@ -41,6 +43,7 @@ PROBE_DEFAULTS = {"initialDelaySeconds": 0, "periodSeconds": 10, "timeoutSeconds
                   "failureThreshold": 3}
 BACKOFF_INITIAL_S, BACKOFF_MAX_S, BACKOFF_RESET_S = 10.0, 300.0, 600.0
 DEFAULT_GRACE_S = 30.0
+MEM_CHECK_S = 0.2
 
 
 def project_configmap(vol_dir: Path, data: dict[str, str], items: list[dict] | None = None) -> None:
@@ -97,6 +100,9 @@ class Pod:
     labels: dict = field(default_factory=dict)
     cpus: list[int] | None = None  # exclusive cpuset (static CPU manager) or None (shared pool)
     cpu_request: float = 0.0
+    mem_limit: int = 0  # bytes; 0 = none
+    rss_peak: int = 0
+    next_mem_check: float = 0.0
     created: float = field(default_factory=time.monotonic)
     scheduled: bool = False
     pending_reason: str = ""
@@ -151,6 +157,7 @@ class Pod:
         return {"name": self.name, "ip": self.ip, "status": self.status(), "ready": self.ready,
                 "restarts": self.restarts, "revision": self.revision, "owner": self.owner,
                 "cpus": self.cpus, "pid": self.proc.pid if self.running else None,
+                "rss_peak_mb": round(self.rss_peak / 2**20, 1),
                 "last_probe": self.last_probe, "pending_reason": self.pending_reason}
 
 
@@ -270,6 +277,7 @@ class Kubelet:
             return
         log.close()
         pod.started_at = now
+        pod.next_mem_check = now + 0.05  # a container over its limit from the start dies before probing
         pod.ready = False
         pod.probe_ok = pod.probe_fail = 0
         ps = self._probe_spec(pod)
@@ -304,7 +312,30 @@ class Kubelet:
             return
         if pod.last_exit is not None or not pod.running:
             return
+        if now >= pod.next_mem_check:
+            self._check_memory(pod, now)
+            if not pod.running:
+                return
         self._tick_probe(pod, now)
+
+    def _check_memory(self, pod: Pod, now: float) -> None:
+        """limits.memory, as the cgroup's OOM killer applies it: a container whose resident
+        memory exceeds the limit is SIGKILLed (reason OOMKilled) and restarted with back-off.
+        Sampled every 0.2 s from /proc (the executor cannot write cgroup limits)."""
+        pod.next_mem_check = now + MEM_CHECK_S
+        limit = pod.mem_limit
+        if limit <= 0:
+            return
+        try:
+            status = Path(f"/proc/{pod.proc.pid}/status").read_text()
+            rss = int(next(l for l in status.splitlines() if l.startswith("VmRSS:")).split()[1]) * 1024
+        except (OSError, StopIteration, ValueError):
+            return
+        pod.rss_peak = max(pod.rss_peak, rss)
+        if rss > limit:
+            pod.proc.kill()
+            pod.proc.wait()
+            self.cluster.event(pod.name, "OOMKilled", f"resident {rss >> 20} MiB > limit {limit >> 20} MiB")
 
     def _tick_probe(self, pod: Pod, now: float) -> None:
         ps = self._probe_spec(pod)

@@ -349,3 +349,20 @@ def test_prestop_hook_runs_before_sigterm(cluster):
     c.wait(lambda: c.rollout_status()["complete"] and c.rollout_status()["revision"] == 3, 30, "rollout")
     c.wait(lambda: len(c.get_pods()) == 1, 30, "old pod gone")
     assert any(e[2] == "Deleted" for e in c.events)
+
+
+def test_memory_limit_is_enforced_as_oomkilled(cluster):
+    """limits.memory below the server's resident memory: the container is killed as the cgroup
+    OOM killer would (OOMKilled), restarted, and never becomes an endpoint."""
+    c = cluster(replicas=1)
+    c.wait_ready(1, timeout=30)
+    c.patch({"spec": {"template": {"spec": {"containers": [
+        {"name": "hola", "resources": {"limits": {"memory": "1Mi", "cpu": "2"}, "requests": {"memory": "1Mi"}}}]}}}})
+    c.wait(lambda: sum(1 for e in c.events if e[2] == "OOMKilled") >= 2, 40, "two OOM kills")
+    new = [p for p in c.get_pods() if p["revision"] == 2]
+    assert new and new[0]["restarts"] >= 1
+    published = {e for _, eps in c.endpoint_history.get("hola", []) for e in eps}
+    assert new[0]["ip"] + ":8080" not in published  # never routed to
+    assert c.rollout_status()["revision"] == 2 and not c.rollout_status()["complete"]
+    # the old revision keeps serving: maxUnavailable 25 % of 1 rounds down to 0
+    assert len(c.endpoints()) == 1 and all(p["revision"] == 1 for p in c.get_pods() if p["ready"])
