@@ -11,6 +11,7 @@
     python -m hola_amd oc rollout status dc/hola
     python -m hola_amd oc apply -f translation-configmap.yaml            # ConfigMap edit
     python -m hola_amd oc delete pod hola-1-abcde
+    python -m hola_amd oc logs hola-1-abcde; python -m hola_amd oc describe pod hola-1-abcde
 
 `apply` serves a control socket in its state directory (`--state-dir`, default
 `$HOLA_CLUSTER_DIR` or /tmp/hola-cluster); `oc` talks to it.
@@ -147,6 +148,17 @@ def _dispatch(c, req: dict, stop: threading.Event):
         return c.kill_container(req["name"], getattr(signal, "SIG" + req.get("signal", "KILL").upper()))
     if op == "rollout-status":
         return c.rollout_status()
+    if op == "logs":
+        path = c.state / "pods" / req["name"] / "container.log"
+        if not path.exists():
+            raise KeyError(f"no pod {req['name']!r}")
+        lines = path.read_text(errors="replace").splitlines()
+        return lines[-int(req["tail"]):] if req.get("tail") else lines
+    if op == "describe":
+        pod = next((p for p in c.get_pods() if p["name"] == req["name"]), None)
+        if pod is None:
+            raise KeyError(f"no pod {req['name']!r}")
+        return {"pod": pod, "events": [list(e) for e in c.events if e[1] == req["name"]]}
     if op == "service-url":
         return c.service_url(req.get("service"))
     if op == "shutdown":
@@ -218,6 +230,12 @@ def oc_main(argv: list[str]) -> int:
     r.add_argument("what", choices=["status"])
     r.add_argument("target")
     r.add_argument("--timeout", type=float, default=600.0)
+    lg = sub.add_parser("logs", help="a pod's container log")
+    lg.add_argument("name")
+    lg.add_argument("--tail", type=int, default=0)
+    de = sub.add_parser("describe", help="a pod's state and its events")
+    de.add_argument("what", choices=["pod", "po"])
+    de.add_argument("name")
     sub.add_parser("url")
     sub.add_parser("stop")
     a = ap.parse_args(argv)
@@ -269,6 +287,15 @@ def oc_main(argv: list[str]) -> int:
                     print(f"timed out: {st}", file=sys.stderr)
                     return 1
                 time.sleep(0.5)
+        elif a.verb == "logs":
+            print("\n".join(_request(state, {"op": "logs", "name": a.name, "tail": a.tail})))
+        elif a.verb == "describe":
+            d = _request(state, {"op": "describe", "name": a.name})
+            for k, v in d["pod"].items():
+                print(f"{k + ':':<16}{v}")
+            print("Events:")
+            for t, _obj, reason, msg in d["events"]:
+                print(f"  {t:9.3f}  {reason:<16} {msg}")
         elif a.verb == "url":
             print(_request(state, {"op": "service-url"}))
         elif a.verb == "stop":

@@ -320,6 +320,10 @@ def test_oc_command_line(tmp_path, hola_bin):
             raise AssertionError(now)
         eps = oc("get", "endpoints").stdout.strip().split(",")
         assert len(eps) == 3 and all(e.endswith(":8080") for e in eps)
+        some = json.loads(oc("get", "pods", "-o", "json").stdout)[0]["name"]
+        assert "hola listening on" in oc("logs", some).stdout
+        desc = oc("describe", "pod", some).stdout
+        assert "ready:" in desc and "Started" in desc and "Ready" in desc
     finally:
         oc("stop")
         ap.wait(timeout=30)
