@@ -119,6 +119,9 @@ def parse_args():
                          "and manifests start it (deploy/Dockerfile ENTRYPOINT + deploy/openshift args and "
                          "env: no --busy-poll-us) on its server CPUs, with the same load generator, for about "
                          "this long; reported as deployed_*. 0 = skip. `value` is untouched")
+    ap.add_argument("--server-busy-poll", default="",
+                    help="the replica's own --busy-poll-us (N, auto or auto:N) when it should differ from "
+                         "the load generator's --busy-poll-us; default: the same N")
     ap.add_argument("--busy-poll-us", type=int, default=20,
                     help="spin this long in epoll before sleeping (server and load generator); "
                          "20 us measured best on the box (profiles/r11_box_session), 0 = off")
@@ -199,8 +202,9 @@ def main() -> int:
         args += ["--host", host]
     if a.epoll_lt:
         args += ["--epoll-lt"]
-    if a.busy_poll_us:
-        args += ["--busy-poll-us", str(a.busy_poll_us)]
+    server_bp = a.server_busy_poll or str(a.busy_poll_us)
+    if server_bp != "0":
+        args += ["--busy-poll-us", server_bp]
         if a.busy_poll_pause:
             args += ["--busy-poll-pause", str(a.busy_poll_pause)]
     if a.profile_dir:
@@ -374,7 +378,8 @@ def main() -> int:
                             "(hola_zipkin_sink) as the deployed ZIPKIN_SERVER_URL does" if plan[0]["sink_port"] else
                             "B3 tracing on without a collector: spans counted and dropped, as Brave "
                             "does with ZIPKIN_SERVER_URL unset")
-                         + (f", --busy-poll-us {a.busy_poll_us}" if a.busy_poll_us else "") + ")",
+                         + (f", --busy-poll-us {a.server_busy_poll or a.busy_poll_us}"
+                            if (a.server_busy_poll or str(a.busy_poll_us)) != "0" else "") + ")",
                 "global_batch": a.connections * world,
                 "seq_len": 1,
                 "parallelism": f"replicas{world}",
@@ -388,6 +393,7 @@ def main() -> int:
                 "server_threads_per_replica": s_threads,
                 "loadgen_threads_per_replica": len(load_cpus),
                 "busy_poll_us": a.busy_poll_us,
+                "server_busy_poll": a.server_busy_poll or str(a.busy_poll_us),
                 "busy_poll_pause": a.busy_poll_pause,
                 "epoll": "level" if a.epoll_lt else "edge",
                 "smt": smt,

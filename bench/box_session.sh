@@ -20,6 +20,8 @@
 #   tracing            headline without a collector, with the native Zipkin sink (default 1000-span
 #                      export budget, and unbounded), and with tracing off
 #   soak MINUTES [ARGS] mixed-load soak sampling RSS and FDs (ARGS go to bench/soak.py)
+#   busypoll [REPS]    the replica's busy-polling fixed / adaptive (auto) / off: saturated headline
+#                      and server CPU at light load (open-loop curve)
 #   uringchain         io_uring vs epoll on the chaining hop's four syscalls (bench/probes/uring_chain.cc)
 #   kube [ARGS]        BASELINE config 5: deploy/openshift applied by the local executor at real
 #                      timings (8 pods, probes, rollouts under 512-connection load, SIGKILL,
@@ -48,6 +50,27 @@ uringchain)
   g++ -O2 -std=c++20 -pthread bench/probes/uring_chain.cc -o /tmp/uring_chain &&
   timeout -k 10 200 /tmp/uring_chain --hop-cpu 8 --aloha-cpu 9 --client-cpus 10,11 --connections 64 \
     --rounds 6 --seconds 3 > "$OUT/uring_chain.jsonl" 2>> "$OUT/err.log"
+  ;;
+busypoll)
+  # the replica's busy-polling: fixed 20 us (the headline), adaptive (auto) and off, under the
+  # headline's saturation (interleaved benches), and the server CPU it costs at light load
+  # (open-loop latency curve)
+  REPS=${1:-3}
+  for rep in $(seq 1 "$REPS"); do
+    for v in fixed:20 auto:auto off:0; do
+      label=${v%%:*}; bp=${v#*:}
+      timeout -k 10 240 python bench.py --steps 12 --warmup 3 --c1-seconds 0 --deployed-seconds 0 \
+        --server-busy-poll "$bp" > "$OUT/${label}_${rep}.json" 2>> "$OUT/err.log" || exit 1
+      python3 -c "import json; d=json.load(open('$OUT/${label}_${rep}.json')); print('$label', $rep, d['value'], d['p50_ms'], d['p99_ms'], d['server_cpu_us_per_req'], d['host_load'][0]['siblings'])" \
+        >> "$OUT/summary.txt"
+    done
+  done
+  for v in fixed:20 auto:auto off:0; do
+    label=${v%%:*}; bp=${v#*:}
+    timeout -k 10 200 python bench/latency_curve.py --rates 50000,200000,1000000,2000000 --duration 4 \
+      --busy-poll-us 20 --server-busy-poll "$bp" --out "$OUT/curve_${label}.json" > "$OUT/curve_${label}.log" 2>&1 || exit 1
+  done
+  cat "$OUT/summary.txt"
   ;;
 kube)
   timeout -k 10 540 python -u bench/kube_rollout.py --out "$OUT/run" "$@" > "$OUT/kube.json" 2> "$OUT/kube.log"

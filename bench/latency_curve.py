@@ -24,13 +24,16 @@ ap.add_argument("--duration", type=float, default=8)
 ap.add_argument("--connections", type=int, default=64)
 ap.add_argument("--busy-poll-us", type=int, default=0, help="server and load generator spin in epoll this long")
 ap.add_argument("--spin-us", type=int, default=0, help="load generator spins when its next send is this close")
+ap.add_argument("--server-busy-poll", default="",
+                help="the server's --busy-poll-us (N, auto or auto:N); default: --busy-poll-us")
 ap.add_argument("--out", default="")
 a = ap.parse_args()
 
 cores = plan_node(1)[0]
 srv, lg = split_server_loadgen(cores, max(1, len(cores) // 2))
 rows = []
-server_args = ["--busy-poll-us", str(a.busy_poll_us)] if a.busy_poll_us else []
+server_bp = a.server_busy_poll or str(a.busy_poll_us)
+server_args = ["--busy-poll-us", server_bp] if server_bp != "0" else []
 with HolaProcess(args=server_args, env={"HOSTNAME": "h"}, threads=len(srv), cpu_list=format_cpu_list(srv),
                  log_level="warn") as s:
     def server_cpu():
@@ -56,6 +59,6 @@ with HolaProcess(args=server_args, env={"HOSTNAME": "h"}, threads=len(srv), cpu_
         rows.append(row)
         print(json.dumps(row), flush=True)
 out = {"cpu_map": {"server": format_cpu_list(srv), "loadgen": format_cpu_list(lg)}, "connections": a.connections,
-       "busy_poll_us": a.busy_poll_us, "spin_us": a.spin_us, "rows": rows}
+       "busy_poll_us": a.busy_poll_us, "server_busy_poll": server_bp, "spin_us": a.spin_us, "rows": rows}
 if a.out:
     Path(a.out).write_text(json.dumps(out, indent=1))

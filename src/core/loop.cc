@@ -4,6 +4,7 @@
 #include <sys/eventfd.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 
@@ -127,6 +128,29 @@ int EventLoop::next_timeout_ms() {
   return d > 1000000 ? 1000000 : int(d);
 }
 
+namespace {
+constexpr uint32_t kSpinWindow = 64;        // spins per decision
+constexpr uint32_t kSpinHitPercent = 75;    // keep spinning while >= this share finds work
+constexpr int64_t kSpinBackoffMinMs = 50, kSpinBackoffMaxMs = 1600;
+}  // namespace
+
+void EventLoop::note_spin(bool hit) {
+  if (hit) ++spin_hits_;
+  else ++spin_misses_;
+  if (spin_hits_ + spin_misses_ < kSpinWindow) return;
+  spin_hits_total_.fetch_add(spin_hits_, std::memory_order_relaxed);
+  spin_misses_total_.fetch_add(spin_misses_, std::memory_order_relaxed);
+  if (spin_hits_ * 100 < kSpinHitPercent * (spin_hits_ + spin_misses_)) {
+    // mostly waiting in vain: stop spinning for a while, longer each time it repeats
+    spin_backoff_ms_ = spin_backoff_ms_ ? std::min(kSpinBackoffMaxMs, spin_backoff_ms_ * 2) : kSpinBackoffMinMs;
+    spin_off_until_ms_ = now_ms_ + spin_backoff_ms_;
+    spin_offs_.fetch_add(1, std::memory_order_relaxed);
+  } else {
+    spin_backoff_ms_ = 0;
+  }
+  spin_hits_ = spin_misses_ = 0;
+}
+
 void EventLoop::run() {
   constexpr int kMaxEvents = 256;
   epoll_event evs[kMaxEvents];
@@ -135,16 +159,19 @@ void EventLoop::run() {
     if (tick_) tick_();
     int n = 0;
     int64_t t = 0;  // mono_ns() at (or just before) the moment events were found
-    if (busy_poll_ns_ > 0) {
+    if (busy_poll_ns_ > 0 && (!busy_auto_ || now_ms_ >= spin_off_until_ms_)) {
       t = mono_ns();
       const int64_t until = t + busy_poll_ns_;
+      bool spun = false;  // the first poll came back empty: this pass is a real spin
       for (;;) {
         n = epoll_wait(epfd_, evs, kMaxEvents, 0);
         if (n != 0 || stop_.load(std::memory_order_relaxed)) break;
+        spun = true;
         t = mono_ns();
         if (t >= until) break;
         for (int i = 0; i < busy_poll_pause_; ++i) __builtin_ia32_pause();
       }
+      if (busy_auto_ && spun) note_spin(n > 0);
     }
     if (n == 0) {
       n = epoll_wait(epfd_, evs, kMaxEvents, next_timeout_ms());

@@ -65,6 +65,16 @@ class EventLoop {
   // While busy-polling, execute this many PAUSE instructions after each empty poll, so a
   // spinning thread leaves issue slots to its SMT sibling. 0 = poll back to back.
   void set_busy_poll_pause(int n) { busy_poll_pause_ = n; }
+  // Adaptive busy-polling: the spin stays on while it mostly finds work before its budget
+  // runs out (a saturated loop, where it saves the sleep/wake-up per request), and is
+  // switched off for a growing interval (50 ms .. 1.6 s) while it mostly waits in vain (light
+  // load, where it would only burn CPU). Each interval ends with a short re-probe.
+  void set_busy_poll_auto(bool on) { busy_auto_ = on; }
+  // Adaptive spin statistics (loop thread; tests and metrics): spins that found work, spins
+  // that ran out, and how many times spinning was switched off.
+  uint64_t spin_hits() const { return spin_hits_total_.load(std::memory_order_relaxed); }
+  uint64_t spin_misses() const { return spin_misses_total_.load(std::memory_order_relaxed); }
+  uint64_t spin_offs() const { return spin_offs_.load(std::memory_order_relaxed); }
 
  private:
   struct WakeHandler : Handler {
@@ -98,6 +108,11 @@ class EventLoop {
   std::function<void()> tick_, on_exit_;
   int64_t busy_poll_ns_ = 0;
   int busy_poll_pause_ = 0;
+  bool busy_auto_ = false;
+  uint32_t spin_hits_ = 0, spin_misses_ = 0;  // current measurement window
+  int64_t spin_off_until_ms_ = 0, spin_backoff_ms_ = 0;
+  std::atomic<uint64_t> spin_hits_total_{0}, spin_misses_total_{0}, spin_offs_{0};
+  void note_spin(bool hit);
 };
 
 }  // namespace hola

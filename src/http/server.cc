@@ -358,6 +358,7 @@ Worker::Worker(Server* s, int index) : server_(s), index_(index) {
   loop_.set_tick([this] { tick(); });
   loop_.set_busy_poll_us(s->options().busy_poll_us);
   loop_.set_busy_poll_pause(s->options().busy_poll_pause);
+  loop_.set_busy_poll_auto(s->options().busy_poll_auto);
 }
 
 Worker::~Worker() {

@@ -150,6 +150,7 @@ struct ServerOptions {
   int backlog = 4096;
   size_t read_chunk = 64 * 1024;
   int busy_poll_us = 0;  // see EventLoop::set_busy_poll_us
+  bool busy_poll_auto = false;  // adaptive spinning, see EventLoop::set_busy_poll_auto
   int busy_poll_pause = 0;  // see EventLoop::set_busy_poll_pause
   bool edge_triggered = true;  // EPOLLET on connection sockets (--epoll-lt turns it off)
   bool profile = false;  // per-stage latency histograms (SURVEY.md §5.1 --profile)

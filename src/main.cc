@@ -80,7 +80,9 @@ void usage() {
           "                           rolling update outlasts endpoint propagation). A second signal\n"
           "                           ends the delay early\n"
           "  --port-file PATH         write the bound port here once listening\n"
-          "  --busy-poll-us N         spin up to N us in epoll before sleeping (default 0)\n"
+          "  --busy-poll-us N|auto[:N] spin up to N us in epoll before sleeping (default 0); auto = adaptive:\n"
+          "                           spin (20 us, or N) while spinning mostly finds work (saturation),\n"
+          "                           back off while it mostly waits in vain (light load)\n"
           "  --busy-poll-pause N      PAUSE instructions between empty polls (SMT-friendly spin)\n"
           "  --idle-timeout-ms N      close connections with nothing read or written this long\n"
           "                           (default 60000, 0 = never)\n"
@@ -97,6 +99,8 @@ void usage() {
           "  --log-level L            debug|info|warn|error|off (default info)\n"
           "  --no-metrics             disable the /metrics endpoint\n");
 }
+
+constexpr int kAutoBusyPollUs = 20;  // spin budget of --busy-poll-us auto
 
 bool need(int i, int argc, const char* flag) {
   if (i + 1 >= argc) {
@@ -209,7 +213,11 @@ int main(int argc, char** argv) {
     else if (a == "--drain-ms") drain_ms = atoi(val("--drain-ms").c_str());
     else if (a == "--shutdown-delay-ms") shutdown_delay_ms = std::max(0, atoi(val("--shutdown-delay-ms").c_str()));
     else if (a == "--port-file") port_file = val("--port-file");
-    else if (a == "--busy-poll-us") so.busy_poll_us = atoi(val("--busy-poll-us").c_str());
+    else if (a == "--busy-poll-us") {
+      const std::string v = val("--busy-poll-us");
+      so.busy_poll_auto = v == "auto" || v.rfind("auto:", 0) == 0;
+      so.busy_poll_us = so.busy_poll_auto ? (v.size() > 5 ? atoi(v.c_str() + 5) : kAutoBusyPollUs) : atoi(v.c_str());
+    }
     else if (a == "--busy-poll-pause") so.busy_poll_pause = atoi(val("--busy-poll-pause").c_str());
     else if (a == "--profile") so.profile = true;
     else if (a == "--no-steer") so.steer_l3 = false;

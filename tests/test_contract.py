@@ -644,3 +644,29 @@ def test_drain_closes_busy_keepalive_connections_between_responses(hola):
         t.join(timeout=10)
     assert s.proc.wait(timeout=10) == 0
     assert len(results) == 4 and all(r[0] == "ok" and r[1] > 0 and r[2] == b"" for r in results), results
+
+
+def _metric_value(s, name: str) -> float:
+    for line in s.get("/metrics")[2].decode().splitlines():
+        if line.startswith(name + " "):
+            return float(line.split()[1])
+    raise AssertionError(f"{name} missing")
+
+
+def test_adaptive_busy_poll_backs_off_under_light_load(hola):
+    """`--busy-poll-us auto`: spinning that mostly waits in vain (requests 10 ms apart) is
+    switched off, so a lightly loaded replica does not burn its CPU; an idle one sleeps."""
+    s = hola(args=["--busy-poll-us", "auto"], threads=1)
+    for _ in range(150):
+        assert s.get("/api/hola")[0] == 200
+        time.sleep(0.01)
+    assert _metric_value(s, "hola_busy_poll_backoffs_total") >= 1
+    body = s.get("/metrics")[2].decode()
+    hits = float(next(l for l in body.splitlines() if 'result="hit"' in l).split()[1])
+    misses = float(next(l for l in body.splitlines() if 'result="miss"' in l).split()[1])
+    assert misses > hits
+    # idle: well under a tenth of a CPU
+    cpu = lambda: sum(int(x) for x in open(f"/proc/{s.proc.pid}/stat").read().rsplit(")", 1)[1].split()[11:13])  # noqa: E731
+    c0 = cpu()
+    time.sleep(1.0)
+    assert (cpu() - c0) / os.sysconf("SC_CLK_TCK") < 0.1
