@@ -74,6 +74,9 @@ def parse_args():
                          "Dockerfile:6): start a native discard Zipkin collector (hola_zipkin_sink) and "
                          "point every replica at it; the JSON gains a `tracing` block with spans "
                          "recorded/reported/dropped per second and the reporter thread's CPU")
+    ap.add_argument("--zipkin-url", default="",
+                    help="the replicas' collector URL as given (e.g. the image's http://zipkin-query:9411, "
+                         "which does not resolve on a bare host); --zipkin-sink starts a real one instead")
     ap.add_argument("--trace-queue", type=int, default=-1,
                     help="replicas' --trace-queue (spans exported per flush interval; -1 = server "
                          "default 1000, Brave 3's collector queue; 0 = bounded only by the rings)")
@@ -196,6 +199,8 @@ def main() -> int:
     args = ["--no-tracing"] if a.no_tracing else []
     if plan[0]["sink_port"]:
         args += ["--zipkin-url", f"http://127.0.0.1:{plan[0]['sink_port']}/"]
+    elif a.zipkin_url and not a.no_tracing:
+        args += ["--zipkin-url", a.zipkin_url]
     if a.trace_queue >= 0:
         args += ["--trace-queue", str(a.trace_queue)]
     if host != "127.0.0.1":
@@ -376,6 +381,7 @@ def main() -> int:
                          + ("tracing off" if a.no_tracing else
                             "B3 tracing on, spans posted to a native discard Zipkin collector "
                             "(hola_zipkin_sink) as the deployed ZIPKIN_SERVER_URL does" if plan[0]["sink_port"] else
+                            f"B3 tracing on, collector URL {a.zipkin_url}" if a.zipkin_url else
                             "B3 tracing on without a collector: spans counted and dropped, as Brave "
                             "does with ZIPKIN_SERVER_URL unset")
                          + (f", --busy-poll-us {a.server_busy_poll or a.busy_poll_us}"
@@ -454,6 +460,7 @@ def _tracing_block(a, gathered: list[dict], t: float, sink_port: int) -> dict:
             spans[k] = spans.get(k, 0) + v
     per_s = {k: round(v / t, 1) for k, v in sorted(spans.items())} if t > 0 else {}
     out = {"mode": "collector: native discard sink (hola_zipkin_sink)" if sink_port else
+           f"collector URL {a.zipkin_url} (as given)" if a.zipkin_url else
            "no collector (ZIPKIN_SERVER_URL unset): spans counted and dropped at the source",
            "trace_queue_per_flush": a.trace_queue if a.trace_queue >= 0 else 1000,
            "spans_per_s": per_s,
