@@ -120,7 +120,7 @@ def parse_args():
     ap.add_argument("--deployed-seconds", type=float, default=3.0,
                     help="after the timed region, rank 0 also drives a replica started exactly as the image "
                          "and manifests start it (deploy/Dockerfile ENTRYPOINT + deploy/openshift args and "
-                         "env: no --busy-poll-us) on its server CPUs, with the same load generator, for about "
+                         "env) on its server CPUs, with the same load generator, for about "
                          "this long; reported as deployed_*. 0 = skip. `value` is untouched")
     ap.add_argument("--server-busy-poll", default="",
                     help="the replica's own --busy-poll-us (N, auto or auto:N) when it should differ from "

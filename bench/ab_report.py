@@ -29,7 +29,8 @@ _T95 = {1: 12.706, 2: 4.303, 3: 3.182, 4: 2.776, 5: 2.571, 6: 2.447, 7: 2.365, 8
 def t95(df: int) -> float:
     if df in _T95:
         return _T95[df]
-    return next((v for k, v in sorted(_T95.items()) if k >= df), 1.96)
+    # between table rows take the smaller df's (larger, conservative) quantile
+    return next(v for k, v in sorted(_T95.items(), reverse=True) if k <= df)
 
 
 def ci(diffs: list[float]) -> tuple[float, float, float]:
@@ -51,7 +52,8 @@ def load(d: Path, label: str) -> dict[int, dict]:
 
 
 def sib(r: dict) -> float:
-    return max(h.get("siblings", 0.0) for h in r.get("host_load", [{}]))
+    # None in SMT-pair layouts: both threads of each core are ours, so no other tenant shares them
+    return max((h.get("siblings") or 0.0) for h in r.get("host_load", [{}]))
 
 
 def adjusted(rows: list[dict]) -> dict | None:
@@ -65,17 +67,20 @@ def adjusted(rows: list[dict]) -> dict | None:
     if len(ys) < 5:
         return None
     X, y = np.array(xs), np.array(ys)
+    if np.ptp(X[:, 2]) == 0.0:  # no sibling load varies (e.g. SMT-pair layouts): plain two-group fit
+        X = X[:, :2]
     coef, *_ = np.linalg.lstsq(X, y, rcond=None)
     resid = y - X @ coef
-    dof = len(y) - 3
+    dof = len(y) - X.shape[1]
     s2 = float(resid @ resid) / dof
     cov = s2 * np.linalg.inv(X.T @ X)
     se = math.sqrt(cov[1, 1])
-    base = coef[0] + coef[2] * statistics.fmean([r["sib_base"] for r in rows])
+    slope = float(coef[2]) if X.shape[1] == 3 else 0.0
+    base = coef[0] + slope * statistics.fmean([r["sib_base"] for r in rows])
     h = t95(dof) * se
     return {"delta_us": round(float(coef[1]), 4), "delta_pct": round(100 * float(coef[1]) / base, 2),
             "ci95_pct": [round(100 * float(coef[1] - h) / base, 2), round(100 * float(coef[1] + h) / base, 2)],
-            "us_per_sibling_pct": round(float(coef[2]) / 100, 4), "runs": len(y)}
+            "us_per_sibling_pct": round(slope / 100, 4), "runs": len(y)}
 
 
 def main() -> int:
@@ -120,7 +125,7 @@ def main() -> int:
         res["server_us_per_req_adjusted"] = adj
         print(f"  adjusted for sibling load (all {len(rows)} pairs): candidate {adj['delta_pct']:+.2f} % server us/req "
               f"(95 % CI {adj['ci95_pct'][0]:+.2f} .. {adj['ci95_pct'][1]:+.2f}); "
-              f"+{adj['us_per_sibling_pct']:.3f} us per sibling-load percent")
+              f"{adj['us_per_sibling_pct']:+.3f} us per sibling-load percent")
     if a.json:
         Path(a.json).write_text(json.dumps(res, indent=1) + "\n")
     return 0

@@ -38,9 +38,9 @@ def test_bench_json_contract_on_host():
     assert out["body_checked"] == out["requests"] and out["body_mismatch"] == 0
     # BASELINE config 2 ran after the timed region, and placement was reported
     assert out["c1_errors"] == 0 and out["c1_rps"] > 10000 and out["c1_body_checked"] == out["c1_requests"]
-    # ... and the replica exactly as the image and manifests start it (no busy-polling)
+    # ... and the replica exactly as the image and manifests start it (adaptive busy-polling)
     assert out["deployed_errors"] == 0 and out["deployed_non2xx"] == 0 and out["deployed_rps"] > 10000
-    assert "--shutdown-delay-ms 5000" in out["deployed_args"] and "--busy-poll" not in out["deployed_args"]
+    assert "--shutdown-delay-ms 5000" in out["deployed_args"] and "--busy-poll-us auto" in out["deployed_args"]
     assert out["config"]["smt"] in ("off", "split", "pair") and "GPU slot" in out["config"]["layout_note"]
     assert abs(sum(out["locality"]["fraction"].values()) - 1.0) < 1e-3
 
