@@ -123,12 +123,17 @@ def parse_args():
                          "env) on its server CPUs, with the same load generator, for about "
                          "this long; reported as deployed_*. 0 = skip. `value` is untouched")
     ap.add_argument("--server-busy-poll", default="",
-                    help="the replica's own --busy-poll-us (N, auto or auto:N) when it should differ from "
-                         "the load generator's --busy-poll-us; default: the same N")
+                    help="the replica's own --busy-poll-us (N, auto or auto:N); default: adaptive with the "
+                         "load generator's N (`auto`, as the manifests start the replica), 0 when that is 0")
     ap.add_argument("--busy-poll-us", type=int, default=20,
-                    help="spin this long in epoll before sleeping (server and load generator); "
-                         "20 us measured best on the box (profiles/r11_box_session), 0 = off")
-    return ap.parse_args()
+                    help="spin this long in epoll before sleeping (the load generator; the replica spins "
+                         "adaptively up to this long); 20 us measured best on the box "
+                         "(profiles/r11_box_session), 0 = off")
+    a = ap.parse_args()
+    if not a.server_busy_poll:
+        # the manifests' setting: at saturation equal to a fixed spin (profiles/round3/10_auto)
+        a.server_busy_poll = ("auto" if a.busy_poll_us == 20 else f"auto:{a.busy_poll_us}") if a.busy_poll_us else "0"
+    return a
 
 
 def main() -> int:
@@ -207,7 +212,7 @@ def main() -> int:
         args += ["--host", host]
     if a.epoll_lt:
         args += ["--epoll-lt"]
-    server_bp = a.server_busy_poll or str(a.busy_poll_us)
+    server_bp = a.server_busy_poll
     if server_bp != "0":
         args += ["--busy-poll-us", server_bp]
         if a.busy_poll_pause:
@@ -384,8 +389,7 @@ def main() -> int:
                             f"B3 tracing on, collector URL {a.zipkin_url}" if a.zipkin_url else
                             "B3 tracing on without a collector: spans counted and dropped, as Brave "
                             "does with ZIPKIN_SERVER_URL unset")
-                         + (f", --busy-poll-us {a.server_busy_poll or a.busy_poll_us}"
-                            if (a.server_busy_poll or str(a.busy_poll_us)) != "0" else "") + ")",
+                         + (f", --busy-poll-us {a.server_busy_poll}" if a.server_busy_poll != "0" else "") + ")",
                 "global_batch": a.connections * world,
                 "seq_len": 1,
                 "parallelism": f"replicas{world}",
@@ -399,7 +403,7 @@ def main() -> int:
                 "server_threads_per_replica": s_threads,
                 "loadgen_threads_per_replica": len(load_cpus),
                 "busy_poll_us": a.busy_poll_us,
-                "server_busy_poll": a.server_busy_poll or str(a.busy_poll_us),
+                "server_busy_poll": a.server_busy_poll,
                 "busy_poll_pause": a.busy_poll_pause,
                 "epoll": "level" if a.epoll_lt else "edge",
                 "smt": smt,
