@@ -36,6 +36,7 @@ Logger& Logger::instance() {
 struct Logger::Ring {
   static constexpr size_t kSize = 128 * 1024;  // power of two
   alignas(64) std::atomic<uint64_t> head{0};
+  uint64_t seen_tail = 0;  // producer's last look at tail: it re-reads tail only when this looks full
   alignas(64) std::atomic<uint64_t> tail{0};
   std::atomic<bool> orphan{false};  // its thread has exited: free for the next new thread
   char buf[kSize];
@@ -64,7 +65,9 @@ thread_local ThreadRing tls_ring;
 // Bounded waits against the system clock: libstdc++ implements steady-clock waits with
 // pthread_cond_clockwait, which the toolchain's ThreadSanitizer does not intercept.
 constexpr auto kPoll = std::chrono::milliseconds(1);
-constexpr int kIdlePolls = 10;  // empty polls in a row before the writer sleeps until woken
+constexpr int kIdlePolls = 10;  // empty polls in a row before the writer sleeps longer
+// The writer's longest sleep, and so the longest a line can wait when no producer wakes it.
+constexpr auto kIdleSleep = std::chrono::milliseconds(50);
 }  // namespace
 
 Logger::Logger() : th_([this] { run(); }) { pthread_setname_np(th_.native_handle(), "hola-log"); }
@@ -116,11 +119,7 @@ void Logger::raw(const char* fmt, ...) {
 
 void Logger::raw_line(std::string_view line) {
   if (level() == LogLevel::kOff) return;
-  char buf[2048];
-  const size_t n = std::min(line.size(), sizeof buf - 1);
-  memcpy(buf, line.data(), n);
-  buf[n] = '\n';
-  enqueue(buf, n + 1);
+  enqueue(line.data(), std::min(line.size(), size_t(2047)), true);
 }
 
 Logger::Ring* Logger::ring_for_this_thread() {
@@ -143,20 +142,32 @@ Logger::Ring* Logger::ring_for_this_thread() {
   return tls_ring.r = r;
 }
 
-void Logger::enqueue(const char* line, size_t n) {
+void Logger::enqueue(const char* line, size_t n, bool newline) {
   Ring* r = ring_for_this_thread();
-  const uint32_t len = uint32_t(n);
-  const uint64_t h = r ? r->head.load(std::memory_order_relaxed) : 0;
-  if (!r || Ring::kSize - (h - r->tail.load(std::memory_order_acquire)) < sizeof len + n) {
+  const uint32_t len = uint32_t(n + newline);
+  const uint64_t need = sizeof len + len;
+  if (!r) {
     dropped_.fetch_add(1, std::memory_order_relaxed);
     return;
   }
+  const uint64_t h = r->head.load(std::memory_order_relaxed);
+  if (Ring::kSize - (h - r->seen_tail) < need) {
+    // only now touch the writer's cache line
+    r->seen_tail = r->tail.load(std::memory_order_acquire);
+    if (Ring::kSize - (h - r->seen_tail) < need) {
+      dropped_.fetch_add(1, std::memory_order_relaxed);
+      return;
+    }
+  }
   r->put(h, &len, sizeof len);
   r->put(h + sizeof len, line, n);
-  // seq_cst pairs with the writer's store of sleeping_ before its last look at the rings:
-  // either it sees this line, or this thread sees it asleep and wakes it.
-  r->head.store(h + sizeof len + n, std::memory_order_seq_cst);
-  if (sleeping_.load(std::memory_order_seq_cst)) wake();
+  if (newline) r->put(h + sizeof len + n, "\n", 1);
+  // A release store, not a full fence: on x86 a seq_cst store would wait here for every
+  // store into the ring (lines the writer last read, so each is a cross-core miss) to
+  // complete. The price is that this thread may miss the writer falling asleep; the writer
+  // therefore never sleeps longer than kIdleSleep.
+  r->head.store(h + need, std::memory_order_release);
+  if (sleeping_.load(std::memory_order_relaxed)) wake();
 }
 
 void Logger::wake() {
@@ -171,7 +182,7 @@ bool Logger::rings_empty() const {
   const int n = nrings_.load(std::memory_order_acquire);
   for (int i = 0; i < n; ++i) {
     const Ring* r = rings_[i].load(std::memory_order_acquire);
-    if (r->head.load(std::memory_order_seq_cst) != r->tail.load(std::memory_order_relaxed)) return false;
+    if (r->head.load(std::memory_order_acquire) != r->tail.load(std::memory_order_relaxed)) return false;
   }
   return true;
 }
@@ -238,14 +249,16 @@ void Logger::run() {
       cv_.wait_until(g, std::chrono::system_clock::now() + kPoll, woken);
       continue;
     }
-    sleeping_.store(true, std::memory_order_seq_cst);
+    // Idle: sleep until a producer sees sleeping_ (best effort, see enqueue) or kIdleSleep
+    // passes. idle stays >= kIdlePolls, so an empty look afterwards sleeps long again.
+    sleeping_.store(true, std::memory_order_relaxed);
     if (!rings_empty()) {
       sleeping_.store(false, std::memory_order_relaxed);
       continue;
     }
-    cv_.wait(g, [&] { return !sleeping_.load(std::memory_order_relaxed) || woken(); });
+    cv_.wait_until(g, std::chrono::system_clock::now() + kIdleSleep,
+                   [&] { return !sleeping_.load(std::memory_order_relaxed) || woken(); });
     sleeping_.store(false, std::memory_order_relaxed);
-    idle = 0;
   }
   std::lock_guard<std::mutex> g(mu_);
   flush_done_ = flush_req_;

@@ -49,7 +49,7 @@ class Logger {
  private:
   Logger();
   void run();
-  void enqueue(const char* line, size_t n);
+  void enqueue(const char* line, size_t n, bool newline = false);  // newline: append '\n'
   Ring* ring_for_this_thread();
   size_t drain(std::string* out);  // appends every ring's lines; returns how many
   bool rings_empty() const;

@@ -339,14 +339,22 @@ std::pair<size_t, size_t> span_ring(size_t capacity, size_t pushes) {
 // Logs `lines` raw lines "<tag> <thread> <i>" from each of `threads` threads (each a new
 // thread, so rings of exited threads are reused across calls), then flushes; returns the
 // lines dropped meanwhile (ring full).
-uint64_t log_stress(int threads, int lines, const std::string& tag) {
+uint64_t log_stress(int threads, int lines, const std::string& tag, bool prebuilt) {
   py::gil_scoped_release nogil;
   Logger& l = Logger::instance();
   const uint64_t d0 = l.dropped();
   std::vector<std::thread> ts;
   for (int t = 0; t < threads; ++t)
-    ts.emplace_back([&l, t, lines, &tag] {
-      for (int i = 0; i < lines; ++i) l.raw("%s %d %d", tag.c_str(), t, i);
+    ts.emplace_back([&l, t, lines, &tag, prebuilt] {
+      std::string line;
+      for (int i = 0; i < lines; ++i) {
+        if (!prebuilt) {
+          l.raw("%s %d %d", tag.c_str(), t, i);
+          continue;
+        }
+        line = tag + " " + std::to_string(t) + " " + std::to_string(i);  // the Feign BASIC path
+        l.raw_line(line);
+      }
     });
   for (auto& t : ts) t.join();
   l.flush();
@@ -419,7 +427,10 @@ PYBIND11_MODULE(_native, m) {
   }, py::arg("attempt"), py::arg("policy") = "default");
   m.def("loop_timer_order", &loop_timer_order, py::arg("delays"), py::arg("cancel") = std::vector<int>{});
   m.def("span_ring", &span_ring);
-  m.def("log_stress", &log_stress, py::arg("threads"), py::arg("lines"), py::arg("tag") = "stress");
+  m.def("log_stress", &log_stress, py::arg("threads"), py::arg("lines"), py::arg("tag") = "stress",
+        py::arg("prebuilt") = false);
+  m.def("log_raw_line", [](const std::string& s) { Logger::instance().raw_line(s); },
+        "one raw line, no flush: it reaches stderr when the writer next drains");
   m.def("hystrix_stress", &hystrix_stress, py::arg("threads"), py::arg("iters"), py::arg("pool") = 10,
         py::arg("fail_every") = 0, py::arg("volume") = 20);
   py::class_<PyCommand>(m, "HystrixCommand")

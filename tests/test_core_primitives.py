@@ -69,8 +69,8 @@ def test_logger_per_thread_rings_keep_every_line_in_order(native, capfd):
     """Lines from many threads at once all reach stderr, each thread's in its own order, and
     flush() returns only after they are written. Threads exit between the two calls, so the
     second reuses their rings."""
-    for tag in ("first", "second"):
-        dropped = native.log_stress(8, 2000, tag)
+    for tag, prebuilt in (("first", False), ("second", False), ("third", True)):
+        dropped = native.log_stress(8, 2000, tag, prebuilt)
         err = capfd.readouterr().err
         assert dropped == 0
         seen = {}
@@ -81,6 +81,26 @@ def test_logger_per_thread_rings_keep_every_line_in_order(native, capfd):
                 assert i == seen.get(t, -1) + 1, (t, i)
                 seen[t] = i
         assert seen == {t: 1999 for t in range(8)}
+
+
+def test_logger_line_reaches_stderr_without_flush_while_the_writer_idles(native, capfd):
+    """Producers publish with a release store and may miss the writer falling asleep, so the
+    idle writer wakes on its own within its longest sleep (50 ms): a line logged into a quiet
+    logger shows up without flush(), and a long line is cut at 2047 bytes plus its newline."""
+    import time
+
+    for i in range(3):
+        time.sleep(0.2)  # > 10 empty 1 ms polls: the writer is in its long sleep
+        native.log_raw_line(f"idle-line {i} " + "x" * (3000 if i == 2 else 0))
+        t0, err = time.monotonic(), ""
+        while f"idle-line {i}" not in err and time.monotonic() - t0 < 2.0:
+            time.sleep(0.005)
+            err += capfd.readouterr().err
+        assert f"idle-line {i}" in err
+        assert time.monotonic() - t0 < 0.5
+        if i == 2:
+            line = next(l for l in err.splitlines() if l.startswith("idle-line 2"))
+            assert len(line) == 2047
 
 
 def test_logger_drops_and_counts_when_a_ring_overflows(native, capfd):
