@@ -165,6 +165,7 @@ struct ClientPool::PConn final : EventLoop::Handler {
   ClientPool* pool = nullptr;
   int fd = -1;
   bool connecting = false, dead = false, dirty = false;
+  bool draining = false;  // a call on it was abandoned: no new calls; closes once none waits
   std::string out, in;
   size_t off = 0;
   std::deque<Pending> q;
@@ -656,9 +657,11 @@ void ClientPool::destroy(Conn* c) {
 
 void ClientPool::cancel(uint64_t id) {
   if (auto pt = pactive_.find(id); pt != pactive_.end()) {
-    // Abandoned (timed out) on a shared connection: its answer may never come, and every call
-    // queued behind it would wait for it. The socket is given up, as on the plain path, and
-    // the other calls waiting on it are re-sent on fresh connections.
+    // Abandoned (its Hystrix timeout fired) on a shared connection. Aloha already has the
+    // calls queued behind it, so re-sending them would duplicate work exactly when aloha is
+    // slow, and spend their transport retries. Instead the connection takes no new calls; the
+    // calls already on it complete as their answers arrive (this one's is read and dropped)
+    // or at their own deadlines, and it closes once no call on it is waited for.
     PConn* c = pt->second.conn;
     for (auto& p : c->q)
       if (p.id == id) {
@@ -666,7 +669,10 @@ void ClientPool::cancel(uint64_t id) {
         p.cb = nullptr;
       }
     pactive_.erase(pt);
-    pfail(c, "SocketException: connection abandoned");
+    c->draining = true;
+    if (std::all_of(c->q.begin(), c->q.end(), [](const PConn::Pending& p) { return p.abandoned; })) pdestroy(c);
+    if (!read_fifo_.q.empty()) pop_finished(read_fifo_);
+    if (!connect_fifo_.q.empty()) pop_finished(connect_fifo_);
     return;
   }
   auto it = active_.find(id);
@@ -705,13 +711,13 @@ bool ClientPool::get_pipelined(uint64_t id, std::string& req, Callback& cb) {
   const size_t depth = size_t(pipeline_);
   PConn* c = nullptr;
   for (PConn* p : dirty_)
-    if (!p->dead && p->q.size() < depth) {
+    if (!p->dead && !p->draining && p->q.size() < depth) {
       c = p;
       break;
     }
   if (!c)
     for (PConn* p : pconns_)
-      if (!p->dead && p->q.size() < depth) {
+      if (!p->dead && !p->draining && p->q.size() < depth) {
         c = p;
         break;
       }
@@ -850,6 +856,10 @@ void ClientPool::PConn::do_read() {
       }
       pool->pfail(this, in.empty() || q.empty() ? "NoHttpResponseException: connection closed"
                                                 : "TruncatedChunkException: premature EOF");
+      return;
+    }
+    if (draining && std::all_of(q.begin(), q.end(), [](const Pending& p) { return p.abandoned; })) {
+      pool->pdestroy(this);  // nothing on it is waited for any more
       return;
     }
     if (size_t(n) < sizeof buf) return;

@@ -767,8 +767,9 @@ def test_pipelined_mode_keeps_no_idle_plain_connections(hola, aloha):
     _concurrent_chains(s, 8)
     base = fds()
     for _ in range(4):
-        # one slow answer at the head of a pipelined connection: its call times out and the
-        # calls behind it are re-sent on fresh plain connections, where they succeed
+        # one slow answer at the head of a pipelined connection: its call times out, the calls
+        # queued behind it wait for their answers or their own timeouts (not re-sent), and the
+        # connection closes once none of them is waited for
         aloha.set_mode("slow", delay_s=0.8)
         threading.Thread(target=lambda: s.get("/api/hola-chaining", timeout=10), daemon=True).start()
         time.sleep(0.05)
@@ -828,6 +829,35 @@ def test_malformed_status_line_is_not_resent_by_the_transport(hola, aloha, pipel
     assert r.get("feign", 0) >= 2
     assert len(aloha.requests) - n0 == r["feign"] + 1
     assert "<--- ERROR ClientProtocolException: malformed response" in _wait_log(s2, "ClientProtocolException", 1)
+
+
+def test_pipelined_timeout_does_not_resend_the_calls_behind_it(hola, aloha):
+    """A call abandoned on its Hystrix timeout no longer makes the client re-send the calls
+    pipelined behind it, which aloha already has (that doubled aloha's load exactly when it was
+    slow). Aloha sees each call once, no transport retry is spent, the connection is closed once
+    every call on it is given up, and the next calls run on a fresh one."""
+    import os
+    aloha.set_mode("slow", delay_s=1.0)
+    s = hola(args=["--aloha-url", aloha.url, "--no-tracing", "--feign-log", "none", "--feign-retry", "off",
+                   "-Dhystrix.command.default.circuitBreaker.enabled=false"] + _PIPE, threads=1)
+    fds = lambda: len(os.listdir(f"/proc/{s.proc.pid}/fd"))  # noqa: E731
+    base = fds()
+    res = _concurrent_chains(s, 4)
+    assert all(st == 200 and body[1:] == [FALLBACK] for st, body in res), res
+    assert _events(s).get("TIMEOUT") == 4
+    time.sleep(0.3)
+    # the fake answers a connection's requests one at a time, so it has read only the first
+    # by now; what matters is that nothing arrived on any other connection (a re-send)
+    assert 1 <= len(aloha.requests) <= 4
+    assert len({r["peer_port"] for r in aloha.requests}) == 1, aloha.requests
+    assert _retries(s).get("transport", 0) == 0
+    deadline = time.monotonic() + 2.0  # (the test client's own connections close asynchronously)
+    while fds() > base and time.monotonic() < deadline:
+        time.sleep(0.02)
+    assert fds() <= base, (base, fds())  # given up once all four were abandoned
+    aloha.set_mode("ok")
+    assert chain(s)[1] == "Aloha mai aloha-1"
+    assert len({r["peer_port"] for r in aloha.requests}) == 2
 
 
 @pytest.mark.parametrize("pipelined", [False, True], ids=["plain", "pipelined"])
