@@ -202,6 +202,11 @@ bool Connection::process(const char* data, size_t len, size_t* consumed) {
     off += total;
     WorkerStats::bump(st.requests);
     ++handled;
+    // Read before the handler chooses its Connection header: the flag only goes from false to
+    // true, so when it is set here the handler sees it too and answers `Connection: close`.
+    // Re-reading it after the handler would race with begin_termination() on another thread
+    // and close a connection whose response had just announced keep-alive.
+    const bool closing = worker_->server().closing();
     if (prof) {
       int64_t th = mono_ns();
       h.on_request(*this, r);
@@ -209,7 +214,7 @@ bool Connection::process(const char* data, size_t len, size_t* consumed) {
     } else {
       h.on_request(*this, r);
     }
-    if (worker_->server().closing()) close_after_flush_ = true;
+    if (closing) close_after_flush_ = true;
   }
   in_process_ = false;
   if (StageProfile* prof = worker_->profile(); prof && handled) prof->batch.add(handled);
@@ -237,7 +242,9 @@ void Connection::complete(std::string_view response, bool keep_alive) {
     return;
   }
   parked_ = false;
-  if (!keep_alive || worker_->server().closing()) close_after_flush_ = true;
+  // keep_alive is what the response announced; the caller chose it with closing() (reading
+  // the flag again here could close a connection whose response said keep-alive)
+  if (!keep_alive) close_after_flush_ = true;
   out_.append(response.data(), response.size());
   if (in_process_) return;
   // Continue with pipelined requests that arrived while parked.

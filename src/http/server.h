@@ -56,7 +56,8 @@ class Connection final : public EventLoop::Handler {
   void close_after_response() { close_after_flush_ = true; }
 
   // Async requests: park() from inside on_request; later call complete() (on the worker
-  // thread) with the full response. Input processing resumes after completion.
+  // thread) with the full response. Input processing resumes after completion. keep_alive is
+  // what the response announces (false once the server is closing(); the caller decides).
   void park() { parked_ = true; }
   void complete(std::string_view response, bool keep_alive);
 

@@ -646,6 +646,38 @@ def test_drain_closes_busy_keepalive_connections_between_responses(hola):
     assert len(results) == 4 and all(r[0] == "ok" and r[1] > 0 and r[2] == b"" for r in results), results
 
 
+def test_no_keepalive_response_is_followed_by_a_close_when_termination_begins(hola):
+    """SIGTERM under closed-loop keep-alive load, many times: a response that announced
+    keep-alive is never followed by the server closing that connection. The Connection header
+    and the close decision come from one read of the closing flag; before that fix the server
+    read it again after the handler, so a SIGTERM landing between the two reads closed a
+    connection right after a keep-alive response, and the client's next request failed
+    (7 loadgen errors in 80 terminations on the old binary, 0 after)."""
+    import json as _json
+    import signal
+    import subprocess
+
+    from hola_amd import native
+
+    loadgen = str(native.binary("hola_loadgen"))
+    errors = requests = 0
+    for _ in range(40):
+        s = hola(args=["--shutdown-delay-ms", "150", "--log-level", "warn"], threads=2)
+        lg = subprocess.Popen([loadgen, "-t", "2", "-c", "32", "-d", "5s", "--json", f"{s.url}/api/hola"],
+                              stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
+        time.sleep(0.25)
+        s.proc.send_signal(signal.SIGTERM)
+        time.sleep(0.1)  # inside the delay: the clients are being moved off with Connection: close
+        lg.send_signal(signal.SIGINT)
+        out, _ = lg.communicate(timeout=30)
+        assert s.proc.wait(timeout=10) == 0
+        lat = _json.loads([ln for ln in out.splitlines() if ln.startswith("{")][-1])["latency"]
+        errors += lat["errors"]
+        requests += lat["count"]
+    assert requests > 10000
+    assert errors == 0, errors
+
+
 def _metric_value(s, name: str) -> float:
     for line in s.get("/metrics")[2].decode().splitlines():
         if line.startswith(name + " "):
