@@ -3,15 +3,13 @@
 // The GPU boxes have no perf and rocprofv3 sees no kernels here (the service dispatches none),
 // so this is the host-side profile: each registered thread arms a timer on its own CPU-time
 // clock (timer_create(CLOCK_THREAD_CPUTIME_ID) delivering SIGPROF to that thread), and the
-// handler records a short call stack (_Unwind_Backtrace, which walks .eh_frame, so frames of
-// libc and of code built without frame pointers are found too) into a preallocated buffer.
-// Time spent inside a syscall is charged to the libc wrapper the thread returns to (send,
-// recv, epoll_wait), so the profile also splits kernel time by call. At exit the samples and
-// the executable mappings are written as text; `bench/cpuprof_report.py` symbolises them.
-//
-// The unwinder is not async-signal-safe in general: it may take the loader's lock (glibc's
-// dl_iterate_phdr). That lock is recursive, and the profiled threads load no libraries after
-// start-up, so a sample cannot deadlock them; still, this is a diagnostic mode, off by default.
+// handler records a short call stack into a preallocated buffer by walking the frame-pointer
+// chain from the interrupted context's RBP (the native code is built with
+// -fno-omit-frame-pointer; every read is bounds-checked against the thread's stack). The walk
+// is async-signal-safe: no unwinder, no loader lock, no allocation. Time spent inside a
+// syscall is charged to the libc wrapper the thread returns to (send, recv, epoll_wait), so
+// the profile also splits kernel time by call. At exit the samples and the executable
+// mappings are written as text; `bench/cpuprof_report.py` symbolises them.
 #pragma once
 #include <string>
 

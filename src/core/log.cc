@@ -1,6 +1,7 @@
 #include "core/log.h"
 
 #include <pthread.h>
+#include <signal.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -217,6 +218,13 @@ void Logger::flush() {
 }
 
 void Logger::run() {
+  // The writer may be started before main() blocks its termination signals (`--log-level`
+  // touches the logger while the flags are parsed). A process-directed SIGTERM must never be
+  // delivered here, where its default action would kill the process: main takes it with
+  // sigwait/sigtimedwait.
+  sigset_t all;
+  sigfillset(&all);
+  pthread_sigmask(SIG_BLOCK, &all, nullptr);
   std::string out;
   int idle = 0;
   for (;;) {

@@ -5,6 +5,7 @@ import os
 import shutil
 import socket
 import time
+from pathlib import Path
 
 import pytest
 
@@ -608,6 +609,27 @@ def test_second_signal_ends_the_shutdown_delay(hola):
     assert s.proc.wait(timeout=10) == 0
     assert time.monotonic() - t0 < 5
     assert "ending the delay early" in s.log()
+
+
+def test_every_thread_blocks_the_termination_signals(hola):
+    """A process-directed SIGTERM goes to any thread that does not block it. Only main takes
+    it (sigwait); a thread with it unblocked would die of its default action and take the
+    replica with it, skipping the shutdown delay and the drain. The log writer, started while
+    `--log-level` is parsed (before main blocks the signals), once was such a thread: the
+    second SIGTERM of test_second_signal_ends_the_shutdown_delay killed the process."""
+    import signal
+
+    s = hola(args=["--shutdown-delay-ms", "1000"], threads=2)
+    want = (1 << (signal.SIGTERM - 1)) | (1 << (signal.SIGINT - 1))
+    names = []
+    for task in Path(f"/proc/{s.proc.pid}/task").iterdir():
+        if task.name == str(s.proc.pid):
+            continue  # main: inside sigwait the waited signals show as unblocked
+        status = (task / "status").read_text()
+        fields = dict(line.split(":\t", 1) for line in status.splitlines() if ":\t" in line)
+        names.append(fields["Name"].strip())
+        assert int(fields["SigBlk"], 16) & want == want, (fields["Name"], fields["SigBlk"])
+    assert "hola-log" in names, names
 
 
 def test_drain_closes_busy_keepalive_connections_between_responses(hola):
