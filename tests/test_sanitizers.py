@@ -95,14 +95,26 @@ def tsan_wrapper():
     return ["setarch", platform.machine(), "-R"] if shutil.which("setarch") else []
 
 
+# "default": the server's defaults. "round3": the round-3 paths together — pipelined aloha
+# calls (shared connections drained on Hystrix timeouts), Feign BASIC logging through the log
+# rings, adaptive busy-polling, and a SIGTERM that first runs the shutdown delay (readiness
+# failing, `Connection: close` on every response) before the drain.
+VARIANTS = {
+    "default": ["--feign-log", "none"],
+    "round3": ["--feign-log", "basic", "--aloha-pipeline", "4", "--busy-poll-us", "auto",
+               "--shutdown-delay-ms", "300"],
+}
+
+
+@pytest.mark.parametrize("variant", sorted(VARIANTS))
 @pytest.mark.parametrize("preset", ["tsan", "asan"])
-def test_sanitized_server(preset, tmp_path):
+def test_sanitized_server(preset, variant, tmp_path):
     build(preset)
     exe = build_dir(preset) / "hola"
     conf = tmp_path / "t.properties"
     conf.write_text("hello=v %s\n")
     with FakeAloha() as aloha, FakeZipkin() as zipkin:
-        s = HolaProcess(args=["--aloha-url", aloha.url, "--zipkin-url", zipkin.url, "--feign-log", "none",
+        s = HolaProcess(args=["--aloha-url", aloha.url, "--zipkin-url", zipkin.url, *VARIANTS[variant],
                               f"-Dconf={conf}", "-Dhystrix.command.default.metrics.healthSnapshot.intervalInMilliseconds=0"],
                         env={"HOSTNAME": "san", **SAN_ENV[preset]}, threads=4, exe=exe, log_level="warn",
                         wrapper=tsan_wrapper() if preset == "tsan" else None)
