@@ -128,6 +128,7 @@ class Pod:
     prestop: subprocess.Popen | None = None
     prestop_http: Future | None = None
     term_sent: bool = False
+    kill_sent: bool = False
     gone: bool = False
 
     @property
@@ -403,8 +404,9 @@ class Kubelet:
         if not pod.term_sent and (hook_done or now >= pod.grace_deadline):
             pod.proc.send_signal(signal.SIGTERM)
             pod.term_sent = True
-        if now >= pod.grace_deadline:
-            pod.proc.kill()
+        if now >= pod.grace_deadline and not pod.kill_sent:
+            pod.proc.kill()  # once: the next tick sees the exit
+            pod.kill_sent = True
             self.cluster.event(pod.name, "Killed", "grace period expired: SIGKILL")
 
     def kill_container(self, pod: Pod, sig: int = signal.SIGKILL) -> None:

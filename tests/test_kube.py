@@ -370,3 +370,23 @@ def test_memory_limit_is_enforced_as_oomkilled(cluster):
     assert c.rollout_status()["revision"] == 2 and not c.rollout_status()["complete"]
     # the old revision keeps serving: maxUnavailable 25 % of 1 rounds down to 0
     assert len(c.endpoints()) == 1 and all(p["revision"] == 1 for p in c.get_pods() if p["ready"])
+
+
+def test_grace_period_expiry_kills_once(cluster):
+    """A container still running when terminationGracePeriodSeconds runs out gets one SIGKILL
+    (here: a 30 s shutdown delay against a 1 s grace period); the pod is then gone."""
+    c = cluster(replicas=1)
+    c.patch({"spec": {"template": {"spec": {"terminationGracePeriodSeconds": 1, "containers": [
+        {"name": "hola", "args": ["--shutdown-delay-ms", "30000"]}]}}}})
+    c.wait(lambda: c.rollout_status()["complete"] and c.rollout_status()["revision"] == 2, 30, "rollout")
+    c.wait(lambda: len(c.get_pods()) == 1, 30, "old pod gone")
+    name = c.get_pods()[0]["name"]
+    t0 = time.monotonic()
+    c.delete_pod(name)
+    c.wait(lambda: all(p["name"] != name for p in c.get_pods()), 10, "pod gone")
+    assert 0.9 <= time.monotonic() - t0 < 5
+    mine = [e for e in c.events if e[1] == name]
+    assert sum(1 for e in mine if e[2] == "Killed") == 1, mine
+    assert any(e[2] == "Deleted" and "exit -9" in e[3] for e in mine), mine
+    log = (c.state / "pods" / name / "container.log").read_text()
+    assert "readiness failing, still serving for 30000 ms" in log
