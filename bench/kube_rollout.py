@@ -8,6 +8,10 @@
   2. `oc set env dc/hola ...` under 512 kept-alive connections through the Service, with the
      manifests' --shutdown-delay-ms 5000: rollout time, load-generator errors / non-2xx;
   3. the same rollout with the delay patched to 0 (the pre-round-3 shutdown);
+     2 and 3 run once per Service data path (--service): "proxy" through hola_rrproxy
+     (kube-proxy's userspace mode: one proxy hop per request) and "dnat", where each new
+     connection is DNATed at connect time to a published endpoint (the iptables/IPVS modes:
+     no hop, an established connection keeps its pod);
   4. a SIGKILLed pod: when it leaves the Service endpoints and when it rejoins;
   5. a ConfigMap edit: when all 8 pods serve the new greeting.
 
@@ -49,12 +53,14 @@ def greetings(c: Cluster, n: int = 64) -> list[str]:
     return out
 
 
-def rollout_under_load(c: Cluster, env: dict, conns: int, threads: int, settle_s: float) -> dict:
+def rollout_under_load(c: Cluster, env: dict, conns: int, threads: int, settle_s: float,
+                       service: str = "proxy") -> dict:
     """Starts the load, rolls the template, waits for the rollout and for the old pods to
     exit, lets the load run `settle_s` more, and returns the load generator's counters."""
+    extra = ["--verify-body", "--endpoints-file", str(c.endpoints_file())] if service == "dnat" else []
     lg = subprocess.Popen([str(native.binary("hola_loadgen")), "-t", str(threads), "-c", str(conns), "-d", "600s",
-                           "--json", c.service_url() + "/api/hola"], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
-                          text=True)
+                           "--json", *extra, c.service_url() + "/api/hola"], stdout=subprocess.PIPE,
+                          stderr=subprocess.PIPE, text=True)
     time.sleep(3.0)
     rev0 = c.rollout_status()["revision"]
     t0 = time.monotonic()
@@ -69,9 +75,11 @@ def rollout_under_load(c: Cluster, env: dict, conns: int, threads: int, settle_s
     lines = [ln for ln in out.strip().splitlines() if ln.startswith("{")]
     r = json.loads(lines[-1]) if lines else {"error": err[-2000:]}
     lat = r.get("latency", {})
-    return {"rollout_s": round(t_roll, 2), "old_pods_gone_s": round(t_gone, 2), "revision": c.rollout_status()["revision"],
+    return {"service": service, "rollout_s": round(t_roll, 2), "old_pods_gone_s": round(t_gone, 2),
+            "revision": c.rollout_status()["revision"],
             "requests": lat.get("count"), "rps": r.get("rps"), "errors": lat.get("errors"),
-            "non2xx": lat.get("non2xx"), "reconnects": lat.get("reconnects"),
+            "non2xx": lat.get("non2xx"), "reconnects": lat.get("reconnects"), "pods_reached": r.get("targets"),
+            "body_checked": lat.get("body_checked"), "body_mismatch": lat.get("body_mismatch"),
             "p50_ms": round(lat.get("p50_ns", 0) / 1e6, 3), "p99_ms": round(lat.get("p99_ns", 0) / 1e6, 3)}
 
 
@@ -88,6 +96,8 @@ def main() -> int:
     ap.add_argument("--connections", type=int, default=512)
     ap.add_argument("--loadgen-threads", type=int, default=4)
     ap.add_argument("--settle-s", type=float, default=2.0)
+    ap.add_argument("--service", choices=["proxy", "dnat", "both"], default="both",
+                    help="Service data path under the rollouts (default: both, one after the other)")
     a = ap.parse_args()
     out = Path(a.out)
     if out.exists():
@@ -114,19 +124,27 @@ def main() -> int:
                                                      for p in pods)
         log(f"{a.replicas} pods ready after {res['ready_s']} s; {len(seen)} distinct greetings")
 
-        res["rollout_with_delay"] = rollout_under_load(c, {"JAVA_OPTIONS": "-Xmx512m "
-                                                           "-Dconf=/etc/config/translation.properties -Drollout=1"},
-                                                       a.connections, a.loadgen_threads, a.settle_s)
-        log(f"rollout with --shutdown-delay-ms 5000: {res['rollout_with_delay']}")
+        services = ["proxy", "dnat"] if a.service == "both" else [a.service]
+        k = 0
+        for svc in services:
+            k += 1
+            key = "rollout_with_delay" + ("" if svc == "proxy" else "_dnat")
+            res[key] = rollout_under_load(c, {"JAVA_OPTIONS": "-Xmx512m -Dconf=/etc/config/translation.properties "
+                                                              f"-Drollout={k}"},
+                                          a.connections, a.loadgen_threads, a.settle_s, svc)
+            log(f"rollout with --shutdown-delay-ms 5000 ({svc}): {res[key]}")
         # the pre-round-3 behaviour: no delay (a rollout of its own, without load)
         rev = c.rollout_status()["revision"]
         c.patch({"spec": {"template": {"spec": {"containers": [{"name": "hola", "args": ["--shutdown-delay-ms", "0"]}]}}}})
         c.wait(lambda: c.rollout_status()["revision"] > rev and c.rollout_status()["complete"], 600, "patch rollout")
         c.wait(lambda: all(p["status"] != "Terminating" for p in c.get_pods()), 120, "old pods gone")
-        res["rollout_without_delay"] = rollout_under_load(c, {"JAVA_OPTIONS": "-Xmx512m "
-                                                              "-Dconf=/etc/config/translation.properties -Drollout=2"},
-                                                          a.connections, a.loadgen_threads, a.settle_s)
-        log(f"rollout with --shutdown-delay-ms 0: {res['rollout_without_delay']}")
+        for svc in services:
+            k += 1
+            key = "rollout_without_delay" + ("" if svc == "proxy" else "_dnat")
+            res[key] = rollout_under_load(c, {"JAVA_OPTIONS": "-Xmx512m -Dconf=/etc/config/translation.properties "
+                                                              f"-Drollout={k}"},
+                                          a.connections, a.loadgen_threads, a.settle_s, svc)
+            log(f"rollout with --shutdown-delay-ms 0 ({svc}): {res[key]}")
 
         victim = c.get_pods()[0]
         ip = victim["ip"]

@@ -23,6 +23,15 @@
 // each target; a mismatch counts as an error (and in "body_mismatch"), so a server that
 // answers fast with the wrong bytes cannot inflate req/s.
 //
+// Service mode (`--endpoints-file F`): the load generator addresses a Kubernetes Service (the
+// --targets / URL address, used in the Host header) and each new connection is DNATed at
+// connect time to one of the Service's current endpoints, read from F (the file the local
+// manifest executor publishes, `ip:port` per line, re-read when it changes). That is what
+// kube-proxy's iptables/IPVS modes do in the client's kernel: an established connection keeps
+// its pod whatever the endpoints do later, a new one (after `Connection: close`) goes to a
+// current endpoint, and there is no failover: a connection refused by a pod that stopped
+// listening counts as an error. Endpoints are taken in round-robin order (IPVS `rr`).
+//
 // wrk-style invocation: `hola_loadgen -t8 -c64 -d30s [--latency] http://host:port/path`
 // takes the target from the URL, accepts wrk's duration suffixes (s/m/h) and prints a
 // wrk-like text summary (`--json` keeps the JSON line).
@@ -33,6 +42,7 @@
 #include <sys/prctl.h>
 #include <sys/eventfd.h>
 #include <sys/socket.h>
+#include <sys/stat.h>
 #include <signal.h>
 #include <unistd.h>
 
@@ -42,7 +52,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <fstream>
 #include <iostream>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -93,6 +105,7 @@ struct Options {
   std::vector<std::string> expect_bodies;  // --expect-body: per target, or one for all
   bool verify_body = false;                // --verify-body: learn the first 2xx body per target
   std::vector<int> conn_targets;           // --conn-targets: target index of connection i (cycled)
+  std::string endpoints_file;              // --endpoints-file: Service mode (connect-time DNAT)
 };
 
 struct Conn {
@@ -140,8 +153,83 @@ void signal_done() {
   (void)w;
 }
 
+// Service mode: the endpoints of the Service as last published, and every endpoint ever seen
+// (its index is the connection's `target`, so bodies are checked per pod).
+struct Dnat {
+  std::mutex mu;
+  std::string path;
+  ino_t ino = 0;
+  off_t size = -1;
+  timespec mtime{};
+  std::vector<Target> all;
+  std::map<std::string, int> ids;
+  std::vector<int> current;
+  uint64_t rr = 0;
+
+  void reload_locked() {
+    struct stat st {};
+    if (stat(path.c_str(), &st) != 0) {
+      current.clear();
+      return;
+    }
+    if (st.st_ino == ino && st.st_size == size && st.st_mtim.tv_sec == mtime.tv_sec &&
+        st.st_mtim.tv_nsec == mtime.tv_nsec)
+      return;
+    ino = st.st_ino;
+    size = st.st_size;
+    mtime = st.st_mtim;
+    std::ifstream f(path);
+    std::vector<int> next;
+    for (std::string line; std::getline(f, line);) {
+      while (!line.empty() && isspace((unsigned char)line.back())) line.pop_back();
+      if (line.empty() || line[0] == '#') continue;
+      auto it = ids.find(line);
+      if (it == ids.end()) {
+        const size_t colon = line.rfind(':');
+        if (colon == std::string::npos) continue;
+        Target t;
+        t.host = line.substr(0, colon);
+        if (t.host.size() > 2 && t.host.front() == '[') t.host = t.host.substr(1, t.host.size() - 2);
+        t.port = atoi(line.c_str() + colon + 1);
+        if (!resolve_host(t.host, t.port, &t.addr, &t.len, nullptr)) continue;
+        it = ids.emplace(line, int(all.size())).first;
+        all.push_back(t);
+      }
+      next.push_back(it->second);
+    }
+    current.swap(next);
+  }
+  // The next endpoint for a new connection; false when the Service has none.
+  bool pick(Target* out, int* id) {
+    std::lock_guard<std::mutex> g(mu);
+    reload_locked();
+    if (current.empty()) return false;
+    *id = current[rr++ % current.size()];
+    *out = all[size_t(*id)];
+    return true;
+  }
+  size_t seen() {
+    std::lock_guard<std::mutex> g(mu);
+    return all.size();
+  }
+};
+Dnat g_dnat;
+
 bool connect_once(Conn* c, const Options& o) {
-  const Target& t = o.targets[size_t(c->target)];
+  Target picked;
+  const Target* tp = nullptr;
+  if (!o.endpoints_file.empty()) {
+    int id = 0;
+    if (!g_dnat.pick(&picked, &id)) {
+      errno = EHOSTUNREACH;  // a Service without endpoints (kube-proxy rejects it)
+      return false;
+    }
+    c->target = id;
+    tp = &picked;
+  } else {
+    tp = &o.targets[size_t(c->target)];
+  }
+  const Target& t = *tp;
   c->fd = connect_blocking(t.addr, t.len, 1000);
   if (c->fd < 0) return false;
   set_nonblocking(c->fd, true);
@@ -152,11 +240,19 @@ bool connect_once(Conn* c, const Options& o) {
 }
 
 // Reconnect after a failure: like a client-side load balancer, fail over to the next
-// target when the current one refuses, retrying for up to ~5 s (a replica restart).
-bool connect_conn(Conn* c, const Options& o) {
+// target when the current one refuses, retrying for up to ~5 s (a replica restart). In
+// Service mode every attempt is DNATed afresh, and each failed one is a client-visible
+// connection error (`*failed`): there is no failover below the Service.
+bool connect_conn(Conn* c, const Options& o, uint64_t* failed = nullptr) {
   const int n = int(o.targets.size());
+  const bool dnat = !o.endpoints_file.empty();
   for (int attempt = 0; attempt < 100; ++attempt) {
     if (connect_once(c, o)) return true;
+    if (dnat) {
+      if (failed && errno != EHOSTUNREACH) ++*failed;
+      usleep(errno == EHOSTUNREACH ? 50000 : 1000);
+      continue;
+    }
     c->target = (c->target + 1) % n;
     if ((attempt + 1) % n == 0) usleep(50000);
   }
@@ -244,7 +340,7 @@ void thread_main(ThreadState* ts, const Options* o) {
     auto c = std::make_unique<Conn>();
     c->target = o->conn_targets.empty() ? (i + o->target_offset) % int(o->targets.size())
                                         : o->conn_targets[size_t(i) % o->conn_targets.size()];
-    const Target& t = o->targets[size_t(c->target)];
+    const Target& t = o->targets[size_t(c->target)];  // Service mode: the Service's address
     const bool v6 = t.host.find(':') != std::string::npos;  // RFC 3986 IP-literal in Host
     c->req = o->method + " " + o->path + " HTTP/1.1\r\nHost: " + (v6 ? "[" + t.host + "]" : t.host) + ":" +
              std::to_string(t.port) + "\r\n";
@@ -263,9 +359,10 @@ void thread_main(ThreadState* ts, const Options* o) {
     ts->expected[k] = o->expect_bodies[e];
     ts->have_expected[k] = true;
   }
+  const bool dnat = !o->endpoints_file.empty();
   for (auto& c : ts->conns) {
-    if (!connect_once(c.get(), *o)) {
-      const Target& t = o->targets[size_t(c->target)];
+    if (!(dnat ? connect_conn(c.get(), *o) : connect_once(c.get(), *o))) {
+      const Target& t = o->targets[dnat ? 0 : size_t(c->target)];
       if (!g_connect_failed.exchange(true))
         snprintf(g_connect_error, sizeof g_connect_error, "connect %s:%d failed: %s", t.host.c_str(), t.port,
                  strerror(errno));
@@ -419,7 +516,7 @@ void thread_main(ThreadState* ts, const Options* o) {
         ++ts->errors;
         ++run_errors;
         ++ts->reconnects;
-        if (!connect_conn(c, *o)) {
+        if (!connect_conn(c, *o, &ts->errors)) {
           g_stop.store(true);
           signal_done();
           break;
@@ -456,6 +553,16 @@ void thread_main(ThreadState* ts, const Options* o) {
           ++ts->non2xx;
         } else if (verify) {
           const size_t t = size_t(c->target);
+          if (t >= ts->expected.size()) {  // Service mode: an endpoint first seen since start-up
+            ts->expected.resize(t + 1);
+            ts->have_expected.resize(t + 1, false);
+            if (o->expect_bodies.size() == 1)
+              for (size_t k = 0; k <= t; ++k)
+                if (!ts->have_expected[k]) {
+                  ts->expected[k] = o->expect_bodies[0];
+                  ts->have_expected[k] = true;
+                }
+          }
           const size_t blen = at + used - body_at;
           if (!ts->have_expected[t]) {
             ts->expected[t].assign(c->buf + body_at, blen);
@@ -482,7 +589,7 @@ void thread_main(ThreadState* ts, const Options* o) {
         epoll_ctl(ts->epfd, EPOLL_CTL_DEL, c->fd, nullptr);
         ::close(c->fd);
         ++ts->reconnects;
-        if (!connect_conn(c, *o)) {
+        if (!connect_conn(c, *o, &ts->errors)) {
           g_stop.store(true);
           signal_done();
           break;
@@ -670,6 +777,7 @@ int main(int argc, char** argv) {
     else if (a == "--expect-body") o.expect_bodies.push_back(unescape(val()));
     else if (a == "--verify-body") o.verify_body = true;
     else if (a == "--cpu-profile") cpu_profile = val();
+    else if (a == "--endpoints-file") o.endpoints_file = val();
     else if (a == "--conn-targets") {
       if (!parse_cpu_list(val(), &o.conn_targets)) {  // same "0,1,1,0" / "0-3" syntax
         fprintf(stderr, "loadgen: bad --conn-targets\n");
@@ -683,6 +791,7 @@ int main(int argc, char** argv) {
               "                    [--target-offset K] [--busy-poll-us N [--busy-poll-pause P]] [--epoll-lt] [-H 'Name: v']\n"
               "                    [--pipeline P] [--expect-body B]... [--verify-body] [--conn-targets i,j,..]\n"
               "                    [--cpu-profile FILE]  (sampled call stacks, bench/cpuprof_report.py --threads hola-lg)\n"
+              "                    [--endpoints-file F]  (Service mode: --targets is the Service, F its endpoints)\n"
               "       hola_loadgen -t T -c C -d 30s [--latency] [--json] [-H 'Name: v'] http://host:port/path   (wrk style)\n");
       return 2;
     }
@@ -695,6 +804,13 @@ int main(int argc, char** argv) {
   }
   const bool wrk_text = !url.empty() && !json && !o.control;
   if (!parse_targets(targets, &o.targets)) return 2;
+  if (!o.endpoints_file.empty()) {
+    if (o.targets.size() != 1 || !o.conn_targets.empty() || o.expect_bodies.size() > 1) {
+      fprintf(stderr, "loadgen: --endpoints-file takes one Service address, one --expect-body at most\n");
+      return 2;
+    }
+    g_dnat.path = o.endpoints_file;
+  }
   for (int t : o.conn_targets)
     if (t < 0 || size_t(t) >= o.targets.size()) {
       fprintf(stderr, "loadgen: --conn-targets index %d out of range\n", t);
@@ -789,8 +905,8 @@ int main(int argc, char** argv) {
       return 0;
     }
     printf("{\"mode\":\"%s\",\"duration_s\":%.3f,\"connections\":%d,\"threads\":%d,\"targets\":%zu,\"target_rate\":%.1f,\"rps\":%.1f,\"latency\":%s}\n",
-           o.rate > 0 ? "open-loop" : "duration", o.duration_s, o.connections, o.threads, o.targets.size(), o.rate, rps,
-           s.c_str());
+           o.rate > 0 ? "open-loop" : "duration", o.duration_s, o.connections, o.threads,
+           o.endpoints_file.empty() ? o.targets.size() : g_dnat.seen(), o.rate, rps, s.c_str());
     return 0;
   }
 

@@ -21,7 +21,10 @@ reference's `mvn fabric8:json fabric8:apply` created (`/root/reference/pom.xml:6
   exactly the Ready, non-terminating pods the selector matches, as the endpoints controller
   publishes them, applied `endpoint_sync_s` after each change (kube-proxy's sync delay). A
   connection to an endpoint that stopped listening fails as it does through kube-proxy's DNAT
-  (no failover);
+  (no failover). That is kube-proxy's old userspace mode, one proxy hop per request. The
+  iptables/IPVS modes DNAT each new connection in the client's kernel instead: a client that
+  reads `endpoints_file()` at connect time (`hola_loadgen --endpoints-file`) gets exactly that,
+  with no hop;
 * **ConfigMaps**: projected into every pod that mounts one, updated `configmap_sync_s` after an
   edit through the kubelet's `..data` symlink swap;
 * **cluster DNS**: a URL in a pod's env or args naming a Service of this cluster (`aloha`,
@@ -99,8 +102,7 @@ class Cluster:
         # pod network: 127.<a>.0.0/16 per cluster (127.<a>.0.1 = stand-in Services, pods from
         # 127.<a>.0.2 on; .0 and .255 host parts are skipped): room for 65 k pods over the
         # executor's life, so rollouts never exhaust it
-        rnd = random.Random()
-        self.net = f"127.{rnd.randrange(100, 250)}"
+        self._net_lock = self._claim_network()
         self.subnet = f"{self.net}.0"
         self._ips = (f"{self.net}.{b}.{c}" for b in range(256) for c in range(1, 255) if (b, c) != (0, 1))
         self.services: dict[str, dict] = {}
@@ -145,6 +147,26 @@ class Cluster:
         self._stop = threading.Event()
         self._thread: threading.Thread | None = None
 
+    def _claim_network(self):
+        """Takes a free 127.<a>.0.0/16 for this cluster's pods and stand-in Services: every pod
+        binds :8080 on its own address, so two clusters on one host (parallel tests, a bench
+        next to a test) must never share one. The claim is an flock held for the cluster's
+        life, so it also holds across processes, and is released when the process exits."""
+        import fcntl
+
+        lock_dir = Path(tempfile.gettempdir()) / "hola-kube-nets"
+        lock_dir.mkdir(exist_ok=True)
+        for a in random.sample(range(100, 250), 150):
+            f = open(lock_dir / f"127.{a}.lock", "w")
+            try:
+                fcntl.flock(f, fcntl.LOCK_EX | fcntl.LOCK_NB)
+            except OSError:
+                f.close()
+                continue
+            self.net = f"127.{a}"
+            return f
+        raise ClusterError("no free 127.x.0.0/16 pod network on this host")
+
     # ------------------------------------------------------------------ lifecycle
     def start(self) -> "Cluster":
         try:
@@ -180,6 +202,7 @@ class Cluster:
         self._stop_services()
         self.kubelet.shutdown()
         self._events_f.close()
+        self._net_lock.close()  # releases the pod network
 
     def _stop_services(self) -> None:
         for proc in [*self.proxies, self.sink]:
@@ -247,6 +270,13 @@ class Cluster:
     def service_url(self, name: str | None = None) -> str:
         host, port = self.service_ports[name or next(iter(self.services))]
         return f"http://{host}:{port}"
+
+    def endpoints_file(self, name: str | None = None) -> Path:
+        """The Service's endpoints as the executor publishes them (`ip:port` per line, replaced
+        atomically on each sync): the DNAT table of kube-proxy's iptables/IPVS modes, for a
+        client that resolves the Service at connect time (`hola_loadgen --endpoints-file`)
+        instead of going through the userspace proxy."""
+        return self.state / "endpoints" / (name or next(iter(self.services)))
 
     def rewrite_service_urls(self, value: str) -> str:
         import re

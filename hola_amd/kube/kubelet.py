@@ -405,9 +405,10 @@ class Kubelet:
             pod.proc.send_signal(signal.SIGTERM)
             pod.term_sent = True
         if now >= pod.grace_deadline and not pod.kill_sent:
+            threads = _thread_states(pod.proc.pid)  # what it was doing when the grace ran out
             pod.proc.kill()  # once: the next tick sees the exit
             pod.kill_sent = True
-            self.cluster.event(pod.name, "Killed", "grace period expired: SIGKILL")
+            self.cluster.event(pod.name, "Killed", f"grace period expired: SIGKILL (threads: {threads})")
 
     def kill_container(self, pod: Pod, sig: int = signal.SIGKILL) -> None:
         if pod.running:
@@ -415,6 +416,29 @@ class Kubelet:
 
     def shutdown(self) -> None:
         self.pool.shutdown(wait=False, cancel_futures=True)
+
+
+def _thread_states(pid: int) -> str:
+    """`name:state:wchan` of each thread of a process, from /proc (the kernel's view of where a
+    container that outlived its grace period was waiting)."""
+    out = []
+    try:
+        tasks = sorted(os.listdir(f"/proc/{pid}/task"), key=int)
+    except OSError:
+        return "?"
+    for t in tasks:
+        base = f"/proc/{pid}/task/{t}"
+        try:
+            with open(f"{base}/stat") as f:
+                stat = f.read()
+            with open(f"{base}/wchan") as f:
+                wchan = f.read().strip() or "-"
+        except OSError:
+            continue
+        name = stat[stat.index("(") + 1:stat.rindex(")")]
+        state = stat[stat.rindex(")") + 2:].split(" ", 1)[0]
+        out.append(f"{name}:{state}:{wchan}")
+    return " ".join(out) or "?"
 
 
 def _port_number(container: dict, port) -> int:
