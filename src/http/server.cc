@@ -667,19 +667,38 @@ uint64_t Server::total_requests() const {
   return n;
 }
 
+namespace {
+// A worker's answer to a task posted by shutdown(). Shared, so the task may still run after
+// shutdown() stopped waiting for it (a worker that does not answer by the drain deadline is
+// not waited for forever).
+struct Answer {
+  std::atomic<bool> done{false};
+  std::atomic<size_t> open{0};
+};
+
+bool wait_answer(const Answer& a, std::chrono::steady_clock::time_point until) {
+  while (!a.done.load()) {
+    if (std::chrono::steady_clock::now() >= until) return false;
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
+  return true;
+}
+}  // namespace
+
 void Server::shutdown(int drain_ms) {
   closing_.store(true);
   draining_.store(true);
+  auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(drain_ms);
   for (auto& a : acceptors_) {
     Acceptor* ap = a.get();
-    std::atomic<bool> done{false};
-    ap->worker->loop().post([ap, &done] {
+    auto ans = std::make_shared<Answer>();
+    ap->worker->loop().post([ap, ans] {
       ap->worker->loop().del(ap->fd);
       ::close(ap->fd);
       ap->fd = -1;
-      done.store(true);
+      ans->done.store(true);
     });
-    while (!done.load()) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    if (!wait_answer(*ans, deadline)) LOG_WARN("drain: worker %d did not close its listener in time", ap->worker->index());
   }
   // Streaming connections close now, and kept-alive ones that have been idle for the grace
   // period; busy ones close after their current response (process() sets close_after_flush_
@@ -688,22 +707,25 @@ void Server::shutdown(int drain_ms) {
   // a closed-loop client has its next request on the way within microseconds, and closing
   // under it would fail that request.
   const int64_t grace_ms = std::min<int64_t>(kDrainIdleGraceMs, drain_ms);
-  auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(drain_ms);
   for (;;) {
     size_t open = 0;
+    bool answered = true;
     for (auto& w : workers_) {
-      std::atomic<size_t> n{0};
-      std::atomic<bool> done{false};
       Worker* wp = w.get();
-      wp->loop().post([wp, &n, &done, grace_ms] {
+      auto ans = std::make_shared<Answer>();
+      wp->loop().post([wp, ans, grace_ms] {
         wp->close_idle_connections(grace_ms);
-        n.store(wp->open_connections());
-        done.store(true);
+        ans->open.store(wp->open_connections());
+        ans->done.store(true);
       });
-      while (!done.load()) std::this_thread::sleep_for(std::chrono::microseconds(200));
-      open += n.load();
+      if (!wait_answer(*ans, deadline)) {
+        LOG_WARN("drain: worker %d did not answer by the drain deadline", wp->index());
+        answered = false;
+        break;
+      }
+      open += ans->open.load();
     }
-    if (open == 0 || std::chrono::steady_clock::now() >= deadline) break;
+    if (!answered || open == 0 || std::chrono::steady_clock::now() >= deadline) break;
     std::this_thread::sleep_for(std::chrono::milliseconds(10));
   }
   for (auto& w : workers_) w->loop().stop();

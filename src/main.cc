@@ -11,11 +11,13 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
 #include <string>
+#include <thread>
 
 #include "app/aloha_chainer.h"
 #include "app/hola_app.h"
@@ -79,6 +81,8 @@ void usage() {
           "                           connection, then drain (default 0; the manifests set it so a\n"
           "                           rolling update outlasts endpoint propagation). A second signal\n"
           "                           ends the delay early\n"
+          "  --exit-deadline-ms N     a termination still running N ms after the signal exits with status 3\n"
+          "                           (default: shutdown delay + drain budget + 10000; 0 = never)\n"
           "  --port-file PATH         write the bound port here once listening\n"
           "  --busy-poll-us N|auto[:N] spin up to N us in epoll before sleeping (default 0); auto = adaptive:\n"
           "                           spin (20 us, or N) while spinning mostly finds work (saturation),\n"
@@ -112,6 +116,10 @@ bool need(int i, int argc, const char* flag) {
 
 }  // namespace
 
+// See the exit watchdog in main(): the time a termination may take beyond the shutdown delay
+// and the drain budget (the reporter's last span export alone may take its 2 s timeout).
+constexpr int64_t kExitMarginMs = 10000;
+
 int main(int argc, char** argv) {
   http::ServerOptions so;
   std::map<std::string, std::string> sysprops;
@@ -126,6 +134,7 @@ int main(int argc, char** argv) {
   const char* hn = getenv("HOSTNAME");
   if (hn) ao.hostname = hn;  // HolaResource.java:57 getOrDefault("HOSTNAME", "unknown")
   int threads = 0, drain_ms = 5000, stream_max = -1, shutdown_delay_ms = 0;
+  int64_t exit_deadline_ms = -1;  // -1: delay + drain + kExitMarginMs; 0: no watchdog
   int64_t stream_stall_ms = 30000;
   std::string cpu_list, port_file, profile_out, cpu_profile;
   int cpu_profile_hz = 1000;
@@ -212,6 +221,7 @@ int main(int argc, char** argv) {
     else if (a == "--config-poll-ms") mo.poll_ms = atoi(val("--config-poll-ms").c_str());
     else if (a == "--drain-ms") drain_ms = atoi(val("--drain-ms").c_str());
     else if (a == "--shutdown-delay-ms") shutdown_delay_ms = std::max(0, atoi(val("--shutdown-delay-ms").c_str()));
+    else if (a == "--exit-deadline-ms") exit_deadline_ms = std::max<int64_t>(0, atoll(val("--exit-deadline-ms").c_str()));
     else if (a == "--port-file") port_file = val("--port-file");
     else if (a == "--busy-poll-us") {
       const std::string v = val("--busy-poll-us");
@@ -394,6 +404,24 @@ int main(int argc, char** argv) {
   int sig = 0;
   sigwait(&sigs, &sig);
   const char* sig_name = sig == SIGTERM ? "SIGTERM" : sig == SIGINT ? "SIGINT" : "SIGHUP";
+  {
+    // Exit watchdog: a termination that has not finished within the delay, the drain and a
+    // margin for the span flush and the helper threads ends here, with a line saying so,
+    // rather than at the kubelet's SIGKILL (terminationGracePeriodSeconds 30 in the
+    // manifests; the defaults sum to 20 s). The line is written straight to fd 2: the log
+    // writer may be what is stuck.
+    const int64_t limit_ms = exit_deadline_ms >= 0 ? exit_deadline_ms
+                                                   : int64_t(shutdown_delay_ms) + std::max(0, drain_ms) + kExitMarginMs;
+    if (limit_ms > 0) std::thread([limit_ms] {
+      std::this_thread::sleep_for(std::chrono::milliseconds(limit_ms));
+      char line[160];
+      const int n = snprintf(line, sizeof line, "hola: termination did not complete within %lld ms; exiting\n",
+                             (long long)limit_ms);
+      ssize_t w = ::write(2, line, size_t(n));
+      (void)w;
+      _exit(3);
+    }).detach();
+  }
   if (shutdown_delay_ms > 0) {
     // Phase 1: fail readiness, keep accepting, close connections between responses. The
     // pod's endpoint removal takes a while to reach every proxy (kube-proxy's sync); new

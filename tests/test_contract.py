@@ -611,6 +611,29 @@ def test_second_signal_ends_the_shutdown_delay(hola):
     assert "ending the delay early" in s.log()
 
 
+def test_exit_deadline_ends_a_termination_that_runs_too_long(hola):
+    """The exit watchdog: a termination still running --exit-deadline-ms after the signal (here
+    a 30 s shutdown delay against a 1 s deadline) ends with status 3 and a line saying so,
+    before the kubelet's SIGKILL would (terminationGracePeriodSeconds)."""
+    import signal
+
+    s = hola(args=["--shutdown-delay-ms", "30000", "--exit-deadline-ms", "1000"])
+    t0 = time.monotonic()
+    s.proc.send_signal(signal.SIGTERM)
+    assert s.proc.wait(timeout=10) == 3
+    assert 0.9 <= time.monotonic() - t0 < 5
+    assert "termination did not complete within 1000 ms; exiting" in s.log()
+
+
+def test_default_exit_deadline_leaves_a_normal_termination_alone(hola):
+    s = hola(args=["--shutdown-delay-ms", "200", "--drain-ms", "300"])
+    import signal
+
+    s.proc.send_signal(signal.SIGTERM)
+    assert s.proc.wait(timeout=10) == 0
+    assert "did not complete" not in s.log()
+
+
 def test_every_thread_blocks_the_termination_signals(hola):
     """A process-directed SIGTERM goes to any thread that does not block it. Only main takes
     it (sigwait); a thread with it unblocked would die of its default action and take the
