@@ -346,4 +346,6 @@ def test_concurrent_accounting_adds_up(native, fail_every):
     if fail_every == 1:  # every call fails: the breaker must open and short-circuit most calls
         assert r["short_circuited"] > total // 2
     if fail_every == 0:
-        assert r["short_circuited"] == 0
+        # no call fails, but bulkhead rejections count as errors in Hystrix's health counts:
+        # the breaker may open only if some were rejected (8 threads share 4 slots)
+        assert r["short_circuited"] == 0 or r["rejected"] > 0, r
