@@ -3,7 +3,8 @@
 // A diagnostic for a process that is alive but not progressing (a replica that outlives its
 // grace period): each thread is stopped briefly with PTRACE_SEIZE + PTRACE_INTERRUPT, its
 // registers read, and its RBP chain walked through /proc/PID/mem (the native code is built
-// with frame pointers; a libc leaf frame shows as its caller). The box has no gdb or perf.
+// with frame pointers; libc has none, so the stack above rsp is also scanned for return
+// addresses into the other mappings). The box has no gdb or perf.
 // Output: one line per thread, `tid name state pc frame...`, addresses as `module+offset`,
 // ready for `addr2line -f -C -e <module>`.
 //
@@ -113,6 +114,22 @@ int main(int argc, char** argv) {
         // a libc leaf (syscall wrapper) keeps no frame: its return address is at rsp
         uintptr_t ret = 0;
         if (pread(mem, &ret, sizeof ret, off_t(r.rsp)) == sizeof ret) printf(" [rsp]=%s", where(maps, ret).c_str());
+        // libc keeps no frame pointers, so a thread waiting in libc has no usable chain: scan
+        // the stack above rsp for words that point into other executable mappings (the
+        // nearest are the return addresses of its callers; a scan can also find stale ones)
+        {
+          uintptr_t words[512];
+          const ssize_t got = pread(mem, words, sizeof words, off_t(r.rsp));
+          int shown = 0;
+          printf(" scan:");
+          for (ssize_t k = 0; k < got / ssize_t(sizeof(uintptr_t)) && shown < 6; ++k) {
+            const std::string w = where(maps, words[k]);
+            if (w.rfind("0x", 0) == 0 || w.rfind("libc.so", 0) == 0) continue;
+            printf(" %s", w.c_str());
+            ++shown;
+          }
+          printf(" |");
+        }
         uintptr_t fp = uintptr_t(r.rbp);
         for (int k = 0; k < 24 && fp; ++k) {
           uintptr_t fr[2];

@@ -406,9 +406,10 @@ class Kubelet:
             pod.term_sent = True
         if now >= pod.grace_deadline and not pod.kill_sent:
             threads = _thread_states(pod.proc.pid)  # what it was doing when the grace ran out
+            stacks = _fpstack(pod.proc.pid, pod.dir / "fpstack.txt")
             pod.proc.kill()  # once: the next tick sees the exit
             pod.kill_sent = True
-            self.cluster.event(pod.name, "Killed", f"grace period expired: SIGKILL (threads: {threads})")
+            self.cluster.event(pod.name, "Killed", f"grace period expired: SIGKILL (threads: {threads}{stacks})")
 
     def kill_container(self, pod: Pod, sig: int = signal.SIGKILL) -> None:
         if pod.running:
@@ -439,6 +440,25 @@ def _thread_states(pid: int) -> str:
         state = stat[stat.rindex(")") + 2:].split(" ", 1)[0]
         out.append(f"{name}:{state}:{wchan}")
     return " ".join(out) or "?"
+
+
+def _fpstack(pid: int, out: Path) -> str:
+    """User-space stacks of every thread (`hola_fpstack`, a frame-pointer walk under ptrace)
+    written to `out`; returns a note for the event, or "" when the tool is not built."""
+    from hola_amd import native
+
+    try:
+        exe = native.binary("hola_fpstack", build_if_missing=False)
+    except Exception:  # noqa: BLE001 - a diagnostic only
+        return ""
+    if not exe.exists():
+        return ""
+    try:
+        r = subprocess.run([str(exe), str(pid)], capture_output=True, text=True, timeout=5)
+        out.write_text(r.stdout + r.stderr)
+    except (OSError, subprocess.SubprocessError):
+        return ""
+    return f"; stacks in {out}"
 
 
 def _port_number(container: dict, port) -> int:
