@@ -86,7 +86,8 @@ def apply_main(argv: list[str]) -> int:
         signal.signal(s, on_signal)
     threading.Thread(target=_serve, args=(srv, c, stop), daemon=True).start()
     print(f"apply: {c.kind.lower()}/{c.name} x{c.desired}, service {c.service_url()} (state {state}; "
-          f"`python -m hola_amd oc --state-dir {state} get pods`)", flush=True)
+          f"`python -m hola_amd oc --state-dir {state} get pods`; connect-time DNAT to the endpoints: "
+          f"`hola_loadgen --endpoints-file {c.endpoints_file()} {c.service_url()}/api/hola`)", flush=True)
     try:
         while not stop.is_set():
             stop.wait(0.5)
