@@ -23,6 +23,8 @@
 #   busypoll [REPS]    the replica's busy-polling fixed / adaptive (auto) / off: saturated headline
 #                      and server CPU at light load (open-loop curve)
 #   uringchain         io_uring vs epoll on the chaining hop's four syscalls (bench/probes/uring_chain.cc)
+#   kubesoak [MIN] [ARGS]  config 5 soak: back-to-back rollouts of the 8 pods under one continuous
+#                      load (bench/kube_soak.py; ARGS e.g. --service proxy)
 #   kube [ARGS]        BASELINE config 5: deploy/openshift applied by the local executor at real
 #                      timings (8 pods, probes, rollouts under 512-connection load, SIGKILL,
 #                      ConfigMap edit; ARGS go to bench/kube_rollout.py)
@@ -74,6 +76,11 @@ busypoll)
   ;;
 kube)
   timeout -k 10 540 python -u bench/kube_rollout.py --out "$OUT/run" "$@" > "$OUT/kube.json" 2> "$OUT/kube.log"
+  ;;
+kubesoak)
+  MIN=${1:-6}; shift || true
+  timeout -k 10 $((MIN * 60 + 240)) python -u bench/kube_soak.py --minutes "$MIN" --out "$OUT/run" "$@" \
+    > "$OUT/soak.json" 2> "$OUT/soak.log"
   ;;
 repeat)
   # the default bench REPS times back to back: run-to-run spread of the headline on this host
