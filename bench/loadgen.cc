@@ -42,7 +42,6 @@
 #include <sys/prctl.h>
 #include <sys/eventfd.h>
 #include <sys/socket.h>
-#include <sys/stat.h>
 #include <signal.h>
 #include <unistd.h>
 
@@ -158,29 +157,31 @@ void signal_done() {
 struct Dnat {
   std::mutex mu;
   std::string path;
-  ino_t ino = 0;
-  off_t size = -1;
-  timespec mtime{};
+  std::string text;  // the file as last read
   std::vector<Target> all;
   std::map<std::string, int> ids;
   std::vector<int> current;
   uint64_t rr = 0;
 
+  // Read at every new connection and compared by content: a replacement (by rename) can keep
+  // the inode number, the size and the coarse mtime of the file before it.
   void reload_locked() {
-    struct stat st {};
-    if (stat(path.c_str(), &st) != 0) {
+    std::ifstream f(path);
+    if (!f) {
       current.clear();
+      text.clear();
       return;
     }
-    if (st.st_ino == ino && st.st_size == size && st.st_mtim.tv_sec == mtime.tv_sec &&
-        st.st_mtim.tv_nsec == mtime.tv_nsec)
-      return;
-    ino = st.st_ino;
-    size = st.st_size;
-    mtime = st.st_mtim;
-    std::ifstream f(path);
+    std::string now((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+    if (now == text) return;
+    text = now;
     std::vector<int> next;
-    for (std::string line; std::getline(f, line);) {
+    size_t at = 0;
+    while (at < now.size()) {
+      size_t eol = now.find('\n', at);
+      if (eol == std::string::npos) eol = now.size();
+      std::string line = now.substr(at, eol - at);
+      at = eol + 1;
       while (!line.empty() && isspace((unsigned char)line.back())) line.pop_back();
       if (line.empty() || line[0] == '#') continue;
       auto it = ids.find(line);

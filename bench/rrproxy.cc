@@ -131,30 +131,28 @@ void publish_set(std::vector<Backend*> list) {
   g_sets.push_back(std::move(set));
 }
 
-// Follows --endpoints-file: re-read when its inode, size or mtime changes (the writer
-// replaces it with a rename, so a reader never sees half a file).
+// Follows --endpoints-file. The writer replaces it with a rename, so a reader never sees half
+// a file; the file is read again every pass and compared by content, because a replacement
+// can keep the inode number (recycled), the size and the (coarse) mtime of the one before.
 void endpoints_loop(std::string path) {
-  struct stat last {};
+  std::string last;
   bool have = false;
   while (!g_stop.load()) {
-    struct stat st {};
-    if (stat(path.c_str(), &st) == 0 &&
-        (!have || st.st_ino != last.st_ino || st.st_size != last.st_size || st.st_mtim.tv_sec != last.st_mtim.tv_sec ||
-         st.st_mtim.tv_nsec != last.st_mtim.tv_nsec)) {
-      std::ifstream f(path);
+    std::ifstream f(path);
+    if (f) {
       std::string text((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
       std::vector<Backend*> list;
-      if (parse_backends(text, &list)) {
+      if ((!have || text != last) && parse_backends(text, &list)) {
         publish_set(std::move(list));
         fprintf(stderr, "rrproxy: endpoints now %zu backends\n", current_set().list.size());
-        last = st;
+        last = text;
         have = true;
         unsigned long long gen = 0;
         if (sscanf(text.c_str(), "# gen %llu", &gen) == 1) {
           const std::string tmp = path + ".applied.tmp";
-          if (FILE* f = fopen(tmp.c_str(), "w")) {
-            fprintf(f, "%llu\n", gen);
-            fclose(f);
+          if (FILE* out = fopen(tmp.c_str(), "w")) {
+            fprintf(out, "%llu\n", gen);
+            fclose(out);
             rename(tmp.c_str(), (path + ".applied").c_str());
           }
         }
