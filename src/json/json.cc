@@ -98,6 +98,19 @@ struct Parser {
     ++i;
     out->clear();
     while (i < s.size()) {
+      // the run of plain characters up to the next quote, escape or control character goes
+      // in with one append (aloha's greetings have no escapes)
+      size_t run = i;
+      while (run < s.size()) {
+        const unsigned char u = static_cast<unsigned char>(s[run]);
+        if (u == '"' || u == '\\' || u < 0x20) break;
+        ++run;
+      }
+      if (run != i) {
+        out->append(s.data() + i, run - i);
+        i = run;
+        if (i >= s.size()) break;
+      }
       char c = s[i++];
       if (c == '"') return true;
       if ((unsigned char)c < 0x20) return fail("control character in string");
