@@ -22,6 +22,7 @@ namespace hola::http {
 namespace {
 constexpr size_t kMaxBufferedOutput = 1 << 20;  // stop reading while this much is unsent
 constexpr int64_t kDrainIdleGraceMs = 100;       // see Server::shutdown
+constexpr int64_t kAnswerGraceMs = 1000;          // ditto: the least time a worker gets to answer
 constexpr int64_t kMaxBody = 1 << 20;           // request bodies are read and discarded
 
 const char* reason_phrase(int status) {
@@ -688,7 +689,11 @@ bool wait_answer(const Answer& a, std::chrono::steady_clock::time_point until) {
 void Server::shutdown(int drain_ms) {
   closing_.store(true);
   draining_.store(true);
-  auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(drain_ms);
+  const auto start = std::chrono::steady_clock::now();
+  const auto deadline = start + std::chrono::milliseconds(drain_ms);
+  // A healthy loop answers a posted task within microseconds; even with a zero drain budget
+  // each gets this long before it is given up on.
+  const auto answer_by = std::max(deadline, start + std::chrono::milliseconds(kAnswerGraceMs));
   for (auto& a : acceptors_) {
     Acceptor* ap = a.get();
     auto ans = std::make_shared<Answer>();
@@ -698,7 +703,7 @@ void Server::shutdown(int drain_ms) {
       ap->fd = -1;
       ans->done.store(true);
     });
-    if (!wait_answer(*ans, deadline)) LOG_WARN("drain: worker %d did not close its listener in time", ap->worker->index());
+    if (!wait_answer(*ans, answer_by)) LOG_WARN("drain: worker %d did not close its listener in time", ap->worker->index());
   }
   // Streaming connections close now, and kept-alive ones that have been idle for the grace
   // period; busy ones close after their current response (process() sets close_after_flush_
@@ -718,7 +723,7 @@ void Server::shutdown(int drain_ms) {
         ans->open.store(wp->open_connections());
         ans->done.store(true);
       });
-      if (!wait_answer(*ans, deadline)) {
+      if (!wait_answer(*ans, answer_by)) {
         LOG_WARN("drain: worker %d did not answer by the drain deadline", wp->index());
         answered = false;
         break;
