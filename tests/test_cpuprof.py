@@ -46,3 +46,24 @@ def test_loadgen_cpu_profile(hola, tmp_path):
         lg.close()
     text = prof.read_text()
     assert " hola-lg0\n" in text and " hola-lg1\n" in text and "\nstack " in text
+
+
+def test_fpstack_prints_every_thread_of_a_live_server(hola):
+    """`hola_fpstack PID` (the executor runs it on a pod that outlives its grace period): one
+    line per thread with its name and state, and return addresses inside the hola binary
+    (the worker threads wait in EventLoop::run)."""
+    from hola_amd import native
+
+    s = hola(threads=2)
+    out = subprocess.run([str(native.binary("hola_fpstack", build_if_missing=False)), str(s.proc.pid)],
+                         capture_output=True, text=True, timeout=30).stdout
+    lines = out.splitlines()
+    names = {ln.split()[1] for ln in lines}
+    assert {"hola", "hola-log", "hola-w0", "hola-w1"} <= names, out
+    tasks = list(Path(f"/proc/{s.proc.pid}/task").iterdir())
+    assert len(lines) == len(tasks), out
+    w0 = next(ln for ln in lines if ln.split()[1] == "hola-w0")
+    if "seize:" not in w0:  # ptrace may be restricted (yama ptrace_scope) where this runs
+        assert "hola+0x" in w0, w0
+    assert s.proc.poll() is None  # detached, still serving
+    assert s.get("/api/health")[0] == 200
