@@ -164,6 +164,7 @@ def main() -> int:
         c.wait(lambda: sorted(set(greetings(c, 16 * a.replicas))) == want, 600, "ConfigMap edit on every pod")
         res["configmap_edit_all_pods_s"] = round(time.monotonic() - t_cm, 2)
         res["restarts_total"] = sum(p["restarts"] for p in c.get_pods())
+        res["grace_kills"] = sum(1 for e in c.events if e[2] == "Killed")  # pods SIGKILLed at the grace period
         log(f"ConfigMap edit on all pods after {res['configmap_edit_all_pods_s']} s")
     finally:
         c.close(grace_s=10)
