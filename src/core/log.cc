@@ -196,9 +196,21 @@ size_t Logger::drain(std::string* out) {
     uint64_t t = r->tail.load(std::memory_order_relaxed);
     const uint64_t h = r->head.load(std::memory_order_acquire);
     if (t == h) continue;
+    if (t > h) {  // cannot happen either; resynchronise instead of reporting a non-empty ring forever
+      dropped_.fetch_add(1, std::memory_order_relaxed);
+      r->tail.store(h, std::memory_order_release);
+      continue;
+    }
     while (t < h) {
       uint32_t len;
       r->get(t, &len, sizeof len);
+      if (len > Ring::kSize || h - t < sizeof len + len || h - t > Ring::kSize) {
+        // Cannot happen with one producer per ring. Should it anyway, the rest of the ring
+        // is dropped (and counted) rather than read past its head or spun on forever.
+        dropped_.fetch_add(1, std::memory_order_relaxed);
+        t = h;
+        break;
+      }
       const size_t old = out->size();
       out->resize(old + len);
       r->get(t + sizeof len, &(*out)[old], len);
