@@ -7,6 +7,7 @@
 //   /hystrix.stream             (HystrixServlet.java)
 //   HTTP server on :8080        (Dockerfile:8, pom.xml:74)
 // SIGTERM/SIGINT/SIGHUP: stop accepting, drain in-flight requests, flush spans, exit 0.
+#include <errno.h>
 #include <signal.h>
 #include <unistd.h>
 
@@ -24,6 +25,7 @@
 #include "config/manager.h"
 #include "config/resolver.h"
 #include "core/affinity.h"
+#include "core/clock.h"
 #include "core/cpuprof.h"
 #include "core/log.h"
 #include "core/net.h"
@@ -429,9 +431,20 @@ int main(int argc, char** argv) {
     server.begin_termination();  // before the log line: the line says it has happened
     LOG_INFO("received %s: readiness failing, still serving for %d ms", sig_name, shutdown_delay_ms);
     Logger::instance().flush();
-    timespec ts{shutdown_delay_ms / 1000, long(shutdown_delay_ms % 1000) * 1000000L};
-    siginfo_t si;
-    if (sigtimedwait(&sigs, &si, &ts) > 0) LOG_INFO("second termination signal: ending the delay early");
+    // sigtimedwait returns early with EINTR when the thread is stopped and resumed (SIGSTOP /
+    // SIGCONT, a ptrace attach such as the executor's stack sampler): wait out the rest.
+    const int64_t until = mono_ns() + int64_t(shutdown_delay_ms) * 1000000;
+    for (;;) {
+      const int64_t left = until - mono_ns();
+      if (left <= 0) break;
+      timespec ts{time_t(left / 1000000000), long(left % 1000000000)};
+      siginfo_t si;
+      if (sigtimedwait(&sigs, &si, &ts) > 0) {
+        LOG_INFO("second termination signal: ending the delay early");
+        break;
+      }
+      if (errno != EINTR) break;  // EAGAIN: the delay is over
+    }
   }
   LOG_INFO("received %s: draining (up to %d ms)", sig_name, drain_ms);
   server.shutdown(drain_ms);

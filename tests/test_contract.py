@@ -611,6 +611,28 @@ def test_second_signal_ends_the_shutdown_delay(hola):
     assert "ending the delay early" in s.log()
 
 
+def test_stop_and_continue_do_not_cut_the_shutdown_delay(hola):
+    """SIGSTOP/SIGCONT (or a ptrace attach, such as the executor's stack sampler) interrupts
+    the delay's sigtimedwait with EINTR; the replica waits out the rest of the delay instead of
+    draining at once (it did, before)."""
+    import signal
+
+    s = hola(args=["--shutdown-delay-ms", "1500"])
+    t0 = time.monotonic()
+    s.proc.send_signal(signal.SIGTERM)
+    deadline = time.monotonic() + 5
+    while "readiness failing" not in s.log() and time.monotonic() < deadline:
+        time.sleep(0.01)
+    s.proc.send_signal(signal.SIGSTOP)
+    time.sleep(0.1)
+    s.proc.send_signal(signal.SIGCONT)
+    time.sleep(0.5)
+    assert s.proc.poll() is None, s.log()[-2000:]
+    assert s.proc.wait(timeout=10) == 0
+    assert time.monotonic() - t0 >= 1.4
+    assert "ending the delay early" not in s.log()
+
+
 def test_exit_deadline_ends_a_termination_that_runs_too_long(hola):
     """The exit watchdog: a termination still running --exit-deadline-ms after the signal (here
     a 30 s shutdown delay against a 1 s deadline) ends with status 3 and a line saying so,
