@@ -4,6 +4,7 @@ restarts, graceful shutdown."""
 import json
 import os
 import signal
+import socket
 import subprocess
 import threading
 import time
@@ -301,3 +302,54 @@ def test_proxy_backs_off_at_fd_limit():
 def test_server_backs_off_at_fd_limit(hola):
     s = hola(env={"HOSTNAME": "h"}, threads=1)
     _exhaust_fds_then_recover(s.proc.pid, s.port, 48)
+
+
+def test_loadgen_service_mode_dnats_each_new_connection(tmp_path, hola):
+    """`hola_loadgen --endpoints-file F` (the Service's iptables/IPVS semantics in the client):
+    each new connection goes to a current endpoint of F, established ones keep their pod when
+    F changes, bodies are checked per pod, and a connect refused by a listed endpoint that is
+    gone counts as an error (no failover)."""
+    from hola_amd import native
+
+    a = hola(env={"HOSTNAME": "a"}, threads=1)
+    b = hola(env={"HOSTNAME": "b"}, threads=1)
+    eps = tmp_path / "eps"
+
+    def publish(*ports):
+        tmp = tmp_path / "eps.tmp"
+        tmp.write_text("# gen\n" + "".join(f"127.0.0.1:{p}\n" for p in ports))
+        os.replace(tmp, eps)
+
+    def run(seconds, conns, *extra):
+        r = subprocess.run([str(native.binary("hola_loadgen")), "-t", "2", "-c", str(conns), "-d", f"{seconds}s",
+                            "--json", "--verify-body", "--endpoints-file", str(eps), *extra,
+                            "http://127.0.0.2:9/api/hola"],
+                           capture_output=True, text=True, timeout=60)
+        assert r.returncode == 0, r.stderr
+        return json.loads(r.stdout.strip().splitlines()[-1])
+
+    publish(a.port, b.port)
+    r = run(1, 8)
+    lat = r["latency"]
+    assert r["targets"] == 2 and lat["errors"] == 0 and lat["body_mismatch"] == 0
+    assert lat["body_checked"] == lat["count"] > 100
+    # a listed endpoint that refuses: each refused (re)connect is an error, the other endpoint
+    # still serves (every request on its own connection here, so connects keep happening)
+    gone = socket.socket()
+    gone.bind(("127.0.0.1", 0))
+    dead_port = gone.getsockname()[1]
+    gone.close()
+    publish(a.port, dead_port)
+    r = run(1, 4, "-H", "Connection: close")
+    assert r["latency"]["errors"] > 0 and r["latency"]["count"] > 100, r
+    assert r["latency"]["reconnects"] > 100 and r["latency"]["body_mismatch"] == 0
+    # established connections keep their pod: the file changes under a running load
+    publish(a.port)
+    lg = subprocess.Popen([str(native.binary("hola_loadgen")), "-t", "1", "-c", "4", "-d", "3s", "--json",
+                           "--verify-body", "--endpoints-file", str(eps), "http://127.0.0.2:9/api/hola"],
+                          stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    time.sleep(1.0)
+    publish(b.port)
+    out, err = lg.communicate(timeout=30)
+    r = json.loads(out.strip().splitlines()[-1])
+    assert r["targets"] == 1 and r["latency"]["errors"] == 0, r  # never reconnected, never saw b
