@@ -132,7 +132,15 @@ def qos_class(container: dict) -> str:
     if not lim and not req:
         return "BestEffort"
     req = {**lim, **req}
-    if lim and all(k in lim for k in ("cpu", "memory")) and all(str(req.get(k)) == str(lim.get(k)) for k in lim):
+
+    def same(k):  # quantities compare by value: cpu "2" == 2 == "2000m", memory "1Gi" == "1024Mi"
+        parse = parse_cpu if k == "cpu" else parse_memory if k == "memory" else str
+        try:
+            return parse(req.get(k)) == parse(lim.get(k))
+        except (TypeError, ValueError):
+            return str(req.get(k)) == str(lim.get(k))
+
+    if lim and all(k in lim for k in ("cpu", "memory")) and all(same(k) for k in lim):
         return "Guaranteed"
     return "Burstable"
 

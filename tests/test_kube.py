@@ -87,6 +87,11 @@ def test_quantities_and_qos():
     assert m.qos_class(dc["spec"]["template"]["spec"]["containers"][0]) == "Guaranteed"
     assert m.qos_class({"resources": {"requests": {"cpu": "1"}}}) == "Burstable"
     assert m.qos_class({}) == "BestEffort"
+    # quantities compare by value, not by spelling
+    assert m.qos_class({"resources": {"limits": {"cpu": "2", "memory": "1Gi"},
+                                      "requests": {"cpu": "2000m", "memory": "1024Mi"}}}) == "Guaranteed"
+    assert m.qos_class({"resources": {"limits": {"cpu": 2, "memory": "1Gi"},
+                                      "requests": {"cpu": "1", "memory": "1Gi"}}}) == "Burstable"
 
 
 def test_image_is_read_from_the_dockerfile():
