@@ -196,6 +196,77 @@ def test_sanitized_proxy(preset, tmp_path):
     assert len(errors) <= 12, errors[:5]
 
 
+@pytest.mark.parametrize("preset", ["tsan", "asan"])
+def test_sanitized_proxy_endpoints_mode(preset, tmp_path):
+    """hola_rrproxy in the executor's Service mode (--endpoints-file, no failover) built with a
+    sanitizer: keep-alive sessions through it while the endpoints file is replaced again and
+    again (the follower thread publishing new backend sets under the session loops), then
+    SIGTERM with sessions open."""
+    import subprocess
+
+    from hola_amd.parallel.replicas import ReplicaSet
+
+    build(preset)
+    exe = build_dir(preset) / "hola_rrproxy"
+    port_file = tmp_path / "port"
+    eps = tmp_path / "eps"
+    log_path = tmp_path / "proxy.log"
+    with ReplicaSet(3, threads_per_replica=1, supervise=False) as rs, open(log_path, "wb") as log:
+        targets = [f"{h}:{p}" for h, p in rs.targets]
+
+        def publish(gen, chosen):
+            tmp = tmp_path / "eps.tmp"
+            tmp.write_text(f"# gen {gen}\n" + "".join(t + "\n" for t in chosen))
+            os.replace(tmp, eps)
+
+        publish(1, targets)
+        cmd = (tsan_wrapper() if preset == "tsan" else []) + [
+            str(exe), "--host", "127.0.0.1", "--port", "0", "--threads", "3", "--endpoints-file", str(eps),
+            "--health-ms", "0", "--no-failover", "--idle-timeout-ms", "0", "--port-file", str(port_file)]
+        proc = subprocess.Popen(cmd, stderr=log, env={**os.environ, **SAN_ENV[preset]})
+        deadline = time.monotonic() + 60
+        while not port_file.exists() and time.monotonic() < deadline and proc.poll() is None:
+            time.sleep(0.02)
+        assert port_file.exists(), log_path.read_text(errors="replace")[-3000:]
+        port = int(port_file.read_text())
+        errors = []
+        stop = threading.Event()
+
+        def client():
+            while not stop.is_set():
+                try:
+                    with socket.create_connection(("127.0.0.1", port), timeout=10) as sk:
+                        for _ in range(20):
+                            sk.sendall(b"GET /api/hola HTTP/1.1\r\nHost: x\r\n\r\n")
+                            data = sk.recv(1 << 16)
+                            if b"200 OK" not in data:
+                                errors.append(data[:100])
+                                break
+                except OSError as e:
+                    errors.append(repr(e))
+
+        ts = [threading.Thread(target=client) for _ in range(4)]
+        for t in ts:
+            t.start()
+        for gen in range(2, 40):  # every backend stays up: sets change, no connection may fail
+            publish(gen, targets[gen % 3:] + targets[:gen % 3][:1])
+            time.sleep(0.03)
+        stop.set()
+        for t in ts:
+            t.join()
+        applied = (tmp_path / "eps.applied").read_text().strip()
+        idle = socket.create_connection(("127.0.0.1", port), timeout=10)
+        time.sleep(0.1)
+        proc.send_signal(signal.SIGTERM)
+        rc = proc.wait(timeout=60)
+        idle.close()
+    text = log_path.read_text(errors="replace")
+    assert "Sanitizer" not in text and "runtime error" not in text, text[-6000:]
+    assert rc == 0, (rc, text[-3000:])
+    assert not errors, errors[:5]
+    assert int(applied) >= 30  # the follower acknowledged the sets as they came
+
+
 @pytest.mark.parametrize("preset", ["asan", "tsan"])
 def test_shutdown_with_parked_calls_and_streams_frees_everything(preset, tmp_path):
     """SIGTERM while a chaining call is parked on a slow aloha (past a short drain), an SSE
