@@ -647,6 +647,43 @@ def test_exit_deadline_ends_a_termination_that_runs_too_long(hola):
     assert "termination did not complete within 1000 ms; exiting" in s.log()
 
 
+def test_a_stuck_worker_cannot_hold_the_termination_forever(hola):
+    """One worker thread held stopped (ptrace) stands for a worker stuck in its loop: the drain
+    stops waiting for its answer (a warning names it), and the exit watchdog ends the process
+    with status 3 at --exit-deadline-ms instead of hanging until a SIGKILL."""
+    import ctypes
+    import signal
+
+    s = hola(args=["--drain-ms", "300", "--exit-deadline-ms", "3000"], threads=2)
+    libc = ctypes.CDLL(None, use_errno=True)
+    libc.ptrace.argtypes = [ctypes.c_long, ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p]
+    PTRACE_SEIZE, PTRACE_INTERRUPT, WALL = 0x4206, 0x4207, 0x40000000
+    tid = next(int(t.name) for t in Path(f"/proc/{s.proc.pid}/task").iterdir()
+               if (t / "comm").read_text().strip() == "hola-w1")
+    if libc.ptrace(PTRACE_SEIZE, tid, None, None) != 0:
+        pytest.skip(f"ptrace not permitted here (errno {ctypes.get_errno()})")
+    libc.ptrace(PTRACE_INTERRUPT, tid, None, None)
+    os.waitpid(tid, WALL)  # hola-w1 is stopped now
+    t0 = time.monotonic()
+    s.proc.send_signal(signal.SIGTERM)
+    # this process traces hola-w1, so it must reap that thread's exit itself, or the replica's
+    # own exit status never reaches its parent (this process too)
+    rc = None
+    while rc is None and time.monotonic() - t0 < 20:
+        try:
+            os.waitpid(tid, os.WNOHANG | WALL)
+        except ChildProcessError:
+            pass
+        rc = s.proc.poll()
+        time.sleep(0.02)
+    took = time.monotonic() - t0
+    log = s.log()
+    assert rc == 3, (rc, log[-2000:])
+    assert 2.5 <= took < 10
+    assert "drain: worker 1 did not answer by the drain deadline" in log
+    assert "termination did not complete within 3000 ms; exiting" in log
+
+
 def test_default_exit_deadline_leaves_a_normal_termination_alone(hola):
     s = hola(args=["--shutdown-delay-ms", "200", "--drain-ms", "300"])
     import signal
