@@ -86,7 +86,7 @@ void usage() {
           "  --exit-deadline-ms N     a termination still running N ms after the signal exits with status 3\n"
           "                           (default: shutdown delay + drain budget + 10000; 0 = never)\n"
           "  --port-file PATH         write the bound port here once listening\n"
-          "  --busy-poll-us N|auto[:N] spin up to N us in epoll before sleeping (default 0); auto = adaptive:\n"
+          "  --busy-poll-us N|auto[:N] spin up to N us in epoll before sleeping (default auto; 0 = off); auto = adaptive:\n"
           "                           spin (20 us, or N) while spinning mostly finds work (saturation),\n"
           "                           back off while it mostly waits in vain (light load)\n"
           "  --busy-poll-pause N      PAUSE instructions between empty polls (SMT-friendly spin)\n"
@@ -124,6 +124,11 @@ constexpr int64_t kExitMarginMs = 10000;
 
 int main(int argc, char** argv) {
   http::ServerOptions so;
+  // Adaptive busy-polling by default: the same saturation throughput as a fixed spin, less CPU
+  // than no spinning at light load, and a microsecond p99 (profiles/round3/08_busypoll);
+  // `--busy-poll-us 0` turns it off.
+  so.busy_poll_auto = true;
+  so.busy_poll_us = kAutoBusyPollUs;
   std::map<std::string, std::string> sysprops;
   const char* jo = getenv("JAVA_OPTIONS");
   if (jo) sysprops = config::parse_java_options(jo);  // `oc env dc/hola JAVA_OPTIONS=-Dconf=...`
