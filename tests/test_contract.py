@@ -669,13 +669,17 @@ def test_a_stuck_worker_cannot_hold_the_termination_forever(hola):
     # this process traces hola-w1, so it must reap that thread's exit itself, or the replica's
     # own exit status never reaches its parent (this process too)
     rc = None
-    while rc is None and time.monotonic() - t0 < 20:
-        try:
-            os.waitpid(tid, os.WNOHANG | WALL)
-        except ChildProcessError:
-            pass
-        rc = s.proc.poll()
-        time.sleep(0.02)
+    try:
+        while rc is None and time.monotonic() - t0 < 20:
+            try:
+                os.waitpid(tid, os.WNOHANG | WALL)
+            except ChildProcessError:
+                pass
+            rc = s.proc.poll()
+            time.sleep(0.02)
+    finally:
+        if rc is None:  # let the thread go, so the fixture's teardown can stop the replica
+            libc.ptrace(17, tid, None, None)  # PTRACE_DETACH
     took = time.monotonic() - t0
     log = s.log()
     assert rc == 3, (rc, log[-2000:])
