@@ -56,6 +56,10 @@ def main() -> int:
     ap.add_argument("--time-scale", type=float, default=1.0)
     ap.add_argument("--connections", type=int, default=512)
     ap.add_argument("--loadgen-threads", type=int, default=4)
+    ap.add_argument("--shutdown-delay-ms", type=int, default=None,
+                    help="patch the pods' --shutdown-delay-ms before the soak (0 = the pre-round-3 "
+                         "termination: drain at once; the rollouts then drop connections, and the run "
+                         "hunts for drains that do not finish instead)")
     a = ap.parse_args()
     out = Path(a.out)
     if out.exists():
@@ -71,6 +75,13 @@ def main() -> int:
     lg = None
     try:
         c.wait_ready(a.replicas, timeout=300)
+        if a.shutdown_delay_ms is not None:
+            rev = c.rollout_status()["revision"]
+            c.patch({"spec": {"template": {"spec": {"containers": [{"name": "hola", "args": [
+                "--shutdown-delay-ms", str(a.shutdown_delay_ms), "--busy-poll-us", "auto"]}]}}}})
+            c.wait(lambda: c.rollout_status()["revision"] > rev and c.rollout_status()["complete"], 600, "patch")
+            c.wait(lambda: all(p["status"] != "Terminating" for p in c.get_pods()), 120, "old pods gone")
+            res["shutdown_delay_ms"] = a.shutdown_delay_ms
         extra = ["--verify-body", "--endpoints-file", str(c.endpoints_file())] if a.service == "dnat" else []
         lg = subprocess.Popen([str(native.binary("hola_loadgen")), "-t", str(a.loadgen_threads), "-c",
                                str(a.connections), "-d", "86400s", "--json", *extra, c.service_url() + "/api/hola"],
@@ -112,6 +123,9 @@ def main() -> int:
             "executor_fds": [fds0] + [x["executor_fds"] for x in rollouts],
             "executor_threads": [th0] + [x["executor_threads"] for x in rollouts],
             "restarts_total": sum(p["restarts"] for p in c.get_pods()),
+            # terminations that did not finish on their own: the drain's stall reports and the
+            # exit watchdog's (status 3), each with the worker's activity record and stack
+            **_stalls(c, out),
         })
         lg = None
     finally:
@@ -123,6 +137,19 @@ def main() -> int:
     print(json.dumps(res), flush=True)
     (out / "result.json").write_text(json.dumps(res, indent=1) + "\n")
     return 0
+
+
+def _stalls(c: Cluster, out: Path) -> dict:
+    stalled = []
+    for log_path in sorted((c.state / "pods").glob("*/container.log")):
+        text = log_path.read_text(errors="replace")
+        if "did not answer" in text or "termination did not complete" in text:
+            stalled.append(log_path.parent.name)
+            dst = out / "stalls"
+            dst.mkdir(exist_ok=True)
+            shutil.copy(log_path, dst / f"{log_path.parent.name}.log")
+    watchdog = [e for e in c.events if e[2] == "Deleted" and "exit 3 " in e[3]]
+    return {"stalled_pods": stalled, "watchdog_exits": len(watchdog)}
 
 
 if __name__ == "__main__":

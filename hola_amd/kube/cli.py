@@ -55,7 +55,10 @@ def apply_main(argv: list[str]) -> int:
     ap.add_argument("--configmap-sync-s", type=float, default=60.0, help="kubelet's ConfigMap volume sync period")
     ap.add_argument("--service-host", default="127.0.0.1", help="address of the LoadBalancer Service")
     ap.add_argument("--service-port", type=int, default=None, help="default: the Service's port (8080)")
-    ap.add_argument("--proxy-threads", type=int, default=2)
+    ap.add_argument("--proxy-threads", type=int, default=0,
+                    help="threads of the userspace Service proxy (0 = a quarter of the node's CPUs, 2..16); "
+                         "for load tests read the endpoints file and DNAT at connect time instead "
+                         "(hola_loadgen --endpoints-file: no proxy hop, docs/OPERATIONS.md)")
     ap.add_argument("--no-zipkin", action="store_true", help="no stand-in collector for zipkin-query:9411")
     a = ap.parse_args(argv)
     state = Path(a.state_dir)

@@ -51,7 +51,7 @@ from pathlib import Path
 from hola_amd import native
 from hola_amd.kube import manifests as m
 from hola_amd.kube.image import Image
-from hola_amd.kube.kubelet import Kubelet, Pod, project_configmap
+from hola_amd.kube.kubelet import Kubelet, Pod, die_with_parent, project_configmap
 
 TICK_S = 0.02
 
@@ -72,7 +72,7 @@ class Cluster:
                  replicas: int | None = None, node_cpus: float | None = None, reserved_cpus: int = 1,
                  cpu_manager_policy: str = "none", time_scale: float = 1.0, endpoint_sync_s: float = 1.0,
                  configmap_sync_s: float = 60.0, service_host: str = "127.0.0.1", service_port: int | None = None,
-                 zipkin: bool = True, proxy_threads: int = 2, proxy_cpus: str | None = None,
+                 zipkin: bool = True, proxy_threads: int = 0, proxy_cpus: str | None = None,
                  namespace: str = "myproject", dockerfile: str | Path | None = None):
         if cpu_manager_policy not in ("none", "static"):
             raise ValueError("cpu_manager_policy is 'none' or 'static'")
@@ -89,7 +89,11 @@ class Cluster:
         self.node_cpus = float(node_cpus) if node_cpus else float(len(self.real_cpus))
         self.reserved = list(self.real_cpus[:reserved_cpus]) if reserved_cpus else []
         self.allocatable = self.node_cpus - len(self.reserved)
-        self.proxy_threads, self.proxy_cpus = proxy_threads, proxy_cpus
+        # The userspace Service proxy carries every request twice (in and out), so a fixed 2
+        # threads capped a rollout under load at ~160 k req/s (profiles/round3/13_kube): by
+        # default it gets a quarter of the node's CPUs, 2 to 16 threads.
+        self.proxy_threads = proxy_threads or max(2, min(16, len(self.real_cpus) // 4))
+        self.proxy_cpus = proxy_cpus
         self.service_host, self.service_port_override = service_host, service_port
         self.want_zipkin = zipkin
         self.image = Image.from_dockerfile(dockerfile) if dockerfile else Image.from_dockerfile()
@@ -146,6 +150,7 @@ class Cluster:
         self.service_ports: dict[str, tuple[str, int]] = {}
         self._stop = threading.Event()
         self._thread: threading.Thread | None = None
+        self.ticks = 0  # control-loop passes (a stalled loop shows as a count that stops)
 
     def _claim_network(self):
         """Takes a free 127.<a>.0.0/16 for this cluster's pods and stand-in Services: every pod
@@ -232,7 +237,8 @@ class Cluster:
             pf = self.state / "zipkin.port"
             self._logs.append(open(self.state / "zipkin.log", "ab"))
             self.sink = subprocess.Popen([str(native.binary("hola_zipkin_sink")), "--host", ip, "--port", "9411",
-                                          "--port-file", str(pf)], stdout=subprocess.DEVNULL, stderr=self._logs[-1])
+                                          "--port-file", str(pf)], stdout=subprocess.DEVNULL, stderr=self._logs[-1],
+                                         preexec_fn=die_with_parent)
             self.service_ports["zipkin-query"] = (ip, self._wait_port(pf, self.sink))
         for name, svc in self.services.items():
             port = svc["spec"]["ports"][0]
@@ -246,7 +252,7 @@ class Cluster:
             if self.proxy_cpus:
                 cmd += ["--cpu-list", self.proxy_cpus]
             self._logs.append(open(self.state / f"service-{name}.log", "ab"))
-            proxy = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=self._logs[-1])
+            proxy = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=self._logs[-1], preexec_fn=die_with_parent)
             self.proxies.append(proxy)
             self.service_ports[name] = (self.service_host, self._wait_port(pf, proxy))
             self.event(f"service/{name}", "Listening",
@@ -514,6 +520,7 @@ class Cluster:
                         self.pods.pop(name)
                 except Exception as e:  # noqa: BLE001 - keep the control plane running, record why
                     self.event("control-loop", "Error", repr(e))
+                self.ticks += 1
             self._stop.wait(TICK_S)
 
     # ------------------------------------------------------------------ the `oc` surface

@@ -28,6 +28,7 @@ cluster's `time_scale` so tests can run the same state machine faster; deadlines
 """
 from __future__ import annotations
 
+import ctypes
 import http.client
 import os
 import re
@@ -44,6 +45,9 @@ PROBE_DEFAULTS = {"initialDelaySeconds": 0, "periodSeconds": 10, "timeoutSeconds
 BACKOFF_INITIAL_S, BACKOFF_MAX_S, BACKOFF_RESET_S = 10.0, 300.0, 600.0
 DEFAULT_GRACE_S = 30.0
 MEM_CHECK_S = 0.2
+KILL_CAPTURE_S = 6.0  # the grace-expiry capture's limit (hola_fpstack gets 5 s) before a plain SIGKILL
+# resolved in the parent: a forked child of this multi-threaded process only calls it
+_PRCTL = ctypes.CDLL(None, use_errno=True).prctl
 
 
 def project_configmap(vol_dir: Path, data: dict[str, str], items: list[dict] | None = None) -> None:
@@ -129,6 +133,7 @@ class Pod:
     prestop_http: Future | None = None
     term_sent: bool = False
     kill_sent: bool = False
+    kill_future: Future | None = None  # grace-expiry capture + SIGKILL, in the diagnostics thread
     gone: bool = False
 
     @property
@@ -169,6 +174,8 @@ class Kubelet:
     def __init__(self, cluster, probe_workers: int = 16):
         self.cluster = cluster
         self.pool = ThreadPoolExecutor(max_workers=probe_workers, thread_name_prefix="kube-probe")
+        # grace-expiry captures + SIGKILLs, off the control loop and off the probes' pool
+        self.diag = ThreadPoolExecutor(max_workers=4, thread_name_prefix="kube-diag")
 
     # ------------------------------------------------------------------ container start
     def _probe_spec(self, pod: Pod) -> dict | None:
@@ -265,8 +272,7 @@ class Kubelet:
         log.flush()
         try:
             pod.proc = subprocess.Popen(argv, env=env, cwd=workdir, stdout=log, stderr=log,
-                                        preexec_fn=(lambda: os.sched_setaffinity(0, cpus)) if cpus else None,
-                                        start_new_session=True)
+                                        preexec_fn=lambda: die_with_parent(cpus), start_new_session=True)
         except OSError as e:
             # CreateContainerError / RunContainerError: retried with the restart back-off
             log.write(f"--- cannot start the container: {e}\n".encode())
@@ -384,7 +390,8 @@ class Kubelet:
         if pod.running and "exec" in pre:
             cmd = [self.map_paths(pod, a) for a in pre["exec"]["command"]]
             pod.prestop = subprocess.Popen(cmd, env=self._env(pod), stdout=subprocess.DEVNULL,
-                                           stderr=subprocess.DEVNULL, start_new_session=True)
+                                           stderr=subprocess.DEVNULL, start_new_session=True,
+                                           preexec_fn=die_with_parent)
         elif pod.running and "httpGet" in pre:  # off the control loop, like the probes
             hg = pre["httpGet"]
             pod.prestop_http = self.pool.submit(http_probe, pod.ip, _port_number(pod.container, hg.get("port", 8080)),
@@ -392,6 +399,18 @@ class Kubelet:
         self.cluster.event(pod.name, "Killing", f"grace {pod.grace_deadline - now:.0f}s")
 
     def _tick_terminating(self, pod: Pod, now: float) -> None:
+        kf = pod.kill_future
+        if kf is not None:
+            if not kf.done():
+                if now >= pod.grace_deadline + KILL_CAPTURE_S:  # the capture is stuck: kill anyway
+                    pod.proc.kill()
+                if pod.running or now < pod.grace_deadline + KILL_CAPTURE_S:
+                    return  # "Killed" comes before "Deleted"
+                note = "capture did not finish"
+            else:
+                note = kf.result()
+            pod.kill_future = None
+            self.cluster.event(pod.name, "Killed", f"grace period expired: SIGKILL ({note})")
         if not pod.running:
             pod.gone = True
             if pod.prestop and pod.prestop.poll() is None:
@@ -405,11 +424,22 @@ class Kubelet:
             pod.proc.send_signal(signal.SIGTERM)
             pod.term_sent = True
         if now >= pod.grace_deadline and not pod.kill_sent:
-            threads = _thread_states(pod.proc.pid)  # what it was doing when the grace ran out
-            stacks = _fpstack(pod.proc.pid, pod.dir / "fpstack.txt")
-            pod.proc.kill()  # once: the next tick sees the exit
+            # What it was doing when the grace ran out (thread states, user-space stacks), then
+            # the SIGKILL: in the diagnostics thread, so a slow capture (ptrace of every thread)
+            # never holds the control loop, whose other pods' probes, endpoint syncs and rollout
+            # steps go on meanwhile. The next ticks see the exit.
             pod.kill_sent = True
-            self.cluster.event(pod.name, "Killed", f"grace period expired: SIGKILL (threads: {threads}{stacks})")
+            pod.kill_future = self.diag.submit(self.capture_and_kill, pod.proc, pod.dir / "fpstack.txt")
+
+    def capture_and_kill(self, proc: subprocess.Popen, stacks_out: Path) -> str:
+        """Diagnostics thread: thread states and stacks of a container whose grace period ran
+        out, then its SIGKILL; returns the note for the `Killed` event."""
+        try:
+            threads = _thread_states(proc.pid)
+            stacks = _fpstack(proc.pid, stacks_out)
+        finally:
+            proc.kill()
+        return f"threads: {threads}{stacks}"
 
     def kill_container(self, pod: Pod, sig: int = signal.SIGKILL) -> None:
         if pod.running:
@@ -417,6 +447,17 @@ class Kubelet:
 
     def shutdown(self) -> None:
         self.pool.shutdown(wait=False, cancel_futures=True)
+        self.diag.shutdown(wait=False, cancel_futures=True)
+
+
+def die_with_parent(cpus: list[int] | None = None) -> None:
+    """preexec_fn of every process the executor starts: the kernel SIGKILLs it when the thread
+    that started it (the control loop) ends, so an executor that dies, or a test process cut
+    off before its teardown, leaves no pods behind (a pod keeps its own session, so a signal to
+    the executor's process group would not reach it). Optionally applies the cpuset."""
+    _PRCTL(1, int(signal.SIGKILL), 0, 0, 0)  # PR_SET_PDEATHSIG
+    if cpus:
+        os.sched_setaffinity(0, cpus)
 
 
 def _thread_states(pid: int) -> str:

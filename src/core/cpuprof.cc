@@ -10,6 +10,9 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <string>
+#include <thread>
 #include <cstdint>
 #include <cstdio>
 #include <fstream>
@@ -76,9 +79,43 @@ void load_exec_ranges() {
 // Async-signal-safe: walks the interrupted thread's frame-pointer chain from the ucontext's
 // RBP (the native code is built with -fno-omit-frame-pointer), reading only inside the
 // thread's own stack and stopping at the first address that is not code. No unwinder, no
-// locks, no allocation. When the sample lands in code from another object (libc's syscall
+// locks, no allocation. When the context is in code from another object (libc's syscall
 // wrappers: send, recv, epoll_wait), which keeps no frame pointer, the caller is found by
 // scanning the top of the stack for the first return address into a different mapping.
+int walk(const ucontext_t* uc, uintptr_t* out, int max) {
+  const uintptr_t pc = uintptr_t(uc->uc_mcontext.gregs[REG_RIP]);
+  const uintptr_t sp = uintptr_t(uc->uc_mcontext.gregs[REG_RSP]);
+  uintptr_t fp = uintptr_t(uc->uc_mcontext.gregs[REG_RBP]);
+  int depth = 0;
+  out[depth++] = pc;
+  const bool bounded = t_stack_hi > t_stack_lo;
+  auto in_stack = [&](uintptr_t a) { return bounded && a >= t_stack_lo && a + 16 <= t_stack_hi && !(a & 7); };
+  const int pc_range = exec_range(pc);
+  uintptr_t caller = 0;
+  if (pc_range != g_own_range) {
+    for (int k = 0; k < 16 && depth < max && in_stack(sp + 8 * uintptr_t(k)); ++k) {
+      const uintptr_t w = *reinterpret_cast<const uintptr_t*>(sp + 8 * uintptr_t(k));
+      const int r = exec_range(w);
+      if (r >= 0 && r != pc_range) {
+        caller = w;
+        out[depth++] = w;
+        break;
+      }
+    }
+  }
+  bool first = true;
+  while (depth < max && in_stack(fp)) {
+    const uintptr_t ret = *reinterpret_cast<const uintptr_t*>(fp + 8);
+    const uintptr_t next = *reinterpret_cast<const uintptr_t*>(fp);
+    if (!executable(ret)) break;
+    if (!(first && ret == caller)) out[depth++] = ret;
+    first = false;
+    if (next <= fp) break;  // the chain must climb the stack
+    fp = next;
+  }
+  return depth;
+}
+
 void on_prof(int, siginfo_t*, void* ucv) {
   if (!g_on.load(std::memory_order_relaxed) || t_index < 0) return;
   const size_t i = g_next.fetch_add(1, std::memory_order_relaxed);
@@ -86,37 +123,23 @@ void on_prof(int, siginfo_t*, void* ucv) {
   const int saved_errno = errno;
   Sample& s = g_samples[i];
   s.thread = uint16_t(t_index);
-  const auto* uc = static_cast<const ucontext_t*>(ucv);
-  const uintptr_t pc = uintptr_t(uc->uc_mcontext.gregs[REG_RIP]);
-  const uintptr_t sp = uintptr_t(uc->uc_mcontext.gregs[REG_RSP]);
-  uintptr_t fp = uintptr_t(uc->uc_mcontext.gregs[REG_RBP]);
-  s.pc[0] = pc;
-  s.depth = 1;
-  const bool bounded = t_stack_hi > t_stack_lo;
-  auto in_stack = [&](uintptr_t a) { return bounded && a >= t_stack_lo && a + 16 <= t_stack_hi && !(a & 7); };
-  const int pc_range = exec_range(pc);
-  uintptr_t caller = 0;
-  if (pc_range != g_own_range) {
-    for (int k = 0; k < 16 && in_stack(sp + 8 * uintptr_t(k)); ++k) {
-      const uintptr_t w = *reinterpret_cast<const uintptr_t*>(sp + 8 * uintptr_t(k));
-      const int r = exec_range(w);
-      if (r >= 0 && r != pc_range) {
-        caller = w;
-        s.pc[s.depth++] = w;
-        break;
-      }
-    }
-  }
-  bool first = true;
-  while (s.depth < kDepth && in_stack(fp)) {
-    const uintptr_t ret = *reinterpret_cast<const uintptr_t*>(fp + 8);
-    const uintptr_t next = *reinterpret_cast<const uintptr_t*>(fp);
-    if (!executable(ret)) break;
-    if (!(first && ret == caller)) s.pc[s.depth++] = ret;
-    first = false;
-    if (next <= fp) break;  // the chain must climb the stack
-    fp = next;
-  }
+  s.depth = uint8_t(walk(static_cast<const ucontext_t*>(ucv), s.pc, kDepth));
+  errno = saved_errno;
+}
+
+// ---- on-demand capture of another thread's stack (stall reports) ----
+constexpr int kCaptureSignal = 40;  // a real-time signal no thread blocks (SIGRTMIN is 34)
+std::mutex g_cap_mu;                // one capture at a time
+std::atomic<int> g_cap_state{0};    // 0 idle, 1 requested, 2 done
+uintptr_t g_cap_pcs[kMaxCaptureDepth];
+std::atomic<int> g_cap_depth{0};
+std::atomic<bool> g_cap_installed{false};
+
+void on_capture(int, siginfo_t*, void* ucv) {
+  if (g_cap_state.load(std::memory_order_acquire) != 1) return;
+  const int saved_errno = errno;
+  g_cap_depth.store(walk(static_cast<const ucontext_t*>(ucv), g_cap_pcs, kMaxCaptureDepth), std::memory_order_relaxed);
+  g_cap_state.store(2, std::memory_order_release);
   errno = saved_errno;
 }
 
@@ -132,6 +155,87 @@ void note_stack_bounds() {
   pthread_attr_destroy(&attr);
 }
 }  // namespace
+
+int current_tid() { return int(syscall(SYS_gettid)); }
+
+void note_thread() {
+  if (t_stack_hi <= t_stack_lo) note_stack_bounds();
+}
+
+bool enable_capture() {
+  if (g_cap_installed.load()) return true;
+  struct sigaction sa {};
+  sa.sa_sigaction = on_capture;
+  sa.sa_flags = SA_SIGINFO | SA_RESTART;
+  sigemptyset(&sa.sa_mask);
+  if (sigaction(kCaptureSignal, &sa, nullptr) != 0) return false;
+  g_cap_installed.store(true);
+  return true;
+}
+
+int capture(int tid, uintptr_t* pcs, int max, int timeout_ms) {
+  if (!g_cap_installed.load() || max <= 0) return 0;
+  std::lock_guard<std::mutex> g(g_cap_mu);
+  if (!g_on.load()) {
+    load_exec_ranges();  // the profiler keeps its own (read by its handler meanwhile)
+    g_own_range = exec_range(uintptr_t(&on_prof));
+  }
+  g_cap_depth.store(0);
+  g_cap_state.store(1, std::memory_order_release);
+  if (tid <= 0 || syscall(SYS_tgkill, getpid(), tid, kCaptureSignal) != 0) {
+    g_cap_state.store(0);
+    return 0;
+  }
+  const auto until = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
+  while (g_cap_state.load(std::memory_order_acquire) != 2) {
+    if (std::chrono::steady_clock::now() >= until) {
+      // The handler may still run later: it only writes g_cap_pcs, which the next capture
+      // re-initialises under the lock. Report nothing for this thread.
+      g_cap_state.store(0);
+      return 0;
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(200));
+  }
+  const int n = std::min(max, g_cap_depth.load());
+  for (int i = 0; i < n; ++i) pcs[i] = g_cap_pcs[i];
+  g_cap_state.store(0);
+  return n;
+}
+
+std::string describe_pcs(const uintptr_t* pcs, int n) {
+  // Each frame as object+offset (symbolise with `addr2line -f -C -e OBJECT OFFSET`, or
+  // bench/cpuprof_report.py): the maps are read now, outside any signal handler.
+  struct Map {
+    uintptr_t lo, hi, off;
+    std::string path;
+  };
+  std::vector<Map> maps;
+  std::ifstream f("/proc/self/maps");
+  for (std::string line; std::getline(f, line);) {
+    unsigned long lo = 0, hi = 0, off = 0;
+    char perms[5] = {};
+    int pos = 0;
+    if (sscanf(line.c_str(), "%lx-%lx %4s %lx %*s %*s%n", &lo, &hi, perms, &off, &pos) < 4 || perms[2] != 'x') continue;
+    std::string path = pos > 0 && size_t(pos) < line.size() ? line.substr(size_t(pos)) : "";
+    path.erase(0, path.find_first_not_of(' '));
+    maps.push_back({lo, hi, off, path.empty() ? "?" : path});
+  }
+  std::string out;
+  char buf[64];
+  for (int i = 0; i < n; ++i) {
+    const uintptr_t pc = i ? pcs[i] - 1 : pcs[i];  // return addresses: the call's own line
+    auto it = std::find_if(maps.begin(), maps.end(), [pc](const Map& m) { return pc >= m.lo && pc < m.hi; });
+    if (it == maps.end()) {
+      snprintf(buf, sizeof buf, " #%d ?(0x%lx)", i, (unsigned long)pc);
+      out += buf;
+      continue;
+    }
+    const std::string base = it->path.substr(it->path.rfind('/') == std::string::npos ? 0 : it->path.rfind('/') + 1);
+    snprintf(buf, sizeof buf, "+0x%lx", (unsigned long)(pc - it->lo + it->off));
+    out += " #" + std::to_string(i) + " " + base + buf;
+  }
+  return out;
+}
 
 bool start(const std::string& path, int hz) {
   if (g_on.load() || hz <= 0) return false;

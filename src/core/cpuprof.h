@@ -11,6 +11,7 @@
 // the profile also splits kernel time by call. At exit the samples and the executable
 // mappings are written as text; `bench/cpuprof_report.py` symbolises them.
 #pragma once
+#include <cstdint>
 #include <string>
 
 namespace hola::cpuprof {
@@ -24,5 +25,22 @@ void register_thread();
 void unregister_thread();
 // Disarms every timer and writes the profile file. Call once, after the threads have stopped.
 bool write();
+
+// ---- stacks of a thread that stopped answering (stall reports) ----
+// The same frame-pointer walk, run on demand in the target thread by a real-time signal
+// (40), whose handler only copies return addresses. Threads whose stacks may be captured call
+// note_thread() once at start (it records their stack bounds, read by the walk).
+constexpr int kMaxCaptureDepth = 32;
+void note_thread();
+// Installs the capture signal's handler (idempotent; false on failure).
+bool enable_capture();
+// Stack of the thread with kernel id `tid` in this process (innermost first), or 0 frames if it
+// did not answer within timeout_ms (a thread stopped by ptrace, or blocking the signal). By
+// tid, not pthread_t: a handle of a thread that has exited and been joined may not be used.
+int capture(int tid, uintptr_t* pcs, int max, int timeout_ms = 200);
+// The calling thread's kernel id.
+int current_tid();
+// " #0 hola+0x1234 #1 libc.so.6+0x5678 ..." from the current mappings.
+std::string describe_pcs(const uintptr_t* pcs, int n);
 
 }  // namespace hola::cpuprof

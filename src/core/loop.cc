@@ -90,11 +90,18 @@ void EventLoop::stop() {
   (void)r;
 }
 
+const char* EventLoop::phase_name(uint32_t p) {
+  static const char* const names[] = {"starting", "wait", "events", "timers", "deferred", "posted", "tick", "exited"};
+  return p < sizeof names / sizeof names[0] ? names[p] : "?";
+}
+
 void EventLoop::WakeHandler::on_event(uint32_t) {
   uint64_t v;
   while (::read(loop->wakefd_, &v, sizeof v) > 0) {
   }
+  loop->set_phase(kPosted);
   loop->drain_posted();
+  loop->set_phase(kEvents);
 }
 
 void EventLoop::drain_posted() {
@@ -115,6 +122,7 @@ void EventLoop::run_timers() {
     auto cb = std::move(it->second);
     timers_.erase(it);
     pending_.store(timers_.size(), std::memory_order_relaxed);
+    note(0, id, 0);
     cb();
   }
   // Drop cancelled entries at the top so they do not cause spurious wakeups.
@@ -155,8 +163,12 @@ void EventLoop::run() {
   constexpr int kMaxEvents = 256;
   epoll_event evs[kMaxEvents];
   t_loop_now_ms = &now_ms_;  // LoopClock on this thread reads the pass's time
+  uint64_t passes = 0;
   while (!stop_.load(std::memory_order_relaxed)) {
+    act_.passes.store(++passes, std::memory_order_relaxed);
+    set_phase(kTick);
     if (tick_) tick_();
+    set_phase(kWait);
     int n = 0;
     int64_t t = 0;  // mono_ns() at (or just before) the moment events were found
     if (busy_poll_ns_ > 0 && (!busy_auto_ || now_ms_ >= spin_off_until_ms_)) {
@@ -182,12 +194,24 @@ void EventLoop::run() {
       break;
     }
     now_ms_ = t / 1000000;
-    for (int i = 0; i < n; ++i) static_cast<Handler*>(evs[i].data.ptr)->on_event(evs[i].events);
-    if (!heap_.empty()) run_timers();
-    while (!deferred_.empty()) {
-      deferred_run_.swap(deferred_);
-      for (auto& f : deferred_run_) f();
-      deferred_run_.clear();
+    act_.pass_ns.store(t, std::memory_order_relaxed);
+    if (n > 0) {
+      set_phase(kEvents);
+      for (int i = 0; i < n; ++i) static_cast<Handler*>(evs[i].data.ptr)->on_event(evs[i].events);
+    }
+    if (!heap_.empty()) {
+      set_phase(kTimers);
+      run_timers();
+    }
+    if (!deferred_.empty()) {
+      set_phase(kDeferred);
+      uint64_t rounds = 0;
+      while (!deferred_.empty()) {
+        note(0, ++rounds, deferred_.size());
+        deferred_run_.swap(deferred_);
+        for (auto& f : deferred_run_) f();
+        deferred_run_.clear();
+      }
     }
     if (!retired_.empty()) {
       for (Handler* h : retired_) delete h;
@@ -195,8 +219,10 @@ void EventLoop::run() {
     }
   }
   t_loop_now_ms = nullptr;
+  set_phase(kPosted);
   drain_posted();
   if (on_exit_) on_exit_();
+  set_phase(kExited);
 }
 
 }  // namespace hola

@@ -76,7 +76,33 @@ class EventLoop {
   uint64_t spin_misses() const { return spin_misses_total_.load(std::memory_order_relaxed); }
   uint64_t spin_offs() const { return spin_offs_.load(std::memory_order_relaxed); }
 
+  // What the loop thread is doing, published with relaxed stores as it goes, so another
+  // thread can say where a loop that stopped answering is: Server::shutdown logs it for a
+  // worker that misses the drain deadline, the exit watchdog for every worker. `passes` counts
+  // loop iterations (a loop stuck inside one handler shows a count that stops); `subject` and
+  // `state` are set by the handler being run (a connection: its id and state bits, see
+  // http::Connection::on_event), `pass_ns` is the mono_ns() at which the current pass began.
+  enum Phase : uint32_t { kStarting = 0, kWait, kEvents, kTimers, kDeferred, kPosted, kTick, kExited };
+  struct Activity {
+    std::atomic<uint64_t> passes{0};
+    std::atomic<uint32_t> phase{kStarting};
+    std::atomic<uint32_t> handler_kind{0};  // handler-defined tag of the running handler
+    std::atomic<uint64_t> subject{0};
+    std::atomic<uint64_t> state{0};
+    std::atomic<int64_t> pass_ns{0};
+  };
+  static const char* phase_name(uint32_t p);
+  const Activity& activity() const { return act_; }
+  // Loop thread: the handler now running and its state (cheap: three relaxed stores).
+  void note(uint32_t kind, uint64_t subject, uint64_t state) {
+    act_.handler_kind.store(kind, std::memory_order_relaxed);
+    act_.subject.store(subject, std::memory_order_relaxed);
+    act_.state.store(state, std::memory_order_relaxed);
+  }
+  void note_state(uint64_t state) { act_.state.store(state, std::memory_order_relaxed); }
+
  private:
+  void set_phase(Phase p) { act_.phase.store(p, std::memory_order_relaxed); }
   struct WakeHandler : Handler {
     EventLoop* loop;
     void on_event(uint32_t) override;
@@ -113,6 +139,7 @@ class EventLoop {
   int64_t spin_off_until_ms_ = 0, spin_backoff_ms_ = 0;
   std::atomic<uint64_t> spin_hits_total_{0}, spin_misses_total_{0}, spin_offs_{0};
   void note_spin(bool hit);
+  alignas(64) Activity act_;  // own cache line: written by the loop thread only
 };
 
 }  // namespace hola

@@ -53,7 +53,27 @@ Connection::~Connection() {
   if (fd_ >= 0) ::close(fd_);
 }
 
+uint64_t Connection::state_bits(uint32_t iterations) const {
+  const uint64_t flags = uint64_t(parked_) | uint64_t(close_after_flush_) << 1 | uint64_t(reading_) << 2 |
+                         uint64_t(want_write_) << 3 | uint64_t(streaming_) << 4 | uint64_t(closed_) << 5 |
+                         uint64_t(in_process_) << 6 | uint64_t(read_pending_) << 7;
+  return flags | uint64_t(std::min<size_t>(in_.size(), 0xFFFFFF)) << 8 |
+         uint64_t(std::min<size_t>(unsent(), 0xFFFFFF)) << 32 | uint64_t(std::min<uint32_t>(iterations, 255)) << 56;
+}
+
+std::string Connection::describe_state(uint64_t s) {
+  static const char* const names[] = {"parked", "close_after_flush", "reading", "want_write",
+                                      "streaming", "closed", "in_process", "read_pending"};
+  std::string out = "{";
+  for (int b = 0; b < 8; ++b)
+    if (s >> b & 1) out += std::string(out.size() > 1 ? "," : "") + names[b];
+  out += "} in=" + std::to_string(s >> 8 & 0xFFFFFF) + " unsent=" + std::to_string(s >> 32 & 0xFFFFFF) +
+         " read_iterations=" + std::to_string(s >> 56);
+  return out;
+}
+
 void Connection::on_event(uint32_t ev) {
+  worker_->loop().note(kConnectionHandler, id_, state_bits(0));
   if (closed_) return;
   if (ev & EPOLLERR) {
     close();
@@ -90,7 +110,9 @@ void Connection::on_readable(bool peer_closed) {
   }
   StageProfile* prof = worker_->profile();
   bool more = false;
+  uint32_t iterations = 0;
   while (!parked_ && reading_ && !streaming_ && !closed_) {
+    if (++iterations > 1) worker_->loop().note_state(state_bits(iterations));
     int64_t t0 = prof ? mono_ns() : 0;
     if (in_.empty()) {
       char* buf = worker_->scratch();
@@ -590,6 +612,7 @@ bool Server::bind(std::string* err) {
 }
 
 void Server::Acceptor::on_event(uint32_t) {
+  worker->loop().note(kAcceptorHandler, uint64_t(fd), 0);
   const bool prof = server->opts_.profile;
   for (int i = 0; i < 256; ++i) {
     const int64_t t0 = prof ? mono_ns() : 0;
@@ -640,6 +663,8 @@ void Server::start() {
       char name[16];
       snprintf(name, sizeof name, "hola-w%d", wp->index());
       pthread_setname_np(pthread_self(), name);
+      cpuprof::note_thread();  // stack bounds for a stall report's capture
+      wp->tid_.store(cpuprof::current_tid());
       cpuprof::register_thread();
       wp->scratch_.assign(opts_.read_chunk, 0);
       handler_->on_worker_start(*wp);
@@ -658,6 +683,7 @@ void Server::start() {
       wp->loop().run();
       handler_->on_worker_stop(*wp);
       cpuprof::unregister_thread();
+      wp->tid_.store(0);  // gone: no capture signal may be sent to this id any more
     });
   }
 }
@@ -685,6 +711,44 @@ bool wait_answer(const Answer& a, std::chrono::steady_clock::time_point until) {
   return true;
 }
 }  // namespace
+
+std::string Server::activity(size_t i) const {
+  const Worker& w = *workers_[i];
+  const EventLoop::Activity& a = w.loop().activity();
+  const uint64_t passes = a.passes.load(std::memory_order_relaxed);
+  const uint32_t phase = a.phase.load(std::memory_order_relaxed);
+  const uint32_t kind = a.handler_kind.load(std::memory_order_relaxed);
+  const uint64_t subject = a.subject.load(std::memory_order_relaxed);
+  const uint64_t state = a.state.load(std::memory_order_relaxed);
+  const int64_t pass_ns = a.pass_ns.load(std::memory_order_relaxed);
+  char head[200];
+  snprintf(head, sizeof head, "worker %zu: pass %llu, phase %s, pass began %.1f ms ago, last handler ", i,
+           (unsigned long long)passes, EventLoop::phase_name(phase), pass_ns ? (mono_ns() - pass_ns) / 1e6 : -1.0);
+  std::string out = head;
+  char id[40];
+  snprintf(id, sizeof id, "%llx", (unsigned long long)subject);
+  if (kind == kConnectionHandler) out += std::string("connection ") + id + " " + Connection::describe_state(state);
+  else if (kind == kAcceptorHandler) out += "acceptor fd " + std::to_string(subject);
+  else if (kind == 0) out += "loop-internal " + std::to_string(subject) + "/" + std::to_string(state) + " (timer id or deferred round/size)";
+  else out += "kind " + std::to_string(kind) + " subject " + id + " state " + std::to_string(state);
+  return out;
+}
+
+std::string Server::stall_report(size_t i, bool with_stack) {
+  const uint64_t p0 = workers_[i]->loop().activity().passes.load(std::memory_order_relaxed);
+  std::this_thread::sleep_for(std::chrono::milliseconds(100));
+  const uint64_t p1 = workers_[i]->loop().activity().passes.load(std::memory_order_relaxed);
+  std::string out = activity(i) + (p1 == p0 ? "; passes NOT advancing over 100 ms" : "; passes advancing (" +
+                                                  std::to_string(p1 - p0) + " in 100 ms)");
+  const int tid = workers_[i]->tid_.load();
+  if (with_stack && tid == 0) out += "; thread exited";
+  if (with_stack && tid > 0) {
+    uintptr_t pcs[cpuprof::kMaxCaptureDepth];
+    const int n = cpuprof::capture(tid, pcs, cpuprof::kMaxCaptureDepth);
+    out += n ? "; stack" + cpuprof::describe_pcs(pcs, n) : "; stack: no answer to the capture signal";
+  }
+  return out;
+}
 
 void Server::shutdown(int drain_ms) {
   closing_.store(true);
@@ -724,7 +788,12 @@ void Server::shutdown(int drain_ms) {
         ans->done.store(true);
       });
       if (!wait_answer(*ans, answer_by)) {
-        LOG_WARN("drain: worker %d did not answer by the drain deadline", wp->index());
+        // Where it is, straight to stderr too: the log writer is not needed to say it.
+        const std::string why = stall_report(size_t(wp->index()), true);
+        LOG_WARN("drain: worker %d did not answer by the drain deadline: %s", wp->index(), why.c_str());
+        const std::string line = "hola: drain: worker did not answer: " + why + "\n";
+        ssize_t wr = ::write(2, line.data(), line.size());
+        (void)wr;
         answered = false;
         break;
       }

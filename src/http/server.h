@@ -22,6 +22,9 @@ namespace hola::http {
 class Worker;
 class Server;
 
+// EventLoop::note() handler kinds of the server's handlers (0 is the loop's own).
+constexpr uint32_t kConnectionHandler = 1, kAcceptorHandler = 2;
+
 // Per-worker request counters, readable (relaxed) from other threads for /metrics.
 struct alignas(64) WorkerStats {
   std::atomic<uint64_t> requests{0};
@@ -90,6 +93,10 @@ class Connection final : public EventLoop::Handler {
   size_t unsent() const { return out_.size() - out_off_; }
   // Bytes the socket has taken over the connection's life.
   uint64_t bytes_sent() const { return sent_total_; }
+  // The state published in the loop's activity record: flag bits, buffered input, unsent
+  // output and the current read loop's iteration count; describe_state() decodes it.
+  uint64_t state_bits(uint32_t iterations) const;
+  static std::string describe_state(uint64_t bits);
 
  private:
   void on_readable(bool peer_closed);
@@ -222,6 +229,7 @@ class Worker {
   Connection* conns_ = nullptr;
   std::unique_ptr<StageProfile> profile_;
   std::shared_ptr<std::function<void()>> sweep_;  // idle-timeout sweeper (owned here)
+  std::atomic<int> tid_{0};  // kernel id of the worker's thread while it runs (stall reports)
 };
 
 // Counted reference to a Connection for asynchronous callbacks (aloha calls, SSE tickers):
@@ -285,6 +293,11 @@ class Server {
   size_t open_connections() const { return open_.load(std::memory_order_relaxed); }
   // JSON summary of the --profile histograms (call after join()).
   std::string profile_json() const;
+  // Worker i's activity record, decoded (any thread, any time).
+  std::string activity(size_t i) const;
+  // A worker that stopped answering: its activity, whether its loop passes advance over the
+  // next 100 ms, and (with_stack) its stack captured by signal. Any thread but worker i's.
+  std::string stall_report(size_t i, bool with_stack);
 
   // Where each accepted connection's client ran (SO_INCOMING_CPU: for loopback clients the
   // CPU of the sending thread) relative to the pinned worker that serves it.

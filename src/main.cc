@@ -386,6 +386,7 @@ int main(int argc, char** argv) {
     fprintf(stderr, "hola: cannot start the CPU profiler\n");
     return 1;
   }
+  cpuprof::enable_capture();  // stall reports capture worker stacks by signal
   chainer.start();
   tracer.start();
   server.start();
@@ -419,12 +420,17 @@ int main(int argc, char** argv) {
     // writer may be what is stuck.
     const int64_t limit_ms = exit_deadline_ms >= 0 ? exit_deadline_ms
                                                    : int64_t(shutdown_delay_ms) + std::max(0, drain_ms) + kExitMarginMs;
-    if (limit_ms > 0) std::thread([limit_ms] {
+    if (limit_ms > 0) std::thread([limit_ms, &server] {
       std::this_thread::sleep_for(std::chrono::milliseconds(limit_ms));
       char line[160];
       const int n = snprintf(line, sizeof line, "hola: termination did not complete within %lld ms; exiting\n",
                              (long long)limit_ms);
       ssize_t w = ::write(2, line, size_t(n));
+      // where every event loop was, with its stack (the report that names a stuck handler)
+      for (size_t i = 0; i < server.num_workers(); ++i) {
+        const std::string r = "hola: " + server.stall_report(i, true) + "\n";
+        w = ::write(2, r.data(), r.size());
+      }
       (void)w;
       _exit(3);
     }).detach();

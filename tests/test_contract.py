@@ -1,6 +1,7 @@
 """The behavioural contract of the reference service, end to end against the
 native server binary."""
 import json
+import re
 import os
 import shutil
 import socket
@@ -686,6 +687,9 @@ def test_a_stuck_worker_cannot_hold_the_termination_forever(hola):
     assert 2.5 <= took < 10
     assert "drain: worker 1 did not answer by the drain deadline" in log
     assert "termination did not complete within 3000 ms; exiting" in log
+    # the stall report: where the stopped worker's loop was, and that it is not advancing
+    assert re.search(r"drain: worker did not answer: worker 1: pass \d+, phase \w+, .*passes NOT advancing", log), log
+    print(log)
 
 
 def test_default_exit_deadline_leaves_a_normal_termination_alone(hola):
@@ -715,6 +719,9 @@ def test_every_thread_blocks_the_termination_signals(hola):
         fields = dict(line.split(":\t", 1) for line in status.splitlines() if ":\t" in line)
         names.append(fields["Name"].strip())
         assert int(fields["SigBlk"], 16) & want == want, (fields["Name"], fields["SigBlk"])
+        # ... and only those: SIGPROF (--cpu-profile's sampling timer, the log writer
+        # included) and the stall reports' capture signal (40) stay deliverable
+        assert not int(fields["SigBlk"], 16) & (1 << (signal.SIGPROF - 1) | 1 << 39), (fields["Name"], fields["SigBlk"])
     assert "hola-log" in names, names
 
 
@@ -810,3 +817,31 @@ def test_adaptive_busy_poll_backs_off_under_light_load(hola):
     c0 = cpu()
     time.sleep(1.0)
     assert (cpu() - c0) / os.sysconf("SC_CLK_TCK") < 0.1
+
+
+def test_exit_watchdog_reports_where_every_worker_is(hola):
+    """The exit watchdog's stall report: for each worker its loop's pass counter, phase and last
+    handler, and its stack, taken in the worker by a signal whose handler walks the frame
+    pointers. Here the termination outlasts --exit-deadline-ms (a 5 s delay against a 1 s
+    limit), so the workers are alive and waiting in epoll: their stacks name the event loop."""
+    import signal
+    import subprocess
+
+    s = hola(args=["--shutdown-delay-ms", "5000", "--exit-deadline-ms", "1000"], threads=2)
+    s.get("/api/hola")  # one request: worker 0 or 1 has run a connection handler
+    s.proc.send_signal(signal.SIGTERM)
+    assert s.proc.wait(timeout=10) == 3
+    log = s.log()
+    reports = re.findall(r"hola: worker (\d): pass (\d+), phase (\w+), .*?; stack((?: #\d+ \S+)+)", log)
+    assert {r[0] for r in reports} == {"0", "1"}, log[-3000:]
+    exe = str(s.exe)
+    for worker, passes, phase, stack in reports:
+        assert phase == "wait" and int(passes) >= 1, (worker, phase)
+        frames = re.findall(r"#\d+ (\S+)\+0x([0-9a-f]+)", stack)
+        own = [off for obj, off in frames if obj == Path(exe).name]
+        assert own, stack
+        names = subprocess.run(["addr2line", "-f", "-C", "-e", exe, *[f"0x{o}" for o in own]],
+                               capture_output=True, text=True).stdout
+        assert "hola::EventLoop::run()" in names, names
+    # the connection handler's record is decoded with its state bits
+    assert re.search(r"last handler (connection [0-9a-f]+ \{[a-z_,]*\} in=\d+ unsent=\d+|loop-internal)", log), log
