@@ -15,9 +15,11 @@ K timed steps between barriers; the elapsed time is the MAX over ranks, `value` 
 node-wide total req/s, and p50/p99 come from the merged latency histograms of all ranks.
 Every response body in the timed region is compared with the greeting of the replica behind
 its connection (a mismatch is an error). After the timed region rank 0 runs BASELINE config
-2 (one connection, ~3 s) and reports it as c1_* keys, then the as-deployed replica (the
-image's exact ENTRYPOINT + the manifests' args and env: no busy-polling; deployed_* keys);
-the JSON also carries span accounting
+2 (one connection, 30 s) and reports it as c1_* keys with the host load of that run, then the
+as-deployed replica (the image's exact ENTRYPOINT + the manifests' args and env:
+`--shutdown-delay-ms 5000 --busy-poll-us auto`; deployed_* keys), then the chaining endpoint
+(load generator -> hola A -> hola B as aloha; chain_* keys); the JSON also carries span
+accounting
 (`tracing`, with a native collector under --zipkin-sink), connection placement (`locality`)
 and how busy the replicas' cores and their idle SMT siblings were (`host_load`: other
 tenants on the siblings are what moves the number between runs on a shared host).
@@ -52,11 +54,12 @@ BASELINE_VALUE = None  # the reference publishes no numbers
 def parse_args():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1, help="replicas on this node (one per rank)")
-    # Defaults give a ~30 s timed region at ~4M req/s (BASELINE configs 3/4 are 30 s wrk runs).
-    ap.add_argument("--steps", type=int, default=40)
+    # A step is sized so that the driver's `--steps 20` times ~30 s at ~4.1 M req/s, the length
+    # of BASELINE configs 3/4 (30 s wrk runs): 20 x 64 x 96,000 requests.
+    ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--connections", type=int, default=64, help="keep-alive connections per replica")
-    ap.add_argument("--reqs-per-conn", type=int, default=50000, help="requests per connection per step")
+    ap.add_argument("--reqs-per-conn", type=int, default=96000, help="requests per connection per step")
     ap.add_argument("--cores", type=int, default=0,
                     help="physical host cores per replica (server + load generator); 0 = one GPU "
                          "slot's share of the node: min(CPU budget, physical cores) / GPUs on the node "
@@ -67,7 +70,7 @@ def parse_args():
     ap.add_argument("--path", default="/api/hola")
     ap.add_argument("--host", default="auto",
                     help="loopback address of the replicas; auto = ::1 when IPv6 loopback works (2.6%% "
-                         "more req/s than 127.0.0.1 on the box, profiles/r20_v6), else 127.0.0.1")
+                         "more req/s than 127.0.0.1 on the box, profiles/round1/r20_v6), else 127.0.0.1")
     ap.add_argument("--no-tracing", action="store_true", help="run replicas with tracing off")
     ap.add_argument("--zipkin-sink", action="store_true",
                     help="the deployed tracing configuration (ZIPKIN_SERVER_URL is set in the image, "
@@ -97,7 +100,7 @@ def parse_args():
     ap.add_argument("--smt", choices=("auto", "off", "split", "pair"), default="auto",
                     help="use the SMT sibling of each planned physical core: off = idle, split = "
                          "same side, pair = server worker + its load-generator thread on one core "
-                         "(1.55x req/s per physical core, profiles/r16_smt); auto = pair when one GPU "
+                         "(1.55x req/s per physical core, profiles/round1/r16_smt); auto = pair when one GPU "
                          "slot's CPU share (budget / GPUs on the node) holds both threads of --cores "
                          "cores, else off. Decided per node, so every N runs replicas alike")
     ap.add_argument("--epoll-lt", action="store_true",
@@ -105,15 +108,16 @@ def parse_args():
     ap.add_argument("--busy-poll-pause", type=int, default=-1,
                     help="PAUSE instructions between empty polls while busy-polling (both sides); "
                          "-1 = 16 with --smt pair (+6%% req/s: the spinning sibling leaves issue slots "
-                         "to the working one, profiles/r19_pause), else 0")
+                         "to the working one, profiles/round1/r19_pause), else 0")
     ap.add_argument("--pipeline", type=int, default=1,
                     help="requests per connection sent back to back before waiting for their "
                          "responses (wrk's pipeline.lua, as in the TechEmpower plaintext test); "
                          "1 = wrk's default and the headline (BASELINE configs 2-4)")
-    ap.add_argument("--c1-seconds", type=float, default=3.0,
+    ap.add_argument("--c1-seconds", type=float, default=30.0,
                     help="after the timed region, rank 0 drives its own replica over ONE connection for "
-                         "about this long (BASELINE config 2) and reports c1_rps/c1_p50_ms/c1_p99_ms; "
-                         "0 = skip. Outside the timed region: `value` is untouched")
+                         "about this long (BASELINE config 2: 30 s) and reports c1_rps/c1_p50_ms/c1_p99_ms "
+                         "with the host load of that run; 0 = skip. Outside the timed region: `value` is "
+                         "untouched")
     ap.add_argument("--c1-reqs", type=int, default=0,
                     help="config-2 request count instead of --c1-seconds (0 = sized from a warm-up "
                          "run to last --c1-seconds)")
@@ -122,13 +126,30 @@ def parse_args():
                          "and manifests start it (deploy/Dockerfile ENTRYPOINT + deploy/openshift args and "
                          "env) on its server CPUs, with the same load generator, for about "
                          "this long; reported as deployed_*. 0 = skip. `value` is untouched")
+    ap.add_argument("--chain-seconds", type=float, default=5.0,
+                    help="after the timed region, rank 0 also measures GET /api/hola-chaining: load generator "
+                         "-> hola A -> hola B (B answering as aloha), 64 connections, about this long, on "
+                         "the rank's CPUs; reported as chain_* (rps, latency, A's CPU per request, Hystrix "
+                         "events: fallbacks must be 0). 0 = skip. `value` is untouched")
+    ap.add_argument("--chain-pool", type=int, default=128,
+                    help="hola A's Hystrix thread-pool (bulkhead) size in the chain sub-run: the reference's "
+                         "10 would turn most of 64 concurrent calls into fallbacks (SURVEY.md D2)")
     ap.add_argument("--server-busy-poll", default="",
                     help="the replica's own --busy-poll-us (N, auto or auto:N); default: adaptive with the "
                          "load generator's N (`auto`, as the manifests start the replica), 0 when that is 0")
+    ap.add_argument("--gpu-slots", type=int, default=0,
+                    help="rehearsal only: plan as if the node had this many GPUs (replica slots) instead "
+                         "of the ones it has (0 = detect)")
+    ap.add_argument("--ignore-quota", action="store_true",
+                    help="rehearsal only: plan on the whole affinity mask, ignoring the cgroup CPU quota "
+                         "(the 1-GPU box is a 16-CPU quota over a 256-CPU host: with --gpu-slots 8 this "
+                         "plans the unconstrained 8-GPU node's layout on its real topology)")
+    ap.add_argument("--plan-only", action="store_true",
+                    help="print the core plan of every slot of the node (one JSON line) and exit")
     ap.add_argument("--busy-poll-us", type=int, default=20,
                     help="spin this long in epoll before sleeping (the load generator; the replica spins "
                          "adaptively up to this long); 20 us measured best on the box "
-                         "(profiles/r11_box_session), 0 = off")
+                         "(profiles/round1/r11_box_session), 0 = off")
     a = ap.parse_args()
     if not a.server_busy_poll:
         # the manifests' setting: at saturation equal to a fixed spin (profiles/round3/10_auto)
@@ -138,6 +159,10 @@ def parse_args():
 
 def main() -> int:
     a = parse_args()
+    if a.ignore_quota:
+        os.environ["HOLA_IGNORE_QUOTA"] = "1"  # read by cpu_budget(); inherited by every rank
+    if a.plan_only:
+        return _plan_only(a)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
@@ -162,7 +187,7 @@ def main() -> int:
     if rank == 0 and a.zipkin_sink and not a.no_tracing:
         sink = start_zipkin_sink()
     if rank == 0:
-        slots = max(local_world, _gpu_slots())
+        slots = max(local_world, a.gpu_slots or _gpu_slots())
         cores = a.cores or slot_cores(slots)
         per_rank = min(cores, max(1, cpu_budget() // local_world))
         host = a.host if a.host != "auto" else ("::1" if _can_bind("::1") else "127.0.0.1")
@@ -280,7 +305,7 @@ def main() -> int:
         sibs = {x for c in own for x in siblings(c)} - own
         st = loadgen.stats()
         mem = server.memory_kb()
-        c1 = _config2_subrun(a, host, port, load_cpus, bodies and [bodies[local_rank]]) if local_rank == 0 else None
+        c1 = _config2_subrun(a, host, port, server_cpus, load_cpus, bodies and [bodies[local_rank]]) if local_rank == 0 else None
 
         local = {"elapsed": elapsed, "requests": reqs, "errors": errs, "hist": st.get("hist", ""),
                  "non2xx": st.get("non2xx", 0), "body_checked": st.get("body_checked", 0),
@@ -309,17 +334,23 @@ def main() -> int:
         if loadgen:
             loadgen.close()
         server.stop()
-    # The as-deployed replica, on the same CPUs once the headline replica is gone (rank 0).
-    deployed = None
+    # The as-deployed replica, then the chaining path, on the same CPUs once the headline
+    # replica is gone (rank 0).
+    deployed = chain = None
     if local_rank == 0 and a.deployed_seconds > 0:
         try:
             deployed = _deployed_subrun(a, server_cpus, load_cpus)
         except Exception as e:  # noqa: BLE001 - reported in the JSON; the other ranks must not hang
             deployed = {"error": f"{type(e).__name__}: {e}"}
+    if local_rank == 0 and a.chain_seconds > 0:
+        try:
+            chain = _chain_subrun(a, list(server_cpus) + list(load_cpus))
+        except Exception as e:  # noqa: BLE001 - as above
+            chain = {"error": f"{type(e).__name__}: {e}"}
     if dist:
         both = [None] * world
-        dist.all_gather_object(both, deployed)
-        deployed = both[0]
+        dist.all_gather_object(both, (deployed, chain))
+        deployed, chain = both[0]
         if sink:
             sink[0].terminate()
             sink[0].wait(timeout=10)
@@ -372,8 +403,11 @@ def main() -> int:
             "body_mismatch": sum(g["body_mismatch"] for g in gathered),
             # BASELINE config 2 (1 connection, 1 replica), measured after the timed region
             **_c1_keys(gathered[0]["c1"]),
-            # the replica as the image and manifests run it (no busy-polling), same load generator
+            # the replica as the image and manifests run it (--shutdown-delay-ms 5000
+            # --busy-poll-us auto), same load generator
             **_deployed_keys(deployed),
+            # GET /api/hola-chaining through two replicas (the endpoint with real work behind it)
+            **_chain_keys(chain),
             # span accounting over the timed region, all replicas (per second)
             "tracing": _tracing_block(a, gathered, t, plan[0]["sink_port"]),
             # client thread vs. serving worker placement of every accepted connection
@@ -422,6 +456,30 @@ def main() -> int:
         with _stdout_to_stderr():
             dist.barrier()
             dist.destroy_process_group()
+    return 0
+
+
+def _plan_only(a) -> int:
+    """The core plan of a whole node (one replica per GPU slot), as rank 0 computes it, without
+    starting anything: the cpu map an N = slots run would use."""
+    from hola_amd.utils.cpu import l3_domain, package_of, physical_cores
+
+    slots = a.gpu_slots or max(1, _gpu_slots())
+    cores = a.cores or slot_cores(slots)
+    per_rank = min(cores, max(1, cpu_budget() // slots))
+    smt = a.smt
+    if smt == "auto":
+        smt = "pair" if smt_fits(slots, per_rank) else "off"
+    plan = plan_replicas_with_loadgen(slots, per_rank, a.server_threads, avoid_busy=False, smt=smt)
+    print(json.dumps({"gpu_slots": slots, "cores_per_slot": per_rank, "smt": smt, "cpu_budget": cpu_budget(),
+                      "cgroup_quota": cgroup_cpu_quota(), "physical_cores": len(physical_cores()),
+                      "ranks": [{"server": p["server"], "loadgen": p["loadgen"], "thread_targets": p["thread_targets"],
+                                 "dealing": p["dealing"],
+                                 "server_sockets": sorted({package_of(c) for c in p["server"]}),
+                                 "server_l3": sorted({l3_domain(c) for c in p["server"]}),
+                                 "loadgen_sockets": sorted({package_of(c) for c in p["loadgen"]}),
+                                 "siblings": {str(c): siblings(c) for c in p["server"] + p["loadgen"]}}
+                                for p in plan]}), flush=True)
     return 0
 
 
@@ -487,7 +545,7 @@ def _expected_bodies(path: str, ranks: list[int]) -> list[str] | None:
     return None
 
 
-def _config2_subrun(a, host: str, port: int, load_cpus, bodies) -> dict | None:
+def _config2_subrun(a, host: str, port: int, server_cpus, load_cpus, bodies) -> dict | None:
     """BASELINE config 2: one keep-alive connection against this rank's replica, run after
     the timed region (so the headline is unaffected)."""
     if a.c1_reqs <= 0 and a.c1_seconds <= 0:
@@ -496,20 +554,27 @@ def _config2_subrun(a, host: str, port: int, load_cpus, bodies) -> dict | None:
                            busy_poll_us=a.busy_poll_us, busy_poll_pause=a.busy_poll_pause, epoll_lt=a.epoll_lt,
                            expect_bodies=bodies, verify_body=bodies is None)
     try:
-        warm = lg.run(max(1000, a.c1_reqs // 10) if a.c1_reqs > 0 else 20000)
+        warm = lg.run(max(1000, a.c1_reqs // 10) if a.c1_reqs > 0 else 50000)
         n = a.c1_reqs
         if n <= 0:  # size the run from the warm-up rate: about --c1-seconds, within bounds
             rate = warm["requests"] / max(1e-9, warm["elapsed_ns"] / 1e9)
-            n = int(min(5_000_000, max(20_000, rate * a.c1_seconds)))
+            n = int(min(30_000_000, max(20_000, rate * a.c1_seconds)))
         lg.reset()
+        own = set(server_cpus) | {load_cpus[0]}
+        sibs = {x for c in own for x in siblings(c)} - own
+        t0 = cpu_times()
         r = lg.run(n)
+        t1 = cpu_times()
         st = lg.stats()
     finally:
         lg.close()
     el = r["elapsed_ns"] / 1e9
     return {"rps": r["requests"] / el if el > 0 else 0.0, "requests": r["requests"], "elapsed_s": el,
             "p50_ns": st["p50_ns"], "p99_ns": st["p99_ns"], "errors": r["errors"],
-            "body_checked": st.get("body_checked", 0), "client_cpu": load_cpus[0]}
+            "body_checked": st.get("body_checked", 0), "client_cpu": load_cpus[0],
+            # as for the headline: busy share of the replica's + client's CPUs and of their idle
+            # SMT siblings over this run (another tenant on a sibling slows the one connection)
+            "host_load": {"own": busy_fraction(t0, t1, own), "siblings": busy_fraction(t0, t1, sibs)}}
 
 
 def _layout_note(slots: int, smt: str, server_cpus, load_cpus) -> str:
@@ -592,6 +657,75 @@ def _deployed_subrun(a, server_cpus, load_cpus) -> dict | None:
             "env": " ".join(f"{k}={v}" for k, v in sorted(env.items()) if k in img.env or k == "HOSTNAME")}
 
 
+def _chain_subrun(a, cpus: list[int]) -> dict:
+    """GET /api/hola-chaining end to end (HolaResource.java:69-78,94-113): load generator ->
+    hola A -> hola B, where B plays aloha (B's own aloha is unreachable, so B answers its
+    fallback list at once: ["Hola de B", "Aloha response (fallback)"], which A decodes as the
+    aloha's List<String>). Every request crosses A's pooled keep-alive client, the Hystrix
+    command (breaker, bulkhead, 600 ms timer), B3 propagation and the JSON decode. Each body is
+    checked; an A-side fallback would differ from the expected body. The CPUs are the rank's
+    own, split 2:1:1 (A does two hops' work) with each L3 holding a share of all three."""
+    from hola_amd.parallel.loadgen import run_duration
+    from hola_amd.utils.cpu import split_mirrored
+
+    plan = split_mirrored(sorted(cpus), {"A": 2, "B": 1, "loadgen": 1})
+    with HolaProcess(args=["--aloha-url", "http://127.0.0.1:1/", "--feign-log", "none", "--no-tracing",
+                           "--feign-retry", "off", "--log-level", "warn"], env={"HOSTNAME": "B"},
+                     threads=len(plan["B"]), cpu_list=format_cpu_list(plan["B"])) as b:
+        with HolaProcess(args=["--aloha-url", f"http://127.0.0.1:{b.port}/", "--aloha-path", "api/hola-chaining",
+                               "--feign-log", "none", "--hystrix-pool-size", str(a.chain_pool), "--log-level", "warn"],
+                         env={"HOSTNAME": "A"}, threads=len(plan["A"]), cpu_list=format_cpu_list(plan["A"])) as s:
+            st, _, body = s.get("/api/hola-chaining")
+            want = json.dumps(["Hola de A", "Hola de B", "Aloha response (fallback)"], separators=(",", ":"))
+            if st != 200 or json.loads(body) != json.loads(want):
+                return {"error": f"unexpected first answer {st} {body[:200]!r}"}
+            ev0 = _hystrix_events(s)
+            c0 = proc_cpu_s(s.proc.pid), proc_cpu_s(b.proc.pid)
+            w0 = time.perf_counter()
+            res = run_duration([("127.0.0.1", s.port)], a.connections, len(plan["loadgen"]), a.chain_seconds, 1.0,
+                               cpu_list=format_cpu_list(plan["loadgen"]), path="/api/hola-chaining",
+                               expect_bodies=[body.decode()])
+            wall = time.perf_counter() - w0
+            c1 = proc_cpu_s(s.proc.pid), proc_cpu_s(b.proc.pid)
+            ev1 = _hystrix_events(s)
+    lat = res["latency"]
+    rps = res["rps"]
+    # CPU over the whole run (its 1 s warm-up included) per request at the measured rate
+    busy = ((c1[0] - c0[0]) / wall, (c1[1] - c0[1]) / wall)
+    return {"rps": rps, "p50_ns": lat["p50_ns"], "p99_ns": lat["p99_ns"], "requests": lat.get("count", 0),
+            "errors": lat["errors"], "non2xx": lat.get("non2xx", 0), "body_checked": lat.get("body_checked", 0),
+            "body_mismatch": lat.get("body_mismatch", 0),
+            "a_cpu_us_per_req": 1e6 * busy[0] / rps if rps else 0.0,
+            "b_cpu_us_per_req": 1e6 * busy[1] / rps if rps else 0.0,
+            "hystrix": {k: ev1.get(k, 0) - ev0.get(k, 0) for k in sorted(set(ev0) | set(ev1))},
+            "cpus": {k: format_cpu_list(v) for k, v in plan.items()}, "pool": a.chain_pool}
+
+
+def _hystrix_events(s: HolaProcess) -> dict:
+    _, _, metrics = s.get("/metrics")
+    return {ln.split('event="')[1].split('"')[0]: int(float(ln.split()[-1])) for ln in metrics.decode().splitlines()
+            if ln.startswith("hola_hystrix_events_total")}
+
+
+def _chain_keys(c: dict | None) -> dict:
+    if not c:
+        return {}
+    if "error" in c:
+        return {"chain_error": c["error"]}
+    h = c["hystrix"]
+    return {"chain_rps": round(c["rps"], 1), "chain_p50_ms": round(c["p50_ns"] / 1e6, 4),
+            "chain_p99_ms": round(c["p99_ns"] / 1e6, 4), "chain_requests": c["requests"],
+            "chain_errors": c["errors"], "chain_non2xx": c["non2xx"], "chain_body_checked": c["body_checked"],
+            "chain_body_mismatch": c["body_mismatch"],
+            # hola A's own CPU per chained request (it serves the client and calls B)
+            "chain_a_cpu_us_per_req": round(c["a_cpu_us_per_req"], 3),
+            "chain_b_cpu_us_per_req": round(c["b_cpu_us_per_req"], 3),
+            # A's Hystrix command over the run (1 s warm-up included): all SUCCESS, no FALLBACK / TIMEOUT
+            "chain_hystrix_success": h.get("SUCCESS", 0), "chain_hystrix_fallback": h.get("FALLBACK_SUCCESS", 0),
+            "chain_hystrix_timeout": h.get("TIMEOUT", 0), "chain_hystrix_events": h,
+            "chain_cpus": c["cpus"], "chain_pool": c["pool"]}
+
+
 def _deployed_keys(d: dict | None) -> dict:
     if not d:
         return {}
@@ -613,6 +747,7 @@ def _c1_keys(c1: dict | None) -> dict:
     return {"c1_rps": round(c1["rps"], 1), "c1_p50_ms": round(c1["p50_ns"] / 1e6, 4),
             "c1_p99_ms": round(c1["p99_ns"] / 1e6, 4), "c1_requests": c1["requests"],
             "c1_errors": c1["errors"], "c1_body_checked": c1["body_checked"],
+            "c1_elapsed_s": round(c1["elapsed_s"], 2), "c1_host_load": c1.get("host_load"),
             # the client's CPU: with --smt pair it is the SMT sibling of a server worker, and the
             # connection is served on that same physical core (r18: slower for one connection)
             "c1_client_cpu": c1["client_cpu"]}

@@ -68,7 +68,9 @@ class _AlohaHandler(BaseHTTPRequestHandler):
             owner.requests.append({"path": self.path, "headers": {k.lower(): v for k, v in self.headers.items()},
                                    "peer_port": self.client_address[1]})
             mode, delay, payload = owner.mode, owner.delay_s, owner.payload
-        if mode == "slow":
+            if mode == "slow_once":  # this request is slow, the ones after it are not
+                owner.mode = "ok"
+        if mode in ("slow", "slow_once"):
             time.sleep(delay)
         if mode == "close":
             self.close_connection = True

@@ -55,10 +55,11 @@ def cgroup_cpu_quota() -> float:
 
 
 def cpu_budget() -> int:
-    """Number of CPUs this process tree may keep busy."""
+    """Number of CPUs this process tree may keep busy. HOLA_IGNORE_QUOTA=1 plans as if the
+    cgroup quota were absent (layout rehearsals of an unconstrained node on a quota'd box)."""
     n = len(allowed_cpus())
     q = cgroup_cpu_quota()
-    if q > 0:
+    if q > 0 and os.environ.get("HOLA_IGNORE_QUOTA") != "1":
         n = min(n, int(q))
     return max(1, n)
 
@@ -102,6 +103,15 @@ def physical_cores(cpus: list[int] | None = None) -> list[int]:
 def l3_domain(cpu: int) -> int:
     """Id of the L3 (CCD on EPYC) a CPU belongs to; 0 when unknown."""
     v = _read(f"/sys/devices/system/cpu/cpu{cpu}/cache/index3/id")
+    try:
+        return int(v) if v is not None else 0
+    except ValueError:
+        return 0
+
+
+def package_of(cpu: int) -> int:
+    """Physical package (socket) of a CPU; 0 when unknown."""
+    v = _read(f"/sys/devices/system/cpu/cpu{cpu}/topology/physical_package_id")
     try:
         return int(v) if v is not None else 0
     except ValueError:
@@ -155,8 +165,18 @@ def plan_node(local_world: int, per_rank: int | None = None, avoid_busy: bool = 
     domains: dict[int, list[int]] = {}
     for c in phys:
         domains.setdefault(l3_domain(c), []).append(c)
-    # quietest domains first; inside a domain, quietest cores first (stable by id)
-    order = sorted(domains, key=lambda d: (round(sum(load[c] for c in domains[d]) / len(domains[d]), 1), d))
+    # Ranks take consecutive slices of the pool, so the pool runs socket by socket: a rank's
+    # L3 domains then share a socket whenever its slice fits in one (L3 ids alternate between
+    # the sockets on the 2-socket EPYC node, so id order alone spread a 2-domain rank over
+    # both). Quietest socket first; inside it quietest domains first; inside a domain quietest
+    # cores first (each stable by id).
+    def dom_load(d: int) -> float:
+        return round(sum(load[c] for c in domains[d]) / len(domains[d]), 1)
+    sockets: dict[int, list[int]] = {}
+    for d in domains:
+        sockets.setdefault(package_of(domains[d][0]), []).append(d)
+    sock_order = sorted(sockets, key=lambda k: (round(sum(dom_load(d) for d in sockets[k]) / len(sockets[k]), 1), k))
+    order = [d for k in sock_order for d in sorted(sockets[k], key=lambda d: (dom_load(d), d))]
     pool = []
     for d in order:
         pool.extend(sorted(domains[d], key=lambda c: (round(load[c], 1), c)))
@@ -321,8 +341,12 @@ def plan_mirrored(weights: dict[str, int], total: int | None = None, avoid_busy:
     (SO_INCOMING_CPU) then keeps each hop inside one L3: a connection lands on a worker in
     the domain of the thread that opened it. Returns {name: [cores...]}, each non-empty.
     """
+    return split_mirrored(plan_node(1, total, avoid_busy=avoid_busy)[0], weights)
+
+
+def split_mirrored(cores: list[int], weights: dict[str, int]) -> dict[str, list[int]]:
+    """plan_mirrored's split of a given CPU set (e.g. the CPUs a bench rank already owns)."""
     names = list(weights)
-    cores = plan_node(1, total, avoid_busy=avoid_busy)[0]
     by_dom: dict[int, list[int]] = {}
     for c in cores:
         by_dom.setdefault(l3_domain(c), []).append(c)

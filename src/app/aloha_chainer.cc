@@ -253,7 +253,10 @@ void AlohaChainer::call(http::Worker& w, const tracing::SpanContext* parent,
   // between them.
   const int timeout_ms = timeout_ms_.load(std::memory_order_relaxed);
   if (timeout_ms <= 0) return;
-  const WorkerCalls::Pending e{start_ms + timeout_ms, slot, gen};
+  // Deadlines are kept on mono_ms(), the clock arm() and expire() compare them with: start_ms
+  // is the loop pass's time (LoopClock), taken before the events handled so far in this pass,
+  // so a deadline built on it would fire early by that much.
+  const WorkerCalls::Pending e{mono_ms() + timeout_ms, slot, gen};
   if (wc.fifo.empty() || wc.fifo.back().deadline_ms <= e.deadline_ms) {
     wc.fifo.push_back(e);
   } else {

@@ -64,6 +64,8 @@ struct AlohaOptions {
 
 class AlohaChainer final : public Chainer {
  public:
+  // `clock` times the Hystrix command (latencies, the breaker's window) and must be monotonic
+  // and on mono_ms()'s scale: the timeout deadlines themselves are kept on mono_ms().
   AlohaChainer(AlohaOptions o, resilience::Settings s, int num_workers, tracing::Tracer* tracer,
                const Clock& clock = LoopClock::instance());
   ~AlohaChainer() override;

@@ -121,6 +121,9 @@ bool AddressCache::get(sockaddr_storage* out, socklen_t* len, std::string* err) 
 // ---------------------------------------------------------------- connection
 
 constexpr int kTransportRetries = 3;  // DefaultHttpRequestRetryHandler(3, false)
+// How long the calls queued behind an abandoned pipelined call wait for its answer before they
+// are re-sent on fresh connections (see ClientPool::cancel).
+constexpr int kDrainGraceMs = 50;
 
 struct ClientPool::Conn final : EventLoop::Handler {
   enum State { kConnecting, kWriting, kReading, kIdle, kDead };
@@ -166,6 +169,8 @@ struct ClientPool::PConn final : EventLoop::Handler {
   int fd = -1;
   bool connecting = false, dead = false, dirty = false;
   bool draining = false;  // a call on it was abandoned: no new calls; closes once none waits
+  bool drain_timer = false;  // the head-of-line check (ClientPool::cancel) is armed
+  uint64_t cid = 0;          // tells this connection from a later one (timers look it up)
   std::string out, in;
   size_t off = 0;
   std::deque<Pending> q;
@@ -671,6 +676,7 @@ void ClientPool::cancel(uint64_t id) {
     pactive_.erase(pt);
     c->draining = true;
     if (std::all_of(c->q.begin(), c->q.end(), [](const PConn::Pending& p) { return p.abandoned; })) pdestroy(c);
+    else check_head_of_line(c);
     if (!read_fifo_.q.empty()) pop_finished(read_fifo_);
     if (!connect_fifo_.q.empty()) pop_finished(connect_fifo_);
     return;
@@ -686,6 +692,30 @@ void ClientPool::cancel(uint64_t id) {
 
 // ---------------------------------------------------------------- pipelined connections
 
+void ClientPool::check_head_of_line(PConn* c) {
+  // The wait for an abandoned call's answer is bounded: responses come back in order, so a
+  // slow answer at the head would hold every call queued behind it until each hits its own
+  // timeout (a Hystrix TIMEOUT that counts against the breaker). If the abandoned call is
+  // still at the head after kDrainGraceMs, the calls behind it are re-sent on fresh
+  // connections (a transport re-send, as when the connection fails); while an abandoned call
+  // still waits further back, the check runs again.
+  if (c->dead || c->drain_timer) return;
+  if (std::none_of(c->q.begin(), c->q.end(), [](const PConn::Pending& p) { return p.abandoned; })) return;
+  c->drain_timer = true;
+  const uint64_t cid = c->cid;
+  loop_.add_timer(kDrainGraceMs, [this, cid] {
+    auto it = std::find_if(pconns_.begin(), pconns_.end(), [cid](const PConn* p) { return p->cid == cid; });
+    if (it == pconns_.end()) return;  // closed meanwhile
+    PConn* pc = *it;
+    pc->drain_timer = false;
+    if (pc->dead || pc->q.empty()) return;
+    if (pc->q.front().abandoned)
+      pfail(pc, "NoHttpResponseException: the answer ahead on a pipelined connection did not come");
+    else
+      check_head_of_line(pc);
+  });
+}
+
 
 ClientPool::PConn* ClientPool::open_pconn() {
   sockaddr_storage ss{};
@@ -696,6 +726,7 @@ ClientPool::PConn* ClientPool::open_pconn() {
   if (fd < 0) return nullptr;
   auto* c = new PConn();
   c->pool = this;
+  c->cid = next_cid_++;
   c->fd = fd;
   c->connecting = inprog;
   c->interest = inprog ? uint32_t(EPOLLOUT) : uint32_t(EPOLLIN | EPOLLRDHUP);

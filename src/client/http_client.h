@@ -153,6 +153,8 @@ class ClientPool {
   PConn* open_pconn();
   void flush_dirty();
   void pdestroy(PConn* c);
+  void check_head_of_line(PConn* c);
+  uint64_t next_cid_ = 1;
   // Ends a pipelined connection. The request `failed` (if any: timed out, or answered with a
   // malformed or truncated response) fails with `why` (`failed_retryable` = no valid response
   // head arrived, so Feign may retry it). Every other request still waiting on the connection

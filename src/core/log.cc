@@ -71,7 +71,23 @@ constexpr int kIdlePolls = 10;  // empty polls in a row before the writer sleeps
 constexpr auto kIdleSleep = std::chrono::milliseconds(50);
 }  // namespace
 
-Logger::Logger() : th_([this] { run(); }) { pthread_setname_np(th_.native_handle(), "hola-log"); }
+Logger::Logger() {
+  // The writer may be started before main() blocks its termination signals (`--log-level`
+  // touches the logger while the flags are parsed). A process-directed SIGTERM must never be
+  // delivered there, where its default action would kill the process: main takes it with
+  // sigwait/sigtimedwait. So they are blocked before the thread exists (it inherits the mask:
+  // no window after its start), and only they: SIGPROF (--cpu-profile samples the writer too)
+  // and the stall reports' capture signal stay deliverable.
+  sigset_t term, saved;
+  sigemptyset(&term);
+  sigaddset(&term, SIGTERM);
+  sigaddset(&term, SIGINT);
+  sigaddset(&term, SIGHUP);
+  pthread_sigmask(SIG_BLOCK, &term, &saved);
+  th_ = std::thread([this] { run(); });
+  pthread_sigmask(SIG_SETMASK, &saved, nullptr);
+  pthread_setname_np(th_.native_handle(), "hola-log");
+}
 
 Logger::~Logger() {
   {
@@ -230,13 +246,6 @@ void Logger::flush() {
 }
 
 void Logger::run() {
-  // The writer may be started before main() blocks its termination signals (`--log-level`
-  // touches the logger while the flags are parsed). A process-directed SIGTERM must never be
-  // delivered here, where its default action would kill the process: main takes it with
-  // sigwait/sigtimedwait.
-  sigset_t all;
-  sigfillset(&all);
-  pthread_sigmask(SIG_BLOCK, &all, nullptr);
   std::string out;
   int idle = 0;
   for (;;) {

@@ -912,3 +912,28 @@ def test_read_timeout_runs_after_a_slow_connect(hola):
     t.join()
     for c in accepted + [filler, filler2, lsock]:
         c.close()
+
+
+def test_pipelined_calls_behind_a_slow_answer_are_not_held_to_their_timeouts(hola, aloha):
+    """One slow aloha answer, then fast ones, on a shared pipelined connection: the
+    slow call times out on its own 600 ms Hystrix deadline, and the calls queued behind it are
+    re-sent on fresh connections shortly after (kDrainGraceMs) instead of waiting for the slow
+    answer until their own deadlines: they succeed, no extra TIMEOUT reaches the breaker."""
+    aloha.set_mode("slow_once", delay_s=3.0)
+    s = hola(args=["--aloha-url", aloha.url, "--no-tracing", "--feign-log", "none", "--feign-retry", "off",
+                   "-Dhystrix.command.default.circuitBreaker.enabled=false"] + _PIPE, env={"HOSTNAME": "h"},
+             threads=1)
+    slow = {}
+    t = threading.Thread(target=lambda: slow.update(r=chain(s)), daemon=True)
+    t.start()
+    time.sleep(0.3)  # the slow call is on the connection; the next calls queue behind it
+    t0 = time.monotonic()
+    res = _concurrent_chains(s, 3)
+    took = time.monotonic() - t0
+    t.join(timeout=5)
+    assert slow["r"][1:] == [FALLBACK]
+    assert all(st == 200 and body[1] == "Aloha mai aloha-1" for st, body in res), res
+    assert took < 1.5, took  # re-sent ~50 ms after the slow call was abandoned (at ~0.3 s from t0)
+    ev = _events(s)
+    assert ev.get("TIMEOUT") == 1 and ev.get("SUCCESS") == 3, ev
+    assert _retries(s).get("transport", 0) == 3  # each queued call went out once more

@@ -201,3 +201,21 @@ def test_one_thread_per_rank_drives_same_l3_replicas(epyc):
         for x in cpu.connection_targets(p["thread_targets"], 64):
             per_replica[x] += 1
     assert per_replica == [64] * n
+
+
+def test_a_rank_stays_in_one_socket_when_l3_ids_alternate(epyc, monkeypatch):
+    """The 2-socket box numbers its L3 domains alternately across the sockets, so taking
+    domains in id order gave a 16-core rank one CCD on each socket (found by the box's
+    8-slot plan test). The planner now fills socket by socket."""
+    monkeypatch.setattr(cpu, "cgroup_cpu_quota", lambda: 0.0)
+    monkeypatch.setattr(cpu, "package_of", lambda c: ((c % 128) // 8) % 2)
+    plans = cpu.plan_replicas_with_loadgen(8, 16, smt="pair")
+    for p in plans:
+        assert len({cpu.package_of(c) for c in p["server"]}) == 1, p["server"]
+    servers = [c for p in plans for c in p["server"]]
+    assert len(servers) == len(set(servers)) == 128
+    # quietest socket first: a busy socket 0 moves a single rank to socket 1
+    for c in range(256):
+        epyc[c] = 1.0 if cpu.package_of(c) == 0 else 0.0
+    one = cpu.plan_node(1, 16)[0]
+    assert {cpu.package_of(c) for c in one} == {1}

@@ -21,8 +21,8 @@ def test_native_module_loaded_from_tree(native):
 @pytest.mark.gpu
 def test_bench_json_contract_on_host():
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--steps", "3", "--warmup", "1",
-                        "--reqs-per-conn", "200"], capture_output=True, text=True, timeout=600,
-                       env={**os.environ, "HOLA_BENCH_PORT": "18700"})
+                        "--reqs-per-conn", "200", "--c1-seconds", "2", "--chain-seconds", "2"],
+                       capture_output=True, text=True, timeout=600, env={**os.environ, "HOLA_BENCH_PORT": "18700"})
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.strip()]
     assert len(lines) == 1, r.stdout[-2000:]  # the driver's contract: ONE JSON line
@@ -43,6 +43,15 @@ def test_bench_json_contract_on_host():
     assert "--shutdown-delay-ms 5000" in out["deployed_args"] and "--busy-poll-us auto" in out["deployed_args"]
     assert out["config"]["smt"] in ("off", "split", "pair") and "GPU slot" in out["config"]["layout_note"]
     assert abs(sum(out["locality"]["fraction"].values()) - 1.0) < 1e-3
+    # config 2 carries its own host load
+    assert set(out["c1_host_load"]) == {"own", "siblings"}
+    # ... and GET /api/hola-chaining through two replicas: every call a Hystrix SUCCESS, no
+    # fallback or timeout, every body (three greetings, two hops) checked
+    assert out["chain_errors"] == 0 and out["chain_non2xx"] == 0 and out["chain_rps"] > 10000, out
+    assert out["chain_body_checked"] == out["chain_requests"] and out["chain_body_mismatch"] == 0
+    assert out["chain_hystrix_fallback"] == 0 and out["chain_hystrix_timeout"] == 0
+    assert out["chain_hystrix_success"] >= out["chain_requests"]  # its warm-up counts too
+    assert out["chain_a_cpu_us_per_req"] > 0
 
 
 @pytest.mark.gpu
@@ -51,7 +60,8 @@ def test_bench_two_ranks_on_host():
     replicas, cross-rank L3-aware load-generator placement) on the real host."""
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", "29517", str(ROOT / "bench.py"),
-                        "--gpus", "2", "--steps", "3", "--warmup", "1", "--reqs-per-conn", "500"],
+                        "--gpus", "2", "--steps", "3", "--warmup", "1", "--reqs-per-conn", "500",
+                        "--c1-seconds", "1", "--deployed-seconds", "0", "--chain-seconds", "0"],
                        capture_output=True, text=True, timeout=600,
                        env={**os.environ, "HOLA_BENCH_PORT": "18760"})
     assert r.returncode == 0, r.stderr[-3000:]
@@ -74,7 +84,8 @@ def test_tracing_as_deployed_on_host():
     reference image. Spans beyond the Brave-parity budget are dropped and counted, the rest
     reach the collector, and the request path does not slow down."""
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--steps", "4", "--warmup", "1",
-                        "--reqs-per-conn", "20000", "--c1-seconds", "0", "--zipkin-sink"],
+                        "--reqs-per-conn", "20000", "--c1-seconds", "0", "--deployed-seconds", "0",
+                        "--chain-seconds", "0", "--zipkin-sink"],
                        capture_output=True, text=True, timeout=600, env={**os.environ, "HOLA_BENCH_PORT": "18720"})
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads(r.stdout.strip().splitlines()[-1])
@@ -89,7 +100,8 @@ def test_tracing_as_deployed_on_host():
 def test_pipelined_bench_on_host():
     """`bench.py --pipeline 16` on the real host: 16 requests share each loopback segment."""
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--pipeline", "16", "--steps", "2", "--warmup", "1",
-                        "--reqs-per-conn", "16000"], capture_output=True, text=True, timeout=300,
+                        "--reqs-per-conn", "16000", "--c1-seconds", "0", "--deployed-seconds", "0",
+                        "--chain-seconds", "0"], capture_output=True, text=True, timeout=300,
                        env={**os.environ, "HOLA_BENCH_PORT": "18780"})
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads(r.stdout.strip().splitlines()[-1])
@@ -135,3 +147,73 @@ def test_manifests_execute_on_host():
     assert res["rollout_with_delay"]["requests"] > 10000
     assert res["sigkill"]["restarts"] == 1
     assert res["configmap_edit_all_pods_s"] < 60
+
+
+def _node_plan(slots: int) -> dict:
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--plan-only", "--gpu-slots", str(slots),
+                        "--ignore-quota"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+@pytest.mark.gpu
+def test_eight_slot_plan_on_the_real_topology():
+    """The 8-GPU node's layout (SCALE N = 8), planned on this host's real topology with the
+    box's CPU quota set aside: 8 replica slots of 16 physical cores,
+    every CPU used once; each replica's server workers inside one socket, on L3 domains no
+    other replica's workers use; and with --smt pair every load-generator thread on the other
+    SMT thread of a core of the replica it drives (the client and the worker serving its
+    connections share that physical core)."""
+    from hola_amd.utils.cpu import physical_cores
+
+    if len(physical_cores()) < 128:
+        pytest.skip("the 8-slot layout needs the node's 2 x 64 physical cores")
+    plan = _node_plan(8)
+    ranks = plan["ranks"]
+    assert plan["gpu_slots"] == 8 and len(ranks) == 8 and plan["smt"] == "pair", plan["smt"]
+    assert plan["cores_per_slot"] == 16
+    used = [c for r in ranks for c in r["server"] + r["loadgen"]]
+    assert len(used) == len(set(used)) == 256, "a CPU planned twice"
+    l3_owner: dict[int, int] = {}
+    for i, r in enumerate(ranks):
+        assert len(r["server"]) == len(r["loadgen"]) == 16
+        assert len(r["server_sockets"]) == 1, (i, r["server_sockets"])
+        for d in r["server_l3"]:
+            assert l3_owner.setdefault(d, i) == i, f"L3 {d} holds workers of replicas {l3_owner[d]} and {i}"
+    for i, r in enumerate(ranks):
+        assert r["thread_targets"], i
+        for t, l_cpu in enumerate(r["loadgen"]):
+            target = ranks[r["thread_targets"][t][0]]
+            sib = set(r["siblings"][str(l_cpu)]) - {l_cpu}
+            assert sib & set(target["server"]), (i, t, l_cpu)
+    out = ROOT / "gpurun_out" / "plan8.json"
+    out.parent.mkdir(exist_ok=True)
+    out.write_text(json.dumps(plan, indent=1))
+
+
+@pytest.mark.gpu
+def test_eight_ranks_run_under_the_node_plan():
+    """The N = 8 torchrun command under the 8-slot plan for a couple of tiny steps. Inside
+    the box's 16-CPU quota the 256 threads are squeezed, so the throughput means nothing (no
+    scaling curve is measured here); what is checked is that the layout runs end to end with
+    no errors, and that accept steering puts each connection on the worker that shares its
+    client thread's physical core."""
+    from hola_amd.utils.cpu import physical_cores
+
+    if len(physical_cores()) < 128:
+        pytest.skip("the 8-slot layout needs the node's 2 x 64 physical cores")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+                        "--master-addr", "127.0.0.1", "--master-port", "29537", str(ROOT / "bench.py"),
+                        "--gpus", "8", "--gpu-slots", "8", "--ignore-quota", "--steps", "2", "--warmup", "1",
+                        "--reqs-per-conn", "200", "--busy-poll-us", "0", "--c1-seconds", "0",
+                        "--deployed-seconds", "0", "--chain-seconds", "0"],
+                       capture_output=True, text=True, timeout=300,
+                       env={**os.environ, "HOLA_BENCH_PORT": "18800", "HOLA_BENCH_CUDA_SYNC": "0"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    (ROOT / "gpurun_out").mkdir(exist_ok=True)
+    (ROOT / "gpurun_out" / "n8_plan_run.json").write_text(json.dumps(out, indent=1))
+    assert out["n_gpus"] == 8 and out["config"]["smt"] == "pair" and out["config"]["gpu_slots_on_node"] == 8
+    assert out["requests"] == 8 * 64 * 200 * 2
+    assert out["errors"] == 0 and out["non2xx"] == 0 and out["body_mismatch"] == 0
+    assert out["locality"]["fraction"]["same_core"] >= 0.9, out["locality"]
