@@ -106,7 +106,7 @@ struct AlohaChainer::Call {
   bool has_parent = false;
   tracing::SpanContext ctx;  // client span of the current execution
   bool traced = false;
-  std::function<void(const ChainResult&)> cb;
+  ChainDone cb;
 };
 
 // Per worker, touched only on its loop thread. Every call's execution timeout has the same
@@ -215,7 +215,7 @@ ChainResult AlohaChainer::failed_result(const char* why) const {
 }
 
 void AlohaChainer::call(http::Worker& w, const tracing::SpanContext* parent,
-                        std::function<void(const ChainResult&)> done) {
+                        ChainDone done) {
   const int64_t start_ms = clock_.now_ms();
   Command* cmd = cmd_.get();
   if (!url_ok_) {

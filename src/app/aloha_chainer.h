@@ -74,7 +74,7 @@ class AlohaChainer final : public Chainer {
   void stop();
 
   void call(http::Worker& w, const tracing::SpanContext* parent,
-            std::function<void(const ChainResult&)> done) override;
+            ChainDone done) override;
 
   resilience::Command& command() { return *cmd_; }
   void update_settings(const resilience::Settings& s) {

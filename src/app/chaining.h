@@ -2,11 +2,12 @@
 // handler asks a Chainer for aloha's greetings and gets either the decoded list or the
 // Hystrix fallback `["Aloha response (fallback)"]` (HolaResource.java:111-112).
 #pragma once
-#include <functional>
 #include <optional>
 #include <string>
 #include <string_view>
 #include <vector>
+
+#include "core/inline_function.h"
 
 namespace hola::http {
 class Worker;
@@ -32,6 +33,10 @@ struct ChainResult {
   std::string reason;  // why the fallback was used (timeout, short-circuited, ...)
 };
 
+// The continuation of a parked /api/hola-chaining request: its captures (connection,
+// content, server span, start time) live inline, so a call allocates nothing for it.
+using ChainDone = InlineFunction<void(const ChainResult&), 256>;
+
 class Chainer {
  public:
   virtual ~Chainer() = default;
@@ -39,7 +44,7 @@ class Chainer {
   // before call() returns: Hystrix runs the fallback of a short-circuited or rejected command
   // on the caller's thread, and so does this (no timer round trip).
   virtual void call(http::Worker& w, const tracing::SpanContext* parent,
-                    std::function<void(const ChainResult&)> done) = 0;
+                    ChainDone done) = 0;
 };
 
 }  // namespace hola::app

@@ -198,7 +198,7 @@ void ClientPool::Conn::fail(const std::string& why, bool io) {
     std::string r = std::move(out);
     const int t = tries + 1;
     if (p->transport_retries_) p->transport_retries_->fetch_add(1, std::memory_order_relaxed);
-    p->active_.erase(rid);
+    p->untrack(rid);
     p->destroy(this);
     auto* fresh = new Conn();
     fresh->pool = p;
@@ -366,7 +366,8 @@ void ClientPool::Conn::do_read() {
       fail(std::string("SocketException: ") + strerror(errno));
       return;
     }
-    ClientResult r;
+    ClientResult& r = pool->scratch_;
+    r.clear();
     bool keep = false;
     int rc = try_parse(&r, &keep, eof);
     if (rc < 0) {
@@ -572,7 +573,7 @@ void ClientPool::start_on(Conn* c, uint64_t id, std::string* req, Callback cb, b
   c->in.clear();
   c->reused = reused;
   c->head_ok = false;
-  active_[id] = c;
+  track(id, c);
   if (reused) {
     c->st = Conn::kWriting;
     arm_read_deadline(id, c->serial);
@@ -630,8 +631,25 @@ void ClientPool::arm_read_deadline(uint64_t id, uint64_t serial) {
   if (rt > 0) push_deadline(read_fifo_, rt, id, serial);
 }
 
+void ClientPool::track(uint64_t id, Conn* c) {
+  if (spare_nodes_.empty()) {
+    active_.emplace(id, c);
+    return;
+  }
+  auto nh = std::move(spare_nodes_.back());
+  spare_nodes_.pop_back();
+  nh.key() = id;
+  nh.mapped() = c;
+  active_.insert(std::move(nh));
+}
+
+void ClientPool::untrack(std::unordered_map<uint64_t, Conn*>::iterator it) {
+  auto nh = active_.extract(it);
+  if (spare_nodes_.size() < 1024) spare_nodes_.push_back(std::move(nh));
+}
+
 void ClientPool::finish(Conn* c, ClientResult&& r, bool reusable) {
-  active_.erase(c->id);
+  untrack(c->id);
   if (!read_fifo_.q.empty()) pop_finished(read_fifo_);
   if (!connect_fifo_.q.empty()) pop_finished(connect_fifo_);
   Callback cb = std::move(c->cb);
@@ -684,7 +702,7 @@ void ClientPool::cancel(uint64_t id) {
   auto it = active_.find(id);
   if (it == active_.end()) return;
   Conn* c = it->second;
-  active_.erase(it);
+  untrack(it);
   destroy(c);
   if (!read_fifo_.q.empty()) pop_finished(read_fifo_);
   if (!connect_fifo_.q.empty()) pop_finished(connect_fifo_);

@@ -63,6 +63,16 @@ struct ClientResult {
   // RetryableException.
   bool has_retry_after = false;
   int64_t retry_after_ms = 0;
+  // Back to a default result, keeping the strings' capacity (the pool reuses one result for
+  // every response it reads, so a body costs no allocation).
+  void clear() {
+    ok = retryable = has_retry_after = false;
+    status = 0;
+    retry_after_ms = 0;
+    reason.clear();
+    body.clear();
+    error.clear();
+  }
 };
 
 // Retry-After value (delta-seconds or RFC 1123 date) as milliseconds from now_ms (wall
@@ -116,6 +126,17 @@ class ClientPool {
   size_t max_idle_;
   std::vector<Conn*> idle_;
   std::unordered_map<uint64_t, Conn*> active_;
+  // Map nodes of finished requests, reused for the next ones: a request in flight costs no
+  // allocation for its entry.
+  std::vector<std::unordered_map<uint64_t, Conn*>::node_type> spare_nodes_;
+  void track(uint64_t id, Conn* c);
+  void untrack(std::unordered_map<uint64_t, Conn*>::iterator it);
+  void untrack(uint64_t id) {
+    if (auto it = active_.find(id); it != active_.end()) untrack(it);
+  }
+  // The result every plain connection parses its responses into (see ClientResult::clear).
+  // A callback only reads it before returning, and no read runs inside a callback.
+  ClientResult scratch_;
   uint64_t next_id_ = 1;
   uint64_t opened_ = 0;
   std::string host_header_;
