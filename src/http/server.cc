@@ -738,8 +738,10 @@ std::string Server::stall_report(size_t i, bool with_stack) {
   const uint64_t p0 = workers_[i]->loop().activity().passes.load(std::memory_order_relaxed);
   std::this_thread::sleep_for(std::chrono::milliseconds(100));
   const uint64_t p1 = workers_[i]->loop().activity().passes.load(std::memory_order_relaxed);
-  std::string out = activity(i) + (p1 == p0 ? "; passes NOT advancing over 100 ms" : "; passes advancing (" +
-                                                  std::to_string(p1 - p0) + " in 100 ms)");
+  const bool waiting = workers_[i]->loop().activity().phase.load(std::memory_order_relaxed) == EventLoop::kWait;
+  std::string out = activity(i) + (p1 != p0 ? "; passes advancing (" + std::to_string(p1 - p0) + " in 100 ms)"
+                                   : waiting ? "; idle in epoll_wait over 100 ms"
+                                             : "; passes NOT advancing over 100 ms");
   const int tid = workers_[i]->tid_.load();
   if (with_stack && tid == 0) out += "; thread exited";
   if (with_stack && tid > 0) {

@@ -27,6 +27,11 @@
 #include "core/loop.h"
 #include "core/clock.h"
 #include "core/log.h"
+#include "core/cpuprof.h"
+#include "http/server.h"
+
+#include <sys/socket.h>
+#include <unistd.h>
 
 namespace py = pybind11;
 using namespace hola;
@@ -361,6 +366,62 @@ uint64_t log_stress(int threads, int lines, const std::string& tag, bool prebuil
   return l.dropped() - d0;
 }
 
+// A handler that never returns while `hold` is set: the state of a livelocked worker (a loop
+// stuck inside one connection's handler). The spin is a named, never-inlined function so a
+// captured stack can be checked for it.
+std::atomic<bool> g_spinning{false};
+}  // namespace
+// Exported (not in the anonymous namespace) so that symbolisers find its name in the module.
+extern "C" __attribute__((noinline, visibility("default"))) void hola_stall_probe_spin(const std::atomic<bool>* hold) {
+  g_spinning.store(true);
+  while (hold->load(std::memory_order_relaxed)) __builtin_ia32_pause();
+  asm volatile("" ::: "memory");  // keep a frame of its own
+}
+namespace {
+struct SpinHandler : http::RequestHandler {
+  std::atomic<bool> hold{true};
+  void on_request(http::Connection& c, const http::Request& r) override {
+    if (r.path == "/spin") hola_stall_probe_spin(&hold);
+    static constexpr std::string_view k = "HTTP/1.1 200 OK\r\nContent-Length: 2\r\n\r\nok";
+    c.send(k);
+  }
+};
+
+// Server::stall_report of a worker stuck in a handler: one worker, one connection whose
+// request spins in the handler; returns (report while stuck, report after release).
+std::pair<std::string, std::string> stall_report_probe() {
+  py::gil_scoped_release nogil;
+  cpuprof::enable_capture();
+  SpinHandler h;
+  http::ServerOptions so;
+  so.host = "127.0.0.1";
+  so.port = 0;
+  so.threads = 1;
+  so.idle_timeout_ms = 0;
+  http::Server s(so, &h);
+  std::string err;
+  if (!s.bind(&err)) throw std::runtime_error(err);
+  s.start();
+  g_spinning.store(false);
+  sockaddr_storage ss{};
+  socklen_t len = 0;
+  if (!resolve_host("127.0.0.1", s.port(), &ss, &len, &err)) throw std::runtime_error(err);
+  int fd = connect_blocking(ss, len, 2000);
+  if (fd < 0) throw std::runtime_error("connect");
+  static constexpr std::string_view req = "GET /spin HTTP/1.1\r\nHost: x\r\n\r\n";
+  if (!write_all(fd, req.data(), req.size())) throw std::runtime_error("send");
+  while (!g_spinning.load()) std::this_thread::sleep_for(std::chrono::milliseconds(1));
+  std::string stuck = s.stall_report(0, true);
+  h.hold.store(false);
+  char buf[256];
+  (void)::recv(fd, buf, sizeof buf, 0);
+  std::string after = s.stall_report(0, false);
+  ::close(fd);
+  s.shutdown(100);
+  s.join();
+  return {stuck, after};
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_native, m) {
@@ -425,6 +486,7 @@ PYBIND11_MODULE(_native, m) {
     if (!app::parse_retry_policy(policy, &p)) return py::none();
     return py::make_tuple(p.backoff_ms(attempt), p.max_attempts);
   }, py::arg("attempt"), py::arg("policy") = "default");
+  m.def("stall_report_probe", &stall_report_probe);
   m.def("loop_timer_order", &loop_timer_order, py::arg("delays"), py::arg("cancel") = std::vector<int>{});
   m.def("span_ring", &span_ring);
   m.def("log_stress", &log_stress, py::arg("threads"), py::arg("lines"), py::arg("tag") = "stress",

@@ -1,6 +1,7 @@
 """Core primitives of the native runtime: latency histogram accuracy, event-loop timer
 ordering/cancellation and cross-thread posts, the SPSC span ring."""
 import random
+from pathlib import Path
 
 
 def test_histogram_relative_error(native):
@@ -111,3 +112,24 @@ def test_logger_drops_and_counts_when_a_ring_overflows(native, capfd):
     got = [int(l.split()[2]) for l in err.splitlines() if l.startswith("burst 0 ")]
     assert len(got) + dropped == 200000
     assert got == sorted(got)
+
+
+def test_stall_report_names_a_handler_that_never_returns(native):
+    """A worker stuck inside one connection's handler (a livelock: the thread runs, its loop
+    never comes back to epoll): the stall report says the loop's passes have stopped in the
+    events phase, names the connection, and the stack captured by signal from the stuck thread
+    reaches the spinning function. Once released, the loop is idle again."""
+    import re
+    import subprocess
+
+    stuck, after = native.stall_report_probe()
+    assert re.match(r"worker 0: pass \d+, phase events, .*last handler connection \w+ \{[a-z_,]*\}", stuck), stuck
+    assert "passes NOT advancing over 100 ms" in stuck
+    frames = re.findall(r"#\d+ (\S+)\+0x([0-9a-f]+)", stuck)
+    lib = Path(native.__file__)
+    own = [off for obj, off in frames if obj == lib.name]
+    assert own, stuck
+    names = subprocess.run(["addr2line", "-f", "-C", "-e", str(lib), *[f"0x{o}" for o in own]],
+                           capture_output=True, text=True).stdout
+    assert "hola_stall_probe_spin" in names and "Connection::process" in names, names
+    assert "phase wait" in after and "idle in epoll_wait" in after, after
