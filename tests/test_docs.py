@@ -11,7 +11,7 @@ OPS = (ROOT / "docs" / "OPERATIONS.md").read_text()
 
 def test_operations_metrics_are_exported(hola):
     # (the package and the native binaries are not metrics)
-    names = set(re.findall(r"`(hola_[a-z_]+)", OPS)) - {"hola_amd", "hola_loadgen", "hola_rrproxy", "hola_zipkin_sink"}
+    names = set(re.findall(r"`(hola_[a-z_]+)", OPS)) - {"hola_amd", "hola_loadgen", "hola_rrproxy", "hola_zipkin_sink", "hola_fpstack"}
     with FakeAloha() as aloha, FakeZipkin() as zipkin:
         s = hola(args=["--aloha-url", aloha.url, "--zipkin-url", zipkin.url, "--feign-log", "none",
                        "--busy-poll-us", "auto"])  # the spin counters exist only while spinning adapts
@@ -30,6 +30,26 @@ def test_operations_flags_are_accepted(hola_bin):
     help_text = subprocess.run([str(hola_bin), "--help"], capture_output=True, text=True).stdout + \
         subprocess.run([str(hola_bin), "--help"], capture_output=True, text=True).stderr
     flags = set(re.findall(r"`(--[a-z][a-z0-9-]+)", OPS)) - {"--replicas", "--out", "--lb", "--minutes", "--zipkin-sink",
-                                                              "--profile-out"}
+                                                              "--profile-out", "--proxy-threads"}
     missing = sorted(f for f in flags if f not in help_text)
     assert not missing, missing
+
+
+def test_bench_describes_the_deployed_replica_as_it_runs():
+    """bench.py's deployed_* sub-run starts the replica with the manifests' container args;
+    its docstring must describe exactly those (it said "no busy-polling"
+    while the manifests pass --busy-poll-us auto)."""
+    import yaml
+
+    dc = next(o for o in yaml.safe_load((ROOT / "deploy/openshift/hola-dc.yaml").read_text())["items"]
+              if o["kind"] == "DeploymentConfig")
+    args = dc["spec"]["template"]["spec"]["containers"][0]["args"]
+    pairs = [f"{args[i]} {args[i + 1]}" for i in range(0, len(args), 2)]
+    bench = (ROOT / "bench.py").read_text()
+    doc = bench.split('"""')[1]
+    flat = " ".join(doc.split())
+    for p in pairs:
+        assert f"`{p}" in flat or f"{p}`" in flat or p in flat, (p, flat)
+    assert "no busy-polling" not in bench and "no busy polling" not in bench
+    # the key comment next to deployed_* in the JSON
+    assert all(p in " ".join(bench.split("**_deployed_keys(deployed)")[0].split()[-40:]) for p in pairs)
