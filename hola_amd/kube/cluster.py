@@ -49,6 +49,7 @@ import time
 from pathlib import Path
 
 from hola_amd import native
+from hola_amd.utils.cpu import cpu_budget
 from hola_amd.kube import manifests as m
 from hola_amd.kube.image import Image
 from hola_amd.kube.kubelet import Kubelet, Pod, die_with_parent, project_configmap
@@ -91,8 +92,9 @@ class Cluster:
         self.allocatable = self.node_cpus - len(self.reserved)
         # The userspace Service proxy carries every request twice (in and out), so a fixed 2
         # threads capped a rollout under load at ~160 k req/s (profiles/round3/13_kube): by
-        # default it gets a quarter of the node's CPUs, 2 to 16 threads.
-        self.proxy_threads = proxy_threads or max(2, min(16, len(self.real_cpus) // 4))
+        # default it gets a quarter of the CPUs this executor may keep busy (its affinity mask
+        # within any cgroup quota), 2 to 16 threads.
+        self.proxy_threads = proxy_threads or max(2, min(16, cpu_budget() // 4))
         self.proxy_cpus = proxy_cpus
         self.service_host, self.service_port_override = service_host, service_port
         self.want_zipkin = zipkin

@@ -740,7 +740,7 @@ std::string Server::stall_report(size_t i, bool with_stack) {
   const uint64_t p1 = workers_[i]->loop().activity().passes.load(std::memory_order_relaxed);
   const bool waiting = workers_[i]->loop().activity().phase.load(std::memory_order_relaxed) == EventLoop::kWait;
   std::string out = activity(i) + (p1 != p0 ? "; passes advancing (" + std::to_string(p1 - p0) + " in 100 ms)"
-                                   : waiting ? "; idle in epoll_wait over 100 ms"
+                                   : waiting ? "; in epoll_wait, no pass over 100 ms"
                                              : "; passes NOT advancing over 100 ms");
   const int tid = workers_[i]->tid_.load();
   if (with_stack && tid == 0) out += "; thread exited";
