@@ -131,12 +131,14 @@ void on_prof(int, siginfo_t*, void* ucv) {
 constexpr int kCaptureSignal = 40;  // a real-time signal no thread blocks (SIGRTMIN is 34)
 std::mutex g_cap_mu;                // one capture at a time
 std::atomic<int> g_cap_state{0};    // 0 idle, 1 requested, 2 done
+std::atomic<int> g_cap_tid{0};      // the thread asked: a late signal to an earlier target is ignored
 uintptr_t g_cap_pcs[kMaxCaptureDepth];
 std::atomic<int> g_cap_depth{0};
 std::atomic<bool> g_cap_installed{false};
 
 void on_capture(int, siginfo_t*, void* ucv) {
   if (g_cap_state.load(std::memory_order_acquire) != 1) return;
+  if (int(syscall(SYS_gettid)) != g_cap_tid.load(std::memory_order_relaxed)) return;
   const int saved_errno = errno;
   g_cap_depth.store(walk(static_cast<const ucontext_t*>(ucv), g_cap_pcs, kMaxCaptureDepth), std::memory_order_relaxed);
   g_cap_state.store(2, std::memory_order_release);
@@ -181,6 +183,7 @@ int capture(int tid, uintptr_t* pcs, int max, int timeout_ms) {
     g_own_range = exec_range(uintptr_t(&on_prof));
   }
   g_cap_depth.store(0);
+  g_cap_tid.store(tid, std::memory_order_relaxed);
   g_cap_state.store(1, std::memory_order_release);
   if (tid <= 0 || syscall(SYS_tgkill, getpid(), tid, kCaptureSignal) != 0) {
     g_cap_state.store(0);

@@ -734,20 +734,34 @@ std::string Server::activity(size_t i) const {
   return out;
 }
 
-std::string Server::stall_report(size_t i, bool with_stack) {
-  const uint64_t p0 = workers_[i]->loop().activity().passes.load(std::memory_order_relaxed);
+std::string Server::stall_report(size_t i, bool with_stack) { return stall_reports({i}, with_stack)[0]; }
+
+std::vector<std::string> Server::stall_reports(const std::vector<size_t>& which, bool with_stack) {
+  // One 100 ms window for all of them (whether each loop's passes advance), then the stacks,
+  // within an overall budget: the exit watchdog reports every worker and must finish well
+  // before the kubelet's SIGKILL.
+  std::vector<uint64_t> p0;
+  for (size_t i : which) p0.push_back(workers_[i]->loop().activity().passes.load(std::memory_order_relaxed));
   std::this_thread::sleep_for(std::chrono::milliseconds(100));
-  const uint64_t p1 = workers_[i]->loop().activity().passes.load(std::memory_order_relaxed);
-  const bool waiting = workers_[i]->loop().activity().phase.load(std::memory_order_relaxed) == EventLoop::kWait;
-  std::string out = activity(i) + (p1 != p0 ? "; passes advancing (" + std::to_string(p1 - p0) + " in 100 ms)"
-                                   : waiting ? "; in epoll_wait, no pass over 100 ms"
-                                             : "; passes NOT advancing over 100 ms");
-  const int tid = workers_[i]->tid_.load();
-  if (with_stack && tid == 0) out += "; thread exited";
-  if (with_stack && tid > 0) {
-    uintptr_t pcs[cpuprof::kMaxCaptureDepth];
-    const int n = cpuprof::capture(tid, pcs, cpuprof::kMaxCaptureDepth);
-    out += n ? "; stack" + cpuprof::describe_pcs(pcs, n) : "; stack: no answer to the capture signal";
+  const int64_t stacks_until = mono_ns() + int64_t(2000) * 1000000;
+  std::vector<std::string> out;
+  for (size_t k = 0; k < which.size(); ++k) {
+    const size_t i = which[k];
+    const EventLoop::Activity& a = workers_[i]->loop().activity();
+    const uint64_t p1 = a.passes.load(std::memory_order_relaxed);
+    const bool waiting = a.phase.load(std::memory_order_relaxed) == EventLoop::kWait;
+    std::string r = activity(i) + (p1 != p0[k] ? "; passes advancing (" + std::to_string(p1 - p0[k]) + " in 100 ms)"
+                                   : waiting  ? "; in epoll_wait, no pass over 100 ms"
+                                              : "; passes NOT advancing over 100 ms");
+    const int tid = workers_[i]->tid_.load();
+    if (with_stack && tid == 0) r += "; thread exited";
+    if (with_stack && tid > 0) {
+      uintptr_t pcs[cpuprof::kMaxCaptureDepth];
+      const int n = mono_ns() < stacks_until ? cpuprof::capture(tid, pcs, cpuprof::kMaxCaptureDepth) : -1;
+      r += n > 0 ? "; stack" + cpuprof::describe_pcs(pcs, n)
+                 : n == 0 ? "; stack: no answer to the capture signal" : "; stack: skipped (report budget spent)";
+    }
+    out.push_back(std::move(r));
   }
   return out;
 }

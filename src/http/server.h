@@ -298,6 +298,8 @@ class Server {
   // A worker that stopped answering: its activity, whether its loop passes advance over the
   // next 100 ms, and (with_stack) its stack captured by signal. Any thread but worker i's.
   std::string stall_report(size_t i, bool with_stack);
+  // The same for several workers at once (one 100 ms window; stacks within a 2 s budget).
+  std::vector<std::string> stall_reports(const std::vector<size_t>& which, bool with_stack);
 
   // Where each accepted connection's client ran (SO_INCOMING_CPU: for loopback clients the
   // CPU of the sending thread) relative to the pinned worker that serves it.

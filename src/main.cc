@@ -427,9 +427,11 @@ int main(int argc, char** argv) {
                              (long long)limit_ms);
       ssize_t w = ::write(2, line, size_t(n));
       // where every event loop was, with its stack (the report that names a stuck handler)
-      for (size_t i = 0; i < server.num_workers(); ++i) {
-        const std::string r = "hola: " + server.stall_report(i, true) + "\n";
-        w = ::write(2, r.data(), r.size());
+      std::vector<size_t> all(server.num_workers());
+      for (size_t i = 0; i < all.size(); ++i) all[i] = i;
+      for (const std::string& r : server.stall_reports(all, true)) {
+        const std::string line = "hola: " + r + "\n";
+        w = ::write(2, line.data(), line.size());
       }
       (void)w;
       _exit(3);
