@@ -15,6 +15,7 @@
 #   latency            BASELINE config 2 (1 connection) and the open-loop latency curve
 #   chain              two-hop chaining bench (loadgen -> hola A -> hola B)
 #   chainab [REPS]     chaining with Feign BASIC logging on/off, this server vs. PREV_BIN
+#   chainab2 [REPS]    chaining, this server vs. PREV_BIN (BASIC logging), order swapped each round
 #   chainpipe [REPS]   chaining with --aloha-pipeline 8 vs. one request per connection
 #   cpuprof            sampled CPU profiles (hola --cpu-profile) of the headline and of chaining
 #   tracing            headline without a collector, with the native Zipkin sink (default 1000-span
@@ -151,6 +152,23 @@ chainab)
       timeout -k 10 120 python bench/chain_bench.py --duration 8 --feign-log "$log" ${exe:+--exe-a "$exe"} \
         --out "$OUT/${label}_${rep}.json" > "$OUT/${label}_${rep}.log" 2>&1 || exit 1
       python3 -c "import json; d=json.load(open('$OUT/${label}_${rep}.json')); print('$label', $rep, d['rps'], d['p50_ms'], d['p99_ms'], d['cpu_us_per_req']['A'], d['user_share']['A'])" \
+        >> "$OUT/summary.txt"
+    done
+  done
+  cat "$OUT/summary.txt"
+  ;;
+chainab2)
+  # chaining, this server vs PREV_BIN, both with Feign BASIC logging, REPS rounds with the
+  # order of the two sides swapped every round (an order effect would show as a difference
+  # that flips with the order)
+  REPS=${1:-6}; PREV=${PREV_BIN:-build/prev/hola}
+  for rep in $(seq 1 "$REPS"); do
+    if [ $((rep % 2)) -eq 1 ]; then order="new prev"; else order="prev new"; fi
+    for v in $order; do
+      exe=""; [ "$v" = prev ] && exe="$PREV"
+      timeout -k 10 120 python bench/chain_bench.py --duration 8 --feign-log basic ${exe:+--exe-a "$exe"} \
+        --out "$OUT/${v}_${rep}.json" > "$OUT/${v}_${rep}.log" 2>&1 || exit 1
+      python3 -c "import json; d=json.load(open('$OUT/${v}_${rep}.json')); print('$v', $rep, d['rps'], d['p50_ms'], d['p99_ms'], d['cpu_us_per_req']['A'], d['user_share']['A'])" \
         >> "$OUT/summary.txt"
     done
   done
