@@ -198,8 +198,7 @@ void ClientPool::Conn::fail(const std::string& why, bool io) {
     std::string r = std::move(out);
     const int t = tries + 1;
     if (p->transport_retries_) p->transport_retries_->fetch_add(1, std::memory_order_relaxed);
-    p->untrack(rid);
-    p->destroy(this);
+    p->destroy(this);  // the id stays live: start_on points it at the fresh connection
     auto* fresh = new Conn();
     fresh->pool = p;
     fresh->tries = t;
@@ -441,13 +440,16 @@ ClientPool::~ClientPool() {
     if (c->fd >= 0) ::close(c->fd);
     delete c;
   }
-  for (auto& [id, c] : active_) {
+  auto drop = [this](Conn* c) {
     if (c->fd >= 0) {
       loop_.del(c->fd);
       ::close(c->fd);
     }
     delete c;
-  }
+  };
+  for (Slot& sl : slots_)
+    if (sl.conn) drop(sl.conn);
+  for (auto& [id, c] : resent_) drop(c);
 }
 
 std::string ClientPool::build_request(const std::string& path, const std::string& extra) const {
@@ -471,12 +473,52 @@ void ClientPool::build_request_into(std::string* out, const std::string& path, c
   r += "\r\n";
 }
 
-uint64_t ClientPool::get(const std::string& path, const std::string& extra_headers, Callback cb) {
-  uint64_t id = next_id_++;
-  if (pipeline_ > 1) {
-    std::string req = build_request(path, extra_headers);
-    if (get_pipelined(id, req, cb)) return id;
+uint64_t ClientPool::new_id() {
+  uint32_t s;
+  if (!free_slots_.empty()) {
+    s = free_slots_.back();
+    free_slots_.pop_back();
+  } else {
+    s = uint32_t(slots_.size());
+    slots_.emplace_back();
   }
+  return uint64_t(slots_[s].gen & 0x7fffffffu) << 32 | s;
+}
+
+void ClientPool::set_active(uint64_t id, Conn* c) {
+  if (id & kPipeBit) resent_[id] = c;
+  else slots_[uint32_t(id)].conn = c;
+}
+
+ClientPool::Conn* ClientPool::active(uint64_t id) const {
+  if (id & kPipeBit) {
+    auto it = resent_.find(id);
+    return it == resent_.end() ? nullptr : it->second;
+  }
+  const uint32_t s = uint32_t(id);
+  if (s >= slots_.size() || (slots_[s].gen & 0x7fffffffu) != uint32_t(id >> 32)) return nullptr;
+  return slots_[s].conn;
+}
+
+void ClientPool::release(uint64_t id) {
+  if (id & kPipeBit) {
+    resent_.erase(id);
+    return;
+  }
+  const uint32_t s = uint32_t(id);
+  if (s >= slots_.size() || (slots_[s].gen & 0x7fffffffu) != uint32_t(id >> 32)) return;
+  slots_[s].conn = nullptr;
+  ++slots_[s].gen;  // a late timer or cancel with the old id finds nothing
+  free_slots_.push_back(s);
+}
+
+uint64_t ClientPool::get(const std::string& path, const std::string& extra_headers, Callback cb) {
+  if (pipeline_ > 1) {
+    const uint64_t pid = kPipeBit | next_id_++;
+    std::string req = build_request(path, extra_headers);
+    if (get_pipelined(pid, req, cb)) return pid;
+  }
+  const uint64_t id = new_id();
   const bool reused = !idle_.empty();
   Conn* c;
   if (reused) {
@@ -492,8 +534,7 @@ uint64_t ClientPool::get(const std::string& path, const std::string& extra_heade
 }
 
 bool ClientPool::live(const Deadline& d) const {
-  auto it = active_.find(d.id);
-  if (it != active_.end()) return it->second->serial == d.serial;
+  if (const Conn* c = active(d.id)) return c->serial == d.serial;
   auto pt = pactive_.find(d.id);
   return pt != pactive_.end() && pt->second.serial == d.serial;
 }
@@ -546,7 +587,7 @@ void ClientPool::expire(DeadlineFifo& f) {
                       " failed: connect timed out", 0, true, false);
       continue;
     }
-    Conn* c = active_.find(d.id)->second;
+    Conn* c = active(d.id);
     // fail() runs the callback, which may start (and push deadlines for) further requests
     if (f.connect) {
       if (c->st == Conn::kConnecting)
@@ -573,7 +614,7 @@ void ClientPool::start_on(Conn* c, uint64_t id, std::string* req, Callback cb, b
   c->in.clear();
   c->reused = reused;
   c->head_ok = false;
-  track(id, c);
+  set_active(id, c);
   if (reused) {
     c->st = Conn::kWriting;
     arm_read_deadline(id, c->serial);
@@ -587,12 +628,12 @@ void ClientPool::start_on(Conn* c, uint64_t id, std::string* req, Callback cb, b
     // Report asynchronously: callers expect the callback after get() returns.
     c->st = Conn::kDead;
     loop_.add_timer(0, [this, id, err] {
-      auto it = active_.find(id);
-      if (it == active_.end()) return;
+      Conn* c = active(id);
+      if (!c) return;
       ClientResult r;
       r.error = err;
       r.retryable = true;  // UnknownHostException is an IOException
-      finish(it->second, std::move(r), false);
+      finish(c, std::move(r), false);
     });
     return;
   }
@@ -602,12 +643,12 @@ void ClientPool::start_on(Conn* c, uint64_t id, std::string* req, Callback cb, b
     std::string e = connect_error(errno);
     c->st = Conn::kDead;
     loop_.add_timer(0, [this, id, e] {
-      auto it = active_.find(id);
-      if (it == active_.end()) return;
+      Conn* c = active(id);
+      if (!c) return;
       ClientResult r;
       r.error = e;
       r.retryable = true;
-      finish(it->second, std::move(r), false);
+      finish(c, std::move(r), false);
     });
     return;
   }
@@ -631,25 +672,8 @@ void ClientPool::arm_read_deadline(uint64_t id, uint64_t serial) {
   if (rt > 0) push_deadline(read_fifo_, rt, id, serial);
 }
 
-void ClientPool::track(uint64_t id, Conn* c) {
-  if (spare_nodes_.empty()) {
-    active_.emplace(id, c);
-    return;
-  }
-  auto nh = std::move(spare_nodes_.back());
-  spare_nodes_.pop_back();
-  nh.key() = id;
-  nh.mapped() = c;
-  active_.insert(std::move(nh));
-}
-
-void ClientPool::untrack(std::unordered_map<uint64_t, Conn*>::iterator it) {
-  auto nh = active_.extract(it);
-  if (spare_nodes_.size() < 1024) spare_nodes_.push_back(std::move(nh));
-}
-
 void ClientPool::finish(Conn* c, ClientResult&& r, bool reusable) {
-  untrack(c->id);
+  release(c->id);
   if (!read_fifo_.q.empty()) pop_finished(read_fifo_);
   if (!connect_fifo_.q.empty()) pop_finished(connect_fifo_);
   Callback cb = std::move(c->cb);
@@ -699,10 +723,9 @@ void ClientPool::cancel(uint64_t id) {
     if (!connect_fifo_.q.empty()) pop_finished(connect_fifo_);
     return;
   }
-  auto it = active_.find(id);
-  if (it == active_.end()) return;
-  Conn* c = it->second;
-  untrack(it);
+  Conn* c = active(id);
+  if (!c) return;
+  release(id);
   destroy(c);
   if (!read_fifo_.q.empty()) pop_finished(read_fifo_);
   if (!connect_fifo_.q.empty()) pop_finished(connect_fifo_);

@@ -125,15 +125,23 @@ class ClientPool {
   AddressCache* addr_;
   size_t max_idle_;
   std::vector<Conn*> idle_;
-  std::unordered_map<uint64_t, Conn*> active_;
-  // Map nodes of finished requests, reused for the next ones: a request in flight costs no
-  // allocation for its entry.
-  std::vector<std::unordered_map<uint64_t, Conn*>::node_type> spare_nodes_;
-  void track(uint64_t id, Conn* c);
-  void untrack(std::unordered_map<uint64_t, Conn*>::iterator it);
-  void untrack(uint64_t id) {
-    if (auto it = active_.find(id); it != active_.end()) untrack(it);
-  }
+  // Requests in flight on plain connections, by id. An id made by get() names a slot of a
+  // table: (generation << 32) | slot, so finding a request is an index and a compare, with no
+  // hashing and no allocation (a hash map cost 2-4 % of hola A's CPU on the chaining path,
+  // profiles/round4/03_chainab). Ids of pipelined requests carry kPipeBit; the few of those
+  // re-sent on plain connections after their pipelined one failed are kept in a map.
+  static constexpr uint64_t kPipeBit = uint64_t(1) << 63;
+  struct Slot {
+    Conn* conn = nullptr;
+    uint32_t gen = 1;  // from 1: no id is 0 (callers use 0 for "no request")
+  };
+  std::vector<Slot> slots_;
+  std::vector<uint32_t> free_slots_;
+  std::unordered_map<uint64_t, Conn*> resent_;
+  uint64_t new_id();                        // a free slot's id (get())
+  void set_active(uint64_t id, Conn* c);   // the connection carrying request `id`
+  Conn* active(uint64_t id) const;          // null once finished or cancelled
+  void release(uint64_t id);                // finished or cancelled: the id is dead
   // The result every plain connection parses its responses into (see ClientResult::clear).
   // A callback only reads it before returning, and no read runs inside a callback.
   ClientResult scratch_;
