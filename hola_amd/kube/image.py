@@ -66,6 +66,8 @@ class Image:
                     else:
                         host = REPO / src
                     target = dst if not dst.endswith("/") else dst + Path(src).name
+                    if host == build_dir / "hola" and os.environ.get("HOLA_SERVER_BIN"):
+                        host = native.binary("hola")  # another server build (A/B runs, old trees)
                     img.files[os.path.normpath(target)] = host
         return img
 
