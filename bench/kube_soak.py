@@ -60,6 +60,9 @@ def main() -> int:
                     help="patch the pods' --shutdown-delay-ms before the soak (0 = the pre-round-3 "
                          "termination: drain at once; the rollouts then drop connections, and the run "
                          "hunts for drains that do not finish instead)")
+    ap.add_argument("--busy-poll-us", default="auto",
+                    help="the pods' --busy-poll-us with --shutdown-delay-ms (0 = sleeping event loops, the "
+                         "server's default before round 3's session 2)")
     a = ap.parse_args()
     out = Path(a.out)
     if out.exists():
@@ -78,7 +81,7 @@ def main() -> int:
         if a.shutdown_delay_ms is not None:
             rev = c.rollout_status()["revision"]
             c.patch({"spec": {"template": {"spec": {"containers": [{"name": "hola", "args": [
-                "--shutdown-delay-ms", str(a.shutdown_delay_ms), "--busy-poll-us", "auto"]}]}}}})
+                "--shutdown-delay-ms", str(a.shutdown_delay_ms), "--busy-poll-us", a.busy_poll_us]}]}}}})
             c.wait(lambda: c.rollout_status()["revision"] > rev and c.rollout_status()["complete"], 600, "patch")
             c.wait(lambda: all(p["status"] != "Terminating" for p in c.get_pods()), 120, "old pods gone")
             res["shutdown_delay_ms"] = a.shutdown_delay_ms
