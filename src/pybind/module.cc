@@ -28,6 +28,7 @@
 #include "core/clock.h"
 #include "core/log.h"
 #include "core/cpuprof.h"
+#include "core/inline_function.h"
 #include "http/server.h"
 
 #include <sys/socket.h>
@@ -422,6 +423,44 @@ std::pair<std::string, std::string> stall_report_probe() {
   return {stuck, after};
 }
 
+// InlineFunction: a move-only capture is destroyed exactly once, through moves, move-assignment,
+// reset and destruction; calls reach the stored callable. Returns the counters.
+py::dict inline_function_selftest() {
+  struct Tracker {
+    int* live;
+    int* destroyed;
+    explicit Tracker(int* l, int* d) : live(l), destroyed(d) { ++*live; }
+    Tracker(Tracker&& o) noexcept : live(o.live), destroyed(o.destroyed) { ++*live; }
+    Tracker(const Tracker&) = delete;
+    ~Tracker() {
+      --*live;
+      ++*destroyed;
+    }
+  };
+  int live = 0, destroyed = 0, calls = 0, sum = 0;
+  {
+    auto owned = std::make_unique<int>(7);  // move-only capture
+    InlineFunction<int(int), 64> f([t = Tracker(&live, &destroyed), p = std::move(owned), &calls](int x) {
+      ++calls;
+      return x + *p;
+    });
+    sum += f(1);
+    InlineFunction<int(int), 64> g(std::move(f));
+    if (f) sum += 1000;  // moved-from is empty
+    sum += g(2);
+    InlineFunction<int(int), 64> h;
+    h = std::move(g);
+    sum += h(3);
+    h = nullptr;  // destroys the callable
+  }
+  py::dict d;
+  d["live"] = live;
+  d["calls"] = calls;
+  d["sum"] = sum;
+  d["destroyed_tracked"] = destroyed > 0;
+  return d;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_native, m) {
@@ -487,6 +526,7 @@ PYBIND11_MODULE(_native, m) {
     return py::make_tuple(p.backoff_ms(attempt), p.max_attempts);
   }, py::arg("attempt"), py::arg("policy") = "default");
   m.def("stall_report_probe", &stall_report_probe);
+  m.def("inline_function_selftest", &inline_function_selftest);
   m.def("loop_timer_order", &loop_timer_order, py::arg("delays"), py::arg("cancel") = std::vector<int>{});
   m.def("span_ring", &span_ring);
   m.def("log_stress", &log_stress, py::arg("threads"), py::arg("lines"), py::arg("tag") = "stress",

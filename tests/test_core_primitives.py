@@ -133,3 +133,12 @@ def test_stall_report_names_a_handler_that_never_returns(native):
                            capture_output=True, text=True).stdout
     assert "hola_stall_probe_spin" in names and "Connection::process" in names, names
     assert "phase wait" in after and "in epoll_wait, no pass over 100 ms" in after, after
+
+
+def test_inline_function_owns_its_callable_once(native):
+    """InlineFunction (the chaining continuation's inline storage): calls reach the callable
+    through moves and move-assignment, a moved-from function is empty, and a move-only
+    capture is alive in exactly one place until the function is reset."""
+    r = native.inline_function_selftest()
+    assert r["calls"] == 3 and r["sum"] == (1 + 7) + (2 + 7) + (3 + 7)
+    assert r["live"] == 0 and r["destroyed_tracked"]
