@@ -9,6 +9,7 @@
 // SIGTERM/SIGINT/SIGHUP: stop accepting, drain in-flight requests, flush spans, exit 0.
 #include <errno.h>
 #include <signal.h>
+#include <atomic>
 #include <unistd.h>
 
 #include <algorithm>
@@ -121,6 +122,12 @@ bool need(int i, int argc, const char* flag) {
 // See the exit watchdog in main(): the time a termination may take beyond the shutdown delay
 // and the drain budget (the reporter's last span export alone may take its 2 s timeout).
 constexpr int64_t kExitMarginMs = 10000;
+
+namespace {
+// The termination step main is in, for the exit watchdog's report (a string literal).
+std::atomic<const char*> g_term_step{"serving"};
+void term_step(const char* s) { g_term_step.store(s, std::memory_order_relaxed); }
+}  // namespace
 
 int main(int argc, char** argv) {
   http::ServerOptions so;
@@ -387,6 +394,7 @@ int main(int argc, char** argv) {
     return 1;
   }
   cpuprof::enable_capture();  // stall reports capture worker stacks by signal
+  cpuprof::note_thread();     // ... and main's
   chainer.start();
   tracer.start();
   server.start();
@@ -420,13 +428,22 @@ int main(int argc, char** argv) {
     // writer may be what is stuck.
     const int64_t limit_ms = exit_deadline_ms >= 0 ? exit_deadline_ms
                                                    : int64_t(shutdown_delay_ms) + std::max(0, drain_ms) + kExitMarginMs;
-    if (limit_ms > 0) std::thread([limit_ms, &server] {
+    const int main_tid = cpuprof::current_tid();
+    if (limit_ms > 0) std::thread([limit_ms, &server, main_tid] {
       std::this_thread::sleep_for(std::chrono::milliseconds(limit_ms));
       char line[160];
       const int n = snprintf(line, sizeof line, "hola: termination did not complete within %lld ms; exiting\n",
                              (long long)limit_ms);
       ssize_t w = ::write(2, line, size_t(n));
-      // where every event loop was, with its stack (the report that names a stuck handler)
+      // where main is (the termination step and its stack), then every event loop, with its
+      // stack (the report that names a stuck handler)
+      {
+        uintptr_t pcs[cpuprof::kMaxCaptureDepth];
+        const int k = cpuprof::capture(main_tid, pcs, cpuprof::kMaxCaptureDepth);
+        const std::string m = std::string("hola: main: ") + g_term_step.load(std::memory_order_relaxed) +
+                              (k > 0 ? "; stack" + cpuprof::describe_pcs(pcs, k) : "; stack: no answer") + "\n";
+        w = ::write(2, m.data(), m.size());
+      }
       std::vector<size_t> all(server.num_workers());
       for (size_t i = 0; i < all.size(); ++i) all[i] = i;
       for (const std::string& r : server.stall_reports(all, true)) {
@@ -441,6 +458,7 @@ int main(int argc, char** argv) {
     // Phase 1: fail readiness, keep accepting, close connections between responses. The
     // pod's endpoint removal takes a while to reach every proxy (kube-proxy's sync); new
     // connections routed here meanwhile are still served.
+    term_step("shutdown delay");
     server.begin_termination();  // before the log line: the line says it has happened
     LOG_INFO("received %s: readiness failing, still serving for %d ms", sig_name, shutdown_delay_ms);
     Logger::instance().flush();
@@ -460,7 +478,9 @@ int main(int argc, char** argv) {
     }
   }
   LOG_INFO("received %s: draining (up to %d ms)", sig_name, drain_ms);
+  term_step("drain (Server::shutdown)");
   server.shutdown(drain_ms);
+  term_step("joining the workers");
   server.join();
   if (so.profile) {
     std::string pj = server.profile_json();
@@ -471,9 +491,13 @@ int main(int argc, char** argv) {
       f << pj << "\n";
     }
   }
+  term_step("stopping the config watcher");
   cfg.stop();
+  term_step("stopping the aloha client");
   chainer.stop();
+  term_step("flushing spans (Tracer::stop)");
   tracer.stop();
+  term_step("writing the CPU profile and the last log lines");
   if (!cpu_profile.empty() && !cpuprof::write()) LOG_WARN("could not write the CPU profile to %s", cpu_profile.c_str());
   LOG_INFO("shutdown complete (%llu requests served)", (unsigned long long)server.total_requests());
   Logger::instance().flush();

@@ -846,3 +846,10 @@ def test_exit_watchdog_reports_where_every_worker_is(hola):
         assert "hola::EventLoop::run()" in names, names
     # the connection handler's record is decoded with its state bits
     assert re.search(r"last handler (connection [0-9a-f]+ \{[a-z_,]*\} in=\d+ unsent=\d+|loop-internal)", log), log
+    # and main says which termination step it is in, with its own stack
+    m = re.search(r"hola: main: shutdown delay; stack((?: #\d+ \S+)+)", log)
+    assert m, log[-3000:]
+    own = [off for obj, off in re.findall(r"#\d+ (\S+)\+0x([0-9a-f]+)", m.group(1)) if obj == Path(exe).name]
+    names = subprocess.run(["addr2line", "-f", "-C", "-e", exe, *[f"0x{o}" for o in own]],
+                           capture_output=True, text=True).stdout
+    assert re.search(r"^main$", names, re.M), names
