@@ -82,6 +82,9 @@ void load_exec_ranges() {
 // locks, no allocation. When the context is in code from another object (libc's syscall
 // wrappers: send, recv, epoll_wait), which keeps no frame pointer, the caller is found by
 // scanning the top of the stack for the first return address into a different mapping.
+// Not instrumented by the sanitizers: it reads saved frame pointers and return addresses of
+// another function's frames, which AddressSanitizer's stack redzones would flag.
+__attribute__((no_sanitize("address", "thread", "undefined")))
 int walk(const ucontext_t* uc, uintptr_t* out, int max) {
   const uintptr_t pc = uintptr_t(uc->uc_mcontext.gregs[REG_RIP]);
   const uintptr_t sp = uintptr_t(uc->uc_mcontext.gregs[REG_RSP]);

@@ -306,3 +306,31 @@ def test_shutdown_with_parked_calls_and_streams_frees_everything(preset, tmp_pat
         log = s.log()
     assert "Sanitizer" not in log and "runtime error" not in log, log[-6000:]
     assert rc == 0, (rc, log[-3000:])
+
+
+@pytest.mark.parametrize("preset", ["asan", "tsan"])
+def test_sanitized_exit_watchdog_stall_report(preset, tmp_path):
+    """The exit watchdog's stall report under the sanitizers: the loops' activity records are
+    read from another thread, and each worker's stack is captured by a signal whose handler
+    walks the frame pointers. A termination that outlasts --exit-deadline-ms (a 3 s delay
+    against a 0.5 s limit) takes that path with the workers alive."""
+    build(preset)
+    exe = build_dir(preset) / "hola"
+    s = HolaProcess(args=["--shutdown-delay-ms", "3000", "--exit-deadline-ms", "500"],
+                    env={"HOSTNAME": "san", **SAN_ENV[preset]}, threads=4, exe=exe, log_level="warn",
+                    wrapper=tsan_wrapper() if preset == "tsan" else None)
+    s.start(timeout=60)
+    try:
+        for _ in range(50):
+            assert s.get("/api/hola")[0] == 200
+        s.proc.send_signal(signal.SIGTERM)
+        rc = s.proc.wait(timeout=60)
+    finally:
+        if s.proc.poll() is None:
+            s.proc.kill()
+            s.proc.wait()
+    log = s.log()
+    assert "ThreadSanitizer" not in log, log[-6000:]
+    assert "AddressSanitizer" not in log and "runtime error" not in log, log[-6000:]
+    assert rc == 3, (rc, log[-3000:])
+    assert log.count("hola: worker ") == 4 and "hola: main: shutdown delay" in log, log[-3000:]
