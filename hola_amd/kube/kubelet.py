@@ -408,7 +408,10 @@ class Kubelet:
                     return  # "Killed" comes before "Deleted"
                 note = "capture did not finish"
             else:
-                note = kf.result()
+                try:
+                    note = kf.result()
+                except Exception as e:  # noqa: BLE001 - a diagnostic; the SIGKILL was sent (finally)
+                    note = f"capture failed: {e!r}"
             pod.kill_future = None
             self.cluster.event(pod.name, "Killed", f"grace period expired: SIGKILL ({note})")
         if not pod.running:
