@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 
 #include "core/clock.h"
 
@@ -190,8 +191,16 @@ void EventLoop::run() {
       t = mono_ns();
     }
     if (n < 0 && errno != EINTR) {
-      perror("epoll_wait");
-      break;
+      // Only a broken epoll descriptor gets here (EBADF, EINVAL, EFAULT). The loop cannot serve
+      // its connections or answer posted tasks any more; leaving the thread would leave a
+      // replica that looks alive with a dead worker and a drain that waits for it. Fail fast
+      // (the supervisor or kubelet restarts the process), saying why, straight to stderr.
+      char line[128];
+      const int k = snprintf(line, sizeof line, "hola: event loop: epoll_wait(%d) failed: %s; aborting\n", epfd_,
+                             strerror(errno));
+      ssize_t w = ::write(2, line, size_t(k));
+      (void)w;
+      std::abort();
     }
     now_ms_ = t / 1000000;
     act_.pass_ns.store(t, std::memory_order_relaxed);

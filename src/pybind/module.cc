@@ -5,6 +5,7 @@
 
 #include <pybind11/stl.h>
 
+#include <algorithm>
 #include <atomic>
 #include <thread>
 
@@ -423,6 +424,26 @@ std::pair<std::string, std::string> stall_report_probe() {
   return {stuck, after};
 }
 
+// An event loop whose epoll descriptor is gone (closed behind its back): run() must fail fast
+// (abort with a line on stderr) instead of leaving the thread. Run it in a child process.
+void loop_lost_epoll_probe() {
+  auto before = [] {
+    std::vector<int> fds;
+    for (int fd = 3; fd < 1024; ++fd) {
+      char path[64], target[128];
+      snprintf(path, sizeof path, "/proc/self/fd/%d", fd);
+      const ssize_t n = readlink(path, target, sizeof target - 1);
+      if (n > 0 && std::string_view(target, size_t(n)) == "anon_inode:[eventpoll]") fds.push_back(fd);
+    }
+    return fds;
+  };
+  const std::vector<int> old = before();
+  EventLoop loop;
+  for (int fd : before())
+    if (std::find(old.begin(), old.end(), fd) == old.end()) ::close(fd);  // the loop's own
+  loop.run();  // does not return
+}
+
 // InlineFunction: a move-only capture is destroyed exactly once, through moves, move-assignment,
 // reset and destruction; calls reach the stored callable. Returns the counters.
 py::dict inline_function_selftest() {
@@ -527,6 +548,7 @@ PYBIND11_MODULE(_native, m) {
   }, py::arg("attempt"), py::arg("policy") = "default");
   m.def("stall_report_probe", &stall_report_probe);
   m.def("inline_function_selftest", &inline_function_selftest);
+  m.def("loop_lost_epoll_probe", &loop_lost_epoll_probe);
   m.def("loop_timer_order", &loop_timer_order, py::arg("delays"), py::arg("cancel") = std::vector<int>{});
   m.def("span_ring", &span_ring);
   m.def("log_stress", &log_stress, py::arg("threads"), py::arg("lines"), py::arg("tag") = "stress",

@@ -142,3 +142,16 @@ def test_inline_function_owns_its_callable_once(native):
     r = native.inline_function_selftest()
     assert r["calls"] == 3 and r["sum"] == (1 + 7) + (2 + 7) + (3 + 7)
     assert r["live"] == 0 and r["destroyed_tracked"]
+
+
+def test_event_loop_fails_fast_when_its_epoll_descriptor_is_gone(native):
+    """A loop whose epoll descriptor was closed behind its back cannot serve or answer posted
+    tasks; it aborts with a line on stderr instead of leaving its thread (which would leave a
+    replica that looks alive with a dead worker, and a drain waiting for it)."""
+    import subprocess
+    import sys
+
+    r = subprocess.run([sys.executable, "-c", "from hola_amd import native; native.load_native().loop_lost_epoll_probe()"],
+                       capture_output=True, text=True, timeout=60, cwd=str(Path(__file__).resolve().parent.parent))
+    assert r.returncode == -6, (r.returncode, r.stderr[-2000:])
+    assert "hola: event loop: epoll_wait(" in r.stderr and "Bad file descriptor; aborting" in r.stderr, r.stderr
