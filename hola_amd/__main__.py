@@ -106,7 +106,7 @@ def _cluster(argv: list[str]) -> int:
 
 
 def _info() -> int:
-    from hola_amd.utils.cpu import (allowed_cpus, cgroup_cpu_quota, cpu_budget, format_cpu_list, l3_domain,
+    from hola_amd.utils.cpu import (allowed_cpus, cgroup_cpu_quota, cpu_budget, format_cpu_list, l3_domain, package_of,
                                     physical_cores, plan_node)
 
     phys = physical_cores()
@@ -152,8 +152,9 @@ def _info() -> int:
             continue
         print(f"bench N={n}: {per_rank} cores/replica, smt {smt}, {plans[0]['dealing']}")
         for r, p in enumerate(plans):
+            socks = sorted({package_of(c) for c in p["server"]})
             print(f"  rank{r}: server {format_cpu_list(p['server'])} loadgen {format_cpu_list(p['loadgen'])} "
-                  f"threads->replicas {p['thread_targets']}")
+                  f"threads->replicas {p['thread_targets']} server socket(s) {socks}")
     return 0
 
 
