@@ -53,13 +53,6 @@ bool parse_uint(std::string_view s, int64_t* out) {
 
 }  // namespace
 
-bool iequals(std::string_view a, std::string_view b) {
-  if (a.size() != b.size()) return false;
-  for (size_t i = 0; i < a.size(); ++i)
-    if (lower(a[i]) != lower(b[i])) return false;
-  return true;
-}
-
 bool percent_decode(std::string_view in, char* out, size_t* out_len, bool keep_encoded_slash) {
   auto hex = [](char c) -> int {
     if (c >= '0' && c <= '9') return c - '0';

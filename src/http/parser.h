@@ -45,8 +45,17 @@ Parse skip_chunked_body(const char* buf, size_t len, size_t* consumed);
 // meaningful only on kOk: pass a fresh string per attempt.
 Parse decode_chunked_body(const char* buf, size_t len, size_t* consumed, std::string* body);
 
-// Case-insensitive ASCII equality.
-bool iequals(std::string_view a, std::string_view b);
+// Case-insensitive ASCII equality. Inline: callers compare against literals, so the length
+// test and the loop fold into a few compares (an out-of-line call per header name cost 0.6 %
+// of hola A's CPU on the chaining path).
+inline bool iequals(std::string_view a, std::string_view b) {
+  if (a.size() != b.size()) return false;
+  for (size_t i = 0; i < a.size(); ++i) {
+    const char x = a[i], y = b[i];
+    if (x != y && ((x | 0x20) != (y | 0x20) || unsigned((x | 0x20) - 'a') > unsigned('z' - 'a'))) return false;
+  }
+  return true;
+}
 // Percent-decodes a path; false on malformed escapes. Output written to out (len <= in len).
 // With keep_encoded_slash, "%2F" stays encoded (Undertow's default allow-encoded-slash=false),
 // so an encoded slash never becomes a path separator.
