@@ -133,18 +133,28 @@ void on_prof(int, siginfo_t*, void* ucv) {
 // ---- on-demand capture of another thread's stack (stall reports) ----
 constexpr int kCaptureSignal = 40;  // a real-time signal no thread blocks (SIGRTMIN is 34)
 std::mutex g_cap_mu;                // one capture at a time
-std::atomic<int> g_cap_state{0};    // 0 idle, 1 requested, 2 done
-std::atomic<int> g_cap_tid{0};      // the thread asked: a late signal to an earlier target is ignored
+// Request word: (sequence << 2) | state, state 0 idle, 1 requested, 3 being written, 2 done.
+// The handler walks into its own buffer and publishes only if the word still names its
+// request, so a signal that arrives after its capture gave up can never write into a later
+// capture's result.
+std::atomic<uint64_t> g_cap_word{0};
+std::atomic<int> g_cap_tid{0};      // the thread asked
 uintptr_t g_cap_pcs[kMaxCaptureDepth];
-std::atomic<int> g_cap_depth{0};
+int g_cap_depth = 0;
 std::atomic<bool> g_cap_installed{false};
 
 void on_capture(int, siginfo_t*, void* ucv) {
-  if (g_cap_state.load(std::memory_order_acquire) != 1) return;
+  uint64_t w = g_cap_word.load(std::memory_order_acquire);
+  if ((w & 3) != 1) return;
   if (int(syscall(SYS_gettid)) != g_cap_tid.load(std::memory_order_relaxed)) return;
   const int saved_errno = errno;
-  g_cap_depth.store(walk(static_cast<const ucontext_t*>(ucv), g_cap_pcs, kMaxCaptureDepth), std::memory_order_relaxed);
-  g_cap_state.store(2, std::memory_order_release);
+  uintptr_t pcs[kMaxCaptureDepth];
+  const int n = walk(static_cast<const ucontext_t*>(ucv), pcs, kMaxCaptureDepth);
+  if (g_cap_word.compare_exchange_strong(w, (w & ~uint64_t(3)) | 3, std::memory_order_acq_rel)) {
+    for (int i = 0; i < n; ++i) g_cap_pcs[i] = pcs[i];
+    g_cap_depth = n;
+    g_cap_word.store((w & ~uint64_t(3)) | 2, std::memory_order_release);
+  }
   errno = saved_errno;
 }
 
@@ -179,32 +189,37 @@ bool enable_capture() {
 }
 
 int capture(int tid, uintptr_t* pcs, int max, int timeout_ms) {
-  if (!g_cap_installed.load() || max <= 0) return 0;
+  if (!g_cap_installed.load() || max <= 0 || tid <= 0) return 0;
   std::lock_guard<std::mutex> g(g_cap_mu);
   if (!g_on.load()) {
     load_exec_ranges();  // the profiler keeps its own (read by its handler meanwhile)
     g_own_range = exec_range(uintptr_t(&on_prof));
   }
-  g_cap_depth.store(0);
   g_cap_tid.store(tid, std::memory_order_relaxed);
-  g_cap_state.store(1, std::memory_order_release);
-  if (tid <= 0 || syscall(SYS_tgkill, getpid(), tid, kCaptureSignal) != 0) {
-    g_cap_state.store(0);
+  const uint64_t seq = (g_cap_word.load() >> 2) + 1;
+  const uint64_t requested = seq << 2 | 1;
+  g_cap_word.store(requested, std::memory_order_release);
+  if (syscall(SYS_tgkill, getpid(), tid, kCaptureSignal) != 0) {
+    g_cap_word.store(seq << 2);
     return 0;
   }
   const auto until = std::chrono::steady_clock::now() + std::chrono::milliseconds(timeout_ms);
-  while (g_cap_state.load(std::memory_order_acquire) != 2) {
-    if (std::chrono::steady_clock::now() >= until) {
-      // The handler may still run later: it only writes g_cap_pcs, which the next capture
-      // re-initialises under the lock. Report nothing for this thread.
-      g_cap_state.store(0);
-      return 0;
+  for (;;) {
+    const uint64_t w = g_cap_word.load(std::memory_order_acquire);
+    if ((w & 3) == 2) break;
+    if ((w & 3) == 1 && std::chrono::steady_clock::now() >= until) {
+      // No answer (a stopped thread, or one that blocks the signal): withdraw the request; a
+      // handler that runs later finds it gone. If the handler is writing right now (state 3),
+      // wait for it instead.
+      uint64_t expect = requested;
+      if (g_cap_word.compare_exchange_strong(expect, seq << 2, std::memory_order_acq_rel)) return 0;
+      continue;
     }
     std::this_thread::sleep_for(std::chrono::microseconds(200));
   }
-  const int n = std::min(max, g_cap_depth.load());
+  const int n = std::min(max, g_cap_depth);
   for (int i = 0; i < n; ++i) pcs[i] = g_cap_pcs[i];
-  g_cap_state.store(0);
+  g_cap_word.store(seq << 2, std::memory_order_release);
   return n;
 }
 
