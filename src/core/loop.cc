@@ -208,7 +208,7 @@ void EventLoop::run() {
       set_phase(kEvents);
       for (int i = 0; i < n; ++i) static_cast<Handler*>(evs[i].data.ptr)->on_event(evs[i].events);
     }
-    if (!heap_.empty()) {
+    if (!heap_.empty() && heap_.top().deadline <= now_ms_) {  // a heap peek per pass, no lookup
       set_phase(kTimers);
       run_timers();
     }
