@@ -482,7 +482,7 @@ uint64_t ClientPool::new_id() {
     s = uint32_t(slots_.size());
     slots_.emplace_back();
   }
-  return uint64_t(slots_[s].gen & 0x7fffffffu) << 32 | s;
+  return uint64_t(slots_[s].gen) << 32 | s;
 }
 
 void ClientPool::set_active(uint64_t id, Conn* c) {
@@ -496,7 +496,7 @@ ClientPool::Conn* ClientPool::active(uint64_t id) const {
     return it == resent_.end() ? nullptr : it->second;
   }
   const uint32_t s = uint32_t(id);
-  if (s >= slots_.size() || (slots_[s].gen & 0x7fffffffu) != uint32_t(id >> 32)) return nullptr;
+  if (s >= slots_.size() || slots_[s].gen != uint32_t(id >> 32)) return nullptr;
   return slots_[s].conn;
 }
 
@@ -506,9 +506,9 @@ void ClientPool::release(uint64_t id) {
     return;
   }
   const uint32_t s = uint32_t(id);
-  if (s >= slots_.size() || (slots_[s].gen & 0x7fffffffu) != uint32_t(id >> 32)) return;
+  if (s >= slots_.size() || slots_[s].gen != uint32_t(id >> 32)) return;
   slots_[s].conn = nullptr;
-  ++slots_[s].gen;  // a late timer or cancel with the old id finds nothing
+  slots_[s].gen = next_generation(slots_[s].gen);  // a late timer or cancel with the old id finds nothing
   free_slots_.push_back(s);
 }
 

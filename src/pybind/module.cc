@@ -548,6 +548,7 @@ PYBIND11_MODULE(_native, m) {
   }, py::arg("attempt"), py::arg("policy") = "default");
   m.def("stall_report_probe", &stall_report_probe);
   m.def("inline_function_selftest", &inline_function_selftest);
+  m.def("client_next_generation", [](uint32_t g) { return client::ClientPool::next_generation(g); });
   m.def("loop_lost_epoll_probe", &loop_lost_epoll_probe);
   m.def("loop_timer_order", &loop_timer_order, py::arg("delays"), py::arg("cancel") = std::vector<int>{});
   m.def("span_ring", &span_ring);

@@ -144,6 +144,16 @@ def test_inline_function_owns_its_callable_once(native):
     assert r["live"] == 0 and r["destroyed_tracked"]
 
 
+def test_client_slot_generations_never_make_id_zero(native):
+    """The client pool's request ids are (generation << 32) | slot. Generations stay within 31
+    bits (bit 63 marks pipelined ids) and skip 0 when they wrap, so slot 0 never hands out id 0,
+    the callers' "no request"."""
+    g = native.client_next_generation
+    assert g(1) == 2 and g(0x7FFFFFFE) == 0x7FFFFFFF
+    assert g(0x7FFFFFFF) == 1  # wraps past 0
+    assert g(0xFFFFFFFF) == 1 and g(0) == 1
+
+
 def test_event_loop_fails_fast_when_its_epoll_descriptor_is_gone(native):
     """A loop whose epoll descriptor was closed behind its back cannot serve or answer posted
     tasks; it aborts with a line on stderr instead of leaving its thread (which would leave a
