@@ -19,6 +19,7 @@
 #include <cstring>
 #include <fstream>
 #include <string>
+#include <mutex>
 #include <thread>
 
 #include "app/aloha_chainer.h"
@@ -127,6 +128,11 @@ namespace {
 // The termination step main is in, for the exit watchdog's report (a string literal).
 std::atomic<const char*> g_term_step{"serving"};
 void term_step(const char* s) { g_term_step.store(s, std::memory_order_relaxed); }
+// The watchdog reports while holding this; main takes it before its locals (the server the
+// report reads) go away, so a watchdog that fires just as main returns either finishes its
+// report and exits first or finds the termination complete.
+std::mutex g_watchdog_mu;
+bool g_terminated = false;
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -431,6 +437,8 @@ int main(int argc, char** argv) {
     const int main_tid = cpuprof::current_tid();
     if (limit_ms > 0) std::thread([limit_ms, &server, main_tid] {
       std::this_thread::sleep_for(std::chrono::milliseconds(limit_ms));
+      std::lock_guard<std::mutex> g(g_watchdog_mu);
+      if (g_terminated) return;
       char line[160];
       const int n = snprintf(line, sizeof line, "hola: termination did not complete within %lld ms; exiting\n",
                              (long long)limit_ms);
@@ -501,5 +509,9 @@ int main(int argc, char** argv) {
   if (!cpu_profile.empty() && !cpuprof::write()) LOG_WARN("could not write the CPU profile to %s", cpu_profile.c_str());
   LOG_INFO("shutdown complete (%llu requests served)", (unsigned long long)server.total_requests());
   Logger::instance().flush();
+  {
+    std::lock_guard<std::mutex> g(g_watchdog_mu);
+    g_terminated = true;
+  }
   return 0;
 }
