@@ -176,15 +176,33 @@ class Cluster:
 
     # ------------------------------------------------------------------ lifecycle
     def start(self) -> "Cluster":
-        try:
-            self._start_services()
-        except BaseException:
-            self._stop_services()
-            raise
+        # Every process the executor starts gets a parent-death signal (kubelet.die_with_parent),
+        # which the kernel ties to the *thread* that started it. The Services' proxies and the
+        # collector are therefore started by the control-loop thread itself, like the pods, so
+        # they live exactly as long as the executor whichever thread calls start().
+        started = threading.Event()
+        failed: list[BaseException] = []
+
+        def run() -> None:
+            try:
+                self._start_services()
+            except BaseException as e:  # noqa: BLE001 - re-raised in the caller's thread
+                failed.append(e)
+                self._stop_services()
+                started.set()
+                return
+            started.set()
+            self._loop()
+
+        self._thread = threading.Thread(target=run, name="kube-control", daemon=True)
+        self._thread.start()
+        started.wait()
+        if failed:
+            self._thread.join()
+            self._thread = None
+            raise failed[0]
         with self.lock:
             self._new_revision(self.workload["spec"]["template"], initial=True)
-        self._thread = threading.Thread(target=self._loop, name="kube-control", daemon=True)
-        self._thread.start()
         return self
 
     def close(self, grace_s: float = 10.0) -> None:

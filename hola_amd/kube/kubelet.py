@@ -134,6 +134,7 @@ class Pod:
     term_sent: bool = False
     kill_sent: bool = False
     kill_future: Future | None = None  # grace-expiry capture + SIGKILL, in the diagnostics thread
+    prestop_cmd: list[str] | None = None  # an exec preStop hook the control loop starts next tick
     gone: bool = False
 
     @property
@@ -388,10 +389,10 @@ class Kubelet:
         pod.grace_deadline = now + float(spec_grace if grace_s is None else grace_s)
         pre = ((pod.container.get("lifecycle") or {}).get("preStop") or {})
         if pod.running and "exec" in pre:
-            cmd = [self.map_paths(pod, a) for a in pre["exec"]["command"]]
-            pod.prestop = subprocess.Popen(cmd, env=self._env(pod), stdout=subprocess.DEVNULL,
-                                           stderr=subprocess.DEVNULL, start_new_session=True,
-                                           preexec_fn=die_with_parent)
+            # Started by the control loop's next tick (_tick_terminating), not here: begin_delete
+            # also runs on `oc` request threads, and a process started there would get its
+            # parent-death signal when that thread ends (die_with_parent).
+            pod.prestop_cmd = [self.map_paths(pod, a) for a in pre["exec"]["command"]]
         elif pod.running and "httpGet" in pre:  # off the control loop, like the probes
             hg = pre["httpGet"]
             pod.prestop_http = self.pool.submit(http_probe, pod.ip, _port_number(pod.container, hg.get("port", 8080)),
@@ -421,6 +422,11 @@ class Kubelet:
             self.cluster.event(pod.name, "Deleted",
                                f"exit {pod.proc.returncode if pod.proc else None} after {now - pod.deletion_at:.2f}s")
             return
+        if pod.prestop_cmd is not None:
+            cmd, pod.prestop_cmd = pod.prestop_cmd, None
+            pod.prestop = subprocess.Popen(cmd, env=self._env(pod), stdout=subprocess.DEVNULL,
+                                           stderr=subprocess.DEVNULL, start_new_session=True,
+                                           preexec_fn=die_with_parent)
         hook_done = (pod.prestop is None or pod.prestop.poll() is not None) and \
             (pod.prestop_http is None or pod.prestop_http.done())
         if not pod.term_sent and (hook_done or now >= pod.grace_deadline):
@@ -455,7 +461,7 @@ class Kubelet:
 
 def die_with_parent(cpus: list[int] | None = None) -> None:
     """preexec_fn of every process the executor starts: the kernel SIGKILLs it when the thread
-    that started it (the control loop) ends, so an executor that dies, or a test process cut
+    that started it ends (the control loop, which starts every pod, hook and Service process), so an executor that dies, or a test process cut
     off before its teardown, leaves no pods behind (a pod keeps its own session, so a signal to
     the executor's process group would not reach it). Optionally applies the cpuset."""
     _PRCTL(1, int(signal.SIGKILL), 0, 0, 0)  # PR_SET_PDEATHSIG

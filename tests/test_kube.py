@@ -373,6 +373,39 @@ def test_prestop_hook_runs_before_sigterm(cluster):
     assert any(e[2] == "Deleted" for e in c.events)
 
 
+def test_processes_outlive_the_threads_that_asked_for_them(tmp_path, hola_bin):
+    """The parent-death signal is tied to the thread that starts a process. A cluster started
+    from a thread that then ends keeps its Service proxy and collector, and an exec preStop
+    hook asked for by `oc delete pod` on a request thread (the CLI's control server answers
+    each command on a thread of its own) still runs to completion before the SIGTERM."""
+    box: dict = {}
+
+    def starter():
+        box["c"] = Cluster([DC], state_dir=tmp_path / "c", replicas=1, time_scale=TS, node_cpus=64,
+                           service_port=0).start()
+    t = threading.Thread(target=starter)
+    t.start()
+    t.join()
+    c = box["c"]
+    try:
+        c.patch({"spec": {"template": {"spec": {"containers": [{"name": "hola", "args": ["--shutdown-delay-ms", "0"],
+                 "lifecycle": {"preStop": {"exec": {"command": ["sleep", "1"]}}}}]}}}})
+        c.wait(lambda: c.rollout_status()["complete"] and c.rollout_status()["revision"] == 2, 30, "rollout")
+        c.wait(lambda: len(c.get_pods()) == 1, 30, "old pod gone")
+        assert all(p.poll() is None for p in c.proxies) and c.sink.poll() is None
+        st, _ = _greet(c)
+        assert st == 200
+        name = c.get_pods()[0]["name"]
+        t0 = time.monotonic()
+        d = threading.Thread(target=c.delete_pod, args=(name,))
+        d.start()
+        d.join()
+        c.wait(lambda: all(p["name"] != name for p in c.get_pods()), 30, "pod gone")
+        assert time.monotonic() - t0 >= 0.95  # the hook was not killed with the request thread
+    finally:
+        c.close(grace_s=5)
+
+
 def test_memory_limit_is_enforced_as_oomkilled(cluster):
     """limits.memory below the server's resident memory: the container is killed as the cgroup
     OOM killer would (OOMKilled), restarted, and never becomes an endpoint."""
