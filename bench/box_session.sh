@@ -7,7 +7,7 @@
 #   final              smoke(), pytest -m gpu, the default bench (the driver's round-end tiers)
 #   bench ARGS...      one bench.py run with ARGS
 #   repeat REPS [ARGS] the default bench REPS times (run-to-run spread)
-#   ab REPS "label|args[|VAR=value]" ...   interleaved A/B of bench.py variants, REPS rounds
+#   ab REPS "label|args[|VAR=value]" ...   interleaved A/B of bench.py variants, REPS rounds; AB_SWAP=1 alternates the order
 #   rehearsal [Ns]     the driver's own N>1 command line (default N = 2 4 8) inside the box's
 #                      CPU slice, plus --profile-dir stage profiles for locality attribution
 #   locality           N = 1, 2, 4, 8 in the box's slice, L3-grouped vs. plain connection dealing
@@ -93,7 +93,13 @@ repeat)
 ab)
   REPS=${1:?reps}; shift
   for rep in $(seq 1 "$REPS"); do
-    for v in "$@"; do
+    # AB_SWAP=1: every other round runs the sides in reverse order (the first slot of a round
+    # can be the slow one on this box: profiles/round4/03_chainab)
+    sides=("$@")
+    if [ "${AB_SWAP:-0}" = 1 ] && [ $((rep % 2)) = 0 ]; then
+      sides=(); for ((k = $#; k >= 1; k--)); do sides+=("${!k}"); done
+    fi
+    for v in "${sides[@]}"; do
       # "label|bench args" or "label|bench args|VAR=value ..." (environment for that variant)
       label=${v%%|*}; rest=${v#*|}; args=${rest%%|*}; envs=""
       [ "$rest" != "$args" ] && envs=${rest#*|}
