@@ -1,10 +1,30 @@
 #include "http/parser.h"
 
+#include <immintrin.h>
+
 #include <cstring>
+#include <type_traits>
 
 namespace hola::http {
 
 namespace {
+
+// A fresh Request, copied from a constant in 32-byte vector moves. `*req = Request()` built the
+// temporary on the stack with `rep stos` and copied it out with 16-byte loads of 8-byte
+// stores, which miss store forwarding; a plain copy or memset of the constant compiles to
+// `rep stos`/`rep movs` too, whose start-up alone costs tens of cycles at this size. Together
+// about half of parse_request's time for a wrk-style request (bench/micro.cc).
+static_assert(std::is_trivially_copyable_v<Request>);
+const Request kFreshRequest{};
+inline void reset_request(Request* req) {
+  constexpr size_t kVec = sizeof(Request) / 32, kTail = sizeof(Request) % 32;
+  const auto* src = reinterpret_cast<const unsigned char*>(&kFreshRequest);
+  auto* dst = reinterpret_cast<unsigned char*>(req);
+  for (size_t i = 0; i < kVec; ++i)
+    _mm256_storeu_si256(reinterpret_cast<__m256i*>(dst + 32 * i),
+                        _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + 32 * i)));
+  if constexpr (kTail > 0) memcpy(dst + 32 * kVec, src + 32 * kVec, kTail);
+}
 
 inline char lower(char c) { return (c >= 'A' && c <= 'Z') ? char(c + 32) : c; }
 
@@ -124,7 +144,7 @@ bool remove_dot_segments(std::string_view in, char* out, size_t* out_len) {
 }
 
 Parse parse_request(const char* buf, size_t len, Request* req, int* status) {
-  *req = Request();
+  reset_request(req);
   size_t pos = 0;
   // RFC 9112 §2.2: ignore at least one empty line before the request-line.
   while (pos < len && (buf[pos] == '\r' || buf[pos] == '\n')) ++pos;
