@@ -7,6 +7,7 @@
 #   final              smoke(), pytest -m gpu, the default bench (the driver's round-end tiers)
 #   bench ARGS...      one bench.py run with ARGS
 #   repeat REPS [ARGS] the default bench REPS times (run-to-run spread)
+#   instr label=BIN ... [--rounds N]   user-space instructions per request (bench/instr_ab.py)
 #   ab REPS "label|args[|VAR=value]" ...   interleaved A/B of bench.py variants, REPS rounds; AB_SWAP=1 alternates the order
 #   rehearsal [Ns]     the driver's own N>1 command line (default N = 2 4 8) inside the box's
 #                      CPU slice, plus --profile-dir stage profiles for locality attribution
@@ -47,6 +48,10 @@ final)
   ;;
 bench)
   timeout -k 10 400 python bench.py "$@" > "$OUT/bench.json" 2>> "$OUT/err.log"
+  ;;
+instr)
+  # user-space instructions per request of server binaries (bench/instr_ab.py: label=path ...)
+  timeout -k 10 900 python -u bench/instr_ab.py "$OUT" "$@" > "$OUT/instr.log" 2>> "$OUT/err.log"
   ;;
 uringchain)
   # the chaining hop's four syscalls per request: epoll vs one io_uring batch per loop pass
