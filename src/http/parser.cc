@@ -210,7 +210,8 @@ Parse parse_request(const char* buf, size_t len, Request* req, int* status) {
   req->path = req->target.substr(0, q);
   if (q != std::string_view::npos) req->query = req->target.substr(q + 1);
   // Absolute-form targets (proxies): strip scheme://authority.
-  if (req->path.size() > 7 && (req->path.substr(0, 7) == "http://" || req->path.substr(0, 8) == "https://")) {
+  if (req->path.size() > 7 && req->path[0] != '/' &&
+      (req->path.substr(0, 7) == "http://" || req->path.substr(0, 8) == "https://")) {
     size_t s = req->path.find('/', req->path.find("//") + 2);
     req->path = s == std::string_view::npos ? std::string_view("/") : req->path.substr(s);
   }
