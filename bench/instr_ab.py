@@ -2,6 +2,7 @@
 """User-space instructions per request of several server binaries, interleaved.
 
   python bench/instr_ab.py OUT_DIR head=build/release/hola r1=build/r1/hola [--rounds 3]
+  python bench/instr_ab.py OUT_DIR 'traced=build/release/hola' 'untraced=build/release/hola|--no-tracing'
 
 The CPU-time A/Bs (`bench/ab_report.py`) resolve about ±0.7 % per session on the shared box,
 as large as what is left between trees. The server's own code, though, is deterministic work
@@ -43,6 +44,8 @@ def build_counter(out: Path) -> Path:
 
 def run_side(counter: Path, label: str, exe: str, out: Path, rnd: int, cpus: list[int], lg_cpus: list[int],
              seconds: float, conns: int) -> dict:
+    exe, _, more = exe.partition("|")  # "path/to/hola|--no-tracing ...": extra server flags
+    extra = more.split()
     tag = f"{label}_{rnd}"
     pf = out / f"{tag}.port"
     pf.unlink(missing_ok=True)
@@ -50,7 +53,7 @@ def run_side(counter: Path, label: str, exe: str, out: Path, rnd: int, cpus: lis
     threads = len(cpus)
     srv = subprocess.Popen([str(counter), str(out / f"{tag}.counters.json"), "--", exe, "--host", "127.0.0.1",
                             "--port", "0", "--port-file", str(pf), "--threads", str(threads), "--cpu-list",
-                            ",".join(map(str, cpus)), "--busy-poll-us", "0", "--hostname", "ab"],
+                            ",".join(map(str, cpus)), "--busy-poll-us", "0", "--hostname", "ab", *extra],
                            stdout=log, stderr=log)
     deadline = time.monotonic() + 20
     while not (pf.exists() and pf.read_text().strip()):
@@ -84,7 +87,7 @@ def run_side(counter: Path, label: str, exe: str, out: Path, rnd: int, cpus: lis
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("out")
-    ap.add_argument("sides", nargs="+", help="label=path/to/hola")
+    ap.add_argument("sides", nargs="+", help="label=path/to/hola[|extra server flags]")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--seconds", type=float, default=5.0)
     ap.add_argument("--threads", type=int, default=4, help="server workers (and load-generator threads)")
