@@ -43,15 +43,19 @@ def build_counter(out: Path) -> Path:
 
 
 def run_side(counter: Path, label: str, exe: str, out: Path, rnd: int, cpus: list[int], lg_cpus: list[int],
-             seconds: float, conns: int) -> dict:
+             seconds: float, conns: int, count_loadgen: bool = False) -> dict:
     exe, _, more = exe.partition("|")  # "path/to/hola|--no-tracing ...": extra server flags
     extra = more.split()
+    # --count loadgen: the counters go on the load generator instead (its instructions per
+    # completed request); the server runs plainly
+    srv_wrap = [] if count_loadgen else [str(counter), str(out / f"{label}_{rnd}.counters.json"), "--"]
+    lg_wrap = [str(counter), str(out / f"{label}_{rnd}.counters.json"), "--"] if count_loadgen else []
     tag = f"{label}_{rnd}"
     pf = out / f"{tag}.port"
     pf.unlink(missing_ok=True)
     log = open(out / f"{tag}.log", "w")
     threads = len(cpus)
-    srv = subprocess.Popen([str(counter), str(out / f"{tag}.counters.json"), "--", exe, "--host", "127.0.0.1",
+    srv = subprocess.Popen([*srv_wrap, exe, "--host", "127.0.0.1",
                             "--port", "0", "--port-file", str(pf), "--threads", str(threads), "--cpu-list",
                             ",".join(map(str, cpus)), "--busy-poll-us", "0", "--hostname", "ab", *extra],
                            stdout=log, stderr=log)
@@ -61,7 +65,7 @@ def run_side(counter: Path, label: str, exe: str, out: Path, rnd: int, cpus: lis
             raise RuntimeError(f"{label}: server did not start (see {tag}.log)")
         time.sleep(0.02)
     port = int(pf.read_text().strip())
-    lg = subprocess.run([str(native.binary("hola_loadgen")), "--targets", f"127.0.0.1:{port}", "-c", str(conns),
+    lg = subprocess.run([*lg_wrap, str(native.binary("hola_loadgen")), "--targets", f"127.0.0.1:{port}", "-c", str(conns),
                          "-t", str(len(lg_cpus)), "--cpu-list", ",".join(map(str, lg_cpus)), "--path", "/api/hola",
                          "--expect-body", "Hola de ab", "--duration", str(seconds)],
                         capture_output=True, text=True, timeout=seconds + 60)
@@ -92,6 +96,8 @@ def main() -> int:
     ap.add_argument("--seconds", type=float, default=5.0)
     ap.add_argument("--threads", type=int, default=4, help="server workers (and load-generator threads)")
     ap.add_argument("--connections", type=int, default=64)
+    ap.add_argument("--count", choices=["server", "loadgen"], default="server",
+                    help="which side runs under the counters (per request served either way)")
     a = ap.parse_args()
     out = Path(a.out)
     out.mkdir(parents=True, exist_ok=True)
@@ -106,7 +112,8 @@ def main() -> int:
         for rnd in range(1, a.rounds + 1):
             order = sides if rnd % 2 else sides[::-1]
             for label, exe in order:
-                r = run_side(counter, label, exe, out, rnd, cpus, lg_cpus, a.seconds, a.connections)
+                r = run_side(counter, label, exe, out, rnd, cpus, lg_cpus, a.seconds, a.connections,
+                             a.count == "loadgen")
                 results.append(r)
                 f.write(json.dumps(r) + "\n")
                 f.flush()
