@@ -42,6 +42,33 @@ constexpr TcharTable kTchar;
 
 inline bool is_tchar(unsigned char c) { return kTchar.t[c]; }
 
+// Header-name comparison with a lowercase literal, eight bytes at a time. OR 0x20 folds the
+// letters, and on token characters (a validated field name) it maps nothing else onto a
+// literal's letters, digits or '-': the only other preimages, 0x0d/0x10-0x19, are controls. Not
+// for field values, which may hold control characters. (The per-character iequals loop was
+// ~35 instructions per known header.)
+template <size_t N>
+inline bool name_is(std::string_view name, const char (&lit)[N]) {
+  constexpr size_t n = N - 1;
+  static_assert(n >= 2 && n <= 24);
+  if (name.size() != n) return false;
+  auto word = [](const char* p, size_t k) {
+    uint64_t w = 0;
+    memcpy(&w, p, k);
+    return w;
+  };
+  constexpr uint64_t kFold = 0x2020202020202020ull;
+  if constexpr (n <= 8) {
+    const uint64_t mask = n == 8 ? kFold : kFold & ((uint64_t(1) << (8 * n)) - 1);
+    return (word(name.data(), n) | mask) == word(lit, n);
+  } else {
+    // words at 0, 8, ... and one ending at the last byte (overlapping)
+    for (size_t off = 0; off + 8 < n; off += 8)
+      if ((word(name.data() + off, 8) | kFold) != word(lit + off, 8)) return false;
+    return (word(name.data() + n - 8, 8) | kFold) == word(lit + n - 8, 8);
+  }
+}
+
 inline std::string_view trim_ows(std::string_view s) {
   while (!s.empty() && (s.front() == ' ' || s.front() == '\t')) s.remove_prefix(1);
   while (!s.empty() && (s.back() == ' ' || s.back() == '\t')) s.remove_suffix(1);
@@ -182,10 +209,33 @@ Parse parse_request(const char* buf, size_t len, Request* req, int* status) {
   const size_t t0 = ++i;
   size_t q = std::string_view::npos;
   bool bad_target = false;
-  for (; i < line_len && line[i] != ' '; ++i) {
-    const unsigned char c = (unsigned char)line[i];
-    if (c <= 0x20 || c == 0x7f) bad_target = true;
-    else if (c == '?' && q == std::string_view::npos) q = i - t0;
+  // Target: up to the next SP. With 32 bytes of the buffer at hand (within `len`: no read past
+  // the data), one AVX2 compare finds the SP, the first '?' and any control byte at once; a
+  // target of 32 bytes or more, or one with a control byte, takes the byte loop below, which
+  // decides the same (about 10 instructions per byte of "/api/hola" before).
+  if (len - pos - t0 >= 32) {
+    const __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(line + t0));
+    const uint32_t sp = uint32_t(_mm256_movemask_epi8(_mm256_cmpeq_epi8(v, _mm256_set1_epi8(' '))));
+    if (sp != 0) {
+      const uint32_t p = uint32_t(__builtin_ctz(sp));
+      const uint32_t before = (uint32_t(1) << p) - 1;  // p <= 31
+      const uint32_t ctl =
+          uint32_t(_mm256_movemask_epi8(_mm256_or_si256(
+              _mm256_cmpeq_epi8(_mm256_min_epu8(v, _mm256_set1_epi8(0x1f)), v),
+              _mm256_cmpeq_epi8(v, _mm256_set1_epi8(0x7f)))));
+      if (t0 + p < line_len && (ctl & before) == 0) {
+        const uint32_t qm = uint32_t(_mm256_movemask_epi8(_mm256_cmpeq_epi8(v, _mm256_set1_epi8('?')))) & before;
+        if (qm) q = __builtin_ctz(qm);
+        i = t0 + p;
+      }
+    }
+  }
+  if (i == t0) {
+    for (; i < line_len && line[i] != ' '; ++i) {
+      const unsigned char c = (unsigned char)line[i];
+      if (c <= 0x20 || c == 0x7f) bad_target = true;
+      else if (c == '?' && q == std::string_view::npos) q = i - t0;
+    }
   }
   if (i == line_len || i == t0) {
     *status = 400;
@@ -257,15 +307,15 @@ Parse parse_request(const char* buf, size_t len, Request* req, int* status) {
     std::string_view value = trim_ows(h.substr(colon + 1));
     switch (name.size()) {
       case 2:
-        if (iequals(name, "b3")) req->b3_single = value;
+        if (name_is(name, "b3")) req->b3_single = value;
         break;
       case 4:
-        if (iequals(name, "host")) req->host = value;
+        if (name_is(name, "host")) req->host = value;
         break;
       case 6:
-        if (iequals(name, "expect")) {
+        if (name_is(name, "expect")) {
           req->expect_continue = iequals(value, "100-continue");
-        } else if (iequals(name, "accept")) {
+        } else if (name_is(name, "accept")) {
           // Multiple Accept fields are equivalent to one comma-joined field; keep the first
           // and let the negotiation treat a second one conservatively (rare in practice).
           if (!req->has_accept) req->accept = value;
@@ -273,24 +323,24 @@ Parse parse_request(const char* buf, size_t len, Request* req, int* status) {
         }
         break;
       case 10:
-        if (iequals(name, "connection")) {
+        if (name_is(name, "connection")) {
           for_each_token(value, [&](std::string_view t) {
             if (iequals(t, "close")) conn_close = true;
             else if (iequals(t, "keep-alive")) conn_keep = true;
           });
-        } else if (iequals(name, "x-b3-flags")) {
+        } else if (name_is(name, "x-b3-flags")) {
           req->b3_flags = value;
         }
         break;
       case 12:
-        if (iequals(name, "x-b3-traceid")) req->b3_trace_id = value;
-        else if (iequals(name, "x-b3-sampled")) req->b3_sampled = value;
+        if (name_is(name, "x-b3-traceid")) req->b3_trace_id = value;
+        else if (name_is(name, "x-b3-sampled")) req->b3_sampled = value;
         break;
       case 11:
-        if (iequals(name, "x-b3-spanid")) req->b3_span_id = value;
+        if (name_is(name, "x-b3-spanid")) req->b3_span_id = value;
         break;
       case 14:
-        if (iequals(name, "content-length")) {
+        if (name_is(name, "content-length")) {
           int64_t v;
           if (!parse_uint(value, &v) || (have_cl && v != req->content_length)) {
             *status = 400;
@@ -301,7 +351,7 @@ Parse parse_request(const char* buf, size_t len, Request* req, int* status) {
         }
         break;
       case 17:
-        if (iequals(name, "transfer-encoding")) {
+        if (name_is(name, "transfer-encoding")) {
           have_te = true;
           std::string_view last;
           for_each_token(value, [&](std::string_view t) { last = t; });
@@ -311,7 +361,7 @@ Parse parse_request(const char* buf, size_t len, Request* req, int* status) {
             *status = 501;
             return Parse::kError;
           }
-        } else if (iequals(name, "x-b3-parentspanid")) {
+        } else if (name_is(name, "x-b3-parentspanid")) {
           req->b3_parent_id = value;
         }
         break;

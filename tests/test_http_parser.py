@@ -118,6 +118,52 @@ def test_fuzz_parser_total(native, data):
     assert r == "incomplete" or isinstance(r, (int, dict))
 
 
+_target_bytes = st.lists(st.sampled_from([b"a", b"Z", b"/", b"?", b"%", b".", b" ", b"\t", b"\x01", b"\x7f", b"\x1f",
+                                          b"=", b"\x80", b"~"]), min_size=0, max_size=45).map(b"".join)
+
+
+def _without_head_bytes(r):
+    return {k: v for k, v in r.items() if k != "head_bytes"} if isinstance(r, dict) else r
+
+
+@settings(max_examples=600, deadline=None)
+@given(_target_bytes, st.sampled_from([b"HTTP/1.1", b"HTTP/1.0", b"HTTP/2.0", b"HTTP/1.x"]))
+def test_vector_and_byte_target_scans_agree(native, target, version):
+    """The request target is scanned 32 bytes at a time when the buffer holds 32 more bytes,
+    byte by byte otherwise. A padding header makes the same request line take the vector path:
+    every outcome (fields, '?' split, 400 for control bytes or a missing SP, 505) must match."""
+    def parse(raw):
+        try:
+            return native.parse_request(raw)
+        except UnicodeDecodeError:  # parsed, but the binding cannot hand a 0x80 target to Python
+            return "parsed, not UTF-8"
+
+    line = b"GET " + target + b" " + version + b"\r\n"
+    short = parse(line + b"\r\n")
+    padded = parse(line + b"X-Pad: " + b"p" * 40 + b"\r\n\r\n")
+    assert _without_head_bytes(short) == _without_head_bytes(padded), (target, version)
+
+
+_known = ["Host", "Accept", "Expect", "Connection", "Content-Length", "Transfer-Encoding", "b3", "X-B3-TraceId",
+          "X-B3-SpanId", "X-B3-ParentSpanId", "X-B3-Sampled", "X-B3-Flags"]
+
+
+@settings(max_examples=300, deadline=None)
+@given(st.sampled_from(_known), st.data())
+def test_header_names_match_case_insensitively_and_nothing_else(native, name, data):
+    """Header names are compared eight bytes at a time with a case fold: any mix of case
+    matches, a name one token character off does not."""
+    mixed = "".join(c.upper() if data.draw(st.booleans()) else c.lower() for c in name)
+    assert native.parse_request(f"GET / HTTP/1.1\r\n{mixed}: 7\r\n\r\n".encode()) == \
+        native.parse_request(f"GET / HTTP/1.1\r\n{name.lower()}: 7\r\n\r\n".encode())
+    pos = data.draw(st.integers(min_value=0, max_value=len(name) - 1))
+    other = data.draw(st.sampled_from([c for c in "abcxyz0189-^~_!" if c.lower() != name[pos].lower()]))
+    off = name[:pos] + other + name[pos + 1:]
+    r = native.parse_request(f"GET / HTTP/1.1\r\n{off}: 7\r\n\r\n".encode())
+    plain = native.parse_request(b"GET / HTTP/1.1\r\n\r\n")
+    assert _without_head_bytes(r) == _without_head_bytes(plain), off  # an unknown header changes nothing
+
+
 # ---- negotiation ----
 
 @pytest.mark.parametrize("accept,ok", [
