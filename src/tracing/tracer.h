@@ -45,7 +45,7 @@ struct ServerSpan {
   uint8_t method_len = 0;
   char method[8] = {0};
   uint16_t url_len = 0;
-  char url[kMaxUrl] = {0};
+  char url[kMaxUrl];  // the first url_len bytes; not cleared (a span per request, most never recorded)
 };
 
 enum class Kind : uint8_t { kServer = 0, kClient = 1 };
