@@ -126,11 +126,12 @@ void EventLoop::run_timers() {
     note(0, id, 0);
     cb();
   }
-  // Drop cancelled entries at the top so they do not cause spurious wakeups.
-  while (!heap_.empty() && !timers_.count(heap_.top().id)) heap_.pop();
 }
 
 int EventLoop::next_timeout_ms() {
+  // About to block: drop cancelled entries at the top first, so that a cancelled timer cannot
+  // wake the loop at its old deadline (passes that find work skip this lookup; see run()).
+  while (!heap_.empty() && !timers_.count(heap_.top().id)) heap_.pop();
   if (heap_.empty()) return -1;
   int64_t d = heap_.top().deadline - mono_ms();
   if (d <= 0) return 0;

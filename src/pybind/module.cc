@@ -417,6 +417,10 @@ std::pair<std::string, std::string> stall_report_probe() {
   h.hold.store(false);
   char buf[256];
   (void)::recv(fd, buf, sizeof buf, 0);
+  // The response leaves from inside the handler: wait for the worker to finish that pass and
+  // block in epoll_wait again before watching its passes.
+  for (int k = 0; k < 1000 && s.activity(0).find("phase wait") == std::string::npos; ++k)
+    std::this_thread::sleep_for(std::chrono::milliseconds(1));
   std::string after = s.stall_report(0, false);
   ::close(fd);
   s.shutdown(100);
