@@ -65,6 +65,7 @@
 #include "core/affinity.h"
 #include "core/clock.h"
 #include "core/net.h"
+#include "core/scan.h"
 
 using namespace hola;
 using hola::Histogram;
@@ -295,7 +296,7 @@ int response_complete(Conn* c, size_t from, int* status, bool* close, size_t* us
   const char* s = c->buf + from;
   const size_t n = c->have - from;
   auto incomplete = [&] { return (from == 0 && c->have >= sizeof c->buf) ? -1 : 0; };  // head > buf
-  const char* nl = static_cast<const char*>(memchr(s, '\n', n));
+  const char* nl = hola::find_newline(s, n);
   if (!nl) return incomplete();
   if (nl - s < 12 || memcmp(s, "HTTP/", 5) != 0) return -1;
   *status = (s[9] - '0') * 100 + (s[10] - '0') * 10 + (s[11] - '0');
@@ -303,7 +304,7 @@ int response_complete(Conn* c, size_t from, int* status, bool* close, size_t* us
   size_t cl = 0, p = size_t(nl - s) + 1;
   for (;;) {
     const char* line = s + p;
-    const char* e = static_cast<const char*>(memchr(line, '\n', n - p));
+    const char* e = hola::find_newline(line, n - p);
     if (!e) return incomplete();
     size_t len = size_t(e - line);
     p += len + 1;

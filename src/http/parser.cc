@@ -1,5 +1,7 @@
 #include "http/parser.h"
 
+#include "core/scan.h"
+
 #include <immintrin.h>
 
 #include <cstring>
@@ -183,7 +185,7 @@ Parse parse_request(const char* buf, size_t len, Request* req, int* status) {
 
   // ---- request line ----
   const char* line = buf + pos;
-  const char* nl = static_cast<const char*>(memchr(line, '\n', len - pos));
+  const char* nl = find_newline(line, len - pos);
   if (!nl) {
     if (len - pos > kMaxRequestLine) {
       *status = 414;
@@ -278,7 +280,7 @@ Parse parse_request(const char* buf, size_t len, Request* req, int* status) {
       return Parse::kIncomplete;
     }
     const char* hl = buf + p;
-    const char* he = static_cast<const char*>(memchr(hl, '\n', len - p));
+    const char* he = find_newline(hl, len - p);
     if (!he) {
       if (len > kMaxHeadBytes) {
         *status = 431;
