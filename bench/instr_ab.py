@@ -43,9 +43,14 @@ def build_counter(out: Path) -> Path:
 
 
 def run_side(counter: Path, label: str, exe: str, out: Path, rnd: int, cpus: list[int], lg_cpus: list[int],
-             seconds: float, conns: int, count_loadgen: bool = False) -> dict:
+             seconds: float, conns: int, count_loadgen: bool = False, aloha_port: int = 0) -> dict:
     exe, _, more = exe.partition("|")  # "path/to/hola|--no-tracing ...": extra server flags
     extra = more.split()
+    path, expect = "/api/hola", ["--expect-body", "Hola de ab"]
+    if aloha_port:  # --chain: this server is hola A, calling hola B as its aloha
+        extra += ["--aloha-url", f"http://127.0.0.1:{aloha_port}/", "--aloha-path", "api/hola-chaining",
+                  "--feign-log", "none", "--hystrix-pool-size", "128"]
+        path, expect = "/api/hola-chaining", ["--verify-body"]
     # --count loadgen: the counters go on the load generator instead (its instructions per
     # completed request); the server runs plainly
     srv_wrap = [] if count_loadgen else [str(counter), str(out / f"{label}_{rnd}.counters.json"), "--"]
@@ -66,8 +71,8 @@ def run_side(counter: Path, label: str, exe: str, out: Path, rnd: int, cpus: lis
         time.sleep(0.02)
     port = int(pf.read_text().strip())
     lg = subprocess.run([*lg_wrap, str(native.binary("hola_loadgen")), "--targets", f"127.0.0.1:{port}", "-c", str(conns),
-                         "-t", str(len(lg_cpus)), "--cpu-list", ",".join(map(str, lg_cpus)), "--path", "/api/hola",
-                         "--expect-body", "Hola de ab", "--duration", str(seconds)],
+                         "-t", str(len(lg_cpus)), "--cpu-list", ",".join(map(str, lg_cpus)), "--path", path,
+                         *expect, "--duration", str(seconds)],
                         capture_output=True, text=True, timeout=seconds + 60)
     srv.send_signal(signal.SIGTERM)
     srv.wait(timeout=30)
@@ -98,6 +103,9 @@ def main() -> int:
     ap.add_argument("--connections", type=int, default=64)
     ap.add_argument("--count", choices=["server", "loadgen"], default="server",
                     help="which side runs under the counters (per request served either way)")
+    ap.add_argument("--chain", action="store_true",
+                    help="/api/hola-chaining: each side is hola A, calling one uncounted hola B (as "
+                         "bench/chain_bench.py: B answers with its own fallback) on cores of its own")
     a = ap.parse_args()
     out = Path(a.out)
     out.mkdir(parents=True, exist_ok=True)
@@ -107,17 +115,39 @@ def main() -> int:
     if len(cores) < 2 * a.threads:
         raise SystemExit(f"need {2 * a.threads} physical cores, have {len(cores)}")
     cpus, lg_cpus = cores[:a.threads], cores[a.threads:2 * a.threads]
+    b_proc, aloha_port = None, 0
+    if a.chain:
+        b_cpus = cores[2 * a.threads:3 * a.threads]
+        if len(b_cpus) < a.threads:
+            raise SystemExit(f"--chain needs {3 * a.threads} physical cores, have {len(cores)}")
+        pf = out / "b.port"
+        pf.unlink(missing_ok=True)
+        b_log = open(out / "b.log", "w")
+        b_proc = subprocess.Popen([str(native.binary("hola")), "--host", "127.0.0.1", "--port", "0", "--port-file",
+                                   str(pf), "--threads", str(len(b_cpus)), "--cpu-list", ",".join(map(str, b_cpus)),
+                                   "--hostname", "B", "--aloha-url", "http://127.0.0.1:1/", "--feign-log", "none",
+                                   "--no-tracing", "--feign-retry", "off", "--log-level", "warn"],
+                                  stdout=b_log, stderr=b_log)
+        deadline = time.monotonic() + 20
+        while not (pf.exists() and pf.read_text().strip()):
+            if b_proc.poll() is not None or time.monotonic() > deadline:
+                raise SystemExit("hola B did not start (b.log)")
+            time.sleep(0.02)
+        aloha_port = int(pf.read_text().strip())
     results = []
     with open(out / "runs.jsonl", "w") as f:
         for rnd in range(1, a.rounds + 1):
             order = sides if rnd % 2 else sides[::-1]
             for label, exe in order:
                 r = run_side(counter, label, exe, out, rnd, cpus, lg_cpus, a.seconds, a.connections,
-                             a.count == "loadgen")
+                             a.count == "loadgen", aloha_port)
                 results.append(r)
                 f.write(json.dumps(r) + "\n")
                 f.flush()
                 print(json.dumps(r), flush=True)
+    if b_proc:
+        b_proc.terminate()
+        b_proc.wait(timeout=30)
     summary = {}
     for label, _ in sides:
         ipr = [r["instructions_per_req"] for r in results if r["side"] == label and "instructions_per_req" in r]
