@@ -23,14 +23,17 @@ import sys
 
 
 def parse(path: str) -> dict:
-    prof = {"threads": {}, "maps": [], "stacks": [], "period_ns": 0, "samples": 0, "dropped": 0}
+    prof = {"threads": {}, "maps": [], "stacks": [], "period_ns": 0, "samples": 0, "dropped": 0,
+            "event": "cpu-time", "period_cycles": 0}
     with open(path) as f:
         for line in f:
             parts = line.split()
             if not parts or parts[0].startswith("#"):
                 continue
-            if parts[0] in ("period_ns", "samples", "dropped"):
+            if parts[0] in ("period_ns", "samples", "dropped", "period_cycles"):
                 prof[parts[0]] = int(parts[1])
+            elif parts[0] == "event":  # HOLA_CPUPROF_EVENT=user-cycles
+                prof["event"] = parts[1]
             elif parts[0] == "thread":
                 prof["threads"][int(parts[1])] = parts[2] if len(parts) > 2 else "?"
             elif parts[0] == "map":
@@ -163,8 +166,14 @@ def main() -> int:
     ap.add_argument("--json", default="", help="also write the report here")
     a = ap.parse_args()
     rep = report(parse(a.profile), a.top, a.threads)
-    cpu_s = rep["samples"] * rep["period_ns"] / 1e9
-    print(f"{rep['samples']} samples ({cpu_s:.2f} CPU-s) of threads '{a.threads or '*'}'; dropped {rep['dropped']}")
+    prof = parse(a.profile)
+    if prof["event"] == "user-cycles":
+        print(f"{rep['samples']} samples of {prof['period_cycles']} user-space cycles each "
+              f"({rep['samples'] * prof['period_cycles'] / 1e9:.2f} G cycles) of threads '{a.threads or '*'}'; "
+              f"dropped {rep['dropped']}")
+    else:
+        cpu_s = rep["samples"] * rep["period_ns"] / 1e9
+        print(f"{rep['samples']} samples ({cpu_s:.2f} CPU-s) of threads '{a.threads or '*'}'; dropped {rep['dropped']}")
     print("threads:", ", ".join(f"{k} {v}" for k, v in rep["threads"].items()))
     print("\nby object (self):")
     for k, v in rep["by_object"].items():

@@ -1,7 +1,10 @@
 #include "core/cpuprof.h"
 
 #include <errno.h>
+#include <fcntl.h>
+#include <linux/perf_event.h>
 #include <pthread.h>
+#include <sys/ioctl.h>
 #include <signal.h>
 #include <sys/syscall.h>
 #include <time.h>
@@ -15,6 +18,8 @@
 #include <thread>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <fstream>
 #include <map>
 #include <memory>
@@ -258,10 +263,47 @@ std::string describe_pcs(const uintptr_t* pcs, int n) {
   return out;
 }
 
+// HOLA_CPUPROF_EVENT=user-cycles: sample every HOLA_CPUPROF_PERIOD (default 200,000) cycles
+// spent in user space instead of every period of CPU time. The hardware counter's overflow
+// signal is routed to the thread as SIGPROF (same handler, same stacks). The CPU-time profile
+// of a syscall-bound server is ~93 % send/recv/epoll_wait; this one shows only the server's
+// own work (and libc's). Threads fall back to the CPU-time timer where no PMU is present.
+bool g_user_cycles = false;
+uint64_t g_cycles_period = 200000;
+std::vector<int> g_event_fds;  // under g_mu
+thread_local int t_event_fd = -1;
+
+int open_user_cycles() {
+  perf_event_attr a;
+  memset(&a, 0, sizeof a);
+  a.type = PERF_TYPE_HARDWARE;
+  a.size = sizeof a;
+  a.config = PERF_COUNT_HW_CPU_CYCLES;
+  a.sample_period = g_cycles_period;
+  a.wakeup_events = 1;
+  a.exclude_kernel = 1;
+  a.exclude_hv = 1;
+  a.disabled = 1;
+  const int fd = int(syscall(SYS_perf_event_open, &a, 0, -1, -1, PERF_FLAG_FD_CLOEXEC));
+  if (fd < 0) return -1;
+  f_owner_ex owner{F_OWNER_TID, pid_t(syscall(SYS_gettid))};
+  if (fcntl(fd, F_SETFL, O_ASYNC | O_NONBLOCK) != 0 || fcntl(fd, F_SETSIG, SIGPROF) != 0 ||
+      fcntl(fd, F_SETOWN_EX, &owner) != 0 || ioctl(fd, PERF_EVENT_IOC_RESET, 0) != 0 ||
+      ioctl(fd, PERF_EVENT_IOC_ENABLE, 0) != 0) {
+    close(fd);
+    return -1;
+  }
+  return fd;
+}
+
 bool start(const std::string& path, int hz) {
   if (g_on.load() || hz <= 0) return false;
   g_path = path;
   g_period_ns = 1000000000L / hz;
+  if (const char* e = getenv("HOLA_CPUPROF_EVENT"); e && strcmp(e, "user-cycles") == 0) {
+    g_user_cycles = true;
+    if (const char* p = getenv("HOLA_CPUPROF_PERIOD"); p && atoll(p) > 0) g_cycles_period = uint64_t(atoll(p));
+  }
   g_samples.reset(new Sample[kCapacity]);
   load_exec_ranges();
   g_own_range = exec_range(uintptr_t(&on_prof));
@@ -283,11 +325,30 @@ void register_thread() {
   sev.sigev_signo = SIGPROF;
   sev._sigev_un._tid = pid_t(syscall(SYS_gettid));
   note_stack_bounds();
+  if (g_user_cycles) {
+    // t_index first: an overflow may arrive as soon as the counter is enabled
+    {
+      std::lock_guard<std::mutex> g(g_mu);
+      t_index = int(g_names.size());
+      g_names.push_back(name);
+    }
+    t_event_fd = open_user_cycles();
+    if (t_event_fd >= 0) {
+      std::lock_guard<std::mutex> g(g_mu);
+      g_event_fds.push_back(t_event_fd);
+      t_armed = true;
+      return;
+    }
+    std::lock_guard<std::mutex> g(g_mu);
+    g_names[size_t(t_index)] += " (CPU-time timer: no cycle counter)";
+  }
   if (timer_create(CLOCK_THREAD_CPUTIME_ID, &sev, &t_timer) != 0) return;
   {
     std::lock_guard<std::mutex> g(g_mu);
-    t_index = int(g_names.size());
-    g_names.push_back(name);
+    if (t_index < 0) {
+      t_index = int(g_names.size());
+      g_names.push_back(name);
+    }
     g_timers.push_back(t_timer);
   }
   itimerspec its{};
@@ -299,8 +360,12 @@ void register_thread() {
 
 void unregister_thread() {
   if (!t_armed) return;
-  itimerspec off{};
-  timer_settime(t_timer, 0, &off, nullptr);
+  if (t_event_fd >= 0) {
+    ioctl(t_event_fd, PERF_EVENT_IOC_DISABLE, 0);
+  } else {
+    itimerspec off{};
+    timer_settime(t_timer, 0, &off, nullptr);
+  }
   t_armed = false;
 }
 
@@ -310,6 +375,7 @@ bool write() {
     std::lock_guard<std::mutex> g(g_mu);
     itimerspec off{};
     for (timer_t t : g_timers) timer_settime(t, 0, &off, nullptr);
+    for (int fd : g_event_fds) ioctl(fd, PERF_EVENT_IOC_DISABLE, 0);
   }
   const size_t n = std::min(g_next.load(), kCapacity);
   // identical (thread, stack) samples are written once with their count
@@ -320,7 +386,9 @@ bool write() {
   }
   std::ofstream f(g_path);
   if (!f) return false;
-  f << "# hola cpu profile\nperiod_ns " << g_period_ns << "\nsamples " << n << "\ndropped "
+  f << "# hola cpu profile\n";
+  if (g_user_cycles && !g_event_fds.empty()) f << "event user-cycles\nperiod_cycles " << g_cycles_period << "\n";
+  f << "period_ns " << g_period_ns << "\nsamples " << n << "\ndropped "
     << (g_next.load() > kCapacity ? g_next.load() - kCapacity : 0) << "\n";
   {
     std::lock_guard<std::mutex> g(g_mu);
