@@ -33,6 +33,27 @@ def test_cpu_profile_samples_workers_under_load(hola, tmp_path):
     assert any("hola::http::Connection::" in fn for fn in names), names
 
 
+def test_user_cycle_profile_or_its_fallback(hola, tmp_path):
+    """HOLA_CPUPROF_EVENT=user-cycles samples user-space cycles through the hardware counter
+    where there is one (the box), and says so in the file; without a PMU (this container's VM)
+    each thread falls back to the CPU-time timer, says so in its name, and the file is the
+    plain CPU-time profile. Either way the report reads it."""
+    prof = tmp_path / "cyc.prof"
+    s = hola(args=["--cpu-profile", str(prof)], threads=2, env={"HOLA_CPUPROF_EVENT": "user-cycles",
+                                                                "HOLA_CPUPROF_PERIOD": "100000"})
+    res = run_duration([("127.0.0.1", s.port)], 8, 2, 1.0, 0.2)
+    assert res["latency"]["errors"] == 0
+    assert s.stop() == 0
+    text = prof.read_text()
+    if "event user-cycles" in text:
+        assert "period_cycles 100000" in text and " hola-w0\n" in text
+    else:
+        assert " hola-w0 (CPU-time timer: no cycle counter)" in text
+    out = subprocess.run([sys.executable, str(ROOT / "bench/cpuprof_report.py"), str(prof)],
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0 and "samples" in out.stdout, out.stderr
+
+
 def test_loadgen_cpu_profile(hola, tmp_path):
     from hola_amd.parallel.loadgen import ControlledLoadgen
 
