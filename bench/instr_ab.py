@@ -135,19 +135,21 @@ def main() -> int:
             time.sleep(0.02)
         aloha_port = int(pf.read_text().strip())
     results = []
-    with open(out / "runs.jsonl", "w") as f:
-        for rnd in range(1, a.rounds + 1):
-            order = sides if rnd % 2 else sides[::-1]
-            for label, exe in order:
-                r = run_side(counter, label, exe, out, rnd, cpus, lg_cpus, a.seconds, a.connections,
-                             a.count == "loadgen", aloha_port)
-                results.append(r)
-                f.write(json.dumps(r) + "\n")
-                f.flush()
-                print(json.dumps(r), flush=True)
-    if b_proc:
-        b_proc.terminate()
-        b_proc.wait(timeout=30)
+    try:
+        with open(out / "runs.jsonl", "w") as f:
+            for rnd in range(1, a.rounds + 1):
+                order = sides if rnd % 2 else sides[::-1]
+                for label, exe in order:
+                    r = run_side(counter, label, exe, out, rnd, cpus, lg_cpus, a.seconds, a.connections,
+                                 a.count == "loadgen", aloha_port)
+                    results.append(r)
+                    f.write(json.dumps(r) + "\n")
+                    f.flush()
+                    print(json.dumps(r), flush=True)
+    finally:
+        if b_proc:
+            b_proc.terminate()
+            b_proc.wait(timeout=30)
     summary = {}
     for label, _ in sides:
         ipr = [r["instructions_per_req"] for r in results if r["side"] == label and "instructions_per_req" in r]
