@@ -67,16 +67,20 @@ def run_side(counter: Path, label: str, exe: str, out: Path, rnd: int, cpus: lis
     deadline = time.monotonic() + 20
     while not (pf.exists() and pf.read_text().strip()):
         if srv.poll() is not None or time.monotonic() > deadline:
+            srv.kill()
+            srv.wait()
             raise RuntimeError(f"{label}: server did not start (see {tag}.log)")
         time.sleep(0.02)
     port = int(pf.read_text().strip())
-    lg = subprocess.run([*lg_wrap, str(native.binary("hola_loadgen")), "--targets", f"127.0.0.1:{port}", "-c", str(conns),
-                         "-t", str(len(lg_cpus)), "--cpu-list", ",".join(map(str, lg_cpus)), "--path", path,
-                         *expect, "--duration", str(seconds)],
-                        capture_output=True, text=True, timeout=seconds + 60)
-    srv.send_signal(signal.SIGTERM)
-    srv.wait(timeout=30)
-    log.close()
+    try:
+        lg = subprocess.run([*lg_wrap, str(native.binary("hola_loadgen")), "--targets", f"127.0.0.1:{port}", "-c", str(conns),
+                             "-t", str(len(lg_cpus)), "--cpu-list", ",".join(map(str, lg_cpus)), "--path", path,
+                             *expect, "--duration", str(seconds)],
+                            capture_output=True, text=True, timeout=seconds + 60)
+    finally:
+        srv.send_signal(signal.SIGTERM)
+        srv.wait(timeout=30)
+        log.close()
     text = (out / f"{tag}.log").read_text()
     m = re.search(r"shutdown complete \((\d+) requests served\)", text)
     if lg.returncode != 0 or not m:
