@@ -32,7 +32,8 @@ class HolaProcess:
         self.cpu_list = cpu_list
         self.exe = exe or binary("hola", preset)
         keep = ("PATH", "LANG", "LC_ALL", "TMPDIR", "LD_LIBRARY_PATH", "TSAN_OPTIONS", "ASAN_OPTIONS",
-                "UBSAN_OPTIONS", "LSAN_OPTIONS", "SSL_CERT_FILE", "SSL_CERT_DIR")
+                "UBSAN_OPTIONS", "LSAN_OPTIONS", "SSL_CERT_FILE", "SSL_CERT_DIR",
+                "HOLA_CPUPROF_EVENT", "HOLA_CPUPROF_PERIOD")  # --cpu-profile's sampling event
         base = dict(os.environ) if inherit_env else {k: v for k, v in os.environ.items() if k in keep}
         if not inherit_env:
             base.pop("HOSTNAME", None)
