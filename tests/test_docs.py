@@ -11,7 +11,8 @@ OPS = (ROOT / "docs" / "OPERATIONS.md").read_text()
 
 def test_operations_metrics_are_exported(hola):
     # (the package and the native binaries are not metrics)
-    names = set(re.findall(r"`(hola_[a-z_]+)", OPS)) - {"hola_amd", "hola_loadgen", "hola_rrproxy", "hola_zipkin_sink", "hola_fpstack"}
+    names = set(re.findall(r"`(hola_[a-z_]+)", OPS)) - {"hola_amd", "hola_loadgen", "hola_rrproxy", "hola_zipkin_sink", "hola_fpstack",
+                                                      "hola_micro"}
     with FakeAloha() as aloha, FakeZipkin() as zipkin:
         s = hola(args=["--aloha-url", aloha.url, "--zipkin-url", zipkin.url, "--feign-log", "none",
                        "--busy-poll-us", "auto"])  # the spin counters exist only while spinning adapts
@@ -30,7 +31,8 @@ def test_operations_flags_are_accepted(hola_bin):
     help_text = subprocess.run([str(hola_bin), "--help"], capture_output=True, text=True).stdout + \
         subprocess.run([str(hola_bin), "--help"], capture_output=True, text=True).stderr
     flags = set(re.findall(r"`(--[a-z][a-z0-9-]+)", OPS)) - {"--replicas", "--out", "--lb", "--minutes", "--zipkin-sink",
-                                                              "--profile-out", "--proxy-threads"}
+                                                              "--profile-out", "--proxy-threads",
+                                                              "--count", "--chain"}  # bench/instr_ab.py's
     missing = sorted(f for f in flags if f not in help_text)
     assert not missing, missing
 
