@@ -469,7 +469,10 @@ void HolaApp::handle_chaining(http::Connection& c, const http::Request& r, Worke
   std::shared_ptr<const Content> content = wc.content;
   HolaApp* self = this;
   chainer_->call(c.worker(), traced ? &span.ctx : nullptr,
-                 [self, conn, content, ka_req = ka, head, traced, span, t0](const ChainResult& res) {
+                 // conn and content are moved in: a shared_ptr copy is two locked
+                 // read-modify-writes per request, each draining the store buffer
+                 [self, conn = std::move(conn), content = std::move(content), ka_req = ka, head, traced, span,
+                  t0](const ChainResult& res) {
                    http::Worker& w = conn->worker();
                    // termination may have begun while the call was parked
                    const int ka = ka_req && !w.server().closing() ? 1 : 0;
