@@ -422,9 +422,11 @@ bool Command::cancel_queued(const Queued& q) {
 }
 
 void Command::release_slot() {
-  int64_t a = active_.load(std::memory_order_relaxed);
-  while (a > 0 && !active_.compare_exchange_weak(a, a - 1, std::memory_order_acq_rel)) {
-  }
+  // One read-modify-write on the shared counter (every worker's calls update it): a CAS loop
+  // guarding against going below 0 retried under contention, and was most of finish_in's
+  // cycles on the chaining path (profiles/round4/14_user_cycles). A release without its
+  // acquisition cannot happen; should one, the count is put back at once.
+  if (active_.fetch_sub(1, std::memory_order_acq_rel) <= 0) active_.fetch_add(1, std::memory_order_relaxed);
 }
 
 void Command::queued_timeout(int64_t total_ms, bool with_fallback) {
@@ -442,9 +444,7 @@ int64_t Command::queue_size() {
 }
 
 void Command::finish_in(Shard& sh, int64_t now, Event outcome, int64_t execute_ms) {
-  int64_t a = active_.load(std::memory_order_relaxed);
-  while (a > 0 && !active_.compare_exchange_weak(a, a - 1, std::memory_order_acq_rel)) {
-  }
+  release_slot();
   if (!semaphore_.load(std::memory_order_relaxed)) ++sh.completed;  // tasks run on the pool
   sh.counter.add(now, outcome);
   if (outcome == Event::kSuccess || outcome == Event::kFailure) sh.exec_lat.add(now, execute_ms);
