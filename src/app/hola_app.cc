@@ -324,6 +324,27 @@ std::string_view canonical_path(std::string_view path, std::string* storage) {
 // memchr call per path character: +12 % of the headline server's user-space instructions,
 // found by bench/instr_ab.py over every commit since round 1, profiles/round4/11_instr.)
 inline bool needs_canonical(std::string_view p) {
+  // Eight bytes at a time for any ';', '%' or '.' (a word has a byte equal to c when
+  // (x - 0x01..) & ~x & 0x80.. is non-zero for x = word ^ c*0x01..); only a path holding a '.'
+  // takes the exact "/." pass. The byte loop was a quarter of on_request's user cycles.
+  constexpr uint64_t k1 = 0x0101010101010101ull, k80 = 0x8080808080808080ull;
+  auto has = [](uint64_t w, unsigned char c) {
+    const uint64_t x = w ^ (k1 * c);
+    return ((x - k1) & ~x & k80) != 0;
+  };
+  size_t i = 0;
+  bool dot = false;
+  for (; i + 8 <= p.size() && !dot; i += 8) {
+    uint64_t w;
+    memcpy(&w, p.data() + i, 8);
+    if (has(w, ';') || has(w, '%')) return true;
+    dot = has(w, '.');
+  }
+  for (; i < p.size() && !dot; ++i) {
+    if (p[i] == ';' || p[i] == '%') return true;
+    dot = p[i] == '.';
+  }
+  if (!dot) return false;
   char prev = 0;
   for (const char c : p) {
     if (c == ';' || c == '%' || (c == '.' && prev == '/')) return true;
