@@ -14,6 +14,7 @@
 #include "core/clock.h"
 
 #include "core/net.h"
+#include "core/scan.h"
 #include "http/parser.h"
 
 namespace hola::client {
@@ -260,51 +261,96 @@ namespace {
 // One response from the front of `in`: 1 = complete (*consumed bytes; *close when the
 // connection cannot carry another response), 0 = need more, -1 = malformed. *head_ok is set
 // once a well-formed status line and header block have arrived.
+// Header name (before the colon) against a lower-case literal, a word at a time with a case
+// fold (letters, digits and '-' are fixed by OR 0x20; see http::parser's name_is).
+template <size_t N>
+inline bool field_is(std::string_view k, const char (&lit)[N]) {
+  constexpr size_t n = N - 1;
+  if (k.size() != n) return false;
+  auto word = [](const char* q, size_t m) {
+    uint64_t w = 0;
+    memcpy(&w, q, m);
+    return w;
+  };
+  constexpr uint64_t kFold = 0x2020202020202020ull;
+  for (size_t off = 0; off + 8 < n; off += 8)
+    if ((word(k.data() + off, 8) | kFold) != word(lit + off, 8)) return false;
+  return (word(k.data() + n - 8, 8) | kFold) == word(lit + n - 8, 8);
+}
+
 int parse_response(std::string_view in, bool eof, ClientResult* r, bool* close, size_t* consumed, bool* head_ok) {
-  size_t he = in.find("\r\n\r\n");
-  if (he == std::string_view::npos) return in.size() > 64 * 1024 ? -1 : 0;
-  std::string_view head(in.data(), he);
-  if (head.size() < 12 || head.substr(0, 5) != "HTTP/") return -1;
+  // One pass over the head's lines (each newline found inline when the line is short,
+  // core/scan.h): a find("\r\n\r\n") followed by a find("\r\n") and a find(':') per line
+  // was a memchr call per candidate, most of this function's cycles (profiles/round4/
+  // 14_user_cycles). Lines end in CRLF; a bare LF is accepted as HttpClient does.
+  const char* s = in.data();
+  const size_t n = in.size();
+  auto need_more = [&] { return n > 64 * 1024 ? -1 : 0; };
+  const char* nl = find_newline(s, n);
+  if (!nl) return need_more();
+  std::string_view head(s, size_t(nl - s));
+  if (!head.empty() && head.back() == '\r') head.remove_suffix(1);
+  if (head.size() < 12 || head.substr(0, 5) != "HTTP/") {
+    // a status line may only be judged once it is complete
+    return -1;
+  }
   int status = 0;
   for (size_t k = 9; k < 12; ++k) {
     if (head[k] < '0' || head[k] > '9') return -1;
     status = status * 10 + (head[k] - '0');
   }
   if (status < 100) return -1;
-  bool http10 = head.substr(5, 3) == "1.0";
-  const size_t eol = std::min(head.find("\r\n"), head.size());
-  r->reason.assign(eol > 13 && head[12] == ' ' ? head.substr(13, eol - 13) : std::string_view());
-  r->has_retry_after = false;
+  const bool http10 = head.substr(5, 3) == "1.0";
   int64_t cl = -1;
   bool chunked = false;
-  *close = http10;
-  size_t p = head.find("\r\n");
-  while (p != std::string_view::npos && p + 2 <= head.size()) {
-    size_t n = head.find("\r\n", p + 2);
-    std::string_view line = head.substr(p + 2, n == std::string_view::npos ? std::string_view::npos : n - p - 2);
-    size_t colon = line.find(':');
-    if (colon != std::string_view::npos) {
-      std::string_view k = line.substr(0, colon), v = line.substr(colon + 1);
-      while (!v.empty() && (v.front() == ' ' || v.front() == '\t')) v.remove_prefix(1);
-      if (http::iequals(k, "content-length")) {
-        cl = 0;
-        for (char d : v) {
-          if (d < '0' || d > '9') break;
-          cl = cl * 10 + (d - '0');
-          if (cl > (1 << 20)) break;  // over the body cap: rejected below
+  bool has_retry_after = false;
+  int64_t retry_after_ms = 0;
+  bool conn_close = http10;
+  size_t p = size_t(nl - s) + 1;
+  for (;;) {
+    const char* e = find_newline(s + p, n - p);
+    if (!e) return need_more();
+    std::string_view line(s + p, size_t(e - (s + p)));
+    p = size_t(e - s) + 1;
+    if (!line.empty() && line.back() == '\r') line.remove_suffix(1);
+    if (line.empty()) break;  // end of head
+    const void* c = memchr(line.data(), ':', line.size());
+    if (!c) continue;
+    const size_t colon = size_t(static_cast<const char*>(c) - line.data());
+    std::string_view k = line.substr(0, colon), v = line.substr(colon + 1);
+    while (!v.empty() && (v.front() == ' ' || v.front() == '\t')) v.remove_prefix(1);
+    switch (k.size()) {
+      case 14:
+        if (field_is(k, "content-length")) {
+          cl = 0;
+          for (char d : v) {
+            if (d < '0' || d > '9') break;
+            cl = cl * 10 + (d - '0');
+            if (cl > (1 << 20)) break;  // over the body cap: rejected below
+          }
         }
-      }
-      else if (http::iequals(k, "transfer-encoding") && v.find("chunked") != std::string_view::npos) chunked = true;
-      else if (http::iequals(k, "connection")) {
-        if (http::iequals(v, "close")) *close = true;
-        else if (http::iequals(v, "keep-alive")) *close = false;
-      } else if (http::iequals(k, "retry-after")) {
-        r->has_retry_after = parse_retry_after(v, wall_us() / 1000, &r->retry_after_ms);
-      }
+        break;
+      case 17:
+        if (field_is(k, "transfer-encoding") && v.find("chunked") != std::string_view::npos) chunked = true;
+        break;
+      case 10:
+        if (field_is(k, "connection")) {
+          if (http::iequals(v, "close")) conn_close = true;
+          else if (http::iequals(v, "keep-alive")) conn_close = false;
+        }
+        break;
+      case 11:
+        if (field_is(k, "retry-after")) has_retry_after = parse_retry_after(v, wall_us() / 1000, &retry_after_ms);
+        break;
+      default:
+        break;
     }
-    p = n;
   }
-  size_t body = he + 4;
+  r->reason.assign(head.size() > 13 && head[12] == ' ' ? head.substr(13) : std::string_view());
+  r->has_retry_after = has_retry_after;
+  r->retry_after_ms = retry_after_ms;
+  *close = conn_close;
+  size_t body = p;
   *head_ok = true;
   if (status == 204 || status == 304 || (status >= 100 && status < 200)) {
     r->status = status;
