@@ -507,14 +507,14 @@ std::string ClientPool::build_request(const std::string& path, const std::string
 void ClientPool::build_request_into(std::string* out, const std::string& path, const std::string& extra) const {
   // Into a connection's own buffer: a kept-alive connection reuses its capacity, so the
   // request costs no allocation.
+  if (path != head_path_ || head_.empty()) {
+    head_path_ = path;
+    head_ = "GET " + path + " HTTP/1.1\r\nHost: " + host_header_ + "\r\nAccept: application/json\r\nConnection: keep-alive\r\n";
+  }
   std::string& r = *out;
   r.clear();
-  r.reserve(128 + extra.size());
-  r += "GET ";
-  r += path;
-  r += " HTTP/1.1\r\nHost: ";
-  r += host_header_;
-  r += "\r\nAccept: application/json\r\nConnection: keep-alive\r\n";
+  r.reserve(head_.size() + extra.size() + 2);
+  r += head_;
   r += extra;
   r += "\r\n";
 }

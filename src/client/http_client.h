@@ -158,6 +158,9 @@ class ClientPool {
   uint64_t next_id_ = 1;
   uint64_t opened_ = 0;
   std::string host_header_;
+  // "GET <path> HTTP/1.1\r\nHost: ...\r\n...keep-alive\r\n" for the last path asked for (the
+  // aloha call always asks for the same one): a request is then three appends, not seven.
+  mutable std::string head_path_, head_;
   std::atomic<uint64_t>* transport_retries_;
   int connect_timeout_ms_ = 0;
   const std::atomic<int>* read_timeout_ms_ = nullptr;
