@@ -937,3 +937,28 @@ def test_pipelined_calls_behind_a_slow_answer_are_not_held_to_their_timeouts(hol
     ev = _events(s)
     assert ev.get("TIMEOUT") == 1 and ev.get("SUCCESS") == 3, ev
     assert _retries(s).get("transport", 0) == 3  # each queued call went out once more
+
+
+def test_a_call_parked_across_a_reload_answers_with_its_own_greeting(hola, aloha, tmp_path):
+    """The greeting is computed when the request arrives (HolaResource.java:75): a chaining
+    call still waiting on aloha while the greeting file changes answers with the greeting of
+    its own request, and the next request gets the new one. (The worker keeps the contents of
+    the last configuration generations for such calls; the call holds a plain pointer.)"""
+    conf = tmp_path / "t.properties"
+    conf.write_text("hello=old %s\n")
+    aloha.set_mode("slow_once", delay_s=2.0)
+    s = hola(args=[f"-Dconf={conf}", "--aloha-url", aloha.url, "--no-tracing", "--feign-log", "none",
+                   "--config-poll-ms", "100", "-Dhystrix.command.default.execution.isolation.thread.timeoutInMilliseconds=5000"],
+             env={"HOSTNAME": "h"}, threads=1)
+    parked = {}
+    t = threading.Thread(target=lambda: parked.update(r=chain(s)), daemon=True)
+    t.start()
+    time.sleep(0.3)  # the call is parked on aloha now
+    conf.write_text("hello=new %s\n")
+    deadline = time.monotonic() + 5
+    while s.get("/api/hola")[2] != b"new h" and time.monotonic() < deadline:
+        time.sleep(0.05)
+    assert s.get("/api/hola")[2] == b"new h"
+    t.join(timeout=10)
+    assert parked["r"] == ["old h", "Aloha mai aloha-1", "Bonjour de bonjour-1"], parked
+    assert chain(s) == ["new h", "Aloha mai aloha-1", "Bonjour de bonjour-1"]
