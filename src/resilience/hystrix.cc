@@ -1,5 +1,7 @@
 #include "resilience/hystrix.h"
 
+#include <sched.h>
+
 #include <algorithm>
 #include <cstdlib>
 
@@ -233,8 +235,14 @@ int64_t RollingPercentile::mean(int64_t now) {
 class ShardLock {
  public:
   void lock() {
-    while (locked_.exchange(true, std::memory_order_acquire))
-      while (locked_.load(std::memory_order_relaxed)) __builtin_ia32_pause();
+    while (locked_.exchange(true, std::memory_order_acquire)) {
+      // a holder that was descheduled mid-section (another tenant on its CPU): stop spinning
+      // after a while and let it run
+      for (int spins = 0; locked_.load(std::memory_order_relaxed); ++spins) {
+        if (spins < 1024) __builtin_ia32_pause();
+        else sched_yield();
+      }
+    }
   }
   void unlock() { locked_.store(false, std::memory_order_release); }
 
