@@ -641,6 +641,7 @@ def test_exit_deadline_ends_a_termination_that_runs_too_long(hola):
     import signal
 
     s = hola(args=["--shutdown-delay-ms", "30000", "--exit-deadline-ms", "1000"])
+    s.expected_rc = 3
     t0 = time.monotonic()
     s.proc.send_signal(signal.SIGTERM)
     assert s.proc.wait(timeout=10) == 3
@@ -656,6 +657,7 @@ def test_a_stuck_worker_cannot_hold_the_termination_forever(hola):
     import signal
 
     s = hola(args=["--drain-ms", "300", "--exit-deadline-ms", "3000"], threads=2)
+    s.expected_rc = 3
     libc = ctypes.CDLL(None, use_errno=True)
     libc.ptrace.argtypes = [ctypes.c_long, ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p]
     PTRACE_SEIZE, PTRACE_INTERRUPT, WALL = 0x4206, 0x4207, 0x40000000
@@ -829,6 +831,7 @@ def test_exit_watchdog_reports_where_every_worker_is(hola):
     import subprocess
 
     s = hola(args=["--shutdown-delay-ms", "5000", "--exit-deadline-ms", "1000"], threads=2)
+    s.expected_rc = 3
     s.get("/api/hola")  # one request: worker 0 or 1 has run a connection handler
     s.proc.send_signal(signal.SIGTERM)
     assert s.proc.wait(timeout=10) == 3
