@@ -841,8 +841,13 @@ def test_exit_watchdog_reports_where_every_worker_is(hola):
     reports = re.findall(r"hola: worker (\d): pass (\d+), phase (\w+), .*?; stack((?: #\d+ \S+)+)", log)
     assert {r[0] for r in reports} == {"0", "1"}, log[-3000:]
     exe = str(s.exe)
+    # Under TSan, epoll_wait and sigtimedwait are intercepted by libtsan, whose frames keep no
+    # frame pointer: the walk ends there (test_sanitizers.py checks that report on its own).
+    walks_through = os.environ.get("HOLA_SANITIZER") != "tsan"
     for worker, passes, phase, stack in reports:
         assert phase == "wait" and int(passes) >= 1, (worker, phase)
+        if not walks_through:
+            continue
         frames = re.findall(r"#\d+ (\S+)\+0x([0-9a-f]+)", stack)
         own = [off for obj, off in frames if obj == Path(exe).name]
         assert own, stack
@@ -854,6 +859,8 @@ def test_exit_watchdog_reports_where_every_worker_is(hola):
     # and main says which termination step it is in, with its own stack
     m = re.search(r"hola: main: shutdown delay; stack((?: #\d+ \S+)+)", log)
     assert m, log[-3000:]
+    if not walks_through:
+        return
     own = [off for obj, off in re.findall(r"#\d+ (\S+)\+0x([0-9a-f]+)", m.group(1)) if obj == Path(exe).name]
     names = subprocess.run(["addr2line", "-f", "-C", "-e", exe, *[f"0x{o}" for o in own]],
                            capture_output=True, text=True).stdout
