@@ -9,20 +9,23 @@ One rank per "GPU slot" of the node = one hola replica. Every rank:
     node (client-side round-robin, BASELINE.json config 4: "512 connections against 8
     replicas behind round-robin"; N=1 is config 3: 64 connections, 1 replica), each
     load-generator thread on the L3 (or SMT sibling core) of the replicas it drives.
-A step = connections x `--reqs-per-conn` requests per replica, drawn by the connections from
-a shared budget (weak scaling: the work per replica is fixed). W warmup steps, then exactly
-K timed steps between barriers; the elapsed time is the MAX over ranks, `value` is the
-node-wide total req/s, and p50/p99 come from the merged latency histograms of all ranks.
-Every response body in the timed region is compared with the greeting of the replica behind
-its connection (a mismatch is an error). After the timed region rank 0 runs BASELINE config
-2 (one connection, 30 s) and reports it as c1_* keys with the host load of that run, then the
-as-deployed replica (the image's exact ENTRYPOINT + the manifests' args and env:
-`--shutdown-delay-ms 5000 --busy-poll-us auto`; deployed_* keys), then the chaining endpoint
-(load generator -> hola A -> hola B as aloha; chain_* keys); the JSON also carries span
-accounting
-(`tracing`, with a native collector under --zipkin-sink), connection placement (`locality`)
-and how busy the replicas' cores and their idle SMT siblings were (`host_load`: other
-tenants on the siblings are what moves the number between runs on a shared host).
+A step = connections x R requests per replica, drawn by the connections from a shared budget
+(weak scaling: the work per replica is fixed); R is sized from the last warmup step so that the
+driver's 20 steps time the 30 s of BASELINE configs 3/4 (or fixed with --reqs-per-conn). W
+warmup steps, then exactly K timed steps between barriers; the elapsed time is the MAX over
+ranks, `value` is the node-wide total req/s, and p50/p99 come from the merged latency
+histograms of all ranks. Every response body in the timed region is compared with the
+greeting of the replica behind its connection (a mismatch is an error).
+
+After the timed region rank 0 runs BASELINE config 2 (one connection, 30 s; c1_* keys), and at
+N = 1 the per-node sub-runs of hola_amd/parallel/subruns.py: the as-deployed replica (the
+image's ENTRYPOINT + the manifests' args and env; deployed_*), GET /api/hola-chaining
+engineered (chain_*) and as shipped (pool of 10, Feign BASIC logging; chain_shipped_*), and
+the headline in the other SMT layout (alt_*: BENCH and SCALE's N = 1 each carry the other's
+figure). The JSON also carries span accounting (`tracing`, with a native collector under
+--zipkin-sink), connection placement (`locality`) and how busy the replicas' cores and the
+SMT siblings outside the job were (`host_load`: other tenants on the siblings are what moves
+the number between runs on a shared host).
 
   python bench.py --gpus N --steps K --warmup W
 """
@@ -39,13 +42,14 @@ sys.path.insert(0, str(Path(__file__).resolve().parent))
 
 from hola_amd.native import ensure_built  # noqa: E402
 from hola_amd.parallel.hostmetrics import (  # noqa: E402
-    MetricsProbe, accept_locality, busy_fraction, cgroup_cpu_stat, cpu_times, proc_cpu_s, sink_stats, span_counters,
+    MetricsProbe, accept_locality, cgroup_cpu_stat, cpu_times, proc_cpu_s, sink_stats, span_counters,
     start_zipkin_sink, tcp_counters, thread_cpu_s)
+from hola_amd.parallel import subruns  # noqa: E402
 from hola_amd.parallel.loadgen import ControlledLoadgen, decode_hist, merge_hists, percentile  # noqa: E402
 from hola_amd.server import HolaProcess  # noqa: E402
 from hola_amd.utils.cpu import (  # noqa: E402
-    cgroup_cpu_quota, connection_targets, cpu_budget, format_cpu_list, plan_replicas_with_loadgen, siblings,
-    slot_cores, smt_fits)
+    cgroup_cpu_quota, connection_targets, cpu_budget, format_cpu_list, plan_replicas_with_loadgen, plan_slot_subset,
+    siblings, slot_cores, smt_fits)
 
 METRIC = "HTTP req/sec + p50/p99 latency, GET /api/hola at 1/2/4/8 replicas"
 BASELINE_VALUE = None  # the reference publishes no numbers
@@ -54,12 +58,19 @@ BASELINE_VALUE = None  # the reference publishes no numbers
 def parse_args():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1, help="replicas on this node (one per rank)")
-    # A step is sized so that the driver's `--steps 20` times ~30 s at ~4.1 M req/s, the length
-    # of BASELINE configs 3/4 (30 s wrk runs): 20 x 64 x 96,000 requests.
+    # BASELINE configs 3/4 are 30 s wrk runs: the driver's `--steps 20` is sized to time ~30 s.
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--connections", type=int, default=64, help="keep-alive connections per replica")
-    ap.add_argument("--reqs-per-conn", type=int, default=96000, help="requests per connection per step")
+    ap.add_argument("--reqs-per-conn", type=int, default=0,
+                    help="requests per connection per step; 0 = sized from the last warmup step so that a "
+                         "step lasts --step-seconds (every rank takes the smallest size any rank computed, "
+                         "so each replica does the same work; `requests` stays exact)")
+    ap.add_argument("--step-seconds", type=float, default=1.5,
+                    help="target length of one timed step with --reqs-per-conn 0 (20 x 1.5 s = the 30 s of "
+                         "BASELINE configs 3/4)")
+    ap.add_argument("--warmup-reqs-per-conn", type=int, default=96000,
+                    help="requests per connection of each warmup step with --reqs-per-conn 0")
     ap.add_argument("--cores", type=int, default=0,
                     help="physical host cores per replica (server + load generator); 0 = one GPU "
                          "slot's share of the node: min(CPU budget, physical cores) / GPUs on the node "
@@ -121,16 +132,31 @@ def parse_args():
     ap.add_argument("--c1-reqs", type=int, default=0,
                     help="config-2 request count instead of --c1-seconds (0 = sized from a warm-up "
                          "run to last --c1-seconds)")
-    ap.add_argument("--deployed-seconds", type=float, default=3.0,
+    ap.add_argument("--deployed-seconds", type=float, default=10.0,
                     help="after the timed region, rank 0 also drives a replica started exactly as the image "
                          "and manifests start it (deploy/Dockerfile ENTRYPOINT + deploy/openshift args and "
                          "env) on its server CPUs, with the same load generator, for about "
-                         "this long; reported as deployed_*. 0 = skip. `value` is untouched")
-    ap.add_argument("--chain-seconds", type=float, default=5.0,
+                         "this long; reported as deployed_* with its own host load. 0 = skip. `value` is "
+                         "untouched. N = 1 only (a per-node figure)")
+    ap.add_argument("--deployed-zipkin", choices=("deployed", "unset", "sink"), default="deployed",
+                    help="the deployed sub-run's ZIPKIN_SERVER_URL: as the manifests set it (the cluster's "
+                         "zipkin-query, unresolvable on a bare host), unset, or a native discard collector")
+    ap.add_argument("--chain-seconds", type=float, default=10.0,
                     help="after the timed region, rank 0 also measures GET /api/hola-chaining: load generator "
                          "-> hola A -> hola B (B answering as aloha), 64 connections, about this long, on "
                          "the rank's CPUs; reported as chain_* (rps, latency, A's CPU per request, Hystrix "
-                         "events: fallbacks must be 0). 0 = skip. `value` is untouched")
+                         "events: fallbacks must be 0; host load, accept locality of both hops, busy-poll "
+                         "counters of both replicas). 0 = skip. `value` is untouched. N = 1 only")
+    ap.add_argument("--chain-shipped-seconds", type=float, default=10.0,
+                    help="then the same chain with hola A started exactly as the manifests start it (pool of "
+                         "10, Feign BASIC logging, ZIPKIN_SERVER_URL set): chain_shipped_* (rps, latency, "
+                         "fallback fraction, Hystrix SUCCESS count). 0 = skip. N = 1 only")
+    ap.add_argument("--chain-loadgen-busy-poll", type=int, default=0,
+                    help="the chain sub-runs' load generator busy-poll window in us (0 = sleep in epoll_wait)")
+    ap.add_argument("--alt-seconds", type=float, default=10.0,
+                    help="N = 1 only: the headline replica again in the other SMT layout for about this long "
+                         "(alt_* keys): pair on a 1-GPU box, off on an 8-GPU node, so BENCH and SCALE's N = 1 "
+                         "each carry a figure in the other's layout. 0 = skip")
     ap.add_argument("--chain-pool", type=int, default=128,
                     help="hola A's Hystrix thread-pool (bulkhead) size in the chain sub-run: the reference's "
                          "10 would turn most of 64 concurrent calls into fallbacks (SURVEY.md D2)")
@@ -145,7 +171,15 @@ def parse_args():
                          "(the 1-GPU box is a 16-CPU quota over a 256-CPU host: with --gpu-slots 8 this "
                          "plans the unconstrained 8-GPU node's layout on its real topology)")
     ap.add_argument("--plan-only", action="store_true",
-                    help="print the core plan of every slot of the node (one JSON line) and exit")
+                    help="print the core plan (one JSON line) and exit: of every slot of the node, or of "
+                         "--replicas N replicas as an N-rank run would plan them")
+    ap.add_argument("--replicas", type=int, default=0,
+                    help="with --plan-only: plan this many replicas (ranks) on the node (0 = one per slot)")
+    ap.add_argument("--slot-cores", type=int, default=0,
+                    help="miniature node layout: rank r runs on only the first K physical cores of node slot "
+                         "r (slots placed as the --gpu-slots node plan places them, across both sockets); "
+                         "with --smt pair (the default here) each core carries a server worker and, on its "
+                         "sibling, the load-generator thread driving it. 0 = off")
     ap.add_argument("--busy-poll-us", type=int, default=20,
                     help="spin this long in epoll before sleeping (the load generator; the replica spins "
                          "adaptively up to this long); 20 us measured best on the box "
@@ -187,21 +221,14 @@ def main() -> int:
     if rank == 0 and a.zipkin_sink and not a.no_tracing:
         sink = start_zipkin_sink()
     if rank == 0:
-        slots = max(local_world, a.gpu_slots or _gpu_slots())
-        cores = a.cores or slot_cores(slots)
-        per_rank = min(cores, max(1, cpu_budget() // local_world))
         host = a.host if a.host != "auto" else ("::1" if _can_bind("::1") else "127.0.0.1")
-        smt = a.smt
-        if smt == "auto":
-            smt = "pair" if smt_fits(slots, per_rank) else "off"
-        plan = [{"cores": plan_replicas_with_loadgen(local_world, per_rank, a.server_threads,
-                                                     avoid_busy=not a.no_avoid_busy, smt=smt),
-                 "smt": smt, "gpu_slots": slots,
+        plan = [{**_plan(a, local_world, avoid_busy=not a.no_avoid_busy),
                  "host": host,
-                 "base_port": _free_port_block(a.base_port, local_world, host),
+                 "base_port": subruns.free_port_block(a.base_port, local_world, host),
                  "sink_port": sink[1] if sink else 0}]
         # the rank's own load-generator cores, for --plain-dealing (the r42 layout)
-        plan[0]["own_loadgen"] = _own_loadgen(plan[0]["cores"])
+        plan[0]["own_loadgen"] = (_own_loadgen(plan[0]["cores"]) if not a.slot_cores
+                                  else [p["loadgen"] for p in plan[0]["cores"]])
     if dist:
         dist.broadcast_object_list(plan, src=0)
     server_cpus, load_cpus = plan[0]["cores"][local_rank]["server"], plan[0]["cores"][local_rank]["loadgen"]
@@ -214,6 +241,9 @@ def main() -> int:
         load_cpus = plan[0]["own_loadgen"][local_rank]
     s_threads = len(server_cpus)
     smt = plan[0]["smt"]
+    # every CPU this job planned (all ranks' servers and load generators): a busy SMT sibling
+    # outside this set is another tenant's
+    job_cpus = sorted({c for p in plan[0]["cores"] for c in p["server"] + p["loadgen"]})
     if a.busy_poll_pause < 0:
         a.busy_poll_pause = 16 if smt == "pair" else 0
     base_port = plan[0]["base_port"]
@@ -267,9 +297,22 @@ def main() -> int:
                                     expect_bodies=bodies, verify_body=bodies is None, conn_targets=conn_targets,
                                     cpu_profile=os.path.join(os.path.abspath(a.cpu_profile_dir),
                                                              f"loadgen_cpu_rank{rank}.prof") if a.cpu_profile_dir else None)
+        per_conn = a.reqs_per_conn or a.warmup_reqs_per_conn
+        w = None
         for _ in range(a.warmup):
-            loadgen.run(a.reqs_per_conn)
+            w = loadgen.run(per_conn)
         loadgen.reset()
+        if not a.reqs_per_conn:
+            # size the timed steps from the last warmup step: each step lasts about
+            # --step-seconds; every rank takes the smallest size (the same work per replica)
+            per_conn = 108000
+            if w and w["elapsed_ns"] > 0:
+                rate = w["requests"] / (w["elapsed_ns"] / 1e9)
+                per_conn = max(100, int(rate * a.step_seconds / a.connections))
+            if dist:
+                sizes = [None] * world
+                dist.all_gather_object(sizes, per_conn)
+                per_conn = min(sizes)
 
         cuda = _cuda_sync_fn(local_rank)
         if dist:
@@ -285,7 +328,7 @@ def main() -> int:
         t0 = time.perf_counter()
         reqs = errs = 0
         for _ in range(a.steps):
-            r = loadgen.run(a.reqs_per_conn)
+            r = loadgen.run(per_conn)
             reqs += r["requests"]
             errs += r["errors"]
         if dist:
@@ -302,10 +345,10 @@ def main() -> int:
         thr1 = cgroup_cpu_stat()
         times1 = cpu_times()
         own = set(server_cpus) | set(load_cpus)
-        sibs = {x for c in own for x in siblings(c)} - own
         st = loadgen.stats()
         mem = server.memory_kb()
-        c1 = _config2_subrun(a, host, port, server_cpus, load_cpus, bodies and [bodies[local_rank]]) if local_rank == 0 else None
+        c1 = subruns.config2(a, host, port, server_cpus, load_cpus, bodies and [bodies[local_rank]],
+                             job_cpus) if local_rank == 0 else None
 
         local = {"elapsed": elapsed, "requests": reqs, "errors": errs, "hist": st.get("hist", ""),
                  "non2xx": st.get("non2xx", 0), "body_checked": st.get("body_checked", 0),
@@ -320,10 +363,10 @@ def main() -> int:
                  "startup_ms": server.startup_ms, "rss_peak_kb": mem.get("VmHWM", 0),
                  "tcp": {k: tcp1[k] - tcp0[k] for k in tcp1 if k in tcp0},
                  "cgroup": {k: thr1[k] - thr0[k] for k in thr1 if k in thr0},
-                 # host-wide busy share over the timed region of this rank's CPUs and of their
-                 # SMT siblings that it leaves idle (busy there = another tenant sharing our cores)
-                 "host_load": {"own": busy_fraction(times0, times1, own),
-                               "siblings": busy_fraction(times0, times1, sibs)}}
+                 "per_conn": per_conn,
+                 # host-wide busy share over the timed region of this rank's CPUs and of those of
+                 # their SMT siblings that no part of this job uses (busy there = another tenant)
+                 "host_load": subruns.host_load(times0, times1, own, job_cpus)}
         if dist:
             gathered = [None] * world
             dist.all_gather_object(gathered, local)
@@ -334,26 +377,30 @@ def main() -> int:
         if loadgen:
             loadgen.close()
         server.stop()
-    # The as-deployed replica, then the chaining path, on the same CPUs once the headline
-    # replica is gone (rank 0).
-    deployed = chain = None
-    if local_rank == 0 and a.deployed_seconds > 0:
-        try:
-            deployed = _deployed_subrun(a, server_cpus, load_cpus)
-        except Exception as e:  # noqa: BLE001 - reported in the JSON; the other ranks must not hang
-            deployed = {"error": f"{type(e).__name__}: {e}"}
-    if local_rank == 0 and a.chain_seconds > 0:
-        try:
-            chain = _chain_subrun(a, list(server_cpus) + list(load_cpus))
-        except Exception as e:  # noqa: BLE001 - as above
-            chain = {"error": f"{type(e).__name__}: {e}"}
-    if dist:
-        both = [None] * world
-        dist.all_gather_object(both, (deployed, chain))
-        deployed, chain = both[0]
-        if sink:
-            sink[0].terminate()
-            sink[0].wait(timeout=10)
+    # Per-node sub-runs at N = 1 (BENCH and SCALE's first point), on the rank's CPUs once the
+    # headline replica is gone: the as-deployed replica, the chaining path engineered and as
+    # shipped, and the headline in the other SMT layout. Each is reported in the JSON (an
+    # exception included) without touching `value`.
+    subs: dict[str, dict | None] = {}
+    if world == 1:
+        rank_cpus = list(server_cpus) + list(load_cpus)
+        for key, secs, fn in (
+                ("deployed", a.deployed_seconds,
+                 lambda: subruns.deployed(a, server_cpus, load_cpus, job_cpus, zipkin=a.deployed_zipkin)),
+                ("chain", a.chain_seconds, lambda: subruns.chain(a, rank_cpus, job_cpus)),
+                ("chain_shipped", a.chain_shipped_seconds,
+                 lambda: subruns.chain(a, rank_cpus, job_cpus, shipped=True, seconds=a.chain_shipped_seconds)),
+                ("alt", a.alt_seconds,
+                 lambda: subruns.alt_layout(a, host, server_cpus, load_cpus, smt, job_cpus,
+                                            bodies and [bodies[0]], a.alt_seconds))):
+            if secs > 0:
+                try:
+                    subs[key] = fn()
+                except Exception as e:  # noqa: BLE001 - reported in the JSON
+                    subs[key] = {"error": f"{type(e).__name__}: {e}"}
+    if dist and sink:
+        sink[0].terminate()
+        sink[0].wait(timeout=10)
 
     if rank == 0:
         t = max(g["elapsed"] for g in gathered)
@@ -403,11 +450,15 @@ def main() -> int:
             "body_mismatch": sum(g["body_mismatch"] for g in gathered),
             # BASELINE config 2 (1 connection, 1 replica), measured after the timed region
             **_c1_keys(gathered[0]["c1"]),
-            # the replica as the image and manifests run it (--shutdown-delay-ms 5000
-            # --busy-poll-us auto), same load generator
-            **_deployed_keys(deployed),
-            # GET /api/hola-chaining through two replicas (the endpoint with real work behind it)
-            **_chain_keys(chain),
+            # N = 1 only: the replica as the image and manifests run it (--shutdown-delay-ms 5000
+            # --busy-poll-us auto, ZIPKIN_SERVER_URL set), same load generator
+            **_deployed_keys(subs.get("deployed")),
+            # N = 1 only: GET /api/hola-chaining through two replicas (the endpoint with real work
+            # behind it), engineered (pool 128, logging off) and as shipped (pool 10, BASIC logging)
+            **_chain_keys(subs.get("chain"), "chain"),
+            **_chain_keys(subs.get("chain_shipped"), "chain_shipped"),
+            # N = 1 only: the headline in the other SMT layout (BENCH <-> SCALE N = 1 comparison)
+            **_alt_keys(subs.get("alt")),
             # span accounting over the timed region, all replicas (per second)
             "tracing": _tracing_block(a, gathered, t, plan[0]["sink_port"]),
             # client thread vs. serving worker placement of every accepted connection
@@ -428,12 +479,17 @@ def main() -> int:
                 "seq_len": 1,
                 "parallelism": f"replicas{world}",
                 "connections_per_replica": a.connections,
-                "reqs_per_conn_per_step": a.reqs_per_conn,
+                "reqs_per_conn_per_step": gathered[0]["per_conn"],
+                "step_sizing": (f"sized from the last warmup step to ~{a.step_seconds:g} s per step" if not a.reqs_per_conn
+                                else "fixed (--reqs-per-conn)"),
                 "pipeline": a.pipeline,
                 "lb": "client-side " + ("round-robin over all replicas from the rank's own cores" if a.plain_dealing
                                         else plan[0]["cores"][local_rank].get("dealing", "round-robin")),
                 "loopback": host,
-                "cores_per_replica": len({min(siblings(c)) for c in list(server_cpus) + list(load_cpus)}),
+                # physical cores under the replica's server workers (with smt=pair the load
+                # generator runs on their siblings; with smt=off on as many separate cores)
+                "cores_per_replica": _phys_count(server_cpus),
+                "physical_cores_per_slot": plan[0]["cores_per_slot"] if not a.slot_cores else a.slot_cores,
                 "server_threads_per_replica": s_threads,
                 "loadgen_threads_per_replica": len(load_cpus),
                 "busy_poll_us": a.busy_poll_us,
@@ -441,7 +497,7 @@ def main() -> int:
                 "busy_poll_pause": a.busy_poll_pause,
                 "epoll": "level" if a.epoll_lt else "edge",
                 "smt": smt,
-                "layout_note": _layout_note(plan[0]["gpu_slots"], smt, server_cpus, load_cpus),
+                "layout_note": _layout_note(plan[0]["gpu_slots"], smt, server_cpus, load_cpus, a.slot_cores),
                 "gpu_slots_on_node": plan[0]["gpu_slots"],
                 "cpus_per_replica": len(set(server_cpus) | set(load_cpus)),
                 "step_budget": "per-connection" if a.per_conn_quota else "shared",
@@ -459,28 +515,56 @@ def main() -> int:
     return 0
 
 
-def _plan_only(a) -> int:
-    """The core plan of a whole node (one replica per GPU slot), as rank 0 computes it, without
-    starting anything: the cpu map an N = slots run would use."""
-    from hola_amd.utils.cpu import l3_domain, package_of, physical_cores
+def _plan(a, n: int, avoid_busy: bool = True) -> dict:
+    """Core plan of `n` co-located replicas (one per rank) on this node, as rank 0 computes it.
 
-    slots = a.gpu_slots or max(1, _gpu_slots())
-    cores = a.cores or slot_cores(slots)
-    per_rank = min(cores, max(1, cpu_budget() // slots))
+    Each replica gets one GPU slot's share of the node: slot_cores(slots) physical cores
+    (16 on the 16-CPU box and on a 2 x 64-core 8-GPU node), the SMT layout decided per node
+    (pair when the node's CPU budget holds both threads of every slot's cores), so every N
+    runs each replica on the same resources (weak scaling). With --slot-cores K each replica
+    gets only the first K cores of its node slot (plan_slot_subset)."""
+    slots = max(n, a.gpu_slots or _gpu_slots())
+    if a.slot_cores:
+        smt = "off" if a.smt == "off" else "pair"
+        cores = [{"server": p["server"], "loadgen": p["loadgen"], "thread_targets": [[r]] * len(p["loadgen"]),
+                  "dealing": "round-robin over the replicas: each client thread drives the replica whose worker "
+                             "shares its physical core (the node plan's per-connection placement)" if smt == "pair"
+                             else "each client thread drives the replica in its own node slot"}
+                 for r, p in enumerate(plan_slot_subset(n, slots, a.slot_cores, smt))]
+        return {"cores": cores, "smt": smt, "gpu_slots": slots, "cores_per_slot": a.slot_cores}
+    per_rank = min(a.cores or slot_cores(slots), max(1, cpu_budget() // n))
     smt = a.smt
     if smt == "auto":
         smt = "pair" if smt_fits(slots, per_rank) else "off"
-    plan = plan_replicas_with_loadgen(slots, per_rank, a.server_threads, avoid_busy=False, smt=smt)
-    print(json.dumps({"gpu_slots": slots, "cores_per_slot": per_rank, "smt": smt, "cpu_budget": cpu_budget(),
+    return {"cores": plan_replicas_with_loadgen(n, per_rank, a.server_threads, avoid_busy=avoid_busy, smt=smt),
+            "smt": smt, "gpu_slots": slots, "cores_per_slot": per_rank}
+
+
+def _plan_only(a) -> int:
+    """The core plan of a whole node (one replica per GPU slot), or of --replicas N replicas,
+    as rank 0 computes it, without starting anything: the cpu map such a run would use."""
+    from hola_amd.utils.cpu import l3_domain, package_of, physical_cores
+
+    slots = a.gpu_slots or max(1, _gpu_slots())
+    n = a.replicas or slots
+    p = _plan(a, n, avoid_busy=False)
+    print(json.dumps({"gpu_slots": p["gpu_slots"], "replicas": n, "cores_per_slot": p["cores_per_slot"],
+                      "smt": p["smt"], "cpu_budget": cpu_budget(),
                       "cgroup_quota": cgroup_cpu_quota(), "physical_cores": len(physical_cores()),
-                      "ranks": [{"server": p["server"], "loadgen": p["loadgen"], "thread_targets": p["thread_targets"],
-                                 "dealing": p["dealing"],
-                                 "server_sockets": sorted({package_of(c) for c in p["server"]}),
-                                 "server_l3": sorted({l3_domain(c) for c in p["server"]}),
-                                 "loadgen_sockets": sorted({package_of(c) for c in p["loadgen"]}),
-                                 "siblings": {str(c): siblings(c) for c in p["server"] + p["loadgen"]}}
-                                for p in plan]}), flush=True)
+                      "ranks": [{"server": r["server"], "loadgen": r["loadgen"], "thread_targets": r["thread_targets"],
+                                 "dealing": r["dealing"],
+                                 "server_physical_cores": _phys_count(r["server"]),
+                                 "server_sockets": sorted({package_of(c) for c in r["server"]}),
+                                 "server_l3": sorted({l3_domain(c) for c in r["server"]}),
+                                 "loadgen_sockets": sorted({package_of(c) for c in r["loadgen"]}),
+                                 "siblings": {str(c): siblings(c) for c in r["server"] + r["loadgen"]}}
+                                for r in p["cores"]]}), flush=True)
     return 0
+
+
+def _phys_count(cpus) -> int:
+    """Physical cores under a CPU list (SMT siblings counted once)."""
+    return len({min(siblings(c)) for c in cpus})
 
 
 def _own_loadgen(cores: list[dict]) -> list[list[int]]:
@@ -545,185 +629,68 @@ def _expected_bodies(path: str, ranks: list[int]) -> list[str] | None:
     return None
 
 
-def _config2_subrun(a, host: str, port: int, server_cpus, load_cpus, bodies) -> dict | None:
-    """BASELINE config 2: one keep-alive connection against this rank's replica, run after
-    the timed region (so the headline is unaffected)."""
-    if a.c1_reqs <= 0 and a.c1_seconds <= 0:
-        return None
-    lg = ControlledLoadgen([(host, port)], 1, 1, cpu_list=str(load_cpus[0]), path=a.path,
-                           busy_poll_us=a.busy_poll_us, busy_poll_pause=a.busy_poll_pause, epoll_lt=a.epoll_lt,
-                           expect_bodies=bodies, verify_body=bodies is None)
-    try:
-        warm = lg.run(max(1000, a.c1_reqs // 10) if a.c1_reqs > 0 else 50000)
-        n = a.c1_reqs
-        if n <= 0:  # size the run from the warm-up rate: about --c1-seconds, within bounds
-            rate = warm["requests"] / max(1e-9, warm["elapsed_ns"] / 1e9)
-            n = int(min(30_000_000, max(20_000, rate * a.c1_seconds)))
-        lg.reset()
-        own = set(server_cpus) | {load_cpus[0]}
-        sibs = {x for c in own for x in siblings(c)} - own
-        t0 = cpu_times()
-        r = lg.run(n)
-        t1 = cpu_times()
-        st = lg.stats()
-    finally:
-        lg.close()
-    el = r["elapsed_ns"] / 1e9
-    return {"rps": r["requests"] / el if el > 0 else 0.0, "requests": r["requests"], "elapsed_s": el,
-            "p50_ns": st["p50_ns"], "p99_ns": st["p99_ns"], "errors": r["errors"],
-            "body_checked": st.get("body_checked", 0), "client_cpu": load_cpus[0],
-            # as for the headline: busy share of the replica's + client's CPUs and of their idle
-            # SMT siblings over this run (another tenant on a sibling slows the one connection)
-            "host_load": {"own": busy_fraction(t0, t1, own), "siblings": busy_fraction(t0, t1, sibs)}}
-
-
-def _layout_note(slots: int, smt: str, server_cpus, load_cpus) -> str:
+def _layout_note(slots: int, smt: str, server_cpus, load_cpus, slot_cores_k: int = 0) -> str:
     """One line that tells a SCALE_rNN.json reader why its N=1 point differs from BENCH."""
-    phys = len({min(siblings(c)) for c in list(server_cpus) + list(load_cpus)})
-    how = ("each physical core runs a server worker on one SMT thread and its load-generator "
-           "thread on the other (--smt pair)" if smt == "pair" else
-           "server workers and load-generator threads on separate physical cores, SMT siblings idle")
-    return (f"{slots} GPU slot(s) on this node: each replica's share is {phys} physical cores "
-            f"({len(set(server_cpus) | set(load_cpus))} CPUs); {how}. The 1-GPU box (16-CPU quota) runs "
-            f"smt=off and an unconstrained 8-GPU node smt=pair, so BENCH and SCALE's N=1 differ by layout, "
-            f"not by code; compare config.smt before reading a difference as a regression.")
+    srv = _phys_count(server_cpus)
+    if smt == "pair":
+        how = (f"{srv} physical cores, each running a server worker on one SMT thread and the "
+               f"load-generator thread that drives it on the other (--smt pair)")
+    else:
+        how = (f"{srv} physical cores of server workers and {_phys_count(load_cpus)} more of load-generator "
+               f"threads, SMT siblings idle (--smt off)")
+    mini = (f" Miniature layout (--slot-cores {slot_cores_k}): only the first {slot_cores_k} core(s) of each "
+            f"node slot are used; this is not the 8-GPU node's curve." if slot_cores_k else "")
+    return (f"{slots} GPU slot(s) on this node; each replica runs on {how}.{mini} The 1-GPU box (16-CPU quota) "
+            f"runs smt=off and an unconstrained 8-GPU node smt=pair, so BENCH and SCALE's N=1 differ by layout, "
+            f"not by code: at N=1 each carries the other layout's figure (alt_* keys).")
 
 
-def _deployed_subrun(a, server_cpus, load_cpus) -> dict | None:
-    """The replica exactly as deployed: deploy/Dockerfile's ENTRYPOINT (its /app paths mapped
-    to this tree) + the container args and env of deploy/openshift/hola-dc.yaml, in a cpuset of
-    this rank's server CPUs (a Guaranteed pod under the static CPU manager), HOSTNAME = a pod
-    name. Only the listen port differs (a free one instead of 8080). Same load generator as the
-    headline, about --deployed-seconds long."""
-    import socket
-    import subprocess
-
-    from hola_amd import native
-    from hola_amd.kube import manifests as km
-    from hola_amd.kube.image import Image
-
-    img = Image.from_dockerfile()
-    dc = next(o for o in km.load_objects([Path(__file__).resolve().parent / "deploy/openshift/hola-dc.yaml"])
-              if o["kind"] == "DeploymentConfig")
-    cont = dc["spec"]["template"]["spec"]["containers"][0]
-    argv = [str(img.files.get(x, x)) for x in img.entrypoint] + [str(x) for x in cont.get("args") or []]
-    argv[0] = str(native.binary("hola"))
-    port = _free_port_block(18900, 1)
-    argv += ["--port", str(port)]
-    env = {k: v for k, v in os.environ.items() if k in ("PATH", "LANG", "LD_LIBRARY_PATH")}
-    env.update(img.env)
-    env.update({e["name"]: str(e["value"]) for e in cont.get("env") or [] if "value" in e})
-    env["HOSTNAME"] = "hola-1-deplo"  # fieldRef metadata.name
-    cpus = list(server_cpus)
-    proc = subprocess.Popen(argv, env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
-                            preexec_fn=lambda: os.sched_setaffinity(0, cpus))
-    try:
-        deadline = time.monotonic() + 10
-        while True:
-            try:
-                socket.create_connection(("127.0.0.1", port), timeout=1).close()
-                break
-            except OSError:
-                if proc.poll() is not None or time.monotonic() > deadline:
-                    return {"error": f"deployed replica did not start (rc {proc.poll()})"}
-                time.sleep(0.02)
-        body = ["Hola de hola-1-deplo"] if a.path == "/api/hola" else None
-        lg = ControlledLoadgen([("127.0.0.1", port)], a.connections, len(load_cpus),
-                               cpu_list=",".join(map(str, load_cpus)), path=a.path, busy_poll_us=a.busy_poll_us,
-                               busy_poll_pause=a.busy_poll_pause, epoll_lt=a.epoll_lt,
-                               expect_bodies=body, verify_body=body is None)
-        try:
-            warm = lg.run(2000)
-            rate = warm["requests"] / max(1e-9, warm["elapsed_ns"] / 1e9)
-            per_conn = int(min(200_000, max(2_000, rate * a.deployed_seconds / a.connections)))
-            lg.reset()
-            c0 = proc_cpu_s(proc.pid)
-            r = lg.run(per_conn)
-            c1 = proc_cpu_s(proc.pid)
-            st = lg.stats()
-        finally:
-            lg.close()
-    finally:
-        proc.terminate()
-        try:
-            proc.wait(timeout=15)
-        except subprocess.TimeoutExpired:
-            proc.kill()
-    el = r["elapsed_ns"] / 1e9
-    return {"rps": r["requests"] / el if el > 0 else 0.0, "p50_ns": st["p50_ns"], "p99_ns": st["p99_ns"],
-            "requests": r["requests"], "errors": r["errors"], "non2xx": st.get("non2xx", 0),
-            "cpu_us_per_req": 1e6 * (c1 - c0) / max(1, r["requests"]),
-            "args": " ".join(["hola"] + argv[1:-2]), "cpus": format_cpu_list(cpus),
-            "env": " ".join(f"{k}={v}" for k, v in sorted(env.items()) if k in img.env or k == "HOSTNAME")}
-
-
-def _chain_subrun(a, cpus: list[int]) -> dict:
-    """GET /api/hola-chaining end to end (HolaResource.java:69-78,94-113): load generator ->
-    hola A -> hola B, where B plays aloha (B's own aloha is unreachable, so B answers its
-    fallback list at once: ["Hola de B", "Aloha response (fallback)"], which A decodes as the
-    aloha's List<String>). Every request crosses A's pooled keep-alive client, the Hystrix
-    command (breaker, bulkhead, 600 ms timer), B3 propagation and the JSON decode. Each body is
-    checked; an A-side fallback would differ from the expected body. The CPUs are the rank's
-    own, split 2:1:1 (A does two hops' work) with each L3 holding a share of all three."""
-    from hola_amd.parallel.loadgen import run_duration
-    from hola_amd.utils.cpu import split_mirrored
-
-    plan = split_mirrored(sorted(cpus), {"A": 2, "B": 1, "loadgen": 1})
-    with HolaProcess(args=["--aloha-url", "http://127.0.0.1:1/", "--feign-log", "none", "--no-tracing",
-                           "--feign-retry", "off", "--log-level", "warn"], env={"HOSTNAME": "B"},
-                     threads=len(plan["B"]), cpu_list=format_cpu_list(plan["B"])) as b:
-        with HolaProcess(args=["--aloha-url", f"http://127.0.0.1:{b.port}/", "--aloha-path", "api/hola-chaining",
-                               "--feign-log", "none", "--hystrix-pool-size", str(a.chain_pool), "--log-level", "warn"],
-                         env={"HOSTNAME": "A"}, threads=len(plan["A"]), cpu_list=format_cpu_list(plan["A"])) as s:
-            st, _, body = s.get("/api/hola-chaining")
-            want = json.dumps(["Hola de A", "Hola de B", "Aloha response (fallback)"], separators=(",", ":"))
-            if st != 200 or json.loads(body) != json.loads(want):
-                return {"error": f"unexpected first answer {st} {body[:200]!r}"}
-            ev0 = _hystrix_events(s)
-            c0 = proc_cpu_s(s.proc.pid), proc_cpu_s(b.proc.pid)
-            w0 = time.perf_counter()
-            res = run_duration([("127.0.0.1", s.port)], a.connections, len(plan["loadgen"]), a.chain_seconds, 1.0,
-                               cpu_list=format_cpu_list(plan["loadgen"]), path="/api/hola-chaining",
-                               expect_bodies=[body.decode()])
-            wall = time.perf_counter() - w0
-            c1 = proc_cpu_s(s.proc.pid), proc_cpu_s(b.proc.pid)
-            ev1 = _hystrix_events(s)
-    lat = res["latency"]
-    rps = res["rps"]
-    # CPU over the whole run (its 1 s warm-up included) per request at the measured rate
-    busy = ((c1[0] - c0[0]) / wall, (c1[1] - c0[1]) / wall)
-    return {"rps": rps, "p50_ns": lat["p50_ns"], "p99_ns": lat["p99_ns"], "requests": lat.get("count", 0),
-            "errors": lat["errors"], "non2xx": lat.get("non2xx", 0), "body_checked": lat.get("body_checked", 0),
-            "body_mismatch": lat.get("body_mismatch", 0),
-            "a_cpu_us_per_req": 1e6 * busy[0] / rps if rps else 0.0,
-            "b_cpu_us_per_req": 1e6 * busy[1] / rps if rps else 0.0,
-            "hystrix": {k: ev1.get(k, 0) - ev0.get(k, 0) for k in sorted(set(ev0) | set(ev1))},
-            "cpus": {k: format_cpu_list(v) for k, v in plan.items()}, "pool": a.chain_pool}
-
-
-def _hystrix_events(s: HolaProcess) -> dict:
-    _, _, metrics = s.get("/metrics")
-    return {ln.split('event="')[1].split('"')[0]: int(float(ln.split()[-1])) for ln in metrics.decode().splitlines()
-            if ln.startswith("hola_hystrix_events_total")}
-
-
-def _chain_keys(c: dict | None) -> dict:
+def _chain_keys(c: dict | None, p: str) -> dict:
+    """chain_* (engineered) or chain_shipped_* keys of a chain sub-run."""
     if not c:
         return {}
     if "error" in c:
-        return {"chain_error": c["error"]}
+        return {f"{p}_error": c["error"]}
     h = c["hystrix"]
-    return {"chain_rps": round(c["rps"], 1), "chain_p50_ms": round(c["p50_ns"] / 1e6, 4),
-            "chain_p99_ms": round(c["p99_ns"] / 1e6, 4), "chain_requests": c["requests"],
-            "chain_errors": c["errors"], "chain_non2xx": c["non2xx"], "chain_body_checked": c["body_checked"],
-            "chain_body_mismatch": c["body_mismatch"],
-            # hola A's own CPU per chained request (it serves the client and calls B)
-            "chain_a_cpu_us_per_req": round(c["a_cpu_us_per_req"], 3),
-            "chain_b_cpu_us_per_req": round(c["b_cpu_us_per_req"], 3),
-            # A's Hystrix command over the run (1 s warm-up included): all SUCCESS, no FALLBACK / TIMEOUT
-            "chain_hystrix_success": h.get("SUCCESS", 0), "chain_hystrix_fallback": h.get("FALLBACK_SUCCESS", 0),
-            "chain_hystrix_timeout": h.get("TIMEOUT", 0), "chain_hystrix_events": h,
-            "chain_cpus": c["cpus"], "chain_pool": c["pool"]}
+    n = max(1, c["body_checked"])
+    out = {f"{p}_rps": round(c["rps"], 1), f"{p}_p50_ms": round(c["p50_ns"] / 1e6, 4),
+           f"{p}_p99_ms": round(c["p99_ns"] / 1e6, 4), f"{p}_requests": c["requests"],
+           f"{p}_elapsed_s": round(c["elapsed_s"], 2),
+           f"{p}_errors": c["errors"], f"{p}_non2xx": c["non2xx"], f"{p}_body_checked": c["body_checked"],
+           f"{p}_body_mismatch": c["body_mismatch"],
+           # hola A's own CPU per chained request (it serves the client and calls B)
+           f"{p}_a_cpu_us_per_req": round(c["a_cpu_us_per_req"], 3),
+           f"{p}_b_cpu_us_per_req": round(c["b_cpu_us_per_req"], 3),
+           # A's Hystrix command over the sub-run (its warm-up included)
+           f"{p}_hystrix_success": h.get("SUCCESS", 0), f"{p}_hystrix_fallback": h.get("FALLBACK_SUCCESS", 0),
+           f"{p}_hystrix_timeout": h.get("TIMEOUT", 0), f"{p}_hystrix_events": h,
+           # busy share of the sub-run's CPUs and of their SMT siblings outside the job
+           f"{p}_host_load": c["host_load"],
+           # client thread vs serving worker of every connection accepted in the sub-run, per hop
+           f"{p}_locality": c["locality"],
+           # adaptive busy-polling of A and B: spins that found work / ran out, back-offs, ms backed off
+           f"{p}_spins": c["spins"], f"{p}_loadgen_busy_poll_us": c["loadgen_busy_poll_us"],
+           f"{p}_cpus": c["cpus"], f"{p}_pool": c["pool"]}
+    if c.get("shipped"):
+        # the timed responses that were A's own fallback (the pool of 10 or an open circuit)
+        out[f"{p}_fallback_fraction"] = round(c["body_alt"] / n, 4)
+        out[f"{p}_fallback_bodies"] = c["body_alt"]
+        out[f"{p}_args"] = c.get("args", "")
+    return out
+
+
+def _alt_keys(r: dict | None) -> dict:
+    if not r:
+        return {}
+    if "error" in r:
+        return {"alt_error": r["error"]}
+    return {"alt_smt": r["smt"], "alt_rps": round(r["rps"], 1), "alt_p50_ms": round(r["p50_ns"] / 1e6, 4),
+            "alt_p99_ms": round(r["p99_ns"] / 1e6, 4), "alt_requests": r["requests"], "alt_errors": r["errors"],
+            "alt_body_checked": r["body_checked"], "alt_body_mismatch": r["body_mismatch"],
+            "alt_elapsed_s": round(r["elapsed_s"], 2), "alt_physical_cores": r["physical_cores"],
+            "alt_rps_per_physical_core": round(r["rps_per_physical_core"], 1),
+            "alt_server_cpu_us_per_req": round(r["cpu_us_per_req"], 3), "alt_host_load": r["host_load"],
+            "alt_cpus": {"server": r["server_cpus"], "loadgen": r["loadgen_cpus"]}}
 
 
 def _deployed_keys(d: dict | None) -> dict:
@@ -733,12 +700,15 @@ def _deployed_keys(d: dict | None) -> dict:
         return {"deployed_error": d["error"]}
     return {"deployed_rps": round(d["rps"], 1), "deployed_p50_ms": round(d["p50_ns"] / 1e6, 4),
             "deployed_p99_ms": round(d["p99_ns"] / 1e6, 4), "deployed_requests": d["requests"],
+            "deployed_elapsed_s": round(d["elapsed_s"], 2),
             "deployed_errors": d["errors"], "deployed_non2xx": d["non2xx"],
+            "deployed_body_checked": d["body_checked"], "deployed_body_mismatch": d["body_mismatch"],
             "deployed_server_cpu_us_per_req": round(d["cpu_us_per_req"], 3),
+            "deployed_host_load": d["host_load"],
             "deployed_args": d["args"], "deployed_cpus": d["cpus"],
             # ZIPKIN_SERVER_URL names the cluster's zipkin-query Service, which does not resolve
-            # on a bare host: spans are recorded and dropped, as Brave does without a collector
-            "deployed_env": d["env"]}
+            # on a bare host: spans are recorded and dropped when the post fails
+            "deployed_env": d["env"], "deployed_zipkin": d["zipkin"]}
 
 
 def _c1_keys(c1: dict | None) -> dict:
@@ -777,28 +747,6 @@ def _can_bind(host: str) -> bool:
         return True
     except OSError:
         return False
-
-
-def _free_port_block(start: int, n: int, host: str = "127.0.0.1") -> int:
-    """First base >= start such that base..base+n-1 can all be bound on `host`."""
-    import socket
-
-    base = start
-    for _ in range(200):
-        socks = []
-        try:
-            for i in range(n):
-                sk = socket.socket(socket.AF_INET6 if ":" in host else socket.AF_INET)
-                sk.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
-                sk.bind((host, base + i))
-                socks.append(sk)
-            return base
-        except OSError:
-            base += n + 7
-        finally:
-            for sk in socks:
-                sk.close()
-    return start
 
 
 def _gpu_slots() -> int:

@@ -21,7 +21,9 @@
 // Response bodies are verified against --expect-body (one per target in --targets order, or
 // one for all) and/or, with --verify-body, against the first 2xx body each thread sees from
 // each target; a mismatch counts as an error (and in "body_mismatch"), so a server that
-// answers fast with the wrong bytes cannot inflate req/s.
+// answers fast with the wrong bytes cannot inflate req/s. --alt-body B names an accepted
+// second answer (e.g. the chaining endpoint's Hystrix fallback body): a response equal to it
+// is counted in "body_alt" instead of as a mismatch, so a run reports how many of each came.
 //
 // Service mode (`--endpoints-file F`): the load generator addresses a Kubernetes Service (the
 // --targets / URL address, used in the Host header) and each new connection is DNATed at
@@ -104,6 +106,7 @@ struct Options {
   bool per_conn_quota = false;
   int pipeline = 1;  // requests per batch (closed loop only)
   std::vector<std::string> expect_bodies;  // --expect-body: per target, or one for all
+  std::vector<std::string> alt_bodies;     // --alt-body: accepted alternatives (counted apart)
   bool verify_body = false;                // --verify-body: learn the first 2xx body per target
   std::vector<int> conn_targets;           // --conn-targets: target index of connection i (cycled)
   std::string endpoints_file;              // --endpoints-file: Service mode (connect-time DNAT)
@@ -132,7 +135,7 @@ struct ThreadState {
   Histogram hist;
   std::mutex hist_mu;
   uint64_t completed = 0, errors = 0, non2xx = 0, reconnects = 0, bytes = 0;
-  uint64_t body_checked = 0, body_mismatch = 0;
+  uint64_t body_checked = 0, body_mismatch = 0, body_alt = 0;
   std::vector<std::string> expected;  // per target: the body every response must carry
   std::vector<bool> have_expected;
   std::atomic<int64_t> run_quota{0};  // control: batches per connection for the next run
@@ -586,9 +589,16 @@ void thread_main(ThreadState* ts, const Options* o) {
             ts->expected[t].assign(c->buf + body_at, blen);
             ts->have_expected[t] = true;
           } else if (blen != ts->expected[t].size() || memcmp(c->buf + body_at, ts->expected[t].data(), blen) != 0) {
-            if (ts->recording) ++ts->body_mismatch;
-            ++ts->errors;
-            ++run_errors;
+            bool alt = false;
+            for (const auto& b : o->alt_bodies)
+              if (blen == b.size() && memcmp(c->buf + body_at, b.data(), blen) == 0) alt = true;
+            if (alt) {
+              if (ts->recording) ++ts->body_alt;
+            } else {
+              if (ts->recording) ++ts->body_mismatch;
+              ++ts->errors;
+              ++run_errors;
+            }
           }
           if (ts->recording) ++ts->body_checked;
         }
@@ -660,7 +670,7 @@ bool parse_targets(const std::string& s, std::vector<Target>* out) {
 
 std::string stats_json(std::vector<std::unique_ptr<ThreadState>>& ts, bool with_hist) {
   Histogram h;
-  uint64_t errors = 0, non2xx = 0, reconnects = 0, checked = 0, mismatch = 0;
+  uint64_t errors = 0, non2xx = 0, reconnects = 0, checked = 0, mismatch = 0, alt = 0;
   for (auto& t : ts) {
     std::lock_guard<std::mutex> g(t->hist_mu);
     h.merge(t->hist);
@@ -669,17 +679,18 @@ std::string stats_json(std::vector<std::unique_ptr<ThreadState>>& ts, bool with_
     reconnects += t->reconnects;
     checked += t->body_checked;
     mismatch += t->body_mismatch;
+    alt += t->body_alt;
   }
-  char buf[640];
+  char buf[704];
   snprintf(buf, sizeof buf,
            "{\"count\":%llu,\"mean_ns\":%.0f,\"p50_ns\":%llu,\"p90_ns\":%llu,\"p99_ns\":%llu,\"p999_ns\":%llu,"
            "\"max_ns\":%llu,\"errors\":%llu,\"non2xx\":%llu,\"reconnects\":%llu,\"body_checked\":%llu,"
-           "\"body_mismatch\":%llu",
+           "\"body_mismatch\":%llu,\"body_alt\":%llu",
            (unsigned long long)h.count(), h.mean(), (unsigned long long)h.percentile(50),
            (unsigned long long)h.percentile(90), (unsigned long long)h.percentile(99),
            (unsigned long long)h.percentile(99.9), (unsigned long long)h.max(), (unsigned long long)errors,
            (unsigned long long)non2xx, (unsigned long long)reconnects, (unsigned long long)checked,
-           (unsigned long long)mismatch);
+           (unsigned long long)mismatch, (unsigned long long)alt);
   std::string s = buf;
   if (with_hist) s += ",\"hist\":\"" + h.encode() + "\"";
   return s + "}";
@@ -793,6 +804,7 @@ int main(int argc, char** argv) {
     else if (a == "--per-conn-quota") o.per_conn_quota = true;
     else if (a == "--pipeline") o.pipeline = atoi(val().c_str());
     else if (a == "--expect-body") o.expect_bodies.push_back(unescape(val()));
+    else if (a == "--alt-body") o.alt_bodies.push_back(unescape(val()));
     else if (a == "--verify-body") o.verify_body = true;
     else if (a == "--cpu-profile") cpu_profile = val();
     else if (a == "--endpoints-file") o.endpoints_file = val();
@@ -807,7 +819,7 @@ int main(int argc, char** argv) {
               "usage: hola_loadgen --targets h:p[,h:p..] -c CONNS -t THREADS [--cpu-list L] [--path P]\n"
               "                    (--duration S [--warmup S] [--rate R [--spin-us N]] | --control [--per-conn-quota])\n"
               "                    [--target-offset K] [--busy-poll-us N [--busy-poll-pause P]] [--epoll-lt] [-H 'Name: v']\n"
-              "                    [--pipeline P] [--expect-body B]... [--verify-body] [--conn-targets i,j,..]\n"
+              "                    [--pipeline P] [--expect-body B]... [--alt-body B]... [--verify-body] [--conn-targets i,j,..]\n"
               "                    [--cpu-profile FILE]  (sampled call stacks, bench/cpuprof_report.py --threads hola-lg)\n"
               "                    [--endpoints-file F]  (Service mode: --targets is the Service, F its endpoints)\n"
               "       hola_loadgen -t T -c C -d 30s [--latency] [--json] [-H 'Name: v'] http://host:port/path   (wrk style)\n");
@@ -974,7 +986,7 @@ int main(int argc, char** argv) {
       for (auto& t : ts) {
         std::lock_guard<std::mutex> g(t->hist_mu);
         t->hist.reset();
-        t->errors = t->non2xx = t->reconnects = t->body_checked = t->body_mismatch = 0;
+        t->errors = t->non2xx = t->reconnects = t->body_checked = t->body_mismatch = t->body_alt = 0;
       }
       printf("{\"reset\":true}\n");
       fflush(stdout);

@@ -41,10 +41,12 @@ def escape_body(b: str) -> str:
     return b.replace("\\", "\\\\").replace("\n", "\\n").replace("\r", "\\r").replace("\t", "\\t")
 
 
-def body_args(expect_bodies: list[str] | None, verify_body: bool) -> list[str]:
+def body_args(expect_bodies: list[str] | None, verify_body: bool, alt_bodies: list[str] | None = None) -> list[str]:
     out: list[str] = []
     for b in expect_bodies or []:
         out += ["--expect-body", escape_body(b)]
+    for b in alt_bodies or []:  # accepted second answers, counted as body_alt
+        out += ["--alt-body", escape_body(b)]
     if verify_body:
         out += ["--verify-body"]
     return out
@@ -74,10 +76,11 @@ class ControlledLoadgen:
                  headers: list[str] | None = None, busy_poll_us: int = 0, per_conn_quota: bool = False,
                  busy_poll_pause: int = 0, epoll_lt: bool = False, pipeline: int = 1,
                  expect_bodies: list[str] | None = None, verify_body: bool = False,
-                 conn_targets: list[int] | None = None, cpu_profile: str | None = None):
+                 conn_targets: list[int] | None = None, cpu_profile: str | None = None,
+                 alt_bodies: list[str] | None = None):
         cmd = [str(binary("hola_loadgen")), "--targets", ",".join(f"{h}:{p}" for h, p in targets),
                "-c", str(connections), "-t", str(threads), "--path", path, "--control",
-               "--target-offset", str(target_offset)] + body_args(expect_bodies, verify_body)
+               "--target-offset", str(target_offset)] + body_args(expect_bodies, verify_body, alt_bodies)
         if cpu_list:
             cmd += ["--cpu-list", cpu_list]
         for h in headers or []:
@@ -139,7 +142,7 @@ def run_duration(targets: list[tuple[str, int]], connections: int, threads: int,
                  warmup_s: float = 1.0, cpu_list: str | None = None, path: str = "/api/hola",
                  timeout: float | None = None, rate: float = 0.0, busy_poll_us: int = 0,
                  spin_us: int = 0, pipeline: int = 1, expect_bodies: list[str] | None = None,
-                 verify_body: bool = False) -> dict:
+                 verify_body: bool = False, alt_bodies: list[str] | None = None, busy_poll_pause: int = 0) -> dict:
     """wrk-style timed run (closed loop), or wrk2-style open loop at `rate` req/s with latency
     measured from intended send times; returns the loadgen's JSON summary. `busy_poll_us`
     spins in epoll after activity; `spin_us` (open loop) spins instead of sleeping when the
@@ -147,13 +150,15 @@ def run_duration(targets: list[tuple[str, int]], connections: int, threads: int,
     (closed loop only)."""
     cmd = [str(binary("hola_loadgen")), "--targets", ",".join(f"{h}:{p}" for h, p in targets),
            "-c", str(connections), "-t", str(threads), "--path", path, "--duration", str(duration_s),
-           "--warmup", str(warmup_s)] + body_args(expect_bodies, verify_body)
+           "--warmup", str(warmup_s)] + body_args(expect_bodies, verify_body, alt_bodies)
     if cpu_list:
         cmd += ["--cpu-list", cpu_list]
     if rate > 0:
         cmd += ["--rate", str(rate)]
     if busy_poll_us:
         cmd += ["--busy-poll-us", str(busy_poll_us)]
+        if busy_poll_pause:
+            cmd += ["--busy-poll-pause", str(busy_poll_pause)]
     if spin_us:
         cmd += ["--spin-us", str(spin_us)]
     if pipeline > 1:

@@ -1,0 +1,376 @@
+"""bench.py's sub-runs: measurements taken on rank 0's CPUs after the timed region, so the
+headline `value` is untouched by them.
+
+* `config2`: BASELINE config 2 (one keep-alive connection, ~30 s) against the rank's replica.
+* `deployed`: the replica exactly as the image and manifests start it (deploy/Dockerfile
+  ENTRYPOINT + deploy/openshift/hola-dc.yaml args and env), with its own host load; the
+  `zipkin` variant ("deployed" / "unset" / a collector URL) isolates the tracing path.
+* `chain`: GET /api/hola-chaining, load generator -> hola A -> hola B (B answering as aloha),
+  either engineered (bulkhead widened to 128, Feign logging off: the path's capacity) or
+  as shipped (A started as the manifests start it: the reference's pool of 10 from
+  conf/config.properties defaults, Feign BASIC logging, ZIPKIN_SERVER_URL set), with the
+  attribution the two modes of this path need: host load, accept locality of both hops
+  (load generator -> A from A's /metrics, A -> B from B's) and both replicas' busy-poll
+  spin / back-off counters.
+* `alt_layout`: the headline again in the other SMT layout on the same physical cores, so a
+  1-GPU box (smt=off) and an 8-GPU node's N = 1 (smt=pair) each carry the other's figure.
+
+Reference: HolaResource.java:69-78,94-113 (the chained call), Dockerfile:4-6 and
+src/main/resources/config.properties:17,19 (the shipped configuration), pom.xml:77-94 (the
+Service and the pod).
+"""
+from __future__ import annotations
+
+import json
+import os
+import socket
+import subprocess
+import time
+from pathlib import Path
+
+from hola_amd.parallel.hostmetrics import busy_fraction, cpu_times, proc_cpu_s
+from hola_amd.parallel.loadgen import ControlledLoadgen
+from hola_amd.server import HolaProcess
+from hola_amd.utils import cpu as _cpu
+from hola_amd.utils.cpu import format_cpu_list, split_mirrored, split_server_loadgen
+from hola_amd.utils.net import http_get
+
+REPO = Path(__file__).resolve().parents[2]
+FALLBACK = "Aloha response (fallback)"  # HolaResource.java:111-112
+
+
+# ---------------------------------------------------------------- host load / counters
+
+def other_siblings(own, job_cpus) -> set[int]:
+    """SMT siblings of `own` that the job itself did not plan (busy there = another tenant)."""
+    job = set(job_cpus) | set(own)
+    return {x for c in own for x in _cpu.siblings(c)} - job
+
+
+def host_load(t0: dict, t1: dict, own, job_cpus) -> dict:
+    """Busy share of `own` and of the SMT siblings of `own` that belong to no part of the job."""
+    return {"own": busy_fraction(t0, t1, set(own)), "siblings": busy_fraction(t0, t1, other_siblings(own, job_cpus))}
+
+
+def metrics_counters(port: int, host: str = "127.0.0.1") -> dict:
+    """The /metrics counters the sub-runs attribute with: accept locality, busy-poll spins and
+    back-offs, Hystrix events, requests (empty on a failed scrape)."""
+    try:
+        st, _, body = http_get(host, port, "/metrics", timeout=5.0)
+    except OSError:
+        return {}
+    if st != 200:
+        return {}
+    out: dict[str, float] = {}
+    for ln in body.decode().splitlines():
+        if not ln or ln[0] == "#":
+            continue
+        name, _, val = ln.rpartition(" ")
+        if name.startswith("hola_accept_locality_total{"):
+            out["locality." + name.split('"')[1]] = float(val)
+        elif name.startswith("hola_busy_poll_spins_total{"):
+            out["spins." + name.split('"')[1]] = float(val)
+        elif name == "hola_busy_poll_backoffs_total":
+            out["spins.backoffs"] = float(val)
+        elif name == "hola_busy_poll_backoff_ms_total":
+            out["spins.backoff_ms"] = float(val)
+        elif name.startswith("hola_hystrix_events_total{"):
+            out["hystrix." + name.split('event="')[1].split('"')[0]] = float(val)
+        elif name == "hola_http_requests_total":
+            out["requests"] = float(val)
+    return out
+
+
+def counter_delta(c0: dict, c1: dict, prefix: str) -> dict:
+    return {k[len(prefix):]: int(c1.get(k, 0) - c0.get(k, 0)) for k in sorted(set(c0) | set(c1))
+            if k.startswith(prefix)}
+
+
+def locality_fraction(d: dict) -> dict:
+    n = sum(d.values())
+    return {k: round(v / n, 4) for k, v in d.items() if v} if n else {}
+
+
+# ---------------------------------------------------------------- processes as deployed
+
+def deployed_argv_env(port: int, hostname: str, extra_args: list[str] | None = None,
+                      env_over: dict | None = None) -> tuple[list[str], dict]:
+    """argv and environment of a replica started as the image and manifests start it:
+    deploy/Dockerfile's ENTRYPOINT (its /app paths mapped to this tree) + the container args
+    and env of deploy/openshift/hola-dc.yaml, HOSTNAME = a pod name. `extra_args` are appended
+    (the listen port always; --aloha-url for the shipped chain); `env_over` replaces or (value
+    None) removes variables."""
+    from hola_amd import native
+    from hola_amd.kube import manifests as km
+    from hola_amd.kube.image import Image
+
+    img = Image.from_dockerfile()
+    dc = next(o for o in km.load_objects([REPO / "deploy/openshift/hola-dc.yaml"]) if o["kind"] == "DeploymentConfig")
+    cont = dc["spec"]["template"]["spec"]["containers"][0]
+    argv = [str(img.files.get(x, x)) for x in img.entrypoint] + [str(x) for x in cont.get("args") or []]
+    argv[0] = str(native.binary("hola"))
+    argv += ["--port", str(port)] + list(extra_args or [])
+    env = {k: v for k, v in os.environ.items() if k in ("PATH", "LANG", "LD_LIBRARY_PATH")}
+    env.update(img.env)
+    env.update({e["name"]: str(e["value"]) for e in cont.get("env") or [] if "value" in e})
+    env["HOSTNAME"] = hostname  # fieldRef metadata.name
+    for k, v in (env_over or {}).items():
+        if v is None:
+            env.pop(k, None)
+        else:
+            env[k] = v
+    return argv, env
+
+
+class DeployedProc:
+    """A replica started from deployed_argv_env() in a cpuset (a Guaranteed pod under the
+    static CPU manager); stderr to /dev/null (Feign BASIC logging writes two lines per call)."""
+
+    def __init__(self, cpus, hostname: str, extra_args=None, env_over=None, base_port: int = 18900):
+        self.cpus = list(cpus)
+        self.port = free_port_block(base_port, 1)
+        self.argv, self.env = deployed_argv_env(self.port, hostname, extra_args, env_over)
+        self.proc: subprocess.Popen | None = None
+
+    def __enter__(self) -> "DeployedProc":
+        cpus = self.cpus
+        self.proc = subprocess.Popen(self.argv, env=self.env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                                     preexec_fn=lambda: os.sched_setaffinity(0, cpus))
+        deadline = time.monotonic() + 10
+        while True:
+            try:
+                socket.create_connection(("127.0.0.1", self.port), timeout=1).close()
+                return self
+            except OSError:
+                if self.proc.poll() is not None or time.monotonic() > deadline:
+                    self.__exit__()
+                    raise RuntimeError(f"deployed replica did not start (rc {self.proc.poll()})")
+                time.sleep(0.02)
+
+    def __exit__(self, *exc) -> None:
+        if self.proc and self.proc.poll() is None:
+            self.proc.terminate()
+            try:
+                self.proc.wait(timeout=15)
+            except subprocess.TimeoutExpired:
+                self.proc.kill()
+                self.proc.wait()
+
+    def shown_args(self) -> str:
+        return " ".join(["hola"] + self.argv[1:])
+
+    def shown_env(self, keys) -> str:
+        return " ".join(f"{k}={v}" for k, v in sorted(self.env.items()) if k in keys)
+
+
+def free_port_block(start: int, n: int, host: str = "127.0.0.1") -> int:
+    """First base >= start such that base..base+n-1 can all be bound on `host`."""
+    base = start
+    for _ in range(200):
+        socks = []
+        try:
+            for i in range(n):
+                sk = socket.socket(socket.AF_INET6 if ":" in host else socket.AF_INET)
+                sk.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+                sk.bind((host, base + i))
+                socks.append(sk)
+            return base
+        except OSError:
+            base += n + 7
+        finally:
+            for sk in socks:
+                sk.close()
+    return start
+
+
+# ---------------------------------------------------------------- timed closed-loop runs
+
+def timed_closed_loop(lg: ControlledLoadgen, connections: int, seconds: float, pid: int | None,
+                      own, job_cpus, warm_per_conn: int = 2000, max_per_conn: int = 2_000_000) -> dict:
+    """One controlled run sized from a warm-up to last about `seconds`; latency, errors,
+    bodies, the server's CPU per request and the host load of the run."""
+    warm = lg.run(warm_per_conn)
+    rate = warm["requests"] / max(1e-9, warm["elapsed_ns"] / 1e9)
+    per_conn = int(min(max_per_conn, max(2_000, rate * seconds / connections)))
+    lg.reset()
+    t0, c0 = cpu_times(), proc_cpu_s(pid) if pid else 0.0
+    r = lg.run(per_conn)
+    t1, c1 = cpu_times(), proc_cpu_s(pid) if pid else 0.0
+    st = lg.stats()
+    el = r["elapsed_ns"] / 1e9
+    return {"rps": r["requests"] / el if el > 0 else 0.0, "elapsed_s": el, "requests": r["requests"],
+            "errors": r["errors"], "p50_ns": st["p50_ns"], "p99_ns": st["p99_ns"], "non2xx": st.get("non2xx", 0),
+            "body_checked": st.get("body_checked", 0), "body_mismatch": st.get("body_mismatch", 0),
+            "body_alt": st.get("body_alt", 0),
+            "cpu_us_per_req": 1e6 * (c1 - c0) / max(1, r["requests"]) if pid else None,
+            "host_load": host_load(t0, t1, own, job_cpus)}
+
+
+def config2(a, host: str, port: int, server_cpus, load_cpus, bodies, job_cpus) -> dict | None:
+    """BASELINE config 2: one keep-alive connection against this rank's replica."""
+    if a.c1_reqs <= 0 and a.c1_seconds <= 0:
+        return None
+    lg = ControlledLoadgen([(host, port)], 1, 1, cpu_list=str(load_cpus[0]), path=a.path,
+                           busy_poll_us=a.busy_poll_us, busy_poll_pause=a.busy_poll_pause, epoll_lt=a.epoll_lt,
+                           expect_bodies=bodies, verify_body=bodies is None)
+    try:
+        warm = lg.run(max(1000, a.c1_reqs // 10) if a.c1_reqs > 0 else 50000)
+        n = a.c1_reqs
+        if n <= 0:  # size the run from the warm-up rate: about --c1-seconds, within bounds
+            rate = warm["requests"] / max(1e-9, warm["elapsed_ns"] / 1e9)
+            n = int(min(30_000_000, max(20_000, rate * a.c1_seconds)))
+        lg.reset()
+        own = set(server_cpus) | {load_cpus[0]}
+        t0 = cpu_times()
+        r = lg.run(n)
+        t1 = cpu_times()
+        st = lg.stats()
+    finally:
+        lg.close()
+    el = r["elapsed_ns"] / 1e9
+    return {"rps": r["requests"] / el if el > 0 else 0.0, "requests": r["requests"], "elapsed_s": el,
+            "p50_ns": st["p50_ns"], "p99_ns": st["p99_ns"], "errors": r["errors"],
+            "body_checked": st.get("body_checked", 0), "client_cpu": load_cpus[0],
+            "host_load": host_load(t0, t1, own, job_cpus)}
+
+
+ZIPKIN_VARIANTS = ("deployed", "unset", "sink")
+
+
+def deployed(a, server_cpus, load_cpus, job_cpus, zipkin: str = "deployed", seconds: float | None = None) -> dict:
+    """The replica as deployed, driven by the headline's load generator for about
+    --deployed-seconds. `zipkin`: "deployed" = the manifests' ZIPKIN_SERVER_URL (the cluster's
+    zipkin-query Service, which does not resolve on a bare host: spans are recorded and then
+    dropped when the post fails), "unset" = no collector (spans dropped at the source, the
+    headline's path), "sink" = a native discard collector that accepts every post."""
+    from hola_amd.parallel.hostmetrics import start_zipkin_sink
+
+    sink = None
+    env_over: dict = {}
+    if zipkin == "unset":
+        env_over["ZIPKIN_SERVER_URL"] = None
+    elif zipkin == "sink":
+        sink = start_zipkin_sink()
+        env_over["ZIPKIN_SERVER_URL"] = f"http://127.0.0.1:{sink[1]}"
+    try:
+        with DeployedProc(server_cpus, "hola-1-deplo", env_over=env_over) as d:
+            body = ["Hola de hola-1-deplo"] if a.path == "/api/hola" else None
+            lg = ControlledLoadgen([("127.0.0.1", d.port)], a.connections, len(load_cpus),
+                                   cpu_list=",".join(map(str, load_cpus)), path=a.path, busy_poll_us=a.busy_poll_us,
+                                   busy_poll_pause=a.busy_poll_pause, epoll_lt=a.epoll_lt,
+                                   expect_bodies=body, verify_body=body is None)
+            try:
+                r = timed_closed_loop(lg, a.connections, seconds or a.deployed_seconds, d.proc.pid,
+                                      list(server_cpus) + list(load_cpus), job_cpus)
+            finally:
+                lg.close()
+            r.update({"args": " ".join(d.shown_args().split()[:-2]), "cpus": format_cpu_list(server_cpus),
+                      "env": d.shown_env(set(d.env) - {"PATH", "LANG", "LD_LIBRARY_PATH"}), "zipkin": zipkin})
+            return r
+    finally:
+        if sink:
+            sink[0].terminate()
+            sink[0].wait(timeout=10)
+
+
+def chain(a, cpus, job_cpus, shipped: bool = False, seconds: float | None = None, loadgen_busy_poll: int = -1) -> dict:
+    """GET /api/hola-chaining end to end (HolaResource.java:69-78,94-113): load generator ->
+    hola A -> hola B, where B plays aloha (B's own aloha is unreachable, so B answers its
+    fallback list at once: ["Hola de B", "Aloha response (fallback)"], which A decodes as the
+    aloha's List<String>). Every request crosses A's pooled keep-alive client, the Hystrix
+    command (breaker, bulkhead, 600 ms timer), B3 propagation and the JSON decode. The CPUs
+    are split 2:1:1 (A does two hops' work) with each L3 holding a share of all three.
+
+    Engineered (default): A's bulkhead widened to --chain-pool, Feign logging and tracing off:
+    every body must be the two-hop answer. Shipped: A is started as the manifests start it
+    (image ENTRYPOINT + hola-dc.yaml args and env: the reference's pool of 10, Feign BASIC
+    logging on, ZIPKIN_SERVER_URL set); the only changes are the aloha URL and path (B on
+    loopback instead of the aloha Service) and the listen port. A body is then either the
+    two-hop answer or A's own fallback (counted apart, as body_alt)."""
+    seconds = seconds or a.chain_seconds
+    plan = split_mirrored(sorted(cpus), {"A": 2, "B": 1, "loadgen": 1})
+    lg_bp = a.chain_loadgen_busy_poll if loadgen_busy_poll < 0 else loadgen_busy_poll
+    with HolaProcess(args=["--aloha-url", "http://127.0.0.1:1/", "--feign-log", "none", "--no-tracing",
+                           "--feign-retry", "off", "--log-level", "warn"], env={"HOSTNAME": "B"},
+                     threads=len(plan["B"]), cpu_list=format_cpu_list(plan["B"])) as b:
+        aloha = ["--aloha-url", f"http://127.0.0.1:{b.port}/", "--aloha-path", "api/hola-chaining"]
+        if shipped:
+            a_ctx = DeployedProc(plan["A"], "A", extra_args=aloha)
+        else:
+            a_ctx = HolaProcess(args=aloha + ["--feign-log", "none", "--hystrix-pool-size", str(a.chain_pool),
+                                              "--log-level", "warn"],
+                                env={"HOSTNAME": "A"}, threads=len(plan["A"]), cpu_list=format_cpu_list(plan["A"]))
+        with a_ctx as s:
+            st, _, body = http_get("127.0.0.1", s.port, "/api/hola-chaining", timeout=5.0)
+            want = ["Hola de A", "Hola de B", FALLBACK]
+            if st != 200 or json.loads(body) != want:
+                return {"error": f"unexpected first answer {st} {body[:200]!r}"}
+            fallback_body = json.dumps(["Hola de A", FALLBACK], separators=(",", ":"))
+            m0 = metrics_counters(s.port), metrics_counters(b.port)
+            c0 = proc_cpu_s(s.proc.pid), proc_cpu_s(b.proc.pid)
+            lg = ControlledLoadgen([("127.0.0.1", s.port)], a.connections, len(plan["loadgen"]),
+                                   cpu_list=format_cpu_list(plan["loadgen"]), path="/api/hola-chaining",
+                                   busy_poll_us=lg_bp, expect_bodies=[body.decode()],
+                                   alt_bodies=[fallback_body] if shipped else None)
+            try:
+                w0 = time.perf_counter()
+                r = timed_closed_loop(lg, a.connections, seconds, None, cpus, job_cpus,
+                                      warm_per_conn=1000 if shipped else 5000)
+                wall = time.perf_counter() - w0
+            finally:
+                lg.close()
+            c1 = proc_cpu_s(s.proc.pid), proc_cpu_s(b.proc.pid)
+            m1 = metrics_counters(s.port), metrics_counters(b.port)
+            args = s.shown_args() if shipped else None
+    rps = r["rps"]
+    # CPU over the whole sub-run (its warm-up included) per request at the measured rate
+    busy = ((c1[0] - c0[0]) / wall, (c1[1] - c0[1]) / wall)
+    out = {**r, "a_cpu_us_per_req": 1e6 * busy[0] / rps if rps else 0.0,
+           "b_cpu_us_per_req": 1e6 * busy[1] / rps if rps else 0.0,
+           "hystrix": counter_delta(m0[0], m1[0], "hystrix."),
+           # where each accepted connection's client thread ran relative to the worker serving
+           # it: load generator -> A (A's counters), A's pooled client -> B (B's counters)
+           "locality": {"loadgen_to_a": locality_fraction(counter_delta(m0[0], m1[0], "locality.")),
+                        "a_to_b": locality_fraction(counter_delta(m0[1], m1[1], "locality."))},
+           # adaptive busy-polling of each replica over the sub-run: spins that found work,
+           # spins that ran out, back-offs and the milliseconds spent backed off (summed over
+           # workers)
+           "spins": {"a": counter_delta(m0[0], m1[0], "spins."), "b": counter_delta(m0[1], m1[1], "spins.")},
+           "cpus": {k: format_cpu_list(v) for k, v in plan.items()}, "loadgen_busy_poll_us": lg_bp,
+           "pool": 10 if shipped else a.chain_pool, "shipped": shipped}
+    if args:
+        out["args"] = args
+    return out
+
+
+def alt_layout(a, host: str, server_cpus, load_cpus, smt: str, job_cpus, bodies, seconds: float) -> dict:
+    """The headline replica in the other SMT layout, on the rank's physical cores:
+    smt=off here (1-GPU box)  -> pair on the server's physical cores (worker + its client
+                                 thread on the two threads of one core), i.e. the 8-GPU node's
+                                 per-replica shape at half its cores;
+    smt=pair here (the node)  -> off on the same physical cores (server workers and client
+                                 threads on separate cores, siblings idle): the 1-GPU box's
+                                 BENCH layout when the rank has 16 physical cores."""
+    if smt == "pair":
+        phys = sorted({min(_cpu.siblings(c)) for c in list(server_cpus) + list(load_cpus)})
+        sv, ld = split_server_loadgen(phys, max(1, len(phys) // 2))
+        alt = "off"
+    else:
+        sv = sorted(server_cpus)
+        ld = [next((x for x in _cpu.siblings(c) if x != c), c) for c in sv]
+        alt = "pair"
+    with HolaProcess(args=["--busy-poll-us", a.server_busy_poll] + (["--busy-poll-pause", "16"] if alt == "pair" else [])
+                     + (["--no-tracing"] if a.no_tracing else []),
+                     env={"HOSTNAME": "replica-0"}, threads=len(sv), cpu_list=format_cpu_list(sv),
+                     log_level="warn") as s:
+        lg = ControlledLoadgen([("127.0.0.1", s.port)], a.connections, len(ld), cpu_list=",".join(map(str, ld)),
+                               path=a.path, busy_poll_us=a.busy_poll_us, busy_poll_pause=16 if alt == "pair" else 0,
+                               expect_bodies=bodies, verify_body=bodies is None)
+        try:
+            r = timed_closed_loop(lg, a.connections, seconds, s.proc.pid, sv + ld, job_cpus, warm_per_conn=20000)
+        finally:
+            lg.close()
+    phys_n = len({min(_cpu.siblings(c)) for c in sv + ld})
+    r.update({"smt": alt, "server_cpus": format_cpu_list(sv), "loadgen_cpus": format_cpu_list(ld),
+              "physical_cores": phys_n, "rps_per_physical_core": r["rps"] / max(1, phys_n)})
+    return r

@@ -316,6 +316,38 @@ def plan_replicas_with_loadgen(local_world: int, per_rank: int | None = None, se
     return plans
 
 
+def plan_slot_subset(n: int, slots: int, k: int, smt: str = "pair", extra_cores: int = 0) -> list[dict]:
+    """A miniature of the node plan for weak-scaling curves inside a small CPU quota.
+
+    The node is laid out as `slots` slots of (physical cores / slots) cores each, exactly as
+    plan_node places them on the real topology (socket by socket, L3 domain by domain; the
+    quota is ignored for the layout), and replica r takes only the first `k` physical cores of
+    slot r: with smt=pair its server workers run on one SMT thread of each and the
+    load-generator thread that drives it on the other (the node plan's per-connection
+    placement), with smt=off the next `k` cores of the slot carry the load generator.
+    `extra_cores` more physical cores of the same slot are returned as "extra" (e.g. proxy
+    threads). Per replica: {"server", "loadgen", "extra", "slot"}."""
+    phys = physical_cores()
+    per = max(1, len(phys) // max(1, slots))
+    need = k * (1 if smt == "pair" else 2) + extra_cores
+    if per < need:
+        raise ValueError(f"a slot has {per} physical cores, {need} needed")
+    node = plan_node(slots, per, avoid_busy=False)
+    out = []
+    for r in range(n):
+        cores = node[r % slots]
+        srv = cores[:k]
+        if smt == "pair":
+            ld = [sibling_of(c) for c in srv]
+            if any(c is None for c in ld):
+                raise ValueError("smt=pair needs both SMT threads of every server core")
+            rest = cores[k:]
+        else:
+            ld, rest = cores[k:2 * k], cores[2 * k:]
+        out.append({"server": list(srv), "loadgen": list(ld), "extra": list(rest[:extra_cores]), "slot": r % slots})
+    return out
+
+
 def _groups_share_l3(splits: list[tuple[list[int], list[int]]], per: int) -> bool:
     """True when every group of `per` consecutive replicas has its servers and load-generator
     CPUs in one L3 domain."""

@@ -155,6 +155,7 @@ void EventLoop::note_spin(bool hit) {
     spin_backoff_ms_ = spin_backoff_ms_ ? std::min(kSpinBackoffMaxMs, spin_backoff_ms_ * 2) : kSpinBackoffMinMs;
     spin_off_until_ms_ = now_ms_ + spin_backoff_ms_;
     spin_offs_.fetch_add(1, std::memory_order_relaxed);
+    spin_off_ms_.fetch_add(uint64_t(spin_backoff_ms_), std::memory_order_relaxed);
   } else {
     spin_backoff_ms_ = 0;
   }

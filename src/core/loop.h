@@ -71,10 +71,12 @@ class EventLoop {
   // load, where it would only burn CPU). Each interval ends with a short re-probe.
   void set_busy_poll_auto(bool on) { busy_auto_ = on; }
   // Adaptive spin statistics (loop thread; tests and metrics): spins that found work, spins
-  // that ran out, and how many times spinning was switched off.
+  // that ran out, how many times spinning was switched off, and for how many milliseconds
+  // in total (the back-off intervals as scheduled).
   uint64_t spin_hits() const { return spin_hits_total_.load(std::memory_order_relaxed); }
   uint64_t spin_misses() const { return spin_misses_total_.load(std::memory_order_relaxed); }
   uint64_t spin_offs() const { return spin_offs_.load(std::memory_order_relaxed); }
+  uint64_t spin_off_ms() const { return spin_off_ms_.load(std::memory_order_relaxed); }
 
   // What the loop thread is doing, published with relaxed stores as it goes, so another
   // thread can say where a loop that stopped answering is: Server::shutdown logs it for a
@@ -137,7 +139,7 @@ class EventLoop {
   bool busy_auto_ = false;
   uint32_t spin_hits_ = 0, spin_misses_ = 0;  // current measurement window
   int64_t spin_off_until_ms_ = 0, spin_backoff_ms_ = 0;
-  std::atomic<uint64_t> spin_hits_total_{0}, spin_misses_total_{0}, spin_offs_{0};
+  std::atomic<uint64_t> spin_hits_total_{0}, spin_misses_total_{0}, spin_offs_{0}, spin_off_ms_{0};
   void note_spin(bool hit);
   alignas(64) Activity act_;  // own cache line: written by the loop thread only
 };

@@ -21,7 +21,7 @@ def run(cmd, port):
 
 def test_bench_one_rank():
     out = run([sys.executable, str(ROOT / "bench.py"), "--steps", "2", "--warmup", "1", "--reqs-per-conn", "100",
-               "--c1-reqs", "3000"], 18800)
+               "--c1-reqs", "3000", "--deployed-seconds", "0", "--chain-seconds", "0", "--chain-shipped-seconds", "0", "--alt-seconds", "0"], 18800)
     for k in KEYS:
         assert k in out
     assert out["metric"] == json.loads((ROOT / "BASELINE.json").read_text())["metric"]
@@ -38,6 +38,48 @@ def test_bench_one_rank():
     # loopback TCP: at least one request and one response segment per request
     if out["tcp_per_req"]:
         assert out["tcp_per_req"]["OutSegs"] >= 1.9
+
+
+def test_bench_auto_steps_and_node_subruns():
+    """--reqs-per-conn 0 (the default): the timed steps are sized from the last warmup step
+    and the JSON says how big they were; at N = 1 the per-node sub-runs report the deployed
+    replica with its host load, the chain engineered and as shipped (fallbacks counted apart,
+    per-hop accept locality, both replicas' busy-poll counters) and the other SMT layout."""
+    out = run([sys.executable, str(ROOT / "bench.py"), "--steps", "2", "--warmup", "2", "--warmup-reqs-per-conn",
+               "200", "--step-seconds", "0.2", "--c1-seconds", "0", "--deployed-seconds", "0.5",
+               "--chain-seconds", "0.5", "--chain-shipped-seconds", "0.5", "--alt-seconds", "0.5"], 18870)
+    per = out["config"]["reqs_per_conn_per_step"]
+    assert per >= 100 and out["requests"] == 64 * per * 2 and out["errors"] == 0
+    assert out["config"]["step_sizing"].startswith("sized from the last warmup step")
+    # the replica's own cores, not its load generator's
+    from hola_amd.utils.cpu import parse_cpu_list, siblings
+    srv = parse_cpu_list(out["config"]["cpu_map"]["rank0"]["server"])
+    assert out["config"]["cores_per_replica"] == len({min(siblings(c)) for c in srv})
+    assert out["deployed_errors"] == 0 and out["deployed_body_checked"] == out["deployed_requests"] > 0
+    assert set(out["deployed_host_load"]) == {"own", "siblings"} and out["deployed_zipkin"] == "deployed"
+    assert out["chain_errors"] == 0 and out["chain_hystrix_fallback"] == 0 and out["chain_pool"] == 128
+    assert set(out["chain_locality"]) == {"loadgen_to_a", "a_to_b"}
+    assert abs(sum(out["chain_locality"]["a_to_b"].values()) - 1.0) < 1e-3
+    assert {"hit", "miss", "backoffs", "backoff_ms"} <= set(out["chain_spins"]["a"])
+    # as shipped: every body is the two-hop answer or A's own fallback, and both are counted
+    assert out["chain_shipped_pool"] == 10 and out["chain_shipped_errors"] == 0
+    assert out["chain_shipped_body_mismatch"] == 0 and 0.0 <= out["chain_shipped_fallback_fraction"] <= 1.0
+    assert "--shutdown-delay-ms 5000" in out["chain_shipped_args"]
+    assert out["chain_shipped_hystrix_success"] + out["chain_shipped_hystrix_fallback"] >= out["chain_shipped_requests"]
+    assert out["alt_smt"] == ("pair" if out["config"]["smt"] == "off" else "off") and out["alt_errors"] == 0
+    assert out["alt_body_checked"] == out["alt_requests"] > 0
+
+
+def test_plan_only_replicas():
+    """--plan-only --replicas N: the plan an N-rank run would use (here on the container's CPUs)."""
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--plan-only", "--replicas", "2", "--gpu-slots", "2"],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    plan = json.loads(r.stdout.strip().splitlines()[-1])
+    assert plan["replicas"] == 2 and len(plan["ranks"]) == 2
+    used = [c for rk in plan["ranks"] for c in rk["server"]]
+    assert len(used) == len(set(used))
+    assert all(rk["server_physical_cores"] >= 1 for rk in plan["ranks"])
 
 
 def test_bench_two_ranks_gloo():
@@ -74,7 +116,7 @@ def test_bench_pipelined():
     """--pipeline 16 (wrk's pipeline.lua): a step still completes connections x reqs-per-conn
     requests, every response is counted and checked, and the setting is recorded."""
     out = run([sys.executable, str(ROOT / "bench.py"), "--steps", "2", "--warmup", "1", "--reqs-per-conn", "160",
-               "--pipeline", "16", "--c1-seconds", "0"], 18860)
+               "--pipeline", "16", "--c1-seconds", "0", "--deployed-seconds", "0", "--chain-seconds", "0", "--chain-shipped-seconds", "0", "--alt-seconds", "0"], 18860)
     assert out["requests"] == 64 * 160 * 2 and out["errors"] == 0 and out["non2xx"] == 0
     assert out["config"]["pipeline"] == 16 and "16 pipelined" in out["data"]
     # 16 requests per segment each way: far fewer than 2 segments per request
@@ -121,3 +163,19 @@ def test_loadgen_conn_targets_pin_connections_to_replicas():
         assert lat["body_mismatch"] == 0 and lat["body_checked"] == lat["count"] > 0
         bad = subprocess.run(cmd[:-4] + ["--conn-targets", "0,2"], capture_output=True, text=True, timeout=60)
         assert bad.returncode == 2 and "out of range" in bad.stderr
+
+
+def test_loadgen_alt_body_counted_apart():
+    """--alt-body: a response equal to an accepted second answer (the shipped chain's Hystrix
+    fallback) is counted in body_alt, not as a mismatch; anything else still is one."""
+    from hola_amd.parallel.loadgen import run_duration
+    from hola_amd.server import HolaProcess
+
+    with HolaProcess(env={"HOSTNAME": "hx"}, threads=1) as s:
+        alt = run_duration([("127.0.0.1", s.port)], 2, 1, 0.3, warmup_s=0.1, expect_bodies=["Hola de hy"],
+                           alt_bodies=["Hola de hz", "Hola de hx"])
+        bad = run_duration([("127.0.0.1", s.port)], 2, 1, 0.3, warmup_s=0.1, expect_bodies=["Hola de hy"],
+                           alt_bodies=["Hola de hz"])
+    assert alt["latency"]["body_mismatch"] == 0 and alt["latency"]["errors"] == 0
+    assert alt["latency"]["body_alt"] == alt["latency"]["body_checked"] == alt["latency"]["count"] > 0
+    assert bad["latency"]["body_alt"] == 0 and bad["latency"]["body_mismatch"] == bad["latency"]["count"] > 0

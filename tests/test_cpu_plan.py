@@ -219,3 +219,35 @@ def test_a_rank_stays_in_one_socket_when_l3_ids_alternate(epyc, monkeypatch):
         epyc[c] = 1.0 if cpu.package_of(c) == 0 else 0.0
     one = cpu.plan_node(1, 16)[0]
     assert {cpu.package_of(c) for c in one} == {1}
+
+
+def test_slot_subset_mirrors_the_node_plan(epyc, monkeypatch):
+    """--slot-cores K: replica r takes the first K physical cores of node slot r, so the
+    miniature's slots sit where the 8-slot node plan puts them (both sockets), each server
+    worker with its load-generator thread on the other SMT thread of its core."""
+    monkeypatch.setattr(cpu, "package_of", lambda c: (c % 128) // 64)
+    node = cpu.plan_node(8, 16, avoid_busy=False)
+    for n in (1, 2, 4, 8):
+        sub = cpu.plan_slot_subset(n, 8, 1, smt="pair")
+        assert len(sub) == n
+        for r, p in enumerate(sub):
+            assert p["server"] == node[r][:1] and p["slot"] == r
+            assert p["loadgen"] == [p["server"][0] + 128]  # the sibling of the server core
+    sockets = {cpu.package_of(p["server"][0]) for p in cpu.plan_slot_subset(8, 8, 1)}
+    assert sockets == {0, 1}
+    off = cpu.plan_slot_subset(2, 8, 2, smt="off", extra_cores=1)
+    for r, p in enumerate(off):
+        assert p["server"] == node[r][:2] and p["loadgen"] == node[r][2:4] and p["extra"] == node[r][4:5]
+    with pytest.raises(ValueError):
+        cpu.plan_slot_subset(1, 8, 16, smt="off")  # 32 cores do not fit a 16-core slot
+
+
+def test_host_load_siblings_exclude_the_job(epyc):
+    """host_load.siblings counts only SMT siblings that no part of the job planned: in pair
+    mode a rank's siblings are other ranks' load-generator threads, not another tenant."""
+    from hola_amd.parallel import subruns
+
+    own = [0, 1]
+    assert subruns.other_siblings(own, []) == {128, 129}
+    assert subruns.other_siblings(own, [128]) == {129}
+    assert subruns.other_siblings(own, [128, 129, 5]) == set()

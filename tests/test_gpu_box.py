@@ -21,7 +21,8 @@ def test_native_module_loaded_from_tree(native):
 @pytest.mark.gpu
 def test_bench_json_contract_on_host():
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--steps", "3", "--warmup", "1",
-                        "--reqs-per-conn", "200", "--c1-seconds", "2", "--chain-seconds", "2"],
+                        "--reqs-per-conn", "200", "--c1-seconds", "2", "--deployed-seconds", "2",
+                        "--chain-seconds", "2", "--chain-shipped-seconds", "2", "--alt-seconds", "2"],
                        capture_output=True, text=True, timeout=600, env={**os.environ, "HOLA_BENCH_PORT": "18700"})
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.strip()]
@@ -52,6 +53,15 @@ def test_bench_json_contract_on_host():
     assert out["chain_hystrix_fallback"] == 0 and out["chain_hystrix_timeout"] == 0
     assert out["chain_hystrix_success"] >= out["chain_requests"]  # its warm-up counts too
     assert out["chain_a_cpu_us_per_req"] > 0
+    # ... with what separates its two modes: host load, per-hop accept locality, spin counters
+    assert set(out["chain_locality"]) == {"loadgen_to_a", "a_to_b"} and out["chain_spins"]["a"]
+    assert set(out["chain_host_load"]) == {"own", "siblings"} and set(out["deployed_host_load"]) == {"own", "siblings"}
+    # ... and as shipped (pool of 10, BASIC logging): every body is the two-hop answer or A's
+    # fallback, the fraction is reported
+    assert out["chain_shipped_pool"] == 10 and out["chain_shipped_body_mismatch"] == 0
+    assert 0.0 <= out["chain_shipped_fallback_fraction"] <= 1.0
+    # ... and the other SMT layout on the rank's cores (BENCH <-> SCALE N = 1)
+    assert out["alt_errors"] == 0 and out["alt_smt"] != out["config"]["smt"] and out["alt_rps"] > 10000
 
 
 @pytest.mark.gpu
@@ -85,7 +95,7 @@ def test_tracing_as_deployed_on_host():
     reach the collector, and the request path does not slow down."""
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--steps", "4", "--warmup", "1",
                         "--reqs-per-conn", "20000", "--c1-seconds", "0", "--deployed-seconds", "0",
-                        "--chain-seconds", "0", "--zipkin-sink"],
+                        "--chain-seconds", "0", "--chain-shipped-seconds", "0", "--alt-seconds", "0", "--zipkin-sink"],
                        capture_output=True, text=True, timeout=600, env={**os.environ, "HOLA_BENCH_PORT": "18720"})
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads(r.stdout.strip().splitlines()[-1])
@@ -101,7 +111,8 @@ def test_pipelined_bench_on_host():
     """`bench.py --pipeline 16` on the real host: 16 requests share each loopback segment."""
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--pipeline", "16", "--steps", "2", "--warmup", "1",
                         "--reqs-per-conn", "16000", "--c1-seconds", "0", "--deployed-seconds", "0",
-                        "--chain-seconds", "0"], capture_output=True, text=True, timeout=300,
+                        "--chain-seconds", "0", "--chain-shipped-seconds", "0", "--alt-seconds", "0"],
+                       capture_output=True, text=True, timeout=300,
                        env={**os.environ, "HOLA_BENCH_PORT": "18780"})
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads(r.stdout.strip().splitlines()[-1])
@@ -149,9 +160,9 @@ def test_manifests_execute_on_host():
     assert res["configmap_edit_all_pods_s"] < 60
 
 
-def _node_plan(slots: int) -> dict:
+def _node_plan(slots: int, replicas: int = 0) -> dict:
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--plan-only", "--gpu-slots", str(slots),
-                        "--ignore-quota"], capture_output=True, text=True, timeout=120)
+                        "--ignore-quota", "--replicas", str(replicas)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr[-2000:]
     return json.loads(r.stdout.strip().splitlines()[-1])
 
@@ -192,6 +203,36 @@ def test_eight_slot_plan_on_the_real_topology():
 
 
 @pytest.mark.gpu
+def test_node_plan_gives_every_n_the_same_replica_shape():
+    """SCALE's weak-scaling curve on the 8-GPU node: at N = 1, 2, 4 and 8 (--plan-only
+    --replicas N, planned on this host's real topology with the quota set aside) every
+    replica gets the same shape: 16 physical cores of server workers, smt=pair, its workers
+    inside one socket, and every load-generator thread on the other SMT thread of a core of
+    the replica it drives."""
+    from hola_amd.utils.cpu import physical_cores
+
+    if len(physical_cores()) < 128:
+        pytest.skip("the 8-slot layout needs the node's 2 x 64 physical cores")
+    shapes = {}
+    for n in (1, 2, 4, 8):
+        plan = _node_plan(8, n)
+        ranks = plan["ranks"]
+        assert plan["replicas"] == n and len(ranks) == n and plan["smt"] == "pair", (n, plan["smt"])
+        used = [c for r in ranks for c in r["server"] + r["loadgen"]]
+        assert len(used) == len(set(used)) == 32 * n, n
+        for i, r in enumerate(ranks):
+            assert r["server_physical_cores"] == 16 and len(r["loadgen"]) == 16, (n, i)
+            assert len(r["server_sockets"]) == 1, (n, i, r["server_sockets"])
+            for t, l_cpu in enumerate(r["loadgen"]):
+                target = ranks[r["thread_targets"][t][0]]
+                assert (set(r["siblings"][str(l_cpu)]) - {l_cpu}) & set(target["server"]), (n, i, t)
+        shapes[n] = plan
+    out = ROOT / "gpurun_out" / "plans_by_n.json"
+    out.parent.mkdir(exist_ok=True)
+    out.write_text(json.dumps(shapes, indent=1))
+
+
+@pytest.mark.gpu
 def test_eight_ranks_run_under_the_node_plan():
     """The N = 8 torchrun command under the 8-slot plan for a couple of tiny steps. Inside
     the box's 16-CPU quota the 256 threads are squeezed, so the throughput means nothing (no
@@ -217,3 +258,7 @@ def test_eight_ranks_run_under_the_node_plan():
     assert out["requests"] == 8 * 64 * 200 * 2
     assert out["errors"] == 0 and out["non2xx"] == 0 and out["body_mismatch"] == 0
     assert out["locality"]["fraction"]["same_core"] >= 0.9, out["locality"]
+    # labels: each replica is 16 physical cores of server workers; its SMT siblings are the
+    # job's own load-generator threads, so no sibling load is charged to other tenants
+    assert out["config"]["cores_per_replica"] == 16 and "16 physical cores" in out["config"]["layout_note"]
+    assert all(h["siblings"] is None for h in out["host_load"]), out["host_load"]
