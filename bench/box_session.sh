@@ -15,6 +15,8 @@
 #   pairmode           N = 1, 2, 4 with --smt pair (the 8-GPU node's per-replica layout shape)
 #   latency            BASELINE config 2 (1 connection) and the open-loop latency curve
 #   chain              two-hop chaining bench (loadgen -> hola A -> hola B)
+#   deployedab REPS [ARGS]  headline replica vs as-deployed (ZIPKIN_SERVER_URL as deployed /
+#                      unset / native sink), interleaved (bench/deployed_ab.py)
 #   chainmodes REPS [ARGS]  bench.py's chain sub-run REPS times per variant with its attribution
 #                      (bench/chain_modes.py; ARGS e.g. --variants lg0,lg20 --seconds 10)
 #   chainab [REPS]     chaining with Feign BASIC logging on/off, this server vs. PREV_BIN
@@ -101,11 +103,7 @@ ab)
   REPS=${1:?reps}; shift
   for rep in $(seq 1 "$REPS"); do
     # AB_SWAP=1: every other round runs the sides in reverse order (the first slot of a round
-    # can be the slow one on this box: profiles/round4/03_chainmodes)
-  REPS=${1:-10}; shift || true
-  timeout -k 10 1000 python -u bench/chain_modes.py --reps "$REPS" --out "$OUT" "$@" > "$OUT/chain_modes.log" 2>&1
-  ;;
-chainab)
+    # can be the slow one on this box: profiles/round4/03_chainab)
     sides=("$@")
     if [ "${AB_SWAP:-0}" = 1 ] && [ $((rep % 2)) = 0 ]; then
       sides=(); for ((k = $#; k >= 1; k--)); do sides+=("${!k}"); done
@@ -158,6 +156,14 @@ latency)
   ;;
 chain)
   timeout -k 10 120 python bench/chain_bench.py --duration 10 --out "$OUT/chain.json" > "$OUT/chain.log" 2>&1
+  ;;
+deployedab)
+  REPS=${1:-4}; shift || true
+  timeout -k 10 1000 python -u bench/deployed_ab.py --reps "$REPS" --out "$OUT" "$@" > "$OUT/deployed_ab.log" 2>&1
+  ;;
+chainmodes)
+  REPS=${1:-10}; shift || true
+  timeout -k 10 1000 python -u bench/chain_modes.py --reps "$REPS" --out "$OUT" "$@" > "$OUT/chain_modes.log" 2>&1
   ;;
 chainab)
   # chaining with A's Feign BASIC logging on (the server default) and off, this tree's server

@@ -187,22 +187,34 @@ def free_port_block(start: int, n: int, host: str = "127.0.0.1") -> int:
 
 def timed_closed_loop(lg: ControlledLoadgen, connections: int, seconds: float, pid: int | None,
                       own, job_cpus, warm_per_conn: int = 2000, max_per_conn: int = 2_000_000) -> dict:
-    """One controlled run sized from a warm-up to last about `seconds`; latency, errors,
-    bodies, the server's CPU per request and the host load of the run."""
+    """A closed-loop run of about `seconds` after a warm-up: controlled runs of ~0.5 s each,
+    each sized from the one before, until `seconds` have passed (the generator's histogram
+    and counters span all of them). Latency, errors, bodies, the server's CPU per request and
+    the host load of the run."""
     warm = lg.run(warm_per_conn)
     rate = warm["requests"] / max(1e-9, warm["elapsed_ns"] / 1e9)
-    per_conn = int(min(max_per_conn, max(2_000, rate * seconds / connections)))
+    if warm["elapsed_ns"] < 300e6:  # a second warm-up of ~0.3 s at the first one's rate
+        warm = lg.run(int(min(max_per_conn, max(warm_per_conn, 0.3 * rate / connections))))
+        rate = warm["requests"] / max(1e-9, warm["elapsed_ns"] / 1e9)
     lg.reset()
     t0, c0 = cpu_times(), proc_cpu_s(pid) if pid else 0.0
-    r = lg.run(per_conn)
+    el_ns = reqs = errs = 0
+    while el_ns < seconds * 1e9:
+        left = seconds - el_ns / 1e9
+        per_conn = int(min(max_per_conn, max(100, rate * min(0.5, left) / connections)))
+        r = lg.run(per_conn)
+        el_ns += r["elapsed_ns"]
+        reqs += r["requests"]
+        errs += r["errors"]
+        rate = r["requests"] / max(1e-9, r["elapsed_ns"] / 1e9)
     t1, c1 = cpu_times(), proc_cpu_s(pid) if pid else 0.0
     st = lg.stats()
-    el = r["elapsed_ns"] / 1e9
-    return {"rps": r["requests"] / el if el > 0 else 0.0, "elapsed_s": el, "requests": r["requests"],
-            "errors": r["errors"], "p50_ns": st["p50_ns"], "p99_ns": st["p99_ns"], "non2xx": st.get("non2xx", 0),
+    el = el_ns / 1e9
+    return {"rps": reqs / el if el > 0 else 0.0, "elapsed_s": el, "requests": reqs,
+            "errors": errs, "p50_ns": st["p50_ns"], "p99_ns": st["p99_ns"], "non2xx": st.get("non2xx", 0),
             "body_checked": st.get("body_checked", 0), "body_mismatch": st.get("body_mismatch", 0),
             "body_alt": st.get("body_alt", 0),
-            "cpu_us_per_req": 1e6 * (c1 - c0) / max(1, r["requests"]) if pid else None,
+            "cpu_us_per_req": 1e6 * (c1 - c0) / max(1, reqs) if pid else None,
             "host_load": host_load(t0, t1, own, job_cpus)}
 
 

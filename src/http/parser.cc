@@ -2,7 +2,9 @@
 
 #include "core/scan.h"
 
+#if defined(__AVX2__)
 #include <immintrin.h>
+#endif
 
 #include <cstring>
 #include <type_traits>
@@ -19,6 +21,9 @@ namespace {
 static_assert(std::is_trivially_copyable_v<Request>);
 const Request kFreshRequest{};
 inline void reset_request(Request* req) {
+#if !defined(__AVX2__)
+  memcpy(static_cast<void*>(req), &kFreshRequest, sizeof(Request));  // portable build (x86-64-v2)
+#else
   constexpr size_t kVec = sizeof(Request) / 32, kTail = sizeof(Request) % 32;
   const auto* src = reinterpret_cast<const unsigned char*>(&kFreshRequest);
   auto* dst = reinterpret_cast<unsigned char*>(req);
@@ -26,6 +31,7 @@ inline void reset_request(Request* req) {
     _mm256_storeu_si256(reinterpret_cast<__m256i*>(dst + 32 * i),
                         _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + 32 * i)));
   if constexpr (kTail > 0) memcpy(dst + 32 * kVec, src + 32 * kVec, kTail);
+#endif
 }
 
 inline char lower(char c) { return (c >= 'A' && c <= 'Z') ? char(c + 32) : c; }
@@ -214,7 +220,9 @@ Parse parse_request(const char* buf, size_t len, Request* req, int* status) {
   // Target: up to the next SP. With 32 bytes of the buffer at hand (within `len`: no read past
   // the data), one AVX2 compare finds the SP, the first '?' and any control byte at once; a
   // target of 32 bytes or more, or one with a control byte, takes the byte loop below, which
-  // decides the same (about 10 instructions per byte of "/api/hola" before).
+  // decides the same (about 10 instructions per byte of "/api/hola" before). A portable
+  // (x86-64-v2) build always takes the byte loop.
+#if defined(__AVX2__)
   if (len - pos - t0 >= 32) {
     const __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(line + t0));
     const uint32_t sp = uint32_t(_mm256_movemask_epi8(_mm256_cmpeq_epi8(v, _mm256_set1_epi8(' '))));
@@ -232,6 +240,7 @@ Parse parse_request(const char* buf, size_t len, Request* req, int* status) {
       }
     }
   }
+#endif
   if (i == t0) {
     for (; i < line_len && line[i] != ' '; ++i) {
       const unsigned char c = (unsigned char)line[i];

@@ -18,6 +18,7 @@
 #include "config/properties.h"
 #include "config/resolver.h"
 #include "http/negotiate.h"
+#include "core/isa.h"
 #include "http/parser.h"
 #include "json/json.h"
 #include "resilience/hystrix.h"
@@ -489,7 +490,13 @@ py::dict inline_function_selftest() {
 }  // namespace
 
 PYBIND11_MODULE(_native, m) {
+  // The module is built at the release -march: on a CPU that lacks it, fail the import with
+  // the reason instead of a SIGILL later (src/core/isa.h).
+  if (const std::string missing = isa::missing_features(); !missing.empty())
+    throw py::import_error(isa::error_line("hola_amd._native"));
   m.doc() = "hola native core (C++20) bindings";
+  m.def("isa_build_level", &isa::build_level);
+  m.def("isa_missing_features", &isa::missing_features);
   m.def("parse_properties", &parse_properties_py, "java.util.Properties.load semantics on UTF-8 bytes");
   m.def("java_format", &java_format_py, "java.lang.String.format subset; bytes or (exception, detail)");
   m.def("java_string_hash", [](const std::string& s) { return config::java_string_hash(s); });
