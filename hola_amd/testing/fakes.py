@@ -85,6 +85,12 @@ class _AlohaHandler(BaseHTTPRequestHandler):
                              b"Transfer-Encoding: chunked\r\n\r\nzz\r\n[]\r\n0\r\n\r\n")
             self.wfile.flush()
             return
+        if mode == "cr_in_name":  # a CR inside a header name: not Transfer-Encoding, must not chunk
+            body = json.dumps(payload).encode()
+            self.wfile.write(b"HTTP/1.1 200 OK\r\nContent-Type: application/json\r\nTransfer\rEncoding: chunked\r\n"
+                             b"Content-Length: %d\r\n\r\n%s" % (len(body), body))
+            self.wfile.flush()
+            return
         if self.path != "/api/aloha-chaining":
             body, status = b"not found", 404
         elif mode == "error":

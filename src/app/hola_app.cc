@@ -38,16 +38,18 @@ struct HolaApp::WorkerCache {
   uint64_t gen = ~0ull;
   uint64_t date_version = ~0ull;
   std::shared_ptr<const Content> content;
-  // The contents of the last configuration generations, kept so that a chaining call parked
-  // across a reload can still answer with the greeting of its own request (it holds a plain
-  // pointer: a shared_ptr copy per call was two locked reference-count operations).
-  std::deque<std::shared_ptr<const Content>> retired;
+  // The contents of the last configuration generations, by generation, kept so that a
+  // chaining call parked across a reload can still answer with the greeting of its own
+  // request. The call holds the generation number, not the content (a shared_ptr copy per call
+  // was two locked reference-count operations) and not its address: once a content is retired
+  // past kRetired and freed, the allocator may hand the same address to the next one.
+  std::deque<std::pair<uint64_t, std::shared_ptr<const Content>>> retired;
   static constexpr size_t kRetired = 8;
-  // The content a call parked with, if still kept; null once it was retired that long ago.
-  const Content* alive(const Content* c) const {
-    if (c == content.get()) return c;
+  // The content of generation `g`, if still kept; null once it was retired that long ago.
+  const Content* alive(uint64_t g) const {
+    if (g == gen) return content.get();
     for (const auto& r : retired)
-      if (r.get() == c) return c;
+      if (r.first == g) return r.second.get();
     return nullptr;
   }
   // [keep_alive][head]
@@ -130,14 +132,13 @@ void HolaApp::on_worker_stop(http::Worker& w) {
 void HolaApp::refresh(http::Worker& w, WorkerCache& wc) {
   uint64_t g = gen_.load(std::memory_order_acquire);
   if (g != wc.gen) {
-    wc.gen = g;
-    // A private copy per worker: every chaining call holds a reference to its worker's
-    // content while it waits, and one control block shared by all workers would bounce its
-    // reference count between their cores on every call.
+    // A private copy per worker: one control block shared by all workers would bounce its
+    // reference count between their cores on every reload.
     if (wc.content) {
-      wc.retired.push_back(std::move(wc.content));
+      wc.retired.emplace_back(wc.gen, std::move(wc.content));
       if (wc.retired.size() > WorkerCache::kRetired) wc.retired.pop_front();
     }
+    wc.gen = g;
     if (auto shared = content()) wc.content = std::make_shared<const Content>(*shared);
     else wc.content = nullptr;
     const Content* c = wc.content.get();
@@ -504,12 +505,12 @@ void HolaApp::handle_chaining(http::Connection& c, const http::Request& r, Worke
   // Async: the connection is parked until aloha answers, times out or is short-circuited.
   c.park();
   http::ConnRef conn(&c);  // held until the callback is gone, run or not
-  const Content* content = wc.content.get();  // kept alive by wc (see WorkerCache::retired)
+  const uint64_t cgen = wc.gen;  // the request's configuration (see WorkerCache::retired)
   HolaApp* self = this;
   chainer_->call(c.worker(), traced ? &span.ctx : nullptr,
-                 // conn is moved in; content is a plain pointer (a shared_ptr copy is two locked
-                 // read-modify-writes per request, each draining the store buffer)
-                 [self, conn = std::move(conn), content, ka_req = ka, head, traced, span, t0](const ChainResult& res) {
+                 // conn is moved in; the content is named by its generation (a shared_ptr copy
+                 // is two locked read-modify-writes per request, each draining the store buffer)
+                 [self, conn = std::move(conn), cgen, ka_req = ka, head, traced, span, t0](const ChainResult& res) {
                    http::Worker& w = conn->worker();
                    // termination may have begun while the call was parked
                    const int ka = ka_req && !w.server().closing() ? 1 : 0;
@@ -530,16 +531,16 @@ void HolaApp::handle_chaining(http::Connection& c, const http::Request& r, Worke
                      // configuration has not changed since the request arrived.
                      if (wc.gen != self->gen_.load(std::memory_order_relaxed) || wc.date_version != w.date_version())
                        self->refresh(w, wc);
-                     if (wc.content.get() == content) {
+                     if (wc.gen == cgen) {
                        conn->complete(wc.chaining_fallback[ka][head].view(), ka);
                        answered = true;
                      }
                    }
-                   if (!answered && !conn->closed() && wc.content.get() == content && !wc.chain_json_prefix.empty()) {
+                   if (!answered && !conn->closed() && wc.gen == cgen && !wc.chain_json_prefix.empty()) {
                      // One allocation: [greeting, ...aloha] written straight into the response.
                      if (wc.gen != self->gen_.load(std::memory_order_relaxed) || wc.date_version != w.date_version())
                        self->refresh(w, wc);
-                     if (wc.content.get() == content) {
+                     if (wc.gen == cgen) {
                        size_t body_len = wc.chain_json_prefix.size() + 1;
                        for (auto& it : res.items) body_len += 1 + (it ? it->size() + 2 : 4);
                        std::string& resp = wc.chain_resp;
@@ -569,7 +570,7 @@ void HolaApp::handle_chaining(http::Connection& c, const http::Request& r, Worke
                    if (!answered && !conn->closed()) {
                      // the configuration changed while the call was parked: the greeting of the
                      // request's own configuration (the current one if that was retired long ago)
-                     const Content* own = wc.alive(content);
+                     const Content* own = wc.alive(cgen);
                      if (!own) own = wc.content.get();
                      std::vector<std::optional<std::string>> items;
                      items.reserve(1 + res.items.size());

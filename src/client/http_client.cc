@@ -125,6 +125,13 @@ constexpr int kTransportRetries = 3;  // DefaultHttpRequestRetryHandler(3, false
 // How long the calls queued behind an abandoned pipelined call wait for its answer before they
 // are re-sent on fresh connections (see ClientPool::cancel).
 constexpr int kDrainGraceMs = 50;
+// Those re-sends draw on a budget (Finagle's and Envoy's retry budgets): each pipelined call
+// sent earns 0.1 of a re-send, up to a burst of 10. Calls are abandoned exactly when aloha is
+// slower than the Hystrix timeout, and every re-send is a second GET to a downstream that is
+// probably still working on the first, so without a bound the load on aloha would grow as it
+// slows. Over budget, the calls stay on their connection until their answers arrive or their
+// own deadlines abandon them; at most ~10 % more requests reach aloha.
+constexpr double kHolResendPerCall = 0.1, kHolResendBurst = 10.0;
 
 struct ClientPool::Conn final : EventLoop::Handler {
   enum State { kConnecting, kWriting, kReading, kIdle, kDead };
@@ -261,21 +268,38 @@ namespace {
 // One response from the front of `in`: 1 = complete (*consumed bytes; *close when the
 // connection cannot carry another response), 0 = need more, -1 = malformed. *head_ok is set
 // once a well-formed status line and header block have arrived.
-// Header name (before the colon) against a lower-case literal, a word at a time with a case
-// fold (letters, digits and '-' are fixed by OR 0x20; see http::parser's name_is).
+// Header name (before the colon) against a lower-case literal, a word at a time: letters
+// compare case-insensitively (OR 0x20 at their positions only), every other byte exactly. A
+// fold of every byte would also map CR (0x0d) onto '-' and control bytes onto digits, and
+// the client does not check response header names for token characters first, so
+// "Content\rLength" must not read as Content-Length. The words and fold masks are built at
+// compile time from the literal (the last word overlaps the one before it, as read).
 template <size_t N>
-inline bool field_is(std::string_view k, const char (&lit)[N]) {
-  constexpr size_t n = N - 1;
-  if (k.size() != n) return false;
-  auto word = [](const char* q, size_t m) {
-    uint64_t w = 0;
-    memcpy(&w, q, m);
-    return w;
-  };
-  constexpr uint64_t kFold = 0x2020202020202020ull;
-  for (size_t off = 0; off + 8 < n; off += 8)
-    if ((word(k.data() + off, 8) | kFold) != word(lit + off, 8)) return false;
-  return (word(k.data() + n - 8, 8) | kFold) == word(lit + n - 8, 8);
+struct FieldName {
+  static_assert(N - 1 >= 8, "names of 8 bytes or more");
+  static constexpr size_t n = N - 1;
+  static constexpr size_t kWords = (n + 7) / 8;
+  uint64_t word[kWords] = {}, fold[kWords] = {};
+  static constexpr size_t offset(size_t w) { return w + 1 < kWords ? 8 * w : n - 8; }
+  constexpr FieldName(const char (&lit)[N]) {
+    for (size_t w = 0; w < kWords; ++w)
+      for (size_t i = 0; i < 8; ++i) {
+        const char c = lit[offset(w) + i];
+        word[w] |= uint64_t((unsigned char)c) << (8 * i);
+        if (c >= 'a' && c <= 'z') fold[w] |= uint64_t(0x20) << (8 * i);
+      }
+  }
+};
+
+template <FieldName F>
+inline bool field_is(std::string_view k) {
+  if (k.size() != F.n) return false;
+  for (size_t w = 0; w < F.kWords; ++w) {
+    uint64_t x;
+    memcpy(&x, k.data() + F.offset(w), 8);
+    if ((x | F.fold[w]) != F.word[w]) return false;
+  }
+  return true;
 }
 
 int parse_response(std::string_view in, bool eof, ClientResult* r, bool* close, size_t* consumed, bool* head_ok) {
@@ -321,7 +345,7 @@ int parse_response(std::string_view in, bool eof, ClientResult* r, bool* close, 
     while (!v.empty() && (v.front() == ' ' || v.front() == '\t')) v.remove_prefix(1);
     switch (k.size()) {
       case 14:
-        if (field_is(k, "content-length")) {
+        if (field_is<"content-length">(k)) {
           cl = 0;
           for (char d : v) {
             if (d < '0' || d > '9') break;
@@ -331,16 +355,16 @@ int parse_response(std::string_view in, bool eof, ClientResult* r, bool* close, 
         }
         break;
       case 17:
-        if (field_is(k, "transfer-encoding") && v.find("chunked") != std::string_view::npos) chunked = true;
+        if (field_is<"transfer-encoding">(k) && v.find("chunked") != std::string_view::npos) chunked = true;
         break;
       case 10:
-        if (field_is(k, "connection")) {
+        if (field_is<"connection">(k)) {
           if (http::iequals(v, "close")) conn_close = true;
           else if (http::iequals(v, "keep-alive")) conn_close = false;
         }
         break;
       case 11:
-        if (field_is(k, "retry-after")) has_retry_after = parse_retry_after(v, wall_us() / 1000, &retry_after_ms);
+        if (field_is<"retry-after">(k)) has_retry_after = parse_retry_after(v, wall_us() / 1000, &retry_after_ms);
         break;
       default:
         break;
@@ -796,10 +820,19 @@ void ClientPool::check_head_of_line(PConn* c) {
     PConn* pc = *it;
     pc->drain_timer = false;
     if (pc->dead || pc->q.empty()) return;
-    if (pc->q.front().abandoned)
-      pfail(pc, "NoHttpResponseException: the answer ahead on a pipelined connection did not come");
-    else
+    if (!pc->q.front().abandoned) {
       check_head_of_line(pc);
+      return;
+    }
+    const double behind = double(std::count_if(pc->q.begin(), pc->q.end(), [](const PConn::Pending& p) {
+      return !p.abandoned && p.cb;
+    }));
+    if (behind > hol_budget_) {  // over the re-send budget: keep waiting on this connection
+      check_head_of_line(pc);
+      return;
+    }
+    hol_budget_ -= behind;
+    pfail(pc, "NoHttpResponseException: the answer ahead on a pipelined connection did not come");
   });
 }
 
@@ -841,6 +874,7 @@ bool ClientPool::get_pipelined(uint64_t id, std::string& req, Callback& cb) {
       }
   if (!c && !(c = open_pconn())) return false;
   const uint64_t serial = next_serial_++;
+  hol_budget_ = std::min(kHolResendBurst, hol_budget_ + kHolResendPerCall);
   c->out += req;
   c->q.push_back({id, serial, std::move(req), std::move(cb)});
   pactive_[id] = {c, serial};

@@ -196,6 +196,7 @@ class ClientPool {
   void flush_dirty();
   void pdestroy(PConn* c);
   void check_head_of_line(PConn* c);
+  double hol_budget_ = 10.0;     // head-of-line re-sends available (kHolResendBurst at start)
   uint64_t next_cid_ = 1;
   // Ends a pipelined connection. The request `failed` (if any: timed out, or answered with a
   // malformed or truncated response) fails with `why` (`failed_retryable` = no valid response

@@ -123,6 +123,12 @@ bool need(int i, int argc, const char* flag) {
 // See the exit watchdog in main(): the time a termination may take beyond the shutdown delay
 // and the drain budget (the reporter's last span export alone may take its 2 s timeout).
 constexpr int64_t kExitMarginMs = 10000;
+// What the watchdog's report may take (main's stack: 200 ms capture; each worker: a 100 ms
+// pass window and a 2 s budget for the stacks): the watchdog starts that much before the
+// deadline, so the process has exited with status 3 by the deadline itself and a kubelet
+// SIGKILL timed to it (--exit-deadline-ms = terminationGracePeriodSeconds) cannot cut the
+// report short. A deadline under twice the budget starts the report half way instead.
+constexpr int64_t kExitReportBudgetMs = 2500;
 
 namespace {
 // The termination step main is in, for the exit watchdog's report (a string literal).
@@ -435,13 +441,16 @@ int main(int argc, char** argv) {
     const int64_t limit_ms = exit_deadline_ms >= 0 ? exit_deadline_ms
                                                    : int64_t(shutdown_delay_ms) + std::max(0, drain_ms) + kExitMarginMs;
     const int main_tid = cpuprof::current_tid();
-    if (limit_ms > 0) std::thread([limit_ms, &server, main_tid] {
-      std::this_thread::sleep_for(std::chrono::milliseconds(limit_ms));
+    const int64_t report_ms = limit_ms > 2 * kExitReportBudgetMs ? limit_ms - kExitReportBudgetMs : limit_ms / 2;
+    if (limit_ms > 0) std::thread([limit_ms, report_ms, &server, main_tid] {
+      std::this_thread::sleep_for(std::chrono::milliseconds(report_ms));
       std::lock_guard<std::mutex> g(g_watchdog_mu);
       if (g_terminated) return;
-      char line[160];
-      const int n = snprintf(line, sizeof line, "hola: termination did not complete within %lld ms; exiting\n",
-                             (long long)limit_ms);
+      char line[200];
+      const int n = snprintf(line, sizeof line,
+                             "hola: termination did not complete within %lld ms; exiting (exit deadline %lld ms, "
+                             "less the report's budget)\n",
+                             (long long)report_ms, (long long)limit_ms);
       ssize_t w = ::write(2, line, size_t(n));
       // where main is (the termination step and its stack), then every event loop, with its
       // stack (the report that names a stuck handler)

@@ -49,6 +49,16 @@ def test_chunked_response(hola, aloha, mode):
         assert chain(s)[1:] == ["Aloha mai aloha-1", "Bonjour de bonjour-1"]
 
 
+def test_header_name_with_a_cr_is_not_a_known_field(hola, aloha):
+    """the client's case fold must not map CR onto '-': "Transfer\rEncoding:
+    chunked" is some other header, so the Content-Length body is read as is (a chunked
+    decode of it would fail and fall back)."""
+    aloha.set_mode("cr_in_name")
+    s = hola(args=["--aloha-url", aloha.url, "--no-tracing", "--feign-log", "none"], env={"HOSTNAME": "h"})
+    for _ in range(2):
+        assert chain(s) == ["Hola de h", "Aloha mai aloha-1", "Bonjour de bonjour-1"]
+
+
 def _events(s) -> dict:
     """Rolling Hystrix event counts of the aloha command from /metrics."""
     _, _, body = s.get("/metrics")
@@ -779,6 +789,33 @@ def test_pipelined_mode_keeps_no_idle_plain_connections(hola, aloha):
     assert fds() <= base + 4, (base, fds())
 
 
+def test_uniformly_slow_aloha_gets_bounded_head_of_line_resends(hola, aloha):
+    """aloha uniformly slower than the Hystrix timeout with --aloha-pipeline 8. A call
+    is abandoned at its timeout; calls queued behind it on its pipelined connection with later
+    deadlines would all be re-sent 50 ms later, second GETs to a downstream still working on
+    the first, growing the load as it slows. The re-sends draw on a budget of 0.1 per call
+    (burst 10): the requests reaching aloha stay near one per call."""
+    aloha.set_mode("slow", delay_s=0.3)
+    s = hola(args=["--aloha-url", aloha.url, "--no-tracing", "--feign-log", "none", "--aloha-pipeline", "8",
+                   "--feign-retry", "off", "--hystrix-timeout-ms", "200", "-Dhystrix.threadpool.default.coreSize=64",
+                   "-Dhystrix.command.default.circuitBreaker.enabled=false"], env={"HOSTNAME": "h"}, threads=1)
+    calls = 0
+    for _ in range(12):
+        # one call, then 7 more 70 ms later on the same pipelined connection: their deadlines
+        # fall after the head's timeout plus the 50 ms grace, while its answer is still due
+        head = threading.Thread(target=lambda: s.get("/api/hola-chaining", timeout=10))
+        head.start()
+        time.sleep(0.07)
+        res = _concurrent_chains(s, 7)
+        head.join()
+        assert all(st == 200 and body == ["Hola de h", FALLBACK] for st, body in res), res
+        calls += 8
+    time.sleep(0.5)  # re-sends still in flight land in aloha's count
+    resent = _retries(s).get("transport", 0)
+    assert resent <= 10 + 0.1 * calls + 7, (resent, calls)
+    assert len(aloha.requests) <= calls + 10 + 0.1 * calls + 7, (len(aloha.requests), calls)
+
+
 def _retries(s) -> dict:
     out = {}
     for line in s.get("/metrics")[2].decode().splitlines():
@@ -943,7 +980,7 @@ def test_a_call_parked_across_a_reload_answers_with_its_own_greeting(hola, aloha
     """The greeting is computed when the request arrives (HolaResource.java:75): a chaining
     call still waiting on aloha while the greeting file changes answers with the greeting of
     its own request, and the next request gets the new one. (The worker keeps the contents of
-    the last configuration generations for such calls; the call holds a plain pointer.)"""
+    the last configuration generations for such calls; the call holds its generation.)"""
     conf = tmp_path / "t.properties"
     conf.write_text("hello=old %s\n")
     aloha.set_mode("slow_once", delay_s=2.0)
@@ -962,3 +999,27 @@ def test_a_call_parked_across_a_reload_answers_with_its_own_greeting(hola, aloha
     t.join(timeout=10)
     assert parked["r"] == ["old h", "Aloha mai aloha-1", "Bonjour de bonjour-1"], parked
     assert chain(s) == ["new h", "Aloha mai aloha-1", "Bonjour de bonjour-1"]
+
+
+def test_a_call_parked_across_many_reloads_answers_with_the_current_greeting(hola, aloha, tmp_path):
+    """past the 8 kept generations a parked call's own content is gone; it answers
+    with the current greeting (it names its content by generation, so a new content that
+    reuses a freed one's address cannot pass for it)."""
+    conf = tmp_path / "t.properties"
+    conf.write_text("hello=g0 %s\n")
+    aloha.set_mode("slow_once", delay_s=4.0)
+    s = hola(args=[f"-Dconf={conf}", "--aloha-url", aloha.url, "--no-tracing", "--feign-log", "none",
+                   "--config-poll-ms", "50", "-Dhystrix.command.default.execution.isolation.thread.timeoutInMilliseconds=9000"],
+             env={"HOSTNAME": "h"}, threads=1)
+    parked = {}
+    t = threading.Thread(target=lambda: parked.update(r=chain(s)), daemon=True)
+    t.start()
+    time.sleep(0.3)
+    for k in range(1, 11):  # ten reloads, each seen by the worker before the next
+        conf.write_text(f"hello=g{k} %s\n")
+        deadline = time.monotonic() + 3
+        while s.get("/api/hola")[2] != f"g{k} h".encode() and time.monotonic() < deadline:
+            time.sleep(0.02)
+        assert s.get("/api/hola")[2] == f"g{k} h".encode()
+    t.join(timeout=15)
+    assert parked["r"] == ["g10 h", "Aloha mai aloha-1", "Bonjour de bonjour-1"], parked
