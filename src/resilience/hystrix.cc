@@ -285,6 +285,11 @@ void Command::apply_hot(const Settings& s) {
   health_ms_.store(s.health_snapshot_ms, std::memory_order_relaxed);
 }
 
+void Command::hold_shard_for_test(int i, const std::function<void()>& while_held) {
+  std::lock_guard<ShardLock> l(shards_[size_t(i) % shards_.size()]->mu);
+  while_held();
+}
+
 Command::Shard& Command::shard() {
   // Threads are dealt shards round-robin on first use: one event-loop worker per shard up
   // to kShards workers, so shard mutexes are in practice uncontended.

@@ -27,6 +27,7 @@
 #include <deque>
 #include <map>
 #include <memory>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -197,6 +198,10 @@ class Command {
   void update_settings(const Settings& s);
   Settings settings();
   const std::string& name() const { return name_; }
+  // Tests (bench/probes/hystrix_shard_race.cc under TSan): runs `while_held` with shard `i`'s
+  // lock held, as a worker's finish() holds it, so that refreshes and other workers' calls
+  // can be driven against a held shard.
+  void hold_shard_for_test(int i, const std::function<void()>& while_held);
 
  private:
   struct Shard;

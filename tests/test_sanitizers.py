@@ -334,3 +334,26 @@ def test_sanitized_exit_watchdog_stall_report(preset, tmp_path):
     assert "AddressSanitizer" not in log and "runtime error" not in log, log[-6000:]
     assert rc == 3, (rc, log[-3000:])
     assert log.count("hola: worker ") == 4 and "hola: main: shutdown delay" in log, log[-3000:]
+
+
+@pytest.mark.parametrize("preset", ["release", "tsan", "asan"])
+def test_hystrix_shard_lock_held_while_refreshes_and_finishes_run(preset):
+    """one Hystrix shard's test-and-set lock (released with a plain release
+    store) held over and over while eight workers run try_start / complete / circuit_open with
+    a health snapshot refreshed on every call (each refresh walks every shard and meets the
+    held one) and a reader takes snapshots: no sanitizer report, no deadlock, and the event
+    totals add up (bench/probes/hystrix_shard_race.cc)."""
+    import subprocess
+
+    build(preset)
+    exe = build_dir(preset) / "hola_hystrix_race"
+    wrapper = tsan_wrapper() if preset == "tsan" else []
+    env = {**os.environ, **SAN_ENV.get(preset, {})}
+    r = subprocess.run([*wrapper, str(exe), "--iters", "20000" if preset == "release" else "4000"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert "ThreadSanitizer" not in r.stderr and "AddressSanitizer" not in r.stderr, r.stderr[-6000:]
+    assert "runtime error" not in r.stderr, r.stderr[-3000:]
+    assert r.returncode == 0, (r.returncode, r.stdout, r.stderr[-3000:])
+    import json
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["success"] + out["failure"] == out["started"] > 0 and out["holds"] > 0
