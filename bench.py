@@ -19,7 +19,8 @@ greeting of the replica behind its connection (a mismatch is an error).
 
 After the timed region rank 0 runs BASELINE config 2 (one connection, 30 s; c1_* keys), and at
 N = 1 the per-node sub-runs of hola_amd/parallel/subruns.py: the as-deployed replica (the
-image's ENTRYPOINT + the manifests' args and env; deployed_*), GET /api/hola-chaining
+image's ENTRYPOINT + the manifests' args and env: `--shutdown-delay-ms 5000 --busy-poll-us
+auto`, ZIPKIN_SERVER_URL set; deployed_*), GET /api/hola-chaining
 engineered (chain_*) and as shipped (pool of 10, Feign BASIC logging; chain_shipped_*), and
 the headline in the other SMT layout (alt_*: BENCH and SCALE's N = 1 each carry the other's
 figure). The JSON also carries span accounting (`tracing`, with a native collector under

@@ -54,4 +54,41 @@ def test_bench_describes_the_deployed_replica_as_it_runs():
         assert f"`{p}" in flat or f"{p}`" in flat or p in flat, (p, flat)
     assert "no busy-polling" not in bench and "no busy polling" not in bench
     # the key comment next to deployed_* in the JSON
-    assert all(p in " ".join(bench.split("**_deployed_keys(deployed)")[0].split()[-40:]) for p in pairs)
+    assert all(p in " ".join(bench.split("**_deployed_keys(")[0].split()[-40:]) for p in pairs)
+
+
+def _tracked(*paths):
+    import subprocess
+
+    r = subprocess.run(["git", "ls-files", *paths], cwd=ROOT, capture_output=True, text=True)
+    if r.returncode != 0:
+        import pytest
+        pytest.skip("not a git checkout")
+    return r.stdout.split()
+
+
+def test_every_profile_path_the_docs_name_exists():
+    """Numbers in the READMEs and docs point at profile sessions (`profiles/roundN/...`, or
+    relative inside profiles/): each path named must still be in the tree after the per-run
+    files were folded into tables (bench/fold_profiles.py)."""
+    skip = {"SURVEY.md", "VERDICT.md", "ADVICE.md", "PAPERS.md", "SNIPPETS.md", "BASELINE.md"}
+    missing = []
+    for rel in _tracked("*.md"):
+        md = ROOT / rel
+        if md.name in skip:
+            continue
+        text = md.read_text(errors="replace")
+        for m in re.finditer(r"`([^`\s]+)`|\(([^)\s]+)\)", text):
+            tok = (m.group(1) or m.group(2)).strip("`").rstrip(".,:;").split("#")[0]
+            if "://" in tok or "round" not in tok:
+                continue
+            if not re.match(r"^(\.\./)*(profiles/)?round\d|^(\.\./)*\d\d_|^(\.\./)*r\d+_", tok):
+                continue
+            if not any(p.exists() for p in (md.parent / tok, ROOT / tok, ROOT / "profiles" / tok)):
+                missing.append((rel, tok))
+    assert not missing, missing
+
+
+def test_profiles_stay_folded():
+    """VERDICT r4 #7: raw per-run files are folded into tables; the tree keeps < 400 of them."""
+    assert len(_tracked("profiles")) < 400
