@@ -526,12 +526,13 @@ def _plan(a, n: int, avoid_busy: bool = True) -> dict:
     gets only the first K cores of its node slot (plan_slot_subset)."""
     slots = max(n, a.gpu_slots or _gpu_slots())
     if a.slot_cores:
-        smt = "off" if a.smt == "off" else "pair"
+        sub = plan_slot_subset(n, slots, a.slot_cores, a.smt if a.smt in ("off", "pair") else "auto")
+        smt = sub[0]["smt"]
         cores = [{"server": p["server"], "loadgen": p["loadgen"], "thread_targets": [[r]] * len(p["loadgen"]),
                   "dealing": "round-robin over the replicas: each client thread drives the replica whose worker "
                              "shares its physical core (the node plan's per-connection placement)" if smt == "pair"
                              else "each client thread drives the replica in its own node slot"}
-                 for r, p in enumerate(plan_slot_subset(n, slots, a.slot_cores, smt))]
+                 for r, p in enumerate(sub)]
         return {"cores": cores, "smt": smt, "gpu_slots": slots, "cores_per_slot": a.slot_cores}
     per_rank = min(a.cores or slot_cores(slots), max(1, cpu_budget() // n))
     smt = a.smt

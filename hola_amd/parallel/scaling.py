@@ -1,6 +1,15 @@
 """Replica scaling curve for GET /api/hola on one node (BASELINE.json configs 2-4).
 
     python -m hola_amd.parallel.scaling --replicas 1,2,4,8 --duration 10 [--lb client|proxy|reuseport]
+    python -m hola_amd.parallel.scaling --slot-cores 1 --slots 8 --lb client|reuseport|proxy
+
+With ``--slot-cores K`` the plan is a miniature of the 8-GPU node's (``--slots``): replica k
+runs on the first K physical cores of node slot k, placed where the node plan puts the slot
+(both sockets), one server worker per core and the load-generator thread that drives it on
+the core's other SMT thread; with ``--lb proxy`` the proxy gets K more physical cores of the
+same slot (both SMT threads). Each N then gets exactly N times the resources of N = 1, so
+the weak-scaling efficiency total(N) / (N x total(1)) is measurable inside a small CPU quota.
+It is not the 8-GPU node's curve (16 cores per slot there).
 
 For each replica count N the host CPU budget is split into disjoint core sets: one per
 replica (server event loops) plus one for the load generator (and the proxy, with
@@ -18,7 +27,7 @@ import time
 from hola_amd.parallel.loadgen import run_duration
 from hola_amd.parallel.replicas import ReplicaSet, RRProxy
 from hola_amd.utils.cpu import (cgroup_cpu_quota, cpu_budget, format_cpu_list, plan_mirrored, plan_node,
-                                split_server_loadgen)
+                                plan_slot_subset, sibling_of, split_server_loadgen)
 
 
 def plan(n_replicas: int, budget: int, server_share: float, proxy_threads: int) -> dict:
@@ -66,9 +75,27 @@ def plan_proxied(n_replicas: int, budget: int) -> dict:
     return {"replicas": replicas, "proxy": m["proxy"], "loadgen": m["loadgen"]}
 
 
+def plan_slots(n: int, k: int, slots: int, lb: str) -> dict:
+    """The miniature node plan (see the module docstring): replicas on slot cores, load
+    generator thread t on the sibling of replica (t % n)'s core t // n (connection i runs on
+    thread i % T against target i % n, so thread t drives replica t % n), proxy threads on
+    both SMT threads of the slot's next k cores."""
+    sub = plan_slot_subset(n, slots, k, "auto", extra_cores=k if lb == "proxy" else 0)
+    load = [sub[t % n]["loadgen"][t // n] for t in range(n * k)]
+    proxy = []
+    for p in sub:
+        for c in p["extra"]:
+            proxy += [c] + ([sibling_of(c)] if sibling_of(c) is not None else [])
+    return {"replicas": [p["server"] for p in sub], "proxy": proxy, "loadgen": load,
+            "slots": [p["slot"] for p in sub], "smt": sub[0]["smt"] if sub else "pair"}
+
+
 def run_point(n: int, args) -> dict:
     budget = args.budget or cpu_budget()
-    if args.lb == "proxy" and not args.proxy_threads:
+    if args.slot_cores:
+        p = plan_slots(n, args.slot_cores, args.slots, args.lb)
+        proxy_threads = len(p["proxy"])
+    elif args.lb == "proxy" and not args.proxy_threads:
         p = plan_proxied(n, budget)
         proxy_threads = len(p["proxy"])
     else:
@@ -76,8 +103,11 @@ def run_point(n: int, args) -> dict:
         p = plan(n, budget, args.server_share, proxy_threads)
     conns = args.connections_per_replica * n if args.mode == "weak" else args.connections
     extra = ["--no-tracing"] if args.no_tracing else []
-    if args.busy_poll_us:
-        extra += ["--busy-poll-us", str(args.busy_poll_us)]
+    server_bp = args.server_busy_poll or (str(args.busy_poll_us) if args.busy_poll_us else "")
+    if server_bp and server_bp != "0":
+        extra += ["--busy-poll-us", server_bp]
+        if args.busy_poll_pause:
+            extra += ["--busy-poll-pause", str(args.busy_poll_pause)]
     shared = 0 if args.lb == "reuseport" else None
     with ReplicaSet(n, cpu_plan=p["replicas"], args=extra, supervise=False, shared_port=shared) as rs:
         if args.lb == "proxy":
@@ -86,11 +116,13 @@ def run_point(n: int, args) -> dict:
                          exe=args.proxy_exe or None) as px:
                 targets = [("127.0.0.1", px.port)]
                 res = run_duration(targets, conns, len(p["loadgen"]), args.duration, args.warmup,
-                                   cpu_list=",".join(map(str, p["loadgen"])), busy_poll_us=args.busy_poll_us)
+                                   cpu_list=",".join(map(str, p["loadgen"])), busy_poll_us=args.busy_poll_us,
+                                   busy_poll_pause=args.busy_poll_pause)
         else:
             # client-side round-robin: one target per replica, so each target's body is fixed
             res = run_duration(rs.targets, conns, len(p["loadgen"]), args.duration, args.warmup,
                                cpu_list=",".join(map(str, p["loadgen"])), busy_poll_us=args.busy_poll_us,
+                               busy_poll_pause=args.busy_poll_pause,
                                verify_body=args.lb == "client")
     lat = res["latency"]
     return {
@@ -100,6 +132,8 @@ def run_point(n: int, args) -> dict:
         "cpu_map": {"replicas": [format_cpu_list(c) for c in p["replicas"]], "proxy": format_cpu_list(p["proxy"]),
                     "loadgen": format_cpu_list(p["loadgen"])},
         "budget": budget, "quota": cgroup_cpu_quota(), "duration_s": args.duration,
+        **({"slot_cores": args.slot_cores, "node_slots": p["slots"], "layout": f"miniature node plan ({p['smt']})"}
+           if args.slot_cores else {}),
     }
 
 
@@ -120,6 +154,13 @@ def main(argv=None) -> int:
     ap.add_argument("--proxy-exe", default="", help="alternative hola_rrproxy binary (A/B runs)")
     ap.add_argument("--busy-poll-us", type=int, default=0,
                     help="busy-poll window of the replicas, the load generator and the proxy")
+    ap.add_argument("--server-busy-poll", default="",
+                    help="the replicas' own --busy-poll-us (N, auto, auto:N); default --busy-poll-us")
+    ap.add_argument("--busy-poll-pause", type=int, default=0,
+                    help="PAUSE instructions between empty polls (replicas and load generator)")
+    ap.add_argument("--slot-cores", type=int, default=0,
+                    help="miniature node plan: K physical cores per replica at the node slots' places")
+    ap.add_argument("--slots", type=int, default=8, help="node slots of the miniature plan (GPUs on the node)")
     ap.add_argument("--proxy-busy-poll-us", type=int, default=-1, help="-1 = --busy-poll-us")
     ap.add_argument("--budget", type=int, default=0, help="CPUs to use (default: cgroup quota / affinity)")
     ap.add_argument("--server-share", type=float, default=0.5)
@@ -130,15 +171,21 @@ def main(argv=None) -> int:
     for n in [int(x) for x in args.replicas.split(",")]:
         row = run_point(n, args)
         rows.append(row)
+        if args.slot_cores and rows[0]["rps"]:  # weak scaling: N times the N = 1 resources
+            row["efficiency"] = round(row["rps"] / (rows[0]["rps"] * n / rows[0]["replicas"]), 4)
         print(json.dumps(row), flush=True)
         time.sleep(0.5)
     base = rows[0]["rps"] if rows else 0
-    table = ["| replicas | connections | LB | req/s | p50 ms | p99 ms | total vs N=1 (same CPU budget) |",
+    weak = bool(args.slot_cores)
+    table = ["| replicas | connections | LB | req/s | p50 ms | p99 ms | " +
+             ("efficiency = total / (N x N=1) |" if weak else "total vs N=1 (same CPU budget) |"),
              "|---|---|---|---|---|---|---|"]
     for r in rows:
-        eff = r["rps"] / base if base else 0
+        eff = r["rps"] / (base * (r["replicas"] / rows[0]["replicas"] if weak else 1)) if base else 0
+        if not weak:
+            r["vs_first"] = round(eff, 4)
         table.append(f"| {r['replicas']} | {r['connections']} | {r['lb']} | {r['rps']:.0f} | {r['p50_ms']:.3f} | "
-                     f"{r['p99_ms']:.3f} | {eff:.2f} |")
+                     f"{r['p99_ms']:.3f} | {eff:.3f} |")
     print("\n".join(table))
     if args.out:
         with open(args.out, "w") as f:

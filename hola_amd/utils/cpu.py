@@ -326,9 +326,12 @@ def plan_slot_subset(n: int, slots: int, k: int, smt: str = "pair", extra_cores:
     load-generator thread that drives it on the other (the node plan's per-connection
     placement), with smt=off the next `k` cores of the slot carry the load generator.
     `extra_cores` more physical cores of the same slot are returned as "extra" (e.g. proxy
-    threads). Per replica: {"server", "loadgen", "extra", "slot"}."""
+    threads); smt=auto is pair when the cores have SMT siblings, else off. Per replica:
+    {"server", "loadgen", "extra", "slot", "smt"}."""
     phys = physical_cores()
     per = max(1, len(phys) // max(1, slots))
+    if smt == "auto":  # pair where every core has an SMT sibling (not in a container without SMT)
+        smt = "pair" if all(sibling_of(c) is not None for c in phys) else "off"
     need = k * (1 if smt == "pair" else 2) + extra_cores
     if per < need:
         raise ValueError(f"a slot has {per} physical cores, {need} needed")
@@ -344,7 +347,8 @@ def plan_slot_subset(n: int, slots: int, k: int, smt: str = "pair", extra_cores:
             rest = cores[k:]
         else:
             ld, rest = cores[k:2 * k], cores[2 * k:]
-        out.append({"server": list(srv), "loadgen": list(ld), "extra": list(rest[:extra_cores]), "slot": r % slots})
+        out.append({"server": list(srv), "loadgen": list(ld), "extra": list(rest[:extra_cores]), "slot": r % slots,
+                    "smt": smt})
     return out
 
 

@@ -179,3 +179,35 @@ def test_loadgen_alt_body_counted_apart():
     assert alt["latency"]["body_mismatch"] == 0 and alt["latency"]["errors"] == 0
     assert alt["latency"]["body_alt"] == alt["latency"]["body_checked"] == alt["latency"]["count"] > 0
     assert bad["latency"]["body_alt"] == 0 and bad["latency"]["body_mismatch"] == bad["latency"]["count"] > 0
+
+
+def test_bench_slot_cores_miniature_two_ranks():
+    """--slot-cores 1: each rank runs on the first physical core of its node slot (the
+    miniature weak-scaling layout), and the JSON says so rather than passing for the node's."""
+    out = run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+               "--master-addr", "127.0.0.1", "--master-port", "29565", str(ROOT / "bench.py"), "--gpus", "2",
+               "--gpu-slots", "4", "--slot-cores", "1", "--steps", "2", "--warmup", "1", "--reqs-per-conn", "50",
+               "--c1-seconds", "0"], 18880)
+    assert out["n_gpus"] == 2 and out["errors"] == 0 and out["requests"] == 2 * 64 * 50 * 2
+    c = out["config"]
+    assert c["cores_per_replica"] == 1 and c["physical_cores_per_slot"] == 1
+    assert "Miniature layout (--slot-cores 1)" in c["layout_note"] and "not the 8-GPU node's curve" in c["layout_note"]
+
+
+def test_scaling_miniature_weak_efficiency():
+    """hola_amd.parallel.scaling --slot-cores: N = 1 and 2 on the miniature plan, every LB mode;
+    the table reports total / (N x N=1)."""
+    import contextlib
+    import io
+
+    from hola_amd.parallel import scaling
+
+    for lb in ("client", "reuseport", "proxy"):
+        buf = io.StringIO()
+        with contextlib.redirect_stdout(buf):
+            scaling.main(["--slot-cores", "1", "--slots", "2", "--replicas", "1,2", "--lb", lb, "--duration", "0.4",
+                          "--warmup", "0.1"])
+        rows = [json.loads(l) for l in buf.getvalue().splitlines() if l.startswith("{")]
+        assert [r["replicas"] for r in rows] == [1, 2] and all(r["errors"] == 0 for r in rows), rows
+        assert rows[0]["efficiency"] == 1.0 and rows[1]["efficiency"] > 0 and rows[1]["slot_cores"] == 1
+        assert "efficiency = total / (N x N=1)" in buf.getvalue()
