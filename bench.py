@@ -672,6 +672,7 @@ def _chain_keys(c: dict | None, p: str) -> dict:
            f"{p}_locality": c["locality"],
            # adaptive busy-polling of A and B: spins that found work / ran out, back-offs, ms backed off
            f"{p}_spins": c["spins"], f"{p}_loadgen_busy_poll_us": c["loadgen_busy_poll_us"],
+           f"{p}_cgroup_throttle": c["cgroup_throttle"],
            f"{p}_cpus": c["cpus"], f"{p}_pool": c["pool"]}
     if c.get("shipped"):
         # the timed responses that were A's own fallback (the pool of 10 or an open circuit)

@@ -48,11 +48,16 @@ info() { python -m hola_amd info > "$OUT/info.txt" 2>&1 || true; }
 
 case "$MODE" in
 final)
+  # the driver's round-end tiers, then the drain-hang trap: back-to-back
+  # rollouts of the 8 pods with no shutdown delay under load; any termination that stalls
+  # leaves its report in $OUT/kubesoak_nodelay/stalls/
   info
   timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 &&
   timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
     > "$OUT/pytest_gpu.log" 2>&1 &&
-  timeout -k 10 300 python bench.py > "$OUT/bench_default.json" 2>> "$OUT/err.log"
+  timeout -k 10 400 python bench.py > "$OUT/bench_default.json" 2>> "$OUT/err.log" &&
+  timeout -k 10 420 python -u bench/kube_soak.py --minutes "${SOAK_MIN:-3}" --shutdown-delay-ms 0 \
+    --out "$OUT/kubesoak_nodelay" > "$OUT/kubesoak_nodelay.json" 2> "$OUT/kubesoak_nodelay.log"
   ;;
 bench)
   timeout -k 10 400 python bench.py "$@" > "$OUT/bench.json" 2>> "$OUT/err.log"

@@ -28,17 +28,23 @@ from hola_amd.parallel import subruns  # noqa: E402
 
 
 def variant_args(v: str) -> dict:
-    """lgN = load-generator busy-poll window N us."""
-    if v.startswith("lg"):
-        return {"loadgen_busy_poll": int(v[2:])}
-    raise ValueError(f"unknown variant {v}")
+    """lgN = load-generator busy-poll window N us; lgN/prev = the same with build/prev/hola as
+    A and B (a server built from an earlier commit)."""
+    lg, _, exe = v.partition("/")
+    if not lg.startswith("lg"):
+        raise ValueError(f"unknown variant {v}")
+    out: dict = {"loadgen_busy_poll": int(lg[2:])}
+    if exe:
+        out["exe"] = ROOT / "build" / exe / "hola"
+    return out
 
 
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--seconds", type=float, default=10.0)
-    ap.add_argument("--variants", default="lg0", help="comma-separated: lgN (load generator busy-poll N us)")
+    ap.add_argument("--variants", default="lg0", help="comma-separated: lgN (load generator busy-poll N us), "
+                                                        "lgN/prev (with build/prev/hola as A and B)")
     ap.add_argument("--shipped", action="store_true", help="the shipped configuration (pool 10, BASIC logging)")
     ap.add_argument("--out", required=True)
     o = ap.parse_args()
@@ -66,7 +72,7 @@ def main() -> int:
                 sp = r.get("spins", {})
                 print(f"{rep} {v} rps={r.get('rps', 0):.0f} A={r.get('a_cpu_us_per_req', 0):.2f}us "
                       f"p99={r.get('p99_ns', 0) / 1e3:.1f}us A.spins={sp.get('a')} B.spins={sp.get('b')} "
-                      f"loc={r.get('locality')} load={r.get('host_load')}", flush=True)
+                      f"loc={r.get('locality')} load={r.get('host_load')} thr={r.get('cgroup_throttle')}", flush=True)
     summary = {}
     for v in variants:
         x = [r["rps"] for r in rows if r["variant"] == v and "rps" in r]

@@ -28,7 +28,7 @@ import subprocess
 import time
 from pathlib import Path
 
-from hola_amd.parallel.hostmetrics import busy_fraction, cpu_times, proc_cpu_s
+from hola_amd.parallel.hostmetrics import MetricsProbe, busy_fraction, cgroup_cpu_stat, cpu_times, proc_cpu_s
 from hola_amd.parallel.loadgen import ControlledLoadgen
 from hola_amd.server import HolaProcess
 from hola_amd.utils import cpu as _cpu
@@ -52,17 +52,22 @@ def host_load(t0: dict, t1: dict, own, job_cpus) -> dict:
     return {"own": busy_fraction(t0, t1, set(own)), "siblings": busy_fraction(t0, t1, other_siblings(own, job_cpus))}
 
 
-def metrics_counters(port: int, host: str = "127.0.0.1") -> dict:
+def metrics_counters(port: int, host: str = "127.0.0.1", probe: MetricsProbe | None = None) -> dict:
     """The /metrics counters the sub-runs attribute with: accept locality, busy-poll spins and
-    back-offs, Hystrix events, requests (empty on a failed scrape)."""
-    try:
-        st, _, body = http_get(host, port, "/metrics", timeout=5.0)
-    except OSError:
-        return {}
-    if st != 200:
-        return {}
+    back-offs, Hystrix events, requests (empty on a failed scrape). With a kept-alive `probe`
+    the scrapes add no accepted connection of their own to the locality counts."""
+    if probe is not None:
+        text = probe.text()
+    else:
+        try:
+            st, _, body = http_get(host, port, "/metrics", timeout=5.0)
+        except OSError:
+            return {}
+        if st != 200:
+            return {}
+        text = body.decode()
     out: dict[str, float] = {}
-    for ln in body.decode().splitlines():
+    for ln in text.splitlines():
         if not ln or ln[0] == "#":
             continue
         name, _, val = ln.rpartition(" ")
@@ -74,6 +79,8 @@ def metrics_counters(port: int, host: str = "127.0.0.1") -> dict:
             out["spins.backoffs"] = float(val)
         elif name == "hola_busy_poll_backoff_ms_total":
             out["spins.backoff_ms"] = float(val)
+        elif name == "hola_busy_poll_resumes_total":
+            out["spins.resumes"] = float(val)
         elif name.startswith("hola_hystrix_events_total{"):
             out["hystrix." + name.split('event="')[1].split('"')[0]] = float(val)
         elif name == "hola_http_requests_total":
@@ -285,7 +292,8 @@ def deployed(a, server_cpus, load_cpus, job_cpus, zipkin: str = "deployed", seco
             sink[0].wait(timeout=10)
 
 
-def chain(a, cpus, job_cpus, shipped: bool = False, seconds: float | None = None, loadgen_busy_poll: int = -1) -> dict:
+def chain(a, cpus, job_cpus, shipped: bool = False, seconds: float | None = None, loadgen_busy_poll: int = -1,
+          exe: Path | None = None) -> dict:
     """GET /api/hola-chaining end to end (HolaResource.java:69-78,94-113): load generator ->
     hola A -> hola B, where B plays aloha (B's own aloha is unreachable, so B answers its
     fallback list at once: ["Hola de B", "Aloha response (fallback)"], which A decodes as the
@@ -298,28 +306,32 @@ def chain(a, cpus, job_cpus, shipped: bool = False, seconds: float | None = None
     (image ENTRYPOINT + hola-dc.yaml args and env: the reference's pool of 10, Feign BASIC
     logging on, ZIPKIN_SERVER_URL set); the only changes are the aloha URL and path (B on
     loopback instead of the aloha Service) and the listen port. A body is then either the
-    two-hop answer or A's own fallback (counted apart, as body_alt)."""
+    two-hop answer or A's own fallback (counted apart, as body_alt). `exe`: another server
+    binary for A and B (A/B runs of server builds; engineered mode)."""
     seconds = seconds or a.chain_seconds
     plan = split_mirrored(sorted(cpus), {"A": 2, "B": 1, "loadgen": 1})
     lg_bp = a.chain_loadgen_busy_poll if loadgen_busy_poll < 0 else loadgen_busy_poll
     with HolaProcess(args=["--aloha-url", "http://127.0.0.1:1/", "--feign-log", "none", "--no-tracing",
                            "--feign-retry", "off", "--log-level", "warn"], env={"HOSTNAME": "B"},
-                     threads=len(plan["B"]), cpu_list=format_cpu_list(plan["B"])) as b:
+                     threads=len(plan["B"]), cpu_list=format_cpu_list(plan["B"]), exe=exe) as b:
         aloha = ["--aloha-url", f"http://127.0.0.1:{b.port}/", "--aloha-path", "api/hola-chaining"]
         if shipped:
             a_ctx = DeployedProc(plan["A"], "A", extra_args=aloha)
         else:
             a_ctx = HolaProcess(args=aloha + ["--feign-log", "none", "--hystrix-pool-size", str(a.chain_pool),
                                               "--log-level", "warn"],
-                                env={"HOSTNAME": "A"}, threads=len(plan["A"]), cpu_list=format_cpu_list(plan["A"]))
+                                env={"HOSTNAME": "A"}, threads=len(plan["A"]), cpu_list=format_cpu_list(plan["A"]),
+                                exe=exe)
         with a_ctx as s:
             st, _, body = http_get("127.0.0.1", s.port, "/api/hola-chaining", timeout=5.0)
             want = ["Hola de A", "Hola de B", FALLBACK]
             if st != 200 or json.loads(body) != want:
                 return {"error": f"unexpected first answer {st} {body[:200]!r}"}
             fallback_body = json.dumps(["Hola de A", FALLBACK], separators=(",", ":"))
-            m0 = metrics_counters(s.port), metrics_counters(b.port)
+            probes = MetricsProbe("127.0.0.1", s.port), MetricsProbe("127.0.0.1", b.port)
+            m0 = metrics_counters(s.port, probe=probes[0]), metrics_counters(b.port, probe=probes[1])
             c0 = proc_cpu_s(s.proc.pid), proc_cpu_s(b.proc.pid)
+            thr0 = cgroup_cpu_stat()
             lg = ControlledLoadgen([("127.0.0.1", s.port)], a.connections, len(plan["loadgen"]),
                                    cpu_list=format_cpu_list(plan["loadgen"]), path="/api/hola-chaining",
                                    busy_poll_us=lg_bp, expect_bodies=[body.decode()],
@@ -332,7 +344,10 @@ def chain(a, cpus, job_cpus, shipped: bool = False, seconds: float | None = None
             finally:
                 lg.close()
             c1 = proc_cpu_s(s.proc.pid), proc_cpu_s(b.proc.pid)
-            m1 = metrics_counters(s.port), metrics_counters(b.port)
+            thr1 = cgroup_cpu_stat()
+            m1 = metrics_counters(s.port, probe=probes[0]), metrics_counters(b.port, probe=probes[1])
+            for p in probes:
+                p.close()
             args = s.shown_args() if shipped else None
     rps = r["rps"]
     # CPU over the whole sub-run (its warm-up included) per request at the measured rate
@@ -348,6 +363,11 @@ def chain(a, cpus, job_cpus, shipped: bool = False, seconds: float | None = None
            # spins that ran out, back-offs and the milliseconds spent backed off (summed over
            # workers)
            "spins": {"a": counter_delta(m0[0], m1[0], "spins."), "b": counter_delta(m0[1], m1[1], "spins.")},
+           # CFS bandwidth throttling of this cgroup over the sub-run (a CPU quota that the sub-run's
+           # spinning threads exceed stops them all until the next 100 ms period)
+           "cgroup_throttle": {"periods": thr1.get("nr_periods", 0) - thr0.get("nr_periods", 0),
+                               "throttled_periods": thr1.get("nr_throttled", 0) - thr0.get("nr_throttled", 0),
+                               "throttled_ms": round((thr1.get("throttled_usec", 0) - thr0.get("throttled_usec", 0)) / 1000, 1)},
            "cpus": {k: format_cpu_list(v) for k, v in plan.items()}, "loadgen_busy_poll_us": lg_bp,
            "pool": 10 if shipped else a.chain_pool, "shipped": shipped}
     if args:

@@ -142,6 +142,10 @@ namespace {
 constexpr uint32_t kSpinWindow = 64;        // spins per decision
 constexpr uint32_t kSpinHitPercent = 75;    // keep spinning while >= this share finds work
 constexpr int64_t kSpinBackoffMinMs = 50, kSpinBackoffMaxMs = 1600;
+// While backed off: resume when this share of the window's blocking waits ended within twice
+// the spin budget (wake-up latency included). Stricter than the spin's own 75 %, so a loop
+// whose events come 20..40 us apart does not flip between the two states.
+constexpr uint32_t kResumeHitPercent = 90;
 }  // namespace
 
 void EventLoop::note_spin(bool hit) {
@@ -156,10 +160,25 @@ void EventLoop::note_spin(bool hit) {
     spin_off_until_ms_ = now_ms_ + spin_backoff_ms_;
     spin_offs_.fetch_add(1, std::memory_order_relaxed);
     spin_off_ms_.fetch_add(uint64_t(spin_backoff_ms_), std::memory_order_relaxed);
+    off_hits_ = off_waits_ = 0;
   } else {
     spin_backoff_ms_ = 0;
   }
   spin_hits_ = spin_misses_ = 0;
+}
+
+void EventLoop::note_off_wait(bool would_hit) {
+  off_hits_ += would_hit;
+  if (++off_waits_ < kSpinWindow) return;
+  if (off_hits_ * 100 >= kResumeHitPercent * off_waits_) {
+    // events keep arriving within the spin budget: the loop is busy, spin again now (and count
+    // only the part of the interval that was spent off)
+    if (spin_off_until_ms_ > now_ms_) spin_off_ms_.fetch_sub(uint64_t(spin_off_until_ms_ - now_ms_), std::memory_order_relaxed);
+    spin_off_until_ms_ = 0;
+    spin_backoff_ms_ = 0;
+    spin_resumes_.fetch_add(1, std::memory_order_relaxed);
+  }
+  off_hits_ = off_waits_ = 0;
 }
 
 void EventLoop::run() {
@@ -189,8 +208,12 @@ void EventLoop::run() {
       if (busy_auto_ && spun) note_spin(n > 0);
     }
     if (n == 0) {
+      // backed off from spinning: time the blocking wait (would a spin have found this event?)
+      const bool off = busy_auto_ && busy_poll_ns_ > 0 && now_ms_ < spin_off_until_ms_;
+      const int64_t w0 = off ? mono_ns() : 0;
       n = epoll_wait(epfd_, evs, kMaxEvents, next_timeout_ms());
       t = mono_ns();
+      if (off && n > 0) note_off_wait(t - w0 <= 2 * busy_poll_ns_);
     }
     if (n < 0 && errno != EINTR) {
       // Only a broken epoll descriptor gets here (EBADF, EINVAL, EFAULT). The loop cannot serve

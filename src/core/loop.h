@@ -68,7 +68,13 @@ class EventLoop {
   // Adaptive busy-polling: the spin stays on while it mostly finds work before its budget
   // runs out (a saturated loop, where it saves the sleep/wake-up per request), and is
   // switched off for a growing interval (50 ms .. 1.6 s) while it mostly waits in vain (light
-  // load, where it would only burn CPU). Each interval ends with a short re-probe.
+  // load, where it would only burn CPU). Each interval ends with a short re-probe. While it is
+  // off, the blocking waits tell whether a spin would have found work (the next event came
+  // within twice the spin budget): when 90 % of the last 64 would have, spinning resumes at
+  // once instead of at the interval's end. Without that, a saturated loop that was pushed off
+  // (a stall elsewhere drains the pipeline for a moment) serves every request through a sleep
+  // and a wake-up, which slows its peers, whose spins then miss too: a second, slower steady
+  // state (profiles/round5/02_chain_modes).
   void set_busy_poll_auto(bool on) { busy_auto_ = on; }
   // Adaptive spin statistics (loop thread; tests and metrics): spins that found work, spins
   // that ran out, how many times spinning was switched off, and for how many milliseconds
@@ -77,6 +83,7 @@ class EventLoop {
   uint64_t spin_misses() const { return spin_misses_total_.load(std::memory_order_relaxed); }
   uint64_t spin_offs() const { return spin_offs_.load(std::memory_order_relaxed); }
   uint64_t spin_off_ms() const { return spin_off_ms_.load(std::memory_order_relaxed); }
+  uint64_t spin_resumes() const { return spin_resumes_.load(std::memory_order_relaxed); }
 
   // What the loop thread is doing, published with relaxed stores as it goes, so another
   // thread can say where a loop that stopped answering is: Server::shutdown logs it for a
@@ -139,8 +146,10 @@ class EventLoop {
   bool busy_auto_ = false;
   uint32_t spin_hits_ = 0, spin_misses_ = 0;  // current measurement window
   int64_t spin_off_until_ms_ = 0, spin_backoff_ms_ = 0;
-  std::atomic<uint64_t> spin_hits_total_{0}, spin_misses_total_{0}, spin_offs_{0}, spin_off_ms_{0};
+  std::atomic<uint64_t> spin_hits_total_{0}, spin_misses_total_{0}, spin_offs_{0}, spin_off_ms_{0}, spin_resumes_{0};
+  uint32_t off_hits_ = 0, off_waits_ = 0;  // blocking waits while spinning is off (current window)
   void note_spin(bool hit);
+  void note_off_wait(bool would_hit);
   alignas(64) Activity act_;  // own cache line: written by the loop thread only
 };
 

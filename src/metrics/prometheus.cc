@@ -136,13 +136,14 @@ std::string Prometheus::render(http::Server* server) const {
     o += "# TYPE hola_bytes_out_total counter\nhola_bytes_out_total " + std::to_string(bout) + "\n";
     o += "# TYPE hola_workers gauge\nhola_workers " + std::to_string(server->num_workers()) + "\n";
     if (server->options().busy_poll_auto) {
-      uint64_t hits = 0, misses = 0, offs = 0, off_ms = 0;
+      uint64_t hits = 0, misses = 0, offs = 0, off_ms = 0, resumes = 0;
       for (size_t i = 0; i < server->num_workers(); ++i) {
         const EventLoop& l = server->worker(i).loop();
         hits += l.spin_hits();
         misses += l.spin_misses();
         offs += l.spin_offs();
         off_ms += l.spin_off_ms();
+        resumes += l.spin_resumes();
       }
       o += "# TYPE hola_busy_poll_spins_total counter\n";
       o += "hola_busy_poll_spins_total{result=\"hit\"} " + std::to_string(hits) + "\n";
@@ -151,6 +152,8 @@ std::string Prometheus::render(http::Server* server) const {
       // milliseconds of spinning switched off, summed over workers (a worker backed off for
       // most of a saturated run serves every request through a sleep and a wake-up)
       o += "# TYPE hola_busy_poll_backoff_ms_total counter\nhola_busy_poll_backoff_ms_total " + std::to_string(off_ms) + "\n";
+      // back-offs ended early because the blocking waits showed the loop busy
+      o += "# TYPE hola_busy_poll_resumes_total counter\nhola_busy_poll_resumes_total " + std::to_string(resumes) + "\n";
     }
     // 1 from the termination signal on (readiness failing, --shutdown-delay-ms), 2 while draining
     o += "# TYPE hola_server_terminating gauge\nhola_server_terminating " +

@@ -647,7 +647,8 @@ def test_exit_deadline_ends_a_termination_that_runs_too_long(hola):
     assert s.proc.wait(timeout=10) == 3
     # the report starts half way (a deadline under twice its 2.5 s budget), so the process has
     # exited by the deadline itself
-    assert 0.45 <= time.monotonic() - t0 < 1.5
+    # (a sanitizer build takes longer over the report's stack walks)
+    assert 0.45 <= time.monotonic() - t0 < (1.5 if not os.environ.get("HOLA_SANITIZER") else 4.0)
     assert "termination did not complete within 500 ms; exiting (exit deadline 1000 ms" in s.log()
 
 
@@ -663,7 +664,7 @@ def test_exit_watchdog_is_done_by_the_deadline_it_is_given(hola):
     s.proc.send_signal(signal.SIGTERM)
     assert s.proc.wait(timeout=15) == 3
     took = time.monotonic() - t0
-    assert 3.4 <= took < 6.0, took
+    assert 3.4 <= took < (6.0 if not os.environ.get("HOLA_SANITIZER") else 8.0), took
     log = s.log()
     assert "termination did not complete within 3500 ms; exiting (exit deadline 6000 ms" in log
     assert re.search(r"hola: worker \d: pass \d+", log), log[-2000:]
@@ -823,6 +824,27 @@ def _metric_value(s, name: str) -> float:
         if line.startswith(name + " "):
             return float(line.split()[1])
     raise AssertionError(f"{name} missing")
+
+
+def test_adaptive_busy_poll_resumes_when_load_returns(hola, hola_bin):
+    """A worker that backed off its spin under light load spins again as soon as its blocking
+    waits show events arriving within the spin budget, not at the end of its (up to 1.6 s)
+    back-off: a saturated loop pushed off by a momentary stall must not stay in the slow,
+    sleep-and-wake-up state (profiles/round5/02_chain_modes)."""
+    import json as _json
+    import subprocess
+
+    s = hola(args=["--busy-poll-us", "auto"], threads=1)
+    for _ in range(300):  # light load: back-offs escalate towards 1.6 s
+        assert s.get("/api/hola")[0] == 200
+        time.sleep(0.005)
+    assert _metric_value(s, "hola_busy_poll_backoffs_total") >= 1
+    loadgen = hola_bin.parent / "hola_loadgen"
+    r = subprocess.run([str(loadgen), "-t", "1", "-c", "16", "-d", "1s", "--json", f"{s.url}/api/hola"],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    assert _json.loads(r.stdout.strip().splitlines()[-1])["latency"]["errors"] == 0
+    assert _metric_value(s, "hola_busy_poll_resumes_total") >= 1
 
 
 def test_adaptive_busy_poll_backs_off_under_light_load(hola):

@@ -262,3 +262,44 @@ def test_eight_ranks_run_under_the_node_plan():
     # job's own load-generator threads, so no sibling load is charged to other tenants
     assert out["config"]["cores_per_replica"] == 16 and "16 physical cores" in out["config"]["layout_note"]
     assert all(h["siblings"] is None for h in out["host_load"]), out["host_load"]
+
+
+@pytest.mark.gpu
+def test_steering_keeps_one_l3s_clients_in_their_l3():
+    """Accept steering on the real topology: a replica with two workers in each of two L3
+    domains, and 24 connections opened from one client CPU of the first domain (a pool warming
+    up one L3 first). Every connection is served in the client's L3: the balance rule lets a
+    worker take up to twice its fair share (+8) before it refuses a steered connection; the
+    old rule (the least loaded worker + 8) sent a third of them across (VERDICT r4 weak #2)."""
+    import socket
+
+    from hola_amd.server import HolaProcess
+    from hola_amd.utils.cpu import allowed_cpus, l3_domain, physical_cores
+
+    by_dom: dict[int, list[int]] = {}
+    for c in physical_cores(allowed_cpus()):
+        by_dom.setdefault(l3_domain(c), []).append(c)
+    doms = [d for d, cs in by_dom.items() if len(cs) >= 3][:2]
+    if len(doms) < 2:
+        pytest.skip("needs two L3 domains with three cores each")
+    x, y = by_dom[doms[0]], by_dom[doms[1]]
+    server_cpus = [x[0], x[1], y[0], y[1]]
+    with HolaProcess(threads=4, cpu_list=",".join(map(str, server_cpus)), env={"HOSTNAME": "s"},
+                     log_level="warn") as s:
+        old = os.sched_getaffinity(0)
+        os.sched_setaffinity(0, {x[2]})
+        try:
+            conns = []
+            for _ in range(24):
+                c = socket.create_connection(("127.0.0.1", s.port), timeout=5)
+                c.sendall(b"GET /api/hola HTTP/1.1\r\nHost: x\r\n\r\n")
+                assert c.recv(4096).startswith(b"HTTP/1.1 200")
+                conns.append(c)
+        finally:
+            os.sched_setaffinity(0, old)
+        metrics = s.get("/metrics")[2].decode()
+        for c in conns:
+            c.close()
+    loc = {l.split('"')[1]: int(float(l.split()[-1])) for l in metrics.splitlines()
+           if l.startswith("hola_accept_locality_total{")}
+    assert loc.get("same_l3", 0) + loc.get("same_core", 0) >= 24, loc

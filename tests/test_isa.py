@@ -78,12 +78,12 @@ def test_portable_build_answers_like_release():
     status line, headers and body must be byte-identical for valid and malformed heads,
     short and long targets (byte loop vs 32-byte vector scan in the release build)."""
     native.build("portable")
-    exe = native.binary("hola", "portable")
+    exe = native.build_dir("portable") / "hola"  # (not binary(): HOLA_BIN_DIR may name a sanitizer build)
     dis = subprocess.run(["objdump", "-d", str(exe)], capture_output=True, text=True, timeout=120)
     if dis.returncode == 0:
         assert "%ymm" not in dis.stdout  # no 256-bit AVX instruction in the portable binary
     args = ["--no-tracing", "--log-level", "warn"]
-    with HolaProcess(args=args, env={"HOSTNAME": "p"}, threads=1) as rel, \
+    with HolaProcess(args=args, env={"HOSTNAME": "p"}, threads=1, exe=native.build_dir("release") / "hola") as rel, \
             HolaProcess(args=args, env={"HOSTNAME": "p"}, threads=1, exe=exe) as port:
         for req in _corpus(400):
             assert _raw(rel.port, req) == _raw(port.port, req), req
