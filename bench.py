@@ -388,6 +388,10 @@ def main() -> int:
         for key, secs, fn in (
                 ("deployed", a.deployed_seconds,
                  lambda: subruns.deployed(a, server_cpus, load_cpus, job_cpus, zipkin=a.deployed_zipkin)),
+                # the same, sized as the manifests size one pod (limits.cpu: a 2-CPU cpuset)
+                ("deployed_pod", a.deployed_seconds,
+                 lambda: subruns.deployed(a, sorted(server_cpus)[:subruns.manifest_pod_cpus()], load_cpus, job_cpus,
+                                          zipkin=a.deployed_zipkin)),
                 ("chain", a.chain_seconds, lambda: subruns.chain(a, rank_cpus, job_cpus)),
                 ("chain_shipped", a.chain_shipped_seconds,
                  lambda: subruns.chain(a, rank_cpus, job_cpus, shipped=True, seconds=a.chain_shipped_seconds)),
@@ -454,6 +458,12 @@ def main() -> int:
             # N = 1 only: the replica as the image and manifests run it (--shutdown-delay-ms 5000
             # --busy-poll-us auto, ZIPKIN_SERVER_URL set), same load generator
             **_deployed_keys(subs.get("deployed")),
+            # ... in one pod's CPU limit (deploy/openshift: limits.cpu 2): what one pod of
+            # BASELINE config 5 serves on its own
+            **{k.replace("deployed_", "deployed_pod_", 1): v for k, v in _deployed_keys(subs.get("deployed_pod")).items()
+               if k in ("deployed_rps", "deployed_p50_ms", "deployed_p99_ms", "deployed_requests", "deployed_errors",
+                        "deployed_non2xx", "deployed_body_mismatch", "deployed_server_cpu_us_per_req", "deployed_cpus",
+                        "deployed_host_load", "deployed_error")},
             # N = 1 only: GET /api/hola-chaining through two replicas (the endpoint with real work
             # behind it), engineered (pool 128, logging off) and as shipped (pool 10, BASIC logging)
             **_chain_keys(subs.get("chain"), "chain"),

@@ -129,6 +129,16 @@ def deployed_argv_env(port: int, hostname: str, extra_args: list[str] | None = N
     return argv, env
 
 
+def manifest_pod_cpus() -> int:
+    """The pod's CPU limit in deploy/openshift/hola-dc.yaml (whole CPUs; a Guaranteed pod
+    under the static CPU manager gets exactly this many exclusive CPUs)."""
+    from hola_amd.kube import manifests as km
+
+    dc = next(o for o in km.load_objects([REPO / "deploy/openshift/hola-dc.yaml"]) if o["kind"] == "DeploymentConfig")
+    lim = str(dc["spec"]["template"]["spec"]["containers"][0].get("resources", {}).get("limits", {}).get("cpu", "0"))
+    return max(1, int(float(lim[:-1]) / 1000) if lim.endswith("m") else int(float(lim)))
+
+
 class DeployedProc:
     """A replica started from deployed_argv_env() in a cpuset (a Guaranteed pod under the
     static CPU manager); stderr to /dev/null (Feign BASIC logging writes two lines per call)."""

@@ -57,6 +57,9 @@ def test_bench_auto_steps_and_node_subruns():
     assert out["config"]["cores_per_replica"] == len({min(siblings(c)) for c in srv})
     assert out["deployed_errors"] == 0 and out["deployed_body_checked"] == out["deployed_requests"] > 0
     assert set(out["deployed_host_load"]) == {"own", "siblings"} and out["deployed_zipkin"] == "deployed"
+    # ... and sized as the manifests size a pod (limits.cpu 2)
+    assert len(parse_cpu_list(out["deployed_pod_cpus"])) == 2 and out["deployed_pod_errors"] == 0
+    assert out["deployed_pod_rps"] > 0
     assert out["chain_errors"] == 0 and out["chain_hystrix_fallback"] == 0 and out["chain_pool"] == 128
     assert set(out["chain_locality"]) == {"loadgen_to_a", "a_to_b"}
     assert abs(sum(out["chain_locality"]["a_to_b"].values()) - 1.0) < 1e-3
