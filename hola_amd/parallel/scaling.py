@@ -24,7 +24,9 @@ import json
 import sys
 import time
 
+from hola_amd.parallel.hostmetrics import MetricsProbe, proc_cpu_s
 from hola_amd.parallel.loadgen import run_duration
+from hola_amd.parallel.subruns import counter_delta, locality_fraction, metrics_counters
 from hola_amd.parallel.replicas import ReplicaSet, RRProxy
 from hola_amd.utils.cpu import (cgroup_cpu_quota, cpu_budget, format_cpu_list, plan_mirrored, plan_node,
                                 plan_slot_subset, sibling_of, split_server_loadgen)
@@ -110,6 +112,11 @@ def run_point(n: int, args) -> dict:
             extra += ["--busy-poll-pause", str(args.busy_poll_pause)]
     shared = 0 if args.lb == "reuseport" else None
     with ReplicaSet(n, cpu_plan=p["replicas"], args=extra, supervise=False, shared_port=shared) as rs:
+        # per replica: requests served and where each accepted connection's client ran, read
+        # over kept-alive /metrics connections (reuseport: one shared port, so no per-replica view)
+        probes = [MetricsProbe("127.0.0.1", port) for port in rs.ports] if shared is None else []
+        m0 = [metrics_counters(0, probe=pr) for pr in probes]
+        cpu0 = [proc_cpu_s(pr.proc.pid) for pr in rs.procs]
         if args.lb == "proxy":
             with RRProxy(rs.targets, threads=proxy_threads, cpu_list=format_cpu_list(p["proxy"]),
                          busy_poll_us=args.busy_poll_us if args.proxy_busy_poll_us < 0 else args.proxy_busy_poll_us,
@@ -124,6 +131,13 @@ def run_point(n: int, args) -> dict:
                                cpu_list=",".join(map(str, p["loadgen"])), busy_poll_us=args.busy_poll_us,
                                busy_poll_pause=args.busy_poll_pause,
                                verify_body=args.lb == "client")
+        m1 = [metrics_counters(0, probe=pr) for pr in probes]
+        cpu1 = [proc_cpu_s(pr.proc.pid) for pr in rs.procs]
+        for pr in probes:
+            pr.close()
+    per_replica = [{"requests": int(b.get("requests", 0) - a.get("requests", 0)),
+                    "locality": locality_fraction(counter_delta(a, b, "locality.")),
+                    "cpu_s": round(c1 - c0, 3)} for a, b, c0, c1 in zip(m0, m1, cpu0, cpu1)]
     lat = res["latency"]
     return {
         "replicas": n, "connections": conns, "lb": args.lb, "rps": res["rps"],
@@ -131,7 +145,7 @@ def run_point(n: int, args) -> dict:
         "errors": lat["errors"], "non2xx": lat["non2xx"], "body_mismatch": lat.get("body_mismatch", 0),
         "cpu_map": {"replicas": [format_cpu_list(c) for c in p["replicas"]], "proxy": format_cpu_list(p["proxy"]),
                     "loadgen": format_cpu_list(p["loadgen"])},
-        "budget": budget, "quota": cgroup_cpu_quota(), "duration_s": args.duration,
+        "budget": budget, "quota": cgroup_cpu_quota(), "duration_s": args.duration, "per_replica": per_replica,
         **({"slot_cores": args.slot_cores, "node_slots": p["slots"], "layout": f"miniature node plan ({p['smt']})"}
            if args.slot_cores else {}),
     }
