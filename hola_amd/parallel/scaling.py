@@ -25,8 +25,8 @@ import sys
 import time
 
 from hola_amd.parallel.hostmetrics import MetricsProbe, proc_cpu_s
-from hola_amd.parallel.loadgen import run_duration
-from hola_amd.parallel.subruns import counter_delta, locality_fraction, metrics_counters
+from hola_amd.parallel.loadgen import ControlledLoadgen
+from hola_amd.parallel.subruns import counter_delta, locality_fraction, metrics_counters, timed_closed_loop
 from hola_amd.parallel.replicas import ReplicaSet, RRProxy
 from hola_amd.utils.cpu import (cgroup_cpu_quota, cpu_budget, format_cpu_list, plan_mirrored, plan_node,
                                 plan_slot_subset, sibling_of, split_server_loadgen)
@@ -92,6 +92,29 @@ def plan_slots(n: int, k: int, slots: int, lb: str) -> dict:
             "slots": [p["slot"] for p in sub], "smt": sub[0]["smt"] if sub else "pair"}
 
 
+def _measure(targets, conns: int, load_cpus: list[int], args, verify: bool) -> dict:
+    """A closed-loop run of about args.duration after args.warmup, in the load generator's
+    control mode: every connection is made before any request is sent (as bench.py runs it),
+    then timed runs of ~0.5 s follow back to back. In wrk-style duration mode each thread
+    started sending as soon as its own connections were up, and connections made while others
+    were already loaded were placed off their client's core (per-replica locality all
+    `same_socket` in some runs, profiles/round5/04_scale_mini)."""
+    lg = ControlledLoadgen(targets, conns, len(load_cpus), cpu_list=",".join(map(str, load_cpus)),
+                           busy_poll_us=args.busy_poll_us, busy_poll_pause=args.busy_poll_pause, verify_body=verify)
+    try:
+        t_end = time.monotonic() + args.warmup
+        per = 2000
+        while time.monotonic() < t_end:
+            w = lg.run(per)
+            per = int(max(200, min(2_000_000, w["requests"] / max(1e-9, w["elapsed_ns"] / 1e9) * 0.25 / conns)))
+        r = timed_closed_loop(lg, conns, args.duration, None, [], [], warm_per_conn=per)
+    finally:
+        lg.close()
+    return {"rps": r["rps"], "latency": {"p50_ns": r["p50_ns"], "p99_ns": r["p99_ns"], "p999_ns": r.get("p999_ns", 0),
+                                         "errors": r["errors"], "non2xx": r["non2xx"],
+                                         "body_mismatch": r["body_mismatch"]}}
+
+
 def run_point(n: int, args) -> dict:
     budget = args.budget or cpu_budget()
     if args.slot_cores:
@@ -121,16 +144,10 @@ def run_point(n: int, args) -> dict:
             with RRProxy(rs.targets, threads=proxy_threads, cpu_list=format_cpu_list(p["proxy"]),
                          busy_poll_us=args.busy_poll_us if args.proxy_busy_poll_us < 0 else args.proxy_busy_poll_us,
                          exe=args.proxy_exe or None) as px:
-                targets = [("127.0.0.1", px.port)]
-                res = run_duration(targets, conns, len(p["loadgen"]), args.duration, args.warmup,
-                                   cpu_list=",".join(map(str, p["loadgen"])), busy_poll_us=args.busy_poll_us,
-                                   busy_poll_pause=args.busy_poll_pause)
+                res = _measure([("127.0.0.1", px.port)], conns, p["loadgen"], args, verify=False)
         else:
             # client-side round-robin: one target per replica, so each target's body is fixed
-            res = run_duration(rs.targets, conns, len(p["loadgen"]), args.duration, args.warmup,
-                               cpu_list=",".join(map(str, p["loadgen"])), busy_poll_us=args.busy_poll_us,
-                               busy_poll_pause=args.busy_poll_pause,
-                               verify_body=args.lb == "client")
+            res = _measure(rs.targets, conns, p["loadgen"], args, verify=args.lb == "client")
         m1 = [metrics_counters(0, probe=pr) for pr in probes]
         cpu1 = [proc_cpu_s(pr.proc.pid) for pr in rs.procs]
         for pr in probes:

@@ -228,7 +228,8 @@ def timed_closed_loop(lg: ControlledLoadgen, connections: int, seconds: float, p
     st = lg.stats()
     el = el_ns / 1e9
     return {"rps": reqs / el if el > 0 else 0.0, "elapsed_s": el, "requests": reqs,
-            "errors": errs, "p50_ns": st["p50_ns"], "p99_ns": st["p99_ns"], "non2xx": st.get("non2xx", 0),
+            "errors": errs, "p50_ns": st["p50_ns"], "p99_ns": st["p99_ns"], "p999_ns": st.get("p999_ns", 0),
+            "non2xx": st.get("non2xx", 0),
             "body_checked": st.get("body_checked", 0), "body_mismatch": st.get("body_mismatch", 0),
             "body_alt": st.get("body_alt", 0),
             "cpu_us_per_req": 1e6 * (c1 - c0) / max(1, reqs) if pid else None,
