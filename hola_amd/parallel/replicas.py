@@ -126,7 +126,10 @@ class ReplicaSet:
 
     @property
     def targets(self) -> list[tuple[str, int]]:
-        return [("127.0.0.1", p) for p in sorted(set(self.ports))]
+        """One address per replica, in replica order (target i is replica i, whose CPUs are
+        cpu_plan[i]: a load generator that places thread t next to replica t relies on it);
+        one address in all with a shared port."""
+        return [("127.0.0.1", p) for p in dict.fromkeys(self.ports)]
 
     def stop(self) -> None:
         self._stop.set()

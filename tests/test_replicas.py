@@ -353,3 +353,17 @@ def test_loadgen_service_mode_dnats_each_new_connection(tmp_path, hola):
     out, err = lg.communicate(timeout=30)
     r = json.loads(out.strip().splitlines()[-1])
     assert r["targets"] == 1 and r["latency"]["errors"] == 0, r  # never reconnected, never saw b
+
+
+def test_targets_follow_replica_order():
+    """ReplicaSet.targets[i] is replica i (HOSTNAME replica-<i>, CPUs cpu_plan[i]), whatever
+    order the free ports came in: the scaling harness places load-generator thread t next to
+    replica t's cores and deals it target t. (Sorted ports put half of the N = 2 miniature's
+    clients on the wrong replica's core, profiles/round5/04_scale_mini.)"""
+    from hola_amd.parallel.replicas import ReplicaSet
+
+    rs = ReplicaSet(3, supervise=False)
+    rs.ports = [40003, 40001, 40002]
+    assert [p for _, p in rs.targets] == [40003, 40001, 40002]
+    rs.ports = [40005] * 3  # a shared (reuseport) port: one address
+    assert [p for _, p in rs.targets] == [40005]
