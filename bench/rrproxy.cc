@@ -22,6 +22,12 @@
 // --no-failover makes a connection to a backend that refuses fail as it does through
 // kube-proxy's DNAT rules, instead of being retried on the next backend. Sessions keep their
 // backend when it leaves the set (conntrack keeps established flows).
+//
+// Topology hints: a backend given as `host:port@cpus` (e.g. 127.0.0.1:18400@16-17) says where
+// its workers run. A proxy thread then deals its sessions round-robin over the healthy
+// backends that share its L3 domain, and over all of them only when none does (Kubernetes'
+// topology-aware routing, with the L3 as the zone): a session's client, proxy thread and
+// server then stay in one cache domain. Without hints every thread deals over every backend.
 #include <errno.h>
 #include <sys/stat.h>
 #include <signal.h>
@@ -55,6 +61,7 @@ struct Backend {
   int port;
   sockaddr_storage addr;
   socklen_t len;
+  std::vector<int> l3;  // L3 domains of its workers (topology hint); empty = unknown
   std::atomic<bool> healthy{true};
   std::atomic<uint64_t> picked{0};
 };
@@ -75,9 +82,19 @@ bool g_failover = true;
 
 const BackendSet& current_set() { return *g_set.load(std::memory_order_acquire); }
 
-Backend* pick() {
+// `l3` = the calling proxy thread's L3 domain (-1: unknown); `rr` = its own round-robin
+// counter for the backends of that domain.
+Backend* pick(int l3 = -1, uint64_t* rr = nullptr) {
   const BackendSet& set = current_set();
   const size_t n = set.list.size();
+  if (l3 >= 0 && rr) {
+    // topology hints: the healthy backends in this thread's L3, round-robin
+    for (size_t k = 0; k < n; ++k) {
+      Backend* b = set.list[(*rr)++ % n];
+      if (b->healthy.load(std::memory_order_relaxed) && std::find(b->l3.begin(), b->l3.end(), l3) != b->l3.end())
+        return b;
+    }
+  }
   for (size_t k = 0; k < n; ++k) {
     Backend* b = set.list[g_rr.fetch_add(1, std::memory_order_relaxed) % n];
     if (b->healthy.load(std::memory_order_relaxed)) return b;
@@ -112,12 +129,27 @@ bool parse_backends(const std::string& text, std::vector<Backend*>* out) {
     while (!t.empty() && (t.back() == ' ' || t.back() == '\r')) t.pop_back();
     while (!t.empty() && t.front() == ' ') t.erase(0, 1);
     if (t.empty() || t[0] == '#') continue;
+    std::vector<int> cpus;  // topology hint after '@'
+    if (size_t at = t.find('@'); at != std::string::npos) {
+      std::vector<int> tmp;
+      std::string list = t.substr(at + 1);
+      for (char& ch : list)
+        if (ch == ';') ch = ',';  // "0-1;8" inside a comma-separated --backends
+      if (!parse_cpu_list(list, &tmp)) return false;
+      cpus = std::move(tmp);
+      t.resize(at);
+    }
     size_t colon = t.rfind(':');
     if (colon == std::string::npos) return false;
     std::string host = t.substr(0, colon);
     if (host.size() > 2 && host.front() == '[' && host.back() == ']') host = host.substr(1, host.size() - 2);
     Backend* b = backend_for(host, atoi(t.substr(colon + 1).c_str()));
     if (!b) return false;
+    if (!cpus.empty() && b->l3.empty()) {  // set once (a reload may name it again)
+      for (int c : cpus)
+        if (int d = l3_domain_of(c); d >= 0 && std::find(b->l3.begin(), b->l3.end(), d) == b->l3.end())
+          b->l3.push_back(d);
+    }
     if (std::find(out->begin(), out->end(), b) == out->end()) out->push_back(b);
   }
   return true;
@@ -171,10 +203,10 @@ void mark_down(Backend* b, int err) {
 // down) while connect() fails at once. The handshake may still be in progress: bytes sent
 // before it completes wait for the socket's OUT edge, and a refusal reported then fails over
 // from Session::on_event.
-int connect_backend(Backend** chosen, bool* in_progress) {
+int connect_backend(Backend** chosen, bool* in_progress, int l3 = -1, uint64_t* rr = nullptr) {
   const size_t n = g_failover ? current_set().list.size() : 1;
   for (size_t tries = 0; tries < n; ++tries) {
-    Backend* b = pick();
+    Backend* b = pick(l3, rr);
     if (!b) return -1;
     int fd = connect_nonblocking(b->addr, b->len, in_progress);
     if (fd >= 0) {
@@ -235,12 +267,14 @@ struct Session : EventLoop::Handler {
 class ProxyLoop {
  public:
   ProxyLoop(int index, int cpu, int busy_poll_us, int busy_poll_pause, int idle_timeout_ms)
-      : index_(index), cpu_(cpu), idle_timeout_ms_(idle_timeout_ms) {
+      : index_(index), cpu_(cpu), idle_timeout_ms_(idle_timeout_ms), l3_(cpu >= 0 ? l3_domain_of(cpu) : -1) {
     loop_.set_busy_poll_us(busy_poll_us);
     loop_.set_busy_poll_pause(busy_poll_pause);
   }
   EventLoop& loop() { return loop_; }
   int cpu() const { return cpu_; }
+  int l3() const { return l3_; }
+  uint64_t* rr() { return &rr_; }
   int index() const { return index_; }
   std::atomic<int64_t>& sessions() { return sessions_; }
 
@@ -265,7 +299,7 @@ class ProxyLoop {
   void adopt_here(int cfd) {
     Backend* b = nullptr;
     bool inprog = false;
-    int bfd = connect_backend(&b, &inprog);
+    int bfd = connect_backend(&b, &inprog, l3_, &rr_);
     if (bfd < 0) {
       ::close(cfd);
       sessions_.fetch_sub(1, std::memory_order_relaxed);
@@ -304,6 +338,8 @@ class ProxyLoop {
   EventLoop loop_;
   int index_, cpu_;
   int idle_timeout_ms_;
+  int l3_;           // this thread's L3 domain (topology hints)
+  uint64_t rr_ = 0;  // round-robin position over the backends of that domain
   std::atomic<int64_t> sessions_{0};
   Session* head_ = nullptr;
 };
@@ -373,7 +409,7 @@ bool Session::backend_connected(uint32_t ev) {
   bfd = -1;
   if (!g_failover || ++failovers > int(current_set().list.size())) return false;
   bool inprog = false;
-  bfd = connect_backend(&backend, &inprog);
+  bfd = connect_backend(&backend, &inprog, owner->l3(), owner->rr());
   if (bfd < 0) return false;
   connecting = inprog;
   l.add(bfd, ProxyLoop::kEvents, &bside);
@@ -540,6 +576,8 @@ int main(int argc, char** argv) {
               "                    [--health-ms N] [--busy-poll-us N [--busy-poll-pause P]] [--no-steer] [--port-file F]\n"
               "                    [--idle-timeout-ms N (default 60000, 0 = never)]\n"
               "                    [--endpoints-file F (backend set re-read on change)] [--no-failover]\n"
+              "                    (a backend h:p@CPUS names its workers' CPUs: each proxy thread prefers\n"
+              "                     the backends in its own L3; ';' separates CPU ranges inside --backends)\n"
               "                    (--health-ms 0: no probing of backends)\n");
       return 2;
     }

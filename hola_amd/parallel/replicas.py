@@ -156,11 +156,16 @@ class RRProxy:
 
     def __init__(self, backends: list[tuple[str, int]], port: int = 0, threads: int = 1,
                  cpu_list: str | None = None, health_ms: int = 200, busy_poll_us: int = 0,
-                 exe: str | None = None, host: str = "127.0.0.1", idle_timeout_ms: int | None = None):
+                 exe: str | None = None, host: str = "127.0.0.1", idle_timeout_ms: int | None = None,
+                 backend_cpus: list[list[int]] | None = None):
+        """`backend_cpus[i]`: the CPUs backend i's workers run on (topology hints: each proxy
+        thread then prefers the backends in its own L3)."""
         self._tmp = tempfile.TemporaryDirectory(prefix="rrproxy-")
         self.port_file = os.path.join(self._tmp.name, "port")
+        hints = [("@" + ";".join(map(str, c)) if c else "") for c in (backend_cpus or [[]] * len(backends))]
         cmd = [exe or str(binary("hola_rrproxy")), "--host", host, "--port", str(port),
-               "--threads", str(threads), "--backends", ",".join(f"{h}:{p}" for h, p in backends),
+               "--threads", str(threads),
+               "--backends", ",".join(f"{h}:{p}{hint}" for (h, p), hint in zip(backends, hints)),
                "--health-ms", str(health_ms), "--port-file", self.port_file]
         if cpu_list:
             cmd += ["--cpu-list", cpu_list]

@@ -134,6 +134,12 @@ def run_point(n: int, args) -> dict:
         if args.busy_poll_pause:
             extra += ["--busy-poll-pause", str(args.busy_poll_pause)]
     shared = 0 if args.lb == "reuseport" else None
+    reuseport_cpu = args.reuseport_cpu
+    if reuseport_cpu == "auto":  # the client runs on the worker's SMT sibling in the pair plan
+        reuseport_cpu = "sibling" if args.slot_cores and p.get("smt") == "pair" else "none"
+    if shared is not None and reuseport_cpu != "none":
+        extra += ["--reuseport-cpu", reuseport_cpu]
+    hints = args.proxy_hints == "on" or (args.proxy_hints == "auto" and bool(args.slot_cores))
     with ReplicaSet(n, cpu_plan=p["replicas"], args=extra, supervise=False, shared_port=shared) as rs:
         # per replica: requests served and where each accepted connection's client ran, read
         # over kept-alive /metrics connections (reuseport: one shared port, so no per-replica view)
@@ -143,7 +149,7 @@ def run_point(n: int, args) -> dict:
         if args.lb == "proxy":
             with RRProxy(rs.targets, threads=proxy_threads, cpu_list=format_cpu_list(p["proxy"]),
                          busy_poll_us=args.busy_poll_us if args.proxy_busy_poll_us < 0 else args.proxy_busy_poll_us,
-                         exe=args.proxy_exe or None) as px:
+                         exe=args.proxy_exe or None, backend_cpus=p["replicas"] if hints else None) as px:
                 res = _measure([("127.0.0.1", px.port)], conns, p["loadgen"], args, verify=False)
         else:
             # client-side round-robin: one target per replica, so each target's body is fixed
@@ -163,6 +169,8 @@ def run_point(n: int, args) -> dict:
         "cpu_map": {"replicas": [format_cpu_list(c) for c in p["replicas"]], "proxy": format_cpu_list(p["proxy"]),
                     "loadgen": format_cpu_list(p["loadgen"])},
         "budget": budget, "quota": cgroup_cpu_quota(), "duration_s": args.duration, "per_replica": per_replica,
+        "lb_detail": ({"reuseport_cpu": reuseport_cpu} if args.lb == "reuseport" else
+                      {"topology_hints": hints} if args.lb == "proxy" else {"dealing": "thread t -> replica t"}),
         **({"slot_cores": args.slot_cores, "node_slots": p["slots"], "layout": f"miniature node plan ({p['smt']})"}
            if args.slot_cores else {}),
     }
@@ -189,6 +197,12 @@ def main(argv=None) -> int:
                     help="the replicas' own --busy-poll-us (N, auto, auto:N); default --busy-poll-us")
     ap.add_argument("--busy-poll-pause", type=int, default=0,
                     help="PAUSE instructions between empty polls (replicas and load generator)")
+    ap.add_argument("--reuseport-cpu", choices=("auto", "none", "self", "sibling"), default="auto",
+                    help="--lb reuseport: the replicas' --reuseport-cpu (auto = sibling on the miniature "
+                         "pair plan, where each client thread runs on its worker's SMT sibling; else none)")
+    ap.add_argument("--proxy-hints", choices=("auto", "on", "off"), default="auto",
+                    help="--lb proxy: give hola_rrproxy each replica's CPUs (topology hints; auto = on "
+                         "with --slot-cores)")
     ap.add_argument("--slot-cores", type=int, default=0,
                     help="miniature node plan: K physical cores per replica at the node slots' places")
     ap.add_argument("--slots", type=int, default=8, help="node slots of the miniature plan (GPUs on the node)")

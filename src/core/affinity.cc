@@ -114,6 +114,16 @@ int core_of(int cpu) {
   return (cpu >= 0 && size_t(cpu) < table.size()) ? table[size_t(cpu)] : -1;
 }
 
+int sibling_of(int cpu) {
+  std::ifstream f("/sys/devices/system/cpu/cpu" + std::to_string(cpu) + "/topology/thread_siblings_list");
+  std::string line;
+  std::vector<int> sib;
+  if (f && std::getline(f, line) && parse_cpu_list(line, &sib))
+    for (int x : sib)
+      if (x != cpu) return x;
+  return cpu;
+}
+
 int package_of(int cpu) {
   static const std::vector<int> table = [] {
     std::vector<int> v;

@@ -17,6 +17,9 @@ int l3_domain_of(int cpu);
 // Physical core of a CPU: the lowest CPU id among its SMT siblings (sysfs
 // thread_siblings_list); -1 when unknown. Cached.
 int core_of(int cpu);
+// The other SMT thread of `cpu`'s physical core (the first sibling that is not `cpu`), or
+// `cpu` itself when it has none.
+int sibling_of(int cpu);
 // Socket (physical package) of a CPU from sysfs; -1 when unknown. Cached.
 int package_of(int cpu);
 // CPU quota from cgroup v2 cpu.max (e.g. 16.0 for "1600000 100000"); 0 when unlimited.

@@ -25,6 +25,7 @@ int listen_tcp(const ListenOptions& o, std::string* err) {
   int one = 1;
   setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
   if (o.reuseport) setsockopt(fd, SOL_SOCKET, SO_REUSEPORT, &one, sizeof one);
+  if (o.incoming_cpu >= 0) setsockopt(fd, SOL_SOCKET, SO_INCOMING_CPU, &o.incoming_cpu, sizeof o.incoming_cpu);
   // Accepted sockets inherit TCP_NODELAY from the listener on Linux; set it once here.
   setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
   if (::bind(fd, reinterpret_cast<sockaddr*>(&ss), len) != 0) {

@@ -15,6 +15,10 @@ struct ListenOptions {
   int port = 8080;
   int backlog = 4096;
   bool reuseport = false;
+  // SO_INCOMING_CPU on the listener (-1 = unset): in an SO_REUSEPORT group, Linux 6.1+ hands
+  // a new connection to the listener whose incoming CPU is the CPU its SYN was processed on
+  // (the client's CPU for loopback clients), and hashes only when none matches.
+  int incoming_cpu = -1;
 };
 
 // Creates a non-blocking listening TCP socket; returns fd or -1 (errno set, message in *err).

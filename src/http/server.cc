@@ -602,6 +602,11 @@ bool Server::bind(std::string* err) {
   lo.reuseport = opts_.reuseport_accept;
   size_t n = opts_.reuseport_accept ? workers_.size() : 1;
   for (size_t i = 0; i < n; ++i) {
+    lo.incoming_cpu = -1;
+    if (opts_.reuseport_accept && !opts_.cpus.empty() && opts_.reuseport_cpu != ServerOptions::ReuseportCpu::kNone) {
+      const int cpu = opts_.cpus[i % opts_.cpus.size()];
+      lo.incoming_cpu = opts_.reuseport_cpu == ServerOptions::ReuseportCpu::kSibling ? sibling_of(cpu) : cpu;
+    }
     int fd = listen_tcp(lo, err);
     if (fd < 0) return false;
     if (i == 0) {

@@ -155,6 +155,10 @@ struct ServerOptions {
   int threads = 1;
   std::vector<int> cpus;          // pin worker i to cpus[i % size]; empty = no pinning
   bool reuseport_accept = false;  // per-worker SO_REUSEPORT listeners instead of round-robin
+  // With reuseport_accept and pinned workers: the CPU each worker's listener names as its
+  // incoming CPU, so the kernel's group selection sends a connection to the worker (of this
+  // replica or of another one in the group) that expects clients on that CPU.
+  enum class ReuseportCpu { kNone, kSelf, kSibling } reuseport_cpu = ReuseportCpu::kNone;
   int backlog = 4096;
   size_t read_chunk = 64 * 1024;
   int busy_poll_us = 0;  // see EventLoop::set_busy_poll_us

@@ -49,6 +49,9 @@ void usage() {
           "  --threads N              event-loop workers (default: one per allowed CPU, capped by cgroup quota)\n"
           "  --cpu-list LIST          pin workers to these CPUs, e.g. 0-3,8\n"
           "  --accept rr|reuseport    connection distribution (default rr)\n"
+          "  --reuseport-cpu none|self|sibling   with --accept reuseport and pinned workers, each worker's\n"
+          "                           listener names this CPU as its incoming CPU, so the kernel hands a\n"
+          "                           connection to the worker expecting clients there (default none = hash)\n"
           "  --conf PATH              greeting properties file (same as -Dconf=PATH)\n"
           "  --deltaspike-properties PATH   ordinal-100 properties file\n"
           "  --hystrix-config PATH    Hystrix properties (Archaius config.properties role)\n"
@@ -191,6 +194,12 @@ int main(int argc, char** argv) {
       std::string m = val("--accept");
       if (m == "reuseport") so.reuseport_accept = true;
       else if (m != "rr") { fprintf(stderr, "hola: --accept rr|reuseport\n"); return 2; }
+    } else if (a == "--reuseport-cpu") {
+      std::string m = val("--reuseport-cpu");
+      if (m == "none") so.reuseport_cpu = http::ServerOptions::ReuseportCpu::kNone;
+      else if (m == "self") so.reuseport_cpu = http::ServerOptions::ReuseportCpu::kSelf;
+      else if (m == "sibling") so.reuseport_cpu = http::ServerOptions::ReuseportCpu::kSibling;
+      else { fprintf(stderr, "hola: --reuseport-cpu none|self|sibling\n"); return 2; }
     } else if (a == "--conf") sysprops["conf"] = val("--conf");
     else if (a == "--deltaspike-properties") mo.deltaspike_properties = val("--deltaspike-properties");
     else if (a == "--hystrix-config") mo.hystrix_config = val("--hystrix-config");

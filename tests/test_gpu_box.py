@@ -303,3 +303,50 @@ def test_steering_keeps_one_l3s_clients_in_their_l3():
     loc = {l.split('"')[1]: int(float(l.split()[-1])) for l in metrics.splitlines()
            if l.startswith("hola_accept_locality_total{")}
     assert loc.get("same_l3", 0) + loc.get("same_core", 0) >= 24, loc
+
+
+def _two_l3s(n: int = 3):
+    from hola_amd.utils.cpu import allowed_cpus, l3_domain, physical_cores
+
+    by_dom: dict[int, list[int]] = {}
+    for c in physical_cores(allowed_cpus()):
+        by_dom.setdefault(l3_domain(c), []).append(c)
+    doms = [d for d, cs in by_dom.items() if len(cs) >= n][:2]
+    if len(doms) < 2:
+        pytest.skip(f"needs two L3 domains with {n} cores each")
+    return by_dom[doms[0]], by_dom[doms[1]]
+
+
+@pytest.mark.gpu
+def test_proxy_topology_hints_keep_sessions_in_the_clients_l3():
+    """hola_rrproxy with topology hints (backend h:p@cpus): a session accepted by the proxy
+    thread in the client's L3 goes to the replica in that L3, so client, proxy and server share
+    one cache domain (without hints the round-robin crosses L3s for half of them)."""
+    import socket
+
+    from hola_amd.parallel.replicas import RRProxy
+    from hola_amd.server import HolaProcess
+
+    x, y = _two_l3s()
+    with HolaProcess(threads=1, cpu_list=str(x[0]), env={"HOSTNAME": "x"}, log_level="warn") as a, \
+            HolaProcess(threads=1, cpu_list=str(y[0]), env={"HOSTNAME": "y"}, log_level="warn") as b, \
+            RRProxy([("127.0.0.1", a.port), ("127.0.0.1", b.port)], threads=2, cpu_list=f"{x[1]},{y[1]}",
+                    backend_cpus=[[x[0]], [y[0]]]) as px:
+        old = os.sched_getaffinity(0)
+        bodies = []
+        try:
+            for cpu, want in ((x[2], b"Hola de x"), (y[2], b"Hola de y")):
+                os.sched_setaffinity(0, {cpu})
+                for _ in range(16):
+                    with socket.create_connection(("127.0.0.1", px.port), timeout=5) as c:
+                        c.sendall(b"GET /api/hola HTTP/1.1\r\nHost: x\r\nConnection: close\r\n\r\n")
+                        data = b""
+                        while b"\r\n\r\n" not in data or not data.endswith(want):
+                            chunk = c.recv(4096)
+                            if not chunk:
+                                break
+                            data += chunk
+                    bodies.append((cpu, data.split(b"\r\n\r\n", 1)[-1] == want))
+        finally:
+            os.sched_setaffinity(0, old)
+    assert all(ok for _, ok in bodies), bodies

@@ -367,3 +367,40 @@ def test_targets_follow_replica_order():
     assert [p for _, p in rs.targets] == [40003, 40001, 40002]
     rs.ports = [40005] * 3  # a shared (reuseport) port: one address
     assert [p for _, p in rs.targets] == [40005]
+
+
+def test_reuseport_group_hands_connections_by_incoming_cpu(hola_bin):
+    """--accept reuseport --reuseport-cpu self: two replicas share one port, each worker's
+    listener names its own CPU as the incoming CPU, and the kernel (Linux 6.1+) hands each new
+    connection to the replica whose worker sits on the CPU the connection's SYN came from: the
+    replica-local placement client-side round-robin gets, without a client that knows the
+    replicas (profiles/round5/04_scale_mini)."""
+    import os
+    import socket
+
+    from hola_amd.server import HolaProcess
+    from hola_amd.utils.net import free_port
+
+    cpus = sorted(os.sched_getaffinity(0))
+    if len(cpus) < 2:
+        pytest.skip("needs two CPUs")
+    a_cpu, b_cpu = cpus[0], cpus[-1]
+    port = free_port()
+    args = ["--accept", "reuseport", "--reuseport-cpu", "self", "--no-tracing", "--log-level", "warn"]
+    with HolaProcess(args=args, env={"HOSTNAME": "a"}, port=port, threads=1, cpu_list=str(a_cpu)), \
+            HolaProcess(args=args, env={"HOSTNAME": "b"}, port=port, threads=1, cpu_list=str(b_cpu)):
+        old = os.sched_getaffinity(0)
+        seen = {}
+        try:
+            for cpu, want in ((a_cpu, b"Hola de a"), (b_cpu, b"Hola de b")):
+                os.sched_setaffinity(0, {cpu})
+                for _ in range(16):
+                    with socket.create_connection(("127.0.0.1", port), timeout=5) as c:
+                        c.sendall(b"GET /api/hola HTTP/1.1\r\nHost: x\r\nConnection: close\r\n\r\n")
+                        body = c.recv(4096).split(b"\r\n\r\n", 1)[1]
+                    seen.setdefault(cpu, []).append(body == want)
+        finally:
+            os.sched_setaffinity(0, old)
+    if os.uname().release.split(".")[:2] < ["6", "1"] and not all(all(v) for v in seen.values()):
+        pytest.skip("kernel without SO_INCOMING_CPU selection in reuseport groups")
+    assert all(all(v) for v in seen.values()), seen
