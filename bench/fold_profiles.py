@@ -93,6 +93,26 @@ def main() -> int:
         elif f.name == "err.log" and f.resolve() not in keep and not a.dry_run:
             f.unlink()  # a bench's stderr (gloo banners, build lines); nothing a report quotes
             removed += 1
+    # plain-text run logs: two or more unreferenced ones in a directory become one file with a
+    # header per log (same bytes, one tracked file)
+    logs: dict[Path, list[Path]] = {}
+    for f in files_all:
+        if f.suffix == ".log" and f.exists() and f.resolve() not in keep:
+            logs.setdefault(f.parent, []).append(f)
+    for d, fs in sorted(logs.items()):
+        if len(fs) < 2:
+            continue
+        print(f"{d.relative_to(ROOT)}: {len(fs)} logs -> logs.txt")
+        if a.dry_run:
+            continue
+        out = d / ("logs.txt" if not (d / "logs.txt").exists() else "logs_folded.txt")
+        with open(out, "a") as w:
+            for f in sorted(fs):
+                w.write(f"===== {f.name} =====\n")
+                w.write(f.read_text(errors="replace"))
+                w.write("\n")
+                f.unlink()
+                removed += 1
     for (d, table), files in sorted(by_dir.items()):
         if len(files) < a.min_files:
             continue
