@@ -76,6 +76,10 @@ def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--dry-run", action="store_true")
     ap.add_argument("--min-files", type=int, default=2)
+    ap.add_argument("--merge-sessions", default="",
+                    help="comma-separated round directories (e.g. round1,round2) whose session "
+                         "directories are merged into one session.txt each (every unreferenced text "
+                         "file under the session, with a header per file)")
     a = ap.parse_args()
     keep = referenced_paths()
     by_dir: dict[tuple[Path, str], list[Path]] = {}
@@ -139,6 +143,22 @@ def main() -> int:
         for f in gone:
             f.unlink()
             removed += 1
+    for rnd in filter(None, a.merge_sessions.split(",")):
+        for sess in sorted(p for p in (PROFILES / rnd).iterdir() if p.is_dir()):
+            members = [f for f in tracked(sess) if f.exists() and f.resolve() not in keep and f.name != "README.md"
+                       and f.suffix in (".txt", ".tsv", ".json", ".jsonl", ".log", ".md") and f.name != "session.txt"]
+            if len(members) < 2:
+                continue
+            print(f"{sess.relative_to(ROOT)}: {len(members)} files -> session.txt")
+            if a.dry_run:
+                continue
+            with open(sess / "session.txt", "a") as w:
+                for f in sorted(members):
+                    w.write(f"===== {f.relative_to(sess)} =====\n")
+                    w.write(f.read_text(errors="replace"))
+                    w.write("\n")
+                    f.unlink()
+                    removed += 1
     print(f"removed {removed} files")
     return 0
 
