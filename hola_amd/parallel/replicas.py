@@ -50,6 +50,7 @@ class ReplicaSet:
         self.supervise = supervise
         self.log_level = log_level
         self.shared_port = shared_port
+        self._base_port = base_port or (shared_port or 0)
         if shared_port is not None:
             self.shared_port = shared_port or free_port()
             self.ports = [self.shared_port] * n
@@ -68,16 +69,31 @@ class ReplicaSet:
         self._lock = threading.Lock()
         self._sup: threading.Thread | None = None
 
-    def _spawn(self, i: int) -> HolaProcess:
+    def _spawn(self, i: int, may_repick: bool = False) -> HolaProcess:
         cpus = self.cpu_plan[i] if self.cpu_plan else None
-        p = HolaProcess(args=self.args, env={**self.env, "HOSTNAME": f"replica-{i}"}, port=self.ports[i],
-                        threads=len(cpus) if cpus else self.threads,
-                        cpu_list=format_cpu_list(cpus) if cpus else None, log_level=self.log_level)
-        return p.start()
+        for attempt in range(4):
+            p = HolaProcess(args=self.args, env={**self.env, "HOSTNAME": f"replica-{i}"}, port=self.ports[i],
+                            threads=len(cpus) if cpus else self.threads,
+                            cpu_list=format_cpu_list(cpus) if cpus else None, log_level=self.log_level)
+            try:
+                return p.start()
+            except RuntimeError as e:
+                # A port picked by free_port() can be taken by another process before the
+                # replica binds it: pick again (a shared port only before its first replica).
+                # (Only at start-up: a restarted replica keeps its address.)
+                own_pick = may_repick and not self._base_port and (self.shared_port is None or i == 0)
+                if "Address already in use" not in str(e) or not own_pick or attempt == 3:
+                    raise
+                if self.shared_port is None:
+                    self.ports[i] = free_port()
+                else:
+                    self.shared_port = free_port()
+                    self.ports = [self.shared_port] * self.n
+        raise AssertionError("unreachable")
 
     def start(self, timeout: float = 30.0) -> "ReplicaSet":
         for i in range(self.n):
-            self.procs[i] = self._spawn(i)
+            self.procs[i] = self._spawn(i, may_repick=True)
             self._started[i] = time.monotonic()
         for i in range(self.n):
             if not wait_http("127.0.0.1", self.ports[i], timeout=timeout):
