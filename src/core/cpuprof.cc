@@ -5,6 +5,7 @@
 #include <linux/perf_event.h>
 #include <pthread.h>
 #include <sys/ioctl.h>
+#include <sched.h>
 #include <signal.h>
 #include <sys/syscall.h>
 #include <time.h>
@@ -43,6 +44,12 @@ long g_period_ns = 0;
 std::unique_ptr<Sample[]> g_samples;
 std::atomic<size_t> g_next{0};
 std::atomic<bool> g_on{false};
+// Sampling handlers running right now. write() turns g_on off and then waits for this to reach
+// 0 before it reads the samples: a handler that passed the g_on check just before may still be
+// filling its slot (the store of g_on and the load of this count, and the handler's increment
+// and its load of g_on, are sequentially consistent, so one of the two sides sees the other).
+// The handler's release decrement publishes its slot to write()'s acquire load.
+std::atomic<int> g_inflight{0};
 std::mutex g_mu;                  // g_names, g_timers
 std::vector<std::string> g_names;  // one per registered thread
 std::vector<timer_t> g_timers;
@@ -125,14 +132,19 @@ int walk(const ucontext_t* uc, uintptr_t* out, int max) {
 }
 
 void on_prof(int, siginfo_t*, void* ucv) {
-  if (!g_on.load(std::memory_order_relaxed) || t_index < 0) return;
-  const size_t i = g_next.fetch_add(1, std::memory_order_relaxed);
-  if (i >= kCapacity) return;
-  const int saved_errno = errno;
-  Sample& s = g_samples[i];
-  s.thread = uint16_t(t_index);
-  s.depth = uint8_t(walk(static_cast<const ucontext_t*>(ucv), s.pc, kDepth));
-  errno = saved_errno;
+  if (t_index < 0) return;
+  g_inflight.fetch_add(1, std::memory_order_seq_cst);
+  if (g_on.load(std::memory_order_seq_cst)) {
+    const size_t i = g_next.fetch_add(1, std::memory_order_relaxed);
+    if (i < kCapacity) {
+      const int saved_errno = errno;
+      Sample& s = g_samples[i];
+      s.thread = uint16_t(t_index);
+      s.depth = uint8_t(walk(static_cast<const ucontext_t*>(ucv), s.pc, kDepth));
+      errno = saved_errno;
+    }
+  }
+  g_inflight.fetch_sub(1, std::memory_order_release);
 }
 
 // ---- on-demand capture of another thread's stack (stall reports) ----
@@ -370,13 +382,15 @@ void unregister_thread() {
 }
 
 bool write() {
-  if (!g_on.exchange(false)) return false;
+  if (!g_on.exchange(false, std::memory_order_seq_cst)) return false;
   {
     std::lock_guard<std::mutex> g(g_mu);
     itimerspec off{};
     for (timer_t t : g_timers) timer_settime(t, 0, &off, nullptr);
     for (int fd : g_event_fds) ioctl(fd, PERF_EVENT_IOC_DISABLE, 0);
   }
+  // a handler already past its g_on check finishes its sample first (it runs for microseconds)
+  while (g_inflight.load(std::memory_order_acquire) != 0) sched_yield();
   const size_t n = std::min(g_next.load(), kCapacity);
   // identical (thread, stack) samples are written once with their count
   std::map<std::pair<int, std::vector<uintptr_t>>, uint64_t> stacks;

@@ -684,6 +684,12 @@ def test_a_stuck_worker_cannot_hold_the_termination_forever(hola):
     PTRACE_SEIZE, PTRACE_INTERRUPT, WALL = 0x4206, 0x4207, 0x40000000
     tid = next(int(t.name) for t in Path(f"/proc/{s.proc.pid}/task").iterdir()
                if (t / "comm").read_text().strip() == "hola-w1")
+    # the worker must be in its loop (blocked in epoll_wait) before it is stopped: a sanitizer
+    # build can still be starting it when the listener is up
+    deadline = time.monotonic() + 10
+    while "ep_poll" not in (Path(f"/proc/{s.proc.pid}/task/{tid}/wchan").read_text() or "") \
+            and time.monotonic() < deadline:
+        time.sleep(0.02)
     if libc.ptrace(PTRACE_SEIZE, tid, None, None) != 0:
         pytest.skip(f"ptrace not permitted here (errno {ctypes.get_errno()})")
     libc.ptrace(PTRACE_INTERRUPT, tid, None, None)
