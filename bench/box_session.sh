@@ -12,7 +12,7 @@
 #   rehearsal [Ns]     the driver's own N>1 command line (default N = 2 4 8) inside the box's
 #                      CPU slice, plus --profile-dir stage profiles for locality attribution
 #   locality           N = 1, 2, 4, 8 in the box's slice, L3-grouped vs. plain connection dealing
-#   scalemini [K]      the miniature weak-scaling curve: K physical cores per replica at the
+#   scalemini [K] [NS] [PLAIN]  the miniature weak-scaling curve: K physical cores per replica at the
 #                      8-slot node plan's places. bench.py's torchrun path at N = 1, 2, 4, 8 (node-plan
 #                      dealing, then plain round-robin dealing), then hola_amd.parallel.scaling with
 #                      client round-robin, reuseport and hola_rrproxy
@@ -148,16 +148,18 @@ locality)
   done
   ;;
 scalemini)
-  K=${1:-1}
-  for spec in "1|" "2|" "4|" "8|" "2|--plain-dealing" "4|--plain-dealing" "8|--plain-dealing"; do
+  # K = physical cores per replica; NS = the replica counts (K x N x 2 CPUs must fit the quota)
+  K=${1:-1}; NS=${2:-"1 2 4 8"}; PLAIN=${3:-"2 4 8"}
+  specs=(); for n in $NS; do specs+=("$n|"); done; for n in $PLAIN; do specs+=("$n|--plain-dealing"); done
+  for spec in "${specs[@]}"; do
     n=${spec%%|*}; extra=${spec#*|}; tag=n$n${extra:+_plain}
     timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$n" \
       --master-addr 127.0.0.1 --master-port $((29800 + n)) bench.py --gpus "$n" --gpu-slots 8 --slot-cores "$K" \
       --steps 10 --warmup 3 --c1-seconds 0 --deployed-seconds 0 --chain-seconds 0 --chain-shipped-seconds 0 \
       --alt-seconds 0 $extra > "$OUT/bench_$tag.json" 2> "$OUT/bench_err_$tag.log" || exit $?
   done
-  for lb in client reuseport proxy; do
-    ns=1,2,4,8; [ "$lb" = proxy ] && ns=1,2,4
+  for lb in ${LBS:-client reuseport proxy}; do
+    ns=$(echo $NS | tr ' ' ,); [ "$lb" = proxy ] && ns=${PROXY_NS:-1,2,4}
     timeout -k 10 400 python -m hola_amd.parallel.scaling --slot-cores "$K" --slots 8 --replicas $ns --lb $lb \
       --duration 10 --warmup 2 --busy-poll-us 20 --server-busy-poll auto --busy-poll-pause 16 \
       --out "$OUT/scaling_$lb.json" > "$OUT/scaling_$lb.log" 2>&1 || exit $?
