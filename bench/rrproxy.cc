@@ -80,6 +80,19 @@ std::atomic<uint64_t> g_rr{0};
 std::atomic<bool> g_stop{false};
 bool g_failover = true;
 
+// Why sessions ended other than by both sides' FIN, reported at exit: a client that sees a
+// reset can then be matched to its cause (the backend's side, its own side, or a connect).
+struct CloseStats {
+  std::atomic<uint64_t> sessions{0}, client_err{0}, backend_err{0}, connect_fail{0};
+  std::atomic<int> client_errno{0}, backend_errno{0}, connect_errno{0};
+};
+CloseStats g_close;
+
+void note_connect_fail(int err) {
+  g_close.connect_fail.fetch_add(1, std::memory_order_relaxed);
+  g_close.connect_errno.store(err, std::memory_order_relaxed);
+}
+
 const BackendSet& current_set() { return *g_set.load(std::memory_order_acquire); }
 
 // `l3` = the calling proxy thread's L3 domain (-1: unknown); `rr` = its own round-robin
@@ -194,6 +207,13 @@ void endpoints_loop(std::string path) {
   }
 }
 
+int socket_error(int fd) {
+  int e = 0;
+  socklen_t sl = sizeof e;
+  if (getsockopt(fd, SOL_SOCKET, SO_ERROR, &e, &sl) != 0) e = errno;
+  return e ? e : EIO;
+}
+
 void mark_down(Backend* b, int err) {
   if (b->healthy.exchange(false))
     fprintf(stderr, "rrproxy: backend %s:%d is DOWN (%s)\n", b->host.c_str(), b->port, strerror(err));
@@ -207,13 +227,17 @@ int connect_backend(Backend** chosen, bool* in_progress, int l3 = -1, uint64_t* 
   const size_t n = g_failover ? current_set().list.size() : 1;
   for (size_t tries = 0; tries < n; ++tries) {
     Backend* b = pick(l3, rr);
-    if (!b) return -1;
+    if (!b) {
+      note_connect_fail(EHOSTUNREACH);  // no healthy backend
+      return -1;
+    }
     int fd = connect_nonblocking(b->addr, b->len, in_progress);
     if (fd >= 0) {
       b->picked.fetch_add(1, std::memory_order_relaxed);
       *chosen = b;
       return fd;
     }
+    note_connect_fail(errno);
     // Out of local fds, memory or ephemeral ports: the next backend would fail the same
     // way, and none of them is at fault.
     if (is_local_resource_error(errno)) return -1;
@@ -249,6 +273,8 @@ struct Session : EventLoop::Handler {
   bool connecting = false;  // backend handshake not confirmed yet
   int failovers = 0;
   bool closed = false;
+  int err = 0;              // the first hard socket error (errno), 0 = none
+  bool err_client = false;  // ... and whether it was on the client's socket
   int64_t last_active_ms = 0;  // for the idle timeout
   Session *prev = nullptr, *next = nullptr;  // the owning loop's list of open sessions
 
@@ -262,6 +288,12 @@ struct Session : EventLoop::Handler {
   bool pump(bool from_client);
   void close();
   bool backend_connected(uint32_t ev);
+  void note_err(bool on_client, int e) {
+    if (err == 0 && e != 0) {
+      err = e;
+      err_client = on_client;
+    }
+  }
 };
 
 class ProxyLoop {
@@ -351,7 +383,9 @@ bool Session::flush(Pipe& p, int to) {
     ssize_t m = ::send(to, p.buf + p.off, p.len - p.off, MSG_NOSIGNAL);
     if (m < 0) {
       if (errno == EINTR) continue;
-      return errno == EAGAIN;
+      if (errno == EAGAIN) return true;
+      note_err(to == cfd, errno);
+      return false;
     }
     p.off += size_t(m);
   }
@@ -383,7 +417,9 @@ bool Session::pump(bool from_client) {
     }
     if (n < 0) {
       if (errno == EINTR) continue;
-      return errno == EAGAIN;
+      if (errno == EAGAIN) return true;
+      note_err(from_client, errno);
+      return false;
     }
     p.len = size_t(n);
     // A short read drained the source, unless this edge also carried its FIN: then read on
@@ -402,6 +438,7 @@ bool Session::backend_connected(uint32_t ev) {
     connecting = false;
     return true;
   }
+  note_connect_fail(soerr ? soerr : ECONNRESET);
   if (g_failover) mark_down(backend, soerr ? soerr : ECONNRESET);
   EventLoop& l = owner->loop();
   l.del(bfd);
@@ -423,7 +460,10 @@ void Session::on_event(bool client_side, uint32_t ev) {
     // The client is not read until the backend accepted, so a refusal can still fail over.
     if (client_side) {
       if (ev & (EPOLLRDHUP | EPOLLHUP)) c2b.hup = true;
-      if (ev & EPOLLERR) close();
+      if (ev & EPOLLERR) {
+        note_err(true, socket_error(cfd));
+        close();
+      }
       return;
     }
     if (!(ev & (EPOLLOUT | EPOLLERR | EPOLLHUP))) return;
@@ -436,6 +476,7 @@ void Session::on_event(bool client_side, uint32_t ev) {
     return;
   }
   bool ok = !(ev & EPOLLERR);
+  if (!ok) note_err(client_side, socket_error(client_side ? cfd : bfd));
   // Writable: deliver what was parked for this side, then read the other side again (it
   // was not read while the bytes waited).
   if (ok && (ev & EPOLLOUT)) {
@@ -453,6 +494,11 @@ void Session::on_event(bool client_side, uint32_t ev) {
 void Session::close() {
   if (closed) return;
   closed = true;
+  g_close.sessions.fetch_add(1, std::memory_order_relaxed);
+  if (err) {
+    (err_client ? g_close.client_err : g_close.backend_err).fetch_add(1, std::memory_order_relaxed);
+    (err_client ? g_close.client_errno : g_close.backend_errno).store(err, std::memory_order_relaxed);
+  }
   EventLoop& l = owner->loop();
   l.del(cfd);
   ::close(cfd);
@@ -647,5 +693,15 @@ int main(int argc, char** argv) {
   ::close(acc.fd);
   for (auto& b : g_backends)
     fprintf(stderr, "rrproxy: %s:%d picked %llu\n", b->host.c_str(), b->port, (unsigned long long)b->picked.load());
+  auto why = [](const std::atomic<uint64_t>& n, const std::atomic<int>& e) {
+    return n.load() ? strerror(e.load()) : "-";
+  };
+  fprintf(stderr,
+          "rrproxy: sessions closed %llu; on an error: client side %llu (last %s), backend side %llu (last %s); "
+          "backend connects failed %llu (last %s)\n",
+          (unsigned long long)g_close.sessions.load(), (unsigned long long)g_close.client_err.load(),
+          why(g_close.client_err, g_close.client_errno), (unsigned long long)g_close.backend_err.load(),
+          why(g_close.backend_err, g_close.backend_errno), (unsigned long long)g_close.connect_fail.load(),
+          why(g_close.connect_fail, g_close.connect_errno));
   return 0;
 }

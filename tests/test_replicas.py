@@ -116,6 +116,35 @@ def test_proxy_fails_over_on_refused_connect():
         rs.stop()
 
 
+def test_proxy_reports_why_sessions_ended():
+    """At exit the proxy accounts for sessions that ended on an error, by side, with the last
+    errno: a client that resets its connection, and a connect refused by a dead backend."""
+    import struct
+
+    rs = ReplicaSet(2, threads_per_replica=1, supervise=False).start()
+    try:
+        with RRProxy(rs.targets, health_ms=60000) as px:
+            sk = socket.create_connection(("127.0.0.1", px.port), timeout=5)
+            sk.sendall(b"GET /api/health HTTP/1.1\r\nHost: x\r\n\r\n")
+            assert sk.recv(4096).startswith(b"HTTP/1.1 200")
+            sk.setsockopt(socket.SOL_SOCKET, socket.SO_LINGER, struct.pack("ii", 1, 0))
+            sk.close()  # RST to the proxy
+            time.sleep(0.2)
+            rs.kill(0)
+            time.sleep(0.1)
+            for _ in range(4):  # one of these meets the dead backend and fails over
+                assert greeting_via(px.port) == "Hola de replica-1"
+            px.stop()
+            stats = [ln for ln in px.log().splitlines() if "sessions closed" in ln]
+    finally:
+        rs.stop()
+    assert len(stats) == 1, stats
+    line = stats[0]
+    assert "client side 1 (last Connection reset by peer)" in line, line
+    assert "backend side 0 (last -)" in line, line
+    assert "backend connects failed 1 (last Connection refused)" in line, line
+
+
 def test_supervisor_restarts_crashed_replica():
     with ReplicaSet(2, threads_per_replica=1, supervise=True) as rs:
         old = rs.procs[0].proc.pid

@@ -263,7 +263,9 @@ def test_sanitized_proxy_endpoints_mode(preset, tmp_path):
     text = log_path.read_text(errors="replace")
     assert "Sanitizer" not in text and "runtime error" not in text, text[-6000:]
     assert rc == 0, (rc, text[-3000:])
-    assert not errors, (errors[:5], text[-3000:])  # the proxy's own account of a failed session
+    stats = [ln for ln in text.splitlines() if "sessions closed" in ln]
+    assert stats, text[-3000:]  # the proxy's own account of why sessions ended
+    assert not errors, (errors[:5], stats, text[-3000:])
     assert int(applied) >= 30  # the follower acknowledged the sets as they came
 
 
