@@ -149,8 +149,10 @@ locality)
   ;;
 scalemini)
   # K = physical cores per replica; NS = the replica counts (K x N x 2 CPUs must fit the quota)
-  K=${1:-1}; NS=${2:-"1 2 4 8"}; PLAIN=${3:-"2 4 8"}
+  # PLAIN = the counts also run with --plain-dealing ("" = none); HARNESS_ONLY=1 skips bench.py
+  K=${1:-1}; NS=${2:-"1 2 4 8"}; PLAIN=${3-"2 4 8"}
   specs=(); for n in $NS; do specs+=("$n|"); done; for n in $PLAIN; do specs+=("$n|--plain-dealing"); done
+  [ "${HARNESS_ONLY:-0}" = 1 ] && specs=()
   for spec in "${specs[@]}"; do
     n=${spec%%|*}; extra=${spec#*|}; tag=n$n${extra:+_plain}
     timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$n" \

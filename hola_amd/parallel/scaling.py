@@ -24,7 +24,7 @@ import json
 import sys
 import time
 
-from hola_amd.parallel.hostmetrics import MetricsProbe, proc_cpu_s
+from hola_amd.parallel.hostmetrics import MetricsProbe, busy_fraction, cpu_times, proc_cpu_s
 from hola_amd.parallel.loadgen import ControlledLoadgen
 from hola_amd.parallel.subruns import counter_delta, locality_fraction, metrics_counters, timed_closed_loop
 from hola_amd.parallel.replicas import ReplicaSet, RRProxy
@@ -146,6 +146,7 @@ def run_point(n: int, args) -> dict:
         probes = [MetricsProbe("127.0.0.1", port) for port in rs.ports] if shared is None else []
         m0 = [metrics_counters(0, probe=pr) for pr in probes]
         cpu0 = [proc_cpu_s(pr.proc.pid) for pr in rs.procs]
+        t0 = cpu_times()
         if args.lb == "proxy":
             with RRProxy(rs.targets, threads=proxy_threads, cpu_list=format_cpu_list(p["proxy"]),
                          busy_poll_us=args.busy_poll_us if args.proxy_busy_poll_us < 0 else args.proxy_busy_poll_us,
@@ -156,11 +157,21 @@ def run_point(n: int, args) -> dict:
             res = _measure(rs.targets, conns, p["loadgen"], args, verify=args.lb == "client")
         m1 = [metrics_counters(0, probe=pr) for pr in probes]
         cpu1 = [proc_cpu_s(pr.proc.pid) for pr in rs.procs]
+        t1 = cpu_times()
         for pr in probes:
             pr.close()
+    # Per replica, over warm-up and timed run: requests, where its clients ran, its process's CPU
+    # time, its busy-poll spins / back-offs, and how busy its server CPUs and the CPUs of the
+    # client threads that drive it (slot plans: thread t drives replica t % n) were (/proc/stat: every task and interrupt on them). A replica
+    # whose CPUs read busier than its own CPU time shares them with something else.
+    drivers = [[c for t, c in enumerate(p["loadgen"]) if t % n == r] for r in range(n)]
     per_replica = [{"requests": int(b.get("requests", 0) - a.get("requests", 0)),
                     "locality": locality_fraction(counter_delta(a, b, "locality.")),
-                    "cpu_s": round(c1 - c0, 3)} for a, b, c0, c1 in zip(m0, m1, cpu0, cpu1)]
+                    "cpu_s": round(c1 - c0, 3), "spins": counter_delta(a, b, "spins."),
+                    "server_cpus_busy": busy_fraction(t0, t1, set(p["replicas"][r])),
+                    "client_cpus_busy": (busy_fraction(t0, t1, set(drivers[r]))
+                                         if args.lb == "client" and args.slot_cores else None)}
+                   for r, (a, b, c0, c1) in enumerate(zip(m0, m1, cpu0, cpu1))]
     lat = res["latency"]
     return {
         "replicas": n, "connections": conns, "lb": args.lb, "rps": res["rps"],
