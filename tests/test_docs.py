@@ -28,8 +28,10 @@ def test_operations_metrics_are_exported(hola):
 def test_operations_flags_are_accepted(hola_bin):
     import subprocess
 
-    help_text = subprocess.run([str(hola_bin), "--help"], capture_output=True, text=True).stdout + \
-        subprocess.run([str(hola_bin), "--help"], capture_output=True, text=True).stderr
+    help_text = ""
+    for exe in (hola_bin, hola_bin.parent / "hola_rrproxy"):  # the server's flags and the proxy's
+        r = subprocess.run([str(exe), "--help"], capture_output=True, text=True)
+        help_text += r.stdout + r.stderr
     flags = set(re.findall(r"`(--[a-z][a-z0-9-]+)", OPS)) - {"--replicas", "--out", "--lb", "--minutes", "--zipkin-sink",
                                                               "--profile-out", "--proxy-threads",
                                                               "--count", "--chain"}  # bench/instr_ab.py's
