@@ -91,6 +91,9 @@ class _AlohaHandler(BaseHTTPRequestHandler):
                              b"Content-Length: %d\r\n\r\n%s" % (len(body), body))
             self.wfile.flush()
             return
+        if mode == "interim":  # unasked-for 1xx responses before the final one (RFC 9110 §15.2)
+            self.wfile.write(b"HTTP/1.1 100 Continue\r\n\r\n"
+                             b"HTTP/1.1 103 Early Hints\r\nLink: </aloha.css>; rel=preload\r\n\r\n")
         if self.path != "/api/aloha-chaining":
             body, status = b"not found", 404
         elif mode == "error":
@@ -165,10 +168,13 @@ class _ZipkinHandler(BaseHTTPRequestHandler):
         body = self.rfile.read(n)
         with owner.lock:
             owner.posts.append({"path": self.path, "content_type": self.headers.get("Content-Type"),
-                                "spans": json.loads(body)})
-            status = owner.status
+                                "spans": json.loads(body), "peer_port": self.client_address[1]})
+            status, interim = owner.status, owner.interim
+        if interim:  # a 100 Continue nobody asked for, as some fronts send (RFC 9110 §15.2)
+            self.wfile.write(b"HTTP/1.1 100 Continue\r\n\r\n")
         self.send_response(status)
-        self.send_header("Content-Length", "0")
+        if status != 204:  # a 204 carries no Content-Length (RFC 9110 §8.6)
+            self.send_header("Content-Length", "0")
         self.end_headers()
 
 
@@ -176,10 +182,11 @@ class FakeZipkin(_Base):
     """Zipkin collector stand-in. With ``tls=(certfile, keyfile)`` it serves HTTPS (the URL
     becomes https://127.0.0.1:PORT/)."""
 
-    def __init__(self, status: int = 202, tls: tuple[str, str] | None = None):
+    def __init__(self, status: int = 202, tls: tuple[str, str] | None = None, interim: bool = False):
         self.lock = threading.Lock()
         self.posts: list[dict] = []
         self.status = status
+        self.interim = interim
         super().__init__(_ZipkinHandler)
         self.tls = tls
         if tls:

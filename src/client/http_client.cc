@@ -302,7 +302,8 @@ inline bool field_is(std::string_view k) {
   return true;
 }
 
-int parse_response(std::string_view in, bool eof, ClientResult* r, bool* close, size_t* consumed, bool* head_ok) {
+int parse_one(std::string_view in, bool eof, ClientResult* r, bool* close, size_t* consumed, bool* head_ok,
+              bool* interim) {
   // One pass over the head's lines (each newline found inline when the line is short,
   // core/scan.h): a find("\r\n\r\n") followed by a find("\r\n") and a find(':') per line
   // was a memchr call per candidate, most of this function's cycles (profiles/round4/
@@ -375,10 +376,11 @@ int parse_response(std::string_view in, bool eof, ClientResult* r, bool* close, 
   r->retry_after_ms = retry_after_ms;
   *close = conn_close;
   size_t body = p;
-  *head_ok = true;
+  *head_ok = true;  // the server has answered: the call is no longer safe to send again
   if (status == 204 || status == 304 || (status >= 100 && status < 200)) {
     r->status = status;
     *consumed = body;
+    *interim = status < 200 && status != 101;
     return 1;
   }
   if (chunked) {
@@ -407,6 +409,25 @@ int parse_response(std::string_view in, bool eof, ClientResult* r, bool* close, 
   *consumed = in.size();
   *close = true;
   return 1;
+}
+
+// parse_one() past any interim 1xx responses (100 Continue, 102 Processing, 103 Early Hints):
+// a client must accept them before the final response even unasked (RFC 9110 §15.2), and
+// HttpClient's request executor reads past every one. 101 ends the exchange (no upgrade here).
+int parse_response(std::string_view in, bool eof, ClientResult* r, bool* close, size_t* consumed, bool* head_ok) {
+  size_t off = 0;
+  for (;;) {
+    bool interim = false;
+    size_t used = 0;
+    const int rc = parse_one(in.substr(off), eof, r, close, &used, head_ok, &interim);
+    if (rc != 1) return rc;
+    off += used;
+    if (!interim) {
+      *consumed = off;
+      return 1;
+    }
+    r->clear();
+  }
 }
 }  // namespace
 

@@ -150,17 +150,27 @@ void BlockingConn::close() {
   fd = -1;
 }
 
-bool read_response(BlockingConn* c, BlockingResponse* out, bool* close_delimited) {
+bool read_response(BlockingConn* c, BlockingResponse* out, bool* close_delimited, bool head_request) {
   std::string buf;
-  size_t head_end;
+  size_t head_end, start = 0;
   for (;;) {
-    head_end = buf.find("\r\n\r\n");
-    if (head_end != std::string::npos) break;
-    if (buf.size() > 64 * 1024 || !recv_some(c, &buf)) return false;
+    for (;;) {
+      head_end = buf.find("\r\n\r\n", start);
+      if (head_end != std::string::npos) break;
+      if (buf.size() - start > 64 * 1024 || !recv_some(c, &buf)) return false;
+    }
+    std::string_view head(buf.data() + start, head_end - start);
+    if (head.size() < 12 || head.substr(0, 5) != "HTTP/") return false;
+    out->status = atoi(std::string(head.substr(9, 3)).c_str());
+    // Interim responses (100 Continue, 102, 103) come before the final one, asked for or not
+    // (RFC 9110 §15.2): read past them. 101 would switch protocols; there is no upgrade here.
+    if (out->status >= 100 && out->status < 200 && out->status != 101) {
+      start = head_end + 4;
+      continue;
+    }
+    break;
   }
-  std::string_view head(buf.data(), head_end);
-  if (head.size() < 12 || head.substr(0, 5) != "HTTP/") return false;
-  out->status = atoi(std::string(head.substr(9, 3)).c_str());
+  std::string_view head(buf.data() + start, head_end - start);
   out->headers = std::string(head);
   int64_t cl = -1;
   bool chunked = false, conn_close = false;
@@ -180,6 +190,14 @@ bool read_response(BlockingConn* c, BlockingResponse* out, bool* close_delimited
   }
   size_t body_start = head_end + 4;
   *close_delimited = conn_close;
+  // No body whatever the headers say (RFC 9110 §6.3): a response to HEAD, 1xx, 204 and 304.
+  // Reading one until the peer closes would hold the caller to its timeout (a collector that
+  // answers a POST with a bare 204) and leave the connection out of step.
+  if (head_request || out->status == 204 || out->status == 304 || out->status < 200) {
+    out->body.clear();
+    if (buf.size() > body_start) *close_delimited = true;  // bytes nobody asked for: drop the connection
+    return true;
+  }
   if (chunked) {
     std::string body;
     for (;;) {
@@ -242,7 +260,7 @@ bool blocking_request(const Url& u, BlockingConn* c, const sockaddr_storage* add
       req.append("Content-Length: ").append(std::to_string(body.size())).append("\r\n");
     req.append("\r\n").append(body);
     bool closed = false;
-    if (io_write_all(c, req.data(), req.size()) && read_response(c, out, &closed)) {
+    if (io_write_all(c, req.data(), req.size()) && read_response(c, out, &closed, method == "HEAD")) {
       if (closed) c->close();
       return true;
     }

@@ -53,6 +53,6 @@ bool blocking_request(const Url& u, int* fd, std::string_view method, std::strin
                       BlockingResponse* out);
 // Reads one HTTP/1.1 response (Content-Length / chunked / close-delimited) from a blocking
 // connection.
-bool read_response(BlockingConn* c, BlockingResponse* out, bool* close_delimited);
+bool read_response(BlockingConn* c, BlockingResponse* out, bool* close_delimited, bool head_request = false);
 
 }  // namespace hola::client

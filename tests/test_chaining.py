@@ -59,6 +59,20 @@ def test_header_name_with_a_cr_is_not_a_known_field(hola, aloha):
         assert chain(s) == ["Hola de h", "Aloha mai aloha-1", "Bonjour de bonjour-1"]
 
 
+@pytest.mark.parametrize("pipeline", [1, 8])
+def test_interim_1xx_responses_are_read_past(hola, aloha, pipeline):
+    """aloha (or a front) sends 100 Continue and 103 Early Hints before each final response,
+    unasked: HttpClient reads past interim responses, so the call succeeds (not A's fallback)
+    and the connection stays in step for the next call, pipelined or not."""
+    aloha.set_mode("interim")
+    s = hola(args=["--aloha-url", aloha.url, "--no-tracing", "--feign-log", "none",
+                   "--aloha-pipeline", str(pipeline)], env={"HOSTNAME": "h"}, threads=1)
+    for _ in range(4):
+        assert chain(s) == ["Hola de h", "Aloha mai aloha-1", "Bonjour de bonjour-1"]
+    assert len({r["peer_port"] for r in aloha.requests}) == 1  # one kept-alive connection
+    assert _events(s).get("SUCCESS") == 4
+
+
 def _events(s) -> dict:
     """Rolling Hystrix event counts of the aloha command from /metrics."""
     _, _, body = s.get("/metrics")

@@ -164,6 +164,24 @@ def test_https_urls_parse(native):
     assert native.parse_url("ftp://x") is None
 
 
+def test_collector_interim_and_bare_204_answers(hola):
+    """A collector (or a front) that answers each POST with an unasked-for 100 Continue and
+    then a 204 without Content-Length: the reporter reads past the 1xx, takes the 204 as
+    bodiless instead of reading to the connection's close (its 2 s timeout), and keeps the
+    connection for the next flush."""
+    with FakeZipkin(status=204, interim=True) as z:
+        s = hola(args=["--zipkin-url", z.url.rstrip("/")])
+        t0 = time.monotonic()
+        for k in range(1, 4):
+            assert s.get("/api/hola")[0] == 200
+            z.wait_for(lambda sp, k=k: len(sp) >= k, timeout=5)
+        elapsed = time.monotonic() - t0
+        assert len(z.spans()) == 3, z.posts
+        assert elapsed < 4.5, elapsed  # one ~1 s flush each, no 2 s read timeouts
+        assert _post_failures(s) == 0
+        assert len({p["peer_port"] for p in z.posts}) == 1  # one kept-alive connection throughout
+
+
 def test_spans_flushed_on_shutdown(hola_bin, zipkin):
     from hola_amd.server import HolaProcess
 
