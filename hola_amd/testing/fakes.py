@@ -91,6 +91,20 @@ class _AlohaHandler(BaseHTTPRequestHandler):
                              b"Content-Length: %d\r\n\r\n%s" % (len(body), body))
             self.wfile.flush()
             return
+        if mode == "cl_unparseable":  # HttpClient's lax strategy: the last parseable Content-Length wins
+            body = json.dumps(payload).encode()
+            self.wfile.write(b"HTTP/1.1 200 OK\r\nContent-Type: application/json\r\nContent-Length: %d\r\n"
+                             b"Content-Length: 12abc\r\n\r\n%s" % (len(body), body))
+            self.wfile.flush()
+            return
+        if mode == "te_not_chunked":  # a transfer coding other than chunked: the body runs to the close
+            body = json.dumps(payload).encode()
+            self.close_connection = True
+            self.wfile.write(b"HTTP/1.1 200 OK\r\nContent-Type: application/json\r\nTransfer-Encoding: identity\r\n"
+                             b"Content-Length: 2\r\n\r\n%s" % body)
+            self.wfile.flush()
+            self.connection.shutdown(socket.SHUT_WR)
+            return
         if mode == "interim":  # unasked-for 1xx responses before the final one (RFC 9110 §15.2)
             self.wfile.write(b"HTTP/1.1 100 Continue\r\n\r\n"
                              b"HTTP/1.1 103 Early Hints\r\nLink: </aloha.css>; rel=preload\r\n\r\n")

@@ -302,6 +302,41 @@ inline bool field_is(std::string_view k) {
   return true;
 }
 
+std::string_view trim_ows(std::string_view v) {
+  while (!v.empty() && (v.front() == ' ' || v.front() == '\t')) v.remove_prefix(1);
+  while (!v.empty() && (v.back() == ' ' || v.back() == '\t')) v.remove_suffix(1);
+  return v;
+}
+
+// Content-Length as HttpClient 4.5's LaxContentLengthStrategy reads it: the last header whose
+// value parses as a Java long wins (a negative one means "to the close"), one that does not
+// parse is skipped, none leaves *cl at -1. Values over the body cap stay over it.
+void content_length(std::string_view v, int64_t* cl) {
+  v = trim_ows(v);
+  bool neg = false;
+  if (!v.empty() && (v.front() == '+' || v.front() == '-')) {
+    neg = v.front() == '-';
+    v.remove_prefix(1);
+  }
+  if (v.empty() || v.size() > 19) return;
+  int64_t x = 0;
+  for (char d : v) {
+    if (d < '0' || d > '9') return;
+    if (x <= (1 << 20)) x = x * 10 + (d - '0');
+  }
+  *cl = neg ? -1 : x;
+}
+
+// Transfer-Encoding as HttpClient 4.5 reads the first such header: chunked when its last
+// coding is "chunked" (RFC 9112 §6.1: chunked must be applied last); any other value means the
+// body runs to the close, Content-Length notwithstanding.
+bool last_coding_is_chunked(std::string_view v) {
+  const size_t comma = v.rfind(',');
+  std::string_view last = comma == std::string_view::npos ? v : v.substr(comma + 1);
+  if (const size_t semi = last.find(';'); semi != std::string_view::npos) last = last.substr(0, semi);
+  return http::iequals(trim_ows(last), "chunked");
+}
+
 int parse_one(std::string_view in, bool eof, ClientResult* r, bool* close, size_t* consumed, bool* head_ok,
               bool* interim) {
   // One pass over the head's lines (each newline found inline when the line is short,
@@ -327,7 +362,7 @@ int parse_one(std::string_view in, bool eof, ClientResult* r, bool* close, size_
   if (status < 100) return -1;
   const bool http10 = head.substr(5, 3) == "1.0";
   int64_t cl = -1;
-  bool chunked = false;
+  bool chunked = false, te_seen = false;
   bool has_retry_after = false;
   int64_t retry_after_ms = 0;
   bool conn_close = http10;
@@ -346,17 +381,13 @@ int parse_one(std::string_view in, bool eof, ClientResult* r, bool* close, size_
     while (!v.empty() && (v.front() == ' ' || v.front() == '\t')) v.remove_prefix(1);
     switch (k.size()) {
       case 14:
-        if (field_is<"content-length">(k)) {
-          cl = 0;
-          for (char d : v) {
-            if (d < '0' || d > '9') break;
-            cl = cl * 10 + (d - '0');
-            if (cl > (1 << 20)) break;  // over the body cap: rejected below
-          }
-        }
+        if (field_is<"content-length">(k)) content_length(v, &cl);
         break;
       case 17:
-        if (field_is<"transfer-encoding">(k) && v.find("chunked") != std::string_view::npos) chunked = true;
+        if (field_is<"transfer-encoding">(k) && !te_seen) {
+          te_seen = true;
+          chunked = last_coding_is_chunked(v);
+        }
         break;
       case 10:
         if (field_is<"connection">(k)) {
@@ -371,6 +402,7 @@ int parse_one(std::string_view in, bool eof, ClientResult* r, bool* close, size_
         break;
     }
   }
+  if (te_seen && !chunked) cl = -1;  // another transfer coding: the body runs to the close
   r->reason.assign(head.size() > 13 && head[12] == ' ' ? head.substr(13) : std::string_view());
   r->has_retry_after = has_retry_after;
   r->retry_after_ms = retry_after_ms;
@@ -430,6 +462,11 @@ int parse_response(std::string_view in, bool eof, ClientResult* r, bool* close, 
   }
 }
 }  // namespace
+
+int parse_response_probe(std::string_view in, bool eof, ClientResult* r, bool* close, size_t* consumed,
+                         bool* head_ok) {
+  return parse_response(in, eof, r, close, consumed, head_ok);
+}
 
 int ClientPool::Conn::try_parse(ClientResult* r, bool* keep, bool eof) {
   bool close = false;

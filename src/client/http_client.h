@@ -79,6 +79,11 @@ struct ClientResult {
 // clock, negative for a date in the past); false when it cannot be parsed.
 bool parse_retry_after(std::string_view v, int64_t now_ms, int64_t* out_ms);
 
+// The pool's response parser on its own (tests): one response from the front of `in`;
+// 1 = complete (*consumed bytes), 0 = need more, -1 = malformed.
+int parse_response_probe(std::string_view in, bool eof, ClientResult* r, bool* close, size_t* consumed,
+                         bool* head_ok);
+
 class ClientPool {
  public:
   using Callback = std::function<void(ClientResult&&)>;

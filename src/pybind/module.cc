@@ -559,6 +559,14 @@ PYBIND11_MODULE(_native, m) {
   }, py::arg("attempt"), py::arg("policy") = "default");
   m.def("stall_report_probe", &stall_report_probe);
   m.def("inline_function_selftest", &inline_function_selftest);
+  m.def("client_parse_response", [](py::bytes data, bool eof) {
+    std::string in = data;
+    client::ClientResult r;
+    bool close = false, head_ok = false;
+    size_t consumed = 0;
+    const int rc = client::parse_response_probe(in, eof, &r, &close, &consumed, &head_ok);
+    return py::make_tuple(rc, r.status, py::bytes(r.body), close, consumed, head_ok);
+  }, py::arg("data"), py::arg("eof") = false);
   m.def("client_next_generation", [](uint32_t g) { return client::ClientPool::next_generation(g); });
   m.def("loop_lost_epoll_probe", &loop_lost_epoll_probe);
   m.def("loop_timer_order", &loop_timer_order, py::arg("delays"), py::arg("cancel") = std::vector<int>{});

@@ -59,6 +59,19 @@ def test_header_name_with_a_cr_is_not_a_known_field(hola, aloha):
         assert chain(s) == ["Hola de h", "Aloha mai aloha-1", "Bonjour de bonjour-1"]
 
 
+@pytest.mark.parametrize("mode", ["cl_unparseable", "te_not_chunked"])
+def test_response_framing_as_httpclient_reads_it(hola, aloha, mode):
+    """Framing read like HttpClient 4.5's LaxContentLengthStrategy: a Content-Length that
+    does not parse as a number is skipped for the one before it, and a Transfer-Encoding whose
+    last coding is not chunked makes the body run to the connection's close, whatever
+    Content-Length says (RFC 9112 §6.3)."""
+    aloha.set_mode(mode)
+    s = hola(args=["--aloha-url", aloha.url, "--no-tracing", "--feign-log", "none"], env={"HOSTNAME": "h"})
+    for _ in range(2):
+        assert chain(s) == ["Hola de h", "Aloha mai aloha-1", "Bonjour de bonjour-1"]
+    assert _events(s).get("SUCCESS") == 2
+
+
 @pytest.mark.parametrize("pipeline", [1, 8])
 def test_interim_1xx_responses_are_read_past(hola, aloha, pipeline):
     """aloha (or a front) sends 100 Continue and 103 Early Hints before each final response,

@@ -284,3 +284,65 @@ def test_retry_after_seconds_and_dates(native, secs, skew_s):
     now_ms = 1_700_000_000_000
     date = email.utils.formatdate(now_ms / 1000 + skew_s, usegmt=True)
     assert native.parse_retry_after(date, now_ms) == skew_s * 1000
+
+
+# ---- the aloha client's response parser (src/client/http_client.cc) ----
+
+@settings(max_examples=800, deadline=None)
+@given(st.one_of(st.binary(max_size=300),
+                 st.lists(st.sampled_from([b"HTTP/1.1 ", b"200", b"100", b"204", b" OK", b"\r\n", b"\n", b":",
+                                           b"Content-Length", b"content-length", b"Transfer-Encoding", b"chunked",
+                                           b"Connection", b"close", b" 5", b"-1", b"+3", b"0\r\n\r\n", b"abc",
+                                           b"\x00", b"\r"]), max_size=30).map(b"".join)),
+       st.booleans())
+def test_fuzz_client_response_parser_total(native, data, eof):
+    rc, status, body, close, consumed, head_ok = native.client_parse_response(data, eof)
+    assert rc in (-1, 0, 1)
+    if rc == 1:
+        assert 0 < consumed <= len(data) and status >= 100 and head_ok
+        assert len(body) <= consumed
+
+
+_resp_body = st.binary(max_size=60)
+
+
+@settings(max_examples=300, deadline=None)
+@given(_resp_body, st.sampled_from(["length", "chunked", "close"]), st.integers(min_value=0, max_value=2),
+       st.lists(st.tuples(st.sampled_from(["X-A", "Retry-After", "Vary", "Content-Type"]),
+                          st.text(alphabet="abc 123;=,", max_size=12)), max_size=3),
+       st.integers(min_value=1, max_value=23))
+def test_client_response_parser_prefixes_and_whole(native, body, framing, interims, headers, cut):
+    """A well-formed response after 0-2 interim ones: every proper prefix needs more, the whole
+    parses to the body with every byte consumed, and bytes after it are left alone."""
+    head = b"".join(b"HTTP/1.1 100 Continue\r\n\r\n" if i % 2 == 0 else b"HTTP/1.1 103 Early Hints\r\nLink: </x>\r\n\r\n"
+                    for i in range(interims))
+    head += b"HTTP/1.1 200 OK\r\n" + b"".join(f"{k}: {v.strip()}\r\n".encode() for k, v in headers)
+    if framing == "length":
+        raw = head + b"Content-Length: %d\r\n\r\n" % len(body) + body
+    elif framing == "chunked":
+        chunks = [body[i:i + 7] for i in range(0, len(body), 7)]
+        raw = head + b"Transfer-Encoding: chunked\r\n\r\n" + b"".join(b"%x\r\n%s\r\n" % (len(c), c) for c in chunks) + b"0\r\n\r\n"
+    else:
+        raw = head + b"Connection: close\r\n\r\n" + body
+    for i in range(0, len(raw), cut):
+        rc = native.client_parse_response(raw[:i], False)[0]
+        assert rc == 0, (i, raw[:i])
+    rc, status, got, close, consumed, head_ok = native.client_parse_response(raw, framing == "close")
+    assert (rc, status, got, consumed) == (1, 200, body, len(raw))
+    assert close == (framing == "close")
+    if framing != "close":  # a pipelined next response is not part of this one
+        rc2, _, got2, _, consumed2, _ = native.client_parse_response(raw + b"HTTP/1.1 200 OK\r\n", False)
+        assert (rc2, got2, consumed2) == (1, body, len(raw))
+
+
+@pytest.mark.parametrize("raw,body", [
+    (b"HTTP/1.1 200 OK\r\nContent-Length: 2\r\nContent-Length: 12abc\r\n\r\n[]", b"[]"),  # last parseable wins
+    (b"HTTP/1.1 200 OK\r\nContent-Length: 9\r\nContent-Length: 2\r\n\r\n[]", b"[]"),
+    (b"HTTP/1.1 200 OK\r\nContent-Length:  +2 \r\n\r\n[]", b"[]"),
+    (b"HTTP/1.1 200 OK\r\nTransfer-Encoding: gzip, chunked\r\n\r\n2\r\n[]\r\n0\r\n\r\n", b"[]"),
+    (b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked, identity\r\nContent-Length: 1\r\n\r\n[]", b"[]"),  # to the close
+    (b"HTTP/1.1 200 OK\r\nContent-Length: -1\r\n\r\n[]", b"[]"),  # negative: to the close
+])
+def test_client_response_framing_cases(native, raw, body):
+    rc, status, got, close, consumed, _ = native.client_parse_response(raw, True)
+    assert (rc, status, got, consumed) == (1, 200, body, len(raw))
