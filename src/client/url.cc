@@ -190,18 +190,21 @@ bool read_response(BlockingConn* c, BlockingResponse* out, bool* close_delimited
   }
   size_t body_start = head_end + 4;
   *close_delimited = conn_close;
+  // Below, bytes after the response were not asked for: the connection is out of step and is
+  // dropped (*close_delimited).
   // No body whatever the headers say (RFC 9110 §6.3): a response to HEAD, 1xx, 204 and 304.
   // Reading one until the peer closes would hold the caller to its timeout (a collector that
   // answers a POST with a bare 204) and leave the connection out of step.
   if (head_request || out->status == 204 || out->status == 304 || out->status < 200) {
     out->body.clear();
-    if (buf.size() > body_start) *close_delimited = true;  // bytes nobody asked for: drop the connection
+    if (buf.size() > body_start) *close_delimited = true;
     return true;
   }
   if (chunked) {
     std::string body;
+    size_t consumed = 0;
     for (;;) {
-      size_t consumed = 0;
+      consumed = 0;
       body.clear();
       http::Parse p = http::decode_chunked_body(buf.data() + body_start, buf.size() - body_start, &consumed, &body);
       if (p == http::Parse::kError) return false;
@@ -209,6 +212,7 @@ bool read_response(BlockingConn* c, BlockingResponse* out, bool* close_delimited
       if (buf.size() > (1 << 20) || !recv_some(c, &buf)) return false;
     }
     out->body = std::move(body);
+    if (buf.size() > body_start + consumed) *close_delimited = true;
     return true;
   }
   if (cl >= 0) {
@@ -216,6 +220,7 @@ bool read_response(BlockingConn* c, BlockingResponse* out, bool* close_delimited
     while (buf.size() - body_start < size_t(cl))
       if (!recv_some(c, &buf)) return false;
     out->body = buf.substr(body_start, size_t(cl));
+    if (buf.size() > body_start + size_t(cl)) *close_delimited = true;
     return true;
   }
   // close-delimited
