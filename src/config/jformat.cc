@@ -1,5 +1,6 @@
 #include "config/jformat.h"
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 
@@ -99,6 +100,28 @@ bool parse_int(std::string_view s, size_t* i, int* out) {
   return true;
 }
 
+// Digits as Formatter's width()/precision() read them: a value past Integer.MAX_VALUE fails
+// Integer.parseInt, which Formatter reports as an illegal width/precision of MIN_VALUE.
+bool parse_long(std::string_view s, size_t* i, long long* out) {
+  size_t st = *i;
+  long long v = 0;
+  while (*i < s.size() && s[*i] >= '0' && s[*i] <= '9') {
+    v = v * 10 + (s[*i] - '0');
+    if (v > 1000000000000LL) v = 1000000000000LL;
+    ++*i;
+  }
+  if (*i == st) return false;
+  *out = v;
+  return true;
+}
+constexpr long long kIntMax = 2147483647LL;
+
+// The reference's JVM runs with -Xmx512m (the manifests' JAVA_OPTIONS), so a translation
+// whose widths pad the greeting to hundreds of millions of characters ends in an
+// OutOfMemoryError, a 500. The output here is bounded well below that (32 Mi code units), so
+// such a configuration costs a 500 per request instead of the process's memory.
+constexpr size_t kMaxOutput = size_t(32) << 20;
+
 void justify(std::string* out, const std::vector<uint32_t>& cps, int width, bool left) {
   size_t len = utf16_len(cps);
   std::string body = encode(cps);
@@ -155,11 +178,16 @@ FormatResult java_format(std::string_view fmt, const std::vector<std::string>& a
       sp.flags.push_back(fmt[i]);
       ++i;
     }
-    if (parse_int(fmt, &i, &n)) sp.width = n;
+    long long wide = 0;
+    if (parse_long(fmt, &i, &wide)) {
+      if (wide > kIntMax) return fail("IllegalFormatWidthException", "-2147483648");
+      sp.width = int(wide);
+    }
     if (i < fmt.size() && fmt[i] == '.') {
       size_t j = i + 1;
-      if (parse_int(fmt, &j, &n)) {
-        sp.precision = n;
+      if (parse_long(fmt, &j, &wide)) {
+        if (wide > kIntMax) return fail("IllegalFormatPrecisionException", "-2147483648");
+        sp.precision = int(wide);
         i = j;
       } else {
         return fail("UnknownFormatConversionException", "Conversion = '.'");
@@ -196,6 +224,7 @@ FormatResult java_format(std::string_view fmt, const std::vector<std::string>& a
       for (char f : sp.flags)
         if (f != '-') return fail("IllegalFormatFlagsException", "Flags = '" + sp.flags + "'");
       if (left && sp.width < 0) return fail("MissingFormatWidthException", "%-%");
+      if (size_t(std::max(sp.width, 0)) + out.size() > kMaxOutput) return fail("OutOfMemoryError", "Java heap space");
       justify(&out, {uint32_t('%')}, sp.width, left);
       continue;
     }
@@ -210,6 +239,7 @@ FormatResult java_format(std::string_view fmt, const std::vector<std::string>& a
     if (idx < 0 || size_t(idx) >= args.size())
       return fail("MissingFormatArgumentException", std::string("Format specifier '%") + c + "'");
     last = idx;
+    if (size_t(std::max(sp.width, 0)) + out.size() > kMaxOutput) return fail("OutOfMemoryError", "Java heap space");
     const std::string& arg = args[size_t(idx)];
     switch (c) {
       case 's':
@@ -263,6 +293,7 @@ FormatResult java_format(std::string_view fmt, const std::vector<std::string>& a
         return fail("IllegalFormatConversionException", std::string(1, c) + " != java.lang.String");
     }
   }
+  if (out.size() > kMaxOutput) return fail("OutOfMemoryError", "Java heap space");
   FormatResult r;
   r.value = std::move(out);
   return r;

@@ -69,10 +69,20 @@ def test_precision_and_width_count_utf16_units(native):
     ("%5n", "IllegalFormatWidthException"),
     ("%.2%", "IllegalFormatPrecisionException"),
     ("%--5s", "DuplicateFormatFlagsException"),
+    ("%99999999999s", "IllegalFormatWidthException"),  # past Integer.MAX_VALUE: MIN_VALUE
+    ("%.3000000000s", "IllegalFormatPrecisionException"),
+    ("%100000000s", "OutOfMemoryError"),  # the JVM's -Xmx512m heap; bounded here (32 Mi units)
+    ("%20000000s%1$20000000s", "OutOfMemoryError"),
 ])
 def test_exceptions(native, f, exc):
     r = fmt(native, f, "h")
     assert isinstance(r, tuple) and r[0] == exc
+
+
+def test_width_overflow_detail_and_large_but_bounded_widths(native):
+    assert fmt(native, "%99999999999s", "h") == ("IllegalFormatWidthException", "-2147483648")
+    out = fmt(native, "%1000000s", "h")
+    assert isinstance(out, bytes) and len(out) == 1000000 and out.endswith(b" h")
 
 
 def test_format_error_is_500(hola, tmp_path):
