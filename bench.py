@@ -676,6 +676,9 @@ def _chain_keys(c: dict | None, p: str) -> dict:
            # A's Hystrix command over the sub-run (its warm-up included)
            f"{p}_hystrix_success": h.get("SUCCESS", 0), f"{p}_hystrix_fallback": h.get("FALLBACK_SUCCESS", 0),
            f"{p}_hystrix_timeout": h.get("TIMEOUT", 0), f"{p}_hystrix_events": h,
+           # A's circuit breaker: openings, and closings by the sleep window's trial or by a call
+           # that was already running when it opened
+           f"{p}_circuit": c.get("circuit", {}),
            # busy share of the sub-run's CPUs and of their SMT siblings outside the job
            f"{p}_host_load": c["host_load"],
            # client thread vs serving worker of every connection accepted in the sub-run, per hop

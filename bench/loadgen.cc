@@ -14,6 +14,9 @@
 //   --control                   stdin protocol used by bench.py:
 //        run <R>     every connection completes exactly R requests; replies
 //                    {"elapsed_ns":..,"requests":..,"errors":..}
+//        runfor <MS> every connection sends back to back for MS milliseconds, then finishes
+//                    the request it has in flight; same reply (one continuous run, where a
+//                    series of `run`s leaves every connection idle between them)
 //        stats       {"count":..,"p50_ns":..,...,"hist":"bin:count,..."} (since last reset)
 //        reset       clears the histogram
 //        quit
@@ -946,19 +949,35 @@ int main(int argc, char** argv) {
   std::string line;
   uint64_t gen = 0;
   while (std::getline(std::cin, line)) {
-    if (line.rfind("run ", 0) == 0) {
-      int64_t q = atoll(line.c_str() + 4);
+    const bool run_for = line.rfind("runfor ", 0) == 0;
+    if (run_for && o.per_conn_quota) {
+      printf("{\"error\":\"runfor needs the shared budget (no --per-conn-quota)\"}\n");
+      fflush(stdout);
+    } else if (run_for || line.rfind("run ", 0) == 0) {
+      const int64_t q = run_for ? INT64_MAX / 4 : atoll(line.c_str() + 4);
+      const int64_t for_ms = run_for ? atoll(line.c_str() + 7) : 0;
       ++gen;
       int64_t t0 = mono_ns();
-      // Budgets count batches: with --pipeline P, a claim is P requests.
+      // Budgets count batches: with --pipeline P, a claim is P requests. A timed run starts
+      // with a budget no run can use up and has it taken away at the deadline: each thread then
+      // finishes the requests it holds (at most a claim batch), and the run ends.
       const int64_t P = o.pipeline;
-      g_budget.store((q * int64_t(o.connections) + P - 1) / P);
+      g_budget.store(run_for ? INT64_MAX / 4 : (q * int64_t(o.connections) + P - 1) / P);
       for (auto& t : ts) {
         t->run_quota.store(std::max<int64_t>(1, (q + P - 1) / P));
         t->run_gen.store(gen);
         uint64_t one = 1;
         ssize_t w = ::write(t->wakefd, &one, sizeof one);
         (void)w;
+      }
+      if (run_for) {
+        const int64_t deadline = t0 + for_ms * 1000000;
+        for (int64_t now = mono_ns(); now < deadline && !g_stop.load(); now = mono_ns()) {
+          const int64_t left = deadline - now;
+          struct timespec d {left / 1000000000, left % 1000000000};
+          nanosleep(&d, nullptr);
+        }
+        g_budget.store(INT64_MIN / 4);
       }
       uint64_t reqs = 0, errs = 0;
       for (size_t k = 0; k < ts.size(); ++k) {

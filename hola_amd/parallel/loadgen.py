@@ -121,6 +121,11 @@ class ControlledLoadgen:
     def run(self, reqs_per_conn: int) -> dict:
         return self._cmd(f"run {reqs_per_conn}")
 
+    def run_for(self, seconds: float) -> dict:
+        """One continuous closed-loop run of `seconds` (every connection sends back to back,
+        then finishes its request in flight): no idle gap inside it, as a series of `run`s has."""
+        return self._cmd(f"runfor {max(1, int(round(seconds * 1000)))}")
+
     def stats(self) -> dict:
         return self._cmd("stats")
 

@@ -83,6 +83,10 @@ def metrics_counters(port: int, host: str = "127.0.0.1", probe: MetricsProbe | N
             out["spins.resumes"] = float(val)
         elif name.startswith("hola_hystrix_events_total{"):
             out["hystrix." + name.split('event="')[1].split('"')[0]] = float(val)
+        elif name.startswith("hola_hystrix_circuit_transitions_total{"):
+            to = name.split('to="')[1].split('"')[0]
+            by = name.split('by="')[1].split('"')[0] if 'by="' in name else ""
+            out["circuit." + (f"{to}_{by}" if by else to)] = float(val)
         elif name == "hola_http_requests_total":
             out["requests"] = float(val)
     return out
@@ -204,26 +208,20 @@ def free_port_block(start: int, n: int, host: str = "127.0.0.1") -> int:
 
 def timed_closed_loop(lg: ControlledLoadgen, connections: int, seconds: float, pid: int | None,
                       own, job_cpus, warm_per_conn: int = 2000, max_per_conn: int = 2_000_000) -> dict:
-    """A closed-loop run of about `seconds` after a warm-up: controlled runs of ~0.5 s each,
-    each sized from the one before, until `seconds` have passed (the generator's histogram
-    and counters span all of them). Latency, errors, bodies, the server's CPU per request and
-    the host load of the run."""
+    """A closed-loop run of `seconds` after a warm-up, as one continuous run of the generator
+    (`runfor`): between a series of shorter runs every connection went idle, the server's
+    pools drained, and the first request after each gap met state that steady load never
+    shows (the shipped chain's breaker tripping with no call in flight and staying open a
+    whole sleep window: profiles/round5/11_shipped_breaker). Latency, errors, bodies, the
+    server's CPU per request and the host load of the run."""
     warm = lg.run(warm_per_conn)
     rate = warm["requests"] / max(1e-9, warm["elapsed_ns"] / 1e9)
     if warm["elapsed_ns"] < 300e6:  # a second warm-up of ~0.3 s at the first one's rate
         warm = lg.run(int(min(max_per_conn, max(warm_per_conn, 0.3 * rate / connections))))
-        rate = warm["requests"] / max(1e-9, warm["elapsed_ns"] / 1e9)
     lg.reset()
     t0, c0 = cpu_times(), proc_cpu_s(pid) if pid else 0.0
-    el_ns = reqs = errs = 0
-    while el_ns < seconds * 1e9:
-        left = seconds - el_ns / 1e9
-        per_conn = int(min(max_per_conn, max(100, rate * min(0.5, left) / connections)))
-        r = lg.run(per_conn)
-        el_ns += r["elapsed_ns"]
-        reqs += r["requests"]
-        errs += r["errors"]
-        rate = r["requests"] / max(1e-9, r["elapsed_ns"] / 1e9)
+    r = lg.run_for(seconds)
+    el_ns, reqs, errs = r["elapsed_ns"], r["requests"], r["errors"]
     t1, c1 = cpu_times(), proc_cpu_s(pid) if pid else 0.0
     st = lg.stats()
     el = el_ns / 1e9
@@ -366,6 +364,8 @@ def chain(a, cpus, job_cpus, shipped: bool = False, seconds: float | None = None
     out = {**r, "a_cpu_us_per_req": 1e6 * busy[0] / rps if rps else 0.0,
            "b_cpu_us_per_req": 1e6 * busy[1] / rps if rps else 0.0,
            "hystrix": counter_delta(m0[0], m1[0], "hystrix."),
+           # A's breaker: times it opened, and closed by a trial or by a call already running
+           "circuit": counter_delta(m0[0], m1[0], "circuit."),
            # where each accepted connection's client thread ran relative to the worker serving
            # it: load generator -> A (A's counters), A's pooled client -> B (B's counters)
            "locality": {"loadgen_to_a": locality_fraction(counter_delta(m0[0], m1[0], "locality.")),

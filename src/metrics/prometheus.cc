@@ -183,6 +183,15 @@ std::string Prometheus::render(http::Server* server) const {
     }
     o += "# TYPE hola_hystrix_circuit_open gauge\nhola_hystrix_circuit_open{command=\"" + s.name + "\"} " +
          (s.circuit_open ? "1" : "0") + "\n";
+    // breaker transitions: opened, and closed by the trial call after the sleep window or
+    // earlier by a call already running when it opened (Hystrix 1.5's markSuccess)
+    o += "# TYPE hola_hystrix_circuit_transitions_total counter\n";
+    o += "hola_hystrix_circuit_transitions_total{command=\"" + s.name + "\",to=\"open\"} " +
+         std::to_string(s.circuit_opened) + "\n";
+    o += "hola_hystrix_circuit_transitions_total{command=\"" + s.name + "\",to=\"closed\",by=\"trial\"} " +
+         std::to_string(s.circuit_closed_trial) + "\n";
+    o += "hola_hystrix_circuit_transitions_total{command=\"" + s.name + "\",to=\"closed\",by=\"inflight\"} " +
+         std::to_string(s.circuit_closed_inflight) + "\n";
     // the bulkhead: calls holding a pool slot, and calls waiting in the pool queue
     o += "# TYPE hola_hystrix_pool_active gauge\nhola_hystrix_pool_active{command=\"" + s.name + "\"} " +
          std::to_string(s.pool_active) + "\n";

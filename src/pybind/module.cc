@@ -211,6 +211,14 @@ struct PyCommand {
     return d;
   }
   std::string stream_json() { return metrics::HystrixStream::command_json(cmd->snapshot()); }
+  py::dict transitions() {
+    auto s = cmd->snapshot();
+    py::dict d;
+    d["opened"] = s.circuit_opened;
+    d["closed_trial"] = s.circuit_closed_trial;
+    d["closed_inflight"] = s.circuit_closed_inflight;
+    return d;
+  }
   std::string pool_json() { return metrics::HystrixStream::threadpool_json(cmd->snapshot()); }
   py::dict settings() {
     auto s = cmd->settings();
@@ -590,6 +598,7 @@ PYBIND11_MODULE(_native, m) {
       .def("is_open", &PyCommand::is_open)
       .def("health", &PyCommand::health)
       .def("stream_json", &PyCommand::stream_json)
+      .def("transitions", &PyCommand::transitions)
       .def("pool_json", &PyCommand::pool_json)
       .def("settings", &PyCommand::settings);
 }

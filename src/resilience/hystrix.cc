@@ -336,7 +336,11 @@ bool Command::is_open(int64_t now) {
   if (h.total < volume_.load(std::memory_order_relaxed)) return false;
   if (h.error_pct < error_pct_.load(std::memory_order_relaxed)) return false;
   bool expected = false;
-  if (open_.compare_exchange_strong(expected, true)) opened_or_tested_.store(now, std::memory_order_release);
+  if (open_.compare_exchange_strong(expected, true)) {
+    opened_or_tested_.store(now, std::memory_order_release);
+    opened_at_.store(now, std::memory_order_relaxed);
+    opened_n_.fetch_add(1, std::memory_order_relaxed);
+  }
   return true;
 }
 
@@ -485,8 +489,13 @@ void Command::mark_success(int64_t now) {
   // markSuccess(): close the circuit and reset the health stream (only the thread whose CAS
   // closes it does the reset).
   if (!open_.load(std::memory_order_acquire)) return;
+  const int64_t since = opened_at_.load(std::memory_order_relaxed);
   bool expected = true;
   if (!open_.compare_exchange_strong(expected, false)) return;
+  // No trial runs before the sleep window is over: a success earlier than that is a call that
+  // was admitted before the circuit opened.
+  (now > since + sleep_window_ms_.load(std::memory_order_relaxed) ? closed_trial_n_ : closed_inflight_n_)
+      .fetch_add(1, std::memory_order_relaxed);
   std::lock_guard<std::mutex> h(health_mu_);  // no snapshot refresh may straddle the reset
   for (auto& sh : shards_) {
     std::lock_guard<ShardLock> g(sh->mu);
@@ -570,6 +579,9 @@ CommandSnapshot Command::snapshot() {
   s.pool = pool_;
   s.now_wall_ms = wall_ms();
   s.circuit_open = is_open(now);
+  s.circuit_opened = opened_n_.load(std::memory_order_relaxed);
+  s.circuit_closed_trial = closed_trial_n_.load(std::memory_order_relaxed);
+  s.circuit_closed_inflight = closed_inflight_n_.load(std::memory_order_relaxed);
   s.health = health_at(now);
   RollingPercentile::Bins exec_h{}, total_h{};
   int64_t exec_sum = 0, exec_n = 0, total_sum = 0, total_n = 0;

@@ -137,6 +137,7 @@ struct CommandSnapshot {
   std::string name, group, pool;
   int64_t now_wall_ms = 0;
   bool circuit_open = false;
+  uint64_t circuit_opened = 0, circuit_closed_trial = 0, circuit_closed_inflight = 0;
   HealthCounts health;
   std::array<int64_t, kNumEvents> rolling{}, cumulative{};
   int64_t concurrent = 0, rolling_max_concurrent = 0;
@@ -230,6 +231,10 @@ class Command {
   // breaker (HystrixCircuitBreakerImpl)
   alignas(64) std::atomic<bool> open_{false};
   std::atomic<int64_t> opened_or_tested_{0};
+  // transitions (for /metrics): opened; closed by the sleep window's trial call, or earlier by
+  // a call that was already running when the circuit opened (markSuccess closes on any success)
+  std::atomic<uint64_t> opened_n_{0}, closed_trial_n_{0}, closed_inflight_n_{0};
+  std::atomic<int64_t> opened_at_{0};  // when it last opened (trials start a sleep window later)
   // health snapshot: (total << 32 | errors), refreshed at most every health_ms_
   std::mutex health_mu_;
   std::atomic<int64_t> health_at_{-1};

@@ -88,6 +88,27 @@ def test_single_trial_after_sleep_window(native):
     assert c.try_start() == "run"
 
 
+def test_a_call_running_when_the_circuit_opens_closes_it(native):
+    """Hystrix 1.5.1's markSuccess closes an open circuit on any success, so a call admitted
+    before the trip that then succeeds closes it before the sleep window; /metrics counts the
+    two kinds of close apart (hola_hystrix_circuit_transitions_total)."""
+    c = native.HystrixCommand(TUNED)
+    assert c.try_start() == "run"  # admitted while closed, still running
+    fail_n(c, 5)
+    c.advance(600)
+    assert c.is_open() and c.try_start() == "short_circuited"
+    c.finish("success", 1)  # the running call completes
+    assert not c.is_open() and c.health()["total"] == 0
+    assert c.transitions() == {"opened": 1, "closed_trial": 0, "closed_inflight": 1}
+    fail_n(c, 5)
+    c.advance(600)
+    assert c.is_open()
+    c.advance(5001)
+    assert c.try_start() == "run"  # the sleep window's trial
+    c.finish("success", 1)
+    assert c.transitions() == {"opened": 2, "closed_trial": 1, "closed_inflight": 1}
+
+
 def test_rolling_window_expires_old_failures(native):
     c = native.HystrixCommand(TUNED)
     fail_n(c, 4)
