@@ -38,7 +38,7 @@ def headline(a, sv, ld, job, seconds):
         lg = ControlledLoadgen([("127.0.0.1", s.port)], a.connections, len(ld), cpu_list=",".join(map(str, ld)),
                                busy_poll_us=a.busy_poll_us, expect_bodies=["Hola de replica-0"])
         try:
-            return subruns.timed_closed_loop(lg, a.connections, seconds, s.proc.pid, sv + ld, job, warm_per_conn=20000)
+            return subruns.timed_closed_loop(lg, a.connections, seconds, s.proc.pid, sv + ld, job)
         finally:
             lg.close()
 

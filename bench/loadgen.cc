@@ -14,9 +14,12 @@
 //   --control                   stdin protocol used by bench.py:
 //        run <R>     every connection completes exactly R requests; replies
 //                    {"elapsed_ns":..,"requests":..,"errors":..}
-//        runfor <MS> every connection sends back to back for MS milliseconds, then finishes
-//                    the request it has in flight; same reply (one continuous run, where a
-//                    series of `run`s leaves every connection idle between them)
+//        runfor <MS> [<WARM_MS>]
+//                    every connection sends back to back for WARM_MS + MS milliseconds, then
+//                    finishes the request it has in flight; only responses after the first
+//                    WARM_MS count (requests, errors, latency, bodies), and elapsed_ns covers
+//                    that part: warm-up and measurement are one continuous run, where a
+//                    series of `run`s leaves every connection idle between them
 //        stats       {"count":..,"p50_ns":..,...,"hist":"bin:count,..."} (since last reset)
 //        reset       clears the histogram
 //        quit
@@ -150,6 +153,9 @@ struct ThreadState {
 
 std::atomic<bool> g_stop{false};
 std::atomic<int64_t> g_budget{0};  // control, shared mode: requests left in this run
+// control `runfor` with a warm-up: responses that arrive before this time (mono ns) are not
+// counted (0 = count all)
+std::atomic<int64_t> g_count_from{0};
 int g_donefd = -1;  // EFD_SEMAPHORE: one count per thread finishing a control run
 std::atomic<bool> g_connect_failed{false};
 char g_connect_error[256];
@@ -552,9 +558,12 @@ void thread_main(ThreadState* ts, const Options* o) {
         continue;
       }
       c->have += size_t(r);
-      if (ts->recording) ts->bytes += uint64_t(r);
       bool close = false;
       const int64_t now_rx = mono_ns();
+      // a `runfor` warm-up: the responses go uncounted, the connections stay busy
+      const bool live = !control || now_rx >= g_count_from.load(std::memory_order_relaxed);
+      const bool rec = ts->recording && live;
+      if (rec) ts->bytes += uint64_t(r);
       size_t at = 0;  // responses are consumed in place; what is left moves down once
       for (;;) {  // every complete response in the buffer (several when pipelining)
         int status = 0;
@@ -569,12 +578,12 @@ void thread_main(ThreadState* ts, const Options* o) {
         }
         int64_t lat = now_rx - (rate_mode ? c->intended : c->t0);
         // (the histogram is only read between control runs / after the run: no lock)
-        if (ts->recording) {
+        if (rec) {
           ts->hist.add(uint64_t(lat));
           ++ts->completed;
         }
         if (status < 200 || status > 299) {
-          ++ts->non2xx;
+          if (live) ++ts->non2xx;
         } else if (verify) {
           const size_t t = size_t(c->target);
           if (t >= ts->expected.size()) {  // Service mode: an endpoint first seen since start-up
@@ -596,16 +605,18 @@ void thread_main(ThreadState* ts, const Options* o) {
             for (const auto& b : o->alt_bodies)
               if (blen == b.size() && memcmp(c->buf + body_at, b.data(), blen) == 0) alt = true;
             if (alt) {
-              if (ts->recording) ++ts->body_alt;
+              if (rec) ++ts->body_alt;
             } else {
-              if (ts->recording) ++ts->body_mismatch;
-              ++ts->errors;
-              ++run_errors;
+              if (rec) ++ts->body_mismatch;
+              if (live) {
+                ++ts->errors;
+                ++run_errors;
+              }
             }
           }
-          if (ts->recording) ++ts->body_checked;
+          if (rec) ++ts->body_checked;
         }
-        ++run_requests;
+        if (live) ++run_requests;
         --c->inflight;
         at += used;
         if (close || c->inflight <= 0) break;
@@ -955,9 +966,17 @@ int main(int argc, char** argv) {
       fflush(stdout);
     } else if (run_for || line.rfind("run ", 0) == 0) {
       const int64_t q = run_for ? INT64_MAX / 4 : atoll(line.c_str() + 4);
-      const int64_t for_ms = run_for ? atoll(line.c_str() + 7) : 0;
+      int64_t for_ms = 0, warm_ms = 0;
+      if (run_for) {
+        long long a = 0, b = 0;
+        const int got = sscanf(line.c_str() + 7, "%lld %lld", &a, &b);
+        for_ms = a;
+        warm_ms = got == 2 ? b : 0;
+      }
       ++gen;
-      int64_t t0 = mono_ns();
+      const int64_t started = mono_ns();
+      int64_t t0 = started + warm_ms * 1000000;  // start of the counted part
+      g_count_from.store(warm_ms > 0 ? t0 : 0);
       // Budgets count batches: with --pipeline P, a claim is P requests. A timed run starts
       // with a budget no run can use up and has it taken away at the deadline: each thread then
       // finishes the requests it holds (at most a claim batch), and the run ends.
@@ -971,7 +990,7 @@ int main(int argc, char** argv) {
         (void)w;
       }
       if (run_for) {
-        const int64_t deadline = t0 + for_ms * 1000000;
+        const int64_t deadline = t0 + for_ms * 1000000;  // after the warm-up
         for (int64_t now = mono_ns(); now < deadline && !g_stop.load(); now = mono_ns()) {
           const int64_t left = deadline - now;
           struct timespec d {left / 1000000000, left % 1000000000};
@@ -994,6 +1013,7 @@ int main(int argc, char** argv) {
         reqs += t->done_requests.load();
         errs += t->done_errors.load();
       }
+      g_count_from.store(0);
       int64_t el = mono_ns() - t0;
       printf("{\"elapsed_ns\":%lld,\"requests\":%llu,\"errors\":%llu}\n", (long long)el, (unsigned long long)reqs,
              (unsigned long long)errs);

@@ -121,10 +121,12 @@ class ControlledLoadgen:
     def run(self, reqs_per_conn: int) -> dict:
         return self._cmd(f"run {reqs_per_conn}")
 
-    def run_for(self, seconds: float) -> dict:
-        """One continuous closed-loop run of `seconds` (every connection sends back to back,
-        then finishes its request in flight): no idle gap inside it, as a series of `run`s has."""
-        return self._cmd(f"runfor {max(1, int(round(seconds * 1000)))}")
+    def run_for(self, seconds: float, warm_s: float = 0.0) -> dict:
+        """One continuous closed-loop run: every connection sends back to back for `warm_s` +
+        `seconds`, then finishes its request in flight; only what completes after the warm-up
+        counts (requests, errors, latency, bodies; elapsed_ns is that part). No idle gap inside
+        it, as a series of `run`s has between them."""
+        return self._cmd(f"runfor {max(1, int(round(seconds * 1000)))} {max(0, int(round(warm_s * 1000)))}")
 
     def stats(self) -> dict:
         return self._cmd("stats")

@@ -93,21 +93,16 @@ def plan_slots(n: int, k: int, slots: int, lb: str) -> dict:
 
 
 def _measure(targets, conns: int, load_cpus: list[int], args, verify: bool) -> dict:
-    """A closed-loop run of about args.duration after args.warmup, in the load generator's
-    control mode: every connection is made before any request is sent (as bench.py runs it),
-    then timed runs of ~0.5 s follow back to back. In wrk-style duration mode each thread
-    started sending as soon as its own connections were up, and connections made while others
-    were already loaded were placed off their client's core (per-replica locality all
-    `same_socket` in some runs, profiles/round5/04_scale_mini)."""
+    """A closed-loop run of args.duration after args.warmup, in the load generator's control
+    mode: every connection is made before any request is sent (as bench.py runs it), then
+    warm-up and measurement run as one continuous run (`runfor`). In wrk-style duration mode
+    each thread started sending as soon as its own connections were up, and connections made
+    while others were already loaded were placed off their client's core (per-replica locality
+    all `same_socket` in some runs, profiles/round5/04_scale_mini)."""
     lg = ControlledLoadgen(targets, conns, len(load_cpus), cpu_list=",".join(map(str, load_cpus)),
                            busy_poll_us=args.busy_poll_us, busy_poll_pause=args.busy_poll_pause, verify_body=verify)
     try:
-        t_end = time.monotonic() + args.warmup
-        per = 2000
-        while time.monotonic() < t_end:
-            w = lg.run(per)
-            per = int(max(200, min(2_000_000, w["requests"] / max(1e-9, w["elapsed_ns"] / 1e9) * 0.25 / conns)))
-        r = timed_closed_loop(lg, conns, args.duration, None, [], [], warm_per_conn=per)
+        r = timed_closed_loop(lg, conns, args.duration, None, [], [], warm_s=args.warmup)
     finally:
         lg.close()
     return {"rps": r["rps"], "latency": {"p50_ns": r["p50_ns"], "p99_ns": r["p99_ns"], "p999_ns": r.get("p999_ns", 0),

@@ -207,20 +207,17 @@ def free_port_block(start: int, n: int, host: str = "127.0.0.1") -> int:
 # ---------------------------------------------------------------- timed closed-loop runs
 
 def timed_closed_loop(lg: ControlledLoadgen, connections: int, seconds: float, pid: int | None,
-                      own, job_cpus, warm_per_conn: int = 2000, max_per_conn: int = 2_000_000) -> dict:
-    """A closed-loop run of `seconds` after a warm-up, as one continuous run of the generator
-    (`runfor`): between a series of shorter runs every connection went idle, the server's
-    pools drained, and the first request after each gap met state that steady load never
-    shows (the shipped chain's breaker tripping with no call in flight and staying open a
-    whole sleep window: profiles/round5/11_shipped_breaker). Latency, errors, bodies, the
-    server's CPU per request and the host load of the run."""
-    warm = lg.run(warm_per_conn)
-    rate = warm["requests"] / max(1e-9, warm["elapsed_ns"] / 1e9)
-    if warm["elapsed_ns"] < 300e6:  # a second warm-up of ~0.3 s at the first one's rate
-        warm = lg.run(int(min(max_per_conn, max(warm_per_conn, 0.3 * rate / connections))))
+                      own, job_cpus, warm_s: float = 1.0) -> dict:
+    """A closed-loop run of `seconds` after `warm_s` of warm-up, warm-up and measurement one
+    continuous run of the generator (`runfor`). A series of shorter runs left every connection
+    idle between them: the server's pools drained, and the first request after each gap met
+    state that steady load never shows (the shipped chain's breaker tripping with no call in
+    flight and staying open a whole sleep window: profiles/round5/11_shipped_breaker). Latency,
+    errors, bodies, the server's CPU per request and the host load of the timed part (the CPU
+    and host-load samples bracket the whole run; the warm-up is at the same load)."""
     lg.reset()
     t0, c0 = cpu_times(), proc_cpu_s(pid) if pid else 0.0
-    r = lg.run_for(seconds)
+    r = lg.run_for(seconds, warm_s)
     el_ns, reqs, errs = r["elapsed_ns"], r["requests"], r["errors"]
     t1, c1 = cpu_times(), proc_cpu_s(pid) if pid else 0.0
     st = lg.stats()
@@ -230,7 +227,8 @@ def timed_closed_loop(lg: ControlledLoadgen, connections: int, seconds: float, p
             "non2xx": st.get("non2xx", 0),
             "body_checked": st.get("body_checked", 0), "body_mismatch": st.get("body_mismatch", 0),
             "body_alt": st.get("body_alt", 0),
-            "cpu_us_per_req": 1e6 * (c1 - c0) / max(1, reqs) if pid else None,
+            # the CPU sample spans the warm-up too, at the same load: per request of the whole run
+            "cpu_us_per_req": (1e6 * (c1 - c0) / max(1.0, reqs * (el + warm_s) / max(1e-9, el))) if pid else None,
             "host_load": host_load(t0, t1, own, job_cpus)}
 
 
@@ -347,8 +345,7 @@ def chain(a, cpus, job_cpus, shipped: bool = False, seconds: float | None = None
                                    alt_bodies=[fallback_body] if shipped else None)
             try:
                 w0 = time.perf_counter()
-                r = timed_closed_loop(lg, a.connections, seconds, None, cpus, job_cpus,
-                                      warm_per_conn=1000 if shipped else 5000)
+                r = timed_closed_loop(lg, a.connections, seconds, None, cpus, job_cpus)
                 wall = time.perf_counter() - w0
             finally:
                 lg.close()
@@ -410,7 +407,7 @@ def alt_layout(a, host: str, server_cpus, load_cpus, smt: str, job_cpus, bodies,
                                path=a.path, busy_poll_us=a.busy_poll_us, busy_poll_pause=16 if alt == "pair" else 0,
                                expect_bodies=bodies, verify_body=bodies is None)
         try:
-            r = timed_closed_loop(lg, a.connections, seconds, s.proc.pid, sv + ld, job_cpus, warm_per_conn=20000)
+            r = timed_closed_loop(lg, a.connections, seconds, s.proc.pid, sv + ld, job_cpus)
         finally:
             lg.close()
     phys_n = len({min(_cpu.siblings(c)) for c in sv + ld})
