@@ -184,6 +184,33 @@ def test_loadgen_alt_body_counted_apart():
     assert bad["latency"]["body_alt"] == 0 and bad["latency"]["body_mismatch"] == bad["latency"]["count"] > 0
 
 
+def test_loadgen_runfor_counts_only_after_its_warm_up():
+    """`runfor MS WARM_MS`: one continuous run whose first WARM_MS go uncounted; the reply's
+    requests, the histogram and the body counts cover the measured part only, and elapsed is
+    that part's length. A plain `run` after it counts everything again."""
+    import time
+
+    from hola_amd.parallel.loadgen import ControlledLoadgen
+    from hola_amd.server import HolaProcess
+
+    with HolaProcess(env={"HOSTNAME": "hx"}, threads=1) as s:
+        lg = ControlledLoadgen([("127.0.0.1", s.port)], 4, 1, expect_bodies=["Hola de hx"])
+        try:
+            lg.reset()
+            t0 = time.monotonic()
+            r = lg.run_for(0.6, 0.4)
+            wall = time.monotonic() - t0
+            st = lg.stats()
+            lg.reset()
+            plain = lg.run(50)
+        finally:
+            lg.close()
+    assert r["errors"] == 0 and r["requests"] > 0
+    assert 0.55e9 <= r["elapsed_ns"] <= 0.8e9 and wall >= 0.95  # the warm-up ran, uncounted
+    assert st["count"] == st["body_checked"] == r["requests"] and st["body_mismatch"] == 0
+    assert plain["requests"] == 4 * 50 and plain["errors"] == 0
+
+
 def test_bench_slot_cores_miniature_two_ranks():
     """--slot-cores 1: each rank runs on the first physical core of its node slot (the
     miniature weak-scaling layout), and the JSON says so rather than passing for the node's."""
