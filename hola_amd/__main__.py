@@ -109,6 +109,14 @@ def _info() -> int:
     from hola_amd.utils.cpu import (allowed_cpus, cgroup_cpu_quota, cpu_budget, format_cpu_list, l3_domain, package_of,
                                     physical_cores, plan_node)
 
+    try:
+        from hola_amd.native import binary
+
+        r = subprocess.run([str(binary("hola", build_if_missing=False)), "--version"], capture_output=True,
+                           text=True, timeout=10)
+        print(f"build          : {r.stdout.strip() or r.stderr.strip()}")
+    except Exception as e:  # noqa: BLE001 - a report, not a check
+        print(f"build          : not built ({e})")
     phys = physical_cores()
     doms: dict[int, list[int]] = {}
     for c in phys:

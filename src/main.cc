@@ -27,8 +27,10 @@
 #include "config/manager.h"
 #include "config/resolver.h"
 #include "core/affinity.h"
+#include "core/build_info.h"
 #include "core/clock.h"
 #include "core/cpuprof.h"
+#include "core/isa.h"
 #include "core/log.h"
 #include "core/net.h"
 #include "http/server.h"
@@ -42,7 +44,7 @@ namespace {
 
 void usage() {
   fprintf(stderr,
-          "usage: hola [options] [-Dkey=value ...]\n"
+          "usage: hola [options] [-Dkey=value ...]   (hola --version: release and build)\n"
           "  --port N                 listen port (default: -Dswarm.http.port, 8080, plus\n"
           "                           -Dswarm.port.offset)\n"
           "  --host ADDR              listen address (default: -Dswarm.bind.address, 0.0.0.0)\n"
@@ -280,6 +282,10 @@ int main(int argc, char** argv) {
       Logger::instance().set_level(l);
     } else if (a == "-h" || a == "--help") {
       usage();
+      return 0;
+    } else if (a == "--version") {
+      printf("hola %s (revision %s, %s, %s, %s)\n", build_info::version(), build_info::revision(), isa::build_level(),
+             build_info::compiler(), build_info::build_type());
       return 0;
     } else {
       fprintf(stderr, "hola: unknown argument '%s'\n", a.c_str());

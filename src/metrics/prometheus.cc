@@ -11,6 +11,8 @@
 #include <cstring>
 
 #include "app/hola_app.h"
+#include "core/build_info.h"
+#include "core/isa.h"
 #include "http/server.h"
 #include "metrics/hystrix_stream.h"
 #include "resilience/hystrix.h"
@@ -80,6 +82,17 @@ Prometheus::Prometheus(int num_workers, int num_routes)
 
 std::string Prometheus::render(http::Server* server) const {
   std::string o;
+  // what is running: constant 1, the labels carry the release, revision and ISA level
+  o += "# HELP hola_build_info The build: release, source revision, x86-64 level, compiler.\n"
+       "# TYPE hola_build_info gauge\nhola_build_info{version=\"";
+  o += build_info::version();
+  o += "\",revision=\"";
+  o += build_info::revision();
+  o += "\",isa=\"";
+  o += isa::build_level();
+  o += "\",compiler=\"";
+  o += build_info::compiler();
+  o += "\"} 1\n";
   o += "# HELP hola_requests_total Requests by route.\n# TYPE hola_requests_total counter\n";
   for (int r = 0; r < nroutes_; ++r) {
     uint64_t n = 0;

@@ -18,6 +18,7 @@
 #include "config/properties.h"
 #include "config/resolver.h"
 #include "http/negotiate.h"
+#include "core/build_info.h"
 #include "core/isa.h"
 #include "http/parser.h"
 #include "json/json.h"
@@ -504,6 +505,15 @@ PYBIND11_MODULE(_native, m) {
     throw py::import_error(isa::error_line("hola_amd._native"));
   m.doc() = "hola native core (C++20) bindings";
   m.def("isa_build_level", &isa::build_level);
+  m.def("build_info", [] {
+    py::dict d;
+    d["version"] = build_info::version();
+    d["revision"] = build_info::revision();
+    d["compiler"] = build_info::compiler();
+    d["build_type"] = build_info::build_type();
+    d["isa"] = isa::build_level();
+    return d;
+  });
   m.def("isa_missing_features", &isa::missing_features);
   m.def("parse_properties", &parse_properties_py, "java.util.Properties.load semantics on UTF-8 bytes");
   m.def("java_format", &java_format_py, "java.lang.String.format subset; bytes or (exception, detail)");

@@ -292,6 +292,28 @@ def test_metrics_process_collector(hola):
     assert m["process_cpu_seconds_total"] >= 0
 
 
+def test_version_and_build_info(hola, hola_bin):
+    """`hola --version` and /metrics' hola_build_info name the release (the reference's Maven
+    version, pom.xml:24, which the image is tagged with), the source revision, the x86-64 level
+    and the compiler; all three views agree."""
+    import re
+    import subprocess
+
+    from hola_amd import native
+
+    out = subprocess.run([str(hola_bin), "--version"], capture_output=True, text=True, timeout=10)
+    assert out.returncode == 0, out.stderr
+    info = native.load_native().build_info()
+    m = re.fullmatch(r"hola (\S+) \(revision (\S+), (x86-64(?:-v\d)?), (.+), (\S+)\)\n", out.stdout)
+    assert m, out.stdout
+    assert m.group(1) == info["version"] == "0.0.1-SNAPSHOT"
+    assert re.fullmatch(r"[0-9a-f]{7,40}(-dirty)?|unknown", m.group(2))
+    assert m.group(3) == info["isa"]
+    line = next(ln for ln in hola().get("/metrics")[2].decode().splitlines() if ln.startswith("hola_build_info{"))
+    assert line == (f'hola_build_info{{version="{m.group(1)}",revision="{m.group(2)}",isa="{m.group(3)}",'
+                    f'compiler="{m.group(4)}"}} 1')
+
+
 def test_expect_100_continue(hola):
     s = hola()
     with socket.create_connection(("127.0.0.1", s.port), timeout=3) as c:
