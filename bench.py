@@ -35,13 +35,14 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 from pathlib import Path
 
 sys.path.insert(0, str(Path(__file__).resolve().parent))
 
-from hola_amd.native import ensure_built  # noqa: E402
+from hola_amd.native import binary, ensure_built  # noqa: E402
 from hola_amd.parallel.hostmetrics import (  # noqa: E402
     MetricsProbe, accept_locality, cgroup_cpu_stat, cpu_times, proc_cpu_s, sink_stats, span_counters,
     start_zipkin_sink, tcp_counters, thread_cpu_s)
@@ -450,6 +451,8 @@ def main() -> int:
                                 "throttled_ms": round(gathered[0]["cgroup"].get("throttled_usec", 0) / 1000.0, 1)},
             "errors": sum(g["errors"] for g in gathered),
             "non2xx": sum(g["non2xx"] for g in gathered),
+            # the server binary measured: release, source revision, x86-64 level, compiler
+            "build": _build_line(),
             # every 2xx body of the timed region compared byte for byte with the expected one
             "body_checked": sum(g["body_checked"] for g in gathered),
             "body_mismatch": sum(g["body_mismatch"] for g in gathered),
@@ -655,6 +658,15 @@ def _layout_note(slots: int, smt: str, server_cpus, load_cpus, slot_cores_k: int
     return (f"{slots} GPU slot(s) on this node; each replica runs on {how}.{mini} The 1-GPU box (16-CPU quota) "
             f"runs smt=off and an unconstrained 8-GPU node smt=pair, so BENCH and SCALE's N=1 differ by layout, "
             f"not by code: at N=1 each carries the other layout's figure (alt_* keys).")
+
+
+def _build_line() -> str:
+    """`hola --version` of the server binary the replicas ran (HOLA_SERVER_BIN included)."""
+    try:
+        r = subprocess.run([str(binary("hola")), "--version"], capture_output=True, text=True, timeout=10)
+        return r.stdout.strip() or r.stderr.strip()
+    except Exception as e:  # noqa: BLE001 - reported, not fatal
+        return f"unknown ({type(e).__name__})"
 
 
 def _chain_keys(c: dict | None, p: str) -> dict:

@@ -33,6 +33,7 @@ def test_bench_one_rank():
     assert out["c1_requests"] == 3000 and out["c1_errors"] == 0 and out["c1_body_checked"] == 3000
     assert out["c1_rps"] > 0 and 0 < out["c1_p50_ms"] <= out["c1_p99_ms"]
     assert out["scaling"] == "weak" and out["higher_is_better"] is True and out["vs_baseline"] is None
+    assert out["build"].startswith("hola 0.0.1-SNAPSHOT (revision ")  # the binary measured
     assert out["config"]["global_batch"] == 64 and out["config"]["parallelism"] == "replicas1"
     assert abs(out["value"] - out["requests"] / (out["ms_per_step"] * out["steps"] / 1000)) / out["value"] < 0.01
     # loopback TCP: at least one request and one response segment per request
