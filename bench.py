@@ -23,7 +23,9 @@ image's ENTRYPOINT + the manifests' args and env: `--shutdown-delay-ms 5000 --bu
 auto`, ZIPKIN_SERVER_URL set; deployed_*), GET /api/hola-chaining
 engineered (chain_*) and as shipped (pool of 10, Feign BASIC logging; chain_shipped_*), and
 the headline in the other SMT layout (alt_*: BENCH and SCALE's N = 1 each carry the other's
-figure). The JSON also carries span accounting (`tracing`, with a native collector under
+figure). Each sub-run is one continuous run of the load generator with its warm-up inside it
+(`runfor`): no idle gaps for pools and breakers to drain in. The JSON also names the server
+binary measured (`build`: release, source revision, x86-64 level) and carries span accounting (`tracing`, with a native collector under
 --zipkin-sink), connection placement (`locality`) and how busy the replicas' cores and the
 SMT siblings outside the job were (`host_load`: other tenants on the siblings are what moves
 the number between runs on a shared host).
