@@ -298,6 +298,7 @@ void client(std::vector<int> fds, int cpu) {
 // A connected loopback pair (client end, server end), non-blocking, TCP_NODELAY.
 bool tcp_pair(int lfd, const sockaddr_in& a, int* c, int* s) {
   *c = socket(AF_INET, SOCK_STREAM, 0);
+  if (*c < 0) return false;
   if (connect(*c, reinterpret_cast<const sockaddr*>(&a), sizeof a) != 0) return false;
   *s = accept(lfd, nullptr, nullptr);
   int one = 1;
@@ -341,6 +342,10 @@ int main(int argc, char** argv) {
   for (int round = 0; round < rounds; ++round) {
     for (const char* mode : {"epoll", "uring"}) {
       int lfd = socket(AF_INET, SOCK_STREAM, 0);
+      if (lfd < 0) {
+        perror("socket");
+        return 1;
+      }
       int one = 1;
       setsockopt(lfd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
       sockaddr_in a{};

@@ -280,6 +280,10 @@ int main(int argc, char** argv) {
   for (int round = 0; round < rounds; ++round) {
     for (const char* mode : {"epoll", "uring"}) {
       int lfd = socket(AF_INET, SOCK_STREAM, 0);
+      if (lfd < 0) {
+        perror("socket");
+        return 1;
+      }
       int one = 1;
       setsockopt(lfd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof one);
       sockaddr_in a{};
@@ -292,7 +296,7 @@ int main(int argc, char** argv) {
       std::vector<int> sfds, cfds;
       for (int i = 0; i < conns; ++i) {
         int c = socket(AF_INET, SOCK_STREAM, 0);
-        if (connect(c, reinterpret_cast<sockaddr*>(&a), sizeof a) != 0) {
+        if (c < 0 || connect(c, reinterpret_cast<sockaddr*>(&a), sizeof a) != 0) {
           perror("connect");
           return 1;
         }

@@ -414,7 +414,9 @@ void AlohaChainer::on_response(http::Worker& w, WorkerCalls& wc, uint32_t slot, 
 void AlohaChainer::finish(WorkerCalls& wc, uint32_t slot, const ChainResult& res) {
   auto cb = std::move(wc.slots[slot]->cb);
   release(wc, slot);  // before the callback: it may start the next call on this worker
-  cb(res);
+  // Every live slot holds its caller's callback, and callers finish a slot once (dead()
+  // guards a late answer); an empty one would be a slot finished twice: drop, do not jump.
+  if (cb) cb(res);
 }
 
 // Arms the worker's one timeout timer for the oldest pending deadline, if it is not armed for

@@ -192,6 +192,7 @@ void EventLoop::run() {
     if (tick_) tick_();
     set_phase(kWait);
     int n = 0;
+    int wait_errno = 0;  // errno of a failed epoll_wait, taken before the clock reads below
     int64_t t = 0;  // mono_ns() at (or just before) the moment events were found
     if (busy_poll_ns_ > 0 && (!busy_auto_ || now_ms_ >= spin_off_until_ms_)) {
       t = mono_ns();
@@ -199,6 +200,7 @@ void EventLoop::run() {
       bool spun = false;  // the first poll came back empty: this pass is a real spin
       for (;;) {
         n = epoll_wait(epfd_, evs, kMaxEvents, 0);
+        if (n < 0) wait_errno = errno;
         if (n != 0 || stop_.load(std::memory_order_relaxed)) break;
         spun = true;
         t = mono_ns();
@@ -212,17 +214,18 @@ void EventLoop::run() {
       const bool off = busy_auto_ && busy_poll_ns_ > 0 && now_ms_ < spin_off_until_ms_;
       const int64_t w0 = off ? mono_ns() : 0;
       n = epoll_wait(epfd_, evs, kMaxEvents, next_timeout_ms());
+      if (n < 0) wait_errno = errno;
       t = mono_ns();
       if (off && n > 0) note_off_wait(t - w0 <= 2 * busy_poll_ns_);
     }
-    if (n < 0 && errno != EINTR) {
+    if (n < 0 && wait_errno != EINTR) {
       // Only a broken epoll descriptor gets here (EBADF, EINVAL, EFAULT). The loop cannot serve
       // its connections or answer posted tasks any more; leaving the thread would leave a
       // replica that looks alive with a dead worker and a drain that waits for it. Fail fast
       // (the supervisor or kubelet restarts the process), saying why, straight to stderr.
       char line[128];
       const int k = snprintf(line, sizeof line, "hola: event loop: epoll_wait(%d) failed: %s; aborting\n", epfd_,
-                             strerror(errno));
+                             strerror(wait_errno));
       ssize_t w = ::write(2, line, size_t(k));
       (void)w;
       std::abort();
