@@ -19,8 +19,11 @@ own address, the part of a network namespace the service contract needs). Around
 * resources: under the static CPU manager policy a Guaranteed pod with integer CPUs gets an
   exclusive cpuset (its process affinity); everything else runs on the shared pool. A memory
   limit is enforced the way the cgroup OOM killer would: resident memory above it gets the
-  container SIGKILLed (OOMKilled) and restarted. CPU quotas (CFS) are not enforced: that
-  needs cgroup writes, i.e. root.
+  container SIGKILLed (OOMKilled) and restarted. A CPU limit is CFS bandwidth control from
+  user space (`CpuBandwidth`): limits.cpu x 100 ms of CPU time per 100 ms period, the
+  container stopped (SIGSTOP) for the rest of a period once it has used that, and continued
+  at the next; the container sees its quota as `HOLA_CGROUP_CPU_MAX` (cpu.max's format), as
+  it would see its cgroup's cpu.max, which the executor cannot write without root.
 
 Delays (probe delay and period, restart back-off, ConfigMap sync) are multiplied by the
 cluster's `time_scale` so tests can run the same state machine faster; deadlines
@@ -35,16 +38,22 @@ import re
 import shutil
 import signal
 import subprocess
+import threading
 import time
 from concurrent.futures import Future, ThreadPoolExecutor
 from dataclasses import dataclass, field
 from pathlib import Path
+
+from hola_amd.kube import manifests as m
 
 PROBE_DEFAULTS = {"initialDelaySeconds": 0, "periodSeconds": 10, "timeoutSeconds": 1, "successThreshold": 1,
                   "failureThreshold": 3}
 BACKOFF_INITIAL_S, BACKOFF_MAX_S, BACKOFF_RESET_S = 10.0, 300.0, 600.0
 DEFAULT_GRACE_S = 30.0
 MEM_CHECK_S = 0.2
+CFS_PERIOD_S = 0.1  # cpu.cfs_period_us's default
+CFS_POLL_S = 0.005
+_CLK_TCK = os.sysconf("SC_CLK_TCK")
 KILL_CAPTURE_S = 6.0  # the grace-expiry capture's limit (hola_fpstack gets 5 s) before a plain SIGKILL
 # resolved in the parent: a forked child of this multi-threaded process only calls it
 _PRCTL = ctypes.CDLL(None, use_errno=True).prctl
@@ -105,6 +114,7 @@ class Pod:
     cpus: list[int] | None = None  # exclusive cpuset (static CPU manager) or None (shared pool)
     cpu_request: float = 0.0
     mem_limit: int = 0  # bytes; 0 = none
+    cfs: dict = field(default_factory=dict)  # CPU bandwidth control counters (CpuBandwidth)
     rss_peak: int = 0
     next_mem_check: float = 0.0
     created: float = field(default_factory=time.monotonic)
@@ -165,7 +175,103 @@ class Pod:
                 "restarts": self.restarts, "revision": self.revision, "owner": self.owner,
                 "cpus": self.cpus, "pid": self.proc.pid if self.running else None,
                 "rss_peak_mb": round(self.rss_peak / 2**20, 1),
+                "cpu_throttle": {k: (round(v, 3) if isinstance(v, float) else v) for k, v in self.cfs.items()},
                 "last_probe": self.last_probe, "pending_reason": self.pending_reason}
+
+
+def _proc_cpu_s(pid: int) -> float | None:
+    """User + system CPU time of a process (all its threads), from /proc/PID/stat."""
+    try:
+        f = Path(f"/proc/{pid}/stat").read_text().rsplit(")", 1)[1].split()
+        return (int(f[11]) + int(f[12])) / _CLK_TCK  # utime, stime (fields 14 and 15)
+    except (OSError, IndexError, ValueError):
+        return None
+
+
+@dataclass
+class _Bandwidth:
+    pod: Pod
+    proc: subprocess.Popen
+    quota_s: float  # CPU seconds per period
+    period: int = -1
+    base_s: float = 0.0  # the container's CPU time when the period began
+    stopped: bool = False
+    stopped_at: float = 0.0
+
+
+class CpuBandwidth:
+    """CFS bandwidth control for containers with limits.cpu, from user space: every 100 ms
+    period a container may use limits.cpu x 100 ms of CPU time; once it has, its process group
+    is stopped (SIGSTOP) until the period ends and continued (SIGCONT) at the next, which is
+    what the kernel's throttling does to a cgroup over its cpu.max. Usage is read from /proc
+    every 5 ms at the kernel's accounting granularity (USER_HZ, 10 ms), so a period can run
+    over by a poll and a tick. Each pod's `cfs` counts periods, throttled periods and the time
+    spent stopped (cpu.stat's nr_periods, nr_throttled, throttled_usec)."""
+
+    def __init__(self):
+        self._lock = threading.Lock()
+        self._groups: dict[str, _Bandwidth] = {}
+        self._stop = threading.Event()
+        self._thread = threading.Thread(target=self._run, name="kube-cfs", daemon=True)
+        self._thread.start()
+
+    def add(self, pod: Pod, proc: subprocess.Popen, cpus: float) -> None:
+        with self._lock:
+            old = self._groups.pop(pod.name, None)
+            if old is not None:
+                self._resume(old)
+            self._groups[pod.name] = _Bandwidth(pod, proc, cpus * CFS_PERIOD_S)
+        pod.cfs = {"quota_cpus": cpus, "nr_periods": 0, "nr_throttled": 0, "throttled_s": 0.0}
+
+    def remove(self, pod_name: str) -> None:
+        with self._lock:
+            g = self._groups.pop(pod_name, None)
+            if g is not None:
+                self._resume(g)
+
+    def close(self) -> None:
+        self._stop.set()
+        self._thread.join(timeout=2)
+        with self._lock:
+            for g in self._groups.values():
+                self._resume(g)
+            self._groups.clear()
+
+    @staticmethod
+    def _signal(g: _Bandwidth, sig: int) -> None:
+        if g.proc.poll() is None:  # never a reaped pid (it could be another process's by now)
+            try:
+                os.killpg(g.proc.pid, sig)  # the container's session: its pid is the group
+            except (ProcessLookupError, PermissionError):
+                pass
+
+    def _resume(self, g: _Bandwidth) -> None:
+        if g.stopped:
+            self._signal(g, signal.SIGCONT)
+            g.stopped = False
+            g.pod.cfs["throttled_s"] += time.monotonic() - g.stopped_at
+
+    def _run(self) -> None:
+        t0 = time.monotonic()
+        while not self._stop.wait(CFS_POLL_S):
+            now = time.monotonic()
+            k = int((now - t0) / CFS_PERIOD_S)
+            with self._lock:
+                for name, g in list(self._groups.items()):
+                    if g.proc.poll() is not None:
+                        del self._groups[name]
+                        continue
+                    cpu = _proc_cpu_s(g.proc.pid)
+                    if cpu is None:
+                        continue
+                    if k != g.period:  # a new period: the quota refills
+                        self._resume(g)
+                        g.period, g.base_s = k, cpu
+                        g.pod.cfs["nr_periods"] += 1
+                    elif not g.stopped and cpu - g.base_s >= g.quota_s:
+                        self._signal(g, signal.SIGSTOP)
+                        g.stopped, g.stopped_at = True, now
+                        g.pod.cfs["nr_throttled"] += 1
 
 
 class Kubelet:
@@ -174,6 +280,7 @@ class Kubelet:
 
     def __init__(self, cluster, probe_workers: int = 16):
         self.cluster = cluster
+        self.cfs = CpuBandwidth()
         self.pool = ThreadPoolExecutor(max_workers=probe_workers, thread_name_prefix="kube-probe")
         # grace-expiry captures + SIGKILLs, off the control loop and off the probes' pool
         self.diag = ThreadPoolExecutor(max_workers=4, thread_name_prefix="kube-diag")
@@ -185,9 +292,17 @@ class Kubelet:
             return None
         return {**PROBE_DEFAULTS, **rp}
 
+    @staticmethod
+    def cpu_limit(pod: Pod) -> float:
+        """limits.cpu of the container in cores (0 = none)."""
+        return m.parse_cpu(((pod.container.get("resources") or {}).get("limits") or {}).get("cpu"))
+
     def _env(self, pod: Pod) -> dict[str, str]:
         c = self.cluster
         env = {"PATH": os.environ.get("PATH", "/usr/bin:/bin"), "HOME": str(pod.dir)}
+        limit = self.cpu_limit(pod)
+        if limit > 0:  # the cgroup's cpu.max as the container would read it
+            env["HOLA_CGROUP_CPU_MAX"] = f"{int(round(limit * CFS_PERIOD_S * 1e6))} {int(CFS_PERIOD_S * 1e6)}"
         for k in ("LANG", "LC_ALL", "TMPDIR", "LD_LIBRARY_PATH", "SSL_CERT_FILE", "SSL_CERT_DIR"):
             if k in os.environ:
                 env[k] = os.environ[k]
@@ -284,6 +399,10 @@ class Kubelet:
             self.cluster.event(pod.name, "Failed", f"cannot start the container: {e}")
             return
         log.close()
+        limit = self.cpu_limit(pod)
+        # an exclusive cpuset no larger than the quota cannot exceed it: nothing to enforce
+        if limit > 0 and not (pod.cpus and len(pod.cpus) <= limit):
+            self.cfs.add(pod, pod.proc, limit)
         pod.started_at = now
         pod.next_mem_check = now + 0.05  # a container over its limit from the start dies before probing
         pod.ready = False
@@ -455,6 +574,7 @@ class Kubelet:
             pod.proc.send_signal(sig)
 
     def shutdown(self) -> None:
+        self.cfs.close()
         self.pool.shutdown(wait=False, cancel_futures=True)
         self.diag.shutdown(wait=False, cancel_futures=True)
 

@@ -144,12 +144,33 @@ int package_of(int cpu) {
   return (cpu >= 0 && size_t(cpu) < table.size()) ? table[size_t(cpu)] : -1;
 }
 
+namespace {
+// "QUOTA PERIOD" (cpu.max's format) as CPUs; 0 for "max" or anything unreadable.
+double parse_cpu_max(const std::string& q, const std::string& p) {
+  if (q.empty() || q == "max") return 0;
+  const double qv = atof(q.c_str()), pv = atof(p.c_str());
+  return pv > 0 && qv > 0 ? qv / pv : 0;
+}
+}  // namespace
+
 double cgroup_cpu_quota() {
-  std::ifstream f("/sys/fs/cgroup/cpu.max");
-  std::string q, p;
-  if (!(f >> q >> p) || q == "max") return 0;
-  double qv = atof(q.c_str()), pv = atof(p.c_str());
-  return pv > 0 ? qv / pv : 0;
+  double quota = 0;
+  {
+    std::ifstream f("/sys/fs/cgroup/cpu.max");
+    std::string q, p;
+    if (f >> q >> p) quota = parse_cpu_max(q, p);
+  }
+  // HOLA_CGROUP_CPU_MAX (cpu.max's format) stands in for the pod's own cgroup where the
+  // container runtime cannot write one: the local manifest executor sets it from limits.cpu
+  // and enforces it from user space (hola_amd/kube/kubelet.py, CpuBandwidth). Nested quotas
+  // bound each other, so the lower one counts.
+  if (const char* e = getenv("HOLA_CGROUP_CPU_MAX")) {
+    std::string s(e);
+    const size_t sp = s.find(' ');
+    const double pod = parse_cpu_max(s.substr(0, sp), sp == std::string::npos ? "100000" : s.substr(sp + 1));
+    if (pod > 0 && (quota == 0 || pod < quota)) quota = pod;
+  }
+  return quota;
 }
 
 }  // namespace hola

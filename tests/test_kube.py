@@ -423,6 +423,42 @@ def test_memory_limit_is_enforced_as_oomkilled(cluster):
     assert len(c.endpoints()) == 1 and all(p["revision"] == 1 for p in c.get_pods() if p["ready"])
 
 
+def test_cpu_limit_is_seen_as_the_cgroup_quota(cluster):
+    """limits.cpu 2 under the default CPU manager policy (shared pool): the container sees the
+    quota as its cgroup's cpu.max (HOLA_CGROUP_CPU_MAX from the executor), so hola sizes itself
+    to 2 workers as in a real pod, not to every CPU of the pool."""
+    c = cluster(replicas=1)
+    c.wait_ready(1, timeout=30)
+    pod = c.get_pods()[0]
+    log = (c.state / "pods" / pod["name"] / "container.log").read_text()
+    assert "workers=2," in log, log[-2000:]
+    assert pod["cpu_throttle"]["quota_cpus"] == 2.0
+
+
+def test_cpu_limit_is_enforced_as_cfs_throttling(cluster):
+    """A container that burns CPU under limits.cpu 300m gets about 0.3 CPU-s per second: each
+    100 ms period it is stopped once it has used 30 ms, and continued at the next, as CFS
+    bandwidth control throttles a cgroup over its quota; the pod's counters say so."""
+    c = cluster(replicas=1)
+    c.wait_ready(1, timeout=30)
+    c.patch({"spec": {"template": {"spec": {"containers": [
+        {"name": "hola", "command": [sys.executable, "-c", "while True: pass"], "args": [],
+         "resources": {"limits": {"cpu": "300m", "memory": "256Mi"}, "requests": {"cpu": "300m", "memory": "64Mi"}}}]}}}})
+    c.wait(lambda: any(p["revision"] == 2 and p["pid"] for p in c.get_pods()), 30, "the burner running")
+    pod = next(p for p in c.get_pods() if p["revision"] == 2)
+    from hola_amd.kube.kubelet import _proc_cpu_s
+
+    time.sleep(0.3)
+    cpu0, t0 = _proc_cpu_s(pod["pid"]), time.monotonic()
+    time.sleep(2.0)
+    cpu1, t1 = _proc_cpu_s(pod["pid"]), time.monotonic()
+    share = (cpu1 - cpu0) / (t1 - t0)
+    assert 0.2 <= share <= 0.45, share  # unthrottled it would be ~1.0
+    th = next(p for p in c.get_pods() if p["revision"] == 2)["cpu_throttle"]
+    assert th["quota_cpus"] == 0.3 and th["nr_periods"] >= 15
+    assert th["nr_throttled"] >= 0.8 * th["nr_periods"] - 2 and th["throttled_s"] > 1.0
+
+
 def test_grace_period_expiry_kills_once(cluster):
     """A container still running when terminationGracePeriodSeconds runs out gets one SIGKILL
     (here: a 30 s shutdown delay against a 1 s grace period); the pod is then gone."""
