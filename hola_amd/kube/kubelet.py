@@ -220,8 +220,9 @@ class CpuBandwidth:
             old = self._groups.pop(pod.name, None)
             if old is not None:
                 self._resume(old)
+            if not pod.cfs:  # the counters span the pod's restarts, as a cgroup's cpu.stat does
+                pod.cfs = {"quota_cpus": cpus, "nr_periods": 0, "nr_throttled": 0, "throttled_s": 0.0}
             self._groups[pod.name] = _Bandwidth(pod, proc, cpus * CFS_PERIOD_S)
-        pod.cfs = {"quota_cpus": cpus, "nr_periods": 0, "nr_throttled": 0, "throttled_s": 0.0}
 
     def remove(self, pod_name: str) -> None:
         with self._lock:
@@ -254,24 +255,30 @@ class CpuBandwidth:
     def _run(self) -> None:
         t0 = time.monotonic()
         while not self._stop.wait(CFS_POLL_S):
-            now = time.monotonic()
-            k = int((now - t0) / CFS_PERIOD_S)
-            with self._lock:
-                for name, g in list(self._groups.items()):
-                    if g.proc.poll() is not None:
-                        del self._groups[name]
-                        continue
-                    cpu = _proc_cpu_s(g.proc.pid)
-                    if cpu is None:
-                        continue
-                    if k != g.period:  # a new period: the quota refills
-                        self._resume(g)
-                        g.period, g.base_s = k, cpu
-                        g.pod.cfs["nr_periods"] += 1
-                    elif not g.stopped and cpu - g.base_s >= g.quota_s:
-                        self._signal(g, signal.SIGSTOP)
-                        g.stopped, g.stopped_at = True, now
-                        g.pod.cfs["nr_throttled"] += 1
+            try:
+                self._pass(int((time.monotonic() - t0) / CFS_PERIOD_S))
+            except Exception:  # noqa: BLE001 - the controller must outlive one bad pass
+                pass
+
+    def _pass(self, k: int) -> None:
+        """One poll: `k` is the current period's index."""
+        now = time.monotonic()
+        with self._lock:
+            for name, g in list(self._groups.items()):
+                if g.proc.poll() is not None:
+                    del self._groups[name]
+                    continue
+                cpu = _proc_cpu_s(g.proc.pid)
+                if cpu is None:
+                    continue
+                if k != g.period:  # a new period: the quota refills
+                    self._resume(g)
+                    g.period, g.base_s = k, cpu
+                    g.pod.cfs["nr_periods"] += 1
+                elif not g.stopped and cpu - g.base_s >= g.quota_s:
+                    self._signal(g, signal.SIGSTOP)
+                    g.stopped, g.stopped_at = True, now
+                    g.pod.cfs["nr_throttled"] += 1
 
 
 class Kubelet:
