@@ -12,6 +12,7 @@
     python -m hola_amd oc apply -f translation-configmap.yaml            # ConfigMap edit
     python -m hola_amd oc delete pod hola-1-abcde
     python -m hola_amd oc logs hola-1-abcde; python -m hola_amd oc describe pod hola-1-abcde
+    python -m hola_amd oc top pods
 
 `apply` serves a control socket in its state directory (`--state-dir`, default
 `$HOLA_CLUSTER_DIR` or /tmp/hola-cluster); `oc` talks to it.
@@ -163,6 +164,8 @@ def _dispatch(c, req: dict, stop: threading.Event):
         if pod is None:
             raise KeyError(f"no pod {req['name']!r}")
         return {"pod": pod, "events": [list(e) for e in c.events if e[1] == req["name"]]}
+    if op == "top":
+        return c.top(float(req.get("sample_s", 0.5)))
     if op == "service-url":
         return c.service_url(req.get("service"))
     if op == "shutdown":
@@ -240,6 +243,8 @@ def oc_main(argv: list[str]) -> int:
     de = sub.add_parser("describe", help="a pod's state and its events")
     de.add_argument("what", choices=["pod", "po"])
     de.add_argument("name")
+    t = sub.add_parser("top", help="CPU and memory of each pod (kubectl top pod)")
+    t.add_argument("what", choices=["pods", "pod", "po"])
     sub.add_parser("url")
     sub.add_parser("stop")
     a = ap.parse_args(argv)
@@ -300,6 +305,12 @@ def oc_main(argv: list[str]) -> int:
             print("Events:")
             for t, _obj, reason, msg in d["events"]:
                 print(f"  {t:9.3f}  {reason:<16} {msg}")
+        elif a.verb == "top":
+            print(f"{'NAME':<24}{'CPU(cores)':>12}{'MEMORY(bytes)':>15}  THROTTLED(periods)")
+            for p in _request(state, {"op": "top"}):
+                th = p["cpu_throttle"]
+                thr = f"{th['nr_throttled']}/{th['nr_periods']}" if th else "-"
+                print(f"{p['name']:<24}{round(p['cpu_cores'] * 1000):>11}m{p['memory_bytes'] >> 20:>13}Mi  {thr}")
         elif a.verb == "url":
             print(_request(state, {"op": "service-url"}))
         elif a.verb == "stop":

@@ -590,6 +590,25 @@ class Cluster:
         with self.lock:
             return [p.summary() for p in sorted(self.pods.values(), key=lambda p: p.name) if not p.gone]
 
+    def top(self, sample_s: float = 0.5) -> list[dict]:
+        """`kubectl top pod`: each running container's CPU use over `sample_s` (cores) and its
+        resident memory, read from /proc, with its CPU limit and throttling counters."""
+        from hola_amd.kube.kubelet import _proc_cpu_s, _proc_rss
+
+        pods = [p for p in self.get_pods() if p["pid"]]
+        t0 = time.monotonic()
+        c0 = {p["name"]: _proc_cpu_s(p["pid"]) for p in pods}
+        time.sleep(sample_s)
+        dt = time.monotonic() - t0
+        out = []
+        for p in pods:
+            c1 = _proc_cpu_s(p["pid"])
+            if c1 is None or c0[p["name"]] is None:
+                continue
+            out.append({"name": p["name"], "cpu_cores": round((c1 - c0[p["name"]]) / dt, 3),
+                        "memory_bytes": _proc_rss(p["pid"]) or 0, "cpu_throttle": p["cpu_throttle"]})
+        return out
+
     def endpoints(self, name: str | None = None, published: bool = True) -> list[str]:
         with self.lock:
             name = name or next(iter(self.services))

@@ -188,6 +188,15 @@ def _proc_cpu_s(pid: int) -> float | None:
         return None
 
 
+def _proc_rss(pid: int) -> int | None:
+    """Resident memory of a process in bytes, from /proc/PID/status."""
+    try:
+        status = Path(f"/proc/{pid}/status").read_text()
+        return int(next(ln for ln in status.splitlines() if ln.startswith("VmRSS:")).split()[1]) * 1024
+    except (OSError, StopIteration, ValueError):
+        return None
+
+
 @dataclass
 class _Bandwidth:
     pod: Pod
@@ -460,10 +469,8 @@ class Kubelet:
         limit = pod.mem_limit
         if limit <= 0:
             return
-        try:
-            status = Path(f"/proc/{pod.proc.pid}/status").read_text()
-            rss = int(next(l for l in status.splitlines() if l.startswith("VmRSS:")).split()[1]) * 1024
-        except (OSError, StopIteration, ValueError):
+        rss = _proc_rss(pod.proc.pid)
+        if rss is None:
             return
         pod.rss_peak = max(pod.rss_peak, rss)
         if rss > limit:

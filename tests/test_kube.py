@@ -341,7 +341,13 @@ def test_oc_command_line(tmp_path, hola_bin):
         some = json.loads(oc("get", "pods", "-o", "json").stdout)[0]["name"]
         assert "hola listening on" in oc("logs", some).stdout
         desc = oc("describe", "pod", some).stdout
-        assert "ready:" in desc and "Started" in desc and "Ready" in desc
+        assert "ready:" in desc and "Started" in desc and "Ready" in desc and "cpu_throttle:" in desc
+        # `oc top pods` (kubectl top pod): CPU in millicores, memory, throttled periods
+        top = oc("top", "pods").stdout.splitlines()
+        assert top[0].split()[:3] == ["NAME", "CPU(cores)", "MEMORY(bytes)"]
+        rows = {r.split()[0]: r.split() for r in top[1:]}
+        assert set(rows) == {p["name"] for p in json.loads(oc("get", "pods", "-o", "json").stdout)}
+        assert all(r[1].endswith("m") and r[2].endswith("Mi") and 1 <= int(r[2][:-2]) < 64 for r in rows.values())
     finally:
         oc("stop")
         ap.wait(timeout=30)
