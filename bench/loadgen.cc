@@ -69,6 +69,8 @@
 #include <thread>
 #include <vector>
 
+#include "core/build_info.h"
+#include "core/isa.h"
 #include "core/cpuprof.h"
 #include "core/histogram.h"
 #include "core/affinity.h"
@@ -805,6 +807,11 @@ int main(int argc, char** argv) {
     }
     else if (a == "--latency") latency = true;
     else if (a == "--json") json = true;
+    else if (a == "--version") {
+      printf("hola_loadgen %s (revision %s, %s)\n", hola::build_info::version(), hola::build_info::revision(),
+             hola::isa::build_level());
+      return 0;
+    }
     else if (a.rfind("http://", 0) == 0) url = a;
     else if (a == "--warmup") o.warmup_s = atof(val().c_str());
     else if (a == "--control") o.control = true;

@@ -48,6 +48,8 @@
 #include <vector>
 
 #include "client/url.h"
+#include "core/build_info.h"
+#include "core/isa.h"
 #include "core/affinity.h"
 #include "core/loop.h"
 #include "core/net.h"
@@ -616,6 +618,11 @@ int main(int argc, char** argv) {
     else if (a == "--idle-timeout-ms") idle_timeout_ms = atoi(val().c_str());
     else if (a == "--endpoints-file") endpoints_file = val();
     else if (a == "--no-failover") g_failover = false;
+    else if (a == "--version") {
+      printf("hola_rrproxy %s (revision %s, %s)\n", hola::build_info::version(), hola::build_info::revision(),
+             hola::isa::build_level());
+      return 0;
+    }
     else {
       fprintf(stderr,
               "usage: hola_rrproxy --backends h:p,h:p.. [--port N] [--host H] [--threads N] [--cpu-list L]\n"

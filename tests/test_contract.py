@@ -309,6 +309,9 @@ def test_version_and_build_info(hola, hola_bin):
     assert m.group(1) == info["version"] == "0.0.1-SNAPSHOT"
     assert re.fullmatch(r"[0-9a-f]{7,40}(-dirty)?|unknown", m.group(2))
     assert m.group(3) == info["isa"]
+    for tool in ("hola_rrproxy", "hola_loadgen"):  # built from the same tree: the same revision
+        v = subprocess.run([str(hola_bin.parent / tool), "--version"], capture_output=True, text=True, timeout=10)
+        assert v.stdout == f"{tool} {m.group(1)} (revision {m.group(2)}, {m.group(3)})\n", v.stdout
     line = next(ln for ln in hola().get("/metrics")[2].decode().splitlines() if ln.startswith("hola_build_info{"))
     assert line == (f'hola_build_info{{version="{m.group(1)}",revision="{m.group(2)}",isa="{m.group(3)}",'
                     f'compiler="{m.group(4)}"}} 1')
