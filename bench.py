@@ -70,9 +70,10 @@ def parse_args():
                     help="requests per connection per step; 0 = sized from the last warmup step so that a "
                          "step lasts --step-seconds (every rank takes the smallest size any rank computed, "
                          "so each replica does the same work; `requests` stays exact)")
-    ap.add_argument("--step-seconds", type=float, default=1.5,
-                    help="target length of one timed step with --reqs-per-conn 0 (20 x 1.5 s = the 30 s of "
-                         "BASELINE configs 3/4)")
+    ap.add_argument("--step-seconds", type=float, default=1.55,
+                    help="target length of one timed step with --reqs-per-conn 0: 20 steps time the 30 s of "
+                         "BASELINE configs 3/4 (the timed steps run 0-4 %% faster than the last warmup step "
+                         "they are sized from: 28.8-30.2 s at 1.5 s on the box)")
     ap.add_argument("--warmup-reqs-per-conn", type=int, default=96000,
                     help="requests per connection of each warmup step with --reqs-per-conn 0")
     ap.add_argument("--cores", type=int, default=0,
