@@ -737,6 +737,10 @@ def _deployed_keys(d: dict | None) -> dict:
             "deployed_server_cpu_us_per_req": round(d["cpu_us_per_req"], 3),
             "deployed_host_load": d["host_load"],
             "deployed_args": d["args"], "deployed_cpus": d["cpus"],
+            # the image binds 0.0.0.0, as a pod on an IPv4 pod network: the client connects over
+            # IPv4 loopback, where the headline uses ::1 (2.6 % apart, profiles/round1/r20_v6), which
+            # is the in-bench gap between the two (profiles/round5/03_deployed_ab)
+            "deployed_loopback": "127.0.0.1",
             # ZIPKIN_SERVER_URL names the cluster's zipkin-query Service, which does not resolve
             # on a bare host: spans are recorded and dropped when the post fails
             "deployed_env": d["env"], "deployed_zipkin": d["zipkin"]}
