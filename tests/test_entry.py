@@ -25,6 +25,7 @@ def test_cli_info_and_help(capsys):
     assert main(["info"]) == 0
     out = capsys.readouterr().out
     assert "physical cores" in out and "plan x8" in out
+    assert "build          : hola 0.0.1-SNAPSHOT (revision " in out  # what is installed, first
     assert main([]) == 0
 
 
