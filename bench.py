@@ -52,8 +52,8 @@ from hola_amd.parallel import subruns  # noqa: E402
 from hola_amd.parallel.loadgen import ControlledLoadgen, decode_hist, merge_hists, percentile  # noqa: E402
 from hola_amd.server import HolaProcess  # noqa: E402
 from hola_amd.utils.cpu import (  # noqa: E402
-    cgroup_cpu_quota, connection_targets, cpu_budget, format_cpu_list, plan_replicas_with_loadgen, plan_slot_subset,
-    siblings, slot_cores, smt_fits)
+    cgroup_cpu_quota, connection_targets, cpu_budget, format_cpu_list, physical_cores, plan_replicas_with_loadgen,
+    plan_slot_subset, sibling_of, siblings, slot_cores, smt_fits)
 
 METRIC = "HTTP req/sec + p50/p99 latency, GET /api/hola at 1/2/4/8 replicas"
 BASELINE_VALUE = None  # the reference publishes no numbers
@@ -118,7 +118,8 @@ def parse_args():
                          "same side, pair = server worker + its load-generator thread on one core "
                          "(1.55x req/s per physical core, profiles/round1/r16_smt); auto = pair when one GPU "
                          "slot's CPU share (budget / GPUs on the node) holds both threads of --cores "
-                         "cores, else off. Decided per node, so every N runs replicas alike")
+                         "cores, else off. Decided per node, so every N runs replicas alike. A forced pair "
+                         "in a budget too small for both threads pairs half the cores")
     ap.add_argument("--epoll-lt", action="store_true",
                     help="level-triggered epoll for connection sockets on both sides (default: edge)")
     ap.add_argument("--busy-poll-pause", type=int, default=-1,
@@ -554,6 +555,12 @@ def _plan(a, n: int, avoid_busy: bool = True) -> dict:
     smt = a.smt
     if smt == "auto":
         smt = "pair" if smt_fits(slots, per_rank) else "off"
+    elif smt == "pair" and not smt_fits(slots, per_rank) and any(sibling_of(c) is not None
+                                                                  for c in physical_cores()[:1]):
+        # forced pairing inside a CPU budget that cannot hold both threads of every core: half
+        # the physical cores, both threads each (a 16-CPU quota: 8 paired cores, as alt_* runs),
+        # instead of 32 busy CPUs that the quota throttles to half speed
+        per_rank = min(per_rank, max(1, cpu_budget() // (2 * n)))
     return {"cores": plan_replicas_with_loadgen(n, per_rank, a.server_threads, avoid_busy=avoid_busy, smt=smt),
             "smt": smt, "gpu_slots": slots, "cores_per_slot": per_rank}
 

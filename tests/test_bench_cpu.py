@@ -242,3 +242,33 @@ def test_scaling_miniature_weak_efficiency():
         assert [r["replicas"] for r in rows] == [1, 2] and all(r["errors"] == 0 for r in rows), rows
         assert rows[0]["efficiency"] == 1.0 and rows[1]["efficiency"] > 0 and rows[1]["slot_cores"] == 1
         assert "efficiency = total / (N x N=1)" in buf.getvalue()
+
+
+def test_forced_smt_pair_stays_inside_the_cpu_budget(monkeypatch):
+    """`--smt pair` under a budget that cannot hold both threads of a slot's cores (the 1-GPU
+    box: 16 CPUs, 16 cores per slot) pairs half the cores instead of running 32 busy CPUs that
+    the quota throttles to half speed; with room for both threads the slot keeps its cores,
+    and a host without SMT keeps them too (pair falls back to off there)."""
+    import argparse
+    import importlib
+
+    sys.path.insert(0, str(ROOT))
+    bench = importlib.import_module("bench")
+    seen = {}
+
+    def fake_plan(n, per_rank, server_threads, avoid_busy=True, smt="off"):
+        seen.update(n=n, per_rank=per_rank, smt=smt)
+        return [{"server": [0], "loadgen": [128], "thread_targets": [[0]]}]
+
+    monkeypatch.setattr(bench, "plan_replicas_with_loadgen", fake_plan)
+    monkeypatch.setattr(bench, "slot_cores", lambda slots: 16)
+    monkeypatch.setattr(bench, "physical_cores", lambda: list(range(128)))
+    a = argparse.Namespace(slot_cores=0, cores=0, smt="pair", server_threads=0, gpu_slots=1)
+    for budget, fits, sib, want in ((16, False, lambda c: c + 128, 8),   # the box's quota
+                                    (256, True, lambda c: c + 128, 16),  # an 8-GPU node
+                                    (16, False, lambda c: None, 16)):    # no SMT at all
+        monkeypatch.setattr(bench, "cpu_budget", lambda b=budget: b)
+        monkeypatch.setattr(bench, "smt_fits", lambda slots, per, f=fits: f)
+        monkeypatch.setattr(bench, "sibling_of", sib)
+        p = bench._plan(a, 1, avoid_busy=False)
+        assert seen == {"n": 1, "per_rank": want, "smt": "pair"} and p["cores_per_slot"] == want, (budget, seen)
