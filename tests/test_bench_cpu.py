@@ -58,6 +58,10 @@ def test_bench_auto_steps_and_node_subruns():
     assert out["config"]["cores_per_replica"] == len({min(siblings(c)) for c in srv})
     assert out["deployed_errors"] == 0 and out["deployed_body_checked"] == out["deployed_requests"] > 0
     assert set(out["deployed_host_load"]) == {"own", "siblings"} and out["deployed_zipkin"] == "deployed"
+    assert out["deployed_loopback"] == "127.0.0.1"  # the image binds 0.0.0.0: IPv4, as a pod
+    # every sub-run is one continuous run of its length, its warm-up uncounted
+    assert abs(out["deployed_elapsed_s"] - 0.5) < 0.1 and abs(out["chain_elapsed_s"] - 0.5) < 0.1
+    assert set(out["chain_circuit"]) == {"open", "closed_trial", "closed_inflight"}
     # ... and sized as the manifests size a pod (limits.cpu 2)
     assert len(parse_cpu_list(out["deployed_pod_cpus"])) == 2 and out["deployed_pod_errors"] == 0
     assert out["deployed_pod_rps"] > 0
