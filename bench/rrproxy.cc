@@ -181,33 +181,40 @@ void publish_set(std::vector<Backend*> list) {
 // Follows --endpoints-file. The writer replaces it with a rename, so a reader never sees half
 // a file; the file is read again every pass and compared by content, because a replacement
 // can keep the inode number (recycled), the size and the (coarse) mtime of the one before.
-void endpoints_loop(std::string path) {
-  std::string last;
+struct EndpointsFollower {
+  std::string path, last;
   bool have = false;
-  while (!g_stop.load()) {
+
+  // Publishes the file's set if it changed; true once a set has been read.
+  bool poll() {
     std::ifstream f(path);
-    if (f) {
-      std::string text((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
-      std::vector<Backend*> list;
-      if ((!have || text != last) && parse_backends(text, &list)) {
-        publish_set(std::move(list));
-        fprintf(stderr, "rrproxy: endpoints now %zu backends\n", current_set().list.size());
-        last = text;
-        have = true;
-        unsigned long long gen = 0;
-        if (sscanf(text.c_str(), "# gen %llu", &gen) == 1) {
-          const std::string tmp = path + ".applied.tmp";
-          if (FILE* out = fopen(tmp.c_str(), "w")) {
-            fprintf(out, "%llu\n", gen);
-            fclose(out);
-            rename(tmp.c_str(), (path + ".applied").c_str());
-          }
-        }
+    if (!f) return have;
+    std::string text((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+    std::vector<Backend*> list;
+    if ((have && text == last) || !parse_backends(text, &list)) return have;
+    publish_set(std::move(list));
+    fprintf(stderr, "rrproxy: endpoints now %zu backends\n", current_set().list.size());
+    last = std::move(text);
+    have = true;
+    unsigned long long gen = 0;
+    if (sscanf(last.c_str(), "# gen %llu", &gen) == 1) {
+      const std::string tmp = path + ".applied.tmp";
+      if (FILE* out = fopen(tmp.c_str(), "w")) {
+        fprintf(out, "%llu\n", gen);
+        fclose(out);
+        rename(tmp.c_str(), (path + ".applied").c_str());
       }
     }
-    std::this_thread::sleep_for(std::chrono::milliseconds(10));
+    return true;
   }
-}
+
+  void loop() {
+    while (!g_stop.load()) {
+      poll();
+      std::this_thread::sleep_for(std::chrono::milliseconds(10));
+    }
+  }
+};
 
 int socket_error(int fd) {
   int e = 0;
@@ -643,6 +650,11 @@ int main(int argc, char** argv) {
     return 2;
   }
   publish_set(std::move(initial));
+  // Read the endpoints before listening (and before the port file says so): a client that
+  // connects in between would otherwise meet an empty set and be reset.
+  EndpointsFollower follower;
+  follower.path = endpoints_file;
+  if (!endpoints_file.empty()) follower.poll();
   if (threads < 1) threads = 1;
   std::vector<int> cpus;
   if (!cpu_list.empty() && !parse_cpu_list(cpu_list, &cpus)) {
@@ -686,7 +698,7 @@ int main(int argc, char** argv) {
   std::thread hc;
   if (health_ms > 0) hc = std::thread(health_loop, health_ms);
   std::thread ep;
-  if (!endpoints_file.empty()) ep = std::thread(endpoints_loop, endpoints_file);
+  if (!endpoints_file.empty()) ep = std::thread([&follower] { follower.loop(); });
   std::vector<std::thread> ws;
   for (auto& l : loops) ws.emplace_back([p = l.get()] { p->run(); });
   int sig;

@@ -707,11 +707,15 @@ def test_a_stuck_worker_cannot_hold_the_termination_forever(hola):
     libc = ctypes.CDLL(None, use_errno=True)
     libc.ptrace.argtypes = [ctypes.c_long, ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p]
     PTRACE_SEIZE, PTRACE_INTERRUPT, WALL = 0x4206, 0x4207, 0x40000000
-    tid = next(int(t.name) for t in Path(f"/proc/{s.proc.pid}/task").iterdir()
-               if (t / "comm").read_text().strip() == "hola-w1")
-    # the worker must be in its loop (blocked in epoll_wait) before it is stopped: a sanitizer
-    # build can still be starting it when the listener is up
+    # the worker must be named and in its loop (blocked in epoll_wait) before it is stopped:
+    # under load, or in a sanitizer build, it can still be starting when the listener is up
     deadline = time.monotonic() + 10
+    tid = None
+    while tid is None and time.monotonic() < deadline:
+        tid = next((int(t.name) for t in Path(f"/proc/{s.proc.pid}/task").iterdir()
+                    if (t / "comm").read_text().strip() == "hola-w1"), None)
+        time.sleep(0.0 if tid else 0.02)
+    assert tid is not None, "no hola-w1 thread"
     while "ep_poll" not in (Path(f"/proc/{s.proc.pid}/task/{tid}/wchan").read_text() or "") \
             and time.monotonic() < deadline:
         time.sleep(0.02)

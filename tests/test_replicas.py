@@ -145,6 +145,32 @@ def test_proxy_reports_why_sessions_ended():
     assert "backend connects failed 1 (last Connection refused)" in line, line
 
 
+def test_proxy_reads_its_endpoints_before_it_listens(tmp_path):
+    """Service mode (--endpoints-file): the set is read before the port is bound and the port
+    file written, so the first client is routed, not reset on an empty set (a race the
+    sanitized endpoints test once met as `backend connects failed 2`)."""
+    from hola_amd.native import binary
+
+    eps, port_file, log_path = tmp_path / "eps", tmp_path / "port", tmp_path / "proxy.log"
+    with ReplicaSet(2, threads_per_replica=1, supervise=False) as rs, open(log_path, "wb") as log:
+        eps.write_text("# gen 7\n" + "".join(f"{h}:{p}\n" for h, p in rs.targets))
+        proc = subprocess.Popen([str(binary("hola_rrproxy")), "--host", "127.0.0.1", "--port", "0",
+                                 "--endpoints-file", str(eps), "--health-ms", "0", "--no-failover",
+                                 "--port-file", str(port_file)], stderr=log)
+        try:
+            deadline = time.monotonic() + 10
+            while not port_file.exists() and time.monotonic() < deadline:
+                time.sleep(0.001)
+            assert greeting_via(int(port_file.read_text())).startswith("Hola de replica-")
+        finally:
+            proc.send_signal(signal.SIGTERM)
+            proc.wait(timeout=10)
+    text = log_path.read_text()
+    assert text.index("endpoints now 2 backends") < text.index("listening on"), text
+    assert "-> 2 backends" in text and "backend connects failed 0" in text, text
+    assert (tmp_path / "eps.applied").read_text().strip() == "7"
+
+
 def test_supervisor_restarts_crashed_replica():
     with ReplicaSet(2, threads_per_replica=1, supervise=True) as rs:
         old = rs.procs[0].proc.pid
