@@ -654,7 +654,9 @@ int main(int argc, char** argv) {
   // connects in between would otherwise meet an empty set and be reset.
   EndpointsFollower follower;
   follower.path = endpoints_file;
-  if (!endpoints_file.empty()) follower.poll();
+  if (!endpoints_file.empty() && !follower.poll())
+    fprintf(stderr, "rrproxy: no endpoints in %s yet: connections are closed at once until there are\n",
+            endpoints_file.c_str());
   if (threads < 1) threads = 1;
   std::vector<int> cpus;
   if (!cpu_list.empty() && !parse_cpu_list(cpu_list, &cpus)) {
