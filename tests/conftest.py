@@ -12,6 +12,12 @@ def pytest_sessionstart(session):
     # HOLA_SANITIZER=tsan|asan: build that preset and run every integration test against it
     # (SURVEY.md §5.2), e.g. `HOLA_SANITIZER=asan pytest tests/test_contract.py tests/test_chaining.py`.
     san = os.environ.get("HOLA_SANITIZER")
+    if not san and "PYTEST_XDIST_WORKER" not in os.environ:
+        # build stale binaries once, before any (xdist) worker runs them: a worker's own
+        # rebuild would relink executables that other workers are starting
+        from hola_amd.native import ensure_built
+
+        ensure_built("release")
     if san:
         from hola_amd.native import build, build_dir
 
