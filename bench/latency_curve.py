@@ -33,7 +33,7 @@ cores = plan_node(1)[0]
 srv, lg = split_server_loadgen(cores, max(1, len(cores) // 2))
 rows = []
 server_bp = a.server_busy_poll or str(a.busy_poll_us)
-server_args = ["--busy-poll-us", server_bp] if server_bp != "0" else []
+server_args = ["--busy-poll-us", server_bp]  # always explicit: hola's own default is auto
 with HolaProcess(args=server_args, env={"HOSTNAME": "h"}, threads=len(srv), cpu_list=format_cpu_list(srv),
                  log_level="warn") as s:
     def server_cpu():
