@@ -59,6 +59,6 @@ with HolaProcess(args=server_args, env={"HOSTNAME": "h"}, threads=len(srv), cpu_
         rows.append(row)
         print(json.dumps(row), flush=True)
 out = {"cpu_map": {"server": format_cpu_list(srv), "loadgen": format_cpu_list(lg)}, "connections": a.connections,
-       "busy_poll_us": a.busy_poll_us, "server_busy_poll": server_bp, "spin_us": a.spin_us, "rows": rows}
+       "busy_poll_us": a.busy_poll_us, "server_busy_poll": server_bp, "server_args": server_args, "spin_us": a.spin_us, "rows": rows}
 if a.out:
     Path(a.out).write_text(json.dumps(out, indent=1))

@@ -276,3 +276,18 @@ def test_forced_smt_pair_stays_inside_the_cpu_budget(monkeypatch):
         monkeypatch.setattr(bench, "sibling_of", sib)
         p = bench._plan(a, 1, avoid_busy=False)
         assert seen == {"n": 1, "per_rank": want, "smt": "pair"} and p["cores_per_slot"] == want, (budget, seen)
+
+
+def test_latency_curve_runs_open_loop_with_the_server_busy_poll_it_names(tmp_path):
+    """`bench/latency_curve.py` (the open-loop curve of `box_session.sh latency`): one short
+    rate on the CPU, every body checked, and `server_busy_poll` "0" means the server really ran
+    with `--busy-poll-us 0` (hola's own default is auto, so the flag must be passed)."""
+    out = tmp_path / "curve.json"
+    r = subprocess.run([sys.executable, str(ROOT / "bench" / "latency_curve.py"), "--rates", "20000",
+                        "--duration", "1", "--out", str(out)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads(out.read_text())
+    assert d["server_busy_poll"] == "0"
+    (row,) = d["rows"]
+    assert row["errors"] == 0 and row["achieved_rps"] > 0.9 * row["target_rps"], row
+    assert d["server_args"] == ["--busy-poll-us", "0"]
