@@ -486,8 +486,15 @@ def test_chaining_latency_histogram(hola, aloha):
     aloha.set_mode("slow", delay_s=1.0)
     for _ in range(2):  # both end at the 600 ms Hystrix timeout
         assert chain(s)[1:] == [FALLBACK]
-    _, _, body = s.get("/metrics")
-    b, total, count = _histogram(body, "hola_chaining_duration_seconds")
+    # a call is recorded on its worker as it finishes, which can be just after its answer
+    # left: the scrape (on any worker) sees it within moments
+    deadline = time.monotonic() + 3
+    while True:
+        _, _, body = s.get("/metrics")
+        b, total, count = _histogram(body, "hola_chaining_duration_seconds")
+        if count == 6 or time.monotonic() > deadline:
+            break
+        time.sleep(0.02)
     les = list(b)
     assert les[-1] == "+Inf" and count == 6 and b["+Inf"] == 6
     assert all(b[x] <= b[y] for x, y in zip(les, les[1:]))  # cumulative
