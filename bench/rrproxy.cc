@@ -63,7 +63,10 @@ struct Backend {
   int port;
   sockaddr_storage addr;
   socklen_t len;
-  std::vector<int> l3;  // L3 domains of its workers (topology hint); empty = unknown
+  // L3 domains of its workers (topology hint); empty = unknown. Written and read only by the
+  // thread that parses backend lists (under g_backends_mu); proxy threads read the copy in the
+  // published BackendSet, which never changes once published.
+  std::vector<int> hint;
   std::atomic<bool> healthy{true};
   std::atomic<uint64_t> picked{0};
 };
@@ -75,6 +78,7 @@ std::mutex g_backends_mu;  // guards g_backends growth (the endpoints reloader)
 // is kept (a few pointers) because a loop thread may still be reading it.
 struct BackendSet {
   std::vector<Backend*> list;
+  std::vector<std::vector<int>> l3;  // list[i]'s topology hint, copied at publish
 };
 std::atomic<const BackendSet*> g_set{nullptr};
 std::vector<std::unique_ptr<BackendSet>> g_sets;  // owner of every set published
@@ -105,8 +109,10 @@ Backend* pick(int l3 = -1, uint64_t* rr = nullptr) {
   if (l3 >= 0 && rr) {
     // topology hints: the healthy backends in this thread's L3, round-robin
     for (size_t k = 0; k < n; ++k) {
-      Backend* b = set.list[(*rr)++ % n];
-      if (b->healthy.load(std::memory_order_relaxed) && std::find(b->l3.begin(), b->l3.end(), l3) != b->l3.end())
+      const size_t i = (*rr)++ % n;
+      Backend* b = set.list[i];
+      const std::vector<int>& doms = set.l3[i];
+      if (b->healthy.load(std::memory_order_relaxed) && std::find(doms.begin(), doms.end(), l3) != doms.end())
         return b;
     }
   }
@@ -160,10 +166,13 @@ bool parse_backends(const std::string& text, std::vector<Backend*>* out) {
     if (host.size() > 2 && host.front() == '[' && host.back() == ']') host = host.substr(1, host.size() - 2);
     Backend* b = backend_for(host, atoi(t.substr(colon + 1).c_str()));
     if (!b) return false;
-    if (!cpus.empty() && b->l3.empty()) {  // set once (a reload may name it again)
-      for (int c : cpus)
-        if (int d = l3_domain_of(c); d >= 0 && std::find(b->l3.begin(), b->l3.end(), d) == b->l3.end())
-          b->l3.push_back(d);
+    if (!cpus.empty()) {
+      std::lock_guard<std::mutex> g(g_backends_mu);
+      if (b->hint.empty()) {  // set once (a reload may name it again, with or without a hint)
+        for (int c : cpus)
+          if (int d = l3_domain_of(c); d >= 0 && std::find(b->hint.begin(), b->hint.end(), d) == b->hint.end())
+            b->hint.push_back(d);
+      }
     }
     if (std::find(out->begin(), out->end(), b) == out->end()) out->push_back(b);
   }
@@ -173,6 +182,12 @@ bool parse_backends(const std::string& text, std::vector<Backend*>* out) {
 void publish_set(std::vector<Backend*> list) {
   auto set = std::make_unique<BackendSet>();
   set->list = std::move(list);
+  {
+    // The hints as of now, copied: a later reload that adds a hint to a backend of this set
+    // changes the Backend, never a set a proxy thread may be reading.
+    std::lock_guard<std::mutex> g(g_backends_mu);
+    for (Backend* b : set->list) set->l3.push_back(b->hint);
+  }
   for (Backend* b : set->list) b->healthy.store(true);  // listed = Ready (the executor probed it)
   g_set.store(set.get(), std::memory_order_release);
   g_sets.push_back(std::move(set));

@@ -105,6 +105,16 @@ class _AlohaHandler(BaseHTTPRequestHandler):
             self.wfile.flush()
             self.connection.shutdown(socket.SHUT_WR)
             return
+        if mode == "interim_close_once":  # a 100 Continue, then the connection closes; next ones ok
+            with owner.lock:
+                owner.mode = "ok"
+            self.wfile.write(b"HTTP/1.1 100 Continue\r\n\r\n")
+            self.wfile.flush()
+            self.close_connection = True
+            self.connection.shutdown(socket.SHUT_RDWR)
+            return
+        if mode == "interim_flood":  # 96 KiB of interim responses before the final one
+            self.wfile.write(b"HTTP/1.1 100 Continue\r\n\r\n" * (96 * 1024 // 25))
         if mode == "interim":  # unasked-for 1xx responses before the final one (RFC 9110 §15.2)
             self.wfile.write(b"HTTP/1.1 100 Continue\r\n\r\n"
                              b"HTTP/1.1 103 Early Hints\r\nLink: </aloha.css>; rel=preload\r\n\r\n")

@@ -122,6 +122,9 @@ bool AddressCache::get(sockaddr_storage* out, socklen_t* len, std::string* err) 
 // ---------------------------------------------------------------- connection
 
 constexpr int kTransportRetries = 3;  // DefaultHttpRequestRetryHandler(3, false)
+// Interim 1xx responses accepted before a call's final response: the 64 KiB a response head
+// may take. Past it the answer is treated as malformed.
+constexpr size_t kMaxInterimBytes = 64 * 1024;
 // How long the calls queued behind an abandoned pipelined call wait for its answer before they
 // are re-sent on fresh connections (see ClientPool::cancel).
 constexpr int kDrainGraceMs = 50;
@@ -146,7 +149,8 @@ struct ClientPool::Conn final : EventLoop::Handler {
   Callback cb;
   bool reused = false;  // went out on a kept-alive socket
   int tries = 0;        // transport re-executions so far (DefaultHttpRequestRetryHandler)
-  bool head_ok = false;  // a complete, well-formed status line + header block has arrived
+  bool head_ok = false;  // a complete, well-formed final status line + header block has arrived
+  size_t interim_bytes = 0;  // interim 1xx responses read (and dropped) for the call in flight
   uint32_t interest = 0;
 
   void set_interest(uint32_t ev) {
@@ -182,6 +186,7 @@ struct ClientPool::PConn final : EventLoop::Handler {
   std::string out, in;
   size_t off = 0;
   std::deque<Pending> q;
+  size_t front_interim = 0;  // interim 1xx bytes read (and dropped) for the oldest request
   uint32_t interest = 0;
 
   void set_interest(uint32_t ev) {
@@ -408,11 +413,15 @@ int parse_one(std::string_view in, bool eof, ClientResult* r, bool* close, size_
   r->retry_after_ms = retry_after_ms;
   *close = conn_close;
   size_t body = p;
-  *head_ok = true;  // the server has answered: the call is no longer safe to send again
+  *interim = status < 200 && status != 101;
+  // A final head: the server has answered, the call is no longer safe to send again. An
+  // interim 1xx is not an answer: HttpClient 4.5's HttpRequestExecutor reads past it inside
+  // execute(), and a connection that closes before the final head throws
+  // NoHttpResponseException there, which the retry handler re-sends for an idempotent GET.
+  if (!*interim) *head_ok = true;
   if (status == 204 || status == 304 || (status >= 100 && status < 200)) {
     r->status = status;
     *consumed = body;
-    *interim = status < 200 && status != 101;
     return 1;
   }
   if (chunked) {
@@ -446,13 +455,19 @@ int parse_one(std::string_view in, bool eof, ClientResult* r, bool* close, size_
 // parse_one() past any interim 1xx responses (100 Continue, 102 Processing, 103 Early Hints):
 // a client must accept them before the final response even unasked (RFC 9110 §15.2), and
 // HttpClient's request executor reads past every one. 101 ends the exchange (no upgrade here).
+// When the final response is still incomplete (0), *consumed is the length of the interims
+// before it, so the caller can drop them and never parse them again: re-parsing every interim
+// on each read of a downstream that keeps sending them was quadratic.
 int parse_response(std::string_view in, bool eof, ClientResult* r, bool* close, size_t* consumed, bool* head_ok) {
   size_t off = 0;
   for (;;) {
     bool interim = false;
     size_t used = 0;
     const int rc = parse_one(in.substr(off), eof, r, close, &used, head_ok, &interim);
-    if (rc != 1) return rc;
+    if (rc != 1) {
+      *consumed = rc == 0 ? off : 0;
+      return rc;
+    }
     off += used;
     if (!interim) {
       *consumed = off;
@@ -474,6 +489,14 @@ int ClientPool::Conn::try_parse(ClientResult* r, bool* keep, bool eof) {
   const int rc = parse_response(in, eof, r, &close, &consumed, &head_ok);
   // a response followed by stray bytes leaves a connection that cannot be reused
   if (rc == 1) *keep = !close && consumed == in.size();
+  if (rc == 0 && consumed) {
+    // interim responses before a final one still due: dropped, and bounded per call (the
+    // 64 KiB a response head may take), so a downstream that sends nothing but 1xx fails
+    // the call as malformed instead of holding it until the timeout
+    interim_bytes += consumed;
+    in.erase(0, consumed);
+    if (interim_bytes > kMaxInterimBytes) return -1;
+  }
   return rc;
 }
 
@@ -742,6 +765,7 @@ void ClientPool::start_on(Conn* c, uint64_t id, std::string* req, Callback cb, b
   c->in.clear();
   c->reused = reused;
   c->head_ok = false;
+  c->interim_bytes = 0;
   set_active(id, c);
   if (reused) {
     c->st = Conn::kWriting;
@@ -1035,8 +1059,15 @@ void ClientPool::PConn::do_read() {
       }
       if (rc == 0) {
         front_head = head_ok;
+        used += consumed;  // the front's interim responses: dropped (parse_response)
+        front_interim += consumed;
+        if (front_interim > kMaxInterimBytes) {
+          pool->pfail(this, "ClientProtocolException: malformed response", q.front().id, !head_ok);
+          return;
+        }
         break;
       }
+      front_interim = 0;
       used += consumed;
       Pending p = std::move(q.front());
       q.pop_front();

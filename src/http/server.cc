@@ -550,9 +550,15 @@ Worker* Server::pick_worker(int fd) {
       // L3s for the whole run, +20 % CPU per chained request (profiles/round5/02_chain_modes).
       // Within an L3 the connections are dealt round-robin, so they stay even there.
       auto within_share = [&](size_t w) {
-        int64_t total = 0;
-        for (size_t i = 0; i < n; ++i) total += assigned_[i].load(std::memory_order_relaxed);
-        return int64_t(assigned_[w].load(std::memory_order_relaxed)) <= 2 * total / int64_t(n) + 8;
+        int32_t small[256];
+        std::vector<int32_t> big;  // more than 256 workers in one process: once per accept
+        int32_t* counts = small;
+        if (n > 256) {
+          big.resize(n);
+          counts = big.data();
+        }
+        for (size_t i = 0; i < n; ++i) counts[i] = assigned_[i].load(std::memory_order_relaxed);
+        return steering_within_share(counts, n, w);
       };
       // Same physical core first (the client runs on this worker's SMT sibling).
       const int core = core_workers_.empty() ? -1 : core_of(cpu);
@@ -576,7 +582,16 @@ Worker* Server::pick_worker(int fd) {
           k = cand;
           steered_.fetch_add(1, std::memory_order_relaxed);
         } else {
+          // Refused for balance: the least loaded worker. The round-robin index would alias
+          // with the refusals' period (every third accept refused with three workers: the
+          // same worker every time, the third idle).
           unsteered_.fetch_add(1, std::memory_order_relaxed);
+          int32_t least = INT32_MAX;
+          for (size_t i = 0; i < n; ++i)
+            if (int32_t c = assigned_[i].load(std::memory_order_relaxed); c < least) {
+              least = c;
+              k = i;
+            }
         }
         break;
       }

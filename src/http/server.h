@@ -311,6 +311,25 @@ class Server {
   static const char* locality_name(int l);
   uint64_t locality(int l) const { return locality_[l].load(std::memory_order_relaxed); }
 
+  // Accept steering's balance rule: may worker w (live connections counts[w]) take one more
+  // steered connection? With three or more workers, unless it already holds twice its fair
+  // share + 8: a bound relative to the total, so that clients of one L3 opening theirs before
+  // those of another do not push the late ones off their own L3 for the whole run
+  // (profiles/round5/02_chain_modes). With one or two workers that bound refuses nothing
+  // (counts[w] <= total always), so there the worker may lead the least loaded one by at most
+  // max(8, total / n): two workers in two L3s fed by clients of one L3 keep a 3:1 split at
+  // worst instead of one worker taking every connection.
+  static bool steering_within_share(const int32_t* counts, size_t n, size_t w) {
+    int64_t total = 0, least = INT64_MAX;
+    for (size_t i = 0; i < n; ++i) {
+      total += counts[i];
+      least = counts[i] < least ? counts[i] : least;
+    }
+    if (n >= 3) return counts[w] <= 2 * total / int64_t(n) + 8;
+    const int64_t slack = total / int64_t(n) > 8 ? total / int64_t(n) : 8;
+    return counts[w] - least <= slack;
+  }
+
  private:
   struct Acceptor : EventLoop::Handler {
     Server* server;

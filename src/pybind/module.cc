@@ -498,11 +498,15 @@ py::dict inline_function_selftest() {
 
 }  // namespace
 
+namespace hola::isa {
+extern char g_module_isa_error[512];  // src/pybind/isa_flag.cc
+}
+
 PYBIND11_MODULE(_native, m) {
   // The module is built at the release -march: on a CPU that lacks it, fail the import with
-  // the reason instead of a SIGILL later (src/core/isa.h).
-  if (const std::string missing = isa::missing_features(); !missing.empty())
-    throw py::import_error(isa::error_line("hola_amd._native"));
+  // the reason instead of a SIGILL later (src/core/isa.h). The check itself ran as the
+  // module's first static initialiser (src/pybind/isa_flag.cc), which printed the line.
+  if (isa::g_module_isa_error[0]) throw py::import_error(isa::g_module_isa_error);
   m.doc() = "hola native core (C++20) bindings";
   m.def("isa_build_level", &isa::build_level);
   m.def("build_info", [] {
@@ -586,6 +590,10 @@ PYBIND11_MODULE(_native, m) {
     return py::make_tuple(rc, r.status, py::bytes(r.body), close, consumed, head_ok);
   }, py::arg("data"), py::arg("eof") = false);
   m.def("client_next_generation", [](uint32_t g) { return client::ClientPool::next_generation(g); });
+  m.def("steering_within_share", [](const std::vector<int32_t>& counts, size_t w) {
+    if (w >= counts.size()) throw py::index_error("worker index");
+    return http::Server::steering_within_share(counts.data(), counts.size(), w);
+  });
   m.def("loop_lost_epoll_probe", &loop_lost_epoll_probe);
   m.def("loop_timer_order", &loop_timer_order, py::arg("delays"), py::arg("cancel") = std::vector<int>{});
   m.def("span_ring", &span_ring);

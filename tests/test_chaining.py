@@ -86,6 +86,33 @@ def test_interim_1xx_responses_are_read_past(hola, aloha, pipeline):
     assert _events(s).get("SUCCESS") == 4
 
 
+def test_interim_then_close_is_a_transport_retry(hola, aloha):
+    """a 100 Continue is not an answer. HttpClient 4.5 reads past it inside
+    execute(); a connection that then closes before the final head throws
+    NoHttpResponseException there, which DefaultHttpRequestRetryHandler re-sends for an
+    idempotent GET. So the call is re-sent on a fresh connection and succeeds."""
+    aloha.set_mode("interim_close_once")
+    s = hola(args=["--aloha-url", aloha.url, "--no-tracing", "--feign-log", "none", "--feign-retry", "off"],
+             env={"HOSTNAME": "h"}, threads=1)
+    assert chain(s) == ["Hola de h", "Aloha mai aloha-1", "Bonjour de bonjour-1"]
+    assert len(aloha.requests) == 2
+    assert _events(s).get("SUCCESS") == 1
+
+
+@pytest.mark.parametrize("pipeline", [1, 8])
+def test_interim_flood_is_bounded(hola, aloha, pipeline):
+    """interim responses before a final one are capped at 64 KiB per call (they are
+    dropped as they are read, never re-parsed). 96 KiB of 100 Continue is a malformed answer:
+    the fallback, at once rather than at the 600 ms timeout."""
+    aloha.set_mode("interim_flood")
+    s = hola(args=["--aloha-url", aloha.url, "--no-tracing", "--feign-log", "none", "--feign-retry", "off",
+                   "--aloha-pipeline", str(pipeline)], env={"HOSTNAME": "h"}, threads=1)
+    t0 = time.monotonic()
+    assert chain(s) == ["Hola de h", FALLBACK]
+    assert time.monotonic() - t0 < 0.5
+    assert _events(s).get("TIMEOUT", 0) == 0
+
+
 def _events(s) -> dict:
     """Rolling Hystrix event counts of the aloha command from /metrics."""
     _, _, body = s.get("/metrics")

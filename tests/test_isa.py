@@ -6,6 +6,7 @@ import os
 import random
 import socket
 import subprocess
+import sys
 
 import pytest
 
@@ -23,6 +24,24 @@ def test_missing_feature_is_one_clear_line_and_exit_1(name):
     assert len(lines) == 1, r.stderr
     assert lines[0].startswith(f"{name}: this build needs an x86-64-v3 CPU and this one lacks avx2,bmi2")
     assert "portable" in lines[0] and r.stdout == ""
+
+
+def test_module_import_fails_with_the_line_printed_first():
+    """the Python module checks the CPU in its first static initialiser (baseline
+    code, init priority 101, src/pybind/isa_flag.cc): the line reaches stderr before any
+    initialiser built for the -march runs, and the import then fails with it."""
+    code = ("import sys\n"
+            "try:\n"
+            "    import hola_amd._native\n"
+            "except ImportError as e:\n"
+            "    print('IMPORT ERROR:', e)\n"
+            "    sys.exit(3)\n")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60,
+                       cwd=str(native.REPO), env={**os.environ, "HOLA_ISA_PRETEND_MISSING": "avx2"})
+    assert r.returncode == 3, (r.returncode, r.stdout, r.stderr)
+    line = "hola_amd._native: this build needs an x86-64-v3 CPU and this one lacks avx2"
+    assert r.stderr.startswith(line), r.stderr
+    assert "IMPORT ERROR: " + line in r.stdout
 
 
 def test_features_above_the_build_level_are_not_required(native):

@@ -201,7 +201,9 @@ def test_sanitized_proxy_endpoints_mode(preset, tmp_path):
     """hola_rrproxy in the executor's Service mode (--endpoints-file, no failover) built with a
     sanitizer: keep-alive sessions through it while the endpoints file is replaced again and
     again (the follower thread publishing new backend sets under the session loops), then
-    SIGTERM with sessions open."""
+    SIGTERM with sessions open. From generation 10 on the lines carry topology hints
+    (`h:p@0`), so a reload adds a hint to backends of the set the loops are dealing from: the
+    hints live in the published set, never in a Backend a loop is reading."""
     import subprocess
 
     from hola_amd.parallel.replicas import ReplicaSet
@@ -216,7 +218,8 @@ def test_sanitized_proxy_endpoints_mode(preset, tmp_path):
 
         def publish(gen, chosen):
             tmp = tmp_path / "eps.tmp"
-            tmp.write_text(f"# gen {gen}\n" + "".join(t + "\n" for t in chosen))
+            hint = "@0" if gen >= 10 else ""  # CPU 0's L3, where the proxy threads run here
+            tmp.write_text(f"# gen {gen}\n" + "".join(t + hint + "\n" for t in chosen))
             os.replace(tmp, eps)
 
         publish(1, targets)
