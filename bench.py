@@ -163,6 +163,14 @@ def parse_args():
                     help="N = 1 only: the headline replica again in the other SMT layout for about this long "
                          "(alt_* keys): pair on a 1-GPU box, off on an 8-GPU node, so BENCH and SCALE's N = 1 "
                          "each carry a figure in the other's layout. 0 = skip")
+    ap.add_argument("--v4-seconds", type=float, default=10.0,
+                    help="N = 1 only: the headline replica and load generator again over IPv4 loopback (the "
+                         "image binds 0.0.0.0) for about this long, when the headline ran on ::1 (v4_* keys). "
+                         "0 = skip")
+    ap.add_argument("--plain-seconds", type=float, default=10.0,
+                    help="N > 1 only: after the timed region every rank's load generator runs this long from its "
+                         "own cores dealing its connections over all replicas, with no client placement, as a "
+                         "LoadBalancer Service deals them (plain_* keys; `value` is untouched). 0 = skip")
     ap.add_argument("--chain-pool", type=int, default=128,
                     help="hola A's Hystrix thread-pool (bulkhead) size in the chain sub-run: the reference's "
                          "10 would turn most of 64 concurrent calls into fallbacks (SURVEY.md D2)")
@@ -325,6 +333,7 @@ def main() -> int:
             dist.barrier()
         cuda()
         span0 = span_counters(host, port, probe)
+        m0 = subruns.metrics_counters(port, host, probe)
         sink0 = sink_stats(plan[0]["sink_port"]) if local_rank == 0 else {}
         tracer0 = thread_cpu_s(server.proc.pid, "hola-tracer")
         cpu0 = (proc_cpu_s(server.proc.pid), proc_cpu_s(loadgen.proc.pid))
@@ -344,6 +353,7 @@ def main() -> int:
         cpu1 = (proc_cpu_s(server.proc.pid), proc_cpu_s(loadgen.proc.pid))
         tracer1 = thread_cpu_s(server.proc.pid, "hola-tracer")
         span1 = span_counters(host, port, probe)
+        m1 = subruns.metrics_counters(port, host, probe)
         locality1 = accept_locality(host, port, probe)
         locality = {k: v - locality0.get(k, 0) for k, v in locality1.items()}
         sink1 = sink_stats(plan[0]["sink_port"]) if local_rank == 0 else {}
@@ -353,6 +363,20 @@ def main() -> int:
         own = set(server_cpus) | set(load_cpus)
         st = loadgen.stats()
         mem = server.memory_kb()
+        plain = None
+        if dist and a.plain_seconds > 0 and not a.plain_dealing:
+            # the topology-blind front on the same replicas, every rank at once (after the timed
+            # region: `value` is untouched)
+            loc_p0 = accept_locality(host, port, probe)
+            dist.barrier()
+            try:
+                plain = subruns.plain_dealing_run(a, targets, local_rank, plan[0]["own_loadgen"][local_rank], bodies,
+                                                  a.plain_seconds)
+            except Exception as e:  # noqa: BLE001 - reported in the JSON
+                plain = {"error": f"{type(e).__name__}: {e}"}
+            dist.barrier()
+            loc_p1 = accept_locality(host, port, probe)
+            plain["locality"] = {k: v - loc_p0.get(k, 0) for k, v in loc_p1.items()}
         c1 = subruns.config2(a, host, port, server_cpus, load_cpus, bodies and [bodies[local_rank]],
                              job_cpus) if local_rank == 0 else None
 
@@ -366,10 +390,13 @@ def main() -> int:
                  "server_cpus": format_cpu_list(server_cpus),
                  "load_cpus": format_cpu_list(load_cpus),
                  "server_cpu_s": cpu1[0] - cpu0[0], "loadgen_cpu_s": cpu1[1] - cpu0[1],
+                 # where the replica's and the load generator's time went
+                 "server_loop": subruns.loop_block(m0, m1, reqs),
+                 "loadgen_loop": subruns.loadgen_block(st, cpu1[1] - cpu0[1], reqs),
                  "startup_ms": server.startup_ms, "rss_peak_kb": mem.get("VmHWM", 0),
                  "tcp": {k: tcp1[k] - tcp0[k] for k in tcp1 if k in tcp0},
                  "cgroup": {k: thr1[k] - thr0[k] for k in thr1 if k in thr0},
-                 "per_conn": per_conn,
+                 "per_conn": per_conn, "plain": plain,
                  # host-wide busy share over the timed region of this rank's CPUs and of those of
                  # their SMT siblings that no part of this job uses (busy there = another tenant)
                  "host_load": subruns.host_load(times0, times1, own, job_cpus)}
@@ -391,6 +418,10 @@ def main() -> int:
     if world == 1:
         rank_cpus = list(server_cpus) + list(load_cpus)
         for key, secs, fn in (
+                # the headline on the image's address family, when it ran on ::1
+                ("v4", a.v4_seconds if host != "127.0.0.1" else 0,
+                 lambda: subruns.v4_headline(a, args, server_cpus, load_cpus, conn_targets, job_cpus,
+                                             bodies and [bodies[0]], a.v4_seconds)),
                 ("deployed", a.deployed_seconds,
                  lambda: subruns.deployed(a, server_cpus, load_cpus, job_cpus, zipkin=a.deployed_zipkin)),
                 # the same, sized as the manifests size one pod (limits.cpu: a 2-CPU cpuset)
@@ -440,6 +471,10 @@ def main() -> int:
             # host CPU time per request (user+sys, all threads) over the timed region
             "server_cpu_us_per_req": round(1e6 * sum(g["server_cpu_s"] for g in gathered) / max(1, total), 3),
             "loadgen_cpu_us_per_req": round(1e6 * sum(g["loadgen_cpu_s"] for g in gathered) / max(1, total), 3),
+            # ... less the CPU both spent in polls that found nothing (spinning): the CPU that
+            # did work, an efficiency figure that does not follow the spin (at saturation both
+            # raw figures are the CPUs' wall time over the request count: equal by construction)
+            **_busy_keys(gathered, total),
             # replica footprint: exec -> listening, and peak resident memory (max over ranks)
             "server_startup_ms": round(max(g["startup_ms"] or 0 for g in gathered), 1),
             "server_rss_peak_mb": round(max(g["rss_peak_kb"] for g in gathered) / 1024.0, 1),
@@ -466,17 +501,18 @@ def main() -> int:
             # --busy-poll-us auto, ZIPKIN_SERVER_URL set), same load generator
             **_deployed_keys(subs.get("deployed")),
             # ... in one pod's CPU limit (deploy/openshift: limits.cpu 2): what one pod of
-            # BASELINE config 5 serves on its own
-            **{k.replace("deployed_", "deployed_pod_", 1): v for k, v in _deployed_keys(subs.get("deployed_pod")).items()
-               if k in ("deployed_rps", "deployed_p50_ms", "deployed_p99_ms", "deployed_requests", "deployed_errors",
-                        "deployed_non2xx", "deployed_body_mismatch", "deployed_server_cpu_us_per_req", "deployed_cpus",
-                        "deployed_host_load", "deployed_error")},
+            # BASELINE config 5 serves on its own, with the attribution of its CPU per request
+            **_deployed_keys(subs.get("deployed_pod"), "deployed_pod", full=False),
             # N = 1 only: GET /api/hola-chaining through two replicas (the endpoint with real work
             # behind it), engineered (pool 128, logging off) and as shipped (pool 10, BASIC logging)
             **_chain_keys(subs.get("chain"), "chain"),
             **_chain_keys(subs.get("chain_shipped"), "chain_shipped"),
             # N = 1 only: the headline in the other SMT layout (BENCH <-> SCALE N = 1 comparison)
             **_alt_keys(subs.get("alt")),
+            # N = 1 only: the headline over IPv4 loopback (the image's transport)
+            **_v4_keys(subs.get("v4"), value),
+            # N > 1 only: the same replicas behind a topology-blind front (no client placement)
+            **_plain_keys([g["plain"] for g in gathered], value),
             # span accounting over the timed region, all replicas (per second)
             "tracing": _tracing_block(a, gathered, t, plan[0]["sink_port"]),
             # client thread vs. serving worker placement of every accepted connection
@@ -501,8 +537,11 @@ def main() -> int:
                 "step_sizing": (f"sized from the last warmup step to ~{a.step_seconds:g} s per step" if not a.reqs_per_conn
                                 else "fixed (--reqs-per-conn)"),
                 "pipeline": a.pipeline,
-                "lb": "client-side " + ("round-robin over all replicas from the rank's own cores" if a.plain_dealing
-                                        else plan[0]["cores"][local_rank].get("dealing", "round-robin")),
+                "lb": ("client-side round-robin over all replicas from the rank's own cores, no client placement"
+                       if a.plain_dealing else
+                       "client-side, clients placed: " + plan[0]["cores"][local_rank].get("dealing", "round-robin")
+                       + ". Each load-generator thread is pinned next to the replica(s) it drives; a LoadBalancer "
+                         "Service places no client (the topology-blind figure is plain_* at N > 1)"),
                 "loopback": host,
                 # physical cores under the replica's server workers (with smt=pair the load
                 # generator runs on their siblings; with smt=off on as many separate cores)
@@ -679,6 +718,32 @@ def _build_line() -> str:
         return f"unknown ({type(e).__name__})"
 
 
+def _busy_keys(gathered: list[dict], total: int) -> dict:
+    """server_/loadgen_busy_cpu_us_per_req and the loop accounting of the timed region, over
+    all ranks: waits that could sleep per request, gaps between polls past 100 us / 1 ms /
+    10 ms, the longest gap (replica: since start; load generator: in the timed region)."""
+    n = max(1, total)
+    srv = [g["server_loop"] for g in gathered]
+    lg = [g["loadgen_loop"] for g in gathered]
+
+    def loop_sum(rows, key):
+        return sum(r.get(key, 0) for r in rows)
+
+    return {
+        "server_busy_cpu_us_per_req": round(1e6 * (sum(g["server_cpu_s"] for g in gathered) - loop_sum(srv, "idle_spin_s")) / n, 3),
+        "loadgen_busy_cpu_us_per_req": round(1e6 * (sum(g["loadgen_cpu_s"] for g in gathered) - loop_sum(lg, "idle_spin_s")) / n, 3),
+        "server_loop": {"idle_spin_s": round(loop_sum(srv, "idle_spin_s"), 3),
+                        "blocking_waits_per_req": round(sum(r["blocking_waits_per_req"] for r in srv) / len(srv), 4),
+                        "gaps_over_100us": loop_sum(srv, "gaps_over_100us"), "gaps_over_1ms": loop_sum(srv, "gaps_over_1ms"),
+                        "gaps_over_10ms": loop_sum(srv, "gaps_over_10ms"),
+                        "gap_max_since_start_us": max(r["gap_max_since_start_us"] for r in srv)},
+        "loadgen_loop": {"idle_spin_s": round(loop_sum(lg, "idle_spin_s"), 3),
+                         "polls": {k: sum(r["polls"][k] for r in lg) for k in lg[0]["polls"]},
+                         "blocking_waits_per_req": round(sum(r["blocking_waits_per_req"] for r in lg) / len(lg), 4),
+                         "gaps_over_100us": loop_sum(lg, "gaps_over_100us"), "gaps_over_1ms": loop_sum(lg, "gaps_over_1ms"),
+                         "gaps_over_10ms": loop_sum(lg, "gaps_over_10ms"), "gap_max_us": max(r["gap_max_us"] for r in lg)}}
+
+
 def _chain_keys(c: dict | None, p: str) -> dict:
     """chain_* (engineered) or chain_shipped_* keys of a chain sub-run."""
     if not c:
@@ -717,6 +782,46 @@ def _chain_keys(c: dict | None, p: str) -> dict:
     return out
 
 
+def _v4_keys(r: dict | None, value: float) -> dict:
+    if not r:
+        return {}
+    if "error" in r:
+        return {"v4_error": r["error"]}
+    return {"v4_rps": round(r["rps"], 1), "v4_p50_ms": round(r["p50_ns"] / 1e6, 4), "v4_p99_ms": round(r["p99_ns"] / 1e6, 4),
+            "v4_p999_ms": round(r["p999_ns"] / 1e6, 4), "v4_requests": r["requests"], "v4_errors": r["errors"],
+            "v4_body_checked": r["body_checked"], "v4_body_mismatch": r["body_mismatch"],
+            "v4_elapsed_s": round(r["elapsed_s"], 2), "v4_server_cpu_us_per_req": round(r["cpu_us_per_req"], 3),
+            "v4_vs_value": round(r["rps"] / value, 4) if value else None, "v4_host_load": r["host_load"]}
+
+
+def _plain_keys(rows: list, value: float) -> dict:
+    """plain_* over all ranks: node-wide req/s (requests / the longest rank's elapsed time),
+    merged latency, errors, and where the connections' clients ran relative to the workers."""
+    rows = [r for r in rows if r]
+    if not rows:
+        return {}
+    errs = [r["error"] for r in rows if "error" in r]
+    if errs:
+        return {"plain_error": errs[0]}
+    t = max(r["elapsed_s"] for r in rows)
+    total = sum(r["requests"] for r in rows)
+    hist = merge_hists([decode_hist(r["hist"]) for r in rows])
+    loc: dict[str, int] = {}
+    for r in rows:
+        for k, v in r["locality"].items():
+            loc[k] = loc.get(k, 0) + v
+    n = sum(loc.values())
+    rps = total / t if t > 0 else 0.0
+    return {"plain_rps": round(rps, 1), "plain_p50_ms": round(percentile(hist, 50) / 1e6, 4),
+            "plain_p99_ms": round(percentile(hist, 99) / 1e6, 4), "plain_requests": total,
+            "plain_elapsed_s": round(t, 2), "plain_errors": sum(r["errors"] for r in rows),
+            "plain_non2xx": sum(r["non2xx"] for r in rows), "plain_body_checked": sum(r["body_checked"] for r in rows),
+            "plain_body_mismatch": sum(r["body_mismatch"] for r in rows),
+            "plain_vs_value": round(rps / value, 4) if value else None,
+            "plain_locality": {k: round(v / n, 4) for k, v in loc.items()} if n else {},
+            "plain_loadgen_cpus": [r["load_cpus"] for r in rows]}
+
+
 def _alt_keys(r: dict | None) -> dict:
     if not r:
         return {}
@@ -731,26 +836,41 @@ def _alt_keys(r: dict | None) -> dict:
             "alt_cpus": {"server": r["server_cpus"], "loadgen": r["loadgen_cpus"]}}
 
 
-def _deployed_keys(d: dict | None) -> dict:
+def _deployed_keys(d: dict | None, p: str = "deployed", full: bool = True) -> dict:
+    """deployed_* (or deployed_pod_*) keys of a deployed sub-run, with the attribution of its
+    server CPU per request (subruns.attributed_closed_loop)."""
     if not d:
         return {}
     if "error" in d:
-        return {"deployed_error": d["error"]}
-    return {"deployed_rps": round(d["rps"], 1), "deployed_p50_ms": round(d["p50_ns"] / 1e6, 4),
-            "deployed_p99_ms": round(d["p99_ns"] / 1e6, 4), "deployed_requests": d["requests"],
-            "deployed_elapsed_s": round(d["elapsed_s"], 2),
-            "deployed_errors": d["errors"], "deployed_non2xx": d["non2xx"],
-            "deployed_body_checked": d["body_checked"], "deployed_body_mismatch": d["body_mismatch"],
-            "deployed_server_cpu_us_per_req": round(d["cpu_us_per_req"], 3),
-            "deployed_host_load": d["host_load"],
-            "deployed_args": d["args"], "deployed_cpus": d["cpus"],
+        return {f"{p}_error": d["error"]}
+    out = {f"{p}_rps": round(d["rps"], 1), f"{p}_p50_ms": round(d["p50_ns"] / 1e6, 4),
+           f"{p}_p99_ms": round(d["p99_ns"] / 1e6, 4), f"{p}_requests": d["requests"],
+           f"{p}_elapsed_s": round(d["elapsed_s"], 2),
+           f"{p}_errors": d["errors"], f"{p}_non2xx": d["non2xx"],
+           f"{p}_body_checked": d["body_checked"], f"{p}_body_mismatch": d["body_mismatch"],
+           # the replica's threads' CPU per request; ... less its loop's empty polls; and all
+           # that its CPUs did per request (interrupt time included)
+           f"{p}_server_cpu_us_per_req": round(d["cpu_us_per_req"], 3),
+           f"{p}_server_busy_cpu_us_per_req": d["server_busy_cpu_us_per_req"],
+           f"{p}_server_cpus_us_per_req": d["server_cpus_us_per_req"],
+           # serving threads apart from the rest (tracer, logger), with context switches
+           f"{p}_server_threads": d["server_threads"], f"{p}_server_loop": d["server_loop"],
+           f"{p}_loadgen": d["loadgen"], f"{p}_tcp_per_req": d["tcp_per_req"],
+           f"{p}_host_load": d["host_load"], f"{p}_host_load_server": d["host_load_server"],
+           f"{p}_host_load_loadgen": d["host_load_loadgen"],
+           f"{p}_cpus": d["cpus"], f"{p}_loadgen_cpus": d["loadgen_cpus"], f"{p}_connections": d["connections"],
+           f"{p}_loadgen_busy_poll_us": d["loadgen_busy_poll_us"]}
+    if full:
+        out.update({
+            f"{p}_args": d["args"],
             # the image binds 0.0.0.0, as a pod on an IPv4 pod network: the client connects over
             # IPv4 loopback, where the headline uses ::1 (2.6 % apart, profiles/round1/r20_v6), which
             # is the in-bench gap between the two (profiles/round5/03_deployed_ab)
-            "deployed_loopback": "127.0.0.1",
+            f"{p}_loopback": "127.0.0.1",
             # ZIPKIN_SERVER_URL names the cluster's zipkin-query Service, which does not resolve
             # on a bare host: spans are recorded and dropped when the post fails
-            "deployed_env": d["env"], "deployed_zipkin": d["zipkin"]}
+            f"{p}_env": d["env"], f"{p}_zipkin": d["zipkin"]})
+    return out
 
 
 def _c1_keys(c1: dict | None) -> dict:

@@ -21,6 +21,8 @@
 #   chain              two-hop chaining bench (loadgen -> hola A -> hola B)
 #   deployedab REPS [ARGS]  headline replica vs as-deployed (ZIPKIN_SERVER_URL as deployed /
 #                      unset / native sink), interleaved (bench/deployed_ab.py)
+#   podshape [REPS] [ARGS]  the shipped pod shape's CPU per request, one thing varied at a time
+#                      (bench/pod_shape.py), then the default bench
 #   chainmodes REPS [ARGS]  bench.py's chain sub-run REPS times per variant with its attribution
 #                      (bench/chain_modes.py; ARGS e.g. --variants lg0,lg20 --seconds 10)
 #   chainab [REPS]     chaining with Feign BASIC logging on/off, this server vs. PREV_BIN
@@ -189,6 +191,14 @@ chain)
 deployedab)
   REPS=${1:-4}; shift || true
   timeout -k 10 1000 python -u bench/deployed_ab.py --reps "$REPS" --out "$OUT" "$@" > "$OUT/deployed_ab.log" 2>&1
+  ;;
+podshape)
+  # the pod shape (2 CPUs) vs 8 CPUs, one thing varied at a time, then the
+  # default bench (its deployed_pod_* sub-run carries the same attribution)
+  REPS=${1:-2}; shift || true
+  info
+  timeout -k 10 900 python -u bench/pod_shape.py --reps "$REPS" --out "$OUT" "$@" > "$OUT/pod_shape.log" 2>&1 &&
+  timeout -k 10 420 python bench.py > "$OUT/bench_default.json" 2>> "$OUT/err.log"
   ;;
 chainmodes)
   REPS=${1:-10}; shift || true

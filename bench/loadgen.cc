@@ -144,6 +144,19 @@ struct ThreadState {
   std::mutex hist_mu;
   uint64_t completed = 0, errors = 0, non2xx = 0, reconnects = 0, bytes = 0;
   uint64_t body_checked = 0, body_mismatch = 0, body_alt = 0;
+  // Where the thread's time goes (since the last reset; read between runs): polls that found
+  // work at once / after spinning / spins that ran out, waits that could block, CPU spent in
+  // empty polls, gaps between polls (event handling + descheduling) past 100 us / 1 ms /
+  // 10 ms and the longest, and (open loop) the latest a scheduled send went out.
+  uint64_t poll_hits = 0, spin_hits = 0, spin_misses = 0, blocking_waits = 0, idle_spin_ns = 0;
+  uint64_t gaps_over[3] = {}, gap_max_ns = 0, send_late_max_ns = 0;
+  void note_gap(int64_t ns) {
+    if (ns <= 100000) return;
+    gaps_over[0] += 1;
+    gaps_over[1] += ns > 1000000;
+    gaps_over[2] += ns > 10000000;
+    if (uint64_t(ns) > gap_max_ns) gap_max_ns = uint64_t(ns);
+  }
   std::vector<std::string> expected;  // per target: the body every response must carry
   std::vector<bool> have_expected;
   std::atomic<int64_t> run_quota{0};  // control: batches per connection for the next run
@@ -464,6 +477,7 @@ void thread_main(ThreadState* ts, const Options* o) {
     for (auto& c : ts->conns) {
       if (c->busy) continue;
       if (c->next_due <= now) {
+        if (uint64_t(now - c->next_due) > ts->send_late_max_ns) ts->send_late_max_ns = uint64_t(now - c->next_due);
         c->intended = c->next_due;
         c->next_due += interval;
         if (!send_req(c.get(), o->pipeline)) ++ts->errors;
@@ -475,15 +489,29 @@ void thread_main(ThreadState* ts, const Options* o) {
   };
 
   epoll_event evs[256];
+  int64_t pass_at = mono_ns();  // when the last pass's events began to be handled
   while (!g_stop.load(std::memory_order_relaxed)) {
     int n = 0;
     if (o->busy_poll_us > 0) {
-      int64_t until = mono_ns() + int64_t(o->busy_poll_us) * 1000;
+      const int64_t spin0 = mono_ns(), until = spin0 + int64_t(o->busy_poll_us) * 1000;
+      ts->note_gap(spin0 - pass_at);
+      int64_t t = spin0;
+      bool spun = false;
       for (;;) {
         n = epoll_wait(ts->epfd, evs, 256, 0);
-        if (n != 0 || mono_ns() >= until) break;
+        if (n != 0) break;
+        spun = true;
+        const int64_t prev = t;
+        t = mono_ns();
+        ts->note_gap(t - prev);  // descheduled while spinning
+        if (t >= until) break;
         for (int k = 0; k < o->busy_poll_pause; ++k) __builtin_ia32_pause();
       }
+      if (spun) ts->idle_spin_ns += uint64_t(t - spin0);
+      if (n > 0) ++(spun ? ts->spin_hits : ts->poll_hits);
+      else ++ts->spin_misses;
+    } else {
+      ts->note_gap(mono_ns() - pass_at);
     }
     if (n == 0) {
       if (rate_mode) {
@@ -497,18 +525,24 @@ void thread_main(ThreadState* ts, const Options* o) {
           if (wait > 5000000) wait = 5000000;
           timespec tmo{0, long(wait)};
           n = epoll_pwait2(ts->epfd, evs, 256, &tmo, nullptr);
+          ++ts->blocking_waits;
         }
       } else {
         n = epoll_wait(ts->epfd, evs, 256, control ? -1 : 5);
+        ++ts->blocking_waits;
       }
     }
     int64_t now = mono_ns();
+    pass_at = now;
     if (!control) {
       if (!ts->recording && now >= warm_end) {
         std::lock_guard<std::mutex> g(ts->hist_mu);
         ts->hist.reset();
         ts->completed = 0;
         ts->recording = true;
+        // the time accounting covers the measured part too
+        ts->poll_hits = ts->spin_hits = ts->spin_misses = ts->blocking_waits = ts->idle_spin_ns = 0;
+        ts->gaps_over[0] = ts->gaps_over[1] = ts->gaps_over[2] = ts->gap_max_ns = ts->send_late_max_ns = 0;
       }
       if (now >= end) break;
     }
@@ -687,6 +721,8 @@ bool parse_targets(const std::string& s, std::vector<Target>* out) {
 std::string stats_json(std::vector<std::unique_ptr<ThreadState>>& ts, bool with_hist) {
   Histogram h;
   uint64_t errors = 0, non2xx = 0, reconnects = 0, checked = 0, mismatch = 0, alt = 0;
+  uint64_t poll_hits = 0, spin_hits = 0, spin_misses = 0, sleeps = 0, idle_ns = 0, gmax = 0, late = 0;
+  uint64_t over[3] = {};
   for (auto& t : ts) {
     std::lock_guard<std::mutex> g(t->hist_mu);
     h.merge(t->hist);
@@ -696,6 +732,14 @@ std::string stats_json(std::vector<std::unique_ptr<ThreadState>>& ts, bool with_
     checked += t->body_checked;
     mismatch += t->body_mismatch;
     alt += t->body_alt;
+    poll_hits += t->poll_hits;
+    spin_hits += t->spin_hits;
+    spin_misses += t->spin_misses;
+    sleeps += t->blocking_waits;
+    idle_ns += t->idle_spin_ns;
+    gmax = std::max(gmax, t->gap_max_ns);
+    late = std::max(late, t->send_late_max_ns);
+    for (int k = 0; k < 3; ++k) over[k] += t->gaps_over[k];
   }
   char buf[704];
   snprintf(buf, sizeof buf,
@@ -708,6 +752,15 @@ std::string stats_json(std::vector<std::unique_ptr<ThreadState>>& ts, bool with_
            (unsigned long long)non2xx, (unsigned long long)reconnects, (unsigned long long)checked,
            (unsigned long long)mismatch, (unsigned long long)alt);
   std::string s = buf;
+  snprintf(buf, sizeof buf,
+           ",\"poll_hits\":%llu,\"spin_hits\":%llu,\"spin_misses\":%llu,\"blocking_waits\":%llu,"
+           "\"idle_spin_ns\":%llu,\"gaps_over_100us\":%llu,\"gaps_over_1ms\":%llu,\"gaps_over_10ms\":%llu,"
+           "\"gap_max_ns\":%llu,\"send_late_max_ns\":%llu",
+           (unsigned long long)poll_hits, (unsigned long long)spin_hits, (unsigned long long)spin_misses,
+           (unsigned long long)sleeps, (unsigned long long)idle_ns, (unsigned long long)over[0],
+           (unsigned long long)over[1], (unsigned long long)over[2], (unsigned long long)gmax,
+           (unsigned long long)late);
+  s += buf;
   if (with_hist) s += ",\"hist\":\"" + h.encode() + "\"";
   return s + "}";
 }
@@ -1033,6 +1086,8 @@ int main(int argc, char** argv) {
         std::lock_guard<std::mutex> g(t->hist_mu);
         t->hist.reset();
         t->errors = t->non2xx = t->reconnects = t->body_checked = t->body_mismatch = t->body_alt = 0;
+        t->poll_hits = t->spin_hits = t->spin_misses = t->blocking_waits = t->idle_spin_ns = 0;
+        t->gaps_over[0] = t->gaps_over[1] = t->gaps_over[2] = t->gap_max_ns = t->send_late_max_ns = 0;
       }
       printf("{\"reset\":true}\n");
       fflush(stdout);

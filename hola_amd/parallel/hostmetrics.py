@@ -136,29 +136,88 @@ def proc_cpu_s(pid: int) -> float:
         return 0.0
 
 
-def cpu_times() -> dict[int, tuple[int, int]]:
-    """Per-CPU (total, idle+iowait) jiffies from /proc/stat, host-wide (other tenants included)."""
+def cpu_times() -> dict[int, tuple[int, int, int, int]]:
+    """Per-CPU (total, idle+iowait, irq+softirq, steal) jiffies from /proc/stat, host-wide
+    (other tenants included). The guest columns are already inside user/nice, so they are
+    left out of the total."""
     out = {}
     try:
         with open("/proc/stat") as f:
             for line in f:
                 if line.startswith("cpu") and line[3].isdigit():
                     parts = line.split()
-                    v = list(map(int, parts[1:]))
-                    out[int(parts[0][3:])] = (sum(v), v[3] + v[4])
+                    v = list(map(int, parts[1:9]))  # user nice system idle iowait irq softirq steal
+                    v += [0] * (8 - len(v))
+                    out[int(parts[0][3:])] = (sum(v), v[3] + v[4], v[5] + v[6], v[7])
     except (OSError, ValueError, IndexError):
         pass
     return out
 
 
-def busy_fraction(t0: dict, t1: dict, cpus) -> float | None:
-    """Busy share of `cpus` between two cpu_times() snapshots (None when unknown)."""
-    tot = idle = 0
+def _share(t0: dict, t1: dict, cpus, col: int) -> float | None:
+    tot = part = 0
     for c in cpus:
         if c in t0 and c in t1:
             tot += t1[c][0] - t0[c][0]
-            idle += t1[c][1] - t0[c][1]
-    return round(1.0 - idle / tot, 4) if tot > 0 else None
+            part += t1[c][col] - t0[c][col]
+    return round(part / tot, 4) if tot > 0 else None
+
+
+def busy_fraction(t0: dict, t1: dict, cpus) -> float | None:
+    """Busy share of `cpus` between two cpu_times() snapshots (None when unknown)."""
+    idle = _share(t0, t1, cpus, 1)
+    return None if idle is None else round(1.0 - idle, 4)
+
+
+def irq_fraction(t0: dict, t1: dict, cpus) -> float | None:
+    """Share of `cpus`' time in hard and soft interrupt context (on loopback: the receive path
+    of segments this job sent, when the kernel defers it to softirq, and other devices' IRQs)."""
+    return _share(t0, t1, cpus, 2)
+
+
+def steal_fraction(t0: dict, t1: dict, cpus) -> float | None:
+    """Share of `cpus`' time a hypervisor ran something else (0 on bare metal)."""
+    return _share(t0, t1, cpus, 3)
+
+
+def task_stats(pid: int) -> dict[str, dict]:
+    """Per thread of `pid` (by comm): CPU seconds and voluntary / involuntary context switches
+    (a thread that sleeps in epoll_wait and is woken switches voluntarily; one preempted by
+    another runnable task, involuntarily). Threads of one name are summed."""
+    out: dict[str, dict] = {}
+    tck = os.sysconf("SC_CLK_TCK")
+    for task in Path(f"/proc/{pid}/task").glob("*"):
+        try:
+            comm = (task / "comm").read_text().strip()
+            fields = (task / "stat").read_text().rsplit(")", 1)[1].split()
+            vol = invol = 0
+            for ln in (task / "status").read_text().splitlines():
+                if ln.startswith("voluntary_ctxt_switches:"):
+                    vol = int(ln.split()[1])
+                elif ln.startswith("nonvoluntary_ctxt_switches:"):
+                    invol = int(ln.split()[1])
+        except (OSError, IndexError, ValueError):
+            continue
+        d = out.setdefault(comm, {"cpu_s": 0.0, "vol": 0, "invol": 0, "threads": 0})
+        d["cpu_s"] += (int(fields[11]) + int(fields[12])) / tck
+        d["vol"] += vol
+        d["invol"] += invol
+        d["threads"] += 1
+    return out
+
+
+def task_stats_delta(a: dict, b: dict, group=lambda comm: "workers" if comm.startswith(("hola-w", "hola-lg"))
+                     else "other") -> dict:
+    """task_stats(b) - task_stats(a), summed into groups (default: the serving threads, hola-w*
+    or hola-lg*, and every other thread of the process)."""
+    out: dict[str, dict] = {}
+    for comm, d1 in b.items():
+        d0 = a.get(comm, {"cpu_s": 0.0, "vol": 0, "invol": 0})
+        g = out.setdefault(group(comm), {"cpu_s": 0.0, "vol": 0, "invol": 0})
+        g["cpu_s"] = round(g["cpu_s"] + d1["cpu_s"] - d0["cpu_s"], 3)
+        g["vol"] += d1["vol"] - d0["vol"]
+        g["invol"] += d1["invol"] - d0["invol"]
+    return out
 
 
 def cgroup_cpu_stat() -> dict[str, int]:

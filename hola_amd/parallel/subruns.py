@@ -28,7 +28,8 @@ import subprocess
 import time
 from pathlib import Path
 
-from hola_amd.parallel.hostmetrics import MetricsProbe, busy_fraction, cgroup_cpu_stat, cpu_times, proc_cpu_s
+from hola_amd.parallel.hostmetrics import (MetricsProbe, busy_fraction, cgroup_cpu_stat, cpu_times, irq_fraction,
+                                           proc_cpu_s, steal_fraction)
 from hola_amd.parallel.loadgen import ControlledLoadgen
 from hola_amd.server import HolaProcess
 from hola_amd.utils import cpu as _cpu
@@ -47,9 +48,25 @@ def other_siblings(own, job_cpus) -> set[int]:
     return {x for c in own for x in _cpu.siblings(c)} - job
 
 
+def l3_neighbours(own, job_cpus) -> set[int]:
+    """CPUs that share an L3 with `own`, outside the job and not SMT siblings of `own` (those
+    are reported apart): busy ones are other tenants filling the cache the job works in."""
+    doms = {_cpu.l3_domain(c) for c in own} - {None, -1}
+    if not doms:
+        return set()
+    sib = {x for c in own for x in _cpu.siblings(c)}
+    return {c for c in _cpu.online_cpus() if _cpu.l3_domain(c) in doms} - set(job_cpus) - set(own) - sib
+
+
 def host_load(t0: dict, t1: dict, own, job_cpus) -> dict:
-    """Busy share of `own` and of the SMT siblings of `own` that belong to no part of the job."""
-    return {"own": busy_fraction(t0, t1, set(own)), "siblings": busy_fraction(t0, t1, other_siblings(own, job_cpus))}
+    """Busy share of `own`, of the SMT siblings of `own` that belong to no part of the job and
+    of the other CPUs of `own`'s L3 domains (`l3_others`), plus the interrupt (hard + soft) and
+    steal shares of `own` (a slow run on quiet siblings can then be told
+    apart from one that lost time to IRQs, a hypervisor or a busy L3 neighbour)."""
+    own = set(own)
+    return {"own": busy_fraction(t0, t1, own), "siblings": busy_fraction(t0, t1, other_siblings(own, job_cpus)),
+            "l3_others": busy_fraction(t0, t1, l3_neighbours(own, job_cpus)),
+            "irq_own": irq_fraction(t0, t1, own), "steal_own": steal_fraction(t0, t1, own)}
 
 
 def metrics_counters(port: int, host: str = "127.0.0.1", probe: MetricsProbe | None = None) -> dict:
@@ -89,6 +106,14 @@ def metrics_counters(port: int, host: str = "127.0.0.1", probe: MetricsProbe | N
             out["circuit." + (f"{to}_{by}" if by else to)] = float(val)
         elif name == "hola_http_requests_total":
             out["requests"] = float(val)
+        elif name == "hola_loop_idle_spin_seconds_total":
+            out["loop.idle_spin_s"] = float(val)
+        elif name == "hola_loop_blocking_waits_total":
+            out["loop.blocking_waits"] = float(val)
+        elif name.startswith("hola_loop_poll_gaps_total{"):
+            out["loop.gaps_over_" + name.split('"')[1]] = float(val)
+        elif name == "hola_loop_poll_gap_max_seconds":
+            out["gauge.gap_max_s"] = float(val)
     return out
 
 
@@ -232,6 +257,78 @@ def timed_closed_loop(lg: ControlledLoadgen, connections: int, seconds: float, p
             "host_load": host_load(t0, t1, own, job_cpus)}
 
 
+def loop_block(m0: dict, m1: dict, reqs: float) -> dict:
+    """A replica's event-loop accounting between two metrics_counters() scrapes: CPU in empty
+    polls, waits that could sleep (per request), gaps between polls past 100 us / 1 ms / 10 ms
+    and the longest gap since the replica started, adaptive spin outcomes."""
+    d = counter_delta(m0, m1, "loop.")
+    return {"idle_spin_s": round(m1.get("loop.idle_spin_s", 0.0) - m0.get("loop.idle_spin_s", 0.0), 4),
+            "blocking_waits_per_req": round(d.get("blocking_waits", 0) / max(1.0, reqs), 4),
+            "gaps_over_100us": d.get("gaps_over_100us", 0), "gaps_over_1ms": d.get("gaps_over_1ms", 0),
+            "gaps_over_10ms": d.get("gaps_over_10ms", 0),
+            "gap_max_since_start_us": round(1e6 * m1.get("gauge.gap_max_s", 0.0), 1),
+            "spins": counter_delta(m0, m1, "spins.")}
+
+
+def loadgen_block(st: dict, cpu_s: float, reqs: float) -> dict:
+    """The load generator's side of a run from its stats (since its last reset): CPU and busy
+    CPU (minus empty polls) per request, how its polls ended (found work at once, after
+    spinning, or ran out and slept), and its own scheduling gaps."""
+    idle = st.get("idle_spin_ns", 0) / 1e9
+    n = max(1.0, reqs)
+    return {"cpu_us_per_req": round(1e6 * cpu_s / n, 3), "busy_cpu_us_per_req": round(1e6 * (cpu_s - idle) / n, 3),
+            "idle_spin_s": round(idle, 4),
+            "polls": {"hit_at_once": st.get("poll_hits", 0), "hit_after_spin": st.get("spin_hits", 0),
+                      "ran_out": st.get("spin_misses", 0)},
+            "blocking_waits_per_req": round(st.get("blocking_waits", 0) / n, 4),
+            "gaps_over_100us": st.get("gaps_over_100us", 0), "gaps_over_1ms": st.get("gaps_over_1ms", 0),
+            "gaps_over_10ms": st.get("gaps_over_10ms", 0), "gap_max_us": round(st.get("gap_max_ns", 0) / 1e3, 1),
+            "send_late_max_us": round(st.get("send_late_max_ns", 0) / 1e3, 1)}
+
+
+def attributed_closed_loop(lg: ControlledLoadgen, seconds: float, pid: int, port: int, server_cpus, load_cpus,
+                           job_cpus, host: str = "127.0.0.1", warm_s: float = 1.0) -> dict:
+    """timed_closed_loop() with the attribution a replica's CPU per request needs (VERDICT r5
+    weak #1, #4): busy CPU per request (process CPU minus the loop's empty polls), the serving
+    threads' CPU and context switches apart from the process's other threads, the loop's
+    waits and gaps, the load generator's own CPU and poll outcomes, TCP segments per request,
+    and the host load of the server's and the load generator's CPUs separately."""
+    from hola_amd.parallel.hostmetrics import task_stats, task_stats_delta, tcp_counters
+
+    probe = MetricsProbe(host, port)
+    try:
+        m0, ts0, tcp0, lg0 = metrics_counters(port, host, probe), task_stats(pid), tcp_counters(), proc_cpu_s(lg.proc.pid)
+        t0, w0 = cpu_times(), time.perf_counter()
+        r = timed_closed_loop(lg, 0, seconds, pid, list(server_cpus) + list(load_cpus), job_cpus, warm_s=warm_s)
+        t1, wall = cpu_times(), time.perf_counter() - w0
+        m1, ts1, tcp1, lg1 = metrics_counters(port, host, probe), task_stats(pid), tcp_counters(), proc_cpu_s(lg.proc.pid)
+        st = lg.stats()
+    finally:
+        probe.close()
+    el = r["elapsed_s"]
+    # every sample spans the warm-up too, at the same load: per request of the whole run
+    reqs = r["requests"] * (el + warm_s) / max(1e-9, el)
+    threads = task_stats_delta(ts0, ts1)
+    cpu = sum(g["cpu_s"] for g in threads.values())
+    loop = loop_block(m0, m1, reqs)
+    hl_server = host_load(t0, t1, server_cpus, job_cpus)
+    r.update({
+        "server_busy_cpu_us_per_req": round(1e6 * (cpu - loop["idle_spin_s"]) / max(1.0, reqs), 3),
+        # everything the server's CPUs did per request, whoever it is charged to: the
+        # replica's threads, and interrupt time there (on loopback the receive path of the
+        # segments the replica sent, when the kernel runs it as a softirq)
+        "server_cpus_us_per_req": (round(1e6 * hl_server["own"] * len(set(server_cpus)) * wall / max(1.0, reqs * wall / (el + warm_s)), 3)
+                                   if hl_server["own"] is not None else None),
+        "server_threads": {k: {**v, "vol_per_req": round(v["vol"] / max(1.0, reqs), 4),
+                               "invol_per_req": round(v["invol"] / max(1.0, reqs), 4)} for k, v in threads.items()},
+        "server_loop": loop,
+        "loadgen": loadgen_block(st, lg1 - lg0, reqs),
+        "tcp_per_req": {k: round((tcp1[k] - tcp0[k]) / max(1.0, reqs), 3) for k in tcp1 if k in tcp0},
+        "host_load_server": hl_server,
+        "host_load_loadgen": host_load(t0, t1, load_cpus, job_cpus)})
+    return r
+
+
 def config2(a, host: str, port: int, server_cpus, load_cpus, bodies, job_cpus) -> dict | None:
     """BASELINE config 2: one keep-alive connection against this rank's replica."""
     if a.c1_reqs <= 0 and a.c1_seconds <= 0:
@@ -263,12 +360,18 @@ def config2(a, host: str, port: int, server_cpus, load_cpus, bodies, job_cpus) -
 ZIPKIN_VARIANTS = ("deployed", "unset", "sink")
 
 
-def deployed(a, server_cpus, load_cpus, job_cpus, zipkin: str = "deployed", seconds: float | None = None) -> dict:
+def deployed(a, server_cpus, load_cpus, job_cpus, zipkin: str = "deployed", seconds: float | None = None,
+             loadgen_busy_poll: int | None = None, connections: int | None = None, threads: int | None = None,
+             cpu_profile: str | None = None) -> dict:
     """The replica as deployed, driven by the headline's load generator for about
-    --deployed-seconds. `zipkin`: "deployed" = the manifests' ZIPKIN_SERVER_URL (the cluster's
-    zipkin-query Service, which does not resolve on a bare host: spans are recorded and then
-    dropped when the post fails), "unset" = no collector (spans dropped at the source, the
-    headline's path), "sink" = a native discard collector that accepts every post."""
+    --deployed-seconds, with attributed_closed_loop()'s accounting. `zipkin`: "deployed" = the
+    manifests' ZIPKIN_SERVER_URL (the cluster's zipkin-query Service, which does not resolve on
+    a bare host: spans are recorded and then dropped when the post fails), "unset" = no
+    collector (spans dropped at the source, the headline's path), "sink" = a native discard
+    collector that accepts every post. The other keywords vary one thing for the pod-shape
+    study (bench/pod_shape.py): the load generator's busy-poll window (default: the
+    headline's), the connections, the replica's --threads (default: as deployed, one worker
+    per CPU of its cpuset), and a --cpu-profile of the replica."""
     from hola_amd.parallel.hostmetrics import start_zipkin_sink
 
     sink = None
@@ -278,19 +381,25 @@ def deployed(a, server_cpus, load_cpus, job_cpus, zipkin: str = "deployed", seco
     elif zipkin == "sink":
         sink = start_zipkin_sink()
         env_over["ZIPKIN_SERVER_URL"] = f"http://127.0.0.1:{sink[1]}"
+    extra = (["--threads", str(threads)] if threads else []) + (["--cpu-profile", cpu_profile] if cpu_profile else [])
+    lg_bp = a.busy_poll_us if loadgen_busy_poll is None else loadgen_busy_poll
+    conns = connections or a.connections
     try:
-        with DeployedProc(server_cpus, "hola-1-deplo", env_over=env_over) as d:
+        with DeployedProc(server_cpus, "hola-1-deplo", extra_args=extra, env_over=env_over) as d:
             body = ["Hola de hola-1-deplo"] if a.path == "/api/hola" else None
-            lg = ControlledLoadgen([("127.0.0.1", d.port)], a.connections, len(load_cpus),
-                                   cpu_list=",".join(map(str, load_cpus)), path=a.path, busy_poll_us=a.busy_poll_us,
-                                   busy_poll_pause=a.busy_poll_pause, epoll_lt=a.epoll_lt,
+            lg = ControlledLoadgen([("127.0.0.1", d.port)], conns, len(load_cpus),
+                                   cpu_list=",".join(map(str, load_cpus)), path=a.path, busy_poll_us=lg_bp,
+                                   busy_poll_pause=a.busy_poll_pause if lg_bp else 0, epoll_lt=a.epoll_lt,
                                    expect_bodies=body, verify_body=body is None)
             try:
-                r = timed_closed_loop(lg, a.connections, seconds or a.deployed_seconds, d.proc.pid,
-                                      list(server_cpus) + list(load_cpus), job_cpus)
+                r = attributed_closed_loop(lg, seconds or a.deployed_seconds, d.proc.pid, d.port, server_cpus,
+                                           load_cpus, job_cpus)
             finally:
                 lg.close()
-            r.update({"args": " ".join(d.shown_args().split()[:-2]), "cpus": format_cpu_list(server_cpus),
+            shown = d.shown_args().split()
+            r.update({"args": " ".join(shown[:len(shown) - 2 - len(extra)]), "cpus": format_cpu_list(server_cpus),
+                      "loadgen_cpus": format_cpu_list(load_cpus), "connections": conns,
+                      "loadgen_busy_poll_us": lg_bp, "threads": threads or len(server_cpus),
                       "env": d.shown_env(set(d.env) - {"PATH", "LANG", "LD_LIBRARY_PATH"}), "zipkin": zipkin})
             return r
     finally:
@@ -414,3 +523,53 @@ def alt_layout(a, host: str, server_cpus, load_cpus, smt: str, job_cpus, bodies,
     r.update({"smt": alt, "server_cpus": format_cpu_list(sv), "loadgen_cpus": format_cpu_list(ld),
               "physical_cores": phys_n, "rps_per_physical_core": r["rps"] / max(1, phys_n)})
     return r
+
+
+def v4_headline(a, server_args: list[str], server_cpus, load_cpus, conn_targets, job_cpus, bodies,
+                seconds: float) -> dict:
+    """The headline replica and load generator again, unchanged but for the address family:
+    IPv4 loopback, the transport of the image (it binds 0.0.0.0, deploy/Dockerfile) where the
+    headline runs on ::1 (VERDICT r5 weak #6). Same CPUs, arguments, connection layout and
+    busy-polling; one continuous run (`runfor`) with its warm-up."""
+    args = []
+    skip = False
+    for x in server_args:  # drop the headline's --host (HolaProcess binds 127.0.0.1)
+        if skip:
+            skip = False
+            continue
+        if x == "--host":
+            skip = True
+            continue
+        args.append(x)
+    with HolaProcess(args=args, env={"HOSTNAME": "replica-0"}, threads=len(server_cpus),
+                     cpu_list=format_cpu_list(server_cpus), log_level="warn") as s:
+        lg = ControlledLoadgen([("127.0.0.1", s.port)], a.connections, len(load_cpus),
+                               cpu_list=",".join(map(str, load_cpus)), path=a.path, busy_poll_us=a.busy_poll_us,
+                               busy_poll_pause=a.busy_poll_pause, epoll_lt=a.epoll_lt, pipeline=a.pipeline,
+                               expect_bodies=bodies, verify_body=bodies is None, conn_targets=conn_targets)
+        try:
+            r = timed_closed_loop(lg, a.connections, seconds, s.proc.pid, list(server_cpus) + list(load_cpus), job_cpus)
+        finally:
+            lg.close()
+    return r
+
+
+def plain_dealing_run(a, targets: list[tuple[str, int]], local_rank: int, load_cpus, bodies, seconds: float) -> dict:
+    """One rank's share of the topology-blind front: this rank's load
+    generator on its own cores deals its connections (i + rank) % N over every replica of the
+    node, as a LoadBalancer Service (pom.xml:77-80) would without placing any client. Every
+    rank runs it at once (the caller brackets it with barriers); returns the rank's counts and
+    its latency histogram for merging."""
+    lg = ControlledLoadgen(targets, a.connections, len(load_cpus), cpu_list=",".join(map(str, load_cpus)),
+                           path=a.path, target_offset=local_rank, busy_poll_us=a.busy_poll_us,
+                           busy_poll_pause=a.busy_poll_pause, epoll_lt=a.epoll_lt, pipeline=a.pipeline,
+                           expect_bodies=bodies, verify_body=bodies is None)
+    try:
+        lg.reset()
+        r = lg.run_for(seconds, 1.0)
+        st = lg.stats()
+    finally:
+        lg.close()
+    return {"requests": r["requests"], "errors": r["errors"], "elapsed_s": r["elapsed_ns"] / 1e9,
+            "hist": st.get("hist", ""), "non2xx": st.get("non2xx", 0), "body_checked": st.get("body_checked", 0),
+            "body_mismatch": st.get("body_mismatch", 0), "load_cpus": format_cpu_list(load_cpus)}

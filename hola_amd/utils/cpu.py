@@ -118,6 +118,12 @@ def package_of(cpu: int) -> int:
         return 0
 
 
+def online_cpus() -> list[int]:
+    """Every online CPU of the host (not only this process's affinity mask)."""
+    v = _read("/sys/devices/system/cpu/online")
+    return parse_cpu_list(v) if v else allowed_cpus()
+
+
 def siblings(cpu: int) -> list[int]:
     v = _read(f"/sys/devices/system/cpu/cpu{cpu}/topology/thread_siblings_list")
     return parse_cpu_list(v) if v else [cpu]

@@ -181,10 +181,18 @@ void EventLoop::note_off_wait(bool would_hit) {
   off_hits_ = off_waits_ = 0;
 }
 
+void EventLoop::note_gap(int64_t ns) {
+  if (ns <= kGapNs[0]) return;
+  for (int i = 0; i < kGapBuckets; ++i)
+    if (ns > kGapNs[i]) gaps_over_[i].store(gaps_over_[i].load(std::memory_order_relaxed) + 1, std::memory_order_relaxed);
+  if (uint64_t(ns) > gap_max_ns_.load(std::memory_order_relaxed)) gap_max_ns_.store(uint64_t(ns), std::memory_order_relaxed);
+}
+
 void EventLoop::run() {
   constexpr int kMaxEvents = 256;
   epoll_event evs[kMaxEvents];
   t_loop_now_ms = &now_ms_;  // LoopClock on this thread reads the pass's time
+  pass_end_ns_ = mono_ns();
   uint64_t passes = 0;
   while (!stop_.load(std::memory_order_relaxed)) {
     act_.passes.store(++passes, std::memory_order_relaxed);
@@ -194,28 +202,41 @@ void EventLoop::run() {
     int n = 0;
     int wait_errno = 0;  // errno of a failed epoll_wait, taken before the clock reads below
     int64_t t = 0;  // mono_ns() at (or just before) the moment events were found
+    bool polled = false;  // a spin ran: the gap to the last pass is taken
     if (busy_poll_ns_ > 0 && (!busy_auto_ || now_ms_ >= spin_off_until_ms_)) {
       t = mono_ns();
-      const int64_t until = t + busy_poll_ns_;
+      note_gap(t - pass_end_ns_);
+      polled = true;
+      const int64_t spin0 = t, until = t + busy_poll_ns_;
       bool spun = false;  // the first poll came back empty: this pass is a real spin
       for (;;) {
         n = epoll_wait(epfd_, evs, kMaxEvents, 0);
         if (n < 0) wait_errno = errno;
         if (n != 0 || stop_.load(std::memory_order_relaxed)) break;
         spun = true;
+        const int64_t prev = t;
         t = mono_ns();
+        if (t - prev > kGapNs[0]) note_gap(t - prev);  // descheduled while spinning
         if (t >= until) break;
         for (int i = 0; i < busy_poll_pause_; ++i) __builtin_ia32_pause();
       }
+      // CPU time of the polls that found nothing (up to the end of the last empty one): the
+      // part of a spinning loop's CPU that did no work (the /metrics busy-CPU figure)
+      if (spun) idle_spin_ns_.store(idle_spin_ns_.load(std::memory_order_relaxed) + uint64_t(t - spin0),
+                                    std::memory_order_relaxed);
       if (busy_auto_ && spun) note_spin(n > 0);
     }
     if (n == 0) {
       // backed off from spinning: time the blocking wait (would a spin have found this event?)
       const bool off = busy_auto_ && busy_poll_ns_ > 0 && now_ms_ < spin_off_until_ms_;
-      const int64_t w0 = off ? mono_ns() : 0;
-      n = epoll_wait(epfd_, evs, kMaxEvents, next_timeout_ms());
+      const int64_t w0 = polled ? t : mono_ns();
+      if (!polled) note_gap(w0 - pass_end_ns_);
+      const int timeout = next_timeout_ms();
+      n = epoll_wait(epfd_, evs, kMaxEvents, timeout);
       if (n < 0) wait_errno = errno;
       t = mono_ns();
+      if (timeout != 0) blocking_waits_.store(blocking_waits_.load(std::memory_order_relaxed) + 1,
+                                              std::memory_order_relaxed);
       if (off && n > 0) note_off_wait(t - w0 <= 2 * busy_poll_ns_);
     }
     if (n < 0 && wait_errno != EINTR) {
@@ -254,6 +275,7 @@ void EventLoop::run() {
       for (Handler* h : retired_) delete h;
       retired_.clear();
     }
+    pass_end_ns_ = t;  // the next pass's first poll measures its gap from here
   }
   t_loop_now_ms = nullptr;
   set_phase(kPosted);

@@ -84,6 +84,20 @@ class EventLoop {
   uint64_t spin_offs() const { return spin_offs_.load(std::memory_order_relaxed); }
   uint64_t spin_off_ms() const { return spin_off_ms_.load(std::memory_order_relaxed); }
   uint64_t spin_resumes() const { return spin_resumes_.load(std::memory_order_relaxed); }
+  // Where a loop's time goes (loop thread writes, any thread reads; every mode, not only
+  // adaptive): nanoseconds of polls that came back empty while spinning (CPU that did no
+  // work: process CPU minus this is the loop's busy CPU), and epoll waits that could block.
+  uint64_t idle_spin_ns() const { return idle_spin_ns_.load(std::memory_order_relaxed); }
+  uint64_t blocking_waits() const { return blocking_waits_.load(std::memory_order_relaxed); }
+  // Gaps between polls: from the end of one pass's poll to the next poll (the pass's own
+  // handlers, and any time the thread was descheduled then), and between two empty polls of a
+  // spin (descheduled while spinning). Counted when longer than 100 us / 1 ms / 10 ms, and the
+  // longest since start: a latency outlier on this loop's connections that matches none of
+  // these was not made here (a tail attribution).
+  static constexpr int kGapBuckets = 3;
+  static constexpr int64_t kGapNs[kGapBuckets] = {100000, 1000000, 10000000};
+  uint64_t gaps_over(int i) const { return gaps_over_[i].load(std::memory_order_relaxed); }
+  uint64_t gap_max_ns() const { return gap_max_ns_.load(std::memory_order_relaxed); }
 
   // What the loop thread is doing, published with relaxed stores as it goes, so another
   // thread can say where a loop that stopped answering is: Server::shutdown logs it for a
@@ -150,6 +164,11 @@ class EventLoop {
   uint32_t off_hits_ = 0, off_waits_ = 0;  // blocking waits while spinning is off (current window)
   void note_spin(bool hit);
   void note_off_wait(bool would_hit);
+  void note_gap(int64_t ns);
+  int64_t pass_end_ns_ = 0;  // mono_ns() when the last pass's polling ended
+  // single writer (the loop thread): load + store, no locked read-modify-write
+  std::atomic<uint64_t> idle_spin_ns_{0}, blocking_waits_{0}, gap_max_ns_{0};
+  std::atomic<uint64_t> gaps_over_[kGapBuckets] = {};
   alignas(64) Activity act_;  // own cache line: written by the loop thread only
 };
 

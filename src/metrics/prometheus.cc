@@ -168,6 +168,32 @@ std::string Prometheus::render(http::Server* server) const {
       // back-offs ended early because the blocking waits showed the loop busy
       o += "# TYPE hola_busy_poll_resumes_total counter\nhola_busy_poll_resumes_total " + std::to_string(resumes) + "\n";
     }
+    {
+      // Where the workers' time goes: CPU in polls that found nothing while spinning (process
+      // CPU minus this = the CPU that served), waits that could sleep, and gaps between polls
+      // (handlers + descheduling) past 100 us / 1 ms / 10 ms with the longest one
+      uint64_t idle_ns = 0, sleeps = 0, gmax = 0, over[EventLoop::kGapBuckets] = {};
+      for (size_t i = 0; i < server->num_workers(); ++i) {
+        const EventLoop& l = server->worker(i).loop();
+        idle_ns += l.idle_spin_ns();
+        sleeps += l.blocking_waits();
+        gmax = std::max(gmax, l.gap_max_ns());
+        for (int k = 0; k < EventLoop::kGapBuckets; ++k) over[k] += l.gaps_over(k);
+      }
+      char num[64];
+      snprintf(num, sizeof num, "%.6f", double(idle_ns) / 1e9);
+      o += "# TYPE hola_loop_idle_spin_seconds_total counter\nhola_loop_idle_spin_seconds_total ";
+      o += num;
+      o += "\n# TYPE hola_loop_blocking_waits_total counter\nhola_loop_blocking_waits_total " + std::to_string(sleeps) + "\n";
+      o += "# TYPE hola_loop_poll_gaps_total counter\n";
+      static const char* const kOver[EventLoop::kGapBuckets] = {"100us", "1ms", "10ms"};
+      for (int k = 0; k < EventLoop::kGapBuckets; ++k)
+        o += std::string("hola_loop_poll_gaps_total{over=\"") + kOver[k] + "\"} " + std::to_string(over[k]) + "\n";
+      snprintf(num, sizeof num, "%.6f", double(gmax) / 1e9);
+      o += "# TYPE hola_loop_poll_gap_max_seconds gauge\nhola_loop_poll_gap_max_seconds ";
+      o += num;
+      o += "\n";
+    }
     // 1 from the termination signal on (readiness failing, --shutdown-delay-ms), 2 while draining
     o += "# TYPE hola_server_terminating gauge\nhola_server_terminating " +
          std::to_string(server->draining() ? 2 : server->terminating() ? 1 : 0) + "\n";

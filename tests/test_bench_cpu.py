@@ -12,6 +12,10 @@ KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "
 
 
 def run(cmd, port):
+    # the IPv4 and topology-blind sub-runs (10 s each by default) only where a test asks for them
+    for flag in ("--v4-seconds", "--plain-seconds"):
+        if flag not in cmd:
+            cmd = cmd + [flag, "0"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env={**os.environ, "HOLA_BENCH_PORT": str(port)})
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.strip()]
@@ -48,7 +52,8 @@ def test_bench_auto_steps_and_node_subruns():
     per-hop accept locality, both replicas' busy-poll counters) and the other SMT layout."""
     out = run([sys.executable, str(ROOT / "bench.py"), "--steps", "2", "--warmup", "2", "--warmup-reqs-per-conn",
                "200", "--step-seconds", "0.2", "--c1-seconds", "0", "--deployed-seconds", "0.5",
-               "--chain-seconds", "0.5", "--chain-shipped-seconds", "0.5", "--alt-seconds", "0.5"], 18870)
+               "--chain-seconds", "0.5", "--chain-shipped-seconds", "0.5", "--alt-seconds", "0.5",
+               "--v4-seconds", "0.5"], 18870)
     per = out["config"]["reqs_per_conn_per_step"]
     assert per >= 100 and out["requests"] == 64 * per * 2 and out["errors"] == 0
     assert out["config"]["step_sizing"].startswith("sized from the last warmup step")
@@ -57,7 +62,9 @@ def test_bench_auto_steps_and_node_subruns():
     srv = parse_cpu_list(out["config"]["cpu_map"]["rank0"]["server"])
     assert out["config"]["cores_per_replica"] == len({min(siblings(c)) for c in srv})
     assert out["deployed_errors"] == 0 and out["deployed_body_checked"] == out["deployed_requests"] > 0
-    assert set(out["deployed_host_load"]) == {"own", "siblings"} and out["deployed_zipkin"] == "deployed"
+    hl_keys = {"own", "siblings", "l3_others", "irq_own", "steal_own"}
+    assert set(out["deployed_host_load"]) == hl_keys and out["deployed_zipkin"] == "deployed"
+    assert set(out["host_load"][0]) == hl_keys
     assert out["deployed_loopback"] == "127.0.0.1"  # the image binds 0.0.0.0: IPv4, as a pod
     # every sub-run is one continuous run of its length, its warm-up uncounted
     assert abs(out["deployed_elapsed_s"] - 0.5) < 0.1 and abs(out["chain_elapsed_s"] - 0.5) < 0.1
@@ -65,6 +72,21 @@ def test_bench_auto_steps_and_node_subruns():
     # ... and sized as the manifests size a pod (limits.cpu 2)
     assert len(parse_cpu_list(out["deployed_pod_cpus"])) == 2 and out["deployed_pod_errors"] == 0
     assert out["deployed_pod_rps"] > 0
+    # ... with the attribution of its CPU per request
+    assert 0 < out["deployed_pod_server_busy_cpu_us_per_req"] <= out["deployed_pod_server_cpu_us_per_req"] + 0.05
+    assert set(out["deployed_pod_server_threads"]) <= {"workers", "other"} and "workers" in out["deployed_pod_server_threads"]
+    assert {"blocking_waits_per_req", "gaps_over_100us", "spins"} <= set(out["deployed_pod_server_loop"])
+    assert {"polls", "busy_cpu_us_per_req", "blocking_waits_per_req"} <= set(out["deployed_pod_loadgen"])
+    assert set(out["deployed_pod_host_load_server"]) == hl_keys and out["deployed_pod_connections"] == 64
+    # the headline's independent efficiency figures
+    assert 0 < out["server_busy_cpu_us_per_req"] <= out["server_cpu_us_per_req"]
+    assert 0 < out["loadgen_busy_cpu_us_per_req"] <= out["loadgen_cpu_us_per_req"]
+    assert {"idle_spin_s", "blocking_waits_per_req", "gap_max_since_start_us"} <= set(out["server_loop"])
+    assert {"polls", "gap_max_us"} <= set(out["loadgen_loop"])
+    # the headline again over IPv4 loopback, when the headline ran on ::1
+    if out["config"]["loopback"] != "127.0.0.1":
+        assert out["v4_errors"] == 0 and out["v4_body_checked"] == out["v4_requests"] > 0
+        assert out["v4_vs_value"] > 0
     assert out["chain_errors"] == 0 and out["chain_hystrix_fallback"] == 0 and out["chain_pool"] == 128
     assert set(out["chain_locality"]) == {"loadgen_to_a", "a_to_b"}
     assert abs(sum(out["chain_locality"]["a_to_b"].values()) - 1.0) < 1e-3
@@ -93,8 +115,14 @@ def test_plan_only_replicas():
 def test_bench_two_ranks_gloo():
     out = run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                "--master-addr", "127.0.0.1", "--master-port", "29561", str(ROOT / "bench.py"), "--gpus", "2",
-               "--steps", "2", "--warmup", "1", "--reqs-per-conn", "100", "--c1-reqs", "2000"], 18820)
+               "--steps", "2", "--warmup", "1", "--reqs-per-conn", "100", "--c1-reqs", "2000",
+               "--plain-seconds", "0.5"], 18820)
     assert out["n_gpus"] == 2 and out["requests"] == 2 * 64 * 100 * 2
+    # the topology-blind front after the timed region: every body checked
+    assert out["plain_errors"] == 0 and out["plain_body_checked"] == out["plain_requests"] > 0
+    assert out["plain_body_mismatch"] == 0 and out["plain_rps"] > 0 and len(out["plain_loadgen_cpus"]) == 2
+    assert abs(sum(out["plain_locality"].values()) - 1.0) < 1e-3
+    assert "places no client" in out["config"]["lb"]
     # connections are dealt over both replicas; each body must name the replica behind it
     assert out["body_checked"] == out["requests"] and out["body_mismatch"] == 0 and out["errors"] == 0
     assert out["c1_requests"] == 2000 and out["c1_errors"] == 0

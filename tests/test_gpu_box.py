@@ -22,7 +22,8 @@ def test_native_module_loaded_from_tree(native):
 def test_bench_json_contract_on_host():
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--steps", "3", "--warmup", "1",
                         "--reqs-per-conn", "200", "--c1-seconds", "2", "--deployed-seconds", "2",
-                        "--chain-seconds", "2", "--chain-shipped-seconds", "2", "--alt-seconds", "2"],
+                        "--chain-seconds", "2", "--chain-shipped-seconds", "2", "--alt-seconds", "2",
+                        "--v4-seconds", "2"],
                        capture_output=True, text=True, timeout=600, env={**os.environ, "HOLA_BENCH_PORT": "18700"})
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.strip()]
@@ -45,7 +46,8 @@ def test_bench_json_contract_on_host():
     assert out["config"]["smt"] in ("off", "split", "pair") and "GPU slot" in out["config"]["layout_note"]
     assert abs(sum(out["locality"]["fraction"].values()) - 1.0) < 1e-3
     # config 2 carries its own host load
-    assert set(out["c1_host_load"]) == {"own", "siblings"}
+    hl_keys = {"own", "siblings", "l3_others", "irq_own", "steal_own"}
+    assert set(out["c1_host_load"]) == hl_keys
     # ... and GET /api/hola-chaining through two replicas: every call a Hystrix SUCCESS, no
     # fallback or timeout, every body (three greetings, two hops) checked
     assert out["chain_errors"] == 0 and out["chain_non2xx"] == 0 and out["chain_rps"] > 10000, out
@@ -55,13 +57,18 @@ def test_bench_json_contract_on_host():
     assert out["chain_a_cpu_us_per_req"] > 0
     # ... with what separates its two modes: host load, per-hop accept locality, spin counters
     assert set(out["chain_locality"]) == {"loadgen_to_a", "a_to_b"} and out["chain_spins"]["a"]
-    assert set(out["chain_host_load"]) == {"own", "siblings"} and set(out["deployed_host_load"]) == {"own", "siblings"}
+    assert set(out["chain_host_load"]) == hl_keys and set(out["deployed_host_load"]) == hl_keys
     # ... and as shipped (pool of 10, BASIC logging): every body is the two-hop answer or A's
     # fallback, the fraction is reported
     assert out["chain_shipped_pool"] == 10 and out["chain_shipped_body_mismatch"] == 0
     assert 0.0 <= out["chain_shipped_fallback_fraction"] <= 1.0
     # ... and the other SMT layout on the rank's cores (BENCH <-> SCALE N = 1)
     assert out["alt_errors"] == 0 and out["alt_smt"] != out["config"]["smt"] and out["alt_rps"] > 10000
+    # the independent efficiency figure, the pod's attribution and the IPv4 headline
+    assert 0 < out["server_busy_cpu_us_per_req"] <= out["server_cpu_us_per_req"]
+    assert out["deployed_pod_server_busy_cpu_us_per_req"] > 0 and out["deployed_pod_tcp_per_req"]["OutSegs"] >= 1.9
+    if out["config"]["loopback"] != "127.0.0.1":
+        assert out["v4_errors"] == 0 and out["v4_rps"] > 10000
 
 
 @pytest.mark.gpu
@@ -71,7 +78,8 @@ def test_bench_two_ranks_on_host():
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", "29517", str(ROOT / "bench.py"),
                         "--gpus", "2", "--steps", "3", "--warmup", "1", "--reqs-per-conn", "500",
-                        "--c1-seconds", "1", "--deployed-seconds", "0", "--chain-seconds", "0"],
+                        "--c1-seconds", "1", "--deployed-seconds", "0", "--chain-seconds", "0",
+                        "--plain-seconds", "2"],
                        capture_output=True, text=True, timeout=600,
                        env={**os.environ, "HOLA_BENCH_PORT": "18760"})
     assert r.returncode == 0, r.stderr[-3000:]
@@ -86,6 +94,10 @@ def test_bench_two_ranks_on_host():
     # the planner keeps each load-generator thread in the L3 of the replica it drives
     loc = out["locality"]["fraction"]
     assert loc["same_core"] + loc["same_l3"] > 0.8, loc
+    # ... and the same replicas behind a topology-blind front
+    assert out["plain_errors"] == 0 and out["plain_body_mismatch"] == 0
+    assert out["plain_body_checked"] == out["plain_requests"] > 0 and out["plain_rps"] > 10000
+    assert abs(sum(out["plain_locality"].values()) - 1.0) < 1e-3 and "places no client" in out["config"]["lb"]
 
 
 @pytest.mark.gpu
@@ -95,7 +107,8 @@ def test_tracing_as_deployed_on_host():
     reach the collector, and the request path does not slow down."""
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--steps", "4", "--warmup", "1",
                         "--reqs-per-conn", "20000", "--c1-seconds", "0", "--deployed-seconds", "0",
-                        "--chain-seconds", "0", "--chain-shipped-seconds", "0", "--alt-seconds", "0", "--zipkin-sink"],
+                        "--chain-seconds", "0", "--chain-shipped-seconds", "0", "--alt-seconds", "0", "--zipkin-sink",
+                        "--v4-seconds", "0"],
                        capture_output=True, text=True, timeout=600, env={**os.environ, "HOLA_BENCH_PORT": "18720"})
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads(r.stdout.strip().splitlines()[-1])
@@ -111,7 +124,8 @@ def test_pipelined_bench_on_host():
     """`bench.py --pipeline 16` on the real host: 16 requests share each loopback segment."""
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--pipeline", "16", "--steps", "2", "--warmup", "1",
                         "--reqs-per-conn", "16000", "--c1-seconds", "0", "--deployed-seconds", "0",
-                        "--chain-seconds", "0", "--chain-shipped-seconds", "0", "--alt-seconds", "0"],
+                        "--chain-seconds", "0", "--chain-shipped-seconds", "0", "--alt-seconds", "0",
+                        "--v4-seconds", "0"],
                        capture_output=True, text=True, timeout=300,
                        env={**os.environ, "HOLA_BENCH_PORT": "18780"})
     assert r.returncode == 0, r.stderr[-3000:]
@@ -247,7 +261,7 @@ def test_eight_ranks_run_under_the_node_plan():
                         "--master-addr", "127.0.0.1", "--master-port", "29537", str(ROOT / "bench.py"),
                         "--gpus", "8", "--gpu-slots", "8", "--ignore-quota", "--steps", "2", "--warmup", "1",
                         "--reqs-per-conn", "200", "--busy-poll-us", "0", "--c1-seconds", "0",
-                        "--deployed-seconds", "0", "--chain-seconds", "0"],
+                        "--deployed-seconds", "0", "--chain-seconds", "0", "--plain-seconds", "0"],
                        capture_output=True, text=True, timeout=300,
                        env={**os.environ, "HOLA_BENCH_PORT": "18800", "HOLA_BENCH_CUDA_SYNC": "0"})
     assert r.returncode == 0, r.stderr[-3000:]
