@@ -29,6 +29,8 @@ PRESETS = {
     "asan": ["-DCMAKE_BUILD_TYPE=RelWithDebInfo", "-DHOLA_SANITIZE=address,undefined", "-DHOLA_BUILD_PYTHON=OFF"],
     # gcov line coverage of the native code under the test suite (HOLA_SANITIZER=coverage)
     "coverage": ["-DCMAKE_BUILD_TYPE=Debug", "-DHOLA_COVERAGE=ON", "-DHOLA_BUILD_PYTHON=OFF"],
+    # clock reads counted and exported (tests/test_clock_reads.py)
+    "clockcount": ["-DCMAKE_BUILD_TYPE=Release", "-DHOLA_COUNT_CLOCK_READS=ON", "-DHOLA_BUILD_PYTHON=OFF"],
     # pre-AVX2 nodes: x86-64-v2, the parser's and line scan's byte loops (src/core/isa.h)
     "portable": ["-DCMAKE_BUILD_TYPE=Release", "-DHOLA_MARCH=x86-64-v2", "-DHOLA_MTUNE=generic",
                  "-DHOLA_BUILD_PYTHON=OFF"],

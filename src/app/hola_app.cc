@@ -495,11 +495,14 @@ void HolaApp::handle_chaining(http::Connection& c, const http::Request& r, Worke
     if (traced) tracer_->end_server(c.worker().index(), span, 500);
     return;
   }
-  const int64_t t0 = mono_ns();
+  // The request's latency for /metrics: from this pass's time to the time of the pass that
+  // answers it (loop_now_ns(): no clock read of its own; an answer in this same pass, as a
+  // short-circuit is, counts the pass's own handling time as 0)
+  const int64_t t0 = loop_now_ns();
   if (!chainer_) {
     c.send(wc.chaining_fallback[ka][head].view());
     if (traced) tracer_->end_server(c.worker().index(), span, 200);
-    if (prom_) prom_->observe_chaining_us(c.worker().index(), uint64_t(mono_ns() - t0) / 1000);
+    if (prom_) prom_->observe_chaining_us(c.worker().index(), uint64_t(loop_now_ns() - t0) / 1000);
     return;
   }
   // Async: the connection is parked until aloha answers, times out or is short-circuited.
@@ -523,7 +526,7 @@ void HolaApp::handle_chaining(http::Connection& c, const http::Request& r, Worke
                        self->refresh(w, wc);
                      conn->complete(wc.server_error[ka][head].view(), ka);
                      if (traced) self->tracer_->end_server(w.index(), span, 500);
-                     if (self->prom_) self->prom_->observe_chaining_us(w.index(), uint64_t(mono_ns() - t0) / 1000);
+                     if (self->prom_) self->prom_->observe_chaining_us(w.index(), uint64_t(loop_now_ns() - t0) / 1000);
                      return;
                    }
                    if (!conn->closed() && res.fallback) {
@@ -587,7 +590,7 @@ void HolaApp::handle_chaining(http::Connection& c, const http::Request& r, Worke
                      conn->complete(build_response(s, w.date()).view(), ka);
                    }
                    if (traced) self->tracer_->end_server(w.index(), span, 200);
-                   if (self->prom_) self->prom_->observe_chaining_us(w.index(), uint64_t(mono_ns() - t0) / 1000);
+                   if (self->prom_) self->prom_->observe_chaining_us(w.index(), uint64_t(loop_now_ns() - t0) / 1000);
                  });
 }
 

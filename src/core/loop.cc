@@ -128,12 +128,12 @@ void EventLoop::run_timers() {
   }
 }
 
-int EventLoop::next_timeout_ms() {
+int EventLoop::next_timeout_ms(int64_t now_ns) {
   // About to block: drop cancelled entries at the top first, so that a cancelled timer cannot
   // wake the loop at its old deadline (passes that find work skip this lookup; see run()).
   while (!heap_.empty() && !timers_.count(heap_.top().id)) heap_.pop();
   if (heap_.empty()) return -1;
-  int64_t d = heap_.top().deadline - mono_ms();
+  int64_t d = heap_.top().deadline - now_ns / 1000000;
   if (d <= 0) return 0;
   return d > 1000000 ? 1000000 : int(d);
 }
@@ -192,7 +192,8 @@ void EventLoop::run() {
   constexpr int kMaxEvents = 256;
   epoll_event evs[kMaxEvents];
   t_loop_now_ms = &now_ms_;  // LoopClock on this thread reads the pass's time
-  pass_end_ns_ = mono_ns();
+  t_loop_now_ns = &now_ns_;
+  pass_end_ns_ = now_ns_ = mono_ns();
   uint64_t passes = 0;
   while (!stop_.load(std::memory_order_relaxed)) {
     act_.passes.store(++passes, std::memory_order_relaxed);
@@ -231,7 +232,7 @@ void EventLoop::run() {
       const bool off = busy_auto_ && busy_poll_ns_ > 0 && now_ms_ < spin_off_until_ms_;
       const int64_t w0 = polled ? t : mono_ns();
       if (!polled) note_gap(w0 - pass_end_ns_);
-      const int timeout = next_timeout_ms();
+      const int timeout = next_timeout_ms(w0);  // w0: read just now (no clock read of its own)
       n = epoll_wait(epfd_, evs, kMaxEvents, timeout);
       if (n < 0) wait_errno = errno;
       t = mono_ns();
@@ -252,6 +253,7 @@ void EventLoop::run() {
       std::abort();
     }
     now_ms_ = t / 1000000;
+    now_ns_ = t;
     act_.pass_ns.store(t, std::memory_order_relaxed);
     if (n > 0) {
       set_phase(kEvents);
@@ -278,6 +280,7 @@ void EventLoop::run() {
     pass_end_ns_ = t;  // the next pass's first poll measures its gap from here
   }
   t_loop_now_ms = nullptr;
+  t_loop_now_ns = nullptr;
   set_phase(kPosted);
   drain_posted();
   if (on_exit_) on_exit_();

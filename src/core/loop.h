@@ -139,13 +139,14 @@ class EventLoop {
   };
   void run_timers();
   void drain_posted();
-  int next_timeout_ms();
+  int next_timeout_ms(int64_t now_ns);
 
   int epfd_ = -1;
   int wakefd_ = -1;
   WakeHandler wake_;
   std::atomic<bool> stop_{false};
   int64_t now_ms_ = 0;
+  int64_t now_ns_ = 0;  // the pass's mono_ns() (t_loop_now_ns)
   std::priority_queue<TimerEntry, std::vector<TimerEntry>, std::greater<TimerEntry>> heap_;
   std::unordered_map<TimerId, std::function<void()>> timers_;
   std::atomic<size_t> pending_{0};  // timers_.size(), published for other threads

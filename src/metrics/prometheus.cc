@@ -172,9 +172,10 @@ std::string Prometheus::render(http::Server* server) const {
       // Where the workers' time goes: CPU in polls that found nothing while spinning (process
       // CPU minus this = the CPU that served), waits that could sleep, and gaps between polls
       // (handlers + descheduling) past 100 us / 1 ms / 10 ms with the longest one
-      uint64_t idle_ns = 0, sleeps = 0, gmax = 0, over[EventLoop::kGapBuckets] = {};
+      uint64_t idle_ns = 0, sleeps = 0, gmax = 0, passes = 0, over[EventLoop::kGapBuckets] = {};
       for (size_t i = 0; i < server->num_workers(); ++i) {
         const EventLoop& l = server->worker(i).loop();
+        passes += l.activity().passes.load(std::memory_order_relaxed);
         idle_ns += l.idle_spin_ns();
         sleeps += l.blocking_waits();
         gmax = std::max(gmax, l.gap_max_ns());
@@ -185,6 +186,7 @@ std::string Prometheus::render(http::Server* server) const {
       o += "# TYPE hola_loop_idle_spin_seconds_total counter\nhola_loop_idle_spin_seconds_total ";
       o += num;
       o += "\n# TYPE hola_loop_blocking_waits_total counter\nhola_loop_blocking_waits_total " + std::to_string(sleeps) + "\n";
+      o += "# TYPE hola_loop_passes_total counter\nhola_loop_passes_total " + std::to_string(passes) + "\n";
       o += "# TYPE hola_loop_poll_gaps_total counter\n";
       static const char* const kOver[EventLoop::kGapBuckets] = {"100us", "1ms", "10ms"};
       for (int k = 0; k < EventLoop::kGapBuckets; ++k)
@@ -202,6 +204,11 @@ std::string Prometheus::render(http::Server* server) const {
     for (size_t i = 0; i < server->num_workers(); ++i) timers += server->worker(i).loop().pending_timers();
     o += "# TYPE hola_event_loop_timers gauge\nhola_event_loop_timers " + std::to_string(timers) + "\n";
   }
+#ifdef HOLA_COUNT_CLOCK_READS
+  o += "# TYPE hola_clock_reads_total counter\nhola_clock_reads_total{clock=\"precise\"} " +
+       std::to_string(g_clock_reads.load(std::memory_order_relaxed)) + "\nhola_clock_reads_total{clock=\"coarse\"} " +
+       std::to_string(g_coarse_clock_reads.load(std::memory_order_relaxed)) + "\n";
+#endif
   if (tracer_) {
     tracing::TracerStats t = tracer_->stats();
     o += "# TYPE hola_spans_recorded_total counter\nhola_spans_recorded_total " + std::to_string(t.recorded) + "\n";

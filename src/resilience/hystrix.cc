@@ -99,6 +99,7 @@ RollingCounter::RollingCounter(int window_ms, int buckets)
     : window_ms_(window_ms), nb_(buckets), bucket_ms_(window_ms / buckets), b_(size_t(buckets)) {}
 
 RollingCounter::Bucket& RollingCounter::current(int64_t now) {
+  if (cur_ && now >= cur_start_ && now - cur_start_ < bucket_ms_) return *cur_;
   int64_t start = now - (now % bucket_ms_);
   Bucket& b = b_[size_t((now / bucket_ms_) % nb_)];
   if (b.start != start) {
@@ -106,6 +107,8 @@ RollingCounter::Bucket& RollingCounter::current(int64_t now) {
     b.c.fill(0);
     b.max_conc = 0;
   }
+  cur_ = &b;
+  cur_start_ = start;
   return b;
 }
 
@@ -142,6 +145,7 @@ void RollingCounter::reset(int64_t) {
     b.c.fill(0);
     b.max_conc = 0;
   }
+  cur_ = nullptr;
 }
 
 // ---------------------------------------------------------------- RollingPercentile
@@ -166,6 +170,7 @@ int64_t RollingPercentile::bin_value(int b) {
 }
 
 RollingPercentile::Bucket& RollingPercentile::current(int64_t now) {
+  if (cur_ && now >= cur_start_ && now - cur_start_ < bucket_ms_) return *cur_;
   int64_t start = now - (now % bucket_ms_);
   Bucket& b = b_[size_t((now / bucket_ms_) % nb_)];
   if (b.start != start) {
@@ -173,6 +178,8 @@ RollingPercentile::Bucket& RollingPercentile::current(int64_t now) {
     b.h.fill(0);
     b.sum = b.count = 0;
   }
+  cur_ = &b;
+  cur_start_ = start;
   return b;
 }
 

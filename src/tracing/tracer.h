@@ -106,6 +106,9 @@ class Tracer {
   Tracer(TracerOptions o, int num_workers);
   ~Tracer();
   bool enabled() const { return o_.enabled; }
+  // A collector is configured: spans are recorded (timestamps and all). Without one they are
+  // only counted, so callers skip reading the wall clock for them.
+  bool collecting() const { return collecting_; }
   void start();
   void stop();  // flushes what is buffered
 
