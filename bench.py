@@ -417,6 +417,7 @@ def main() -> int:
     subs: dict[str, dict | None] = {}
     if world == 1:
         rank_cpus = list(server_cpus) + list(load_cpus)
+        pod_cpus = sorted(server_cpus)[:subruns.manifest_pod_cpus()]
         for key, secs, fn in (
                 # the headline on the image's address family, when it ran on ::1
                 ("v4", a.v4_seconds if host != "127.0.0.1" else 0,
@@ -424,10 +425,17 @@ def main() -> int:
                                              bodies and [bodies[0]], a.v4_seconds)),
                 ("deployed", a.deployed_seconds,
                  lambda: subruns.deployed(a, server_cpus, load_cpus, job_cpus, zipkin=a.deployed_zipkin)),
-                # the same, sized as the manifests size one pod (limits.cpu: a 2-CPU cpuset)
+                # the same, sized as the manifests size one pod (limits.cpu: a 2-CPU cpuset), its
+                # load generator on the rank's load-generator CPUs in the pod's L3 (as the
+                # headline's is placed) ...
                 ("deployed_pod", a.deployed_seconds,
-                 lambda: subruns.deployed(a, sorted(server_cpus)[:subruns.manifest_pod_cpus()], load_cpus, job_cpus,
+                 lambda: subruns.deployed(a, pod_cpus, subruns.pod_loadgen_cpus(pod_cpus, load_cpus), job_cpus,
                                           zipkin=a.deployed_zipkin)),
+                # ... and on all of them, across two L3s (round 5's deployed_pod_*): what clients
+                # in another cache domain cost the pod (profiles/round6/01_pod_shape)
+                ("deployed_pod_spanning", a.deployed_seconds / 2,
+                 lambda: subruns.deployed(a, pod_cpus, load_cpus, job_cpus, zipkin=a.deployed_zipkin,
+                                          seconds=a.deployed_seconds / 2)),
                 ("chain", a.chain_seconds, lambda: subruns.chain(a, rank_cpus, job_cpus)),
                 ("chain_shipped", a.chain_shipped_seconds,
                  lambda: subruns.chain(a, rank_cpus, job_cpus, shipped=True, seconds=a.chain_shipped_seconds)),
@@ -503,6 +511,11 @@ def main() -> int:
             # ... in one pod's CPU limit (deploy/openshift: limits.cpu 2): what one pod of
             # BASELINE config 5 serves on its own, with the attribution of its CPU per request
             **_deployed_keys(subs.get("deployed_pod"), "deployed_pod", full=False),
+            **{k: v for k, v in _deployed_keys(subs.get("deployed_pod_spanning"), "deployed_pod_spanning",
+                                               full=False).items()
+               if k.rsplit("deployed_pod_spanning_", 1)[-1] in (
+                   "rps", "p99_ms", "server_cpu_us_per_req", "server_busy_cpu_us_per_req", "loadgen_cpus", "locality",
+                   "error", "errors", "body_mismatch")},
             # N = 1 only: GET /api/hola-chaining through two replicas (the endpoint with real work
             # behind it), engineered (pool 128, logging off) and as shipped (pool 10, BASIC logging)
             **_chain_keys(subs.get("chain"), "chain"),
@@ -729,9 +742,21 @@ def _busy_keys(gathered: list[dict], total: int) -> dict:
     def loop_sum(rows, key):
         return sum(r.get(key, 0) for r in rows)
 
+    def per_req(rows, key):  # a per-request figure of every rank, weighted by its requests
+        if any(r.get(key) is None for r in rows):
+            return None
+        return round(sum(r[key] * g["requests"] for r, g in zip(rows, gathered)) / n, 1)
+
     return {
         "server_busy_cpu_us_per_req": round(1e6 * (sum(g["server_cpu_s"] for g in gathered) - loop_sum(srv, "idle_spin_s")) / n, 3),
         "loadgen_busy_cpu_us_per_req": round(1e6 * (sum(g["loadgen_cpu_s"] for g in gathered) - loop_sum(lg, "idle_spin_s")) / n, 3),
+        # each side's own user-space instructions and cycles per request (hardware counters of
+        # the serving threads; null where the host does not allow them): independent of each
+        # other, where the CPU-time figures of two saturated peers are not
+        "server_user_instr_per_req": per_req(srv, "user_instr_per_req"),
+        "server_user_cycles_per_req": per_req(srv, "user_cycles_per_req"),
+        "loadgen_user_instr_per_req": per_req(lg, "user_instr_per_req"),
+        "loadgen_user_cycles_per_req": per_req(lg, "user_cycles_per_req"),
         "server_loop": {"idle_spin_s": round(loop_sum(srv, "idle_spin_s"), 3),
                         "blocking_waits_per_req": round(sum(r["blocking_waits_per_req"] for r in srv) / len(srv), 4),
                         "gaps_over_100us": loop_sum(srv, "gaps_over_100us"), "gaps_over_1ms": loop_sum(srv, "gaps_over_1ms"),
@@ -858,6 +883,7 @@ def _deployed_keys(d: dict | None, p: str = "deployed", full: bool = True) -> di
            f"{p}_loadgen": d["loadgen"], f"{p}_tcp_per_req": d["tcp_per_req"],
            f"{p}_host_load": d["host_load"], f"{p}_host_load_server": d["host_load_server"],
            f"{p}_host_load_loadgen": d["host_load_loadgen"],
+           f"{p}_locality": d["locality"],
            f"{p}_cpus": d["cpus"], f"{p}_loadgen_cpus": d["loadgen_cpus"], f"{p}_connections": d["connections"],
            f"{p}_loadgen_busy_poll_us": d["loadgen_busy_poll_us"]}
     if full:

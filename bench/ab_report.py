@@ -4,8 +4,13 @@
 Pairs run i of the baseline with run i of the candidate. A pair is kept only when neither
 side's `host_load.siblings` (busy share of the SMT siblings of the replica's cores: other
 tenants on our physical cores) exceeds --max-sibling-load. For the kept pairs it reports the
-paired difference of server CPU µs per request (the primary metric: the server's own cost,
-which sibling load and client jitter move least) and of req/s, with a 95 % t-interval.
+paired difference, with a 95 % t-interval, of the server's own efficiency figures and of
+req/s. The primary efficiency figure is the server's user-space instructions per request
+(`server_user_instr_per_req`, hardware counters of its workers: its own code's work, which
+neither a saturated peer nor sibling load moves), then its user cycles and its busy CPU per
+request (CPU minus empty polls). Raw CPU µs per request is shown last: at saturation a server
+and its load generator both run flat out, so that figure is their CPUs' wall time over the
+request count for both, the same number by construction.
 Because the sibling load moves every run's cost, it also fits one line through all runs of
 both variants, server µs/request = a + d * [candidate] + b * sibling load, and reports d (the
 candidate's cost at equal sibling load) with its 95 % interval: a gate that keeps every run.
@@ -39,6 +44,14 @@ def ci(diffs: list[float]) -> tuple[float, float, float]:
         return m, float("nan"), float("nan")
     h = t95(len(diffs) - 1) * statistics.stdev(diffs) / math.sqrt(len(diffs))
     return m, m - h, m + h
+
+
+# Efficiency figures, primary first (see the module docstring); a figure is reported when both
+# runs of a pair carry it.
+EFFICIENCY = (("server_user_instr_per_req", "server user instr/req"),
+              ("server_user_cycles_per_req", "server user cycles/req"),
+              ("server_busy_cpu_us_per_req", "server busy CPU us/req"),
+              ("server_cpu_us_per_req", "server CPU us/req (raw)"))
 
 
 def load(d: Path, label: str) -> dict[int, dict]:
@@ -109,15 +122,20 @@ def main() -> int:
     res = {"baseline": a.baseline, "candidate": a.candidate, "pairs": len(rows), "kept": len(kept),
            "max_sibling_load": a.max_sibling_load, "rows": rows}
     if kept:
-        us = [100.0 * (r["us_cand"] - r["us_base"]) / r["us_base"] for r in kept]
+        print(f"\n{a.candidate} vs {a.baseline}, {len(kept)} kept pairs (siblings <= {a.max_sibling_load:.0%}):")
+        for key, label in EFFICIENCY:
+            pairs = [(base[r["pair"]].get(key), cand[r["pair"]].get(key)) for r in kept]
+            pairs = [(x, y) for x, y in pairs if x and y]
+            if not pairs:
+                continue
+            m, lo, hi = ci([100.0 * (y - x) / x for x, y in pairs])
+            res[f"{key}_delta_pct"] = {"mean": round(m, 2), "ci95": [round(lo, 2), round(hi, 2)], "pairs": len(pairs)}
+            print(f"  {label:<26}: {m:+.2f} % (95 % CI {lo:+.2f} .. {hi:+.2f}), {len(pairs)} pairs")
+        res["server_us_per_req_delta_pct"] = res.get("server_cpu_us_per_req_delta_pct")
         rps = [100.0 * (r["rps_cand"] - r["rps_base"]) / r["rps_base"] for r in kept]
-        m, lo, hi = ci(us)
-        res["server_us_per_req_delta_pct"] = {"mean": round(m, 2), "ci95": [round(lo, 2), round(hi, 2)]}
         m2, lo2, hi2 = ci(rps)
         res["rps_delta_pct"] = {"mean": round(m2, 2), "ci95": [round(lo2, 2), round(hi2, 2)]}
-        print(f"\n{a.candidate} vs {a.baseline}, {len(kept)} kept pairs (siblings <= {a.max_sibling_load:.0%}):")
-        print(f"  server us/req: {m:+.2f} % (95 % CI {lo:+.2f} .. {hi:+.2f})")
-        print(f"  req/s        : {m2:+.2f} % (95 % CI {lo2:+.2f} .. {hi2:+.2f})")
+        print(f"  {'req/s':<26}: {m2:+.2f} % (95 % CI {lo2:+.2f} .. {hi2:+.2f})")
     else:
         print("\nno pair passed the sibling-load gate")
     adj = adjusted(rows)

@@ -21,6 +21,8 @@
 #   chain              two-hop chaining bench (loadgen -> hola A -> hola B)
 #   deployedab REPS [ARGS]  headline replica vs as-deployed (ZIPKIN_SERVER_URL as deployed /
 #                      unset / native sink), interleaved (bench/deployed_ab.py)
+#   chainwork          instructions per chained request (this tree, r5end, r4end) and user-cycles
+#                      and CPU-time profiles of hola A
 #   podshape [REPS] [ARGS]  the shipped pod shape's CPU per request, one thing varied at a time
 #                      (bench/pod_shape.py), then the default bench
 #   chainmodes REPS [ARGS]  bench.py's chain sub-run REPS times per variant with its attribution
@@ -191,6 +193,22 @@ chain)
 deployedab)
   REPS=${1:-4}; shift || true
   timeout -k 10 1000 python -u bench/deployed_ab.py --reps "$REPS" --out "$OUT" "$@" > "$OUT/deployed_ab.log" 2>&1
+  ;;
+chainwork)
+  # user-space instructions per chained request on hola A (this tree vs
+  # round 5's end and round 4's end), then a user-cycles profile of A's workers (where the
+  # remaining own-code cycles are) with the raw profile kept for address resolution
+  info
+  timeout -k 10 600 python -u bench/instr_ab.py "$OUT/instr" head=build/release/hola r5end=build/r5end/hola \
+    r4end=build/r4end/hola --chain --rounds "${ROUNDS:-3}" > "$OUT/instr.log" 2>&1 &&
+  HOLA_CPUPROF_EVENT=user-cycles timeout -k 10 120 python bench/chain_bench.py --duration 8 \
+    --cpu-profile "$OUT/chain_a_user.prof" --out "$OUT/chain_user.json" > "$OUT/chain_user.log" 2>&1 &&
+  python bench/cpuprof_report.py "$OUT/chain_a_user.prof" --top 60 --json "$OUT/chain_user_report.json" \
+    > "$OUT/chain_user_report.txt" 2>> "$OUT/err.log" &&
+  timeout -k 10 120 python bench/chain_bench.py --duration 8 --cpu-profile "$OUT/chain_a.prof" \
+    --out "$OUT/chain.json" > "$OUT/chain.log" 2>&1 &&
+  python bench/cpuprof_report.py "$OUT/chain_a.prof" --top 60 --json "$OUT/chain_report.json" \
+    > "$OUT/chain_report.txt" 2>> "$OUT/err.log"
   ;;
 podshape)
   # the pod shape (2 CPUs) vs 8 CPUs, one thing varied at a time, then the

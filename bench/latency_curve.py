@@ -14,6 +14,8 @@ from pathlib import Path
 
 sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
 
+from hola_amd.parallel import subruns  # noqa: E402
+from hola_amd.parallel.hostmetrics import cgroup_cpu_stat, cpu_times, task_stats, task_stats_delta  # noqa: E402
 from hola_amd.parallel.loadgen import run_duration  # noqa: E402
 from hola_amd.server import HolaProcess  # noqa: E402
 from hola_amd.utils.cpu import format_cpu_list, plan_node, split_server_loadgen  # noqa: E402
@@ -41,23 +43,43 @@ with HolaProcess(args=server_args, env={"HOSTNAME": "h"}, threads=len(srv), cpu_
             v = f.read().rsplit(")", 1)[1].split()
         return (int(v[11]) + int(v[12])) / os.sysconf("SC_CLK_TCK")
 
+    job = list(srv) + list(lg)
+    probe = subruns.MetricsProbe("127.0.0.1", s.port)
     for rate in [float(x) for x in a.rates.split(",")]:
         c0 = resource.getrusage(resource.RUSAGE_CHILDREN)
         s0 = server_cpu()
+        # what a tail could come from, recorded per point: the replica's
+        # spin / back-off / resume transitions and gaps between its polls, its workers'
+        # involuntary switches (preempted by another task), CFS throttling of the cgroup, the
+        # host load (IRQ time, siblings, L3 neighbours) of both sides, and the load
+        # generator's own gaps and late sends
+        m0, ts0, thr0, t0 = subruns.metrics_counters(s.port, probe=probe), task_stats(s.proc.pid), cgroup_cpu_stat(), cpu_times()
         r = run_duration([("127.0.0.1", s.port)], a.connections, len(lg), a.duration, 2.0,
                          cpu_list=",".join(map(str, lg)), rate=rate, busy_poll_us=a.busy_poll_us,
                          spin_us=a.spin_us, verify_body=True)
+        m1, ts1, thr1, t1 = subruns.metrics_counters(s.port, probe=probe), task_stats(s.proc.pid), cgroup_cpu_stat(), cpu_times()
         c1 = resource.getrusage(resource.RUSAGE_CHILDREN)
         s1 = server_cpu()
         wall = a.duration + 2.0  # warmup included in both CPU figures
         lat = r["latency"]
+        reqs = max(1.0, r["rps"] * a.duration)
         row = {"target_rps": rate, "achieved_rps": r["rps"], "p50_us": lat["p50_ns"] / 1e3,
                "p90_us": lat["p90_ns"] / 1e3, "p99_us": lat["p99_ns"] / 1e3, "p999_us": lat["p999_ns"] / 1e3,
                "max_us": lat["max_ns"] / 1e3, "errors": lat["errors"],
                "server_cpus_busy": round((s1 - s0) / wall, 2),
-               "loadgen_cpus_busy": round((c1.ru_utime + c1.ru_stime - c0.ru_utime - c0.ru_stime) / wall, 2)}
+               "loadgen_cpus_busy": round((c1.ru_utime + c1.ru_stime - c0.ru_utime - c0.ru_stime) / wall, 2),
+               "server_loop": subruns.loop_block(m0, m1, reqs),
+               "server_threads": task_stats_delta(ts0, ts1),
+               "cgroup_throttle": {"periods": thr1.get("nr_periods", 0) - thr0.get("nr_periods", 0),
+                                   "throttled_periods": thr1.get("nr_throttled", 0) - thr0.get("nr_throttled", 0),
+                                   "throttled_ms": round((thr1.get("throttled_usec", 0) - thr0.get("throttled_usec", 0)) / 1e3, 1)},
+               "host_load_server": subruns.host_load(t0, t1, srv, job),
+               "host_load_loadgen": subruns.host_load(t0, t1, lg, job),
+               "loadgen": {k: lat.get(k) for k in ("gaps_over_100us", "gaps_over_1ms", "gaps_over_10ms", "gap_max_ns",
+                                                   "send_late_max_ns", "blocking_waits")}}
         rows.append(row)
         print(json.dumps(row), flush=True)
+    probe.close()
 out = {"cpu_map": {"server": format_cpu_list(srv), "loadgen": format_cpu_list(lg)}, "connections": a.connections,
        "busy_poll_us": a.busy_poll_us, "server_busy_poll": server_bp, "server_args": server_args, "spin_us": a.spin_us, "rows": rows}
 if a.out:

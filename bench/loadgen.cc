@@ -76,6 +76,7 @@
 #include "core/affinity.h"
 #include "core/clock.h"
 #include "core/net.h"
+#include "core/perfcount.h"
 #include "core/scan.h"
 
 using namespace hola;
@@ -150,6 +151,11 @@ struct ThreadState {
   // 10 ms and the longest, and (open loop) the latest a scheduled send went out.
   uint64_t poll_hits = 0, spin_hits = 0, spin_misses = 0, blocking_waits = 0, idle_spin_ns = 0;
   uint64_t gaps_over[3] = {}, gap_max_ns = 0, send_late_max_ns = 0;
+  // the thread's own user-space instructions and cycles (hardware counters, where allowed),
+  // counted from the last reset
+  ThreadCounters pmu;
+  uint64_t pmu_ins0 = 0, pmu_cyc0 = 0;
+  void pmu_reset() { pmu.read(&pmu_ins0, &pmu_cyc0); }
   void note_gap(int64_t ns) {
     if (ns <= 100000) return;
     gaps_over[0] += 1;
@@ -378,6 +384,7 @@ void thread_main(ThreadState* ts, const Options* o) {
     pthread_setname_np(pthread_self(), name);
   }
   hola::cpuprof::register_thread();
+  if (ts->pmu.open()) ts->pmu_reset();
   // Connections (and their receive buffers) are built here, after pinning, so their pages
   // are first touched on this thread's NUMA node: on a 2-socket node a thread may drive a
   // replica on the other socket from main()'s.
@@ -541,6 +548,7 @@ void thread_main(ThreadState* ts, const Options* o) {
         ts->completed = 0;
         ts->recording = true;
         // the time accounting covers the measured part too
+        ts->pmu_reset();
         ts->poll_hits = ts->spin_hits = ts->spin_misses = ts->blocking_waits = ts->idle_spin_ns = 0;
         ts->gaps_over[0] = ts->gaps_over[1] = ts->gaps_over[2] = ts->gap_max_ns = ts->send_late_max_ns = 0;
       }
@@ -722,8 +730,15 @@ std::string stats_json(std::vector<std::unique_ptr<ThreadState>>& ts, bool with_
   Histogram h;
   uint64_t errors = 0, non2xx = 0, reconnects = 0, checked = 0, mismatch = 0, alt = 0;
   uint64_t poll_hits = 0, spin_hits = 0, spin_misses = 0, sleeps = 0, idle_ns = 0, gmax = 0, late = 0;
-  uint64_t over[3] = {};
+  uint64_t over[3] = {}, u_ins = 0, u_cyc = 0;
+  bool pmu = false;
   for (auto& t : ts) {
+    uint64_t a = 0, b = 0;
+    if (t->pmu.read(&a, &b)) {
+      pmu = true;
+      u_ins += a - t->pmu_ins0;
+      u_cyc += b - t->pmu_cyc0;
+    }
     std::lock_guard<std::mutex> g(t->hist_mu);
     h.merge(t->hist);
     errors += t->errors;
@@ -761,6 +776,11 @@ std::string stats_json(std::vector<std::unique_ptr<ThreadState>>& ts, bool with_
            (unsigned long long)over[1], (unsigned long long)over[2], (unsigned long long)gmax,
            (unsigned long long)late);
   s += buf;
+  if (pmu) {
+    snprintf(buf, sizeof buf, ",\"user_instructions\":%llu,\"user_cycles\":%llu", (unsigned long long)u_ins,
+             (unsigned long long)u_cyc);
+    s += buf;
+  }
   if (with_hist) s += ",\"hist\":\"" + h.encode() + "\"";
   return s + "}";
 }
@@ -1086,6 +1106,7 @@ int main(int argc, char** argv) {
         std::lock_guard<std::mutex> g(t->hist_mu);
         t->hist.reset();
         t->errors = t->non2xx = t->reconnects = t->body_checked = t->body_mismatch = t->body_alt = 0;
+        t->pmu_reset();
         t->poll_hits = t->spin_hits = t->spin_misses = t->blocking_waits = t->idle_spin_ns = 0;
         t->gaps_over[0] = t->gaps_over[1] = t->gaps_over[2] = t->gap_max_ns = t->send_late_max_ns = 0;
       }

@@ -16,6 +16,9 @@ waits, the load generator's poll outcomes, TCP segments, host load incl. IRQ tim
   w1 / w4     pod with 1 / 4 server workers inside the 2-CPU cpuset
   c16 / c256  pod with 16 / 256 connections
   lgt2        pod with 2 load-generator threads (as many as the pod has CPUs)
+  lgsame      pod with the load-generator threads in the pod's own L3 only
+  lgcross     pod with the load-generator threads in the other L3 only
+  lgt2x       pod with 2 load-generator threads, in the other L3
 
 and finally one `pod` run with --cpu-profile (cpuprof_pod.txt via bench/cpuprof_report.py).
 
@@ -36,6 +39,7 @@ sys.path.insert(0, str(ROOT))
 import bench  # noqa: E402
 from hola_amd.native import ensure_built  # noqa: E402
 from hola_amd.parallel import subruns  # noqa: E402
+from hola_amd.utils.cpu import parse_cpu_list  # noqa: E402
 
 VARIANTS = {
     "ref8": {},
@@ -47,13 +51,18 @@ VARIANTS = {
     "c16": {"connections": 16},
     "c256": {"connections": 256},
     "lgt2": {},
+    "lgsame": {},
+    "lgcross": {},
+    "lgt2x": {},
 }
 
 
 def run_variant(a, v: str, sv, ld, job, seconds: float, cpu_profile: str | None = None) -> dict:
     pod_cpus = sorted(sv)[:subruns.manifest_pod_cpus()]
     server = sv if v == "ref8" else pod_cpus
-    load = ld[:len(pod_cpus)] if v == "lgt2" else ld
+    same = subruns.pod_loadgen_cpus(pod_cpus, ld)
+    cross = [c for c in ld if c not in same] or ld
+    load = {"lgt2": ld[:len(pod_cpus)], "lgsame": same, "lgcross": cross, "lgt2x": cross[:len(pod_cpus)]}.get(v, ld)
     return subruns.deployed(a, server, load, job, seconds=seconds, cpu_profile=cpu_profile, **VARIANTS[v])
 
 
@@ -68,6 +77,9 @@ def summary_row(v: str, rows: list[dict]) -> dict:
             "p99_us": med(lambda r: r["p99_ns"] / 1e3),
             "server_cpu_us_per_req": med(lambda r: r["cpu_us_per_req"]),
             "server_busy_cpu_us_per_req": med(lambda r: r["server_busy_cpu_us_per_req"]),
+            "server_cpus_us_per_req": med(lambda r: r["server_cpus_us_per_req"]),
+            "loadgen_threads": med(lambda r: len(parse_cpu_list(r["loadgen_cpus"]))),
+            "same_l3_or_core": med(lambda r: r["locality"].get("same_l3", 0) + r["locality"].get("same_core", 0)),
             "workers_cpu_share": med(lambda r: r["server_threads"].get("workers", {}).get("cpu_s", 0) /
                                      max(1e-9, sum(g["cpu_s"] for g in r["server_threads"].values()))),
             "server_vol_per_req": med(lambda r: r["server_threads"].get("workers", {}).get("vol_per_req")),

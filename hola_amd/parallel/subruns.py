@@ -114,6 +114,12 @@ def metrics_counters(port: int, host: str = "127.0.0.1", probe: MetricsProbe | N
             out["loop.gaps_over_" + name.split('"')[1]] = float(val)
         elif name == "hola_loop_poll_gap_max_seconds":
             out["gauge.gap_max_s"] = float(val)
+        elif name == "hola_loop_passes_total":
+            out["loop.passes"] = float(val)
+        elif name == "hola_worker_user_instructions_total":
+            out["pmu.instructions"] = float(val)
+        elif name == "hola_worker_user_cycles_total":
+            out["pmu.cycles"] = float(val)
     return out
 
 
@@ -156,6 +162,16 @@ def deployed_argv_env(port: int, hostname: str, extra_args: list[str] | None = N
         else:
             env[k] = v
     return argv, env
+
+
+def pod_loadgen_cpus(pod_cpus, load_cpus) -> list[int]:
+    """The load-generator CPUs for a pod-sized replica: those of `load_cpus` in the L3 domains
+    of the pod's own CPUs, where the headline places its load generator too (a client thread
+    in another L3 makes every one of its connections a cross-CCD hand-off: twice the server's
+    CPU per request, profiles/round6/01_pod_shape). All of `load_cpus` when none share one."""
+    doms = {_cpu.l3_domain(c) for c in pod_cpus}
+    same = [c for c in load_cpus if _cpu.l3_domain(c) in doms]
+    return same or list(load_cpus)
 
 
 def manifest_pod_cpus() -> int:
@@ -262,7 +278,13 @@ def loop_block(m0: dict, m1: dict, reqs: float) -> dict:
     polls, waits that could sleep (per request), gaps between polls past 100 us / 1 ms / 10 ms
     and the longest gap since the replica started, adaptive spin outcomes."""
     d = counter_delta(m0, m1, "loop.")
+    pmu = counter_delta(m0, m1, "pmu.") if "pmu.instructions" in m1 else {}
     return {"idle_spin_s": round(m1.get("loop.idle_spin_s", 0.0) - m0.get("loop.idle_spin_s", 0.0), 4),
+            # the workers' own user-space instructions and cycles per request (hardware
+            # counters; absent where the host does not allow them)
+            "user_instr_per_req": round(pmu["instructions"] / max(1.0, reqs), 1) if pmu else None,
+            "user_cycles_per_req": round(pmu["cycles"] / max(1.0, reqs), 1) if pmu else None,
+            "passes_per_req": round(d.get("passes", 0) / max(1.0, reqs), 4),
             "blocking_waits_per_req": round(d.get("blocking_waits", 0) / max(1.0, reqs), 4),
             "gaps_over_100us": d.get("gaps_over_100us", 0), "gaps_over_1ms": d.get("gaps_over_1ms", 0),
             "gaps_over_10ms": d.get("gaps_over_10ms", 0),
@@ -277,6 +299,8 @@ def loadgen_block(st: dict, cpu_s: float, reqs: float) -> dict:
     idle = st.get("idle_spin_ns", 0) / 1e9
     n = max(1.0, reqs)
     return {"cpu_us_per_req": round(1e6 * cpu_s / n, 3), "busy_cpu_us_per_req": round(1e6 * (cpu_s - idle) / n, 3),
+            "user_instr_per_req": round(st["user_instructions"] / n, 1) if "user_instructions" in st else None,
+            "user_cycles_per_req": round(st["user_cycles"] / n, 1) if "user_cycles" in st else None,
             "idle_spin_s": round(idle, 4),
             "polls": {"hit_at_once": st.get("poll_hits", 0), "hit_after_spin": st.get("spin_hits", 0),
                       "ran_out": st.get("spin_misses", 0)},
@@ -287,7 +311,8 @@ def loadgen_block(st: dict, cpu_s: float, reqs: float) -> dict:
 
 
 def attributed_closed_loop(lg: ControlledLoadgen, seconds: float, pid: int, port: int, server_cpus, load_cpus,
-                           job_cpus, host: str = "127.0.0.1", warm_s: float = 1.0) -> dict:
+                           job_cpus, host: str = "127.0.0.1", warm_s: float = 1.0,
+                           before_connect: dict | None = None) -> dict:
     """timed_closed_loop() with the attribution a replica's CPU per request needs (VERDICT r5
     weak #1, #4): busy CPU per request (process CPU minus the loop's empty polls), the serving
     threads' CPU and context switches apart from the process's other threads, the loop's
@@ -325,6 +350,10 @@ def attributed_closed_loop(lg: ControlledLoadgen, seconds: float, pid: int, port
         "loadgen": loadgen_block(st, lg1 - lg0, reqs),
         "tcp_per_req": {k: round((tcp1[k] - tcp0[k]) / max(1.0, reqs), 3) for k in tcp1 if k in tcp0},
         "host_load_server": hl_server,
+        # where each connection's client ran relative to the worker serving it (from the
+        # replica's counters taken before the load generator connected)
+        "locality": locality_fraction(counter_delta(before_connect or {}, m1, "locality.")) if before_connect is not None
+        else {},
         "host_load_loadgen": host_load(t0, t1, load_cpus, job_cpus)})
     return r
 
@@ -387,13 +416,14 @@ def deployed(a, server_cpus, load_cpus, job_cpus, zipkin: str = "deployed", seco
     try:
         with DeployedProc(server_cpus, "hola-1-deplo", extra_args=extra, env_over=env_over) as d:
             body = ["Hola de hola-1-deplo"] if a.path == "/api/hola" else None
+            pre = metrics_counters(d.port)
             lg = ControlledLoadgen([("127.0.0.1", d.port)], conns, len(load_cpus),
                                    cpu_list=",".join(map(str, load_cpus)), path=a.path, busy_poll_us=lg_bp,
                                    busy_poll_pause=a.busy_poll_pause if lg_bp else 0, epoll_lt=a.epoll_lt,
                                    expect_bodies=body, verify_body=body is None)
             try:
                 r = attributed_closed_loop(lg, seconds or a.deployed_seconds, d.proc.pid, d.port, server_cpus,
-                                           load_cpus, job_cpus)
+                                           load_cpus, job_cpus, before_connect=pre)
             finally:
                 lg.close()
             shown = d.shown_args().split()

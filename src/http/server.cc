@@ -689,6 +689,7 @@ void Server::start() {
       char name[16];
       snprintf(name, sizeof name, "hola-w%d", wp->index());
       pthread_setname_np(pthread_self(), name);
+      if (opts_.perf_counters) wp->counters_.open();  // counts this thread only
       cpuprof::note_thread();  // stack bounds for a stall report's capture
       wp->tid_.store(cpuprof::current_tid());
       cpuprof::register_thread();

@@ -15,6 +15,7 @@
 
 #include "core/histogram.h"
 #include "core/loop.h"
+#include "core/perfcount.h"
 #include "http/parser.h"
 
 namespace hola::http {
@@ -173,6 +174,9 @@ struct ServerOptions {
   // Steer each accepted connection to a worker in the L3 domain where its packets arrive
   // (SO_INCOMING_CPU), when workers are pinned; otherwise plain round-robin.
   bool steer_l3 = true;
+  // Each worker counts its own user-space instructions and cycles (core/perfcount.h), exported
+  // on /metrics when the host allows it (--no-perf-counters turns it off).
+  bool perf_counters = true;
 };
 
 // Per-worker stage timings (ns) collected with --profile; read after the workers stop.
@@ -216,10 +220,13 @@ class Worker {
   // Per-worker slot for the application.
   void* app_data = nullptr;
   StageProfile* profile() { return profile_.get(); }
+  // The worker thread's own user-space instructions and cycles (open once it runs).
+  const ThreadCounters& counters() const { return counters_; }
 
  private:
   friend class Server;
   void tick();
+  ThreadCounters counters_;
   Server* server_;
   int index_;
   EventLoop loop_;

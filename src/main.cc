@@ -102,6 +102,8 @@ void usage() {
           "  --max-connections N      refuse connections beyond N per replica (default unlimited)\n"
           "  --no-steer               plain round-robin accept (default: L3-domain steering when pinned)\n"
           "  --epoll-lt               level-triggered connection sockets (default: edge-triggered)\n"
+          "  --no-perf-counters       do not count the workers' user-space instructions and cycles\n"
+          "                           (hardware counters on /metrics, where the host allows them)\n"
           "  --no-pin                 leave workers unpinned even when the affinity mask has exactly\n"
           "                           one CPU per worker (e.g. a kubelet static-CPU-manager cpuset)\n"
           "  --profile                per-stage latency histograms (accept/recv/parse/handle/send), dumped at exit\n"
@@ -268,6 +270,7 @@ int main(int argc, char** argv) {
     else if (a == "--busy-poll-pause") so.busy_poll_pause = atoi(val("--busy-poll-pause").c_str());
     else if (a == "--profile") so.profile = true;
     else if (a == "--no-steer") so.steer_l3 = false;
+    else if (a == "--no-perf-counters") so.perf_counters = false;
     else if (a == "--no-pin") auto_pin = false;
     else if (a == "--epoll-lt") so.edge_triggered = false;
     else if (a == "--idle-timeout-ms") so.idle_timeout_ms = atoi(val("--idle-timeout-ms").c_str());

@@ -187,6 +187,23 @@ std::string Prometheus::render(http::Server* server) const {
       o += num;
       o += "\n# TYPE hola_loop_blocking_waits_total counter\nhola_loop_blocking_waits_total " + std::to_string(sleeps) + "\n";
       o += "# TYPE hola_loop_passes_total counter\nhola_loop_passes_total " + std::to_string(passes) + "\n";
+      // the workers' own user-space instructions and cycles (hardware counters), when the
+      // host allows them: the CPU-independent efficiency figure of the serving code
+      uint64_t ins = 0, cyc = 0;
+      bool any = false;
+      for (size_t i = 0; i < server->num_workers(); ++i) {
+        uint64_t a = 0, b = 0;
+        if (server->worker(i).counters().read(&a, &b)) {
+          ins += a;
+          cyc += b;
+          any = true;
+        }
+      }
+      if (any) {
+        o += "# TYPE hola_worker_user_instructions_total counter\nhola_worker_user_instructions_total " +
+             std::to_string(ins) + "\n";
+        o += "# TYPE hola_worker_user_cycles_total counter\nhola_worker_user_cycles_total " + std::to_string(cyc) + "\n";
+      }
       o += "# TYPE hola_loop_poll_gaps_total counter\n";
       static const char* const kOver[EventLoop::kGapBuckets] = {"100us", "1ms", "10ms"};
       for (int k = 0; k < EventLoop::kGapBuckets; ++k)

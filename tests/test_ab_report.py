@@ -53,3 +53,23 @@ def test_pair_layout_without_sibling_load_uses_the_two_group_fit(tmp_path):
 def test_t_quantile_is_conservative_between_table_rows():
     assert ab_report.t95(11) == ab_report.t95(10)
     assert ab_report.t95(100) == ab_report.t95(30)
+
+
+def test_instruction_counts_lead_the_efficiency_report(tmp_path):
+    """with the servers' hardware-counter figures present, the report
+    gives their paired delta first (raw CPU us/request of two saturated peers is the same
+    number on both sides by construction)."""
+    for i in range(1, 5):
+        for label, instr in (("a", 1400.0), ("b", 1330.0 + i)):
+            line = {"value": 4.5e6, "server_cpu_us_per_req": 1.72, "server_busy_cpu_us_per_req": 1.71,
+                    "server_user_instr_per_req": instr, "server_user_cycles_per_req": 900.0,
+                    "host_load": [{"siblings": 0.0}]}
+            (tmp_path / f"{label}_{i}.json").write_text(json.dumps(line) + "\n")
+    out = tmp_path / "r.json"
+    r = subprocess.run([sys.executable, str(ROOT / "bench/ab_report.py"), str(tmp_path), "--baseline", "a",
+                        "--candidate", "b", "--json", str(out)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr
+    res = json.loads(out.read_text())
+    assert res["server_user_instr_per_req_delta_pct"]["mean"] == pytest.approx(100 * (1332.5 - 1400) / 1400, abs=0.01)
+    lines = [ln for ln in r.stdout.splitlines() if "%" in ln and "CI" in ln]
+    assert "instr/req" in lines[0]
