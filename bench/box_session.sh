@@ -19,6 +19,7 @@
 #   pairmode           N = 1, 2, 4 with --smt pair (the 8-GPU node's per-replica layout shape)
 #   latency            BASELINE config 2 (1 connection) and the open-loop latency curve
 #   chain              two-hop chaining bench (loadgen -> hola A -> hola B)
+#   tails              open-loop latency curves (auto x3, off x1) with per-point tail attribution
 #   deployedab REPS [ARGS]  headline replica vs as-deployed (ZIPKIN_SERVER_URL as deployed /
 #                      unset / native sink), interleaved (bench/deployed_ab.py)
 #   chainwork          instructions per chained request (this tree, r5end, r4end) and user-cycles
@@ -190,6 +191,16 @@ latency)
 chain)
   timeout -k 10 120 python bench/chain_bench.py --duration 10 --out "$OUT/chain.json" > "$OUT/chain.log" 2>&1
   ;;
+tails)
+  # open-loop curves of the shipped default (auto) three times and one
+  # with busy-polling off, each point with its tail attribution (bench/latency_curve.py)
+  info
+  for k in ${CURVES:-auto1 auto2 off auto3}; do
+    bp=auto; [ "${k#off}" != "$k" ] && bp=0
+    timeout -k 10 200 python bench/latency_curve.py --duration 6 --server-busy-poll "$bp" \
+      --out "$OUT/curve_$k.json" > "$OUT/curve_$k.log" 2>&1 || exit $?
+  done
+  ;;
 deployedab)
   REPS=${1:-4}; shift || true
   timeout -k 10 1000 python -u bench/deployed_ab.py --reps "$REPS" --out "$OUT" "$@" > "$OUT/deployed_ab.log" 2>&1
@@ -200,11 +211,15 @@ chainwork)
   # remaining own-code cycles are) with the raw profile kept for address resolution
   info
   timeout -k 10 600 python -u bench/instr_ab.py "$OUT/instr" head=build/release/hola r5end=build/r5end/hola \
-    r4end=build/r4end/hola --chain --rounds "${ROUNDS:-3}" > "$OUT/instr.log" 2>&1 &&
+    ${SIDES:-r4end=build/r4end/hola} --chain --rounds "${ROUNDS:-3}" > "$OUT/instr.log" 2>&1 &&
   HOLA_CPUPROF_EVENT=user-cycles timeout -k 10 120 python bench/chain_bench.py --duration 8 \
     --cpu-profile "$OUT/chain_a_user.prof" --out "$OUT/chain_user.json" > "$OUT/chain_user.log" 2>&1 &&
   python bench/cpuprof_report.py "$OUT/chain_a_user.prof" --top 60 --json "$OUT/chain_user_report.json" \
     > "$OUT/chain_user_report.txt" 2>> "$OUT/err.log" &&
+  HOLA_CPUPROF_EVENT=user-instructions timeout -k 10 120 python bench/chain_bench.py --duration 8 \
+    --cpu-profile "$OUT/chain_a_instr.prof" --out "$OUT/chain_instr.json" > "$OUT/chain_instr.log" 2>&1 &&
+  python bench/cpuprof_report.py "$OUT/chain_a_instr.prof" --top 80 --json "$OUT/chain_instr_report.json" \
+    > "$OUT/chain_instr_report.txt" 2>> "$OUT/err.log" &&
   timeout -k 10 120 python bench/chain_bench.py --duration 8 --cpu-profile "$OUT/chain_a.prof" \
     --out "$OUT/chain.json" > "$OUT/chain.log" 2>&1 &&
   python bench/cpuprof_report.py "$OUT/chain_a.prof" --top 60 --json "$OUT/chain_report.json" \

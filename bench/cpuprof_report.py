@@ -32,7 +32,7 @@ def parse(path: str) -> dict:
                 continue
             if parts[0] in ("period_ns", "samples", "dropped", "period_cycles"):
                 prof[parts[0]] = int(parts[1])
-            elif parts[0] == "event":  # HOLA_CPUPROF_EVENT=user-cycles
+            elif parts[0] == "event":  # HOLA_CPUPROF_EVENT=user-cycles / user-instructions
                 prof["event"] = parts[1]
             elif parts[0] == "thread":
                 prof["threads"][int(parts[1])] = parts[2] if len(parts) > 2 else "?"
@@ -167,9 +167,10 @@ def main() -> int:
     a = ap.parse_args()
     rep = report(parse(a.profile), a.top, a.threads)
     prof = parse(a.profile)
-    if prof["event"] == "user-cycles":
-        print(f"{rep['samples']} samples of {prof['period_cycles']} user-space cycles each "
-              f"({rep['samples'] * prof['period_cycles'] / 1e9:.2f} G cycles) of threads '{a.threads or '*'}'; "
+    if prof["event"] in ("user-cycles", "user-instructions"):
+        unit = prof["event"].split("-", 1)[1]
+        print(f"{rep['samples']} samples of {prof['period_cycles']} user-space {unit} each "
+              f"({rep['samples'] * prof['period_cycles'] / 1e9:.2f} G {unit}) of threads '{a.threads or '*'}'; "
               f"dropped {rep['dropped']}")
     else:
         cpu_s = rep["samples"] * rep["period_ns"] / 1e9

@@ -1,5 +1,7 @@
 #include "app/hola_app.h"
 
+#include <charconv>
+
 #include <cstring>
 #include <deque>
 
@@ -62,9 +64,6 @@ struct HolaApp::WorkerCache {
   // "Content-Length: " per keep-alive mode, and the body's `["<greeting>"` prefix.
   std::string chain_head[2];
   std::string chain_json_prefix;
-  // Success responses of /api/hola-chaining are assembled here (capacity kept between calls;
-  // Connection::complete copies the bytes before anything else can run on this worker).
-  std::string chain_resp;
 };
 
 const char* HolaApp::route_name(int r) {
@@ -404,11 +403,11 @@ void HolaApp::on_request(http::Connection& c, const http::Request& r) {
                           tracer_->enabled();
       auto send_traced = [&](std::string_view resp, int status) {
         if (!traced) {
-          c.send(resp);
+          c.send_stable(resp);
           return;
         }
         tracing::ServerSpan span = tracer_->begin_server(w.index(), r);
-        c.send(resp);
+        c.send_stable(resp);
         tracer_->end_server(w.index(), span, status);
       };
       if (m == Method::kOptions) {
@@ -429,40 +428,40 @@ void HolaApp::on_request(http::Connection& c, const http::Request& r) {
       if (route == kHola) {
         if (traced) {
           tracing::ServerSpan span = tracer_->begin_server(w.index(), r);
-          c.send(wc.hola[ka][head].view());
+          c.send_stable(wc.hola[ka][head].view());
           tracer_->end_server(w.index(), span, wc.content && wc.content->ok ? 200 : 500);
         } else {
-          c.send(wc.hola[ka][head].view());
+          c.send_stable(wc.hola[ka][head].view());
         }
       } else if (route == kHealth) {
         // Readiness fails from the first termination signal on (--shutdown-delay-ms): the
         // Service stops routing new connections here while this replica still serves.
-        c.send((w.server().terminating() ? wc.health_unready : wc.health)[ka][head].view());
+        c.send_stable((w.server().terminating() ? wc.health_unready : wc.health)[ka][head].view());
       } else if (route == kSwagger) {
-        c.send(wc.swagger[ka][head].view());
+        c.send_stable(wc.swagger[ka][head].view());
       } else if (route == kSwaggerYaml) {
-        c.send(wc.swagger_yaml[ka][head].view());
+        c.send_stable(wc.swagger_yaml[ka][head].view());
       } else {
         handle_chaining(c, r, wc, traced);
       }
       return;
     }
     case kApiNotFound:
-      c.send(wc.api_not_found[ka].view());
+      c.send_stable(wc.api_not_found[ka].view());
       return;
     case kIndex:
     case kViewer:
-      if (m == Method::kOptions) c.send(wc.static_options[ka].view());
-      else if (m == Method::kOther) c.send(wc.not_allowed[ka].view());
-      else c.send((route == kIndex ? wc.index : wc.viewer)[ka][head].view());
+      if (m == Method::kOptions) c.send_stable(wc.static_options[ka].view());
+      else if (m == Method::kOther) c.send_stable(wc.not_allowed[ka].view());
+      else c.send_stable((route == kIndex ? wc.index : wc.viewer)[ka][head].view());
       return;
     case kHystrix:
       if (hystrix_ && m == Method::kGet) {
         hystrix_->subscribe(c, r);
       } else if (m == Method::kOther || m == Method::kOptions || !hystrix_) {
-        c.send(hystrix_ ? wc.not_allowed[ka].view() : wc.not_found[ka][head].view());
+        c.send_stable(hystrix_ ? wc.not_allowed[ka].view() : wc.not_found[ka][head].view());
       } else {
-        c.send(wc.not_found[ka][head].view());  // HEAD on a stream: nothing to describe
+        c.send_stable(wc.not_found[ka][head].view());  // HEAD on a stream: nothing to describe
       }
       return;
     case kMetrics:
@@ -475,11 +474,11 @@ void HolaApp::on_request(http::Connection& c, const http::Request& r) {
         s.body = body;
         c.send(build_response(s, w.date()).view());
       } else {
-        c.send(wc.not_found[ka][head].view());
+        c.send_stable(wc.not_found[ka][head].view());
       }
       return;
     default:
-      c.send(wc.not_found[ka][head].view());
+      c.send_stable(wc.not_found[ka][head].view());
       return;
   }
 }
@@ -491,7 +490,7 @@ void HolaApp::handle_chaining(http::Connection& c, const http::Request& r, Worke
   if (traced) span = tracer_->begin_server(c.worker().index(), r);
   if (!wc.content || !wc.content->ok) {
     // hola() throws before the downstream call is made (HolaResource.java:75)
-    c.send(wc.server_error[ka][head].view());
+    c.send_stable(wc.server_error[ka][head].view());
     if (traced) tracer_->end_server(c.worker().index(), span, 500);
     return;
   }
@@ -500,7 +499,7 @@ void HolaApp::handle_chaining(http::Connection& c, const http::Request& r, Worke
   // short-circuit is, counts the pass's own handling time as 0)
   const int64_t t0 = loop_now_ns();
   if (!chainer_) {
-    c.send(wc.chaining_fallback[ka][head].view());
+    c.send_stable(wc.chaining_fallback[ka][head].view());
     if (traced) tracer_->end_server(c.worker().index(), span, 200);
     if (prom_) prom_->observe_chaining_us(c.worker().index(), uint64_t(loop_now_ns() - t0) / 1000);
     return;
@@ -509,89 +508,104 @@ void HolaApp::handle_chaining(http::Connection& c, const http::Request& r, Worke
   c.park();
   http::ConnRef conn(&c);  // held until the callback is gone, run or not
   const uint64_t cgen = wc.gen;  // the request's configuration (see WorkerCache::retired)
-  HolaApp* self = this;
-  chainer_->call(c.worker(), traced ? &span.ctx : nullptr,
-                 // conn is moved in; the content is named by its generation (a shared_ptr copy
-                 // is two locked read-modify-writes per request, each draining the store buffer)
-                 [self, conn = std::move(conn), cgen, ka_req = ka, head, traced, span, t0](const ChainResult& res) {
-                   http::Worker& w = conn->worker();
-                   // termination may have begun while the call was parked
-                   const int ka = ka_req && !w.server().closing() ? 1 : 0;
-                   WorkerCache& wc = self->cache(w);
-                   bool answered = false;
-                   if (!conn->closed() && (res.null_list || res.error)) {
-                     // greetings.addAll(null) throws after a successful command, and with
-                     // fallbacks disabled HystrixRuntimeException escapes aloha(): a 500.
-                     if (wc.gen != self->gen_.load(std::memory_order_relaxed) || wc.date_version != w.date_version())
-                       self->refresh(w, wc);
-                     conn->complete(wc.server_error[ka][head].view(), ka);
-                     if (traced) self->tracer_->end_server(w.index(), span, 500);
-                     if (self->prom_) self->prom_->observe_chaining_us(w.index(), uint64_t(loop_now_ns() - t0) / 1000);
-                     return;
-                   }
-                   if (!conn->closed() && res.fallback) {
-                     // The prepared ["<greeting>","Aloha response (fallback)"] response, if the
-                     // configuration has not changed since the request arrived.
-                     if (wc.gen != self->gen_.load(std::memory_order_relaxed) || wc.date_version != w.date_version())
-                       self->refresh(w, wc);
-                     if (wc.gen == cgen) {
-                       conn->complete(wc.chaining_fallback[ka][head].view(), ka);
-                       answered = true;
-                     }
-                   }
-                   if (!answered && !conn->closed() && wc.gen == cgen && !wc.chain_json_prefix.empty()) {
-                     // One allocation: [greeting, ...aloha] written straight into the response.
-                     if (wc.gen != self->gen_.load(std::memory_order_relaxed) || wc.date_version != w.date_version())
-                       self->refresh(w, wc);
-                     if (wc.gen == cgen) {
-                       size_t body_len = wc.chain_json_prefix.size() + 1;
-                       for (auto& it : res.items) body_len += 1 + (it ? it->size() + 2 : 4);
-                       std::string& resp = wc.chain_resp;
-                       resp.clear();
-                       resp.reserve(wc.chain_head[ka].size() + 48 + body_len + 16);
-                       resp += wc.chain_head[ka];
-                       const size_t len_at = resp.size();
-                       resp += "\r\nDate: ";
-                       resp.append(w.date(), 29);
-                       resp += "\r\n\r\n";
-                       const size_t body_at = resp.size();
-                       resp += wc.chain_json_prefix;
-                       for (auto& it : res.items) {
-                         resp += ',';
-                         if (it) json::append_string(&resp, *it);
-                         else resp += "null";
-                       }
-                       resp += ']';
-                       // Content-Length goes in front of the Date line now that the body is known.
-                       std::string len = std::to_string(resp.size() - body_at);
-                       resp.insert(len_at, len);
-                       if (head) resp.resize(body_at + len.size());
-                       conn->complete(resp, ka);
-                       answered = true;
-                     }
-                   }
-                   if (!answered && !conn->closed()) {
-                     // the configuration changed while the call was parked: the greeting of the
-                     // request's own configuration (the current one if that was retired long ago)
-                     const Content* own = wc.alive(cgen);
-                     if (!own) own = wc.content.get();
-                     std::vector<std::optional<std::string>> items;
-                     items.reserve(1 + res.items.size());
-                     if (own) items.push_back(own->greeting);
-                     else items.push_back(std::nullopt);
-                     for (auto& s : res.items) items.push_back(s);
-                     std::string body = json::string_array(items);
-                     ResponseSpec s;
-                     s.keep_alive = ka;
-                     s.head = head;
-                     s.cors = true;
-                     s.content_type = kJson;
-                     s.body = body;
-                     conn->complete(build_response(s, w.date()).view(), ka);
-                   }
-                   if (traced) self->tracer_->end_server(w.index(), span, 200);
-                   if (self->prom_) self->prom_->observe_chaining_us(w.index(), uint64_t(loop_now_ns() - t0) / 1000);
-                 });
+  // The continuation captures the server span only when it is recorded (a collector is
+  // configured): without one end_server() does nothing, and the ~200-byte span would be
+  // copied into the callback and moved into the call's slot for nothing.
+  if (span.record) {
+    chainer_->call(c.worker(), &span.ctx,
+                   [this, conn = std::move(conn), cgen, ka, head, span, t0](const ChainResult& res) {
+                     finish_chaining(conn, cgen, ka, head, &span, t0, res);
+                   });
+  } else {
+    chainer_->call(c.worker(), traced ? &span.ctx : nullptr,
+                   [this, conn = std::move(conn), cgen, ka, head, t0](const ChainResult& res) {
+                     finish_chaining(conn, cgen, ka, head, nullptr, t0, res);
+                   });
+  }
+}
+
+// The answer to a parked /api/hola-chaining request, once aloha answered, timed out or was
+// short-circuited. `conn` names the request's configuration by its generation `cgen` (a
+// shared_ptr copy is two locked read-modify-writes per request, each draining the store
+// buffer); `span` is the recorded server span, if any.
+void HolaApp::finish_chaining(const http::ConnRef& conn, uint64_t cgen, int ka_req, int head,
+                              const tracing::ServerSpan* span, int64_t t0, const ChainResult& res) {
+  http::Worker& w = conn->worker();
+  // termination may have begun while the call was parked
+  const int ka = ka_req && !w.server().closing() ? 1 : 0;
+  WorkerCache& wc = cache(w);
+  bool answered = false;
+  if (!conn->closed() && (res.null_list || res.error)) {
+    // greetings.addAll(null) throws after a successful command, and with
+    // fallbacks disabled HystrixRuntimeException escapes aloha(): a 500.
+    if (wc.gen != gen_.load(std::memory_order_relaxed) || wc.date_version != w.date_version())
+      refresh(w, wc);
+    conn->complete(wc.server_error[ka][head].view(), ka);
+    if (span) tracer_->end_server(w.index(), *span, 500);
+    if (prom_) prom_->observe_chaining_us(w.index(), uint64_t(loop_now_ns() - t0) / 1000);
+    return;
+  }
+  if (!conn->closed() && res.fallback) {
+    // The prepared ["<greeting>","Aloha response (fallback)"] response, if the
+    // configuration has not changed since the request arrived.
+    if (wc.gen != gen_.load(std::memory_order_relaxed) || wc.date_version != w.date_version())
+      refresh(w, wc);
+    if (wc.gen == cgen) {
+      conn->complete(wc.chaining_fallback[ka][head].view(), ka);
+      answered = true;
+    }
+  }
+  if (!answered && !conn->closed() && wc.gen == cgen && !wc.chain_json_prefix.empty()) {
+    // [greeting, ...aloha] written straight into the connection's output
+    // buffer, its exact length first (no intermediate copy, no insert)
+    if (wc.gen != gen_.load(std::memory_order_relaxed) || wc.date_version != w.date_version())
+      refresh(w, wc);
+    if (wc.gen == cgen) {
+      size_t body_len = wc.chain_json_prefix.size() + 1;
+      for (auto& it : res.items) body_len += 1 + (it ? json::quoted_size(*it) : 4);
+      char len[24];
+      const size_t len_n = size_t(std::to_chars(len, len + sizeof len, body_len).ptr - len);
+      std::string& out = conn->response_buffer();
+      out.reserve(out.size() + wc.chain_head[ka].size() + len_n + 39 + (head ? 0 : body_len));
+      out += wc.chain_head[ka];
+      out.append(len, len_n);
+      out += "\r\nDate: ";
+      out.append(w.date(), 29);
+      out += "\r\n\r\n";
+      if (!head) {
+        out += wc.chain_json_prefix;
+        for (auto& it : res.items) {
+          out += ',';
+          if (it) json::append_string(&out, *it);
+          else out += "null";
+        }
+        out += ']';
+      }
+      conn->complete_appended(ka);
+      answered = true;
+    }
+  }
+  if (!answered && !conn->closed()) {
+    // the configuration changed while the call was parked: the greeting of the
+    // request's own configuration (the current one if that was retired long ago)
+    const Content* own = wc.alive(cgen);
+    if (!own) own = wc.content.get();
+    std::vector<std::optional<std::string>> items;
+    items.reserve(1 + res.items.size());
+    if (own) items.push_back(own->greeting);
+    else items.push_back(std::nullopt);
+    for (auto& s : res.items) items.push_back(s);
+    std::string body = json::string_array(items);
+    ResponseSpec s;
+    s.keep_alive = ka;
+    s.head = head;
+    s.cors = true;
+    s.content_type = kJson;
+    s.body = body;
+    conn->complete(build_response(s, w.date()).view(), ka);
+  }
+  if (span) tracer_->end_server(w.index(), *span, 200);
+  if (prom_) prom_->observe_chaining_us(w.index(), uint64_t(loop_now_ns() - t0) / 1000);
 }
 
 }  // namespace hola::app

@@ -21,6 +21,7 @@
 
 namespace hola::tracing {
 class Tracer;
+struct ServerSpan;
 }
 namespace hola::metrics {
 class HystrixStream;
@@ -30,6 +31,7 @@ class Prometheus;
 namespace hola::app {
 
 class Chainer;
+struct ChainResult;
 
 struct AppOptions {
   std::string hostname = "unknown";  // $HOSTNAME (HolaResource.java:57)
@@ -88,6 +90,8 @@ class HolaApp final : public http::RequestHandler {
   void refresh(http::Worker& w, WorkerCache& wc);
   // `traced`: the request matched ZipKinFilter's servlet pattern (server span around it).
   void handle_chaining(http::Connection& c, const http::Request& r, WorkerCache& wc, bool traced);
+  void finish_chaining(const http::ConnRef& conn, uint64_t cgen, int ka_req, int head, const tracing::ServerSpan* span,
+                       int64_t t0, const ChainResult& res);
 
   AppOptions o_;
   http::Server* server_ = nullptr;

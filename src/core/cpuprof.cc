@@ -280,8 +280,11 @@ std::string describe_pcs(const uintptr_t* pcs, int n) {
 // signal is routed to the thread as SIGPROF (same handler, same stacks). The CPU-time profile
 // of a syscall-bound server is ~93 % send/recv/epoll_wait; this one shows only the server's
 // own work (and libc's). Threads fall back to the CPU-time timer where no PMU is present.
+// HOLA_CPUPROF_EVENT=user-instructions samples retired user-space instructions instead (same
+// period variable): where a request's instructions are, for instruction-count work.
 bool g_user_cycles = false;
 uint64_t g_cycles_period = 200000;
+uint64_t g_event_config = PERF_COUNT_HW_CPU_CYCLES;
 std::vector<int> g_event_fds;  // under g_mu
 thread_local int t_event_fd = -1;
 
@@ -290,7 +293,7 @@ int open_user_cycles() {
   memset(&a, 0, sizeof a);
   a.type = PERF_TYPE_HARDWARE;
   a.size = sizeof a;
-  a.config = PERF_COUNT_HW_CPU_CYCLES;
+  a.config = g_event_config;
   a.sample_period = g_cycles_period;
   a.wakeup_events = 1;
   a.exclude_kernel = 1;
@@ -312,8 +315,10 @@ bool start(const std::string& path, int hz) {
   if (g_on.load() || hz <= 0) return false;
   g_path = path;
   g_period_ns = 1000000000L / hz;
-  if (const char* e = getenv("HOLA_CPUPROF_EVENT"); e && strcmp(e, "user-cycles") == 0) {
+  if (const char* e = getenv("HOLA_CPUPROF_EVENT");
+      e && (strcmp(e, "user-cycles") == 0 || strcmp(e, "user-instructions") == 0)) {
     g_user_cycles = true;
+    if (strcmp(e, "user-instructions") == 0) g_event_config = PERF_COUNT_HW_INSTRUCTIONS;
     if (const char* p = getenv("HOLA_CPUPROF_PERIOD"); p && atoll(p) > 0) g_cycles_period = uint64_t(atoll(p));
   }
   g_samples.reset(new Sample[kCapacity]);
@@ -401,7 +406,9 @@ bool write() {
   std::ofstream f(g_path);
   if (!f) return false;
   f << "# hola cpu profile\n";
-  if (g_user_cycles && !g_event_fds.empty()) f << "event user-cycles\nperiod_cycles " << g_cycles_period << "\n";
+  if (g_user_cycles && !g_event_fds.empty())
+    f << "event " << (g_event_config == PERF_COUNT_HW_INSTRUCTIONS ? "user-instructions" : "user-cycles")
+      << "\nperiod_cycles " << g_cycles_period << "\n";
   f << "period_ns " << g_period_ns << "\nsamples " << n << "\ndropped "
     << (g_next.load() > kCapacity ? g_next.load() - kCapacity : 0) << "\n";
   {

@@ -230,6 +230,9 @@ bool Connection::process(const char* data, size_t len, size_t* consumed) {
     // Re-reading it after the handler would race with begin_termination() on another thread
     // and close a connection whose response had just announced keep-alive.
     const bool closing = worker_->server().closing();
+    // a pending prepared response is copied before the next handler runs: that handler may
+    // rebuild the prepared responses it points into (HolaApp::refresh)
+    materialize();
     if (prof) {
       int64_t th = mono_ns();
       h.on_request(*this, r);
@@ -255,11 +258,34 @@ void Connection::error_response(int status) {
 
 void Connection::send(const char* p, size_t n) {
   if (closed_) return;
+  materialize();
   out_.append(p, n);
   if (!in_process_) flush();
 }
 
+void Connection::send_stable(std::string_view s) {
+  if (closed_) return;
+  if (out_off_ == out_.size() && !stable_) {
+    out_.clear();
+    out_off_ = 0;
+    stable_ = s.data();
+    stable_len_ = s.size();
+  } else {
+    materialize();
+    out_.append(s.data(), s.size());
+  }
+  if (!in_process_) flush();
+}
+
 void Connection::complete(std::string_view response, bool keep_alive) {
+  if (!closed_) {
+    materialize();
+    out_.append(response.data(), response.size());
+  }
+  complete_appended(keep_alive);
+}
+
+void Connection::complete_appended(bool keep_alive) {
   if (closed_) {
     parked_ = false;
     return;
@@ -268,7 +294,6 @@ void Connection::complete(std::string_view response, bool keep_alive) {
   // keep_alive is what the response announced; the caller chose it with closing() (reading
   // the flag again here could close a connection whose response said keep-alive)
   if (!keep_alive) close_after_flush_ = true;
-  out_.append(response.data(), response.size());
   if (in_process_) return;
   // Continue with pipelined requests that arrived while parked.
   if (!in_.empty() && !close_after_flush_) {
@@ -297,6 +322,25 @@ void Connection::start_streaming(std::function<void()> on_close) {
 void Connection::flush() {
   WorkerStats& st = worker_->stats();
   StageProfile* prof = worker_->profile();
+  while (stable_) {  // a prepared response, sent from where it lives (out_ is empty)
+    int64_t ts = prof ? mono_ns() : 0;
+    ssize_t w = ::send(fd_, stable_, stable_len_, MSG_NOSIGNAL);
+    if (prof && w > 0) prof->send.add(uint64_t(mono_ns() - ts));
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      if (errno == EAGAIN) {
+        materialize();  // the socket is full: the rest waits in out_ (handled below)
+        break;
+      }
+      close();
+      return;
+    }
+    WorkerStats::bump(st.bytes_out, uint64_t(w));
+    sent_total_ += uint64_t(w);
+    stable_ += w;
+    stable_len_ -= size_t(w);
+    if (!stable_len_) stable_ = nullptr;
+  }
   while (out_off_ < out_.size()) {
     int64_t ts = prof ? mono_ns() : 0;
     ssize_t w = ::send(fd_, out_.data() + out_off_, out_.size() - out_off_, MSG_NOSIGNAL);
@@ -353,6 +397,8 @@ void Connection::update_interest() {
 void Connection::close() {
   if (closed_) return;
   closed_ = true;
+  stable_ = nullptr;
+  stable_len_ = 0;
   worker_->loop().del(fd_);
   ::close(fd_);
   fd_ = -1;

@@ -56,6 +56,11 @@ class Connection final : public EventLoop::Handler {
   // Queue response bytes (copied unless the socket takes them immediately). Order preserved.
   void send(const char* p, size_t n);
   void send(std::string_view s) { send(s.data(), s.size()); }
+  // The same for bytes in a buffer that stays unchanged until this connection's next handler
+  // runs (the worker's prepared responses): written to the socket from there, without the
+  // copy into the output buffer, when nothing else is queued before them. Whatever the socket
+  // does not take at once is copied, as are bytes queued behind other output.
+  void send_stable(std::string_view s);
   // After the current response: close the connection once all queued bytes are written.
   void close_after_response() { close_after_flush_ = true; }
 
@@ -64,6 +69,13 @@ class Connection final : public EventLoop::Handler {
   // what the response announces (false once the server is closing(); the caller decides).
   void park() { parked_ = true; }
   void complete(std::string_view response, bool keep_alive);
+  // complete() for a response written straight into the output buffer: append it to
+  // response_buffer() (nothing else may be queued in between), then call complete_appended().
+  std::string& response_buffer() {
+    materialize();
+    return out_;
+  }
+  void complete_appended(bool keep_alive);
 
   // Long-lived streaming responses (SSE): no further request parsing; `on_close` fires when
   // the peer goes away or close() is called.
@@ -86,12 +98,12 @@ class Connection final : public EventLoop::Handler {
   // Remote address (for tracing / logs).
   std::string peer() const;
   // Idle = no request in progress and nothing buffered either way.
-  bool idle() const { return !parked_ && in_.empty() && out_.size() == out_off_; }
+  bool idle() const { return !parked_ && in_.empty() && unsent() == 0; }
   // No response owed and nothing queued to send (a partial request may be buffered).
-  bool quiet() const { return !parked_ && out_.size() == out_off_; }
+  bool quiet() const { return !parked_ && unsent() == 0; }
   int64_t last_active_ms() const { return last_active_ms_; }
   // Bytes queued for this connection that the socket has not taken yet.
-  size_t unsent() const { return out_.size() - out_off_; }
+  size_t unsent() const { return out_.size() - out_off_ + stable_len_; }
   // Bytes the socket has taken over the connection's life.
   uint64_t bytes_sent() const { return sent_total_; }
   // The state published in the loop's activity record: flag bits, buffered input, unsent
@@ -105,6 +117,14 @@ class Connection final : public EventLoop::Handler {
   // Parses and dispatches buffered requests; returns false if the connection closed.
   bool process(const char* data, size_t len, size_t* consumed);
   void flush();
+  // Copies a pending send_stable() view into out_ (before anything else is queued).
+  void materialize() {
+    if (stable_) {
+      out_.append(stable_, stable_len_);
+      stable_ = nullptr;
+      stable_len_ = 0;
+    }
+  }
   void update_interest();
   void error_response(int status);
 
@@ -114,6 +134,9 @@ class Connection final : public EventLoop::Handler {
   std::string in_;   // unconsumed input carried across reads
   std::string out_;  // unsent output
   size_t out_off_ = 0;
+  // a send_stable() response not copied yet (out_ is empty while it is pending)
+  const char* stable_ = nullptr;
+  size_t stable_len_ = 0;
   uint64_t sent_total_ = 0;
   bool closed_ = false;
   bool parked_ = false;

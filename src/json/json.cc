@@ -39,6 +39,13 @@ void append_string(std::string* out, std::string_view s) {
   out->push_back('"');
 }
 
+size_t quoted_size(std::string_view s) {
+  size_t n = s.size() + 2;
+  for (unsigned char c : s)
+    if (needs_escape(c)) n += (c == '"' || c == '\\' || c == '\b' || c == '\f' || c == '\n' || c == '\r' || c == '\t') ? 1 : 5;
+  return n;
+}
+
 std::string quote(std::string_view s) {
   std::string r;
   append_string(&r, s);

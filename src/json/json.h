@@ -16,6 +16,9 @@ namespace hola::json {
 // Appends `s` as a JSON string literal (Jackson-style escaping: \" \\ \b \f \n \r \t, other
 // control characters as \u00XX, everything else — including non-ASCII UTF-8 — raw).
 void append_string(std::string* out, std::string_view s);
+// The length append_string() writes for `s` (quotes and escapes included): a response's
+// Content-Length before its body is written.
+size_t quoted_size(std::string_view s);
 std::string quote(std::string_view s);
 
 // Serialises a list of optional strings (nullopt -> null), compact: ["a","b"].

@@ -239,14 +239,17 @@ struct PyCommand {
 // admitted call completes (failing every `fail_every`-th, 0 = never), every other call takes
 // the fallback. Returns the callers' own tallies next to the Command's merged snapshot so
 // tests can check the sharded counters and the atomic bulkhead add up.
-py::dict hystrix_stress(int threads, int iters, int pool, int fail_every, int volume) {
+py::dict hystrix_stress(int threads, int iters, int pool, int fail_every, int volume, bool loop_clock) {
   resilience::Settings st;
   st.pool_core_size = pool;
   st.request_volume_threshold = volume;
-  st.health_snapshot_ms = 0;
+  st.health_snapshot_ms = loop_clock ? 500 : 0;  // as configured (500 ms), or a refresh per call
   st.sleep_window_ms = 1;
-  SystemClock clk;
-  resilience::Command cmd("stress", "g", "g", st, clk);
+  // loop_clock: a time that stays put, as the workers' loop clock does within a pass (no
+  // clock read per call: the cost of the command itself); else the system clock
+  FakeClock fake;
+  SystemClock sys;
+  resilience::Command cmd("stress", "g", "g", st, loop_clock ? static_cast<const Clock&>(fake) : sys);
   std::atomic<int64_t> runs{0}, fails{0}, shorts{0}, rejects{0};
   std::vector<std::thread> ts;
   {
@@ -602,7 +605,7 @@ PYBIND11_MODULE(_native, m) {
   m.def("log_raw_line", [](const std::string& s) { Logger::instance().raw_line(s); },
         "one raw line, no flush: it reaches stderr when the writer next drains");
   m.def("hystrix_stress", &hystrix_stress, py::arg("threads"), py::arg("iters"), py::arg("pool") = 10,
-        py::arg("fail_every") = 0, py::arg("volume") = 20);
+        py::arg("fail_every") = 0, py::arg("volume") = 20, py::arg("loop_clock") = false);
   py::class_<PyCommand>(m, "HystrixCommand")
       .def(py::init<const std::map<std::string, std::string>&>(), py::arg("props") = std::map<std::string, std::string>{})
       .def("try_start", &PyCommand::try_start, py::arg("ticket") = -1)
