@@ -3,6 +3,7 @@
 #include <cstdio>
 
 #include "config/properties.h"
+#include "core/scan.h"
 
 namespace hola::json {
 
@@ -12,10 +13,17 @@ constexpr bool needs_escape(unsigned char c) { return c < 0x20 || c == '"' || c 
 }  // namespace
 
 void append_string(std::string* out, std::string_view s) {
-  out->reserve(out->size() + s.size() + 2);
+  const size_t plain = json_plain_prefix(s.data(), s.size());
+  if (plain == s.size()) {  // nothing to escape (aloha's greetings): three appends
+    out->push_back('"');
+    out->append(s.data(), s.size());
+    out->push_back('"');
+    return;
+  }
+  out->reserve(out->size() + s.size() + 8);
   out->push_back('"');
   size_t run = 0;  // start of the pending run of characters copied verbatim
-  for (size_t i = 0; i < s.size(); ++i) {
+  for (size_t i = plain; i < s.size(); ++i) {
     unsigned char c = (unsigned char)s[i];
     if (!needs_escape(c)) continue;
     out->append(s.data() + run, i - run);
@@ -41,7 +49,8 @@ void append_string(std::string* out, std::string_view s) {
 
 size_t quoted_size(std::string_view s) {
   size_t n = s.size() + 2;
-  for (unsigned char c : s)
+  const size_t plain = json_plain_prefix(s.data(), s.size());
+  for (unsigned char c : s.substr(plain))
     if (needs_escape(c)) n += (c == '"' || c == '\\' || c == '\b' || c == '\f' || c == '\n' || c == '\r' || c == '\t') ? 1 : 5;
   return n;
 }
@@ -107,12 +116,7 @@ struct Parser {
     while (i < s.size()) {
       // the run of plain characters up to the next quote, escape or control character goes
       // in with one append (aloha's greetings have no escapes)
-      size_t run = i;
-      while (run < s.size()) {
-        const unsigned char u = static_cast<unsigned char>(s[run]);
-        if (u == '"' || u == '\\' || u < 0x20) break;
-        ++run;
-      }
+      const size_t run = i + json_plain_prefix(s.data() + i, s.size() - i);
       if (run != i) {
         out->append(s.data() + i, run - i);
         i = run;

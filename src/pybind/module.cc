@@ -32,6 +32,7 @@
 #include "core/log.h"
 #include "core/cpuprof.h"
 #include "core/inline_function.h"
+#include "core/scan.h"
 #include "http/server.h"
 
 #include <sys/socket.h>
@@ -554,6 +555,11 @@ PYBIND11_MODULE(_native, m) {
   m.def("decode_string_list_reusing", &decode_string_list_reusing_py);
   m.def("string_array", &string_array_py);
   m.def("json_quote", [](const std::string& s) { return py::bytes(json::quote(s)); });
+  m.def("json_quoted_size", [](const std::string& s) { return json::quoted_size(s); });
+  m.def("json_plain_prefix", [](py::bytes b) {
+    const std::string s = b;
+    return json_plain_prefix(s.data(), s.size());
+  });
   m.def("encode_span", &encode_spans_py, py::arg("v2"), py::arg("trace_id"), py::arg("span_id"),
         py::arg("parent") = py::none(), py::arg("kind") = "server", py::arg("start_us") = 1000,
         py::arg("end_us") = 2000, py::arg("url") = "http://localhost/api/hola", py::arg("status") = 200,

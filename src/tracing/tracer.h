@@ -38,6 +38,8 @@ namespace hola::tracing {
 constexpr size_t kMaxUrl = 112;
 
 struct ServerSpan {
+  // user-provided: `ServerSpan()` then leaves url[] as it is instead of zeroing all of it
+  ServerSpan() {}
   SpanContext ctx;
   int64_t start_us = 0;
   bool record = false;  // sampled: emit on end

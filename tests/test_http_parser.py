@@ -346,3 +346,14 @@ def test_client_response_parser_prefixes_and_whole(native, body, framing, interi
 def test_client_response_framing_cases(native, raw, body):
     rc, status, got, close, consumed, _ = native.client_parse_response(raw, True)
     assert (rc, status, got, consumed) == (1, 200, body, len(raw))
+
+
+@settings(max_examples=2000, deadline=None)
+@given(st.binary(max_size=80) | st.lists(st.sampled_from([b"a", b'"', b"\\", b"\x01", b"\x1f", b" ", b"\x7f",
+                                                          b"\xc3\xa9", b"\x80", b"Hola de "]), max_size=30).map(b"".join))
+def test_json_plain_prefix_matches_a_byte_loop(native, data):
+    """The SSE2 / word-at-a-time scan (src/core/scan.h) against the byte loop it replaced, at
+    every length around its 16- and 8-byte steps; and the encoder's size against its output."""
+    want = next((i for i, c in enumerate(data) if c < 0x20 or c in (0x22, 0x5C)), len(data))
+    assert native.json_plain_prefix(data) == want
+    assert native.json_quoted_size(data) == len(native.json_quote(data))
