@@ -233,6 +233,17 @@ podshape)
   timeout -k 10 900 python -u bench/pod_shape.py --reps "$REPS" --out "$OUT" "$@" > "$OUT/pod_shape.log" 2>&1 &&
   timeout -k 10 420 python bench.py > "$OUT/bench_default.json" 2>> "$OUT/err.log"
   ;;
+chainfinal)
+  # instructions per chained request (this tree, round 5's and round 4's
+  # servers), then bench.py's chain sub-run of each, interleaved with paired CIs, then the
+  # default bench
+  info
+  timeout -k 10 600 python -u bench/instr_ab.py "$OUT/instr" head=build/release/hola r5end=build/r5end/hola \
+    r4end=build/r4end/hola --chain --rounds "${ROUNDS:-3}" > "$OUT/instr.log" 2>&1 &&
+  timeout -k 10 900 python -u bench/chain_modes.py --reps "${REPS:-6}" --seconds 10 \
+    --variants lg0,lg0/r4end,lg0/r5end --out "$OUT/modes" > "$OUT/chain_modes.log" 2>&1 &&
+  timeout -k 10 420 python bench.py > "$OUT/bench_default.json" 2>> "$OUT/err.log"
+  ;;
 chainmodes)
   REPS=${1:-10}; shift || true
   timeout -k 10 1000 python -u bench/chain_modes.py --reps "$REPS" --out "$OUT" "$@" > "$OUT/chain_modes.log" 2>&1

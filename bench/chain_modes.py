@@ -79,6 +79,19 @@ def main() -> int:
         if x:
             summary[v] = {"n": len(x), "mean": statistics.mean(x), "min": min(x), "max": max(x),
                           "spread_pct": 100 * (max(x) - min(x)) / statistics.mean(x)}
+    # each variant against the first, paired by round (the order is swapped every round), with
+    # a 95 % t-interval: req/s and A's CPU per chained request
+    from ab_report import ci
+    base = variants[0]
+    for v in variants[1:]:
+        pairs = [(b, c) for b in rows for c in rows
+                 if b["variant"] == base and c["variant"] == v and b["rep"] == c["rep"] and "rps" in b and "rps" in c]
+        if len(pairs) < 2:
+            continue
+        for key in ("rps", "a_cpu_us_per_req"):
+            m, lo, hi = ci([100.0 * (c[key] - b[key]) / b[key] for b, c in pairs])
+            summary[v][f"{key}_vs_{base}_pct"] = {"mean": round(m, 2), "ci95": [round(lo, 2), round(hi, 2)],
+                                                  "pairs": len(pairs)}
     (out_dir / "summary.json").write_text(json.dumps(summary, indent=1))
     print(json.dumps(summary))
     return 0
