@@ -1,6 +1,9 @@
 #include "tracing/b3.h"
 
 #include <cstring>
+#if defined(__SSSE3__)
+#include <immintrin.h>
+#endif
 
 namespace hola::tracing {
 
@@ -37,11 +40,22 @@ bool parse_trace_id(std::string_view s, uint64_t* hi, uint64_t* lo) {
 }
 
 void hex64(uint64_t v, char out[16]) {
+#if defined(__SSSE3__)
+  // all 16 digits at once: the id's bytes in print order, split into nibbles, interleaved
+  // high/low, looked up in a 16-entry table with one shuffle (three ids per traced
+  // downstream call; the nibble loop was ~64 instructions each)
+  const __m128i x = _mm_cvtsi64_si128(int64_t(__builtin_bswap64(v)));
+  const __m128i mask = _mm_set1_epi8(0x0f);
+  const __m128i nib = _mm_unpacklo_epi8(_mm_and_si128(_mm_srli_epi16(x, 4), mask), _mm_and_si128(x, mask));
+  const __m128i lut = _mm_setr_epi8('0', '1', '2', '3', '4', '5', '6', '7', '8', '9', 'a', 'b', 'c', 'd', 'e', 'f');
+  _mm_storeu_si128(reinterpret_cast<__m128i*>(out), _mm_shuffle_epi8(lut, nib));
+#else
   static const char* d = "0123456789abcdef";
   for (int i = 15; i >= 0; --i) {
     out[i] = d[v & 15];
     v >>= 4;
   }
+#endif
 }
 
 std::string hex64(uint64_t v) {

@@ -4,6 +4,8 @@ import json
 import time
 
 import pytest
+from hypothesis import given, settings
+from hypothesis import strategies as st
 
 from hola_amd.testing.fakes import FakeAloha, FakeZipkin
 
@@ -343,3 +345,13 @@ def test_one_client_span_per_feign_attempt(hola, zipkin):
     # each attempt carried its own B3 span id downstream
     sent = [r["headers"].get("x-b3-spanid") for r in aloha.requests]
     assert sorted(sent) == sorted(sp["id"] for sp in client)
+
+
+@settings(max_examples=500, deadline=None)
+@given(st.integers(min_value=1, max_value=2**64 - 1), st.integers(min_value=1, max_value=2**64 - 1),
+       st.integers(min_value=0, max_value=2**64 - 1))
+def test_b3_inject_hex_matches_python(native, trace, span, parent):
+    """The shuffle-table hex encoder (src/tracing/b3.cc hex64) against Python's formatting."""
+    h = native.b3_inject(f"{trace:016x}", f"{span:016x}", parent=f"{parent:016x}")
+    assert f"X-B3-TraceId: {trace:016x}\r\n" in h and f"X-B3-SpanId: {span:016x}\r\n" in h
+    assert f"X-B3-ParentSpanId: {parent:016x}\r\n" in h
