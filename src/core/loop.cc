@@ -197,8 +197,6 @@ void EventLoop::run() {
   uint64_t passes = 0;
   while (!stop_.load(std::memory_order_relaxed)) {
     act_.passes.store(++passes, std::memory_order_relaxed);
-    set_phase(kTick);
-    if (tick_) tick_();
     set_phase(kWait);
     int n = 0;
     int wait_errno = 0;  // errno of a failed epoll_wait, taken before the clock reads below
@@ -255,6 +253,10 @@ void EventLoop::run() {
     now_ms_ = t / 1000000;
     now_ns_ = t;
     act_.pass_ns.store(t, std::memory_order_relaxed);
+    if (tick_) {  // after the wait: the pass's handlers see state as of its own time
+      set_phase(kTick);
+      tick_();
+    }
     if (n > 0) {
       set_phase(kEvents);
       for (int i = 0; i < n; ++i) static_cast<Handler*>(evs[i].data.ptr)->on_event(evs[i].events);

@@ -55,7 +55,8 @@ class EventLoop {
 
   // Millisecond monotonic time cached at the top of each iteration.
   int64_t now_ms() const { return now_ms_; }
-  // Called once per iteration before blocking (e.g. refresh cached Date header).
+  // Called once per iteration, after the wait and before the pass's events are handled
+  // (e.g. refresh the cached Date header as of the pass's time).
   void set_tick(std::function<void()> fn) { tick_ = std::move(fn); }
   // Optional callback when the loop exits run().
   void set_on_exit(std::function<void()> fn) { on_exit_ = std::move(fn); }

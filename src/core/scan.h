@@ -16,17 +16,20 @@
 
 namespace hola {
 
-inline const char* find_newline(const char* p, size_t avail) {
+template <char C>
+inline const char* find_byte(const char* p, size_t avail) {
 #if defined(__AVX2__)
   if (avail >= 32) {
     const __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(p));
-    const unsigned m = unsigned(_mm256_movemask_epi8(_mm256_cmpeq_epi8(v, _mm256_set1_epi8('\n'))));
+    const unsigned m = unsigned(_mm256_movemask_epi8(_mm256_cmpeq_epi8(v, _mm256_set1_epi8(C))));
     if (m) return p + __builtin_ctz(m);
-    return static_cast<const char*>(memchr(p + 32, '\n', avail - 32));
+    return static_cast<const char*>(memchr(p + 32, C, avail - 32));
   }
 #endif
-  return static_cast<const char*>(memchr(p, '\n', avail));
+  return static_cast<const char*>(memchr(p, C, avail));
 }
+
+inline const char* find_newline(const char* p, size_t avail) { return find_byte<'\n'>(p, avail); }
 
 }  // namespace hola
 

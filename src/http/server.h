@@ -257,6 +257,7 @@ class Worker {
   std::vector<char> scratch_;
   char date_[29];
   int64_t date_sec_ = 0;
+  int64_t next_date_check_ms_ = 0;  // loop time of the next Date refresh (Worker::tick)
   uint64_t date_version_ = 0;
   uint64_t next_conn_id_ = 1;
   size_t nconns_ = 0;

@@ -942,3 +942,18 @@ def test_exit_watchdog_reports_where_every_worker_is(hola):
     names = subprocess.run(["addr2line", "-f", "-C", "-e", exe, *[f"0x{o}" for o in own]],
                            capture_output=True, text=True).stdout
     assert re.search(r"^main$", names, re.M), names
+
+
+def test_date_header_is_current_after_an_idle_spell(hola):
+    """The worker refreshes its Date header after its wait, as of the pass's own time (every
+    4 ms of loop time at most): the first response after an idle spell carries the current
+    second, not the one from before the loop went to sleep."""
+    import email.utils
+
+    s = hola(threads=1, args=["--busy-poll-us", "0"])
+    st, h, _ = s.get("/api/health")
+    assert st == 200
+    time.sleep(2.5)
+    st, h, _ = s.get("/api/health")
+    sent = email.utils.parsedate_to_datetime(h["date"]).timestamp()
+    assert abs(sent - time.time()) < 1.5, h["date"]
