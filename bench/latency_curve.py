@@ -15,7 +15,8 @@ from pathlib import Path
 sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
 
 from hola_amd.parallel import subruns  # noqa: E402
-from hola_amd.parallel.hostmetrics import cgroup_cpu_stat, cpu_times, task_stats, task_stats_delta  # noqa: E402
+from hola_amd.parallel.hostmetrics import (busy_cpu_s, cgroup_cpu_stat, cpu_times, ksoftirqd_cpu_s,  # noqa: E402
+                                           task_stats, task_stats_delta)
 from hola_amd.parallel.loadgen import run_duration  # noqa: E402
 from hola_amd.server import HolaProcess  # noqa: E402
 from hola_amd.utils.cpu import format_cpu_list, plan_node, split_server_loadgen  # noqa: E402
@@ -54,10 +55,12 @@ with HolaProcess(args=server_args, env={"HOSTNAME": "h"}, threads=len(srv), cpu_
         # host load (IRQ time, siblings, L3 neighbours) of both sides, and the load
         # generator's own gaps and late sends
         m0, ts0, thr0, t0 = subruns.metrics_counters(s.port, probe=probe), task_stats(s.proc.pid), cgroup_cpu_stat(), cpu_times()
+        k0 = ksoftirqd_cpu_s(srv)
         r = run_duration([("127.0.0.1", s.port)], a.connections, len(lg), a.duration, 2.0,
                          cpu_list=",".join(map(str, lg)), rate=rate, busy_poll_us=a.busy_poll_us,
                          spin_us=a.spin_us, verify_body=True)
         m1, ts1, thr1, t1 = subruns.metrics_counters(s.port, probe=probe), task_stats(s.proc.pid), cgroup_cpu_stat(), cpu_times()
+        k1 = ksoftirqd_cpu_s(srv)
         c1 = resource.getrusage(resource.RUSAGE_CHILDREN)
         s1 = server_cpu()
         wall = a.duration + 2.0  # warmup included in both CPU figures
@@ -70,13 +73,23 @@ with HolaProcess(args=server_args, env={"HOSTNAME": "h"}, threads=len(srv), cpu_
                "loadgen_cpus_busy": round((c1.ru_utime + c1.ru_stime - c0.ru_utime - c0.ru_stime) / wall, 2),
                "server_loop": subruns.loop_block(m0, m1, reqs),
                "server_threads": task_stats_delta(ts0, ts1),
+               # what else ran on the replica's CPUs: their busy CPU-seconds less the replica's
+               # own (other tasks: kernel threads, other tenants), and the part of it that was
+               # ksoftirqd (softirq work deferred to a thread that preempts the worker)
+               "foreign_on_server_cpus_s": round(busy_cpu_s(t0, t1, srv) - (s1 - s0), 3),
+               "ksoftirqd_on_server_cpus_s": round(k1 - k0, 3),
+               # ... and on the load generator's CPUs (its own CPU from its rusage): a late
+               # send with other tasks there was this generator waiting for its CPU
+               "foreign_on_loadgen_cpus_s": round(busy_cpu_s(t0, t1, lg) - (c1.ru_utime + c1.ru_stime
+                                                                         - c0.ru_utime - c0.ru_stime), 3),
                "cgroup_throttle": {"periods": thr1.get("nr_periods", 0) - thr0.get("nr_periods", 0),
                                    "throttled_periods": thr1.get("nr_throttled", 0) - thr0.get("nr_throttled", 0),
                                    "throttled_ms": round((thr1.get("throttled_usec", 0) - thr0.get("throttled_usec", 0)) / 1e3, 1)},
                "host_load_server": subruns.host_load(t0, t1, srv, job),
                "host_load_loadgen": subruns.host_load(t0, t1, lg, job),
                "loadgen": {k: lat.get(k) for k in ("gaps_over_100us", "gaps_over_1ms", "gaps_over_10ms", "gap_max_ns",
-                                                   "send_late_max_ns", "blocking_waits")}}
+                                                   "send_late_max_ns", "sends_late_1ms", "behind_max_ns",
+                                                   "blocking_waits")}}
         rows.append(row)
         print(json.dumps(row), flush=True)
     probe.close()

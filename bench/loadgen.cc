@@ -133,6 +133,7 @@ struct Conn {
   bool busy = false;
   int64_t next_due = 0;   // --rate: intended send time of the next request
   int64_t intended = 0;   // --rate: intended send time of the in-flight request
+  int64_t free_at = 0;    // --rate: when its last response completed (free to send again)
 };
 
 struct ThreadState {
@@ -150,7 +151,10 @@ struct ThreadState {
   // empty polls, gaps between polls (event handling + descheduling) past 100 us / 1 ms /
   // 10 ms and the longest, and (open loop) the latest a scheduled send went out.
   uint64_t poll_hits = 0, spin_hits = 0, spin_misses = 0, blocking_waits = 0, idle_spin_ns = 0;
-  uint64_t gaps_over[3] = {}, gap_max_ns = 0, send_late_max_ns = 0;
+  // send_late: a scheduled request sent late although its connection was free at the due
+  // time (this generator's own delay); behind: late because the connection was still waiting
+  // for the server's previous response (the server's delay, passed on)
+  uint64_t gaps_over[3] = {}, gap_max_ns = 0, send_late_max_ns = 0, behind_max_ns = 0, sends_late_1ms = 0;
   // the thread's own user-space instructions and cycles (hardware counters, where allowed),
   // counted from the last reset
   ThreadCounters pmu;
@@ -484,7 +488,12 @@ void thread_main(ThreadState* ts, const Options* o) {
     for (auto& c : ts->conns) {
       if (c->busy) continue;
       if (c->next_due <= now) {
-        if (uint64_t(now - c->next_due) > ts->send_late_max_ns) ts->send_late_max_ns = uint64_t(now - c->next_due);
+        // late by the time since it was both due and free: the generator's own delay
+        const int64_t own = now - std::max(c->next_due, c->free_at);
+        if (uint64_t(own) > ts->send_late_max_ns) ts->send_late_max_ns = uint64_t(own);
+        if (own > 1000000) ++ts->sends_late_1ms;
+        if (c->free_at > c->next_due && uint64_t(c->free_at - c->next_due) > ts->behind_max_ns)
+          ts->behind_max_ns = uint64_t(c->free_at - c->next_due);
         c->intended = c->next_due;
         c->next_due += interval;
         if (!send_req(c.get(), o->pipeline)) ++ts->errors;
@@ -551,6 +560,7 @@ void thread_main(ThreadState* ts, const Options* o) {
         ts->pmu_reset();
         ts->poll_hits = ts->spin_hits = ts->spin_misses = ts->blocking_waits = ts->idle_spin_ns = 0;
         ts->gaps_over[0] = ts->gaps_over[1] = ts->gaps_over[2] = ts->gap_max_ns = ts->send_late_max_ns = 0;
+        ts->behind_max_ns = ts->sends_late_1ms = 0;
       }
       if (now >= end) break;
     }
@@ -671,6 +681,7 @@ void thread_main(ThreadState* ts, const Options* o) {
       }
       if (!close && c->inflight > 0) continue;  // the rest of the batch is still due
       c->busy = false;
+      c->free_at = now_rx;
       if (close) {
         epoll_ctl(ts->epfd, EPOLL_CTL_DEL, c->fd, nullptr);
         ::close(c->fd);
@@ -729,7 +740,8 @@ bool parse_targets(const std::string& s, std::vector<Target>* out) {
 std::string stats_json(std::vector<std::unique_ptr<ThreadState>>& ts, bool with_hist) {
   Histogram h;
   uint64_t errors = 0, non2xx = 0, reconnects = 0, checked = 0, mismatch = 0, alt = 0;
-  uint64_t poll_hits = 0, spin_hits = 0, spin_misses = 0, sleeps = 0, idle_ns = 0, gmax = 0, late = 0;
+  uint64_t poll_hits = 0, spin_hits = 0, spin_misses = 0, sleeps = 0, idle_ns = 0, gmax = 0, late = 0, behind = 0,
+           late_1ms = 0;
   uint64_t over[3] = {}, u_ins = 0, u_cyc = 0;
   bool pmu = false;
   for (auto& t : ts) {
@@ -754,6 +766,8 @@ std::string stats_json(std::vector<std::unique_ptr<ThreadState>>& ts, bool with_
     idle_ns += t->idle_spin_ns;
     gmax = std::max(gmax, t->gap_max_ns);
     late = std::max(late, t->send_late_max_ns);
+    behind = std::max(behind, t->behind_max_ns);
+    late_1ms += t->sends_late_1ms;
     for (int k = 0; k < 3; ++k) over[k] += t->gaps_over[k];
   }
   char buf[704];
@@ -770,11 +784,11 @@ std::string stats_json(std::vector<std::unique_ptr<ThreadState>>& ts, bool with_
   snprintf(buf, sizeof buf,
            ",\"poll_hits\":%llu,\"spin_hits\":%llu,\"spin_misses\":%llu,\"blocking_waits\":%llu,"
            "\"idle_spin_ns\":%llu,\"gaps_over_100us\":%llu,\"gaps_over_1ms\":%llu,\"gaps_over_10ms\":%llu,"
-           "\"gap_max_ns\":%llu,\"send_late_max_ns\":%llu",
+           "\"gap_max_ns\":%llu,\"send_late_max_ns\":%llu,\"sends_late_1ms\":%llu,\"behind_max_ns\":%llu",
            (unsigned long long)poll_hits, (unsigned long long)spin_hits, (unsigned long long)spin_misses,
            (unsigned long long)sleeps, (unsigned long long)idle_ns, (unsigned long long)over[0],
            (unsigned long long)over[1], (unsigned long long)over[2], (unsigned long long)gmax,
-           (unsigned long long)late);
+           (unsigned long long)late, (unsigned long long)late_1ms, (unsigned long long)behind);
   s += buf;
   if (pmu) {
     snprintf(buf, sizeof buf, ",\"user_instructions\":%llu,\"user_cycles\":%llu", (unsigned long long)u_ins,
@@ -1109,6 +1123,7 @@ int main(int argc, char** argv) {
         t->pmu_reset();
         t->poll_hits = t->spin_hits = t->spin_misses = t->blocking_waits = t->idle_spin_ns = 0;
         t->gaps_over[0] = t->gaps_over[1] = t->gaps_over[2] = t->gap_max_ns = t->send_late_max_ns = 0;
+        t->behind_max_ns = t->sends_late_1ms = 0;
       }
       printf("{\"reset\":true}\n");
       fflush(stdout);

@@ -8,8 +8,13 @@ For every point with p99.9 above --threshold-us it names what the point's own re
              long, or the thread descheduled: then it also has involuntary switches)
   preempted  the replica's workers were switched out involuntarily (another task on their CPU)
   throttled  CFS bandwidth throttling of the cgroup (every thread stops until the next period)
-  late       the load generator sent a scheduled request more than 1 ms late (its own stall:
-             the latency is counted from the intended time, so it is charged to the server)
+  late       the load generator sent a scheduled request more than 1 ms late although its
+             connection was free at the due time: its own stall, which the open loop charges
+             to the server (latency is counted from the intended time)
+  behind     a connection was still waiting for the server's previous answer more than 1 ms
+             past the next request's due time (the server's delay)
+  foreign    other tasks (kernel threads, other tenants) used the replica's CPUs for more
+             than 1 % of the point; ksoftirqd is named apart (lg-foreign: the load generator's)
   lg-gaps    the load generator's threads went more than 1 ms between polls
   irq/steal  interrupt or hypervisor time on the replica's CPUs above 5 %
   neighbours other tenants on the SMT siblings or elsewhere in the L3 above 5 %
@@ -37,7 +42,16 @@ def causes(row: dict) -> list[str]:
         out.append(f"throttled({thr['throttled_periods']} periods, {thr.get('throttled_ms', 0)} ms)")
     lg = row.get("loadgen", {})
     if (lg.get("send_late_max_ns") or 0) > 1_000_000:
-        out.append(f"late({lg['send_late_max_ns'] / 1e3:.0f} us)")
+        n = lg.get("sends_late_1ms")
+        out.append(f"late({lg['send_late_max_ns'] / 1e3:.0f} us" + (f", {n} sends >1ms" if n is not None else "") + ")")
+    if (lg.get("behind_max_ns") or 0) > 1_000_000:
+        out.append(f"behind({lg['behind_max_ns'] / 1e3:.0f} us)")
+    fs, ks = row.get("foreign_on_server_cpus_s"), row.get("ksoftirqd_on_server_cpus_s")
+    if fs is not None and fs > 0.01 * 8:  # 1 % of 8 CPUs over the 8 s point
+        out.append(f"foreign({fs:.2f} CPU-s" + (f", ksoftirqd {ks:.2f}" if ks else "") + ")")
+    fl = row.get("foreign_on_loadgen_cpus_s")
+    if fl is not None and fl > 0.01 * 8:
+        out.append(f"lg-foreign({fl:.2f} CPU-s)")
     if lg.get("gaps_over_1ms", 0):
         out.append(f"lg-gaps({lg['gaps_over_1ms']} >1ms, max {lg.get('gap_max_ns', 0) / 1e3:.0f} us)")
     hl = row.get("host_load_server", {})

@@ -180,6 +180,29 @@ def steal_fraction(t0: dict, t1: dict, cpus) -> float | None:
     return _share(t0, t1, cpus, 3)
 
 
+def busy_cpu_s(t0: dict, t1: dict, cpus) -> float:
+    """CPU-seconds `cpus` were busy between two cpu_times() snapshots (any task, IRQs included)."""
+    tck = os.sysconf("SC_CLK_TCK")
+    return sum((t1[c][0] - t0[c][0]) - (t1[c][1] - t0[c][1]) for c in cpus if c in t0 and c in t1) / tck
+
+
+_KSOFTIRQD: dict[int, int] = {}
+
+
+def ksoftirqd_cpu_s(cpus) -> float:
+    """CPU-seconds used so far by the ksoftirqd threads of `cpus`: softirq work the kernel
+    deferred to a thread (it then preempts whatever runs on that CPU)."""
+    if not _KSOFTIRQD:
+        for comm in Path("/proc").glob("[0-9]*/comm"):
+            try:
+                name = comm.read_text().strip()
+            except OSError:
+                continue
+            if name.startswith("ksoftirqd/") and name[10:].isdigit():
+                _KSOFTIRQD[int(name[10:])] = int(comm.parent.name)
+    return sum(proc_cpu_s(_KSOFTIRQD[c]) for c in cpus if c in _KSOFTIRQD)
+
+
 def task_stats(pid: int) -> dict[str, dict]:
     """Per thread of `pid` (by comm): CPU seconds and voluntary / involuntary context switches
     (a thread that sleeps in epoll_wait and is woken switches voluntarily; one preempted by
