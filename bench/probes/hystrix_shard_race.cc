@@ -8,7 +8,10 @@
 // /metrics path). Under TSan any unsynchronised access is a report; under ASan a use after
 // free; in every build the event totals must add up and nothing may deadlock.
 //
-//   hola_hystrix_race [--iters N]     exit 0 = consistent, 1 = counts wrong
+// --per-thread runs the same with the per-thread bulkhead (Command::set_per_thread_bulkhead):
+// the workers' shares and their borrowing from each other under the same pressure.
+//
+//   hola_hystrix_race [--iters N] [--per-thread]     exit 0 = consistent, 1 = counts wrong
 #include <atomic>
 #include <chrono>
 #include <cstdio>
@@ -26,13 +29,18 @@ using hola::resilience::Settings;
 
 int main(int argc, char** argv) {
   int iters = 20000;
-  for (int i = 1; i + 1 < argc; ++i)
-    if (!strcmp(argv[i], "--iters")) iters = atoi(argv[i + 1]);
+  bool per_thread = false;
+  for (int i = 1; i < argc; ++i) {
+    if (!strcmp(argv[i], "--iters") && i + 1 < argc) iters = atoi(argv[i + 1]);
+    if (!strcmp(argv[i], "--per-thread")) per_thread = true;
+  }
   Settings s;
   s.health_snapshot_ms = 0;          // every call refreshes the snapshot: walks all shards
   s.request_volume_threshold = 1 << 30;  // keep the breaker closed: every call is admitted
   s.pool_core_size = 1 << 20;
+  if (per_thread) s.pool_core_size = 64;  // 4 slots per share: the workers borrow from each other
   Command cmd("aloha", "AlohaService", "AlohaService", s, hola::SystemClock::instance());
+  cmd.set_per_thread_bulkhead(per_thread);
 
   constexpr int kWorkers = 8;
   std::atomic<bool> stop{false};

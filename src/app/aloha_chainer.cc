@@ -54,6 +54,10 @@ AlohaChainer::AlohaChainer(AlohaOptions o, resilience::Settings s, int num_worke
   full_url_ = "http://" + target_.host + ":" + std::to_string(target_.port) + target_.base_path + o_.path;
   // HystrixFeign keys: command = o_.command_key, group (and pool) = target name (the URL).
   cmd_ = std::make_unique<Command>(o_.command_key, o_.url, o_.url, s, clock_);
+  // Every call starts and finishes on one worker's loop thread, and each worker has a metric
+  // shard of its own (up to 16): the per-thread bulkhead applies (large pools only, see
+  // Command::set_per_thread_bulkhead)
+  cmd_->set_per_thread_bulkhead(num_workers <= 16);
   timeout_ms_.store(s.timeout_enabled ? s.timeout_ms : 0);
   fallback_enabled_.store(s.fallback_enabled);
   read_timeout_armed_.store(read_timeout_for(s));

@@ -192,6 +192,7 @@ struct PyCommand {
   }
   bool cancel_queued(int64_t ticket) { return cmd->cancel_queued({uint64_t(ticket), 0}); }
   void release_slot() { cmd->release_slot(); }
+  void set_per_thread_bulkhead(bool on) { cmd->set_per_thread_bulkhead(on); }
   void queued_timeout(int64_t ms) { cmd->queued_timeout(ms); }
   int64_t queue_size() { return cmd->queue_size(); }
   void finish(const std::string& outcome, int64_t ms) {
@@ -240,7 +241,8 @@ struct PyCommand {
 // admitted call completes (failing every `fail_every`-th, 0 = never), every other call takes
 // the fallback. Returns the callers' own tallies next to the Command's merged snapshot so
 // tests can check the sharded counters and the atomic bulkhead add up.
-py::dict hystrix_stress(int threads, int iters, int pool, int fail_every, int volume, bool loop_clock) {
+py::dict hystrix_stress(int threads, int iters, int pool, int fail_every, int volume, bool loop_clock,
+                        bool per_thread) {
   resilience::Settings st;
   st.pool_core_size = pool;
   st.request_volume_threshold = volume;
@@ -251,6 +253,7 @@ py::dict hystrix_stress(int threads, int iters, int pool, int fail_every, int vo
   FakeClock fake;
   SystemClock sys;
   resilience::Command cmd("stress", "g", "g", st, loop_clock ? static_cast<const Clock&>(fake) : sys);
+  cmd.set_per_thread_bulkhead(per_thread);
   std::atomic<int64_t> runs{0}, fails{0}, shorts{0}, rejects{0};
   std::vector<std::thread> ts;
   {
@@ -611,13 +614,15 @@ PYBIND11_MODULE(_native, m) {
   m.def("log_raw_line", [](const std::string& s) { Logger::instance().raw_line(s); },
         "one raw line, no flush: it reaches stderr when the writer next drains");
   m.def("hystrix_stress", &hystrix_stress, py::arg("threads"), py::arg("iters"), py::arg("pool") = 10,
-        py::arg("fail_every") = 0, py::arg("volume") = 20, py::arg("loop_clock") = false);
+        py::arg("fail_every") = 0, py::arg("volume") = 20, py::arg("loop_clock") = false,
+        py::arg("per_thread") = false);
   py::class_<PyCommand>(m, "HystrixCommand")
       .def(py::init<const std::map<std::string, std::string>&>(), py::arg("props") = std::map<std::string, std::string>{})
       .def("try_start", &PyCommand::try_start, py::arg("ticket") = -1)
       .def("next_queued", &PyCommand::next_queued)
       .def("cancel_queued", &PyCommand::cancel_queued)
       .def("release_slot", &PyCommand::release_slot)
+      .def("set_per_thread_bulkhead", &PyCommand::set_per_thread_bulkhead)
       .def("queued_timeout", &PyCommand::queued_timeout)
       .def("queue_size", &PyCommand::queue_size)
       .def("finish", &PyCommand::finish)

@@ -3,6 +3,7 @@
 #include <sched.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdlib>
 
 namespace hola::resilience {
@@ -262,6 +263,13 @@ struct alignas(64) Command::Shard {
   RollingCounter counter, pool_counter;
   RollingPercentile exec_lat, total_lat;
   int64_t completed = 0;
+  // Per-thread bulkhead: slots charged to this share (its thread's calls, and slots other
+  // threads borrowed from it), on a line of its own; what this shard's thread borrowed from
+  // each other share, and how many of its calls in flight were admitted this way (both
+  // touched by the owning thread only).
+  alignas(64) std::atomic<int64_t> used{0};
+  std::array<int32_t, 16> borrowed{};
+  int64_t per_thread_inflight = 0;
   explicit Shard(const Settings& s)
       : counter(s.rolling_window_ms, s.rolling_buckets),
         pool_counter(s.rolling_window_ms, s.rolling_buckets),
@@ -297,12 +305,74 @@ void Command::hold_shard_for_test(int i, const std::function<void()>& while_held
   while_held();
 }
 
-Command::Shard& Command::shard() {
+int Command::shard_index() {
   // Threads are dealt shards round-robin on first use: one event-loop worker per shard up
   // to kShards workers, so shard mutexes are in practice uncontended.
   static std::atomic<unsigned> next{0};
   thread_local unsigned idx = next.fetch_add(1, std::memory_order_relaxed);
-  return *shards_[idx % kShards];
+  return int(idx % kShards);
+}
+
+bool Command::per_thread_mode(int64_t core) const {
+  return per_thread_.load(std::memory_order_relaxed) && core >= kPerThreadMinPool &&
+         !semaphore_.load(std::memory_order_relaxed) && max_queue_.load(std::memory_order_relaxed) <= 0;
+}
+
+Command::Admit Command::try_start_per_thread(int64_t now, int64_t core) {
+  const int si = shard_index();
+  Shard& sh = *shards_[size_t(si)];
+  auto share = [core](int j) { return core / kShards + (j < core % kShards ? 1 : 0); };
+  auto take = [](Shard& s, int64_t q) {
+    int64_t u = s.used.load(std::memory_order_relaxed);
+    while (u < q)
+      if (s.used.compare_exchange_weak(u, u + 1, std::memory_order_acq_rel, std::memory_order_relaxed)) return true;
+    return false;
+  };
+  int lender = -1;
+  bool ok = take(sh, share(si));
+  for (int k = 1; !ok && k < kShards; ++k) {
+    const int j = (si + k) % kShards;
+    if (take(*shards_[size_t(j)], share(j))) {
+      ok = true;
+      lender = j;
+    }
+  }
+  if (!ok) {
+    // every share is full: the pool is (SynchronousQueue, no waiting room)
+    std::lock_guard<ShardLock> g(sh.mu);
+    sh.counter.add(now, Event::kThreadPoolRejected);
+    sh.pool_counter.add(now, Event::kThreadPoolRejected);
+    return Admit::kRejected;
+  }
+  if (lender >= 0) ++sh.borrowed[size_t(lender)];
+  ++sh.per_thread_inflight;
+  const int64_t mine = sh.used.load(std::memory_order_relaxed);
+  // the pool's largest size, at least this share's count (a read of a line that is rarely
+  // written; snapshots raise it to the pool's total as they see it)
+  if (int64_t l = largest_.load(std::memory_order_relaxed); mine > l)
+    while (mine > l && !largest_.compare_exchange_weak(l, mine, std::memory_order_relaxed)) {
+    }
+  std::lock_guard<ShardLock> g(sh.mu);
+  sh.counter.update_max_concurrency(now, mine);
+  sh.pool_counter.update_max_concurrency(now, mine);
+  sh.pool_counter.add(now, Event::kSuccess);  // "threads executed"
+  return Admit::kRun;
+}
+
+void Command::release_in(Shard& sh) {
+  if (sh.per_thread_inflight > 0) {
+    // a per-thread admission: give a borrowed slot back to its lender first, else our own
+    --sh.per_thread_inflight;
+    for (size_t j = 0; j < sh.borrowed.size(); ++j)
+      if (sh.borrowed[j] > 0) {
+        --sh.borrowed[j];
+        shards_[j]->used.fetch_sub(1, std::memory_order_acq_rel);
+        return;
+      }
+    sh.used.fetch_sub(1, std::memory_order_acq_rel);
+    return;
+  }
+  release_slot();
 }
 
 HealthCounts Command::health_at(int64_t now) {
@@ -394,6 +464,8 @@ Command::Admit Command::try_start(const Queued* q) {
     sh.counter.add(now, Event::kShortCircuited);
     return Admit::kShortCircuited;
   }
+  if (const int64_t core = pool_core_.load(std::memory_order_relaxed); per_thread_mode(core))
+    return try_start_per_thread(now, core);
   const bool sem = semaphore_.load(std::memory_order_relaxed);
   int64_t active = active_.fetch_add(1, std::memory_order_acq_rel) + 1;
   if (sem) {
@@ -486,7 +558,7 @@ int64_t Command::queue_size() {
 }
 
 void Command::finish_in(Shard& sh, int64_t now, Event outcome, int64_t execute_ms) {
-  release_slot();
+  release_in(sh);
   if (!semaphore_.load(std::memory_order_relaxed)) ++sh.completed;  // tasks run on the pool
   sh.counter.add(now, outcome);
   if (outcome == Event::kSuccess || outcome == Event::kFailure) sh.exec_lat.add(now, execute_ms);
@@ -603,13 +675,26 @@ CommandSnapshot Command::snapshot() {
       s.cumulative[size_t(i)] += c[size_t(i)];
       pc[size_t(i)] += p[size_t(i)];
     }
-    s.rolling_max_concurrent = std::max(s.rolling_max_concurrent, sh->counter.max_concurrency(now));
-    s.pool_rolling_max_active = std::max(s.pool_rolling_max_active, sh->pool_counter.max_concurrency(now));
+    // per-thread bulkhead: each share records its own count, so the pool's maximum is
+    // bounded by their sum; one shared count: every shard records the pool's, take the max
+    if (per_thread_.load(std::memory_order_relaxed)) {
+      s.rolling_max_concurrent += sh->counter.max_concurrency(now);
+      s.pool_rolling_max_active += sh->pool_counter.max_concurrency(now);
+    } else {
+      s.rolling_max_concurrent = std::max(s.rolling_max_concurrent, sh->counter.max_concurrency(now));
+      s.pool_rolling_max_active = std::max(s.pool_rolling_max_active, sh->pool_counter.max_concurrency(now));
+    }
+    s.concurrent += sh->used.load(std::memory_order_relaxed);
     s.pool_completed += sh->completed;
     sh->exec_lat.accumulate(now, &exec_h, &exec_sum, &exec_n);
     sh->total_lat.accumulate(now, &total_h, &total_sum, &total_n);
   }
-  s.concurrent = active_.load(std::memory_order_relaxed);
+  s.concurrent += active_.load(std::memory_order_relaxed);
+  if (per_thread_.load(std::memory_order_relaxed)) {  // largest pool size as the snapshots see it
+    int64_t l = largest_.load(std::memory_order_relaxed);
+    while (s.concurrent > l && !largest_.compare_exchange_weak(l, s.concurrent, std::memory_order_relaxed)) {
+    }
+  }
   static const double kPcts[9] = {0, 25, 50, 75, 90, 95, 99, 99.5, 100};
   for (int i = 0; i < 9; ++i) {
     s.latency_execute[size_t(i)] = RollingPercentile::percentile_of(exec_h, exec_n, kPcts[i]);

@@ -203,6 +203,19 @@ class Command {
   // Short-circuit / rejection path: fallback (unless disabled) + total latency in one shard visit.
   void rejected(int64_t total_ms, bool with_fallback = true);
 
+  // Per-thread bulkhead (opt-in, for callers whose calls finish on the thread that started
+  // them: the event-loop workers). With a thread pool of kPerThreadMinPool or more and no
+  // queue, each thread's calls take slots from its own share of the pool (pool / 16 per
+  // shard) with a compare-and-swap on its own cache line; a thread whose share is used up
+  // borrows a slot from another share, so a call is still only rejected when every share is
+  // full, as with one shared count. The shared count was two contended read-modify-writes
+  // per call from every worker. In this mode the pool's rolling maximum concurrency is the
+  // sum of each share's maximum in the window (an upper bound of the pool's), and its
+  // largest size is taken when snapshots are read. Smaller pools (the reference's 10) and
+  // queued pools keep the one exact shared count.
+  static constexpr int64_t kPerThreadMinPool = 64;
+  void set_per_thread_bulkhead(bool on) { per_thread_.store(on, std::memory_order_relaxed); }
+
   bool circuit_open();            // evaluates health like HystrixCircuitBreaker.isOpen()
   HealthCounts health();
   CommandSnapshot snapshot();
@@ -217,8 +230,14 @@ class Command {
  private:
   struct Shard;
   static constexpr int kShards = 16;
-  Shard& shard();
+  static int shard_index();
+  Shard& shard() { return *shards_[size_t(shard_index())]; }
   void finish_in(Shard& sh, int64_t now, Event outcome, int64_t execute_ms);
+  // per-thread bulkhead (see set_per_thread_bulkhead)
+  std::atomic<bool> per_thread_{false};
+  bool per_thread_mode(int64_t core) const;
+  Admit try_start_per_thread(int64_t now, int64_t core);
+  void release_in(Shard& sh);
   void mark_success(int64_t now);
   bool is_open(int64_t now);
   bool allow_request(int64_t now);

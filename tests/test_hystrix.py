@@ -370,3 +370,39 @@ def test_concurrent_accounting_adds_up(native, fail_every):
         # no call fails, but bulkhead rejections count as errors in Hystrix's health counts:
         # the breaker may open only if some were rejected (8 threads share 4 slots)
         assert r["short_circuited"] == 0 or r["rejected"] > 0, r
+
+
+def test_per_thread_bulkhead_is_exact_for_one_thread(native):
+    """The per-thread bulkhead (Command::set_per_thread_bulkhead, pools of 64 or more): one
+    thread's share is pool / 16, and past it the thread borrows from the other shares, so it
+    can still hold the whole pool; the next call is rejected, as with one shared count."""
+    c = native.HystrixCommand({"hystrix.threadpool.default.coreSize": "100",
+                               "hystrix.command.default.circuitBreaker.requestVolumeThreshold": "1000000"})
+    c.set_per_thread_bulkhead(True)
+    assert [c.try_start() for _ in range(100)] == ["run"] * 100
+    assert c.try_start() == "rejected"
+    pool = json.loads(c.pool_json())
+    assert pool["currentActiveCount"] == 100 and pool["currentLargestPoolSize"] == 100
+    for _ in range(100):
+        c.finish("success", 1)
+    assert json.loads(c.pool_json())["currentActiveCount"] == 0
+    assert [c.try_start() for _ in range(100)] == ["run"] * 100  # every borrowed slot went back
+
+
+def test_per_thread_bulkhead_leaves_small_pools_shared(native):
+    """Below 64 slots (the reference's 10) the one shared, exact count stays in use."""
+    c = native.HystrixCommand({"hystrix.threadpool.default.coreSize": "10"})
+    c.set_per_thread_bulkhead(True)
+    assert [c.try_start() for _ in range(11)] == ["run"] * 10 + ["rejected"]
+
+
+@pytest.mark.parametrize("fail_every", [0, 3])
+def test_per_thread_bulkhead_accounting_adds_up(native, fail_every):
+    """Eight C++ threads on one command with the per-thread bulkhead: every call accounted
+    for, no slot left taken, and the pool never exceeded (borrowing included)."""
+    r = native.hystrix_stress(threads=8, iters=20000, pool=64, fail_every=fail_every, volume=1000000,
+                              per_thread=True)
+    ev = r["events"]
+    assert r["runs"] + r["short_circuited"] + r["rejected"] == 8 * 20000
+    assert ev.get("SUCCESS", 0) + ev.get("FAILURE", 0) == r["runs"] == r["completed"]
+    assert r["concurrent"] == 0 and 1 <= r["largest"] <= 64

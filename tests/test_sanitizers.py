@@ -342,7 +342,8 @@ def test_sanitized_exit_watchdog_stall_report(preset, tmp_path):
 
 
 @pytest.mark.parametrize("preset", ["release", "tsan", "asan"])
-def test_hystrix_shard_lock_held_while_refreshes_and_finishes_run(preset):
+@pytest.mark.parametrize("per_thread", [False, True])
+def test_hystrix_shard_lock_held_while_refreshes_and_finishes_run(preset, per_thread):
     """one Hystrix shard's test-and-set lock (released with a plain release
     store) held over and over while eight workers run try_start / complete / circuit_open with
     a health snapshot refreshed on every call (each refresh walks every shard and meets the
@@ -354,7 +355,9 @@ def test_hystrix_shard_lock_held_while_refreshes_and_finishes_run(preset):
     exe = build_dir(preset) / "hola_hystrix_race"
     wrapper = tsan_wrapper() if preset == "tsan" else []
     env = {**os.environ, **SAN_ENV.get(preset, {})}
-    r = subprocess.run([*wrapper, str(exe), "--iters", "20000" if preset == "release" else "4000"],
+    # per_thread: the per-thread bulkhead, 64 slots in 4-slot shares, so the workers borrow
+    r = subprocess.run([*wrapper, str(exe), "--iters", "20000" if preset == "release" else "4000"]
+                       + (["--per-thread"] if per_thread else []),
                        capture_output=True, text=True, timeout=300, env=env)
     assert "ThreadSanitizer" not in r.stderr and "AddressSanitizer" not in r.stderr, r.stderr[-6000:]
     assert "runtime error" not in r.stderr, r.stderr[-3000:]
