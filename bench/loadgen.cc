@@ -136,6 +136,21 @@ struct Conn {
   int64_t free_at = 0;    // --rate: when its last response completed (free to send again)
 };
 
+// A counter one polling thread raises and the control thread reads or zeroes between runs.
+struct Stat {
+  std::atomic<uint64_t> v{0};
+  operator uint64_t() const { return v.load(std::memory_order_relaxed); }
+  Stat& operator=(uint64_t x) {
+    v.store(x, std::memory_order_relaxed);
+    return *this;
+  }
+  void operator++() { v.fetch_add(1, std::memory_order_relaxed); }
+  void operator+=(uint64_t d) { v.fetch_add(d, std::memory_order_relaxed); }
+  void raise(uint64_t x) {
+    if (x > v.load(std::memory_order_relaxed)) v.store(x, std::memory_order_relaxed);
+  }
+};
+
 struct ThreadState {
   int index = 0;
   int epfd = -1;
@@ -150,22 +165,30 @@ struct ThreadState {
   // work at once / after spinning / spins that ran out, waits that could block, CPU spent in
   // empty polls, gaps between polls (event handling + descheduling) past 100 us / 1 ms /
   // 10 ms and the longest, and (open loop) the latest a scheduled send went out.
-  uint64_t poll_hits = 0, spin_hits = 0, spin_misses = 0, blocking_waits = 0, idle_spin_ns = 0;
+  // These are read ("stats") and zeroed ("reset") by the control thread while the thread may
+  // still be polling, so each is a relaxed atomic: counts are exact, a maximum raised in the
+  // same instant as a reset may survive it.
+  Stat poll_hits, spin_hits, spin_misses, blocking_waits, idle_spin_ns;
   // send_late: a scheduled request sent late although its connection was free at the due
   // time (this generator's own delay); behind: late because the connection was still waiting
   // for the server's previous response (the server's delay, passed on)
-  uint64_t gaps_over[3] = {}, gap_max_ns = 0, send_late_max_ns = 0, behind_max_ns = 0, sends_late_1ms = 0;
+  Stat gaps_over[3], gap_max_ns, send_late_max_ns, behind_max_ns, sends_late_1ms;
   // the thread's own user-space instructions and cycles (hardware counters, where allowed),
   // counted from the last reset
   ThreadCounters pmu;
-  uint64_t pmu_ins0 = 0, pmu_cyc0 = 0;
-  void pmu_reset() { pmu.read(&pmu_ins0, &pmu_cyc0); }
+  Stat pmu_ins0, pmu_cyc0;
+  void pmu_reset() {
+    uint64_t i = 0, c = 0;
+    if (!pmu.read(&i, &c)) return;
+    pmu_ins0 = i;
+    pmu_cyc0 = c;
+  }
   void note_gap(int64_t ns) {
     if (ns <= 100000) return;
-    gaps_over[0] += 1;
-    gaps_over[1] += ns > 1000000;
-    gaps_over[2] += ns > 10000000;
-    if (uint64_t(ns) > gap_max_ns) gap_max_ns = uint64_t(ns);
+    ++gaps_over[0];
+    if (ns > 1000000) ++gaps_over[1];
+    if (ns > 10000000) ++gaps_over[2];
+    gap_max_ns.raise(uint64_t(ns));
   }
   std::vector<std::string> expected;  // per target: the body every response must carry
   std::vector<bool> have_expected;
@@ -490,10 +513,9 @@ void thread_main(ThreadState* ts, const Options* o) {
       if (c->next_due <= now) {
         // late by the time since it was both due and free: the generator's own delay
         const int64_t own = now - std::max(c->next_due, c->free_at);
-        if (uint64_t(own) > ts->send_late_max_ns) ts->send_late_max_ns = uint64_t(own);
+        ts->send_late_max_ns.raise(uint64_t(own));
         if (own > 1000000) ++ts->sends_late_1ms;
-        if (c->free_at > c->next_due && uint64_t(c->free_at - c->next_due) > ts->behind_max_ns)
-          ts->behind_max_ns = uint64_t(c->free_at - c->next_due);
+        if (c->free_at > c->next_due) ts->behind_max_ns.raise(uint64_t(c->free_at - c->next_due));
         c->intended = c->next_due;
         c->next_due += interval;
         if (!send_req(c.get(), o->pipeline)) ++ts->errors;
@@ -524,7 +546,10 @@ void thread_main(ThreadState* ts, const Options* o) {
         for (int k = 0; k < o->busy_poll_pause; ++k) __builtin_ia32_pause();
       }
       if (spun) ts->idle_spin_ns += uint64_t(t - spin0);
-      if (n > 0) ++(spun ? ts->spin_hits : ts->poll_hits);
+      if (n > 0) {
+        if (spun) ++ts->spin_hits;
+        else ++ts->poll_hits;
+      }
       else ++ts->spin_misses;
     } else {
       ts->note_gap(mono_ns() - pass_at);
@@ -558,9 +583,10 @@ void thread_main(ThreadState* ts, const Options* o) {
         ts->recording = true;
         // the time accounting covers the measured part too
         ts->pmu_reset();
-        ts->poll_hits = ts->spin_hits = ts->spin_misses = ts->blocking_waits = ts->idle_spin_ns = 0;
-        ts->gaps_over[0] = ts->gaps_over[1] = ts->gaps_over[2] = ts->gap_max_ns = ts->send_late_max_ns = 0;
-        ts->behind_max_ns = ts->sends_late_1ms = 0;
+        for (Stat* x : {&ts->poll_hits, &ts->spin_hits, &ts->spin_misses, &ts->blocking_waits, &ts->idle_spin_ns,
+                        &ts->gaps_over[0], &ts->gaps_over[1], &ts->gaps_over[2], &ts->gap_max_ns,
+                        &ts->send_late_max_ns, &ts->behind_max_ns, &ts->sends_late_1ms})
+          *x = 0;
       }
       if (now >= end) break;
     }
@@ -764,9 +790,9 @@ std::string stats_json(std::vector<std::unique_ptr<ThreadState>>& ts, bool with_
     spin_misses += t->spin_misses;
     sleeps += t->blocking_waits;
     idle_ns += t->idle_spin_ns;
-    gmax = std::max(gmax, t->gap_max_ns);
-    late = std::max(late, t->send_late_max_ns);
-    behind = std::max(behind, t->behind_max_ns);
+    gmax = std::max<uint64_t>(gmax, t->gap_max_ns);
+    late = std::max<uint64_t>(late, t->send_late_max_ns);
+    behind = std::max<uint64_t>(behind, t->behind_max_ns);
     late_1ms += t->sends_late_1ms;
     for (int k = 0; k < 3; ++k) over[k] += t->gaps_over[k];
   }
@@ -1121,9 +1147,10 @@ int main(int argc, char** argv) {
         t->hist.reset();
         t->errors = t->non2xx = t->reconnects = t->body_checked = t->body_mismatch = t->body_alt = 0;
         t->pmu_reset();
-        t->poll_hits = t->spin_hits = t->spin_misses = t->blocking_waits = t->idle_spin_ns = 0;
-        t->gaps_over[0] = t->gaps_over[1] = t->gaps_over[2] = t->gap_max_ns = t->send_late_max_ns = 0;
-        t->behind_max_ns = t->sends_late_1ms = 0;
+        for (Stat* x : {&t->poll_hits, &t->spin_hits, &t->spin_misses, &t->blocking_waits, &t->idle_spin_ns,
+                        &t->gaps_over[0], &t->gaps_over[1], &t->gaps_over[2], &t->gap_max_ns,
+                        &t->send_late_max_ns, &t->behind_max_ns, &t->sends_late_1ms})
+          *x = 0;
       }
       printf("{\"reset\":true}\n");
       fflush(stdout);

@@ -25,27 +25,29 @@ int open_counter(uint64_t config, int group) {
 
 ThreadCounters::~ThreadCounters() {
   if (fd_cycles_ >= 0) ::close(fd_cycles_);
-  if (fd_ >= 0) ::close(fd_);
+  const int fd = fd_.load(std::memory_order_relaxed);
+  if (fd >= 0) ::close(fd);
 }
 
 bool ThreadCounters::open() {
-  if (fd_ >= 0) return true;
-  fd_ = open_counter(PERF_COUNT_HW_INSTRUCTIONS, -1);
-  if (fd_ < 0) return false;
-  fd_cycles_ = open_counter(PERF_COUNT_HW_CPU_CYCLES, fd_);
+  if (fd_.load(std::memory_order_relaxed) >= 0) return true;
+  const int fd = open_counter(PERF_COUNT_HW_INSTRUCTIONS, -1);
+  if (fd < 0) return false;
+  fd_cycles_ = open_counter(PERF_COUNT_HW_CPU_CYCLES, fd);
   if (fd_cycles_ < 0) {
-    ::close(fd_);
-    fd_ = -1;
+    ::close(fd);
     return false;
   }
+  fd_.store(fd, std::memory_order_release);
   return true;
 }
 
 bool ThreadCounters::read(uint64_t* instructions, uint64_t* cycles) const {
-  if (fd_ < 0) return false;
+  const int fd = fd_.load(std::memory_order_acquire);
+  if (fd < 0) return false;
   // PERF_FORMAT_GROUP: nr, time_enabled, time_running, then one value per member
   uint64_t buf[5] = {};
-  if (::read(fd_, buf, sizeof buf) != ssize_t(sizeof buf) || buf[0] != 2) return false;
+  if (::read(fd, buf, sizeof buf) != ssize_t(sizeof buf) || buf[0] != 2) return false;
   const uint64_t enabled = buf[1], running = buf[2];
   auto scaled = [&](uint64_t v) {
     return running && running < enabled ? uint64_t(double(v) * double(enabled) / double(running)) : v;

@@ -9,6 +9,7 @@
 // by construction (their CPUs' wall time over one request count), while the instructions and
 // cycles each spends in its own code are its own.
 #pragma once
+#include <atomic>
 #include <cstdint>
 
 namespace hola {
@@ -22,13 +23,14 @@ class ThreadCounters {
 
   // Opens the counters for the calling thread; false (and no counters) when not permitted.
   bool open();
-  bool is_open() const { return fd_ >= 0; }
+  bool is_open() const { return fd_.load(std::memory_order_acquire) >= 0; }
   // Totals since open(), scaled by the time the PMU actually counted them (when counters are
   // multiplexed with other users). False when closed or unreadable.
   bool read(uint64_t* instructions, uint64_t* cycles) const;
 
  private:
-  int fd_ = -1;        // group leader: instructions
+  // group leader (instructions): published by the opening thread, read by the metrics thread
+  std::atomic<int> fd_{-1};
   int fd_cycles_ = -1;
 };
 
