@@ -195,6 +195,13 @@ tails)
   # open-loop curves of the shipped default (auto) three times and one
   # with busy-polling off, each point with its tail attribution (bench/latency_curve.py)
   info
+  # what the scheduler lets an ordinary user do about other tasks on the job's CPUs
+  { echo "rtprio limit: $(ulimit -r)"; echo "nice limit: $(ulimit -e)";
+    echo "sched_rt_runtime_us: $(cat /proc/sys/kernel/sched_rt_runtime_us 2>/dev/null)";
+    echo "base_slice_ns: $(cat /sys/kernel/debug/sched/base_slice_ns 2>/dev/null || echo n/a)";
+    echo "kernel: $(uname -r)"; grep -h "^CONFIG_HZ=\|^CONFIG_PREEMPT" /boot/config-"$(uname -r)" 2>/dev/null;
+    chrt -f 1 true 2>&1 && echo "SCHED_FIFO: allowed" || echo "SCHED_FIFO: refused";
+    nice -n -5 true 2>&1 && echo "negative nice: allowed" || echo "negative nice: refused"; } > "$OUT/sched.txt" 2>&1
   for k in ${CURVES:-auto1 auto2 off auto3}; do
     bp=auto; [ "${k#off}" != "$k" ] && bp=0
     timeout -k 10 200 python bench/latency_curve.py --duration 6 --server-busy-poll "$bp" \

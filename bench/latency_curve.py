@@ -26,7 +26,10 @@ ap.add_argument("--rates", default="250000,1000000,2000000,3000000,3500000")
 ap.add_argument("--duration", type=float, default=8)
 ap.add_argument("--connections", type=int, default=64)
 ap.add_argument("--busy-poll-us", type=int, default=0, help="server and load generator spin in epoll this long")
-ap.add_argument("--spin-us", type=int, default=0, help="load generator spins when its next send is this close")
+ap.add_argument("--spin-us", type=int, default=1000,
+                help="load generator polls instead of sleeping when its next send is this close (the default "
+                     "keeps it on its CPUs: a generator that sleeps between sends leaves CPUs the scheduler "
+                     "hands to other tasks, and its late wake-ups are charged to the server)")
 ap.add_argument("--server-busy-poll", default="",
                 help="the server's --busy-poll-us (N, auto or auto:N); default: --busy-poll-us")
 ap.add_argument("--out", default="")
@@ -89,7 +92,7 @@ with HolaProcess(args=server_args, env={"HOSTNAME": "h"}, threads=len(srv), cpu_
                "host_load_loadgen": subruns.host_load(t0, t1, lg, job),
                "loadgen": {k: lat.get(k) for k in ("gaps_over_100us", "gaps_over_1ms", "gaps_over_10ms", "gap_max_ns",
                                                    "send_late_max_ns", "sends_late_1ms", "behind_max_ns",
-                                                   "blocking_waits")}}
+                                                   "blocking_waits", "run_delay_ns", "run_delay_max_thread_ns")}}
         rows.append(row)
         print(json.dumps(row), flush=True)
     probe.close()

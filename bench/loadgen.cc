@@ -50,6 +50,7 @@
 #include <sys/prctl.h>
 #include <sys/eventfd.h>
 #include <sys/socket.h>
+#include <sys/syscall.h>
 #include <signal.h>
 #include <unistd.h>
 
@@ -136,6 +137,20 @@ struct Conn {
   int64_t free_at = 0;    // --rate: when its last response completed (free to send again)
 };
 
+// The scheduler's run_delay of one of this process's threads (ns it spent runnable, waiting
+// for a CPU another task held); 0 when schedstats are unavailable.
+uint64_t run_delay_ns(int tid) {
+  if (tid <= 0) return 0;
+  char path[64];
+  snprintf(path, sizeof path, "/proc/self/task/%d/schedstat", tid);
+  FILE* f = fopen(path, "r");
+  if (!f) return 0;
+  unsigned long long on_cpu = 0, delay = 0;
+  const int got = fscanf(f, "%llu %llu", &on_cpu, &delay);
+  fclose(f);
+  return got == 2 ? uint64_t(delay) : 0;
+}
+
 // A counter one polling thread raises and the control thread reads or zeroes between runs.
 struct Stat {
   std::atomic<uint64_t> v{0};
@@ -177,6 +192,11 @@ struct ThreadState {
   // counted from the last reset
   ThreadCounters pmu;
   Stat pmu_ins0, pmu_cyc0;
+  // time the thread was runnable but waiting for its CPU (the scheduler's run_delay: another
+  // task held the CPU), counted from the last reset
+  std::atomic<int> tid{0};
+  Stat run_delay0, run_delay_last;
+  void sched_reset() { run_delay0 = run_delay_ns(tid.load(std::memory_order_relaxed)); }
   void pmu_reset() {
     uint64_t i = 0, c = 0;
     if (!pmu.read(&i, &c)) return;
@@ -411,6 +431,8 @@ void thread_main(ThreadState* ts, const Options* o) {
     pthread_setname_np(pthread_self(), name);
   }
   hola::cpuprof::register_thread();
+  ts->tid.store(int(syscall(SYS_gettid)), std::memory_order_relaxed);
+  ts->sched_reset();
   if (ts->pmu.open()) ts->pmu_reset();
   // Connections (and their receive buffers) are built here, after pinning, so their pages
   // are first touched on this thread's NUMA node: on a 2-socket node a thread may drive a
@@ -583,6 +605,7 @@ void thread_main(ThreadState* ts, const Options* o) {
         ts->recording = true;
         // the time accounting covers the measured part too
         ts->pmu_reset();
+        ts->sched_reset();
         for (Stat* x : {&ts->poll_hits, &ts->spin_hits, &ts->spin_misses, &ts->blocking_waits, &ts->idle_spin_ns,
                         &ts->gaps_over[0], &ts->gaps_over[1], &ts->gaps_over[2], &ts->gap_max_ns,
                         &ts->send_late_max_ns, &ts->behind_max_ns, &ts->sends_late_1ms})
@@ -739,6 +762,8 @@ void thread_main(ThreadState* ts, const Options* o) {
     }
     if (rate_mode) send_due(mono_ns());
   }
+  // the thread's /proc entry goes with it; stats read after the join use this
+  ts->run_delay_last = run_delay_ns(ts->tid.load(std::memory_order_relaxed));
 }
 
 bool parse_targets(const std::string& s, std::vector<Target>* out) {
@@ -768,7 +793,7 @@ std::string stats_json(std::vector<std::unique_ptr<ThreadState>>& ts, bool with_
   uint64_t errors = 0, non2xx = 0, reconnects = 0, checked = 0, mismatch = 0, alt = 0;
   uint64_t poll_hits = 0, spin_hits = 0, spin_misses = 0, sleeps = 0, idle_ns = 0, gmax = 0, late = 0, behind = 0,
            late_1ms = 0;
-  uint64_t over[3] = {}, u_ins = 0, u_cyc = 0;
+  uint64_t over[3] = {}, u_ins = 0, u_cyc = 0, rdelay = 0, rdelay_max = 0;
   bool pmu = false;
   for (auto& t : ts) {
     uint64_t a = 0, b = 0;
@@ -776,6 +801,14 @@ std::string stats_json(std::vector<std::unique_ptr<ThreadState>>& ts, bool with_
       pmu = true;
       u_ins += a - t->pmu_ins0;
       u_cyc += b - t->pmu_cyc0;
+    }
+    if (const int tid = t->tid.load(std::memory_order_relaxed); tid > 0) {
+      uint64_t now_rd = run_delay_ns(tid);
+      if (!now_rd) now_rd = t->run_delay_last;
+      const uint64_t base = t->run_delay0;
+      const uint64_t d = now_rd > base ? now_rd - base : 0;
+      rdelay += d;
+      rdelay_max = std::max(rdelay_max, d);
     }
     std::lock_guard<std::mutex> g(t->hist_mu);
     h.merge(t->hist);
@@ -810,11 +843,13 @@ std::string stats_json(std::vector<std::unique_ptr<ThreadState>>& ts, bool with_
   snprintf(buf, sizeof buf,
            ",\"poll_hits\":%llu,\"spin_hits\":%llu,\"spin_misses\":%llu,\"blocking_waits\":%llu,"
            "\"idle_spin_ns\":%llu,\"gaps_over_100us\":%llu,\"gaps_over_1ms\":%llu,\"gaps_over_10ms\":%llu,"
-           "\"gap_max_ns\":%llu,\"send_late_max_ns\":%llu,\"sends_late_1ms\":%llu,\"behind_max_ns\":%llu",
+           "\"gap_max_ns\":%llu,\"send_late_max_ns\":%llu,\"sends_late_1ms\":%llu,\"behind_max_ns\":%llu,"
+           "\"run_delay_ns\":%llu,\"run_delay_max_thread_ns\":%llu",
            (unsigned long long)poll_hits, (unsigned long long)spin_hits, (unsigned long long)spin_misses,
            (unsigned long long)sleeps, (unsigned long long)idle_ns, (unsigned long long)over[0],
            (unsigned long long)over[1], (unsigned long long)over[2], (unsigned long long)gmax,
-           (unsigned long long)late, (unsigned long long)late_1ms, (unsigned long long)behind);
+           (unsigned long long)late, (unsigned long long)late_1ms, (unsigned long long)behind,
+           (unsigned long long)rdelay, (unsigned long long)rdelay_max);
   s += buf;
   if (pmu) {
     snprintf(buf, sizeof buf, ",\"user_instructions\":%llu,\"user_cycles\":%llu", (unsigned long long)u_ins,
@@ -1147,6 +1182,7 @@ int main(int argc, char** argv) {
         t->hist.reset();
         t->errors = t->non2xx = t->reconnects = t->body_checked = t->body_mismatch = t->body_alt = 0;
         t->pmu_reset();
+        t->sched_reset();
         for (Stat* x : {&t->poll_hits, &t->spin_hits, &t->spin_misses, &t->blocking_waits, &t->idle_spin_ns,
                         &t->gaps_over[0], &t->gaps_over[1], &t->gaps_over[2], &t->gap_max_ns,
                         &t->send_late_max_ns, &t->behind_max_ns, &t->sends_late_1ms})

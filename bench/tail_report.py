@@ -7,6 +7,9 @@ For every point with p99.9 above --threshold-us it names what the point's own re
   gaps       the replica's loops went more than 1 ms between two polls (a handler that ran
              long, or the thread descheduled: then it also has involuntary switches)
   preempted  the replica's workers were switched out involuntarily (another task on their CPU)
+  cpu-wait   the scheduler's run_delay of the replica's workers: time they were runnable but
+             waited for a CPU another task held (total, and the most any one worker waited)
+  lg-cpu-wait the same for the load generator's threads
   throttled  CFS bandwidth throttling of the cgroup (every thread stops until the next period)
   late       the load generator sent a scheduled request more than 1 ms late although its
              connection was free at the due time: its own stall, which the open loop charges
@@ -37,6 +40,9 @@ def causes(row: dict) -> list[str]:
     invol = sum(g.get("invol", 0) for g in row.get("server_threads", {}).values())
     if invol:
         out.append(f"preempted({invol})")
+    w = row.get("server_threads", {}).get("workers", {})
+    if (w.get("run_delay_ms") or 0) > 1.0:
+        out.append(f"cpu-wait({w['run_delay_ms']:.1f} ms, max thread {w.get('run_delay_max_thread_ms', 0):.1f} ms)")
     thr = row.get("cgroup_throttle", {})
     if thr.get("throttled_periods", 0):
         out.append(f"throttled({thr['throttled_periods']} periods, {thr.get('throttled_ms', 0)} ms)")
@@ -46,6 +52,8 @@ def causes(row: dict) -> list[str]:
         out.append(f"late({lg['send_late_max_ns'] / 1e3:.0f} us" + (f", {n} sends >1ms" if n is not None else "") + ")")
     if (lg.get("behind_max_ns") or 0) > 1_000_000:
         out.append(f"behind({lg['behind_max_ns'] / 1e3:.0f} us)")
+    if (lg.get("run_delay_ns") or 0) > 1_000_000:
+        out.append(f"lg-cpu-wait({lg['run_delay_ns'] / 1e6:.1f} ms, max thread {(lg.get('run_delay_max_thread_ns') or 0) / 1e6:.1f} ms)")
     fs, ks = row.get("foreign_on_server_cpus_s"), row.get("ksoftirqd_on_server_cpus_s")
     if fs is not None and fs > 0.01 * 8:  # 1 % of 8 CPUs over the 8 s point
         out.append(f"foreign({fs:.2f} CPU-s" + (f", ksoftirqd {ks:.2f}" if ks else "") + ")")

@@ -204,9 +204,11 @@ def ksoftirqd_cpu_s(cpus) -> float:
 
 
 def task_stats(pid: int) -> dict[str, dict]:
-    """Per thread of `pid` (by comm): CPU seconds and voluntary / involuntary context switches
-    (a thread that sleeps in epoll_wait and is woken switches voluntarily; one preempted by
-    another runnable task, involuntarily). Threads of one name are summed."""
+    """Per thread of `pid` (by comm): CPU seconds, voluntary / involuntary context switches (a
+    thread that sleeps in epoll_wait and is woken switches voluntarily; one preempted by another
+    runnable task, involuntarily) and the scheduler's run_delay (ms it was runnable but waited
+    for a CPU another task held; /proc/<pid>/task/<tid>/schedstat). Threads of one name are
+    summed; `run_delay_max_ms` is the largest single thread's."""
     out: dict[str, dict] = {}
     tck = os.sysconf("SC_CLK_TCK")
     for task in Path(f"/proc/{pid}/task").glob("*"):
@@ -214,6 +216,10 @@ def task_stats(pid: int) -> dict[str, dict]:
             comm = (task / "comm").read_text().strip()
             fields = (task / "stat").read_text().rsplit(")", 1)[1].split()
             vol = invol = 0
+            try:
+                delay_ms = int((task / "schedstat").read_text().split()[1]) / 1e6
+            except (OSError, IndexError, ValueError):
+                delay_ms = 0.0
             for ln in (task / "status").read_text().splitlines():
                 if ln.startswith("voluntary_ctxt_switches:"):
                     vol = int(ln.split()[1])
@@ -221,11 +227,14 @@ def task_stats(pid: int) -> dict[str, dict]:
                     invol = int(ln.split()[1])
         except (OSError, IndexError, ValueError):
             continue
-        d = out.setdefault(comm, {"cpu_s": 0.0, "vol": 0, "invol": 0, "threads": 0})
+        d = out.setdefault(comm, {"cpu_s": 0.0, "vol": 0, "invol": 0, "threads": 0, "run_delay_ms": 0.0,
+                                  "per_tid": {}})
         d["cpu_s"] += (int(fields[11]) + int(fields[12])) / tck
         d["vol"] += vol
         d["invol"] += invol
         d["threads"] += 1
+        d["run_delay_ms"] += delay_ms
+        d["per_tid"][task.name] = delay_ms
     return out
 
 
@@ -235,11 +244,16 @@ def task_stats_delta(a: dict, b: dict, group=lambda comm: "workers" if comm.star
     or hola-lg*, and every other thread of the process)."""
     out: dict[str, dict] = {}
     for comm, d1 in b.items():
-        d0 = a.get(comm, {"cpu_s": 0.0, "vol": 0, "invol": 0})
-        g = out.setdefault(group(comm), {"cpu_s": 0.0, "vol": 0, "invol": 0})
+        d0 = a.get(comm, {"cpu_s": 0.0, "vol": 0, "invol": 0, "run_delay_ms": 0.0, "per_tid": {}})
+        g = out.setdefault(group(comm), {"cpu_s": 0.0, "vol": 0, "invol": 0, "run_delay_ms": 0.0,
+                                         "run_delay_max_thread_ms": 0.0})
         g["cpu_s"] = round(g["cpu_s"] + d1["cpu_s"] - d0["cpu_s"], 3)
         g["vol"] += d1["vol"] - d0["vol"]
         g["invol"] += d1["invol"] - d0["invol"]
+        g["run_delay_ms"] = round(g["run_delay_ms"] + d1.get("run_delay_ms", 0.0) - d0.get("run_delay_ms", 0.0), 3)
+        for tid, v in d1.get("per_tid", {}).items():
+            dt = v - d0.get("per_tid", {}).get(tid, 0.0)
+            g["run_delay_max_thread_ms"] = round(max(g["run_delay_max_thread_ms"], dt), 3)
     return out
 
 

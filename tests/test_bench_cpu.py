@@ -319,3 +319,11 @@ def test_latency_curve_runs_open_loop_with_the_server_busy_poll_it_names(tmp_pat
     (row,) = d["rows"]
     assert row["errors"] == 0 and row["achieved_rps"] > 0.9 * row["target_rps"], row
     assert d["server_args"] == ["--busy-poll-us", "0"]
+    # the tail attribution of the point: the scheduler's run_delay of both sides and the load
+    # generator's own lateness (bench/tail_report.py names causes from these)
+    assert d["spin_us"] == 1000
+    assert {"run_delay_ms", "run_delay_max_thread_ms", "invol"} <= set(row["server_threads"]["workers"])
+    assert {"run_delay_ns", "run_delay_max_thread_ns", "send_late_max_ns", "behind_max_ns"} <= set(row["loadgen"])
+    rep = subprocess.run([sys.executable, str(ROOT / "bench" / "tail_report.py"), str(out), "--threshold-us", "0"],
+                         capture_output=True, text=True, timeout=60)
+    assert rep.returncode == 0 and "with nothing recorded" in rep.stdout, rep.stdout + rep.stderr
