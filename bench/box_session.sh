@@ -202,9 +202,12 @@ tails)
     echo "kernel: $(uname -r)"; grep -h "^CONFIG_HZ=\|^CONFIG_PREEMPT" /boot/config-"$(uname -r)" 2>/dev/null;
     chrt -f 1 true 2>&1 && echo "SCHED_FIFO: allowed" || echo "SCHED_FIFO: refused";
     nice -n -5 true 2>&1 && echo "negative nice: allowed" || echo "negative nice: refused"; } > "$OUT/sched.txt" 2>&1
+  # a name starting "off" runs the server without busy-polling; one ending "s" asks for a
+  # ${SLICE:-100} us scheduler slice for the server's workers and the generator's threads
   for k in ${CURVES:-auto1 auto2 off auto3}; do
     bp=auto; [ "${k#off}" != "$k" ] && bp=0
-    timeout -k 10 200 python bench/latency_curve.py --duration 6 --server-busy-poll "$bp" \
+    sl=0; [ "${k%s}" != "$k" ] && sl=${SLICE:-100}
+    timeout -k 10 200 python bench/latency_curve.py --duration 6 --server-busy-poll "$bp" --sched-slice-us "$sl" \
       --out "$OUT/curve_$k.json" > "$OUT/curve_$k.log" 2>&1 || exit $?
   done
   ;;

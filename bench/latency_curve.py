@@ -32,6 +32,8 @@ ap.add_argument("--spin-us", type=int, default=1000,
                      "hands to other tasks, and its late wake-ups are charged to the server)")
 ap.add_argument("--server-busy-poll", default="",
                 help="the server's --busy-poll-us (N, auto or auto:N); default: --busy-poll-us")
+ap.add_argument("--sched-slice-us", type=int, default=0,
+                help="server workers and load-generator threads ask the scheduler for this time slice (0 = kernel default)")
 ap.add_argument("--out", default="")
 a = ap.parse_args()
 
@@ -40,6 +42,8 @@ srv, lg = split_server_loadgen(cores, max(1, len(cores) // 2))
 rows = []
 server_bp = a.server_busy_poll or str(a.busy_poll_us)
 server_args = ["--busy-poll-us", server_bp]  # always explicit: hola's own default is auto
+if a.sched_slice_us:
+    server_args += ["--sched-slice-us", str(a.sched_slice_us)]
 with HolaProcess(args=server_args, env={"HOSTNAME": "h"}, threads=len(srv), cpu_list=format_cpu_list(srv),
                  log_level="warn") as s:
     def server_cpu():
@@ -61,7 +65,7 @@ with HolaProcess(args=server_args, env={"HOSTNAME": "h"}, threads=len(srv), cpu_
         k0 = ksoftirqd_cpu_s(srv)
         r = run_duration([("127.0.0.1", s.port)], a.connections, len(lg), a.duration, 2.0,
                          cpu_list=",".join(map(str, lg)), rate=rate, busy_poll_us=a.busy_poll_us,
-                         spin_us=a.spin_us, verify_body=True)
+                         spin_us=a.spin_us, verify_body=True, sched_slice_us=a.sched_slice_us)
         m1, ts1, thr1, t1 = subruns.metrics_counters(s.port, probe=probe), task_stats(s.proc.pid), cgroup_cpu_stat(), cpu_times()
         k1 = ksoftirqd_cpu_s(srv)
         c1 = resource.getrusage(resource.RUSAGE_CHILDREN)
@@ -97,6 +101,7 @@ with HolaProcess(args=server_args, env={"HOSTNAME": "h"}, threads=len(srv), cpu_
         print(json.dumps(row), flush=True)
     probe.close()
 out = {"cpu_map": {"server": format_cpu_list(srv), "loadgen": format_cpu_list(lg)}, "connections": a.connections,
-       "busy_poll_us": a.busy_poll_us, "server_busy_poll": server_bp, "server_args": server_args, "spin_us": a.spin_us, "rows": rows}
+       "busy_poll_us": a.busy_poll_us, "server_busy_poll": server_bp, "server_args": server_args, "spin_us": a.spin_us,
+       "sched_slice_us": a.sched_slice_us, "rows": rows}
 if a.out:
     Path(a.out).write_text(json.dumps(out, indent=1))

@@ -109,6 +109,7 @@ struct Options {
   // read drains the socket and no re-poll of level-triggered items is needed.
   bool edge_triggered = true;
   double rate = 0;  // --rate: open-loop total req/s (wrk2-style, latency from intended time)
+  int sched_slice_us = 0;  // each thread asks for this scheduler time slice (0 = the kernel's)
   int spin_us = 0;  // --rate: spin instead of sleeping when the next send is this close (burns CPU)
   // control: a run of R requests per connection is R x connections requests drawn from one
   // shared budget (connections that answer faster do more, so no thread idles at the end of
@@ -432,6 +433,8 @@ void thread_main(ThreadState* ts, const Options* o) {
   }
   hola::cpuprof::register_thread();
   ts->tid.store(int(syscall(SYS_gettid)), std::memory_order_relaxed);
+  if (o->sched_slice_us > 0 && hola::set_current_thread_slice_us(o->sched_slice_us) < 0)
+    fprintf(stderr, "loadgen: could not set a %d us time slice\n", o->sched_slice_us);
   ts->sched_reset();
   if (ts->pmu.open()) ts->pmu_reset();
   // Connections (and their receive buffers) are built here, after pinning, so their pages
@@ -970,6 +973,7 @@ int main(int argc, char** argv) {
     else if (a == "--epoll-lt") o.edge_triggered = false;
     else if (a == "--rate" || a == "-R") o.rate = atof(val().c_str());
     else if (a == "--spin-us") o.spin_us = atoi(val().c_str());
+    else if (a == "--sched-slice-us") o.sched_slice_us = atoi(val().c_str());
     else if (a == "--per-conn-quota") o.per_conn_quota = true;
     else if (a == "--pipeline") o.pipeline = atoi(val().c_str());
     else if (a == "--expect-body") o.expect_bodies.push_back(unescape(val()));
@@ -987,6 +991,7 @@ int main(int argc, char** argv) {
       fprintf(stderr,
               "usage: hola_loadgen --targets h:p[,h:p..] -c CONNS -t THREADS [--cpu-list L] [--path P]\n"
               "                    (--duration S [--warmup S] [--rate R [--spin-us N]] | --control [--per-conn-quota])\n"
+              "                    [--sched-slice-us N]  (each thread asks the scheduler for an N us slice)\n"
               "                    [--target-offset K] [--busy-poll-us N [--busy-poll-pause P]] [--epoll-lt] [-H 'Name: v']\n"
               "                    [--pipeline P] [--expect-body B]... [--alt-body B]... [--verify-body] [--conn-targets i,j,..]\n"
               "                    [--cpu-profile FILE]  (sampled call stacks, bench/cpuprof_report.py --threads hola-lg)\n"

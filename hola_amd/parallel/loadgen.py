@@ -149,7 +149,8 @@ def run_duration(targets: list[tuple[str, int]], connections: int, threads: int,
                  warmup_s: float = 1.0, cpu_list: str | None = None, path: str = "/api/hola",
                  timeout: float | None = None, rate: float = 0.0, busy_poll_us: int = 0,
                  spin_us: int = 0, pipeline: int = 1, expect_bodies: list[str] | None = None,
-                 verify_body: bool = False, alt_bodies: list[str] | None = None, busy_poll_pause: int = 0) -> dict:
+                 verify_body: bool = False, alt_bodies: list[str] | None = None, busy_poll_pause: int = 0,
+                 sched_slice_us: int = 0) -> dict:
     """wrk-style timed run (closed loop), or wrk2-style open loop at `rate` req/s with latency
     measured from intended send times; returns the loadgen's JSON summary. `busy_poll_us`
     spins in epoll after activity; `spin_us` (open loop) spins instead of sleeping when the
@@ -168,6 +169,8 @@ def run_duration(targets: list[tuple[str, int]], connections: int, threads: int,
             cmd += ["--busy-poll-pause", str(busy_poll_pause)]
     if spin_us:
         cmd += ["--spin-us", str(spin_us)]
+    if sched_slice_us:
+        cmd += ["--sched-slice-us", str(sched_slice_us)]
     if pipeline > 1:
         cmd += ["--pipeline", str(pipeline)]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout or duration_s + warmup_s + 60)

@@ -2,6 +2,11 @@
 
 #include <pthread.h>
 #include <sched.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
+#include <cerrno>
+#include <cstdint>
 
 #include <cstdio>
 #include <cstdlib>
@@ -63,6 +68,38 @@ bool pin_current_thread(int cpu) {
   CPU_ZERO(&set);
   CPU_SET(cpu, &set);
   return pthread_setaffinity_np(pthread_self(), sizeof set, &set) == 0;
+}
+
+namespace {
+struct SchedAttr {  // struct sched_attr, SCHED_ATTR_SIZE_VER1
+  uint32_t size;
+  uint32_t sched_policy;
+  uint64_t sched_flags;
+  int32_t sched_nice;
+  uint32_t sched_priority;
+  uint64_t sched_runtime;
+  uint64_t sched_deadline;
+  uint64_t sched_period;
+  uint32_t sched_util_min;
+  uint32_t sched_util_max;
+};
+}  // namespace
+
+long current_thread_slice_us() {
+  SchedAttr a{};
+  if (syscall(SYS_sched_getattr, 0, &a, unsigned(sizeof a), 0u) != 0) return 0;
+  return long(a.sched_runtime / 1000);
+}
+
+long set_current_thread_slice_us(int us) {
+  SchedAttr a{};
+  if (syscall(SYS_sched_getattr, 0, &a, unsigned(sizeof a), 0u) != 0) return -errno;
+  if (a.sched_policy != SCHED_OTHER && a.sched_policy != SCHED_BATCH) return -EINVAL;
+  a.size = sizeof a;
+  a.sched_flags = 0;
+  a.sched_runtime = uint64_t(us) * 1000;  // the kernel clamps it to [0.1 ms, 100 ms]
+  if (syscall(SYS_sched_setattr, 0, &a, 0u) != 0) return -errno;
+  return current_thread_slice_us();
 }
 
 int l3_domain_of(int cpu) {

@@ -12,6 +12,14 @@ std::string format_cpu_list(const std::vector<int>& cpus);
 std::vector<int> allowed_cpus();
 // Pins the calling thread to one CPU; false on failure (e.g. CPU not in the cgroup).
 bool pin_current_thread(int cpu);
+// Asks the scheduler for a `us`-microsecond time slice for the calling thread (EEVDF custom
+// slice: sched_attr::sched_runtime of a SCHED_OTHER task, Linux 6.12+; an unprivileged thread
+// may set its own). A shorter slice gives the thread earlier virtual deadlines, so it wins
+// the CPU back sooner from a task that preempted it. Returns the slice the kernel reports
+// afterwards in microseconds (0 when it does not support custom slices), -errno on failure.
+long set_current_thread_slice_us(int us);
+// The calling thread's current slice in microseconds as sched_getattr reports it (0 unknown).
+long current_thread_slice_us();
 // L3 cache domain (a CCD on EPYC) of a CPU from sysfs; -1 when unknown. Cached.
 int l3_domain_of(int cpu);
 // Physical core of a CPU: the lowest CPU id among its SMT siblings (sysfs

@@ -742,6 +742,11 @@ void Server::start() {
       snprintf(name, sizeof name, "hola-w%d", wp->index());
       pthread_setname_np(pthread_self(), name);
       if (opts_.perf_counters) wp->counters_.open();  // counts this thread only
+      if (opts_.sched_slice_us > 0) {
+        const long got = set_current_thread_slice_us(opts_.sched_slice_us);
+        if (got < 0) LOG_WARN("worker %d: could not set a %d us time slice (errno %ld)", wp->index(), opts_.sched_slice_us, -got);
+      }
+      wp->slice_us_.store(current_thread_slice_us(), std::memory_order_relaxed);
       cpuprof::note_thread();  // stack bounds for a stall report's capture
       wp->tid_.store(cpuprof::current_tid());
       cpuprof::register_thread();

@@ -200,6 +200,9 @@ struct ServerOptions {
   // Each worker counts its own user-space instructions and cycles (core/perfcount.h), exported
   // on /metrics when the host allows it (--no-perf-counters turns it off).
   bool perf_counters = true;
+  // Each worker asks the scheduler for this time slice (us; 0 = the kernel's default): see
+  // set_current_thread_slice_us in core/affinity.h. --sched-slice-us.
+  int sched_slice_us = 0;
 };
 
 // Per-worker stage timings (ns) collected with --profile; read after the workers stop.
@@ -245,6 +248,8 @@ class Worker {
   StageProfile* profile() { return profile_.get(); }
   // The worker thread's own user-space instructions and cycles (open once it runs).
   const ThreadCounters& counters() const { return counters_; }
+  // the slice the scheduler reports for the worker's thread (us; 0 unknown)
+  long sched_slice_us() const { return slice_us_.load(std::memory_order_relaxed); }
 
  private:
   friend class Server;
@@ -264,6 +269,7 @@ class Worker {
   Connection* conns_ = nullptr;
   std::unique_ptr<StageProfile> profile_;
   std::shared_ptr<std::function<void()>> sweep_;  // idle-timeout sweeper (owned here)
+  std::atomic<long> slice_us_{0};
   std::atomic<int> tid_{0};  // kernel id of the worker's thread while it runs (stall reports)
 };
 

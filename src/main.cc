@@ -97,6 +97,8 @@ void usage() {
           "                           spin (20 us, or N) while spinning mostly finds work (saturation),\n"
           "                           back off while it mostly waits in vain (light load)\n"
           "  --busy-poll-pause N      PAUSE instructions between empty polls (SMT-friendly spin)\n"
+          "  --sched-slice-us N       ask the scheduler for an N us time slice per worker (EEVDF custom slice,\n"
+          "                           Linux 6.12+; default: the kernel's)\n"
           "  --idle-timeout-ms N      close connections with nothing read or written this long\n"
           "                           (default 60000, 0 = never)\n"
           "  --max-connections N      refuse connections beyond N per replica (default unlimited)\n"
@@ -268,6 +270,7 @@ int main(int argc, char** argv) {
       so.busy_poll_us = so.busy_poll_auto ? (v.size() > 5 ? atoi(v.c_str() + 5) : kAutoBusyPollUs) : atoi(v.c_str());
     }
     else if (a == "--busy-poll-pause") so.busy_poll_pause = atoi(val("--busy-poll-pause").c_str());
+    else if (a == "--sched-slice-us") so.sched_slice_us = atoi(val("--sched-slice-us").c_str());
     else if (a == "--profile") so.profile = true;
     else if (a == "--no-steer") so.steer_l3 = false;
     else if (a == "--no-perf-counters") so.perf_counters = false;

@@ -213,6 +213,14 @@ std::string Prometheus::render(http::Server* server) const {
       o += num;
       o += "\n";
     }
+    // the scheduler's time slice of the workers (--sched-slice-us; the kernel's default otherwise)
+    if (server->num_workers() && server->worker(0).sched_slice_us() > 0) {
+      char sl[32];
+      snprintf(sl, sizeof sl, "%.6f", double(server->worker(0).sched_slice_us()) / 1e6);
+      o += "# TYPE hola_worker_sched_slice_seconds gauge\nhola_worker_sched_slice_seconds ";
+      o += sl;
+      o += "\n";
+    }
     // 1 from the termination signal on (readiness failing, --shutdown-delay-ms), 2 while draining
     o += "# TYPE hola_server_terminating gauge\nhola_server_terminating " +
          std::to_string(server->draining() ? 2 : server->terminating() ? 1 : 0) + "\n";

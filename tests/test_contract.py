@@ -957,3 +957,14 @@ def test_date_header_is_current_after_an_idle_spell(hola):
     st, h, _ = s.get("/api/health")
     sent = email.utils.parsedate_to_datetime(h["date"]).timestamp()
     assert abs(sent - time.time()) < 1.5, h["date"]
+
+
+def test_sched_slice_option_reaches_the_workers(hola):
+    """--sched-slice-us N: every worker asks the scheduler for an N us time slice (EEVDF custom
+    slice), and /metrics reports the slice the kernel gave it. Kernels without custom slices
+    report none, and the gauge is then absent."""
+    s = hola(args=["--sched-slice-us", "500"])
+    body = s.get("/metrics")[2].decode()
+    vals = [float(l.split()[1]) for l in body.splitlines() if l.startswith("hola_worker_sched_slice_seconds ")]
+    if vals:
+        assert abs(vals[0] - 0.0005) < 1e-6, vals
