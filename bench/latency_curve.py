@@ -76,6 +76,11 @@ with HolaProcess(args=server_args, env={"HOSTNAME": "h"}, threads=len(srv), cpu_
         row = {"target_rps": rate, "achieved_rps": r["rps"], "p50_us": lat["p50_ns"] / 1e3,
                "p90_us": lat["p90_ns"] / 1e3, "p99_us": lat["p99_ns"] / 1e3, "p999_us": lat["p999_ns"] / 1e3,
                "max_us": lat["max_ns"] / 1e3, "errors": lat["errors"],
+               # service time: each response's send() to its arrival in the client host's kernel
+               # (receive timestamp), so none of the generator's own delays (a late send, a late
+               # read) is in it; the open-loop figures above charge those to the server
+               "service_us": ({k: lat[f"service_{k}_ns"] / 1e3 for k in ("p50", "p99", "p999", "max")}
+                              if lat.get("service_count") else None),
                "server_cpus_busy": round((s1 - s0) / wall, 2),
                "loadgen_cpus_busy": round((c1.ru_utime + c1.ru_stime - c0.ru_utime - c0.ru_stime) / wall, 2),
                "server_loop": subruns.loop_block(m0, m1, reqs),

@@ -109,6 +109,7 @@ struct Options {
   // read drains the socket and no re-poll of level-triggered items is needed.
   bool edge_triggered = true;
   double rate = 0;  // --rate: open-loop total req/s (wrk2-style, latency from intended time)
+  bool rx_timestamps = false;  // --rate: kernel receive timestamps (set with --rate)
   int sched_slice_us = 0;  // each thread asks for this scheduler time slice (0 = the kernel's)
   int spin_us = 0;  // --rate: spin instead of sleeping when the next send is this close (burns CPU)
   // control: a run of R requests per connection is R x connections requests drawn from one
@@ -174,6 +175,10 @@ struct ThreadState {
   std::vector<int> conn_ids;  // connection i goes to target (i + offset) % targets
   std::vector<std::unique_ptr<Conn>> conns;
   Histogram hist;
+  // --rate: service time of each response, from its send() to its arrival in this host's
+  // kernel (receive timestamp): what the server and the network took, with none of this
+  // generator's own delays (a late send, a late read) in it
+  Histogram svc;
   std::mutex hist_mu;
   uint64_t completed = 0, errors = 0, non2xx = 0, reconnects = 0, bytes = 0;
   uint64_t body_checked = 0, body_mismatch = 0, body_alt = 0;
@@ -318,6 +323,12 @@ bool connect_once(Conn* c, const Options& o) {
   if (c->fd < 0) return false;
   set_nonblocking(c->fd, true);
   set_nodelay(c->fd);
+  if (o.rx_timestamps) {
+    // the kernel stamps each segment as it arrives: a response's arrival is then known even
+    // when this thread reads it late (the service time below)
+    const int one = 1;
+    setsockopt(c->fd, SOL_SOCKET, SO_TIMESTAMPNS, &one, sizeof one);
+  }
   c->have = 0;
   c->busy = false;
   return true;
@@ -604,6 +615,7 @@ void thread_main(ThreadState* ts, const Options* o) {
       if (!ts->recording && now >= warm_end) {
         std::lock_guard<std::mutex> g(ts->hist_mu);
         ts->hist.reset();
+        ts->svc.reset();
         ts->completed = 0;
         ts->recording = true;
         // the time accounting covers the measured part too
@@ -643,7 +655,33 @@ void thread_main(ThreadState* ts, const Options* o) {
         }
         continue;
       }
-      ssize_t r = ::recv(c->fd, c->buf + c->have, sizeof c->buf - c->have, 0);
+      ssize_t r;
+      int64_t rx_kernel = 0;  // CLOCK_MONOTONIC ns of the data's arrival (0 = unknown)
+      if (o->rx_timestamps) {
+        iovec iov{c->buf + c->have, sizeof c->buf - c->have};
+        alignas(cmsghdr) char cbuf[CMSG_SPACE(sizeof(timespec))];
+        msghdr mh{};
+        mh.msg_iov = &iov;
+        mh.msg_iovlen = 1;
+        mh.msg_control = cbuf;
+        mh.msg_controllen = sizeof cbuf;
+        r = ::recvmsg(c->fd, &mh, 0);
+        if (r > 0)
+          for (cmsghdr* cm = CMSG_FIRSTHDR(&mh); cm; cm = CMSG_NXTHDR(&mh, cm))
+            if (cm->cmsg_level == SOL_SOCKET && cm->cmsg_type == SCM_TIMESTAMPNS) {
+              timespec rx;
+              memcpy(&rx, CMSG_DATA(cm), sizeof rx);
+              // realtime -> monotonic with the two clocks' offset as of now (a slew since the
+              // arrival, microseconds ago, is negligible)
+              timespec rt, mt;
+              clock_gettime(CLOCK_REALTIME, &rt);
+              clock_gettime(CLOCK_MONOTONIC, &mt);
+              const int64_t off = (int64_t(rt.tv_sec) - int64_t(mt.tv_sec)) * 1000000000 + (rt.tv_nsec - mt.tv_nsec);
+              rx_kernel = int64_t(rx.tv_sec) * 1000000000 + rx.tv_nsec - off;
+            }
+      } else {
+        r = ::recv(c->fd, c->buf + c->have, sizeof c->buf - c->have, 0);
+      }
       if (r <= 0) {
         if (r < 0 && (errno == EAGAIN || errno == EINTR)) continue;
         // peer closed: reconnect and retry
@@ -687,6 +725,7 @@ void thread_main(ThreadState* ts, const Options* o) {
         if (rec) {
           ts->hist.add(uint64_t(lat));
           ++ts->completed;
+          if (rx_kernel > c->t0) ts->svc.add(uint64_t(rx_kernel - c->t0));
         }
         if (status < 200 || status > 299) {
           if (live) ++ts->non2xx;
@@ -733,7 +772,9 @@ void thread_main(ThreadState* ts, const Options* o) {
       }
       if (!close && c->inflight > 0) continue;  // the rest of the batch is still due
       c->busy = false;
-      c->free_at = now_rx;
+      // free since the response arrived (its kernel timestamp when known): a late read is
+      // this generator's delay, not the server's
+      c->free_at = rx_kernel > 0 && rx_kernel <= now_rx ? rx_kernel : now_rx;
       if (close) {
         epoll_ctl(ts->epfd, EPOLL_CTL_DEL, c->fd, nullptr);
         ::close(c->fd);
@@ -792,7 +833,7 @@ bool parse_targets(const std::string& s, std::vector<Target>* out) {
 }
 
 std::string stats_json(std::vector<std::unique_ptr<ThreadState>>& ts, bool with_hist) {
-  Histogram h;
+  Histogram h, svc;
   uint64_t errors = 0, non2xx = 0, reconnects = 0, checked = 0, mismatch = 0, alt = 0;
   uint64_t poll_hits = 0, spin_hits = 0, spin_misses = 0, sleeps = 0, idle_ns = 0, gmax = 0, late = 0, behind = 0,
            late_1ms = 0;
@@ -815,6 +856,7 @@ std::string stats_json(std::vector<std::unique_ptr<ThreadState>>& ts, bool with_
     }
     std::lock_guard<std::mutex> g(t->hist_mu);
     h.merge(t->hist);
+    svc.merge(t->svc);
     errors += t->errors;
     non2xx += t->non2xx;
     reconnects += t->reconnects;
@@ -854,6 +896,15 @@ std::string stats_json(std::vector<std::unique_ptr<ThreadState>>& ts, bool with_
            (unsigned long long)late, (unsigned long long)late_1ms, (unsigned long long)behind,
            (unsigned long long)rdelay, (unsigned long long)rdelay_max);
   s += buf;
+  if (svc.count()) {
+    snprintf(buf, sizeof buf,
+             ",\"service_count\":%llu,\"service_p50_ns\":%llu,\"service_p99_ns\":%llu,\"service_p999_ns\":%llu,"
+             "\"service_max_ns\":%llu",
+             (unsigned long long)svc.count(), (unsigned long long)svc.percentile(50),
+             (unsigned long long)svc.percentile(99), (unsigned long long)svc.percentile(99.9),
+             (unsigned long long)svc.max());
+    s += buf;
+  }
   if (pmu) {
     snprintf(buf, sizeof buf, ",\"user_instructions\":%llu,\"user_cycles\":%llu", (unsigned long long)u_ins,
              (unsigned long long)u_cyc);
@@ -971,7 +1022,10 @@ int main(int argc, char** argv) {
     else if (a == "--busy-poll-us") o.busy_poll_us = atoi(val().c_str());
     else if (a == "--busy-poll-pause") o.busy_poll_pause = atoi(val().c_str());
     else if (a == "--epoll-lt") o.edge_triggered = false;
-    else if (a == "--rate" || a == "-R") o.rate = atof(val().c_str());
+    else if (a == "--rate" || a == "-R") {
+      o.rate = atof(val().c_str());
+      o.rx_timestamps = o.rate > 0;
+    }
     else if (a == "--spin-us") o.spin_us = atoi(val().c_str());
     else if (a == "--sched-slice-us") o.sched_slice_us = atoi(val().c_str());
     else if (a == "--per-conn-quota") o.per_conn_quota = true;
@@ -1185,6 +1239,7 @@ int main(int argc, char** argv) {
       for (auto& t : ts) {
         std::lock_guard<std::mutex> g(t->hist_mu);
         t->hist.reset();
+        t->svc.reset();
         t->errors = t->non2xx = t->reconnects = t->body_checked = t->body_mismatch = t->body_alt = 0;
         t->pmu_reset();
         t->sched_reset();

@@ -22,6 +22,11 @@ For every point with p99.9 above --threshold-us it names what the point's own re
   irq/steal  interrupt or hypervisor time on the replica's CPUs above 5 %
   neighbours other tenants on the SMT siblings or elsewhere in the L3 above 5 %
 
+and the point's service-time p99.9 (send() to the response's kernel receive timestamp at the
+client: the server's and the network's time with none of the generator's own delays). A point
+whose open-loop p99.9 is over the threshold while its service p99.9 is not had its tail made
+by the load generator (a late send or a late read), not by the server.
+
     python bench/tail_report.py gpurun_out/r6_06_tails/curve_*.json [--threshold-us 100]
 """
 from __future__ import annotations
@@ -79,26 +84,32 @@ def main() -> int:
     ap.add_argument("--json", default="")
     a = ap.parse_args()
     report = []
-    print(f"| curve | target | achieved | p99 µs | p99.9 µs | max µs | server CPUs | attributed to |")
-    print("|---|---|---|---|---|---|---|---|")
+    print(f"| curve | target | achieved | p99 µs | p99.9 µs | max µs | service p99.9 µs | server CPUs | attributed to |")
+    print("|---|---|---|---|---|---|---|---|---|")
     for path in a.curves:
         d = json.loads(Path(path).read_text())
         name = Path(path).stem
         for row in d["rows"]:
             tail = row["p999_us"] > a.threshold_us
             c = causes(row)
+            svc = (row.get("service_us") or {}).get("p999")
+            if tail and svc is not None and svc <= a.threshold_us:
+                c.insert(0, f"GENERATOR (service p99.9 {svc:.1f} us)")
             report.append({"curve": name, "server_busy_poll": d.get("server_busy_poll"), "target_rps": row["target_rps"],
                            "p99_us": row["p99_us"], "p999_us": row["p999_us"], "max_us": row["max_us"],
-                           "over_threshold": tail, "causes": c})
+                           "service_p999_us": svc, "over_threshold": tail,
+                           "server_over_threshold": tail and (svc is None or svc > a.threshold_us), "causes": c})
             mark = "**" if tail else ""
             print(f"| {name} | {row['target_rps'] / 1e6:g} M | {row['achieved_rps'] / 1e6:.3f} M | {row['p99_us']:.1f} | "
-                  f"{mark}{row['p999_us']:.1f}{mark} | {row['max_us']:.0f} | {row['server_cpus_busy']} | "
+                  f"{mark}{row['p999_us']:.1f}{mark} | {row['max_us']:.0f} | "
+                  f"{'—' if svc is None else f'{svc:.1f}'} | {row['server_cpus_busy']} | "
                   f"{', '.join(c) if c else ('—' if not tail else 'nothing recorded')} |")
     if a.json:
         Path(a.json).write_text(json.dumps(report, indent=1))
     unexplained = [r for r in report if r["over_threshold"] and not r["causes"]]
     print(f"\n{sum(r['over_threshold'] for r in report)} points over {a.threshold_us:g} us, "
-          f"{len(unexplained)} with nothing recorded")
+          f"{len(unexplained)} with nothing recorded; "
+          f"{sum(r['server_over_threshold'] for r in report)} with the service time over it too")
     return 0
 
 
