@@ -324,6 +324,11 @@ def test_latency_curve_runs_open_loop_with_the_server_busy_poll_it_names(tmp_pat
     assert d["spin_us"] == 1000
     assert {"run_delay_ms", "run_delay_max_thread_ms", "invol"} <= set(row["server_threads"]["workers"])
     assert {"run_delay_ns", "run_delay_max_thread_ns", "send_late_max_ns", "behind_max_ns"} <= set(row["loadgen"])
+    # service time from the kernel's receive timestamps: never longer than the open-loop latency
+    # measured from the intended send time (which adds the generator's own delays)
+    svc = row["service_us"]
+    assert svc and 0 < svc["p50"] <= svc["p999"] <= svc["max"], svc
+    assert svc["p50"] <= row["p50_us"] * 1.05 + 5, (svc, row["p50_us"])
     rep = subprocess.run([sys.executable, str(ROOT / "bench" / "tail_report.py"), str(out), "--threshold-us", "0"],
                          capture_output=True, text=True, timeout=60)
     assert rep.returncode == 0 and "with nothing recorded" in rep.stdout, rep.stdout + rep.stderr
