@@ -132,6 +132,8 @@ class _AlohaHandler(BaseHTTPRequestHandler):
             body, status = b"", 204
         elif mode == "garbage":
             body, status = b"{not json", 200
+        elif mode == "compact" or owner.compact:  # as Jackson writes a List<String>: no whitespace
+            body, status = json.dumps(payload, separators=(",", ":"), ensure_ascii=False).encode(), 200
         else:
             body, status = json.dumps(payload).encode(), 200
         self.send_response(status)
@@ -171,6 +173,7 @@ class FakeAloha(_Base):
         self.delay_s = delay_s
         self.retry_after = "0"  # Retry-After value sent in mode "unavailable"
         self.payload = payload if payload is not None else ["Aloha mai aloha-1", "Bonjour de bonjour-1"]
+        self.compact = False  # every list written without whitespace (modes that write a list)
         super().__init__(_AlohaHandler)
 
     def set_mode(self, mode: str, delay_s: float | None = None):

@@ -361,7 +361,8 @@ void AlohaChainer::on_response(http::Worker& w, WorkerCalls& wc, uint32_t slot, 
                              (long long)(now - c.attempt_ms));
   }
   ChainResult& res = wc.result;
-  res.fallback = res.null_list = res.error = false;
+  res.fallback = res.null_list = res.error = res.raw = false;
+  res.raw_list = {};
   res.reason.clear();
   std::string err;
   bool success = false, retryable = false;
@@ -372,7 +373,12 @@ void AlohaChainer::on_response(http::Worker& w, WorkerCalls& wc, uint32_t slot, 
     res.null_list = true;
     res.items.clear();
   } else if (r.ok && r.status >= 200 && r.status < 300) {
-    if (json::decode_string_list(r.body, &res.items, &err)) {
+    if (json::plain_string_list(r.body, &res.raw_count)) {
+      // aloha's list as written: passed on as text, nothing decoded or re-encoded (r lives in
+      // the pool until this call returns, and the callback runs inside it)
+      success = res.raw = true;
+      res.raw_list = r.body;
+    } else if (json::decode_string_list(r.body, &res.items, &err)) {
       success = true;
     } else {
       err = "DecodeException: " + err;  // a FeignException: never retried

@@ -22,6 +22,12 @@ constexpr std::string_view kFallbackGreeting = "Aloha response (fallback)";
 
 struct ChainResult {
   std::vector<std::optional<std::string>> items;
+  // aloha's body when it is a list of plain strings as a serializer writes it
+  // (json::plain_string_list): the list is then passed on as this text and `items` is not
+  // filled. The view is valid only while the callback runs; `raw_count` strings.
+  bool raw = false;
+  std::string_view raw_list;
+  size_t raw_count = 0;
   bool fallback = false;
   // aloha answered 2xx without a list (empty body, or JSON null): Feign's JacksonDecoder
   // returns null, the command succeeds, and greetings.addAll(null) then throws in

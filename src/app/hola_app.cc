@@ -562,7 +562,9 @@ void HolaApp::finish_chaining(const http::ConnRef& conn, uint64_t cgen, int ka_r
       refresh(w, wc);
     if (wc.gen == cgen) {
       size_t body_len = wc.chain_json_prefix.size() + 1;
-      for (auto& it : res.items) body_len += 1 + (it ? json::quoted_size(*it) : 4);
+      if (res.raw) body_len += res.raw_count ? res.raw_list.size() - 1 : 0;  // ","+elements
+      else
+        for (auto& it : res.items) body_len += 1 + (it ? json::quoted_size(*it) : 4);
       char len[24];
       const size_t len_n = size_t(std::to_chars(len, len + sizeof len, body_len).ptr - len);
       std::string& out = conn->response_buffer();
@@ -574,12 +576,22 @@ void HolaApp::finish_chaining(const http::ConnRef& conn, uint64_t cgen, int ka_r
       out += "\r\n\r\n";
       if (!head) {
         out += wc.chain_json_prefix;
-        for (auto& it : res.items) {
-          out += ',';
-          if (it) json::append_string(&out, *it);
-          else out += "null";
+        if (res.raw) {
+          // aloha's elements as it wrote them: "[a,b]" goes in as ",a,b]"
+          if (res.raw_count) {
+            out += ',';
+            out.append(res.raw_list.data() + 1, res.raw_list.size() - 1);
+          } else {
+            out += ']';
+          }
+        } else {
+          for (auto& it : res.items) {
+            out += ',';
+            if (it) json::append_string(&out, *it);
+            else out += "null";
+          }
+          out += ']';
         }
-        out += ']';
       }
       conn->complete_appended(ka);
       answered = true;
@@ -594,7 +606,14 @@ void HolaApp::finish_chaining(const http::ConnRef& conn, uint64_t cgen, int ka_r
     items.reserve(1 + res.items.size());
     if (own) items.push_back(own->greeting);
     else items.push_back(std::nullopt);
-    for (auto& s : res.items) items.push_back(s);
+    if (res.raw) {
+      std::vector<std::optional<std::string>> aloha;
+      std::string err;
+      json::decode_string_list(res.raw_list, &aloha, &err);  // plain_string_list: cannot fail
+      for (auto& s : aloha) items.push_back(std::move(s));
+    } else {
+      for (auto& s : res.items) items.push_back(s);
+    }
     std::string body = json::string_array(items);
     ResponseSpec s;
     s.keep_alive = ka;

@@ -272,6 +272,29 @@ bool parse(std::string_view in, Value* out, std::string* err) {
   return true;
 }
 
+bool plain_string_list(std::string_view in, size_t* count) {
+  const size_t n = in.size();
+  if (n < 2 || in[0] != '[' || in[n - 1] != ']') return false;
+  size_t k = 0;
+  if (n > 2) {
+    const size_t end = n - 1;  // the closing bracket: no string may run into it
+    size_t i = 1;
+    for (;;) {
+      if (in[i] != '"') return false;
+      ++i;
+      i += json_plain_prefix(in.data() + i, end - i);  // stops at the closing quote, an escape or a control
+      if (i >= end || in[i] != '"') return false;
+      ++i;
+      ++k;
+      if (i == end) break;
+      if (in[i] != ',' || i + 1 >= end) return false;
+      ++i;
+    }
+  }
+  *count = k;
+  return true;
+}
+
 bool decode_string_list(std::string_view in, std::vector<std::optional<std::string>>* out,
                         std::string* err) {
   // Streams straight into *out (no DOM): this runs once per aloha response. The elements

@@ -43,4 +43,12 @@ bool parse(std::string_view in, Value* out, std::string* err);
 bool decode_string_list(std::string_view in, std::vector<std::optional<std::string>>* out,
                         std::string* err);
 
+// True when `in` is a list of strings exactly as a serializer writes one: `[` then
+// `"..."` separated by `,` then `]`, no whitespace, nothing escaped in any string. Such a
+// list decodes to strings that re-encode to the same bytes, so a caller that only passes the
+// list on can copy its text instead of decoding and re-encoding every element. *count is the
+// number of strings. Anything else (whitespace, escapes, null, numbers, malformed) is false:
+// decode_string_list() then says what it decodes to or why it fails.
+bool plain_string_list(std::string_view in, size_t* count);
+
 }  // namespace hola::json

@@ -559,6 +559,12 @@ PYBIND11_MODULE(_native, m) {
   m.def("string_array", &string_array_py);
   m.def("json_quote", [](const std::string& s) { return py::bytes(json::quote(s)); });
   m.def("json_quoted_size", [](const std::string& s) { return json::quoted_size(s); });
+  m.def("json_plain_string_list", [](py::bytes b) -> py::object {
+    const std::string s = b;
+    size_t n = 0;
+    if (!json::plain_string_list(s, &n)) return py::none();
+    return py::int_(n);
+  });
   m.def("json_plain_prefix", [](py::bytes b) {
     const std::string s = b;
     return json_plain_prefix(s.data(), s.size());

@@ -33,6 +33,33 @@ def test_success_appends_aloha_list(hola, aloha):
     assert aloha.requests[-1]["path"] == "/api/aloha-chaining"
 
 
+@pytest.mark.parametrize("payload", [
+    ["Aloha mai aloha-1", "Bonjour de bonjour-1"],
+    [],
+    ["één", "a/b", "x"],
+    ['say "hi"', "back\\slash", "tab\tnl\n"],
+    ["a", None, "b"],
+    ["Aloha", 7, True],
+])
+def test_list_passed_on_as_written_or_reencoded_gives_the_same_body(hola, aloha, payload):
+    """A list of plain strings written compactly (as Jackson writes one) is passed on as text
+    (json::plain_string_list); any other list is decoded and re-encoded. Both give the body
+    Jackson would: the same bytes for the same elements, whatever aloha's whitespace."""
+    aloha.payload = payload
+    s = hola(args=["--aloha-url", aloha.url, "--no-tracing", "--feign-log", "none"], env={"HOSTNAME": "h"})
+    bodies = []
+    for mode in ("compact", "ok"):
+        aloha.set_mode(mode)
+        st, h, body = s.get("/api/hola-chaining", timeout=10)
+        assert st == 200, body
+        assert int(h["content-length"]) == len(body)
+        bodies.append(body)
+    assert bodies[0] == bodies[1]
+    want = ["Hola de h"] + [None if v is None else (str(v).lower() if isinstance(v, bool) else str(v)) for v in payload]
+    assert json.loads(bodies[0]) == want
+    assert bodies[0] == json.dumps(want, separators=(",", ":"), ensure_ascii=False).encode()
+
+
 def test_keepalive_reuse(hola, aloha):
     s = hola(args=["--aloha-url", aloha.url, "--no-tracing", "--feign-log", "none"], threads=1)
     for _ in range(5):
@@ -1037,13 +1064,15 @@ def test_pipelined_calls_behind_a_slow_answer_are_not_held_to_their_timeouts(hol
     assert _retries(s).get("transport", 0) == 3  # each queued call went out once more
 
 
-def test_a_call_parked_across_a_reload_answers_with_its_own_greeting(hola, aloha, tmp_path):
+@pytest.mark.parametrize("compact", [False, True])
+def test_a_call_parked_across_a_reload_answers_with_its_own_greeting(hola, aloha, tmp_path, compact):
     """The greeting is computed when the request arrives (HolaResource.java:75): a chaining
     call still waiting on aloha while the greeting file changes answers with the greeting of
     its own request, and the next request gets the new one. (The worker keeps the contents of
     the last configuration generations for such calls; the call holds its generation.)"""
     conf = tmp_path / "t.properties"
     conf.write_text("hello=old %s\n")
+    aloha.compact = compact  # a list passed on as text, or decoded (json::plain_string_list)
     aloha.set_mode("slow_once", delay_s=2.0)
     s = hola(args=[f"-Dconf={conf}", "--aloha-url", aloha.url, "--no-tracing", "--feign-log", "none",
                    "--config-poll-ms", "100", "-Dhystrix.command.default.execution.isolation.thread.timeoutInMilliseconds=5000"],

@@ -357,3 +357,38 @@ def test_json_plain_prefix_matches_a_byte_loop(native, data):
     want = next((i for i, c in enumerate(data) if c < 0x20 or c in (0x22, 0x5C)), len(data))
     assert native.json_plain_prefix(data) == want
     assert native.json_quoted_size(data) == len(native.json_quote(data))
+
+
+_ITEM = st.lists(st.sampled_from([b"a", b'"', b"\\", b"\x01", b" ", b"\x7f", b"\xc3\xa9", b"/", b"Hola de ", b",", b"]"]),
+                 max_size=6).map(b"".join)
+
+
+@settings(max_examples=2000, deadline=None)
+@given(st.lists(_ITEM, max_size=5), st.sampled_from(["compact", "spaced", "escaped"]))
+def test_plain_string_list_is_exactly_what_reencodes_unchanged(native, items, style):
+    """json::plain_string_list (aloha's list passed on as text) holds exactly when decoding the
+    body and re-encoding its elements gives the same bytes: a compact list of strings with
+    nothing to escape. Everything else goes through the decoder."""
+    def enc(b):
+        return native.json_quote(b)
+    if style == "compact":
+        body = b"[" + b",".join(enc(i) for i in items) + b"]"
+    elif style == "spaced":
+        body = b"[ " + b", ".join(enc(i) for i in items) + b" ]"
+    else:  # '/' written escaped, as some encoders do
+        body = b"[" + b",".join(enc(i).replace(b"/", b"\\/") for i in items) + b"]"
+    got = native.json_plain_string_list(body)
+    plain = all(native.json_plain_prefix(i) == len(i) for i in items)
+    if style == "compact" and plain:
+        assert got == len(items), body
+    elif style == "spaced" or (style == "escaped" and any(b"/" in i for i in items)) or not plain:
+        assert got is None, body
+    else:
+        assert got == len(items), body
+
+
+@pytest.mark.parametrize("body", [b"", b"[", b"]", b"[,]", b'["a",]', b'[,"a"]', b'["a""b"]', b'["a]', b'["a"',
+                                  b'[null]', b'["a",null]', b'[1]', b'[true]', b'["a\u0041"]', b'{"a":"b"}',
+                                  b'["a"] ', b' ["a"]', b'["\x01"]'])
+def test_plain_string_list_rejects_what_it_cannot_pass_on(native, body):
+    assert native.json_plain_string_list(body) is None
