@@ -269,6 +269,7 @@ struct alignas(64) Command::Shard {
   // touched by the owning thread only).
   alignas(64) std::atomic<int64_t> used{0};
   std::array<int32_t, 16> borrowed{};
+  int32_t borrowed_total = 0;  // sum of `borrowed`: a release scans it only when non-zero
   int64_t per_thread_inflight = 0;
   explicit Shard(const Settings& s)
       : counter(s.rolling_window_ms, s.rolling_buckets),
@@ -344,7 +345,10 @@ Command::Admit Command::try_start_per_thread(int64_t now, int64_t core) {
     sh.pool_counter.add(now, Event::kThreadPoolRejected);
     return Admit::kRejected;
   }
-  if (lender >= 0) ++sh.borrowed[size_t(lender)];
+  if (lender >= 0) {
+    ++sh.borrowed[size_t(lender)];
+    ++sh.borrowed_total;
+  }
   ++sh.per_thread_inflight;
   const int64_t mine = sh.used.load(std::memory_order_relaxed);
   // the pool's largest size, at least this share's count (a read of a line that is rarely
@@ -363,12 +367,14 @@ void Command::release_in(Shard& sh) {
   if (sh.per_thread_inflight > 0) {
     // a per-thread admission: give a borrowed slot back to its lender first, else our own
     --sh.per_thread_inflight;
-    for (size_t j = 0; j < sh.borrowed.size(); ++j)
-      if (sh.borrowed[j] > 0) {
-        --sh.borrowed[j];
-        shards_[j]->used.fetch_sub(1, std::memory_order_acq_rel);
-        return;
-      }
+    if (sh.borrowed_total > 0)
+      for (size_t j = 0; j < sh.borrowed.size(); ++j)
+        if (sh.borrowed[j] > 0) {
+          --sh.borrowed[j];
+          --sh.borrowed_total;
+          shards_[j]->used.fetch_sub(1, std::memory_order_acq_rel);
+          return;
+        }
     sh.used.fetch_sub(1, std::memory_order_acq_rel);
     return;
   }
