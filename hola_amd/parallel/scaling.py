@@ -92,7 +92,8 @@ def plan_slots(n: int, k: int, slots: int, lb: str) -> dict:
             "slots": [p["slot"] for p in sub], "smt": sub[0]["smt"] if sub else "pair"}
 
 
-def _measure(targets, conns: int, load_cpus: list[int], args, verify: bool) -> dict:
+def _measure(targets, conns: int, load_cpus: list[int], args, verify: bool,
+             conn_targets: list[int] | None = None) -> dict:
     """A closed-loop run of args.duration after args.warmup, in the load generator's control
     mode: every connection is made before any request is sent (as bench.py runs it), then
     warm-up and measurement run as one continuous run (`runfor`). In wrk-style duration mode
@@ -100,7 +101,8 @@ def _measure(targets, conns: int, load_cpus: list[int], args, verify: bool) -> d
     while others were already loaded were placed off their client's core (per-replica locality
     all `same_socket` in some runs, profiles/round5/04_scale_mini)."""
     lg = ControlledLoadgen(targets, conns, len(load_cpus), cpu_list=",".join(map(str, load_cpus)),
-                           busy_poll_us=args.busy_poll_us, busy_poll_pause=args.busy_poll_pause, verify_body=verify)
+                           busy_poll_us=args.busy_poll_us, busy_poll_pause=args.busy_poll_pause, verify_body=verify,
+                           conn_targets=conn_targets)
     try:
         r = timed_closed_loop(lg, conns, args.duration, None, [], [], warm_s=args.warmup)
     finally:
@@ -147,6 +149,13 @@ def run_point(n: int, args) -> dict:
                          busy_poll_us=args.busy_poll_us if args.proxy_busy_poll_us < 0 else args.proxy_busy_poll_us,
                          exe=args.proxy_exe or None, backend_cpus=p["replicas"] if hints else None) as px:
                 res = _measure([("127.0.0.1", px.port)], conns, p["loadgen"], args, verify=False)
+        elif args.lb == "plain":
+            # topology-blind round-robin on the same cores: connection i runs on thread i % T
+            # and goes to replica (i // T) % n, so every thread deals its connections over all
+            # replicas wherever they run, as a LoadBalancer Service deals them (pom.xml:77-80)
+            nthreads = len(p["loadgen"])
+            res = _measure(rs.targets, conns, p["loadgen"], args, verify=True,
+                           conn_targets=[(i // nthreads) % n for i in range(conns)])
         else:
             # client-side round-robin: one target per replica, so each target's body is fixed
             res = _measure(rs.targets, conns, p["loadgen"], args, verify=args.lb == "client")
@@ -176,7 +185,9 @@ def run_point(n: int, args) -> dict:
                     "loadgen": format_cpu_list(p["loadgen"])},
         "budget": budget, "quota": cgroup_cpu_quota(), "duration_s": args.duration, "per_replica": per_replica,
         "lb_detail": ({"reuseport_cpu": reuseport_cpu} if args.lb == "reuseport" else
-                      {"topology_hints": hints} if args.lb == "proxy" else {"dealing": "thread t -> replica t"}),
+                      {"topology_hints": hints} if args.lb == "proxy" else
+                      {"dealing": "thread t -> every replica, blind to topology"} if args.lb == "plain" else
+                      {"dealing": "thread t -> replica t"}),
         **({"slot_cores": args.slot_cores, "node_slots": p["slots"], "layout": f"miniature node plan ({p['smt']})"}
            if args.slot_cores else {}),
     }
@@ -190,9 +201,11 @@ def main(argv=None) -> int:
     ap.add_argument("--mode", choices=["weak", "strong"], default="weak")
     ap.add_argument("--connections-per-replica", type=int, default=64)
     ap.add_argument("--connections", type=int, default=512)
-    ap.add_argument("--lb", choices=["client", "proxy", "reuseport"], default="client",
-                    help="client: load generator round-robins over replica ports; proxy: hola_rrproxy; "
-                         "reuseport: one shared port, the kernel spreads connections")
+    ap.add_argument("--lb", choices=["client", "plain", "proxy", "reuseport"], default="client",
+                    help="client: load generator round-robins over replica ports, each thread next to the "
+                         "replica it drives; plain: the same dealing blind to topology (every thread over "
+                         "every replica); proxy: hola_rrproxy; reuseport: one shared port, the kernel spreads "
+                         "connections")
     ap.add_argument("--proxy-threads", type=int, default=0,
                     help="0 = half the CPU budget, mirrored with the servers and the load generator "
                          "in every L3 domain")

@@ -278,6 +278,25 @@ def test_scaling_harness_smoke():
     assert lines[1]["connections"] == 16
 
 
+def test_scaling_harness_plain_dealing():
+    """--lb plain: the client-side front blind to topology. Every load-generator
+    thread deals its connections over every replica, every body is checked against the replica
+    that answered it, and each replica serves its share."""
+    from hola_amd.parallel import scaling
+    import io
+    import contextlib
+
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        scaling.main(["--replicas", "2", "--duration", "0.5", "--warmup", "0.2", "--budget", "6",
+                      "--connections-per-replica", "8", "--lb", "plain"])
+    (row,) = [json.loads(l) for l in buf.getvalue().splitlines() if l.startswith("{")]
+    assert row["lb"] == "plain" and row["errors"] == 0 and row["body_mismatch"] == 0, row
+    assert row["lb_detail"]["dealing"].startswith("thread t -> every replica")
+    reqs = [r["requests"] for r in row["per_replica"]]
+    assert min(reqs) > 0.25 * sum(reqs), reqs
+
+
 def test_scaling_harness_proxy_mode():
     """--lb proxy: load generator -> hola_rrproxy -> replicas, with the mirrored core plan."""
     from hola_amd.parallel import scaling
