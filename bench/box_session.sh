@@ -110,7 +110,7 @@ repeat)
   # the default bench REPS times back to back: run-to-run spread of the headline on this host
   REPS=${1:-5}; shift
   for rep in $(seq 1 "$REPS"); do
-    timeout -k 10 300 python bench.py "$@" > "$OUT/bench_$rep.json" 2>> "$OUT/err.log" || exit 1
+    timeout -k 10 400 python bench.py "$@" > "$OUT/bench_$rep.json" 2>> "$OUT/err.log" || exit 1
   done
   ;;
 ab)
