@@ -785,6 +785,10 @@ def _chain_keys(c: dict | None, p: str) -> dict:
            # hola A's own CPU per chained request (it serves the client and calls B)
            f"{p}_a_cpu_us_per_req": round(c["a_cpu_us_per_req"], 3),
            f"{p}_b_cpu_us_per_req": round(c["b_cpu_us_per_req"], 3),
+           # ... and what of it was work: without A's empty polls, and A's workers' own user-space
+           # instructions and cycles (hardware counters; null where the host refuses them)
+           f"{p}_a_busy_cpu_us_per_req": round(c["a_busy_cpu_us_per_req"], 3),
+           f"{p}_a_user_instr_per_req": c["a_user_instr_per_req"], f"{p}_a_user_cycles_per_req": c["a_user_cycles_per_req"],
            # A's Hystrix command over the sub-run (its warm-up included)
            f"{p}_hystrix_success": h.get("SUCCESS", 0), f"{p}_hystrix_fallback": h.get("FALLBACK_SUCCESS", 0),
            f"{p}_hystrix_timeout": h.get("TIMEOUT", 0), f"{p}_hystrix_events": h,

@@ -497,8 +497,14 @@ def chain(a, cpus, job_cpus, shipped: bool = False, seconds: float | None = None
     rps = r["rps"]
     # CPU over the whole sub-run (its warm-up included) per request at the measured rate
     busy = ((c1[0] - c0[0]) / wall, (c1[1] - c0[1]) / wall)
+    # A's event loop and its workers' own hardware counters over the same span (VERDICT r5 #4:
+    # an efficiency figure independent of the peer): busy CPU without the empty polls, and
+    # user-space instructions and cycles per chained request
+    a_loop = loop_block(m0[0], m1[0], rps * wall)
     out = {**r, "a_cpu_us_per_req": 1e6 * busy[0] / rps if rps else 0.0,
            "b_cpu_us_per_req": 1e6 * busy[1] / rps if rps else 0.0,
+           "a_busy_cpu_us_per_req": (1e6 * (c1[0] - c0[0] - a_loop["idle_spin_s"]) / (rps * wall)) if rps else 0.0,
+           "a_user_instr_per_req": a_loop["user_instr_per_req"], "a_user_cycles_per_req": a_loop["user_cycles_per_req"],
            "hystrix": counter_delta(m0[0], m1[0], "hystrix."),
            # A's breaker: times it opened, and closed by a trial or by a call already running
            "circuit": counter_delta(m0[0], m1[0], "circuit."),

@@ -88,6 +88,8 @@ def test_bench_auto_steps_and_node_subruns():
         assert out["v4_errors"] == 0 and out["v4_body_checked"] == out["v4_requests"] > 0
         assert out["v4_vs_value"] > 0
     assert out["chain_errors"] == 0 and out["chain_hystrix_fallback"] == 0 and out["chain_pool"] == 128
+    assert 0 < out["chain_a_busy_cpu_us_per_req"] <= out["chain_a_cpu_us_per_req"] + 0.05
+    assert "chain_a_user_instr_per_req" in out and "chain_a_user_cycles_per_req" in out
     assert set(out["chain_locality"]) == {"loadgen_to_a", "a_to_b"}
     assert abs(sum(out["chain_locality"]["a_to_b"].values()) - 1.0) < 1e-3
     assert {"hit", "miss", "backoffs", "backoff_ms"} <= set(out["chain_spins"]["a"])

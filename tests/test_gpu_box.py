@@ -55,6 +55,10 @@ def test_bench_json_contract_on_host():
     assert out["chain_hystrix_fallback"] == 0 and out["chain_hystrix_timeout"] == 0
     assert out["chain_hystrix_success"] >= out["chain_requests"]  # its warm-up counts too
     assert out["chain_a_cpu_us_per_req"] > 0
+    # A's own work per chained request, independent of the peer: busy CPU without empty polls,
+    # and its workers' user-space instructions from hardware counters (the box allows them)
+    assert 0 < out["chain_a_busy_cpu_us_per_req"] <= out["chain_a_cpu_us_per_req"] + 0.05
+    assert out["chain_a_user_instr_per_req"] and 1000 < out["chain_a_user_instr_per_req"] < 20000, out
     # ... with what separates its two modes: host load, per-hop accept locality, spin counters
     assert set(out["chain_locality"]) == {"loadgen_to_a", "a_to_b"} and out["chain_spins"]["a"]
     assert set(out["chain_host_load"]) == hl_keys and set(out["deployed_host_load"]) == hl_keys
