@@ -786,7 +786,9 @@ def _chain_keys(c: dict | None, p: str) -> dict:
            f"{p}_a_cpu_us_per_req": round(c["a_cpu_us_per_req"], 3),
            f"{p}_b_cpu_us_per_req": round(c["b_cpu_us_per_req"], 3),
            # ... and what of it was work: without A's empty polls, and A's workers' own user-space
-           # instructions and cycles (hardware counters; null where the host refuses them)
+           # instructions and cycles (hardware counters; null where the host refuses them; they
+           # include the empty polls' instructions, which bench/instr_ab.py's figure, measured
+           # with busy-polling off, does not)
            f"{p}_a_busy_cpu_us_per_req": round(c["a_busy_cpu_us_per_req"], 3),
            f"{p}_a_user_instr_per_req": c["a_user_instr_per_req"], f"{p}_a_user_cycles_per_req": c["a_user_cycles_per_req"],
            # A's Hystrix command over the sub-run (its warm-up included)
