@@ -193,6 +193,10 @@ struct PyCommand {
   bool cancel_queued(int64_t ticket) { return cmd->cancel_queued({uint64_t(ticket), 0}); }
   void release_slot() { cmd->release_slot(); }
   void set_per_thread_bulkhead(bool on) { cmd->set_per_thread_bulkhead(on); }
+  // a configuration reload (Archaius' dynamic properties): the same keys as the constructor
+  void update(const std::map<std::string, std::string>& props) {
+    cmd->update_settings(resilience::settings_from(props, "AlohaService#aloha()", "aloha"));
+  }
   void queued_timeout(int64_t ms) { cmd->queued_timeout(ms); }
   int64_t queue_size() { return cmd->queue_size(); }
   void finish(const std::string& outcome, int64_t ms) {
@@ -629,6 +633,7 @@ PYBIND11_MODULE(_native, m) {
       .def("cancel_queued", &PyCommand::cancel_queued)
       .def("release_slot", &PyCommand::release_slot)
       .def("set_per_thread_bulkhead", &PyCommand::set_per_thread_bulkhead)
+      .def("update", &PyCommand::update)
       .def("queued_timeout", &PyCommand::queued_timeout)
       .def("queue_size", &PyCommand::queue_size)
       .def("finish", &PyCommand::finish)

@@ -319,10 +319,21 @@ bool Command::per_thread_mode(int64_t core) const {
          !semaphore_.load(std::memory_order_relaxed) && max_queue_.load(std::memory_order_relaxed) <= 0;
 }
 
+int64_t Command::per_thread_in_flight() const {
+  int64_t n = 0;
+  for (const auto& sh : shards_) n += sh->used.load(std::memory_order_relaxed);
+  return n;
+}
+
 Command::Admit Command::try_start_per_thread(int64_t now, int64_t core) {
   const int si = shard_index();
   Shard& sh = *shards_[size_t(si)];
-  auto share = [core](int j) { return core / kShards + (j < core % kShards ? 1 : 0); };
+  if (!per_thread_used_.load(std::memory_order_relaxed)) per_thread_used_.store(true, std::memory_order_relaxed);
+  // Calls admitted through the shared count before a reload switched modes still hold their
+  // slots: the shares divide what they leave (a line only shared-mode calls write, so this
+  // read stays in the cache while the mode holds)
+  const int64_t cap = core - active_.load(std::memory_order_relaxed);
+  auto share = [cap](int j) { return cap / kShards + (j < cap % kShards ? 1 : 0); };
   auto take = [](Shard& s, int64_t q) {
     int64_t u = s.used.load(std::memory_order_relaxed);
     while (u < q)
@@ -474,6 +485,8 @@ Command::Admit Command::try_start(const Queued* q) {
     return try_start_per_thread(now, core);
   const bool sem = semaphore_.load(std::memory_order_relaxed);
   int64_t active = active_.fetch_add(1, std::memory_order_acq_rel) + 1;
+  // calls admitted per thread before a reload switched modes count against the pool too
+  if (per_thread_used_.load(std::memory_order_relaxed)) active += per_thread_in_flight();
   if (sem) {
     // TryableSemaphoreActual.tryAcquire(): the caller's own thread runs the command
     if (active <= sem_max_.load(std::memory_order_relaxed)) {

@@ -235,6 +235,11 @@ class Command {
   void finish_in(Shard& sh, int64_t now, Event outcome, int64_t execute_ms);
   // per-thread bulkhead (see set_per_thread_bulkhead)
   std::atomic<bool> per_thread_{false};
+  // set by the first per-thread admission: from then on a shared-mode admission also counts
+  // the calls still holding per-thread slots (a reload that shrinks the pool below
+  // kPerThreadMinPool switches modes with calls in flight)
+  std::atomic<bool> per_thread_used_{false};
+  int64_t per_thread_in_flight() const;
   bool per_thread_mode(int64_t core) const;
   Admit try_start_per_thread(int64_t now, int64_t core);
   void release_in(Shard& sh);

@@ -406,3 +406,26 @@ def test_per_thread_bulkhead_accounting_adds_up(native, fail_every):
     assert r["runs"] + r["short_circuited"] + r["rejected"] == 8 * 20000
     assert ev.get("SUCCESS", 0) + ev.get("FAILURE", 0) == r["runs"] == r["completed"]
     assert r["concurrent"] == 0 and 1 <= r["largest"] <= 64
+
+
+def test_bulkhead_stays_exact_across_a_reload_that_switches_modes(native):
+    """A reload of coreSize across kPerThreadMinPool switches between the per-thread shares and
+    the one shared count with calls in flight. Hystrix's pool never runs more than coreSize
+    (ThreadPoolExecutor.setCorePoolSize lets the excess finish, and rejects meanwhile), and
+    neither may this: each mode counts the calls the other one admitted."""
+    props = {"hystrix.command.default.circuitBreaker.requestVolumeThreshold": "1000000"}
+    c = native.HystrixCommand({**props, "hystrix.threadpool.default.coreSize": "128"})
+    c.set_per_thread_bulkhead(True)
+    assert [c.try_start() for _ in range(100)] == ["run"] * 100  # per-thread shares
+    c.update({**props, "hystrix.threadpool.default.coreSize": "10"})  # shared count now
+    assert c.try_start() == "rejected"  # 100 still running against a pool of 10
+    for _ in range(95):
+        c.finish("success", 1)
+    assert [c.try_start() for _ in range(6)] == ["run"] * 5 + ["rejected"]
+    c.update({**props, "hystrix.threadpool.default.coreSize": "128"})  # per-thread again
+    assert [c.try_start() for _ in range(119)] == ["run"] * 118 + ["rejected"]
+    assert json.loads(c.pool_json())["currentActiveCount"] == 128
+    for _ in range(128):
+        c.finish("success", 1)
+    assert json.loads(c.pool_json())["currentActiveCount"] == 0
+    assert [c.try_start() for _ in range(129)] == ["run"] * 128 + ["rejected"]
