@@ -13,6 +13,7 @@
 //     response's prefixes need more;
 //   * path decoders never write past their input's length;
 //   * a decoded JSON list re-encodes to a document that decodes to the same list.
+#include <algorithm>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
@@ -29,6 +30,7 @@
 #include "config/resolver.h"
 #include "http/negotiate.h"
 #include "http/parser.h"
+#include "core/scan.h"
 #include "json/json.h"
 #include "tracing/b3.h"
 
@@ -164,6 +166,29 @@ void json_list(std::string_view in) {
     if (!ok2) fprintf(stderr, "re-encoded list does not decode (%s): %s\n", err.c_str(), again.c_str());
     FUZZ_CHECK(ok2);
     FUZZ_CHECK(list == list2);
+    // passed on as written (json::plain_string_list) exactly when re-encoding gives the input
+    // back, with the element count it reports
+    size_t count = 0;
+    const bool plain = json::plain_string_list(in, &count);
+    // (an element that needed escaping was escaped in the input: that input is not plain even
+    // when it re-encodes to itself)
+    const bool all_plain = std::all_of(list.begin(), list.end(), [](const auto& e) {
+      return e && json_plain_prefix(e->data(), e->size()) == e->size();
+    });
+    FUZZ_CHECK(plain == (again == in && all_plain));
+    if (plain) FUZZ_CHECK(count == list.size());
+  } else {
+    size_t count = 0;
+    FUZZ_CHECK(!json::plain_string_list(in, &count));  // what fails to decode is never passed on
+  }
+  {
+    // the plain-prefix scan against its byte loop, and the encoder's size against its output
+    size_t want = 0;
+    while (want < in.size() && (unsigned char)in[want] >= 0x20 && in[want] != '"' && in[want] != '\\') ++want;
+    FUZZ_CHECK(json_plain_prefix(in.data(), in.size()) == want);
+    std::string q;
+    json::append_string(&q, in);
+    FUZZ_CHECK(json::quoted_size(in) == q.size());
   }
   json::Value val;
   (void)json::parse(in, &val, &err);
