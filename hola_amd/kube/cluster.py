@@ -57,6 +57,24 @@ from hola_amd.kube.kubelet import Kubelet, Pod, die_with_parent, project_configm
 TICK_S = 0.02
 
 
+def _listening_127_nets() -> set[int]:
+    """The second octets of 127.<a>.x.x addresses with a listening TCP socket on this host
+    (/proc/net/tcp, state 0A): /16s that a new cluster must not claim."""
+    out: set[int] = set()
+    try:
+        lines = Path("/proc/net/tcp").read_text().splitlines()[1:]
+    except OSError:
+        return out
+    for ln in lines:
+        f = ln.split()
+        if len(f) > 3 and f[3] == "0A":
+            ip_hex = f[1].split(":")[0]
+            b = bytes.fromhex(ip_hex)[::-1]  # little-endian on x86
+            if b[0] == 127:
+                out.add(b[1])
+    return out
+
+
 class ClusterError(RuntimeError):
     pass
 
@@ -163,7 +181,13 @@ class Cluster:
 
         lock_dir = Path(tempfile.gettempdir()) / "hola-kube-nets"
         lock_dir.mkdir(exist_ok=True)
+        busy = _listening_127_nets()
         for a in random.sample(range(100, 250), 150):
+            if a in busy:
+                # something still listens there without holding the claim: pods of an executor
+                # that was SIGKILLed before it could stop them (their parent-death signal goes
+                # with the thread that started them), whose addresses would refuse our pods
+                continue
             f = open(lock_dir / f"127.{a}.lock", "w")
             try:
                 fcntl.flock(f, fcntl.LOCK_EX | fcntl.LOCK_NB)

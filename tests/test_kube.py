@@ -558,3 +558,22 @@ def _alive(pid: int) -> bool:
     except OSError:
         return False
     return st[st.rindex(")") + 2] != "Z"
+
+
+def test_a_pod_network_with_listeners_left_on_it_is_not_claimed():
+    """Pods of an executor that was SIGKILLed can outlive it, still bound to their addresses
+    (a full-suite run once met four of them from a killed run a day earlier: every new pod on
+    those addresses crash-looped on EADDRINUSE). A cluster skips any 127.<a>.0.0/16 where
+    something listens."""
+    import socket
+
+    from hola_amd.kube.cluster import _listening_127_nets
+
+    s = socket.socket()
+    s.bind(("127.123.0.9", 0))
+    s.listen()
+    try:
+        assert 123 in _listening_127_nets()
+    finally:
+        s.close()
+    assert 123 not in _listening_127_nets()
