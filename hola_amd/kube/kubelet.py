@@ -423,6 +423,11 @@ class Kubelet:
         pod.next_mem_check = now + 0.05  # a container over its limit from the start dies before probing
         pod.ready = False
         pod.probe_ok = pod.probe_fail = 0
+        # a probe still in flight was sent to the container that died: its answer (possibly from
+        # this new container, on the same address) must not count, or a restarted container
+        # turns Ready before its initialDelaySeconds, as no kubelet lets it (the probe worker
+        # belongs to the container)
+        pod.probe_future = None
         ps = self._probe_spec(pod)
         pod.next_probe_at = now + (ps["initialDelaySeconds"] * self.cluster.time_scale if ps else 0.0)
         self.cluster.event(pod.name, "Started", f"pid {pod.proc.pid} on {pod.ip}, cpus {cpus}")

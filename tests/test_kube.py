@@ -577,3 +577,23 @@ def test_a_pod_network_with_listeners_left_on_it_is_not_claimed():
     finally:
         s.close()
     assert 123 not in _listening_127_nets()
+
+
+def test_a_restarted_container_waits_its_readiness_delay_again(cluster):
+    """A crashed container is restarted at once (the first restart has no back-off) on the same
+    pod IP. Its readiness starts over: NotReady until initialDelaySeconds has passed and a probe
+    of the *new* container succeeds. A probe still in flight from before the crash must not
+    count, or the pod turns Ready again before the endpoints ever dropped it (a full-suite run
+    once saw Ready 21 ms after the restart)."""
+    c = cluster(replicas=1)
+    c.wait_ready(1, timeout=30)
+    (pod,) = c.get_pods()
+    for k in range(1, 4):
+        c.kill_container(pod["name"])
+        c.wait(lambda: c.get_pods()[0]["restarts"] >= k and c.get_pods()[0]["ready"], 15, "restarted and ready")
+        mine = [(e[0], e[2]) for e in c.events if e[1] == pod["name"]]
+        started = max(t for t, k in mine if k == "Started")
+        ready = [t for t, k in mine if k == "Ready" and t >= started]
+        # readinessProbe initialDelaySeconds 5 in the manifest, at the tests' time scale
+        assert ready and ready[0] - started >= 5 * TS - 0.02, mine[-6:]
+        pod = c.get_pods()[0]
